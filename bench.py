@@ -1,0 +1,256 @@
+"""Benchmark: ICP iterations/s + frames/s on a 640x480 synthetic RGB-D stream
+(BASELINE.json metric, configs[1]).
+
+One step = one incoming frame of the stream, fully on the GPU:
+    u16 depth (already in HBM) -> unprojection -> Morton sort + BVH build
+    (the frame's index, reused as the next pair's target)
+    -> AlignIcp3d(curr, prev) with the reference's P2POINT_REF loop,
+       128 fixed iterations (rs_replay_app.cpp:246-251).
+value = ICP iterations/s over all ranks (steps * 128 / time).  A second timed
+loop runs the build's point-to-plane mode on the same frames (reported as
+extra fields).  Multi-GPU: one process per GPU, each rank tracks its own
+stream (frame pairs are independent; no data-path collective) -> weak
+scaling; barrier + max-over-ranks timing.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import platform
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+from realsensetracker_amd import _lib as L  # noqa: E402
+from realsensetracker_amd import align as A  # noqa: E402
+from realsensetracker_amd import driver  # noqa: E402
+
+METRIC = "ICP iterations/sec + frames/sec, 640×480 RGB-D, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def render_frames(seed: int, n: int, K, stride: int):
+    sc = driver.SyntheticScene(seed)
+    return [sc.render(sc.trajectory(i * stride), K, noise_seed=1000 * seed + i) for i in range(n)]
+
+
+def cpu_baseline(width: int, height: int, iters: int):
+    """The oracle's AlignIcp3d restatement (reference arithmetic, own
+    nanoflann-style kd-tree, 1 core) on one frame pair, first `iters` of the
+    128 iterations; tree build timed separately."""
+    from oracle import oracle as O
+    K = driver.intrinsics(width, height)
+    sc = driver.SyntheticScene(0)
+    da = sc.render(sc.trajectory(0), K, noise_seed=1)
+    db = sc.render(sc.trajectory(1), K, noise_seed=2)
+    K4 = [K.fx, K.fy, K.cx, K.cy]
+    pa, pb = O.unproject(da, K4), O.unproject(db, K4)
+    t0 = time.perf_counter()
+    tree = O.KDTree(pa, 16)
+    t1 = time.perf_counter()
+    O.align_icp(pb, pa, iters, tree=tree)
+    t2 = time.perf_counter()
+    return {"value": iters / (t2 - t1), "unit": "ICP iterations/s", "cores": 1, "kind": "port",
+            "sample": f"1 frame pair {width}x{height} (n={len(pb)}, m={len(pa)}), first {iters} "
+                      f"of 128 P2POINT_REF iterations, oracle/rst_oracle.c -O3, kd-tree leaf 16 "
+                      f"prebuilt ({t1 - t0:.3f} s)",
+            "seconds": t2 - t1, "cpu": cpu_model()}
+
+
+def load_traffic():
+    """Per-launch HBM bytes of the dominant kernel from the committed PMC
+    summary (profiles/pmc_*.json, written by scripts/pmc_summary.py)."""
+    files = sorted(ROOT.glob("profiles/pmc_*.json"))
+    if not files:
+        return None
+    try:
+        d = json.loads(files[-1].read_text())
+        return d.get("k_p2point_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--width", type=int, default=640)
+    ap.add_argument("--height", type=int, default=480)
+    ap.add_argument("--frames", type=int, default=8, help="distinct frames cycled per rank")
+    ap.add_argument("--stride", type=int, default=1, help="trajectory frames between frames")
+    ap.add_argument("--iters", type=int, default=128)
+    ap.add_argument("--no-p2plane", action="store_true")
+    ap.add_argument("--cpu-iters", type=int, default=24)
+    ap.add_argument("--no-cpu", action="store_true")
+    a = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # gloo: timing/barrier only, no data path
+        dist.init_process_group("gloo")
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    def max_over_ranks(x: float) -> float:
+        if dist is None:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum_over_ranks(x: float) -> float:
+        if dist is None:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return float(t.item())
+
+    ctx = A.Context(local)
+    K = driver.intrinsics(a.width, a.height)
+    nfr = max(2, a.frames)
+    frames = render_frames(seed=rank, n=nfr, K=K, stride=a.stride)
+    # depth frames resident in HBM before timing (hipMalloc'd via ctypes)
+    hip = C.CDLL("libamdhip64.so")
+    npx = a.width * a.height
+    d_depth = []
+    for f in frames:
+        p = C.c_void_p()
+        assert hip.hipSetDevice(local) == 0
+        assert hip.hipMalloc(C.byref(p), C.c_size_t(2 * npx)) == 0
+        assert hip.hipMemcpy(p, f.ctypes.data_as(C.c_void_p), C.c_size_t(2 * npx), 1) == 0
+        d_depth.append(p)
+
+    opts_ref = L.default_opts(max_iter=a.iters)
+    opts_pl = L.default_opts(mode=L.RST_P2PLANE, max_iter=30)
+
+    def run(nsteps: int, opts, normals_k: int, stats: dict | None):
+        prev = A.Target.from_depth_device(d_depth[0].value, K, normals_k, ctx)
+        k = 1
+        for s in range(nsteps):
+            cur = A.Target.from_depth_device(d_depth[k % nfr].value, K, normals_k, ctx)
+            r = A.align_prepared(cur, prev, None, opts)
+            if stats is not None:
+                stats["iters"] += r.iterations
+                stats["n"] += len(cur)
+                stats["m"] += len(prev)
+                stats["ok"] += int(r.ok)
+                ms, nl = ctx.last_kernel_time()
+                stats["kernel_ms"] += ms * nl
+                stats["launches"] += nl
+            prev.free()
+            prev = cur
+            k += 1
+        prev.free()
+
+    # ---- reference mode (value) ------------------------------------------------
+    run(a.warmup, opts_ref, 0, None)
+    ctx.enable_kernel_timing(True)
+    st = {"iters": 0, "n": 0, "m": 0, "ok": 0, "kernel_ms": 0.0, "launches": 0}
+    barrier()
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    run(a.steps, opts_ref, 0, st)
+    ctx.synchronize()
+    barrier()
+    dt = max_over_ranks(time.perf_counter() - t0)
+    ctx.enable_kernel_timing(False)
+    iters_all = sum_over_ranks(st["iters"])
+    frames_all = sum_over_ranks(a.steps)
+
+    # ---- point-to-plane mode (extra fields) ---------------------------------------
+    pl = None
+    if not a.no_p2plane:
+        run(a.warmup, opts_pl, 16, None)
+        sp = {"iters": 0, "n": 0, "m": 0, "ok": 0, "kernel_ms": 0.0, "launches": 0}
+        barrier()
+        ctx.synchronize()
+        t1 = time.perf_counter()
+        run(a.steps, opts_pl, 16, sp)
+        ctx.synchronize()
+        barrier()
+        dtp = max_over_ranks(time.perf_counter() - t1)
+        pl = {"iterations_per_s": sum_over_ranks(sp["iters"]) / dtp,
+              "frames_per_s": sum_over_ranks(a.steps) / dtp,
+              "mean_iterations_per_pair": sp["iters"] / max(1, a.steps),
+              "ms_per_pair": 1000.0 * dtp / a.steps,
+              "k_p2plane_avg_us": 1000.0 * sp["kernel_ms"] / max(1, sp["launches"])}
+
+    # ---- roofline of the dominant kernel (k_p2point, HIP events) --------------------
+    avg_ms = st["kernel_ms"] / max(1, st["launches"])
+    n_avg = st["n"] / max(1, a.steps)
+    m_avg = st["m"] / max(1, a.steps)
+    nleaves = 1
+    while nleaves * 16 < m_avg:
+        nleaves *= 2
+    s_idx = 64 * nleaves + 4 * (nleaves + 1)
+    alg_bytes = 12 * n_avg + 12 * m_avg + s_idx  # SURVEY.md §8d fused P2POINT iteration
+    achieved = alg_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    traffic = load_traffic()
+
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+    cpu = None
+    if not a.no_cpu and world == 1:
+        cpu = cpu_baseline(a.width, a.height, a.cpu_iters)
+    value = iters_all / dt
+    out = {
+        "metric": METRIC, "value": value, "unit": "ICP iterations/s", "n_gpus": world,
+        "steps": a.steps, "warmup": a.warmup, "ms_per_step": 1000.0 * dt / a.steps,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (seeded procedural RGB-D room, ray-cast u16 depth, 1 mm noise, "
+                "~3% invalid)",
+        "config": {"workload": f"{a.width}x{a.height} synthetic RGB-D stream, per frame: "
+                               f"unproject + index build + AlignIcp3d P2POINT_REF "
+                               f"{a.iters} iters (reference loop)",
+                   "width": a.width, "height": a.height, "iters_per_pair": a.iters,
+                   "points_per_frame": round(n_avg), "frames_cycled": nfr,
+                   "accumulation": "fp64 partial sums", "parallelism": f"replica{world}"},
+        "frames_per_s": frames_all / dt,
+        "pairs_ok": st["ok"],
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "k_p2point", "avg_us": 1000.0 * avg_ms,
+                     "alg_bytes_per_launch": alg_bytes},
+        "cpu_baseline": cpu,
+    }
+    if pl is not None:
+        out["p2plane"] = pl
+    if cpu is not None:
+        out["speedup_vs_cpu_baseline"] = value / cpu["value"]
+    print(json.dumps(out))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

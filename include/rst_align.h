@@ -1,0 +1,216 @@
+/*
+ * rst_align.h -- C ABI of the MI355X-native rs_tracker/align ICP path.
+ *
+ * Drop-in boundary for the reference's align module
+ * (yycho0108/RealsenseTracker, rs_tracker/align/include/rs_tracker/align/
+ * align_icp.hpp:14-24).  Plain pointers and sizes only; every entry point
+ * returns an int status:
+ *     0  ok
+ *     1  the reference's `false` (fewer than 3 points, or mean cost NaN /
+ *        >= 10000 -- align_icp.cpp:77-79,157-160)
+ *    <0  rst_status error (HIP / RCCL / argument)
+ *
+ * Clouds are AoS xyz float32 (point i at xyz[3i..3i+2]); this is the byte
+ * layout of the reference's Cloud3f = cho::core::PointCloud<float,3>
+ * (Eigen 3xN column-major, types.hpp:14).  Poses are 4x4 float32
+ * column-major, the layout of Eigen::Isometry3f::matrix().
+ *
+ * Entry points ending in _device take device (HBM) pointers; the others take
+ * host pointers and copy through pinned staging buffers owned by the context.
+ * A context is bound to one GPU and one HIP stream; calls on one context are
+ * not thread-safe, distinct contexts are independent (reentrant).
+ */
+#ifndef RST_ALIGN_H_
+#define RST_ALIGN_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RST_ABI_VERSION 1
+
+typedef enum {
+  RST_OK = 0,
+  RST_FALSE = 1,          /* reference bool false */
+  RST_E_ARG = -1,         /* invalid argument */
+  RST_E_HIP = -2,         /* HIP runtime error */
+  RST_E_NOMEM = -3,       /* allocation failure */
+  RST_E_NODEVICE = -4,    /* no GPU / bad device ordinal */
+  RST_E_COMM = -5,        /* RCCL error */
+  RST_E_STATE = -6        /* object in wrong state (e.g. normals missing) */
+} rst_status;
+
+typedef enum {
+  /* the reference's point-to-point ICP with annealed Geman-McClure weights,
+   * fp64 cross-covariance, Kabsch/SVD, fixed max_iter (align_icp.cpp:92-153) */
+  RST_P2POINT_REF = 0,
+  /* build's own point-to-plane Gauss-Newton (no reference counterpart;
+   * needs target normals; converges on |dxi| < eps) */
+  RST_P2PLANE = 1
+} rst_icp_mode;
+
+typedef struct {
+  int32_t max_iter;       /* 128 at both reference call sites */
+  int32_t mode;           /* rst_icp_mode */
+  float mu0;              /* initial mu (align_icp.cpp:91): 1.0 */
+  int32_t anneal_every;   /* mu /= anneal_div every N iters (:96-98): 8 */
+  float anneal_div;       /* 1.4 */
+  float p2plane_eps;      /* P2PLANE: stop when |xi| < eps (1e-6) */
+  float p2plane_mu;       /* P2PLANE: GM scale on plane residual (m^2) */
+  float p2plane_max_dist; /* P2PLANE: reject NN beyond this (m); 0 = off */
+  int32_t reserved[8];
+} rst_icp_opts;
+
+typedef struct {
+  float fx, fy, cx, cy;   /* pinhole intrinsics (rs_driver.cpp:264-280) */
+  int32_t width, height;
+  float depth_scale;      /* metres per depth unit (RealSense: 0.001) */
+  float min_depth, max_depth; /* valid range in metres; 0 = no limit */
+} rst_intrinsics;
+
+typedef struct rst_ctx rst_ctx;
+typedef struct rst_target rst_target;
+typedef struct rst_scene rst_scene;
+typedef struct rst_comm rst_comm;
+
+/* ---- library ------------------------------------------------------------ */
+int rst_abi_version(void);
+const char* rst_status_string(int status);
+void rst_icp_opts_default(rst_icp_opts* opts);
+int rst_device_count(int* count);
+
+/* ---- context (one GPU, one stream) -------------------------------------- */
+int rst_ctx_create(int device, rst_ctx** out);
+int rst_ctx_destroy(rst_ctx* ctx);
+/* Use an external hipStream_t (e.g. torch.cuda.current_stream()); NULL
+ * restores the context's own stream. */
+int rst_ctx_set_stream(rst_ctx* ctx, void* hip_stream);
+int rst_ctx_synchronize(rst_ctx* ctx);
+/* Average duration (ms) of the dominant per-iteration kernel over the last
+ * align call, measured with HIP events on the context's stream; and the
+ * number of launches it covers.  Used by bench.py's roofline. */
+int rst_ctx_last_kernel_time(rst_ctx* ctx, float* avg_ms, int32_t* launches);
+/* Enable/disable per-iteration kernel timing (adds events; default off). */
+int rst_ctx_enable_kernel_timing(rst_ctx* ctx, int enable);
+
+/* ---- target index (replaces KDTree3f{dst,16}; kdtree.hpp:27-57) --------- */
+/* Builds the exact-NN index (Morton-ordered bounding-volume hierarchy) over
+ * m target points.  Unlike the reference's tree the handle owns a device
+ * copy, so dst need not outlive it. */
+int rst_target_build(rst_ctx* ctx, const float* xyz, int64_t m,
+                     rst_target** out);
+int rst_target_build_device(rst_ctx* ctx, const float* d_xyz, int64_t m,
+                            rst_target** out);
+int rst_target_free(rst_target* tgt);
+int64_t rst_target_size(const rst_target* tgt);
+
+/* kNN-PCA normals (ComputeNormals + OrientNormals,
+ * point_cloud_utils.cpp:176-216), stored in the handle for P2PLANE. */
+int rst_target_compute_normals(rst_ctx* ctx, rst_target* tgt, int k,
+                               const float viewpoint[3]);
+/* Copy normals out in the target's original point order (host m*3). */
+int rst_target_get_normals(rst_ctx* ctx, const rst_target* tgt,
+                           float* normals);
+
+/* Exact 1-NN per query (KDTree3f::query(p, 1, &j, &d2), kdtree.hpp:51-57):
+ * idx = target index, d2 = squared L2 distance in float with nanoflann's
+ * op order; ties -> lowest index; non-finite query -> (0, FLT_MAX). */
+int rst_target_query_nn(rst_ctx* ctx, const rst_target* tgt, const float* q,
+                        int64_t nq, int32_t* idx, float* d2);
+int rst_target_query_nn_device(rst_ctx* ctx, const rst_target* tgt,
+                               const float* d_q, int64_t nq, int32_t* d_idx,
+                               float* d_d2);
+/* Exact k-NN (k <= 32), results sorted by (d2, idx). */
+int rst_target_query_knn(rst_ctx* ctx, const rst_target* tgt, const float* q,
+                         int64_t nq, int k, int32_t* idx, float* d2);
+
+/* ---- ICP (AlignIcp3d, align_icp.cpp:73-167) ----------------------------- */
+/* 5-arg overload: prebuilt target.  pose_inout = initial guess in, result
+ * out (left untouched on the early false return).  mean_cost may be NULL;
+ * for RST_P2POINT_REF it is sqrt(sum d2 / n) of the last iteration (:157). */
+int rst_icp_align(rst_ctx* ctx, const float* src, int64_t n,
+                  const rst_target* tgt, const rst_icp_opts* opts,
+                  float pose_inout[16], float* mean_cost);
+/* 4-arg overload: builds the target index from dst first (:163-167). */
+int rst_icp_align_clouds(rst_ctx* ctx, const float* src, int64_t n,
+                         const float* dst, int64_t m,
+                         const rst_icp_opts* opts, float pose_inout[16],
+                         float* mean_cost);
+/* Device-resident source (HBM pointer); pose stays a host array. */
+int rst_icp_align_device(rst_ctx* ctx, const float* d_src, int64_t n,
+                         const rst_target* tgt, const rst_icp_opts* opts,
+                         float pose_inout[16], float* mean_cost);
+/* Source already prepared as a target handle (its Morton order is reused
+ * as a coherent query order -- the replay loop uses each frame twice). */
+int rst_icp_align_prepared(rst_ctx* ctx, const rst_target* src,
+                           const rst_target* tgt, const rst_icp_opts* opts,
+                           float pose_inout[16], float* mean_cost,
+                           int32_t* iterations_run);
+
+/* The per-iteration solve of AlignIcp3d / SolveKabsch (align_icp.cpp:58-69,
+ * 139-151) run by the device solve kernel on a given fp64 cross-covariance
+ * (column-major) and float means: R = float(U V^T), R.col(2) *= -1 when
+ * det(R) < 0, t = dmean - R smean, quaternion round trip. */
+int rst_kabsch_solve(rst_ctx* ctx, const double cov[9], const float smean[3],
+                     const float dmean[3], float pose_out[16]);
+
+/* ComputeCentroid (point_cloud_utils.cpp:92-98), fp64 accumulation. */
+int rst_compute_centroid(rst_ctx* ctx, const float* xyz, int64_t n,
+                         float out[3]);
+
+/* ---- depth -> xyz (rs2::pointcloud::calculate at data_source_rs.cpp:89) -- */
+/* Pinhole deprojection of a u16 depth image.  Invalid pixels (0, or outside
+ * [min_depth,max_depth]) are dropped when keep_invalid == 0 (order
+ * preserving compaction) or written as (0,0,0) like the reference's NaN->0
+ * copy (data_source_rs.cpp:34-41).  n_out receives the point count. */
+int rst_unproject(rst_ctx* ctx, const uint16_t* depth,
+                  const rst_intrinsics* K, int keep_invalid, float* xyz_out,
+                  int64_t* n_out);
+int rst_unproject_device(rst_ctx* ctx, const uint16_t* d_depth,
+                         const rst_intrinsics* K, int keep_invalid,
+                         float* d_xyz_out, int64_t* n_out);
+/* Fused frame preparation: depth (device) -> points -> target handle
+ * (+ normals when normals_k > 0).  One call per incoming frame. */
+int rst_frame_prepare_device(rst_ctx* ctx, const uint16_t* d_depth,
+                             const rst_intrinsics* K, int normals_k,
+                             rst_target** out);
+
+/* ---- synthetic frame source (driver; replaces the camera) --------------- */
+/* Procedural room (walls + random spheres/boxes), seeded. */
+int rst_scene_create(uint64_t seed, rst_scene** out);
+int rst_scene_destroy(rst_scene* scene);
+/* Ray-cast u16 depth for camera pose T_wc (camera->world, col-major 4x4):
+ * z-depth quantised by depth_scale, Gaussian noise sigma (metres), a
+ * fraction of pixels dropped to 0; deterministic in noise_seed. */
+int rst_scene_render_depth(const rst_scene* scene, const float T_wc[16],
+                           const rst_intrinsics* K, uint64_t noise_seed,
+                           float noise_sigma, float invalid_frac,
+                           uint16_t* depth_out);
+/* Smooth camera trajectory through the room; frame -> T_wc. */
+int rst_scene_trajectory(const rst_scene* scene, int32_t frame,
+                         float T_wc_out[16]);
+/* RandomSource::GetCloud (data_source.hpp:29-36): uniform [-1,1]^3,
+ * seeded (the reference's is unseeded). */
+int rst_random_cloud(uint64_t seed, int64_t n, float* xyz_out);
+
+/* ---- multi-GPU: source shards + one RCCL all-reduce per iteration ------- */
+#define RST_COMM_ID_BYTES 128
+int rst_comm_get_unique_id(char id_out[RST_COMM_ID_BYTES]);
+int rst_comm_create(rst_ctx* ctx, const char id[RST_COMM_ID_BYTES],
+                    int nranks, int rank, rst_comm** out);
+int rst_comm_destroy(rst_comm* comm);
+/* Every rank passes its own source shard and the full (replicated) target;
+ * the fp64 partial sums are all-reduced each iteration and every rank
+ * solves the same pose.  n_total = sum of shard sizes (ranks agree). */
+int rst_icp_align_sharded_device(rst_ctx* ctx, rst_comm* comm,
+                                 const float* d_src_shard, int64_t n_shard,
+                                 const rst_target* tgt,
+                                 const rst_icp_opts* opts,
+                                 float pose_inout[16], float* mean_cost);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RST_ALIGN_H_ */

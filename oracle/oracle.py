@@ -1,0 +1,216 @@
+"""ctypes wrapper of the CPU oracle (oracle/liboracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg, always as the checker.  The product
+(realsensetracker_amd/) never imports this module.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+LIB = HERE / "liboracle.so"
+
+_f = C.POINTER(C.c_float)
+_d = C.POINTER(C.c_double)
+_i = C.POINTER(C.c_int32)
+_u16 = C.POINTER(C.c_uint16)
+_lib = None
+
+
+class _Trace(C.Structure):
+    _fields_ = [("pose", _f), ("cost", _f), ("mu", _f), ("cov", _d), ("dmean", _f),
+                ("nn_idx0", _i), ("nn_d20", _f)]
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not LIB.exists():
+            build()
+        L = C.CDLL(str(LIB))
+        P = C.c_void_p
+        L.orc_kdtree_build.restype = P
+        L.orc_kdtree_build.argtypes = [_f, C.c_int64, C.c_int]
+        L.orc_kdtree_free.argtypes = [P]
+        L.orc_kdtree_knn.argtypes = [P, _f, C.c_int, _i, _f]
+        L.orc_nn_batch.argtypes = [P, _f, C.c_int64, _i, _f]
+        L.orc_nn_bruteforce.argtypes = [_f, C.c_int64, _f, C.c_int64, _i, _f]
+        L.orc_centroid.argtypes = [_f, C.c_int64, _f]
+        L.orc_transform_points.argtypes = [_f, _f, C.c_int64, _f]
+        L.orc_jacobi_svd3.argtypes = [_d, _d, _d, _d]
+        L.orc_kabsch_pose.argtypes = [_d, _f, _f, _f]
+        L.orc_align_icp.restype = C.c_int
+        L.orc_align_icp.argtypes = [_f, C.c_int64, _f, C.c_int64, P, C.c_int, _f, _f,
+                                    C.POINTER(_Trace)]
+        L.orc_align_icp_ex.restype = C.c_int
+        L.orc_align_icp_ex.argtypes = [_f, C.c_int64, _f, C.c_int64, P, C.c_int, _f, _f,
+                                       C.POINTER(_Trace), C.c_int]
+        L.orc_p2point_partials.argtypes = [_f, C.c_int64, P, _f, _f, _f, C.c_float, _d]
+        L.orc_compute_normals.argtypes = [_f, C.c_int64, P, C.c_int, _f, _f]
+        L.orc_unproject.restype = C.c_int64
+        L.orc_unproject.argtypes = [_u16, C.c_int, C.c_int, _f, C.c_float, C.c_int, _f]
+        L.orc_align_p2plane.restype = C.c_int
+        L.orc_align_p2plane.argtypes = [_f, C.c_int64, _f, _f, C.c_int64, P, C.c_int,
+                                        C.c_float, C.c_float, C.c_float, _f, _f]
+        _lib = L
+    return _lib
+
+
+def _fp(a):
+    return a.ctypes.data_as(_f)
+
+
+def _cloud(x):
+    a = np.ascontiguousarray(np.asarray(x, np.float32))
+    assert a.ndim == 2 and a.shape[1] == 3
+    return a
+
+
+def _cm(T):
+    return np.ascontiguousarray(np.asarray(T, np.float32).reshape(4, 4).T).reshape(16).copy()
+
+
+def _uncm(b):
+    return np.asarray(b, np.float32).reshape(4, 4).T.copy()
+
+
+class KDTree:
+    def __init__(self, cloud, leaf: int = 16):
+        self.cloud = _cloud(cloud)  # the tree references it (kdtree.hpp:30)
+        self.h = lib().orc_kdtree_build(_fp(self.cloud), self.cloud.shape[0], leaf)
+
+    def query(self, q, k: int = 1):
+        q = _cloud(q)
+        n = q.shape[0]
+        if k == 1:
+            idx = np.zeros(n, np.int32)
+            d2 = np.zeros(n, np.float32)
+            lib().orc_nn_batch(self.h, _fp(q), n, idx.ctypes.data_as(_i), _fp(d2))
+            return idx, d2
+        idx = np.zeros((n, k), np.int32)
+        d2 = np.zeros((n, k), np.float32)
+        for i in range(n):
+            lib().orc_kdtree_knn(self.h, _fp(q[i]), k, idx[i].ctypes.data_as(_i), _fp(d2[i]))
+        return idx, d2
+
+    def __del__(self):
+        try:
+            lib().orc_kdtree_free(self.h)
+        except Exception:
+            pass
+
+
+def nn_bruteforce(dst, q):
+    dst, q = _cloud(dst), _cloud(q)
+    idx = np.zeros(q.shape[0], np.int32)
+    d2 = np.zeros(q.shape[0], np.float32)
+    lib().orc_nn_bruteforce(_fp(dst), dst.shape[0], _fp(q), q.shape[0],
+                            idx.ctypes.data_as(_i), _fp(d2))
+    return idx, d2
+
+
+def centroid(cloud):
+    a = _cloud(cloud)
+    out = np.zeros(3, np.float32)
+    lib().orc_centroid(_fp(a), a.shape[0], _fp(out))
+    return out
+
+
+def transform_points(T, cloud):
+    a = _cloud(cloud)
+    out = np.zeros_like(a)
+    lib().orc_transform_points(_fp(_cm(T)), _fp(a), a.shape[0], _fp(out))
+    return out
+
+
+def jacobi_svd3(A):
+    a = np.ascontiguousarray(np.asarray(A, np.float64).T).reshape(9)
+    u = np.zeros(9)
+    s = np.zeros(3)
+    v = np.zeros(9)
+    lib().orc_jacobi_svd3(a.ctypes.data_as(_d), u.ctypes.data_as(_d), s.ctypes.data_as(_d),
+                          v.ctypes.data_as(_d))
+    return u.reshape(3, 3).T, s, v.reshape(3, 3).T
+
+
+def kabsch_pose(cov, smean, dmean):
+    c = np.ascontiguousarray(np.asarray(cov, np.float64).T).reshape(9)
+    out = np.zeros(16, np.float32)
+    lib().orc_kabsch_pose(c.ctypes.data_as(_d), _fp(np.asarray(smean, np.float32)),
+                          _fp(np.asarray(dmean, np.float32)), _fp(out))
+    return _uncm(out)
+
+
+def align_icp(src, dst, max_iter=128, T=None, tree: KDTree | None = None, trace=False,
+              sum_mode: int = 0):
+    """AlignIcp3d restatement.  Returns (ok, pose, mean_cost, trace-dict|None).
+    sum_mode 0 = the reference's fp32 sequential sums; 1 = fp64 sums (the
+    GPU's reduction arithmetic)."""
+    s, d = _cloud(src), _cloud(dst)
+    buf = _cm(np.eye(4) if T is None else T)
+    mc = C.c_float(0)
+    tr = None
+    trp = None
+    if trace and max_iter > 0:
+        tr = {"pose": np.zeros((max_iter, 16), np.float32), "cost": np.zeros(max_iter, np.float32),
+              "mu": np.zeros(max_iter, np.float32), "cov": np.zeros((max_iter, 9), np.float64),
+              "dmean": np.zeros((max_iter, 3), np.float32),
+              "nn_idx0": np.zeros(s.shape[0], np.int32), "nn_d20": np.zeros(s.shape[0], np.float32)}
+        t = _Trace(_fp(tr["pose"]), _fp(tr["cost"]), _fp(tr["mu"]),
+                   tr["cov"].ctypes.data_as(_d), _fp(tr["dmean"]),
+                   tr["nn_idx0"].ctypes.data_as(_i), _fp(tr["nn_d20"]))
+        trp = C.byref(t)
+    ok = lib().orc_align_icp_ex(_fp(s), s.shape[0], _fp(d), d.shape[0],
+                                tree.h if tree is not None else None, max_iter, _fp(buf),
+                                C.byref(mc), trp, int(sum_mode))
+    if tr is not None:
+        tr["pose"] = np.stack([_uncm(p) for p in tr["pose"]])
+        tr["cov"] = np.stack([c.reshape(3, 3).T for c in tr["cov"]])
+    return bool(ok), _uncm(buf), float(mc.value), tr
+
+
+def p2point_partials(src, tree: KDTree, pose, smean, mu):
+    s = _cloud(src)
+    out = np.zeros(16)
+    lib().orc_p2point_partials(_fp(s), s.shape[0], tree.h, _fp(tree.cloud), _fp(_cm(pose)),
+                               _fp(np.asarray(smean, np.float32)), float(mu),
+                               out.ctypes.data_as(_d))
+    return out
+
+
+def compute_normals(cloud, k=16, viewpoint=(0, 0, 0), tree: KDTree | None = None):
+    a = _cloud(cloud)
+    t = tree or KDTree(a, 16)
+    out = np.zeros_like(a)
+    lib().orc_compute_normals(_fp(a), a.shape[0], t.h, k, _fp(np.asarray(viewpoint, np.float32)),
+                              _fp(out))
+    return out
+
+
+def unproject(depth, K4, depth_scale=0.001, keep_invalid=False):
+    d = np.ascontiguousarray(depth, np.uint16)
+    h, w = d.shape
+    out = np.zeros((h * w, 3), np.float32)
+    n = lib().orc_unproject(d.ctypes.data_as(_u16), w, h, _fp(np.asarray(K4, np.float32)),
+                            depth_scale, int(keep_invalid), _fp(out))
+    return out[:n].copy()
+
+
+def align_p2plane(src, dst, dst_normals, max_iter=30, eps=1e-6, mu=4e-4, max_dist=0.0, T=None,
+                  tree: KDTree | None = None):
+    s, d, nn = _cloud(src), _cloud(dst), _cloud(dst_normals)
+    buf = _cm(np.eye(4) if T is None else T)
+    mc = C.c_float(0)
+    it = lib().orc_align_p2plane(_fp(s), s.shape[0], _fp(d), _fp(nn), d.shape[0],
+                                 tree.h if tree is not None else None, max_iter, eps, mu,
+                                 max_dist, _fp(buf), C.byref(mc))
+    return it, _uncm(buf), float(mc.value)

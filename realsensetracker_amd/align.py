@@ -1,0 +1,269 @@
+"""Host-side mirror of the reference's rs_tracker align / common API.
+
+Same names, argument meaning and failure behaviour as
+rs_tracker/align/include/rs_tracker/align/align_icp.hpp:14-24 and
+rs_tracker/common/include/rs_tracker/common/point_cloud_utils.hpp:9-28, over
+the MI355X C ABI (include/rst_align.h):
+
+    AlignIcp3d(src, dst, max_iter, T)            -> bool  (T updated in place)
+    AlignIcp3d(src, dst, dst_tree, max_iter, T)  -> bool
+    KDTree3f(dst, leaf_max_size=16).query(p, k)  -> (indices, sq_dists)
+    ComputeCentroid(cloud)                       -> (3,) float32
+    ComputeNormals(cloud, tree, k)               -> (n, 3) float32
+    OrientNormals(cloud, viewpoint, normals)     (in place)
+
+Clouds are (n, 3) float32 arrays (the byte layout of Cloud3f); transforms are
+4x4 float32 arrays in math orientation.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import sys
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib as L
+
+
+class Context:
+    """One GPU + one HIP stream (rst_ctx)."""
+
+    def __init__(self, device: int = 0):
+        self._h = C.c_void_p()
+        L.check(L.lib().rst_ctx_create(device, C.byref(self._h)), "rst_ctx_create")
+        self.device = device
+
+    @property
+    def handle(self):
+        return self._h
+
+    def set_stream(self, hip_stream: int | None):
+        L.check(L.lib().rst_ctx_set_stream(self._h, C.c_void_p(hip_stream or 0)),
+                "rst_ctx_set_stream")
+
+    def synchronize(self):
+        L.check(L.lib().rst_ctx_synchronize(self._h), "rst_ctx_synchronize")
+
+    def enable_kernel_timing(self, on: bool = True):
+        L.check(L.lib().rst_ctx_enable_kernel_timing(self._h, int(on)), "timing")
+
+    def last_kernel_time(self):
+        ms = C.c_float(0)
+        n = C.c_int32(0)
+        L.check(L.lib().rst_ctx_last_kernel_time(self._h, C.byref(ms), C.byref(n)), "timing")
+        return ms.value, n.value
+
+    def close(self):
+        if self._h:
+            L.lib().rst_ctx_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        # no HIP calls while the interpreter tears down (objects die in
+        # arbitrary order then; the OS reclaims the device memory)
+        if sys.is_finalizing():
+            return
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+_contexts: dict[int, Context] = {}
+
+
+def get_context(device: int = 0) -> Context:
+    if device not in _contexts:
+        _contexts[device] = Context(device)
+    return _contexts[device]
+
+
+class Target:
+    """Prepared target cloud in HBM: Morton-sorted points + exact-NN BVH
+    (+ normals).  Replaces KDTree3f{dst, 16} (kdtree.hpp:27-57)."""
+
+    def __init__(self, handle: C.c_void_p, ctx: Context):
+        self._h = handle
+        self.ctx = ctx
+
+    @classmethod
+    def build(cls, cloud, ctx: Context | None = None) -> "Target":
+        ctx = ctx or get_context()
+        a = L.as_cloud(cloud)
+        h = C.c_void_p()
+        L.check(L.lib().rst_target_build(ctx.handle, L.fptr(a), a.shape[0], C.byref(h)),
+                "rst_target_build")
+        return cls(h, ctx)
+
+    @classmethod
+    def build_device(cls, d_xyz_ptr: int, m: int, ctx: Context | None = None) -> "Target":
+        ctx = ctx or get_context()
+        h = C.c_void_p()
+        L.check(L.lib().rst_target_build_device(ctx.handle, C.c_void_p(d_xyz_ptr), m,
+                                                C.byref(h)), "rst_target_build_device")
+        return cls(h, ctx)
+
+    @classmethod
+    def from_depth_device(cls, d_depth_ptr: int, K: "L.Intrinsics", normals_k: int = 0,
+                          ctx: Context | None = None) -> "Target":
+        ctx = ctx or get_context()
+        h = C.c_void_p()
+        L.check(L.lib().rst_frame_prepare_device(ctx.handle, C.c_void_p(d_depth_ptr),
+                                                 C.byref(K), normals_k, C.byref(h)),
+                "rst_frame_prepare_device")
+        return cls(h, ctx)
+
+    @property
+    def handle(self):
+        return self._h
+
+    def __len__(self):
+        return int(L.lib().rst_target_size(self._h))
+
+    def query(self, points, num_closest: int = 1):
+        """KDTree3f::query / knnSearch: exact k-NN, (idx, sq_dist) arrays."""
+        q = L.as_cloud(points)
+        n = q.shape[0]
+        if num_closest == 1:
+            idx = np.zeros(n, np.int32)
+            d2 = np.zeros(n, np.float32)
+            L.check(L.lib().rst_target_query_nn(self.ctx.handle, self._h, L.fptr(q), n,
+                                                L.iptr(idx), L.fptr(d2)), "query_nn")
+            return idx, d2
+        idx = np.zeros((n, num_closest), np.int32)
+        d2 = np.zeros((n, num_closest), np.float32)
+        L.check(L.lib().rst_target_query_knn(self.ctx.handle, self._h, L.fptr(q), n,
+                                             num_closest, L.iptr(idx), L.fptr(d2)), "query_knn")
+        return idx, d2
+
+    def compute_normals(self, k: int = 16, viewpoint=(0.0, 0.0, 0.0)):
+        vp = np.asarray(viewpoint, np.float32)
+        L.check(L.lib().rst_target_compute_normals(self.ctx.handle, self._h, k, L.fptr(vp)),
+                "compute_normals")
+
+    def normals(self) -> np.ndarray:
+        out = np.zeros((len(self), 3), np.float32)
+        L.check(L.lib().rst_target_get_normals(self.ctx.handle, self._h, L.fptr(out)),
+                "get_normals")
+        return out
+
+    def free(self):
+        if self._h:
+            L.lib().rst_target_free(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        if sys.is_finalizing():
+            return
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class KDTree3f(Target):
+    """Name-compatible constructor: KDTree3f(dst, leaf_max_size=16)."""
+
+    def __init__(self, cloud, leaf_max_size: int = 16, ctx: Context | None = None):
+        ctx = ctx or get_context()
+        a = L.as_cloud(cloud)
+        h = C.c_void_p()
+        L.check(L.lib().rst_target_build(ctx.handle, L.fptr(a), a.shape[0], C.byref(h)),
+                "rst_target_build")
+        super().__init__(h, ctx)
+        self.leaf_max_size = leaf_max_size
+
+
+@dataclass
+class IcpResult:
+    ok: bool
+    pose: np.ndarray
+    mean_cost: float
+    iterations: int
+
+
+def align(src, target: Target, pose=None, opts: "L.IcpOpts | None" = None) -> IcpResult:
+    """Full-result form of AlignIcp3d over a prepared target."""
+    ctx = target.ctx
+    s = L.as_cloud(src)
+    pose = np.eye(4, dtype=np.float32) if pose is None else np.asarray(pose, np.float32)
+    buf = L.pose_to_cm(pose)
+    mc = C.c_float(0)
+    o = opts if opts is not None else L.default_opts()
+    st = L.check(L.lib().rst_icp_align(ctx.handle, L.fptr(s), s.shape[0], target.handle,
+                                       C.byref(o), L.fptr(buf), C.byref(mc)), "rst_icp_align")
+    return IcpResult(st == L.RST_OK, L.cm_to_pose(buf), float(mc.value), int(o.max_iter))
+
+
+def align_prepared(src: Target, target: Target, pose=None,
+                   opts: "L.IcpOpts | None" = None) -> IcpResult:
+    pose = np.eye(4, dtype=np.float32) if pose is None else np.asarray(pose, np.float32)
+    buf = L.pose_to_cm(pose)
+    mc = C.c_float(0)
+    it = C.c_int32(0)
+    o = opts if opts is not None else L.default_opts()
+    st = L.check(L.lib().rst_icp_align_prepared(target.ctx.handle, src.handle, target.handle,
+                                                C.byref(o), L.fptr(buf), C.byref(mc),
+                                                C.byref(it)), "rst_icp_align_prepared")
+    return IcpResult(st == L.RST_OK, L.cm_to_pose(buf), float(mc.value), int(it.value))
+
+
+def AlignIcp3d(src, dst, *args, opts: "L.IcpOpts | None" = None) -> bool:
+    """AlignIcp3d(src, dst, max_iter, T) / AlignIcp3d(src, dst, dst_tree, max_iter, T).
+
+    T (4x4 float32) is the in/out initial guess, left untouched on the early
+    false return (align_icp.cpp:77-79); returns the reference's bool."""
+    if len(args) == 2:
+        tree, (max_iter, T) = None, args
+    elif len(args) == 3:
+        tree, max_iter, T = args
+    else:
+        raise TypeError("AlignIcp3d(src, dst, [dst_tree,] max_iter, transform)")
+    if not (isinstance(T, np.ndarray) and T.shape == (4, 4) and T.dtype == np.float32):
+        raise TypeError("transform must be a (4, 4) float32 ndarray (updated in place)")
+    o = opts if opts is not None else L.default_opts()
+    o.max_iter = int(max_iter)
+    s = L.as_cloud(src)
+    buf = L.pose_to_cm(T)
+    mc = C.c_float(0)
+    if tree is None:
+        d = L.as_cloud(dst)
+        ctx = get_context()
+        st = L.check(L.lib().rst_icp_align_clouds(ctx.handle, L.fptr(s), s.shape[0], L.fptr(d),
+                                                  d.shape[0], C.byref(o), L.fptr(buf),
+                                                  C.byref(mc)), "rst_icp_align_clouds")
+    else:
+        st = L.check(L.lib().rst_icp_align(tree.ctx.handle, L.fptr(s), s.shape[0], tree.handle,
+                                           C.byref(o), L.fptr(buf), C.byref(mc)),
+                     "rst_icp_align")
+    if len(s) >= 3 and len(dst) >= 3:
+        T[...] = L.cm_to_pose(buf)
+    return st == L.RST_OK
+
+
+def ComputeCentroid(cloud, ctx: Context | None = None) -> np.ndarray:
+    ctx = ctx or get_context()
+    a = L.as_cloud(cloud)
+    out = np.zeros(3, np.float32)
+    L.check(L.lib().rst_compute_centroid(ctx.handle, L.fptr(a), a.shape[0], L.fptr(out)),
+            "rst_compute_centroid")
+    return out
+
+
+def ComputeNormals(cloud, tree: Target, num_neighbors: int = 16,
+                   viewpoint=(0.0, 0.0, 0.0)) -> np.ndarray:
+    """kNN-PCA normals of `tree`'s cloud, oriented toward `viewpoint`
+    (the reference always follows ComputeNormals with OrientNormals:
+    fpfh.cpp:247-248, rs_replay_app.cpp:386-387)."""
+    tree.compute_normals(int(num_neighbors), viewpoint)
+    return tree.normals()
+
+
+def OrientNormals(cloud, viewpoint, normals: np.ndarray) -> None:
+    """point_cloud_utils.cpp:206-216: flip n where (p - viewpoint).n > 0."""
+    p = L.as_cloud(cloud)
+    v = np.asarray(viewpoint, np.float32)
+    ray = p - v
+    dot = ray[:, 0] * normals[:, 0] + (ray[:, 1] * normals[:, 1] + ray[:, 2] * normals[:, 2])
+    normals[dot > 0] *= -1.0

@@ -1,0 +1,114 @@
+"""Build the MI355X library (HIP for gfx950) in-tree.
+
+    python -m realsensetracker_amd.build           # library + app
+    python -m realsensetracker_amd.build --lib     # library only
+
+Outputs (git-ignored, shipped to the GPU box by gpurun):
+    realsensetracker_amd/lib/librst_align.so   C-ABI of include/rst_align.h
+    realsensetracker_amd/lib/rs_replay_app     host C++ replay app
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import hashlib
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+ROOT = PKG.parent
+CSRC = PKG / "csrc"
+LIBDIR = PKG / "lib"
+OBJDIR = ROOT / "build" / "obj"
+INCLUDE = ROOT / "include"
+ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
+ARCH = os.environ.get("RST_OFFLOAD_ARCH", "gfx950")
+
+SOURCES = ["build.hip", "query.hip", "icp.hip", "capi.hip", "unproject.hip", "comm.hip", "synth.cpp"]
+HEADERS = ["rst_internal.hpp", "rst_device.hpp"]
+LIB_NAME = "librst_align.so"
+
+# -ffp-contract=off: reference-exact rounding of the transform / distance /
+# weight arithmetic (DESIGN.md "Numerics").
+CFLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", f"--offload-arch={ARCH}",
+          "-Wall", "-Wno-unused-function", "-Wno-unused-result", f"-I{INCLUDE}", f"-I{CSRC}"]
+
+
+def _hipcc() -> str:
+    h = ROCM / "bin" / "hipcc"
+    return str(h) if h.exists() else "hipcc"
+
+
+def _stamp(src: Path) -> str:
+    h = hashlib.sha1()
+    for p in [src] + [CSRC / x for x in HEADERS] + [INCLUDE / "rst_align.h"]:
+        h.update(p.read_bytes())
+    h.update(" ".join(CFLAGS).encode())
+    return h.hexdigest()[:16]
+
+
+def _compile(src: str) -> Path:
+    s = CSRC / src
+    obj = OBJDIR / (s.stem + "." + _stamp(s) + ".o")
+    if obj.exists():
+        return obj
+    cmd = [_hipcc(), *CFLAGS, "-c", str(s), "-o", str(obj)]
+    if src.endswith(".cpp"):
+        cmd.insert(1, "-x")
+        cmd.insert(2, "hip")
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return obj
+
+
+def build_library(jobs: int = 8) -> Path:
+    OBJDIR.mkdir(parents=True, exist_ok=True)
+    LIBDIR.mkdir(parents=True, exist_ok=True)
+    with cf.ThreadPoolExecutor(max_workers=max(1, min(jobs, len(SOURCES)))) as ex:
+        objs = list(ex.map(_compile, SOURCES))
+    out = LIBDIR / LIB_NAME
+    tmp = LIBDIR / (LIB_NAME + ".tmp")
+    cmd = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", str(tmp),
+           *map(str, objs), f"-L{ROCM / 'lib'}", "-lrccl", f"-Wl,-rpath,{ROCM / 'lib'}"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    os.replace(tmp, out)
+    return out
+
+
+def build_app() -> Path:
+    """Host C++ replay app over the C-ABI (rs_replay_app.cpp's loop)."""
+    src = CSRC / "app" / "rs_replay_app.cpp"
+    out = LIBDIR / "rs_replay_app"
+    if not src.exists():
+        return out
+    cmd = ["g++", "-O2", "-std=c++17", f"-I{INCLUDE}", str(src), "-o", str(out),
+           f"-L{LIBDIR}", "-lrst_align", "-Wl,-rpath,$ORIGIN"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"app build failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return out
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--lib", action="store_true", help="library only")
+    ap.add_argument("--clean", action="store_true")
+    ap.add_argument("-j", type=int, default=8)
+    a = ap.parse_args(argv)
+    if a.clean and OBJDIR.exists():
+        shutil.rmtree(OBJDIR)
+    p = build_library(a.j)
+    print(p)
+    if not a.lib:
+        print(build_app())
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,425 @@
+// build.hip -- target index build: the MI355X replacement of
+// KDTree3f{dst, 16} (align_icp.cpp:165, kdtree.hpp:27-35).
+//
+// Pipeline (all on the context stream, no host round trip):
+//   bbox (2 kernels) -> 30-bit Morton keys -> 4-pass LSD radix sort
+//   (8,8,8,6 bits; per-block digit histograms, one scan, stable scatter with
+//   wave-ballot ranking) -> gather Morton-ordered float4 points
+//   (x, y, z, original-index bits) -> leaf boxes -> internal levels.
+// The BVH is an implicit heap (root 1, children 2k/2k+1) over nleaves =
+// next_pow2(ceil(m/16)) leaves of ~m/nleaves consecutive sorted points.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+
+#include "rst_device.hpp"
+#include "rst_internal.hpp"
+
+namespace rst {
+namespace {
+
+constexpr int kBS = 256;
+
+// ---- bounding box ------------------------------------------------------------
+// AoS xyz input (the reference's Cloud3f layout); non-finite coordinates are
+// ignored (fminf/fmaxf drop NaN; inf filtered explicitly).
+__global__ __launch_bounds__(kBS) void k_bbox_partial(const float* __restrict__ xyz,
+                                                      int64_t m,
+                                                      float* __restrict__ part) {
+  float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX};
+  float mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+  for (int64_t i = blockIdx.x * (int64_t)kBS + threadIdx.x; i < m;
+       i += (int64_t)gridDim.x * kBS) {
+    const float x = xyz[3 * i], y = xyz[3 * i + 1], z = xyz[3 * i + 2];
+    if (__builtin_isfinite(x) && __builtin_isfinite(y) && __builtin_isfinite(z)) {
+      mn[0] = fminf(mn[0], x); mx[0] = fmaxf(mx[0], x);
+      mn[1] = fminf(mn[1], y); mx[1] = fmaxf(mx[1], y);
+      mn[2] = fminf(mn[2], z); mx[2] = fmaxf(mx[2], z);
+    }
+  }
+  __shared__ float s[kBS / kWave][6];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float v[6];
+  for (int d = 0; d < 3; ++d) {
+    v[d] = wave_min(mn[d]);
+    v[3 + d] = wave_max(mx[d]);
+  }
+  if (lane == 0)
+    for (int d = 0; d < 6; ++d) s[w][d] = v[d];
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    const int d = threadIdx.x;
+    float r = s[0][d];
+    for (int k = 1; k < kBS / kWave; ++k)
+      r = d < 3 ? fminf(r, s[k][d]) : fmaxf(r, s[k][d]);
+    part[blockIdx.x * 6 + d] = r;
+  }
+}
+
+__global__ __launch_bounds__(kBS) void k_bbox_final(const float* __restrict__ part,
+                                                    int nparts,
+                                                    float* __restrict__ bbox) {
+  __shared__ float s[kBS][6];
+  float v[6] = {FLT_MAX, FLT_MAX, FLT_MAX, -FLT_MAX, -FLT_MAX, -FLT_MAX};
+  for (int i = threadIdx.x; i < nparts; i += kBS)
+    for (int d = 0; d < 6; ++d)
+      v[d] = d < 3 ? fminf(v[d], part[i * 6 + d]) : fmaxf(v[d], part[i * 6 + d]);
+  for (int d = 0; d < 6; ++d) s[threadIdx.x][d] = v[d];
+  __syncthreads();
+  for (int st = kBS / 2; st > 0; st >>= 1) {
+    if (threadIdx.x < st)
+      for (int d = 0; d < 6; ++d)
+        s[threadIdx.x][d] = d < 3 ? fminf(s[threadIdx.x][d], s[threadIdx.x + st][d])
+                                  : fmaxf(s[threadIdx.x][d], s[threadIdx.x + st][d]);
+    __syncthreads();
+  }
+  if (threadIdx.x < 6) bbox[threadIdx.x] = s[0][threadIdx.x];
+}
+
+// ---- Morton keys ---------------------------------------------------------------
+__device__ __forceinline__ uint32_t spread10(uint32_t v) {
+  v &= 0x3ffu;
+  v = (v | (v << 16)) & 0x030000FFu;
+  v = (v | (v << 8)) & 0x0300F00Fu;
+  v = (v | (v << 4)) & 0x030C30C3u;
+  v = (v | (v << 2)) & 0x09249249u;
+  return v;
+}
+
+__global__ __launch_bounds__(kBS) void k_morton(const float* __restrict__ xyz,
+                                                int64_t m,
+                                                const float* __restrict__ bbox,
+                                                uint32_t* __restrict__ keys,
+                                                uint32_t* __restrict__ vals) {
+  const int64_t i = blockIdx.x * (int64_t)kBS + threadIdx.x;
+  if (i >= m) return;
+  const float lx = bbox[0], ly = bbox[1], lz = bbox[2];
+  const float ext = fmaxf(fmaxf(bbox[3] - lx, bbox[4] - ly), bbox[5] - lz);
+  const float sc = ext > 0.0f ? 1023.0f / ext : 0.0f;
+  const float x = xyz[3 * i], y = xyz[3 * i + 1], z = xyz[3 * i + 2];
+  uint32_t code;
+  if (__builtin_isfinite(x) && __builtin_isfinite(y) && __builtin_isfinite(z)) {
+    const uint32_t qx = (uint32_t)fminf(fmaxf((x - lx) * sc, 0.0f), 1023.0f);
+    const uint32_t qy = (uint32_t)fminf(fmaxf((y - ly) * sc, 0.0f), 1023.0f);
+    const uint32_t qz = (uint32_t)fminf(fmaxf((z - lz) * sc, 0.0f), 1023.0f);
+    code = (spread10(qx) << 2) | (spread10(qy) << 1) | spread10(qz);
+  } else {
+    code = 0x3fffffffu;  // non-finite points sort last
+  }
+  keys[i] = code;
+  vals[i] = (uint32_t)i;
+}
+
+// ---- LSD radix sort (8-bit digits, stable) ---------------------------------------
+constexpr int kRsItems = 8;
+constexpr int kRsTile = kBS * kRsItems;
+
+__global__ __launch_bounds__(kBS) void k_rs_hist(const uint32_t* __restrict__ keys,
+                                                 int64_t n, int shift,
+                                                 uint32_t mask, int nblocks,
+                                                 uint32_t* __restrict__ hist) {
+  __shared__ uint32_t h[256];
+  h[threadIdx.x] = 0;
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * kRsTile;
+#pragma unroll
+  for (int r = 0; r < kRsItems; ++r) {
+    const int64_t i = base + r * kBS + threadIdx.x;
+    if (i < n) atomicAdd(&h[(keys[i] >> shift) & mask], 1u);
+  }
+  __syncthreads();
+  hist[(int64_t)threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
+}
+
+// Exclusive scan of `total` u32 in place by one 1024-thread block.
+__global__ __launch_bounds__(1024) void k_scan_single(uint32_t* __restrict__ a,
+                                                      int64_t total) {
+  __shared__ uint32_t s[1024];
+  const int64_t per = (total + 1023) / 1024;
+  const int64_t b = threadIdx.x * per;
+  const int64_t e = b + per < total ? b + per : total;
+  uint32_t sum = 0;
+  for (int64_t i = b; i < e; ++i) sum += a[i];
+  s[threadIdx.x] = sum;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {
+    uint32_t v = threadIdx.x >= off ? s[threadIdx.x - off] : 0u;
+    __syncthreads();
+    s[threadIdx.x] += v;
+    __syncthreads();
+  }
+  uint32_t run = s[threadIdx.x] - sum;  // exclusive prefix of this chunk
+  for (int64_t i = b; i < e; ++i) {
+    const uint32_t v = a[i];
+    a[i] = run;
+    run += v;
+  }
+}
+
+__global__ __launch_bounds__(kBS) void k_rs_scatter(
+    const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
+    uint32_t* __restrict__ kout, uint32_t* __restrict__ vout, int64_t n,
+    int shift, uint32_t mask, int nblocks, const uint32_t* __restrict__ hist) {
+  __shared__ uint32_t base[256];
+  __shared__ uint32_t wcnt[kBS / kWave][257];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  base[threadIdx.x] = hist[(int64_t)threadIdx.x * nblocks + blockIdx.x];
+  for (int k = 0; k < kBS / kWave; ++k) wcnt[k][threadIdx.x] = 0;
+  if (threadIdx.x == 0)
+    for (int k = 0; k < kBS / kWave; ++k) wcnt[k][256] = 0;
+  __syncthreads();
+  const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  const int64_t tile = (int64_t)blockIdx.x * kRsTile;
+  for (int r = 0; r < kRsItems; ++r) {
+    const int64_t i = tile + r * kBS + threadIdx.x;
+    const bool valid = i < n;
+    const uint32_t key = valid ? kin[i] : 0u;
+    const uint32_t val = valid ? vin[i] : 0u;
+    const uint32_t d = valid ? ((key >> shift) & mask) : 256u;
+    // lanes of this wave holding the same digit (9-bit match incl. sentinel)
+    uint64_t peers = ~0ull;
+#pragma unroll
+    for (int b = 0; b < 9; ++b) {
+      const bool bit = (d >> b) & 1u;
+      const uint64_t bal = __ballot(bit);
+      peers &= bit ? bal : ~bal;
+    }
+    const uint32_t rank = __popcll(peers & lt);
+    const int leader = 63 - __clzll(peers);
+    if (lane == leader) wcnt[w][d] = __popcll(peers);
+    __syncthreads();
+    if (valid) {
+      uint32_t off = 0;
+      for (int k = 0; k < w; ++k) off += wcnt[k][d];
+      const uint32_t pos = base[d] + off + rank;
+      kout[pos] = key;
+      vout[pos] = val;
+    }
+    __syncthreads();
+    {
+      const int dd = threadIdx.x;
+      uint32_t tot = 0;
+      for (int k = 0; k < kBS / kWave; ++k) {
+        tot += wcnt[k][dd];
+        wcnt[k][dd] = 0;
+      }
+      base[dd] += tot;
+      if (threadIdx.x == 0)
+        for (int k = 0; k < kBS / kWave; ++k) wcnt[k][256] = 0;
+    }
+    __syncthreads();
+  }
+}
+
+// ---- sorted points + BVH -------------------------------------------------------
+__global__ __launch_bounds__(kBS) void k_gather(const float* __restrict__ xyz,
+                                                const uint32_t* __restrict__ perm,
+                                                int64_t m, float4* __restrict__ pts) {
+  const int64_t i = blockIdx.x * (int64_t)kBS + threadIdx.x;
+  if (i >= m) return;
+  const uint32_t j = perm[i];
+  pts[i] = make_float4(xyz[3 * (int64_t)j], xyz[3 * (int64_t)j + 1],
+                       xyz[3 * (int64_t)j + 2], __int_as_float((int)j));
+}
+
+// sorted position of original index 0 (the reference's dst.GetPoint(0)
+// when nanoflann returns no neighbour)
+__global__ __launch_bounds__(kBS) void k_find_pos0(const uint32_t* __restrict__ perm, int64_t m,
+                                                   int32_t* __restrict__ out) {
+  const int64_t i = blockIdx.x * (int64_t)kBS + threadIdx.x;
+  if (i < m && perm[i] == 0u) *out = (int32_t)i;
+}
+
+__global__ __launch_bounds__(kBS) void k_leaf_start(int32_t* __restrict__ ls,
+                                                    int64_t m, int nleaves) {
+  const int64_t L = blockIdx.x * (int64_t)kBS + threadIdx.x;
+  if (L > nleaves) return;
+  ls[L] = (int32_t)(L * m / nleaves);
+}
+
+__global__ __launch_bounds__(kBS) void k_leaf_boxes(const float4* __restrict__ pts,
+                                                    const int32_t* __restrict__ ls,
+                                                    int nleaves,
+                                                    float4* __restrict__ nodes) {
+  const int L = blockIdx.x * kBS + threadIdx.x;
+  if (L >= nleaves) return;
+  float4 lo = make_float4(INFINITY, INFINITY, INFINITY, 0.0f);
+  float4 hi = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.0f);
+  for (int i = ls[L]; i < ls[L + 1]; ++i) {
+    const float4 p = pts[i];
+    if (!(__builtin_isfinite(p.x) && __builtin_isfinite(p.y) && __builtin_isfinite(p.z)))
+      continue;
+    lo.x = fminf(lo.x, p.x); lo.y = fminf(lo.y, p.y); lo.z = fminf(lo.z, p.z);
+    hi.x = fmaxf(hi.x, p.x); hi.y = fmaxf(hi.y, p.y); hi.z = fmaxf(hi.z, p.z);
+  }
+  const int k = nleaves + L;
+  nodes[2 * k] = lo;
+  nodes[2 * k + 1] = hi;
+}
+
+__device__ __forceinline__ void make_internal(float4* __restrict__ nodes, int k) {
+  const float4 l0 = nodes[2 * (2 * k)], h0 = nodes[2 * (2 * k) + 1];
+  const float4 l1 = nodes[2 * (2 * k + 1)], h1 = nodes[2 * (2 * k + 1) + 1];
+  float4 lo, hi;
+  lo.x = fminf(l0.x, l1.x); lo.y = fminf(l0.y, l1.y); lo.z = fminf(l0.z, l1.z);
+  hi.x = fmaxf(h0.x, h1.x); hi.y = fmaxf(h0.y, h1.y); hi.z = fmaxf(h0.z, h1.z);
+  const bool e0 = !(l0.x <= h0.x), e1 = !(l1.x <= h1.x);  // empty children
+  float split;
+  int ab;
+  if (e0 || e1) {
+    // near child = the non-empty one: left if right is empty
+    ab = 0;
+    split = e1 ? INFINITY : -INFINITY;
+  } else {
+    const float c0[3] = {0.5f * (l0.x + h0.x), 0.5f * (l0.y + h0.y), 0.5f * (l0.z + h0.z)};
+    const float c1[3] = {0.5f * (l1.x + h1.x), 0.5f * (l1.y + h1.y), 0.5f * (l1.z + h1.z)};
+    int ax = 0;
+    float best = fabsf(c1[0] - c0[0]);
+    for (int a = 1; a < 3; ++a)
+      if (fabsf(c1[a] - c0[a]) > best) {
+        best = fabsf(c1[a] - c0[a]);
+        ax = a;
+      }
+    split = 0.5f * (c0[ax] + c1[ax]);
+    ab = ax | (c0[ax] <= c1[ax] ? 0 : 4);
+  }
+  lo.w = split;
+  hi.w = __int_as_float(ab);
+  nodes[2 * k] = lo;
+  nodes[2 * k + 1] = hi;
+}
+
+__global__ __launch_bounds__(kBS) void k_level(float4* __restrict__ nodes, int lo_k,
+                                               int count) {
+  const int i = blockIdx.x * kBS + threadIdx.x;
+  if (i < count) make_internal(nodes, lo_k + i);
+}
+
+// all levels with fewer than 2*kBS nodes, one block, barrier per level
+__global__ __launch_bounds__(kBS) void k_levels_top(float4* __restrict__ nodes,
+                                                    int top_count) {
+  for (int cnt = top_count; cnt >= 1; cnt >>= 1) {
+    for (int i = threadIdx.x; i < cnt; i += kBS) make_internal(nodes, cnt + i);
+    __syncthreads();
+  }
+}
+
+inline int blocks_for(int64_t n, int per = kBS) {
+  return (int)std::max<int64_t>(1, (n + per - 1) / per);
+}
+
+}  // namespace
+
+int radix_sort_pairs(rst_ctx* ctx, uint32_t* keys, uint32_t* vals, uint32_t* ktmp,
+                     uint32_t* vtmp, uint32_t* hist, int64_t n) {
+  hipStream_t st = ctx->stream;
+  const int nb = blocks_for(n, kRsTile);
+  const int shifts[4] = {0, 8, 16, 24};
+  const uint32_t masks[4] = {0xff, 0xff, 0xff, 0x3f};
+  uint32_t *ka = keys, *va = vals, *kb = ktmp, *vb = vtmp;
+  for (int p = 0; p < 4; ++p) {
+    k_rs_hist<<<nb, kBS, 0, st>>>(ka, n, shifts[p], masks[p], nb, hist);
+    k_scan_single<<<1, 1024, 0, st>>>(hist, (int64_t)256 * nb);
+    k_rs_scatter<<<nb, kBS, 0, st>>>(ka, va, kb, vb, n, shifts[p], masks[p], nb, hist);
+    std::swap(ka, kb);
+    std::swap(va, vb);
+  }
+  RST_HIP(hipGetLastError());
+  return RST_OK;  // 4 passes: result back in keys/vals
+}
+
+size_t target_index_bytes(const rst_target* t) {
+  if (!t->has_bvh) return 0;
+  return (size_t)4 * t->nleaves * sizeof(float4) + (size_t)(t->nleaves + 1) * 4;
+}
+
+int target_build_device(rst_ctx* ctx, const float* d_xyz, int64_t m, bool with_bvh,
+                        rst_target** out) {
+  if (!ctx || !out || m < 0 || (m > 0 && !d_xyz)) return RST_E_ARG;
+  if (m >= (int64_t)1 << 31) return RST_E_ARG;
+  rst_target* t = new rst_target();
+  t->ctx = ctx;
+  t->m = m;
+  hipStream_t st = ctx->stream;
+  int64_t nl = 1;
+  while (nl * kLeafTarget < m) nl <<= 1;
+  t->nleaves = (int32_t)nl;
+  const int64_t mp = std::max<int64_t>(m, 1);
+  if (hipMalloc(&t->pts, sizeof(float4) * mp) != hipSuccess) {
+    delete t;
+    return RST_E_NOMEM;
+  }
+  if (with_bvh) {
+    if (hipMalloc(&t->nodes, sizeof(float4) * 4 * nl) != hipSuccess ||
+        hipMalloc(&t->leaf_start, sizeof(int32_t) * (nl + 1)) != hipSuccess) {
+      rst_target_free(t);
+      return RST_E_NOMEM;
+    }
+    t->has_bvh = true;
+  }
+  if (m == 0) {
+    *out = t;
+    return RST_OK;
+  }
+  // workspace: bbox partials | bbox | keys | vals | ktmp | vtmp | hist
+  const int nbb = std::min(1024, blocks_for(m));
+  const int nb = blocks_for(m, kRsTile);
+  size_t off = 0;
+  auto carve = [&](size_t bytes) {
+    size_t o = off;
+    off += (bytes + 255) & ~(size_t)255;
+    return o;
+  };
+  const size_t o_part = carve(sizeof(float) * 6 * nbb);
+  const size_t o_bbox = carve(sizeof(float) * 8);
+  const size_t o_k = carve(sizeof(uint32_t) * m);
+  const size_t o_v = carve(sizeof(uint32_t) * m);
+  const size_t o_kt = carve(sizeof(uint32_t) * m);
+  const size_t o_vt = carve(sizeof(uint32_t) * m);
+  const size_t o_h = carve(sizeof(uint32_t) * 256 * (size_t)nb);
+  void* ws = nullptr;
+  int s = ctx_workspace(ctx, off, &ws);
+  if (s < 0) {
+    rst_target_free(t);
+    return s;
+  }
+  char* w = (char*)ws;
+  float* part = (float*)(w + o_part);
+  float* bbox = (float*)(w + o_bbox);
+  uint32_t* keys = (uint32_t*)(w + o_k);
+  uint32_t* vals = (uint32_t*)(w + o_v);
+  k_bbox_partial<<<nbb, kBS, 0, st>>>(d_xyz, m, part);
+  k_bbox_final<<<1, kBS, 0, st>>>(part, nbb, bbox);
+  k_morton<<<blocks_for(m), kBS, 0, st>>>(d_xyz, m, bbox, keys, vals);
+  s = radix_sort_pairs(ctx, keys, vals, (uint32_t*)(w + o_kt), (uint32_t*)(w + o_vt),
+                       (uint32_t*)(w + o_h), m);
+  if (s < 0) {
+    rst_target_free(t);
+    return s;
+  }
+  k_gather<<<blocks_for(m), kBS, 0, st>>>(d_xyz, vals, m, t->pts);
+  k_find_pos0<<<blocks_for(m), kBS, 0, st>>>(vals, m, (int32_t*)(bbox + 6));
+  if (with_bvh) {
+    k_leaf_start<<<blocks_for(nl + 1), kBS, 0, st>>>(t->leaf_start, m, (int)nl);
+    k_leaf_boxes<<<blocks_for(nl), kBS, 0, st>>>(t->pts, t->leaf_start, (int)nl, t->nodes);
+    int64_t cnt = nl / 2;
+    while (cnt >= 2 * kBS) {
+      k_level<<<blocks_for(cnt), kBS, 0, st>>>(t->nodes, (int)cnt, (int)cnt);
+      cnt >>= 1;
+    }
+    if (cnt >= 1) k_levels_top<<<1, kBS, 0, st>>>(t->nodes, (int)cnt);
+  }
+  if (hipGetLastError() != hipSuccess ||
+      hipMemcpyAsync(t->bbox, bbox, sizeof(float) * 6, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipMemcpyAsync(&t->pos0, bbox + 6, sizeof(int32_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess) {
+    rst_target_free(t);
+    return RST_E_HIP;
+  }
+  *out = t;
+  return RST_OK;
+}
+
+}  // namespace rst

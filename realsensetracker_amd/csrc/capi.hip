@@ -1,0 +1,400 @@
+// capi.hip -- extern "C" entry points of include/rst_align.h.
+//
+// Host-pointer entry points stage through the context's pinned buffer and
+// device workspace; *_device entry points take HBM pointers directly.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+
+#include "rst_internal.hpp"
+
+namespace rst {
+
+static thread_local char g_last_error[512] = {0};
+
+void set_last_error(hipError_t e, const char* what, const char* file, int line) {
+  snprintf(g_last_error, sizeof(g_last_error), "%s failed: %s (%s:%d)", what,
+           hipGetErrorString(e), file, line);
+  if (getenv("RST_VERBOSE")) fprintf(stderr, "[rst] %s\n", g_last_error);
+}
+
+int ctx_workspace(rst_ctx* ctx, size_t bytes, void** out) {
+  if (bytes > ctx->ws_bytes) {
+    if (ctx->ws) {
+      RST_HIP(hipStreamSynchronize(ctx->stream));
+      RST_HIP(hipFree(ctx->ws));
+      ctx->ws = nullptr;
+      ctx->ws_bytes = 0;
+    }
+    const size_t sz = std::max<size_t>(bytes + bytes / 4, 1 << 20);
+    if (hipMalloc(&ctx->ws, sz) != hipSuccess) return RST_E_NOMEM;
+    ctx->ws_bytes = sz;
+  }
+  *out = ctx->ws;
+  return RST_OK;
+}
+
+int ctx_pinned(rst_ctx* ctx, size_t bytes, void** out) {
+  if (bytes > ctx->pinned_bytes) {
+    if (ctx->pinned) {
+      RST_HIP(hipStreamSynchronize(ctx->stream));
+      RST_HIP(hipHostFree(ctx->pinned));
+      ctx->pinned = nullptr;
+      ctx->pinned_bytes = 0;
+    }
+    const size_t sz = std::max<size_t>(bytes + bytes / 4, 1 << 20);
+    if (hipHostMalloc(&ctx->pinned, sz, hipHostMallocDefault) != hipSuccess) return RST_E_NOMEM;
+    ctx->pinned_bytes = sz;
+  }
+  *out = ctx->pinned;
+  return RST_OK;
+}
+
+int ctx_slab(rst_ctx* ctx, size_t bytes, double** out) {
+  if (bytes > ctx->slab_bytes) {
+    if (ctx->d_slab) {
+      RST_HIP(hipStreamSynchronize(ctx->stream));
+      RST_HIP(hipFree(ctx->d_slab));
+      ctx->d_slab = nullptr;
+      ctx->slab_bytes = 0;
+    }
+    const size_t sz = std::max<size_t>(bytes + bytes / 4, 1 << 16);
+    if (hipMalloc(&ctx->d_slab, sz) != hipSuccess) return RST_E_NOMEM;
+    ctx->slab_bytes = sz;
+  }
+  *out = ctx->d_slab;
+  return RST_OK;
+}
+
+// Upload host AoS xyz (n points) into a dedicated device buffer.
+static int upload_xyz(rst_ctx* ctx, const float* h, int64_t n, float** d_out) {
+  *d_out = nullptr;
+  const size_t bytes = sizeof(float) * 3 * (size_t)std::max<int64_t>(n, 1);
+  float* d = nullptr;
+  if (hipMalloc(&d, bytes) != hipSuccess) return RST_E_NOMEM;
+  if (n > 0) {
+    void* pin = nullptr;
+    int s = ctx_pinned(ctx, bytes, &pin);
+    if (s < 0) {
+      hipFree(d);
+      return s;
+    }
+    memcpy(pin, h, sizeof(float) * 3 * n);
+    if (hipMemcpyAsync(d, pin, sizeof(float) * 3 * n, hipMemcpyHostToDevice, ctx->stream) !=
+        hipSuccess) {
+      hipFree(d);
+      return RST_E_HIP;
+    }
+  }
+  *d_out = d;
+  return RST_OK;
+}
+
+}  // namespace rst
+
+using namespace rst;
+
+extern "C" {
+
+int rst_abi_version(void) { return RST_ABI_VERSION; }
+
+const char* rst_status_string(int s) {
+  switch (s) {
+    case RST_OK: return "ok";
+    case RST_FALSE: return "false (reference failure condition)";
+    case RST_E_ARG: return "invalid argument";
+    case RST_E_HIP: return g_last_error[0] ? g_last_error : "HIP error";
+    case RST_E_NOMEM: return "out of memory";
+    case RST_E_NODEVICE: return "no GPU device";
+    case RST_E_COMM: return "RCCL error";
+    case RST_E_STATE: return "object in wrong state";
+    default: return "unknown status";
+  }
+}
+
+void rst_icp_opts_default(rst_icp_opts* o) {
+  if (!o) return;
+  memset(o, 0, sizeof(*o));
+  o->max_iter = 128;         // rs_align_app.cpp:303, rs_replay_app.cpp:251
+  o->mode = RST_P2POINT_REF;
+  o->mu0 = 1.0f;             // align_icp.cpp:91
+  o->anneal_every = 8;       // :96
+  o->anneal_div = 1.4f;      // :97
+  o->p2plane_eps = 1e-6f;
+  o->p2plane_mu = 4e-4f;     // (2 cm)^2
+  o->p2plane_max_dist = 0.0f;
+}
+
+int rst_device_count(int* count) {
+  if (!count) return RST_E_ARG;
+  int c = 0;
+  if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+  *count = c;
+  return RST_OK;
+}
+
+int rst_ctx_create(int device, rst_ctx** out) {
+  if (!out) return RST_E_ARG;
+  *out = nullptr;
+  int c = 0;
+  if (hipGetDeviceCount(&c) != hipSuccess || c <= 0) return RST_E_NODEVICE;
+  if (device < 0 || device >= c) return RST_E_NODEVICE;
+  RST_HIP(hipSetDevice(device));
+  rst_ctx* ctx = new rst_ctx();
+  ctx->device = device;
+  if (hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipMalloc(&ctx->d_state, sizeof(IcpState)) != hipSuccess ||
+      hipHostMalloc(&ctx->h_state, sizeof(IcpState), hipHostMallocDefault) != hipSuccess) {
+    rst_ctx_destroy(ctx);
+    return RST_E_HIP;
+  }
+  ctx->stream = ctx->own_stream;
+  *out = ctx;
+  return RST_OK;
+}
+
+int rst_ctx_destroy(rst_ctx* ctx) {
+  if (!ctx) return RST_OK;
+  hipSetDevice(ctx->device);
+  if (ctx->stream) hipStreamSynchronize(ctx->stream);
+  for (hipEvent_t e : ctx->ev) hipEventDestroy(e);
+  if (ctx->ws) hipFree(ctx->ws);
+  if (ctx->pinned) hipHostFree(ctx->pinned);
+  if (ctx->d_state) hipFree(ctx->d_state);
+  if (ctx->h_state) hipHostFree(ctx->h_state);
+  if (ctx->d_slab) hipFree(ctx->d_slab);
+  if (ctx->own_stream) hipStreamDestroy(ctx->own_stream);
+  delete ctx;
+  return RST_OK;
+}
+
+int rst_ctx_set_stream(rst_ctx* ctx, void* s) {
+  if (!ctx) return RST_E_ARG;
+  ctx->stream = s ? (hipStream_t)s : ctx->own_stream;
+  return RST_OK;
+}
+
+int rst_ctx_synchronize(rst_ctx* ctx) {
+  if (!ctx) return RST_E_ARG;
+  RST_HIP(hipStreamSynchronize(ctx->stream));
+  return RST_OK;
+}
+
+int rst_ctx_last_kernel_time(rst_ctx* ctx, float* avg_ms, int32_t* launches) {
+  if (!ctx) return RST_E_ARG;
+  if (avg_ms) *avg_ms = ctx->last_kernel_ms;
+  if (launches) *launches = ctx->last_kernel_launches;
+  return RST_OK;
+}
+
+int rst_ctx_enable_kernel_timing(rst_ctx* ctx, int enable) {
+  if (!ctx) return RST_E_ARG;
+  ctx->timing = enable != 0;
+  return RST_OK;
+}
+
+// ---- target ------------------------------------------------------------------
+int rst_target_build(rst_ctx* ctx, const float* xyz, int64_t m, rst_target** out) {
+  if (!ctx || !out || m < 0 || (m > 0 && !xyz)) return RST_E_ARG;
+  RST_HIP(hipSetDevice(ctx->device));
+  float* d = nullptr;
+  RST_CHECK(upload_xyz(ctx, xyz, m, &d));
+  int s = target_build_device(ctx, d, m, true, out);
+  hipStreamSynchronize(ctx->stream);
+  hipFree(d);
+  return s;
+}
+
+int rst_target_build_device(rst_ctx* ctx, const float* d_xyz, int64_t m, rst_target** out) {
+  if (!ctx) return RST_E_ARG;
+  RST_HIP(hipSetDevice(ctx->device));
+  return target_build_device(ctx, d_xyz, m, true, out);
+}
+
+int rst_target_free(rst_target* t) {
+  if (!t) return RST_OK;
+  // hipFree waits for outstanding work on the buffers; the handle does not
+  // touch its context, which may already be gone
+  if (t->pts) hipFree(t->pts);
+  if (t->nodes) hipFree(t->nodes);
+  if (t->leaf_start) hipFree(t->leaf_start);
+  if (t->nrm) hipFree(t->nrm);
+  delete t;
+  return RST_OK;
+}
+
+int64_t rst_target_size(const rst_target* t) { return t ? t->m : -1; }
+
+int rst_target_compute_normals(rst_ctx* ctx, rst_target* t, int k, const float vp[3]) {
+  if (!ctx || !t) return RST_E_ARG;
+  RST_HIP(hipSetDevice(ctx->device));
+  RST_CHECK(compute_normals(ctx, t, k, vp));
+  RST_HIP(hipStreamSynchronize(ctx->stream));
+  return RST_OK;
+}
+
+int rst_target_get_normals(rst_ctx* ctx, const rst_target* t, float* normals) {
+  if (!ctx || !t || (t->m > 0 && !normals)) return RST_E_ARG;
+  if (!t->nrm) return RST_E_STATE;
+  if (t->m == 0) return RST_OK;
+  std::vector<float4> pts(t->m), nrm(t->m);
+  RST_HIP(hipMemcpyAsync(pts.data(), t->pts, sizeof(float4) * t->m, hipMemcpyDeviceToHost,
+                         ctx->stream));
+  RST_HIP(hipMemcpyAsync(nrm.data(), t->nrm, sizeof(float4) * t->m, hipMemcpyDeviceToHost,
+                         ctx->stream));
+  RST_HIP(hipStreamSynchronize(ctx->stream));
+  for (int64_t i = 0; i < t->m; ++i) {
+    int j;
+    memcpy(&j, &pts[i].w, sizeof(int));
+    normals[3 * (int64_t)j + 0] = nrm[i].x;
+    normals[3 * (int64_t)j + 1] = nrm[i].y;
+    normals[3 * (int64_t)j + 2] = nrm[i].z;
+  }
+  return RST_OK;
+}
+
+int rst_target_query_nn_device(rst_ctx* ctx, const rst_target* t, const float* d_q, int64_t nq,
+                               int32_t* d_idx, float* d_d2) {
+  if (!ctx || !t || nq < 0 || (nq > 0 && (!d_q || !d_idx || !d_d2))) return RST_E_ARG;
+  RST_HIP(hipSetDevice(ctx->device));
+  return query_nn_device(ctx, t, d_q, nq, d_idx, d_d2);
+}
+
+int rst_target_query_nn(rst_ctx* ctx, const rst_target* t, const float* q, int64_t nq,
+                        int32_t* idx, float* d2) {
+  if (!ctx || !t || nq < 0 || (nq > 0 && (!q || !idx || !d2))) return RST_E_ARG;
+  if (nq == 0) return RST_OK;
+  RST_HIP(hipSetDevice(ctx->device));
+  float* dq = nullptr;
+  RST_CHECK(upload_xyz(ctx, q, nq, &dq));
+  void* dout = nullptr;
+  int s = ctx_workspace(ctx, (sizeof(int32_t) + sizeof(float)) * nq, &dout);
+  if (s >= 0) s = query_nn_device(ctx, t, dq, nq, (int32_t*)dout, (float*)((int32_t*)dout + nq));
+  if (s >= 0) {
+    if (hipMemcpyAsync(idx, dout, sizeof(int32_t) * nq, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+        hipMemcpyAsync(d2, (int32_t*)dout + nq, sizeof(float) * nq, hipMemcpyDeviceToHost,
+                       ctx->stream) != hipSuccess ||
+        hipStreamSynchronize(ctx->stream) != hipSuccess)
+      s = RST_E_HIP;
+  }
+  hipStreamSynchronize(ctx->stream);
+  hipFree(dq);
+  return s < 0 ? s : RST_OK;
+}
+
+int rst_target_query_knn(rst_ctx* ctx, const rst_target* t, const float* q, int64_t nq, int k,
+                         int32_t* idx, float* d2) {
+  if (!ctx || !t || nq < 0 || k < 1 || k > 32 || (nq > 0 && (!q || !idx || !d2)))
+    return RST_E_ARG;
+  if (nq == 0) return RST_OK;
+  RST_HIP(hipSetDevice(ctx->device));
+  float* dq = nullptr;
+  RST_CHECK(upload_xyz(ctx, q, nq, &dq));
+  void* dout = nullptr;
+  const size_t cnt = (size_t)nq * k;
+  int s = ctx_workspace(ctx, (sizeof(int32_t) + sizeof(float)) * cnt, &dout);
+  if (s >= 0)
+    s = query_knn_device(ctx, t, dq, nq, k, (int32_t*)dout, (float*)((int32_t*)dout + cnt));
+  if (s >= 0) {
+    if (hipMemcpyAsync(idx, dout, sizeof(int32_t) * cnt, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+        hipMemcpyAsync(d2, (int32_t*)dout + cnt, sizeof(float) * cnt, hipMemcpyDeviceToHost,
+                       ctx->stream) != hipSuccess ||
+        hipStreamSynchronize(ctx->stream) != hipSuccess)
+      s = RST_E_HIP;
+  }
+  hipStreamSynchronize(ctx->stream);
+  hipFree(dq);
+  return s < 0 ? s : RST_OK;
+}
+
+// ---- ICP ---------------------------------------------------------------------------
+int rst_icp_align_prepared(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
+                           const rst_icp_opts* opts, float pose_inout[16], float* mean_cost,
+                           int32_t* iterations_run) {
+  if (!ctx || !src || !tgt || !pose_inout) return RST_E_ARG;
+  RST_HIP(hipSetDevice(ctx->device));
+  return icp_align_prepared(ctx, src, tgt, opts, pose_inout, mean_cost, iterations_run, nullptr);
+}
+
+int rst_icp_align_device(rst_ctx* ctx, const float* d_src, int64_t n, const rst_target* tgt,
+                         const rst_icp_opts* opts, float pose_inout[16], float* mean_cost) {
+  if (!ctx || !tgt || !pose_inout || n < 0 || (n > 0 && !d_src)) return RST_E_ARG;
+  if (n < 3 || tgt->m < 3) return RST_FALSE;  // align_icp.cpp:77-79
+  RST_HIP(hipSetDevice(ctx->device));
+  rst_target* s = nullptr;
+  RST_CHECK(target_build_device(ctx, d_src, n, false, &s));
+  int r = icp_align_prepared(ctx, s, tgt, opts, pose_inout, mean_cost, nullptr, nullptr);
+  rst_target_free(s);
+  return r;
+}
+
+int rst_icp_align(rst_ctx* ctx, const float* src, int64_t n, const rst_target* tgt,
+                  const rst_icp_opts* opts, float pose_inout[16], float* mean_cost) {
+  if (!ctx || !tgt || !pose_inout || n < 0 || (n > 0 && !src)) return RST_E_ARG;
+  if (n < 3 || tgt->m < 3) return RST_FALSE;  // align_icp.cpp:77-79
+  RST_HIP(hipSetDevice(ctx->device));
+  float* d = nullptr;
+  RST_CHECK(upload_xyz(ctx, src, n, &d));
+  int r = rst_icp_align_device(ctx, d, n, tgt, opts, pose_inout, mean_cost);
+  hipStreamSynchronize(ctx->stream);
+  hipFree(d);
+  return r;
+}
+
+int rst_icp_align_clouds(rst_ctx* ctx, const float* src, int64_t n, const float* dst, int64_t m,
+                         const rst_icp_opts* opts, float pose_inout[16], float* mean_cost) {
+  if (!ctx || !pose_inout || n < 0 || m < 0 || (n > 0 && !src) || (m > 0 && !dst))
+    return RST_E_ARG;
+  if (n < 3 || m < 3) return RST_FALSE;  // align_icp.cpp:77-79
+  rst_target* t = nullptr;
+  RST_CHECK(rst_target_build(ctx, dst, m, &t));  // :165 KDTree3f{dst,16}
+  int r = rst_icp_align(ctx, src, n, t, opts, pose_inout, mean_cost);
+  rst_target_free(t);
+  return r;
+}
+
+int rst_kabsch_solve(rst_ctx* ctx, const double cov[9], const float smean[3],
+                     const float dmean[3], float pose_out[16]) {
+  if (!ctx || !cov || !smean || !dmean || !pose_out) return RST_E_ARG;
+  RST_HIP(hipSetDevice(ctx->device));
+  return kabsch_device(ctx, cov, smean, dmean, pose_out);
+}
+
+int rst_compute_centroid(rst_ctx* ctx, const float* xyz, int64_t n, float out[3]) {
+  if (!ctx || !out || n <= 0 || !xyz) return RST_E_ARG;
+  RST_HIP(hipSetDevice(ctx->device));
+  rst_target* s = nullptr;
+  float* d = nullptr;
+  RST_CHECK(upload_xyz(ctx, xyz, n, &d));
+  int r = target_build_device(ctx, d, n, false, &s);
+  if (r >= 0) {
+    double* slab = nullptr;
+    r = ctx_slab(ctx, sizeof(double) * 4 * 1100, &slab);
+    if (r >= 0) r = centroid_device(ctx, s->pts, n, slab);
+    if (r >= 0) {
+      std::vector<double> h((size_t)r * 4);
+      if (hipMemcpyAsync(h.data(), slab, sizeof(double) * 4 * r, hipMemcpyDeviceToHost,
+                         ctx->stream) != hipSuccess ||
+          hipStreamSynchronize(ctx->stream) != hipSuccess) {
+        r = RST_E_HIP;
+      } else {
+        double acc[4] = {0, 0, 0, 0};
+        for (int b = 0; b < (int)h.size() / 4; ++b)
+          for (int k = 0; k < 4; ++k) acc[k] += h[b * 4 + k];
+        for (int k = 0; k < 3; ++k) out[k] = (float)(acc[k] / (double)n);
+        r = RST_OK;
+      }
+    }
+  }
+  if (s) rst_target_free(s);
+  hipStreamSynchronize(ctx->stream);
+  hipFree(d);
+  return r;
+}
+
+}  // extern "C"

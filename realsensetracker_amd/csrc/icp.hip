@@ -1,0 +1,615 @@
+// icp.hip -- the ICP loop of AlignIcp3d (align_icp.cpp:73-167) on MI355X.
+//
+// Per iteration two launches on one stream, no host round trip:
+//   k_p2point / k_p2plane : one source point per thread -- transform,
+//       exact NN (BVH), robust weight, fp64 partial sums, wave-shuffle +
+//       LDS block reduction -> one slab row per block;
+//   k_solve_*            : one block -- fixed-order reduction of the slab
+//       (bitwise reproducible), then thread 0 solves the 3x3 Kabsch
+//       (P2POINT_REF) or 6x6 normal equations (P2PLANE) and writes the next
+//       pose into the device-resident IcpState.
+// Multi-GPU: the slab is first reduced to one row, all-reduced over RCCL,
+// and every rank solves the same pose (DESIGN.md "Multi-GPU").
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+
+#include "rst_device.hpp"
+#include "rst_internal.hpp"
+
+namespace rst {
+namespace {
+
+constexpr int kBS = 256;
+constexpr int kNP2Point = 16;  // sum w q u^T (9), sum w u (3), sum q (3), sum d2
+constexpr int kNP2Plane = 30;  // A (21), b (6), sum w r^2, count, sum d2
+
+__device__ __forceinline__ Pose3 load_pose(const IcpState* __restrict__ st) {
+  Pose3 P;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) P.r[k] = st->R[k];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) P.t[k] = st->t[k];
+  return P;
+}
+
+// ---- centroid ------------------------------------------------------------------
+__global__ __launch_bounds__(kBS) void k_centroid_partial(const float4* __restrict__ pts,
+                                                          int64_t n,
+                                                          double* __restrict__ slab) {
+  __shared__ double lds[(kBS / kWave) * 4];
+  double v[4] = {0, 0, 0, 0};
+  for (int64_t i = blockIdx.x * (int64_t)kBS + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kBS) {
+    const float4 p = pts[i];
+    v[0] += p.x;
+    v[1] += p.y;
+    v[2] += p.z;
+    v[3] += 1.0;
+  }
+  block_sum_to_slab<4, kBS>(v, lds, slab + blockIdx.x * 4);
+}
+
+// Reduce `rows` slab rows of NV doubles into out[NV] (fixed order).
+template <int NV>
+__device__ __forceinline__ void reduce_slab_rows(const double* __restrict__ slab, int rows,
+                                                 double* __restrict__ red /*[NV][kBS]*/,
+                                                 double* __restrict__ out) {
+  double acc[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) acc[k] = 0.0;
+  for (int b = threadIdx.x; b < rows; b += kBS) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) acc[k] += slab[(int64_t)b * NV + k];
+  }
+#pragma unroll
+  for (int k = 0; k < NV; ++k) red[k * kBS + threadIdx.x] = acc[k];
+  __syncthreads();
+  for (int s = kBS / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s) {
+#pragma unroll
+      for (int k = 0; k < NV; ++k)
+        red[k * kBS + threadIdx.x] += red[k * kBS + threadIdx.x + s];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x < NV) out[threadIdx.x] = red[threadIdx.x * kBS];
+  __syncthreads();
+}
+
+template <int NV>
+__global__ __launch_bounds__(kBS) void k_slab_reduce(const double* __restrict__ slab, int rows,
+                                                     double* __restrict__ out) {
+  __shared__ double red[NV * kBS];
+  reduce_slab_rows<NV>(slab, rows, red, out);
+}
+
+struct InitArgs {
+  float pose[16];
+  float mu0;
+  int32_t need_centroid;
+};
+
+// State initialisation: pose from the caller, mu0, centroid = fp64 sum / n
+// rounded to float (reference: fp32 sequential sum * float(1.0/n),
+// point_cloud_utils.cpp:92-98; DESIGN.md "Numerics").
+__global__ __launch_bounds__(kBS) void k_init_state(const double* __restrict__ cslab, int rows,
+                                                    InitArgs a, IcpState* __restrict__ st) {
+  __shared__ double red[4 * kBS];
+  __shared__ double tot[4];
+  if (a.need_centroid) reduce_slab_rows<4>(cslab, rows, red, tot);
+  if (threadIdx.x == 0) {
+    for (int c = 0; c < 3; ++c)
+      for (int r = 0; r < 3; ++r) {
+        st->R[c * 3 + r] = a.pose[c * 4 + r];
+        st->Rd[c * 3 + r] = a.pose[c * 4 + r];
+      }
+    for (int r = 0; r < 3; ++r) {
+      st->t[r] = a.pose[12 + r];
+      st->td[r] = a.pose[12 + r];
+    }
+    if (a.need_centroid) {
+      const double n = tot[3] > 0 ? tot[3] : 1.0;
+      for (int r = 0; r < 3; ++r) st->smean[r] = (float)(tot[r] / n);
+    } else {
+      for (int r = 0; r < 3; ++r) st->smean[r] = 0.f;
+    }
+    st->mu = a.mu0;
+    st->iter = 0;
+    st->done = 0;
+    st->fail = 0;
+    st->last_cost = 0.f;
+    st->last_xi = 0;
+    st->last_cnt = 0;
+    st->last_d2 = 0;
+  }
+}
+
+// ---- P2POINT_REF -----------------------------------------------------------------
+// Single pass over the correspondences with the source centroid known:
+//   cov = sum w (q - dbar)(s - sbar)^T = sum w q u^T - dbar (sum w u)^T,
+// u = s - sbar in float as at align_icp.cpp:129, dbar = sum q / n.
+__global__ __launch_bounds__(kBS) void k_p2point(BvhView bv, const float4* __restrict__ src,
+                                                 int64_t n, const IcpState* __restrict__ st,
+                                                 int32_t pos0, int32_t* __restrict__ nnpos,
+                                                 double* __restrict__ slab) {
+  __shared__ double lds[(kBS / kWave) * kNP2Point];
+  const Pose3 P = load_pose(st);
+  const float mu = st->mu;
+  const float sm0 = st->smean[0], sm1 = st->smean[1], sm2 = st->smean[2];
+  double v[kNP2Point];
+#pragma unroll
+  for (int k = 0; k < kNP2Point; ++k) v[k] = 0.0;
+  const int64_t i = blockIdx.x * (int64_t)kBS + threadIdx.x;
+  const bool act = i < n;
+  const float4 s = act ? src[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+  float px, py, pz;
+  xform(P, s.x, s.y, s.z, px, py, pz);  // :107
+  float bd;
+  int bi, bp;
+  // :112 exact 1-NN: warm-started from the previous iteration's neighbour,
+  // then one cooperative BVH walk per wave
+  nn_warm(bv, act ? nnpos[i] : -1, px, py, pz, bd, bi, bp);
+  nn_wave(bv, act, px, py, pz, bd, bi, bp);
+  if (act) {
+    nnpos[i] = bp;
+    const float l = mu / (bd + mu);         // :116-117
+    const float w = l * l;
+    const float4 q = bv.pts[bp >= 0 ? bp : pos0];  // no neighbour -> dst[0]
+    const float u0 = s.x - sm0, u1 = s.y - sm1, u2 = s.z - sm2;
+    const double dw = (double)w;
+    const double wq0 = dw * (double)q.x, wq1 = dw * (double)q.y, wq2 = dw * (double)q.z;
+    v[0] = wq0 * u0; v[1] = wq0 * u1; v[2] = wq0 * u2;
+    v[3] = wq1 * u0; v[4] = wq1 * u1; v[5] = wq1 * u2;
+    v[6] = wq2 * u0; v[7] = wq2 * u1; v[8] = wq2 * u2;
+    v[9] = dw * u0; v[10] = dw * u1; v[11] = dw * u2;
+    v[12] = q.x; v[13] = q.y; v[14] = q.z;
+    v[15] = bd;
+  }
+  block_sum_to_slab<kNP2Point, kBS>(v, lds, slab + (int64_t)blockIdx.x * kNP2Point);
+}
+
+// Kabsch solve (align_icp.cpp:139-151; SolveKabsch :58-69): fp64 SVD,
+// R = float(U V^T), reflection fix, t = dmean - R smean, quaternion trip.
+__device__ void kabsch_solve(const double* cov, const float* smean, const float* dmean,
+                             float* Rq, float* t) {
+  double U[9], S[3], V[9];
+  svd3_jacobi(cov, U, S, V);
+  float R[9];
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < 3; ++c) {
+      const double a0 = RST_M3(U, r, 0) * RST_M3(V, c, 0);
+      const double a1 = RST_M3(U, r, 1) * RST_M3(V, c, 1);
+      const double a2 = RST_M3(U, r, 2) * RST_M3(V, c, 2);
+      RST_M3(R, r, c) = (float)(a0 + (a1 + a2));
+    }
+  if (det3f(R) < 0) {  // :143-145 (non-standard fix kept on purpose)
+    for (int r = 0; r < 3; ++r) RST_M3(R, r, 2) *= -1.0f;
+  }
+  for (int r = 0; r < 3; ++r) t[r] = dmean[r] - mv_row(R, r, smean[0], smean[1], smean[2]);
+  quat_roundtrip(R, Rq);  // :151
+}
+
+__global__ void k_kabsch(const double* __restrict__ in /*cov[9] smean[3] dmean[3]*/,
+                         float* __restrict__ out /*pose[16] col-major*/) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  float sm[3], dm[3], Rq[9], t[3];
+  for (int k = 0; k < 3; ++k) {
+    sm[k] = (float)in[9 + k];
+    dm[k] = (float)in[12 + k];
+  }
+  kabsch_solve(in, sm, dm, Rq, t);
+  for (int c = 0; c < 3; ++c) {
+    for (int r = 0; r < 3; ++r) out[c * 4 + r] = Rq[c * 3 + r];
+    out[c * 4 + 3] = 0.f;
+  }
+  for (int r = 0; r < 3; ++r) out[12 + r] = t[r];
+  out[15] = 1.f;
+}
+
+// Kabsch on the reduced sums (align_icp.cpp:122, 139-151).
+__device__ void p2point_update(const double* tot, const IcpParams& prm, IcpState* st,
+                               float* trace) {
+  const double n = (double)prm.n;
+  float dmean[3];
+  for (int r = 0; r < 3; ++r) dmean[r] = (float)(tot[12 + r] / n);
+  double cov[9];
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < 3; ++c)
+      RST_M3(cov, r, c) = tot[r * 3 + c] - (double)dmean[r] * tot[9 + c];
+  float Rq[9], t[3];
+  kabsch_solve(cov, st->smean, dmean, Rq, t);
+  for (int k = 0; k < 9; ++k) st->R[k] = Rq[k];
+  for (int k = 0; k < 3; ++k) st->t[k] = t[k];
+  st->last_cost = (float)tot[15];
+  const int it = st->iter;
+  if (trace) {
+    float* tp = trace + (int64_t)it * 16;
+    for (int c = 0; c < 3; ++c) {
+      for (int r = 0; r < 3; ++r) tp[c * 4 + r] = Rq[c * 3 + r];
+      tp[c * 4 + 3] = 0.f;
+    }
+    for (int r = 0; r < 3; ++r) tp[12 + r] = t[r];
+    tp[15] = 1.f;
+  }
+  const int next = it + 1;
+  st->iter = next;
+  // :96-98 -- mu for iteration `next`
+  if (next > 0 && prm.anneal_every > 0 && next % prm.anneal_every == 0) st->mu = st->mu / prm.anneal_div;
+}
+
+__global__ __launch_bounds__(kBS) void k_solve_p2point(const double* __restrict__ slab, int rows,
+                                                       IcpParams prm, IcpState* __restrict__ st,
+                                                       float* __restrict__ trace) {
+  __shared__ double red[kNP2Point * kBS];
+  __shared__ double tot[kNP2Point];
+  reduce_slab_rows<kNP2Point>(slab, rows, red, tot);
+  if (threadIdx.x == 0) p2point_update(tot, prm, st, trace);
+}
+
+// ---- P2PLANE (build's own mode) -----------------------------------------------------
+// r = n.(p - q), w = (mu/(r^2+mu))^2, J = [p x n ; n]; 21 + 6 + 3 sums.
+__global__ __launch_bounds__(kBS) void k_p2plane(BvhView bv, const float4* __restrict__ nrm,
+                                                 const float4* __restrict__ src, int64_t n,
+                                                 const IcpState* __restrict__ st, float pmu,
+                                                 float max_d2, int32_t* __restrict__ nnpos,
+                                                 double* __restrict__ slab) {
+  __shared__ double lds[(kBS / kWave) * kNP2Plane];
+  if (st->done) return;  // converged: uniform early exit, slab unused
+  const Pose3 P = load_pose(st);
+  double v[kNP2Plane];
+#pragma unroll
+  for (int k = 0; k < kNP2Plane; ++k) v[k] = 0.0;
+  const int64_t i = blockIdx.x * (int64_t)kBS + threadIdx.x;
+  const bool act = i < n;
+  const float4 s = act ? src[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+  float px, py, pz;
+  xform(P, s.x, s.y, s.z, px, py, pz);
+  float bd;
+  int bi, bp;
+  nn_warm(bv, act ? nnpos[i] : -1, px, py, pz, bd, bi, bp);
+  nn_wave(bv, act, px, py, pz, bd, bi, bp);
+  if (act) {
+    nnpos[i] = bp;
+    if (bp >= 0 && bd <= max_d2) {
+      const float4 q = bv.pts[bp];
+      const float4 nn = nrm[bp];
+      const float e0 = px - q.x, e1 = py - q.y, e2 = pz - q.z;
+      const float r = (nn.x * e0 + nn.y * e1) + nn.z * e2;
+      const double dr = (double)r;
+      const double l = (double)pmu / (dr * dr + (double)pmu);
+      const double w = l * l;
+      const double X = px, Y = py, Z = pz, NX = nn.x, NY = nn.y, NZ = nn.z;
+      const double J[6] = {Y * NZ - Z * NY, Z * NX - X * NZ, X * NY - Y * NX, NX, NY, NZ};
+      int k = 0;
+#pragma unroll
+      for (int a = 0; a < 6; ++a) {
+        const double wa = w * J[a];
+#pragma unroll
+        for (int c = 0; c <= a; ++c) v[k++] = wa * J[c];
+      }
+#pragma unroll
+      for (int a = 0; a < 6; ++a) v[21 + a] = w * J[a] * dr;
+      v[27] = w * dr * dr;
+      v[28] = 1.0;
+      v[29] = bd;
+    }
+  }
+  block_sum_to_slab<kNP2Plane, kBS>(v, lds, slab + (int64_t)blockIdx.x * kNP2Plane);
+}
+
+__device__ bool chol6_solve(const double* Ap /*packed lower 21*/, const double* rhs, double* x) {
+  double L[6][6];
+  int k = 0;
+  double A[6][6];
+  for (int a = 0; a < 6; ++a)
+    for (int c = 0; c <= a; ++c) {
+      A[a][c] = Ap[k];
+      A[c][a] = Ap[k];
+      ++k;
+    }
+  for (int i = 0; i < 6; ++i) {
+    for (int j = 0; j <= i; ++j) {
+      double s = A[i][j];
+      for (int q = 0; q < j; ++q) s -= L[i][q] * L[j][q];
+      if (i == j) {
+        if (!(s > 0.0)) return false;
+        L[i][i] = sqrt(s);
+      } else {
+        L[i][j] = s / L[j][j];
+      }
+    }
+  }
+  double y[6];
+  for (int i = 0; i < 6; ++i) {
+    double s = rhs[i];
+    for (int q = 0; q < i; ++q) s -= L[i][q] * y[q];
+    y[i] = s / L[i][i];
+  }
+  for (int i = 5; i >= 0; --i) {
+    double s = y[i];
+    for (int q = i + 1; q < 6; ++q) s -= L[q][i] * x[q];
+    x[i] = s / L[i][i];
+  }
+  return true;
+}
+
+__device__ void p2plane_update(const double* tot, const IcpParams& prm, IcpState* st,
+                               float* trace) {
+  if (st->done) return;
+  const double cnt = tot[28];
+  double xi[6];
+  double rhs[6];
+  for (int a = 0; a < 6; ++a) rhs[a] = -tot[21 + a];
+  if (cnt < 6.0 || !chol6_solve(tot, rhs, xi)) {
+    st->done = 1;
+    st->fail = 1;
+    return;
+  }
+  // dR = exp([omega]x) (Rodrigues), T <- (dR R, dR t + v)
+  const double wx = xi[0], wy = xi[1], wz = xi[2];
+  const double th = sqrt(wx * wx + wy * wy + wz * wz);
+  double A, B;
+  if (th < 1e-12) {
+    A = 1.0;
+    B = 0.5;
+  } else {
+    A = sin(th) / th;
+    B = (1.0 - cos(th)) / (th * th);
+  }
+  const double K[9] = {0, wz, -wy, -wz, 0, wx, wy, -wx, 0};  // col-major [w]x
+  double dR[9];
+  for (int c = 0; c < 3; ++c)
+    for (int r = 0; r < 3; ++r) {
+      double kk = 0;
+      for (int l = 0; l < 3; ++l) kk += RST_M3(K, r, l) * RST_M3(K, l, c);
+      RST_M3(dR, r, c) = (r == c ? 1.0 : 0.0) + A * RST_M3(K, r, c) + B * kk;
+    }
+  double nR[9], nt[3];
+  for (int c = 0; c < 3; ++c)
+    for (int r = 0; r < 3; ++r) {
+      double s = 0;
+      for (int l = 0; l < 3; ++l) s += RST_M3(dR, r, l) * RST_M3(st->Rd, l, c);
+      RST_M3(nR, r, c) = s;
+    }
+  for (int r = 0; r < 3; ++r) {
+    double s = 0;
+    for (int l = 0; l < 3; ++l) s += RST_M3(dR, r, l) * st->td[l];
+    nt[r] = s + xi[3 + r];
+  }
+  for (int k = 0; k < 9; ++k) {
+    st->Rd[k] = nR[k];
+    st->R[k] = (float)nR[k];
+  }
+  for (int k = 0; k < 3; ++k) {
+    st->td[k] = nt[k];
+    st->t[k] = (float)nt[k];
+  }
+  double nx = 0;
+  for (int a = 0; a < 6; ++a) nx += xi[a] * xi[a];
+  nx = sqrt(nx);
+  st->last_xi = nx;
+  st->last_cnt = cnt;
+  st->last_d2 = tot[29];
+  const int it = st->iter;
+  if (trace) {
+    float* tp = trace + (int64_t)it * 16;
+    for (int c = 0; c < 3; ++c) {
+      for (int r = 0; r < 3; ++r) tp[c * 4 + r] = st->R[c * 3 + r];
+      tp[c * 4 + 3] = 0.f;
+    }
+    for (int r = 0; r < 3; ++r) tp[12 + r] = st->t[r];
+    tp[15] = 1.f;
+  }
+  st->iter = it + 1;
+  if (nx < (double)prm.p2plane_eps) st->done = 1;
+}
+
+__global__ __launch_bounds__(kBS) void k_solve_p2plane(const double* __restrict__ slab, int rows,
+                                                       IcpParams prm, IcpState* __restrict__ st,
+                                                       float* __restrict__ trace) {
+  __shared__ double red[kNP2Plane * kBS];
+  __shared__ double tot[kNP2Plane];
+  if (st->done) return;
+  reduce_slab_rows<kNP2Plane>(slab, rows, red, tot);
+  if (threadIdx.x == 0) p2plane_update(tot, prm, st, trace);
+}
+
+inline int blocks_for(int64_t n) { return (int)std::max<int64_t>(1, (n + kBS - 1) / kBS); }
+
+}  // namespace
+
+int kabsch_device(rst_ctx* ctx, const double cov[9], const float smean[3], const float dmean[3],
+                  float pose_out[16]) {
+  double* buf = nullptr;
+  RST_CHECK(ctx_slab(ctx, sizeof(double) * 64, &buf));
+  double h[15];
+  for (int k = 0; k < 9; ++k) h[k] = cov[k];
+  for (int k = 0; k < 3; ++k) {
+    h[9 + k] = smean[k];
+    h[12 + k] = dmean[k];
+  }
+  hipStream_t st = ctx->stream;
+  RST_HIP(hipMemcpyAsync(buf, h, sizeof(h), hipMemcpyHostToDevice, st));
+  k_kabsch<<<1, 64, 0, st>>>(buf, (float*)(buf + 16));
+  RST_HIP(hipGetLastError());
+  RST_HIP(hipMemcpyAsync(pose_out, buf + 16, sizeof(float) * 16, hipMemcpyDeviceToHost, st));
+  RST_HIP(hipStreamSynchronize(st));
+  return RST_OK;
+}
+
+int centroid_device(rst_ctx* ctx, const float4* d_pts, int64_t n, double* d_out) {
+  const int nb = std::min(1024, blocks_for(n));
+  k_centroid_partial<<<nb, kBS, 0, ctx->stream>>>(d_pts, n, d_out);
+  RST_HIP(hipGetLastError());
+  return nb;
+}
+
+int icp_align_prepared(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
+                       const rst_icp_opts* opts_in, float pose_inout[16], float* mean_cost,
+                       int32_t* iters_run, rst_comm* comm) {
+  if (!ctx || !src || !tgt || !pose_inout) return RST_E_ARG;
+  rst_icp_opts opts;
+  if (opts_in)
+    opts = *opts_in;
+  else
+    rst_icp_opts_default(&opts);
+  const bool p2plane = opts.mode == RST_P2PLANE;
+  if (opts.mode != RST_P2POINT_REF && opts.mode != RST_P2PLANE) return RST_E_ARG;
+  if (opts.max_iter < 0) return RST_E_ARG;
+  if (!tgt->has_bvh) return RST_E_ARG;
+  if (p2plane && !tgt->nrm) return RST_E_STATE;
+  const int64_t n_local = src->m;
+  int64_t n_total = n_local;
+  hipStream_t st = ctx->stream;
+  // one scratch buffer: [centroid slab | per-iteration slab | totals | pos0]
+  const int nblk = blocks_for(n_local);
+  const int NV = p2plane ? kNP2Plane : kNP2Point;
+  const int ncb = std::min(1024, blocks_for(n_local));
+  const size_t slab_doubles = (size_t)std::max(nblk * NV, ncb * 4) + 64;
+  double* slab = nullptr;
+  RST_CHECK(ctx_slab(ctx, sizeof(double) * slab_doubles, &slab));
+  double* totals = slab + (size_t)std::max(nblk * NV, ncb * 4);  // 64 doubles
+
+  // n_total and the centroid are global quantities under sharding
+  if (comm) {
+    double* cnt = totals;
+    double h = (double)n_local;
+    RST_HIP(hipMemcpyAsync(cnt, &h, sizeof(double), hipMemcpyHostToDevice, st));
+    RST_CHECK(comm_allreduce_sum_f64(comm, cnt, 1, st));
+    RST_HIP(hipMemcpyAsync(&h, cnt, sizeof(double), hipMemcpyDeviceToHost, st));
+    RST_HIP(hipStreamSynchronize(st));
+    n_total = (int64_t)h;
+  }
+  // reference early return (:77-79): pose untouched
+  if (n_total < 3 || tgt->m < 3) return RST_FALSE;
+  if (p2plane && n_total < 6) return RST_FALSE;
+
+  InitArgs ia;
+  memcpy(ia.pose, pose_inout, sizeof(ia.pose));
+  ia.mu0 = opts.mu0;
+  ia.need_centroid = p2plane ? 0 : 1;
+  int crows = 0;
+  if (!p2plane) {
+    if (n_local > 0) {
+      crows = centroid_device(ctx, src->pts, n_local, slab);
+      if (crows < 0) return crows;
+    }
+    if (comm) {
+      k_slab_reduce<4><<<1, kBS, 0, st>>>(slab, crows, totals);
+      RST_CHECK(comm_allreduce_sum_f64(comm, totals, 4, st));
+      k_init_state<<<1, kBS, 0, st>>>(totals, 1, ia, ctx->d_state);
+    } else {
+      k_init_state<<<1, kBS, 0, st>>>(slab, crows, ia, ctx->d_state);
+    }
+  } else {
+    k_init_state<<<1, kBS, 0, st>>>(slab, 0, ia, ctx->d_state);
+  }
+  const int32_t pos0 = tgt->pos0;
+  // per source point: sorted target position of its last neighbour (warm
+  // start of the next iteration's exact search); -1 = cold
+  int32_t* nnpos = nullptr;
+  {
+    void* w = nullptr;
+    RST_CHECK(ctx_workspace(ctx, sizeof(int32_t) * (size_t)std::max<int64_t>(n_local, 1), &w));
+    nnpos = (int32_t*)w;
+    RST_HIP(hipMemsetAsync(nnpos, 0xff, sizeof(int32_t) * (size_t)std::max<int64_t>(n_local, 1), st));
+  }
+
+  IcpParams prm;
+  prm.n = n_total;
+  prm.anneal_every = opts.anneal_every;
+  prm.anneal_div = opts.anneal_div;
+  prm.p2plane_eps = opts.p2plane_eps;
+  prm.p2plane_mu = opts.p2plane_mu;
+  prm.p2plane_max_d2 = opts.p2plane_max_dist > 0 ? opts.p2plane_max_dist * opts.p2plane_max_dist
+                                                 : FLT_MAX;
+  prm.max_iter = opts.max_iter;
+
+  BvhView bv;
+  bv.pts = tgt->pts;
+  bv.nodes = tgt->nodes;
+  bv.leaf_start = tgt->leaf_start;
+  bv.nleaves = tgt->nleaves;
+
+  const bool timing = ctx->timing && opts.max_iter > 0;
+  if (timing) {
+    const size_t need = 2 * (size_t)opts.max_iter;
+    while (ctx->ev.size() < need) {
+      hipEvent_t e;
+      RST_HIP(hipEventCreate(&e));
+      ctx->ev.push_back(e);
+    }
+  }
+  for (int it = 0; it < opts.max_iter; ++it) {
+    if (timing) RST_HIP(hipEventRecord(ctx->ev[2 * it], st));
+    if (n_local > 0) {
+      if (p2plane)
+        k_p2plane<<<nblk, kBS, 0, st>>>(bv, tgt->nrm, src->pts, n_local, ctx->d_state,
+                                        opts.p2plane_mu, prm.p2plane_max_d2, nnpos, slab);
+      else
+        k_p2point<<<nblk, kBS, 0, st>>>(bv, src->pts, n_local, ctx->d_state, pos0, nnpos,
+                                        slab);
+    }
+    if (timing) RST_HIP(hipEventRecord(ctx->ev[2 * it + 1], st));
+    const int rows = n_local > 0 ? nblk : 0;
+    if (comm) {
+      if (p2plane) {
+        k_slab_reduce<kNP2Plane><<<1, kBS, 0, st>>>(slab, rows, totals);
+        RST_CHECK(comm_allreduce_sum_f64(comm, totals, kNP2Plane, st));
+        k_solve_p2plane<<<1, kBS, 0, st>>>(totals, 1, prm, ctx->d_state, nullptr);
+      } else {
+        k_slab_reduce<kNP2Point><<<1, kBS, 0, st>>>(slab, rows, totals);
+        RST_CHECK(comm_allreduce_sum_f64(comm, totals, kNP2Point, st));
+        k_solve_p2point<<<1, kBS, 0, st>>>(totals, 1, prm, ctx->d_state, nullptr);
+      }
+    } else {
+      if (p2plane)
+        k_solve_p2plane<<<1, kBS, 0, st>>>(slab, rows, prm, ctx->d_state, nullptr);
+      else
+        k_solve_p2point<<<1, kBS, 0, st>>>(slab, rows, prm, ctx->d_state, nullptr);
+    }
+  }
+  RST_HIP(hipGetLastError());
+  RST_HIP(hipMemcpyAsync(ctx->h_state, ctx->d_state, sizeof(IcpState), hipMemcpyDeviceToHost, st));
+  RST_HIP(hipStreamSynchronize(st));
+  if (timing) {
+    float total = 0.f;
+    for (int it = 0; it < opts.max_iter; ++it) {
+      float ms = 0.f;
+      RST_HIP(hipEventElapsedTime(&ms, ctx->ev[2 * it], ctx->ev[2 * it + 1]));
+      total += ms;
+    }
+    ctx->last_kernel_ms = total / opts.max_iter;
+    ctx->last_kernel_launches = opts.max_iter;
+  }
+  const IcpState& h = *ctx->h_state;
+  if (p2plane && h.fail) {
+    if (iters_run) *iters_run = h.iter;
+    return RST_FALSE;
+  }
+  if (opts.max_iter > 0 || p2plane) {
+    for (int c = 0; c < 3; ++c) {
+      for (int r = 0; r < 3; ++r) pose_inout[c * 4 + r] = h.R[c * 3 + r];
+      pose_inout[c * 4 + 3] = 0.f;
+    }
+    for (int r = 0; r < 3; ++r) pose_inout[12 + r] = h.t[r];
+    pose_inout[15] = 1.f;
+  }
+  if (iters_run) *iters_run = h.iter;
+  float mc;
+  if (p2plane) {
+    mc = h.last_cnt > 0 ? (float)sqrt(h.last_d2 / h.last_cnt) : 0.f;
+  } else {
+    // :157 mean_cost = sqrt(cost / n) with cost the last iteration's sum d2
+    mc = sqrtf(h.last_cost / (float)n_total);
+  }
+  if (mean_cost) *mean_cost = mc;
+  if (p2plane) return RST_OK;
+  return (mc < 10000.0f) ? RST_OK : RST_FALSE;  // :160 (NaN -> false)
+}
+
+}  // namespace rst

@@ -1,0 +1,303 @@
+// query.hip -- exact NN / kNN queries against a target index and kNN-PCA
+// normals.
+//
+//   query_nn_device  : KDTree3f::query(p, 1, &j, &d2)  (kdtree.hpp:51-57)
+//   query_knn_device : KDTree3f index->knnSearch(p, k, ...) (fpfh/normals)
+//   compute_normals  : ComputeNormals + OrientNormals
+//                      (point_cloud_utils.cpp:176-216)
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+
+#include "rst_device.hpp"
+#include "rst_internal.hpp"
+
+namespace rst {
+namespace {
+
+constexpr int kBS = 256;
+
+__global__ __launch_bounds__(kBS) void k_query_nn(BvhView bv,
+                                                  const float* __restrict__ q,
+                                                  int64_t nq,
+                                                  int32_t* __restrict__ idx,
+                                                  float* __restrict__ d2) {
+  const int64_t i = blockIdx.x * (int64_t)kBS + threadIdx.x;
+  if (i >= nq) return;
+  float bd;
+  int bi, bp;
+  nn_exact(bv, q[3 * i], q[3 * i + 1], q[3 * i + 2], bd, bi, bp);
+  idx[i] = bi;
+  d2[i] = bd;
+}
+
+// Sorted (d2, idx) list of K candidates kept in registers; branch-free
+// insertion (static indices only, no scratch).
+template <int K>
+struct KnnList {
+  float d[K];
+  int id[K];
+  int pos[K];
+  __device__ __forceinline__ void init() {
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      d[j] = FLT_MAX;
+      id[j] = 0x7fffffff;
+      pos[j] = -1;
+    }
+  }
+  __device__ __forceinline__ static bool better(float a, int ia, float b, int ib) {
+    return (a < b) || ((a == b) && (ia < ib));
+  }
+  __device__ __forceinline__ float worst() const { return d[K - 1]; }
+  __device__ __forceinline__ void insert(float nd, int nid, int np) {
+    if (!(nd < FLT_MAX) || !better(nd, nid, d[K - 1], id[K - 1])) return;
+#pragma unroll
+    for (int j = K - 1; j >= 1; --j) {
+      const bool shift = better(nd, nid, d[j - 1], id[j - 1]);
+      const bool here = !shift && better(nd, nid, d[j], id[j]);
+      d[j] = shift ? d[j - 1] : (here ? nd : d[j]);
+      id[j] = shift ? id[j - 1] : (here ? nid : id[j]);
+      pos[j] = shift ? pos[j - 1] : (here ? np : pos[j]);
+    }
+    if (better(nd, nid, d[0], id[0])) {
+      d[0] = nd;
+      id[0] = nid;
+      pos[0] = np;
+    }
+  }
+};
+
+// Exact kNN by the same stackless traversal as nn_exact; prune bound is the
+// K-th best d2 (FLT_MAX until K points are held).
+template <int K>
+__device__ __forceinline__ void knn_exact(const BvhView& bv, float qx, float qy,
+                                          float qz, KnnList<K>& L) {
+  L.init();
+  if (!(__builtin_isfinite(qx) && __builtin_isfinite(qy) && __builtin_isfinite(qz)))
+    return;
+  const int nl = bv.nleaves;
+  int cur = 1, prev = 0;
+  while (cur != 0) {
+    const int parent = cur >> 1;
+    const float4 lo = bv.nodes[2 * cur];
+    const float4 hi = bv.nodes[2 * cur + 1];
+    int next;
+    if (prev == parent) {
+      const float bd = box_d2(qx, qy, qz, lo, hi);
+      if (bd > L.worst()) {
+        next = parent;
+      } else if (cur >= nl) {
+        const int Lf = cur - nl;
+        const int b = bv.leaf_start[Lf], e = bv.leaf_start[Lf + 1];
+        for (int i = b; i < e; ++i) {
+          const float4 p = bv.pts[i];
+          L.insert(d2_ref(qx, qy, qz, p.x, p.y, p.z), __float_as_int(p.w), i);
+        }
+        next = parent;
+      } else {
+        next = near_child(cur, lo, hi, qx, qy, qz);
+      }
+    } else {
+      const int nc = near_child(cur, lo, hi, qx, qy, qz);
+      next = (prev == nc) ? (prev ^ 1) : parent;
+    }
+    prev = cur;
+    cur = next;
+  }
+}
+
+template <int K>
+__global__ __launch_bounds__(kBS) void k_query_knn(BvhView bv, const float* __restrict__ q,
+                                                   int64_t nq, int k,
+                                                   int32_t* __restrict__ idx,
+                                                   float* __restrict__ d2) {
+  const int64_t i = blockIdx.x * (int64_t)kBS + threadIdx.x;
+  if (i >= nq) return;
+  KnnList<K> L;
+  knn_exact<K>(bv, q[3 * i], q[3 * i + 1], q[3 * i + 2], L);
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    if (j < k) {
+      const bool filled = L.pos[j] >= 0;
+      idx[i * k + j] = filled ? L.id[j] : 0;
+      d2[i * k + j] = filled ? L.d[j] : FLT_MAX;
+    }
+  }
+}
+
+// Smallest-eigenvalue eigenvector of a symmetric 3x3 (double): eigenvalues
+// from the trigonometric closed form, eigenvector as the best-conditioned
+// cross product of rows of (A - lambda I).
+__device__ inline void sym3_min_vec(const double a[6], double v[3]) {
+  // a = {xx, xy, xz, yy, yz, zz}
+  const double xx = a[0], xy = a[1], xz = a[2], yy = a[3], yz = a[4], zz = a[5];
+  const double p1 = xy * xy + xz * xz + yz * yz;
+  const double q = (xx + yy + zz) / 3.0;
+  const double p2 = (xx - q) * (xx - q) + (yy - q) * (yy - q) + (zz - q) * (zz - q) + 2.0 * p1;
+  const double p = sqrt(p2 / 6.0);
+  double lmin;
+  if (p < 1e-300) {
+    v[0] = 0.0; v[1] = 0.0; v[2] = 1.0;
+    return;
+  }
+  {
+    const double bxx = (xx - q) / p, byy = (yy - q) / p, bzz = (zz - q) / p;
+    const double bxy = xy / p, bxz = xz / p, byz = yz / p;
+    const double detb = bxx * (byy * bzz - byz * byz) - bxy * (bxy * bzz - byz * bxz) +
+                        bxz * (bxy * byz - byy * bxz);
+    double r = detb / 2.0;
+    r = fmin(1.0, fmax(-1.0, r));
+    const double phi = acos(r) / 3.0;
+    lmin = q + 2.0 * p * cos(phi + 2.0 * M_PI / 3.0);
+  }
+  const double r0[3] = {xx - lmin, xy, xz};
+  const double r1[3] = {xy, yy - lmin, yz};
+  const double r2[3] = {xz, yz, zz - lmin};
+  double c[3][3];
+  c[0][0] = r0[1] * r1[2] - r0[2] * r1[1]; c[0][1] = r0[2] * r1[0] - r0[0] * r1[2]; c[0][2] = r0[0] * r1[1] - r0[1] * r1[0];
+  c[1][0] = r0[1] * r2[2] - r0[2] * r2[1]; c[1][1] = r0[2] * r2[0] - r0[0] * r2[2]; c[1][2] = r0[0] * r2[1] - r0[1] * r2[0];
+  c[2][0] = r1[1] * r2[2] - r1[2] * r2[1]; c[2][1] = r1[2] * r2[0] - r1[0] * r2[2]; c[2][2] = r1[0] * r2[1] - r1[1] * r2[0];
+  int bi = 0;
+  double bn = -1.0;
+  for (int i = 0; i < 3; ++i) {
+    const double n2 = c[i][0] * c[i][0] + c[i][1] * c[i][1] + c[i][2] * c[i][2];
+    if (n2 > bn) {
+      bn = n2;
+      bi = i;
+    }
+  }
+  if (bn < 1e-300) {
+    v[0] = 0.0; v[1] = 0.0; v[2] = 1.0;
+    return;
+  }
+  const double inv = 1.0 / sqrt(bn);
+  v[0] = c[bi][0] * inv;
+  v[1] = c[bi][1] * inv;
+  v[2] = c[bi][2] * inv;
+}
+
+template <int K>
+__global__ __launch_bounds__(kBS) void k_normals(BvhView bv, int64_t m, float vx, float vy,
+                                                 float vz, float4* __restrict__ nrm) {
+  const int64_t i = blockIdx.x * (int64_t)kBS + threadIdx.x;
+  if (i >= m) return;
+  const float4 p = bv.pts[i];
+  KnnList<K> L;
+  knn_exact<K>(bv, p.x, p.y, p.z, L);
+  // centroid in result order, fp32 (point_cloud_utils.cpp:186-191)
+  float cx = 0.f, cy = 0.f, cz = 0.f;
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const float4 s = L.pos[j] >= 0 ? bv.pts[L.pos[j]] : make_float4(0.f, 0.f, 0.f, 0.f);
+    cx += s.x;
+    cy += s.y;
+    cz += s.z;
+  }
+  const float kf = (float)K;
+  cx = cx / kf;
+  cy = cy / kf;
+  cz = cz / kf;
+  // fp32 outer-product covariance (:193-198)
+  float c00 = 0, c01 = 0, c02 = 0, c11 = 0, c12 = 0, c22 = 0;
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const float4 s = L.pos[j] >= 0 ? bv.pts[L.pos[j]] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float dx = s.x - cx, dy = s.y - cy, dz = s.z - cz;
+    c00 += dx * dx; c01 += dx * dy; c02 += dx * dz;
+    c11 += dy * dy; c12 += dy * dz; c22 += dz * dz;
+  }
+  const double a[6] = {c00, c01, c02, c11, c12, c22};
+  double v[3];
+  sym3_min_vec(a, v);
+  float nx = (float)v[0], ny = (float)v[1], nz = (float)v[2];
+  // OrientNormals (:206-216): flip if (p - viewpoint).n > 0
+  const float rx = p.x - vx, ry = p.y - vy, rz = p.z - vz;
+  const float dot = rx * nx + (ry * ny + rz * nz);
+  if (dot > 0) {
+    nx = -nx;
+    ny = -ny;
+    nz = -nz;
+  }
+  nrm[i] = make_float4(nx, ny, nz, 0.0f);
+}
+
+inline int blocks_for(int64_t n) { return (int)std::max<int64_t>(1, (n + kBS - 1) / kBS); }
+
+BvhView view_of(const rst_target* t) {
+  BvhView v;
+  v.pts = t->pts;
+  v.nodes = t->nodes;
+  v.leaf_start = t->leaf_start;
+  v.nleaves = t->nleaves;
+  return v;
+}
+
+}  // namespace
+
+int query_nn_device(rst_ctx* ctx, const rst_target* tgt, const float* d_q, int64_t nq,
+                    int32_t* d_idx, float* d_d2) {
+  if (!ctx || !tgt || nq < 0 || !tgt->has_bvh) return RST_E_ARG;
+  if (nq == 0) return RST_OK;
+  if (tgt->m == 0) {
+    // empty index: nothing is ever added -> (0, FLT_MAX)
+    RST_HIP(hipMemsetAsync(d_idx, 0, sizeof(int32_t) * nq, ctx->stream));
+    std::vector<float> f(nq, FLT_MAX);
+    RST_HIP(hipMemcpyAsync(d_d2, f.data(), sizeof(float) * nq, hipMemcpyHostToDevice,
+                           ctx->stream));
+    RST_HIP(hipStreamSynchronize(ctx->stream));
+    return RST_OK;
+  }
+  k_query_nn<<<blocks_for(nq), kBS, 0, ctx->stream>>>(view_of(tgt), d_q, nq, d_idx, d_d2);
+  RST_HIP(hipGetLastError());
+  return RST_OK;
+}
+
+int query_knn_device(rst_ctx* ctx, const rst_target* tgt, const float* d_q, int64_t nq,
+                     int k, int32_t* d_idx, float* d_d2) {
+  if (!ctx || !tgt || nq < 0 || k < 1 || k > 32 || !tgt->has_bvh || tgt->m == 0)
+    return RST_E_ARG;
+  if (nq == 0) return RST_OK;
+  const BvhView v = view_of(tgt);
+  hipStream_t st = ctx->stream;
+  if (k <= 1)
+    k_query_knn<1><<<blocks_for(nq), kBS, 0, st>>>(v, d_q, nq, k, d_idx, d_d2);
+  else if (k <= 4)
+    k_query_knn<4><<<blocks_for(nq), kBS, 0, st>>>(v, d_q, nq, k, d_idx, d_d2);
+  else if (k <= 8)
+    k_query_knn<8><<<blocks_for(nq), kBS, 0, st>>>(v, d_q, nq, k, d_idx, d_d2);
+  else if (k <= 16)
+    k_query_knn<16><<<blocks_for(nq), kBS, 0, st>>>(v, d_q, nq, k, d_idx, d_d2);
+  else
+    k_query_knn<32><<<blocks_for(nq), kBS, 0, st>>>(v, d_q, nq, k, d_idx, d_d2);
+  RST_HIP(hipGetLastError());
+  return RST_OK;
+}
+
+int compute_normals(rst_ctx* ctx, rst_target* tgt, int k, const float vp[3]) {
+  if (!ctx || !tgt || !tgt->has_bvh) return RST_E_ARG;
+  if (k != 8 && k != 16 && k != 32) return RST_E_ARG;  // compiled K values
+  // m < k would leave result slots at the reference's idx 0 default
+  // (std::vector<int> oi(k) zero-initialised); not supported here
+  if (tgt->m < k) return RST_E_ARG;
+  if (!tgt->nrm) {
+    if (hipMalloc(&tgt->nrm, sizeof(float4) * std::max<int64_t>(tgt->m, 1)) != hipSuccess)
+      return RST_E_NOMEM;
+  }
+  if (tgt->m == 0) return RST_OK;
+  const BvhView v = view_of(tgt);
+  hipStream_t st = ctx->stream;
+  const float x = vp ? vp[0] : 0.f, y = vp ? vp[1] : 0.f, z = vp ? vp[2] : 0.f;
+  if (k == 8)
+    k_normals<8><<<blocks_for(tgt->m), kBS, 0, st>>>(v, tgt->m, x, y, z, tgt->nrm);
+  else if (k == 16)
+    k_normals<16><<<blocks_for(tgt->m), kBS, 0, st>>>(v, tgt->m, x, y, z, tgt->nrm);
+  else
+    k_normals<32><<<blocks_for(tgt->m), kBS, 0, st>>>(v, tgt->m, x, y, z, tgt->nrm);
+  RST_HIP(hipGetLastError());
+  return RST_OK;
+}
+
+}  // namespace rst

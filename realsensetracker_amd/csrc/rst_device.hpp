@@ -1,0 +1,409 @@
+// rst_device.hpp -- device-side building blocks shared by the kernels.
+//
+// Arithmetic that must round exactly like the reference is written out
+// operation by operation; the library is compiled with -ffp-contract=off so
+// no multiply-add is fused behind our back (the reference is built for
+// baseline x86-64: SSE2, no FMA).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cstdint>
+
+namespace rst {
+
+constexpr int kWave = 64;
+
+// ---- pose application ----------------------------------------------------
+// Transform<float,3,Isometry> * Vector3f: res = t; res += R*v, each coeff of
+// the lazy 3x3 product an unrolled redux x0 + (x1 + x2)
+// (align_icp.cpp:107, Eigen transform_right_product_impl).
+__device__ __forceinline__ float mv_row(const float* R, int r, float v0,
+                                        float v1, float v2) {
+  const float a0 = R[0 * 3 + r] * v0;
+  const float a1 = R[1 * 3 + r] * v1;
+  const float a2 = R[2 * 3 + r] * v2;
+  return a0 + (a1 + a2);
+}
+
+struct Pose3 {
+  float r[9];
+  float t[3];
+};
+
+__device__ __forceinline__ void xform(const Pose3& P, float sx, float sy,
+                                      float sz, float& px, float& py,
+                                      float& pz) {
+  px = P.t[0] + mv_row(P.r, 0, sx, sy, sz);
+  py = P.t[1] + mv_row(P.r, 1, sx, sy, sz);
+  pz = P.t[2] + mv_row(P.r, 2, sx, sy, sz);
+}
+
+// nanoflann L2_Adaptor::evalMetric for DIM=3: ((dx*dx + dy*dy) + dz*dz),
+// d = query - point (kdtree.hpp:51-57).
+__device__ __forceinline__ float d2_ref(float qx, float qy, float qz,
+                                        float px, float py, float pz) {
+  const float dx = qx - px;
+  const float dy = qy - py;
+  const float dz = qz - pz;
+  float r = dx * dx;
+  r = r + dy * dy;
+  r = r + dz * dz;
+  return r;
+}
+
+// Lower bound of d2_ref over every point of an AABB: per-axis gaps are
+// monotone in float, so this never exceeds any contained point's d2_ref.
+__device__ __forceinline__ float box_d2(float qx, float qy, float qz,
+                                        const float4& lo, const float4& hi) {
+  const float ex = fmaxf(fmaxf(lo.x - qx, qx - hi.x), 0.0f);
+  const float ey = fmaxf(fmaxf(lo.y - qy, qy - hi.y), 0.0f);
+  const float ez = fmaxf(fmaxf(lo.z - qz, qz - hi.z), 0.0f);
+  float r = ex * ex;
+  r = r + ey * ey;
+  r = r + ez * ez;
+  return r;
+}
+
+// ---- BVH view ---------------------------------------------------------------
+struct BvhView {
+  const float4* __restrict__ pts;      // sorted points, .w = orig idx bits
+  const float4* __restrict__ nodes;    // 2 float4 per heap node
+  const int32_t* __restrict__ leaf_start;
+  int32_t nleaves;
+};
+
+__device__ __forceinline__ int near_child(int k, const float4& lo,
+                                          const float4& hi, float qx,
+                                          float qy, float qz) {
+  const int ab = __float_as_int(hi.w);
+  const int ax = ab & 3;
+  const float qa = ax == 0 ? qx : (ax == 1 ? qy : qz);
+  const bool q_low = qa < lo.w;
+  const bool left_low = (ab & 4) == 0;
+  return (q_low == left_low) ? (2 * k) : (2 * k + 1);
+}
+
+// Exact 1-NN by stackless depth-first traversal of the heap BVH (near child
+// first, parent recovered as k>>1).  Result = lexicographic min of
+// (d2, orig idx) over points with d2 < FLT_MAX; nothing found -> (0,FLT_MAX),
+// which is what the reference's out-params hold when nanoflann adds no
+// point (align_icp.cpp:110-112, KNNResultSet::init).
+__device__ __forceinline__ void nn_exact(const BvhView& bv, float qx,
+                                         float qy, float qz, float& best_d2,
+                                         int& best_idx, int& best_pos) {
+  best_d2 = FLT_MAX;
+  best_idx = 0;
+  best_pos = -1;
+  if (!(__builtin_isfinite(qx) && __builtin_isfinite(qy) &&
+        __builtin_isfinite(qz)))
+    return;
+  const int nl = bv.nleaves;
+  int cur = 1, prev = 0;
+  while (cur != 0) {
+    const int parent = cur >> 1;
+    const float4 lo = bv.nodes[2 * cur];
+    const float4 hi = bv.nodes[2 * cur + 1];
+    int next;
+    if (prev == parent) {
+      const float bd = box_d2(qx, qy, qz, lo, hi);
+      if (bd > best_d2) {
+        next = parent;
+      } else if (cur >= nl) {
+        const int L = cur - nl;
+        const int b = bv.leaf_start[L];
+        const int e = bv.leaf_start[L + 1];
+        for (int i = b; i < e; ++i) {
+          const float4 p = bv.pts[i];
+          const float d2 = d2_ref(qx, qy, qz, p.x, p.y, p.z);
+          const int id = __float_as_int(p.w);
+          const bool better =
+              (d2 < best_d2) || ((d2 == best_d2) && (id < best_idx));
+          if (better) {
+            best_d2 = d2;
+            best_idx = id;
+            best_pos = i;
+          }
+        }
+        next = parent;
+      } else {
+        next = near_child(cur, lo, hi, qx, qy, qz);
+      }
+    } else {
+      const int nc = near_child(cur, lo, hi, qx, qy, qz);
+      next = (prev == nc) ? (prev ^ 1) : parent;
+    }
+    prev = cur;
+    cur = next;
+  }
+}
+
+// Wave-cooperative exact 1-NN for 64 spatially coherent queries (the source
+// is Morton-sorted, so a wave holds one compact patch).  The wave walks the
+// BVH once: node boxes and leaf points are read with wave-uniform addresses
+// (scalar loads, no per-lane gather); a subtree is entered when ANY lane's
+// box lower bound is <= that lane's current best (ballot), so every lane's
+// result is the same exact lexicographic (d2, idx) minimum nn_exact returns.
+// best_* may arrive warm (a real candidate, e.g. the previous ICP
+// iteration's neighbour) -- that only tightens the pruning.
+__device__ __forceinline__ void nn_wave(const BvhView& bv, bool active, float qx, float qy,
+                                        float qz, float& best_d2, int& best_idx,
+                                        int& best_pos) {
+  const bool live = active && __builtin_isfinite(qx) && __builtin_isfinite(qy) &&
+                    __builtin_isfinite(qz);
+  const uint64_t lm = __ballot(live);
+  if (lm == 0) return;
+  // representative query (first live lane) steers the near-child order
+  const int rl = __ffsll((unsigned long long)lm) - 1;
+  const float rx = __shfl(qx, rl, kWave);
+  const float ry = __shfl(qy, rl, kWave);
+  const float rz = __shfl(qz, rl, kWave);
+  const int nl = bv.nleaves;
+  int cur = 1, prev = 0;
+  while (cur != 0) {
+    // the walk state is wave-uniform by construction; say so, so node and
+    // point addresses become scalar loads
+    cur = __builtin_amdgcn_readfirstlane(cur);
+    prev = __builtin_amdgcn_readfirstlane(prev);
+    const int parent = cur >> 1;
+    const float4 lo = bv.nodes[2 * cur];
+    const float4 hi = bv.nodes[2 * cur + 1];
+    int next;
+    if (prev == parent) {
+      const float bd = box_d2(qx, qy, qz, lo, hi);
+      const bool want = live && (bd <= best_d2);
+      if (__ballot(want) == 0) {
+        next = parent;
+      } else if (cur >= nl) {
+        const int L = cur - nl;
+        const int b = __builtin_amdgcn_readfirstlane(bv.leaf_start[L]);
+        const int e = __builtin_amdgcn_readfirstlane(bv.leaf_start[L + 1]);
+        for (int i = b; i < e; ++i) {
+          const float4 p = bv.pts[i];
+          const float d2 = d2_ref(qx, qy, qz, p.x, p.y, p.z);
+          const int id = __float_as_int(p.w);
+          const bool better = (d2 < best_d2) || ((d2 == best_d2) && (id < best_idx));
+          best_d2 = better ? d2 : best_d2;
+          best_idx = better ? id : best_idx;
+          best_pos = better ? i : best_pos;
+        }
+        next = parent;
+      } else {
+        next = near_child(cur, lo, hi, rx, ry, rz);
+      }
+    } else {
+      const int nc = near_child(cur, lo, hi, rx, ry, rz);
+      next = (prev == nc) ? (prev ^ 1) : parent;
+    }
+    prev = cur;
+    cur = next;
+  }
+}
+
+// Warm start from a known candidate (sorted position pos): its own exact
+// d2_ref becomes the initial bound.  Lanes with pos < 0 start cold.
+__device__ __forceinline__ void nn_warm(const BvhView& bv, int pos, float qx, float qy,
+                                        float qz, float& best_d2, int& best_idx,
+                                        int& best_pos) {
+  best_d2 = FLT_MAX;
+  best_idx = 0;
+  best_pos = -1;
+  if (pos >= 0) {
+    const float4 p = bv.pts[pos];
+    const float d2 = d2_ref(qx, qy, qz, p.x, p.y, p.z);
+    if (d2 < FLT_MAX) {  // the reference only ever adds points with d2 < FLT_MAX
+      best_d2 = d2;
+      best_idx = __float_as_int(p.w);
+      best_pos = pos;
+    }
+  }
+}
+
+// ---- wave / block reductions ------------------------------------------------
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+  return v;
+}
+
+__device__ __forceinline__ float wave_min(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fminf(v, __shfl_xor(v, off, kWave));
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, kWave));
+  return v;
+}
+
+// Reduce NV doubles per thread over a block of BS threads; lane results land
+// in out[] on thread 0..NV-1 (out must be __shared__ double[BS/64][NV]).
+template <int NV, int BS>
+__device__ __forceinline__ void block_sum_to_slab(double (&v)[NV],
+                                                  double* lds,
+                                                  double* slab_row) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wid = threadIdx.x / kWave;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) v[k] = wave_sum(v[k]);
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) lds[wid * NV + k] = v[k];
+  }
+  __syncthreads();
+  if (threadIdx.x < NV) {
+    double s = 0.0;
+#pragma unroll
+    for (int w = 0; w < BS / kWave; ++w) s += lds[w * NV + threadIdx.x];
+    slab_row[threadIdx.x] = s;
+  }
+}
+
+// ---- 3x3 linear algebra (single thread) -------------------------------------
+#define RST_M3(m, r, c) (m)[(c) * 3 + (r)]
+
+// One-sided Jacobi SVD of a 3x3 double matrix (column-major):
+// a = U diag(s) V^T.  Columns of a are orthogonalised by plane rotations
+// accumulated in V; U = normalised columns.  Rank-2 input: the missing U
+// column is completed as the cross product of the other two.
+__device__ inline void svd3_jacobi(const double* a_in, double* U, double* S,
+                                   double* V) {
+  double A[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    A[i] = a_in[i];
+    V[i] = (i % 4 == 0) ? 1.0 : 0.0;
+  }
+  for (int sweep = 0; sweep < 40; ++sweep) {
+    double off = 0.0;
+#pragma unroll
+    for (int pr = 0; pr < 3; ++pr) {
+      const int p = pr == 2 ? 1 : 0;
+      const int q = pr == 0 ? 1 : 2;
+      double alpha = 0, beta = 0, gamma = 0;
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        alpha += RST_M3(A, r, p) * RST_M3(A, r, p);
+        beta += RST_M3(A, r, q) * RST_M3(A, r, q);
+        gamma += RST_M3(A, r, p) * RST_M3(A, r, q);
+      }
+      const double denom = sqrt(alpha * beta);
+      if (denom == 0.0 || fabs(gamma) <= 1e-15 * denom) continue;
+      off = fmax(off, fabs(gamma) / denom);
+      const double zeta = (beta - alpha) / (2.0 * gamma);
+      const double tt = (zeta >= 0 ? 1.0 : -1.0) /
+                        (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+      const double c = 1.0 / sqrt(1.0 + tt * tt);
+      const double s = c * tt;
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        const double ap = RST_M3(A, r, p), aq = RST_M3(A, r, q);
+        RST_M3(A, r, p) = c * ap - s * aq;
+        RST_M3(A, r, q) = s * ap + c * aq;
+        const double vp = RST_M3(V, r, p), vq = RST_M3(V, r, q);
+        RST_M3(V, r, p) = c * vp - s * vq;
+        RST_M3(V, r, q) = s * vp + c * vq;
+      }
+    }
+    if (off <= 1e-15) break;
+  }
+  double smax = 0.0;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    double n2 = 0;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) n2 += RST_M3(A, r, c) * RST_M3(A, r, c);
+    S[c] = sqrt(n2);
+    smax = fmax(smax, S[c]);
+  }
+  const double tiny = smax * 1e-13;
+  int nz = 0, zc = -1;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    if (S[c] > tiny && S[c] > 0.0) {
+#pragma unroll
+      for (int r = 0; r < 3; ++r) RST_M3(U, r, c) = RST_M3(A, r, c) / S[c];
+      ++nz;
+    } else {
+#pragma unroll
+      for (int r = 0; r < 3; ++r) RST_M3(U, r, c) = 0.0;
+      zc = c;
+    }
+  }
+  if (nz <= 1) {
+    // rank <= 1: degenerate; U = V gives R = U V^T = I (what an all-zero
+    // covariance yields in the reference, whose Jacobi SVD then does nothing)
+#pragma unroll
+    for (int i = 0; i < 9; ++i) U[i] = V[i];
+  } else if (nz == 2) {
+    const int c0 = zc == 0 ? 1 : 0;
+    const int c1 = zc == 2 ? 1 : 2;
+    // u_z = u_c0 x u_c1, in the cyclic orientation of (c0, c1, zc)
+    double x[3];
+    x[0] = RST_M3(U, 1, c0) * RST_M3(U, 2, c1) - RST_M3(U, 2, c0) * RST_M3(U, 1, c1);
+    x[1] = RST_M3(U, 2, c0) * RST_M3(U, 0, c1) - RST_M3(U, 0, c0) * RST_M3(U, 2, c1);
+    x[2] = RST_M3(U, 0, c0) * RST_M3(U, 1, c1) - RST_M3(U, 1, c0) * RST_M3(U, 0, c1);
+    const double sg = (zc == 1) ? -1.0 : 1.0;  // (0,2,1) is an odd order
+    // keep det(U) == det(V) so U V^T is a proper rotation
+    double dv = RST_M3(V, 0, 0) * (RST_M3(V, 1, 1) * RST_M3(V, 2, 2) - RST_M3(V, 1, 2) * RST_M3(V, 2, 1)) -
+                RST_M3(V, 0, 1) * (RST_M3(V, 1, 0) * RST_M3(V, 2, 2) - RST_M3(V, 1, 2) * RST_M3(V, 2, 0)) +
+                RST_M3(V, 0, 2) * (RST_M3(V, 1, 0) * RST_M3(V, 2, 1) - RST_M3(V, 1, 1) * RST_M3(V, 2, 0));
+    const double sd = dv < 0 ? -1.0 : 1.0;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) RST_M3(U, r, zc) = sg * sd * x[r];
+  }
+}
+
+// Matrix3f::determinant (Eigen bruteforce_det3_helper order).
+__device__ __forceinline__ float det3f(const float* m) {
+  const float d0 = RST_M3(m, 0, 0) * (RST_M3(m, 1, 1) * RST_M3(m, 2, 2) - RST_M3(m, 1, 2) * RST_M3(m, 2, 1));
+  const float d1 = RST_M3(m, 0, 1) * (RST_M3(m, 1, 0) * RST_M3(m, 2, 2) - RST_M3(m, 1, 2) * RST_M3(m, 2, 0));
+  const float d2 = RST_M3(m, 0, 2) * (RST_M3(m, 1, 0) * RST_M3(m, 2, 1) - RST_M3(m, 1, 1) * RST_M3(m, 2, 0));
+  return (d0 - d1) + d2;
+}
+
+// Quaternionf(R) then toRotationMatrix() (align_icp.cpp:151; Eigen
+// quaternionbase_assign_impl<3x3> / toRotationMatrix op order).
+__device__ inline void quat_roundtrip(const float* R, float* Rq) {
+  float q[4];  // x y z w
+  const float tr = (RST_M3(R, 0, 0) + RST_M3(R, 1, 1)) + RST_M3(R, 2, 2);
+  if (tr > 0.0f) {
+    float t = sqrtf(tr + 1.0f);
+    q[3] = 0.5f * t;
+    t = 0.5f / t;
+    q[0] = (RST_M3(R, 2, 1) - RST_M3(R, 1, 2)) * t;
+    q[1] = (RST_M3(R, 0, 2) - RST_M3(R, 2, 0)) * t;
+    q[2] = (RST_M3(R, 1, 0) - RST_M3(R, 0, 1)) * t;
+  } else {
+    int i = 0;
+    if (RST_M3(R, 1, 1) > RST_M3(R, 0, 0)) i = 1;
+    if (RST_M3(R, 2, 2) > RST_M3(R, i, i)) i = 2;
+    const int j = (i + 1) % 3;
+    const int k = (j + 1) % 3;
+    float t = sqrtf(RST_M3(R, i, i) - RST_M3(R, j, j) - RST_M3(R, k, k) + 1.0f);
+    q[i] = 0.5f * t;
+    t = 0.5f / t;
+    q[3] = (RST_M3(R, k, j) - RST_M3(R, j, k)) * t;
+    q[j] = (RST_M3(R, j, i) + RST_M3(R, i, j)) * t;
+    q[k] = (RST_M3(R, k, i) + RST_M3(R, i, k)) * t;
+  }
+  const float x = q[0], y = q[1], z = q[2], w = q[3];
+  const float tx = 2.0f * x, ty = 2.0f * y, tz = 2.0f * z;
+  const float twx = tx * w, twy = ty * w, twz = tz * w;
+  const float txx = tx * x, txy = ty * x, txz = tz * x;
+  const float tyy = ty * y, tyz = tz * y, tzz = tz * z;
+  RST_M3(Rq, 0, 0) = 1.0f - (tyy + tzz);
+  RST_M3(Rq, 0, 1) = txy - twz;
+  RST_M3(Rq, 0, 2) = txz + twy;
+  RST_M3(Rq, 1, 0) = txy + twz;
+  RST_M3(Rq, 1, 1) = 1.0f - (txx + tzz);
+  RST_M3(Rq, 1, 2) = tyz - twx;
+  RST_M3(Rq, 2, 0) = txz - twy;
+  RST_M3(Rq, 2, 1) = tyz + twx;
+  RST_M3(Rq, 2, 2) = 1.0f - (txx + tyy);
+}
+
+}  // namespace rst

@@ -1,0 +1,152 @@
+// rst_internal.hpp -- host-side objects of the MI355X ICP library.
+//
+// One rst_ctx = one GPU + one HIP stream + grow-only workspaces.  One
+// rst_target = one prepared cloud resident in HBM: Morton-sorted points
+// (float4 x,y,z,orig-index-bits), the implicit BVH over them, optional
+// normals.  See DESIGN.md "Data layout in HBM".
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <cstdio>
+#include <vector>
+
+#include "rst_align.h"
+
+namespace rst {
+
+// ---- error plumbing -------------------------------------------------------
+#define RST_HIP(call)                                                     \
+  do {                                                                    \
+    hipError_t e_ = (call);                                               \
+    if (e_ != hipSuccess) {                                               \
+      rst::set_last_error(e_, #call, __FILE__, __LINE__);                 \
+      return RST_E_HIP;                                                   \
+    }                                                                     \
+  } while (0)
+
+#define RST_CHECK(expr)            \
+  do {                             \
+    int s_ = (expr);               \
+    if (s_ < 0) return s_;         \
+  } while (0)
+
+void set_last_error(hipError_t e, const char* what, const char* file,
+                    int line);
+
+// ---- geometry of the BVH --------------------------------------------------
+// Heap-ordered complete binary tree, root = 1, children 2k / 2k+1, leaves
+// [nleaves, 2*nleaves).  Node k = two float4: lo (x,y,z,split) and
+// hi (x,y,z,axis-bits).  Leaf L holds sorted points
+// [leaf_start[L], leaf_start[L+1]) = [L*m/nleaves, (L+1)*m/nleaves).
+constexpr int kLeafTarget = 16;   // nanoflann leaf_max_size at align_icp.cpp:165
+
+// ---- device-resident state of one ICP solve --------------------------------
+// Written only by the single-block solve kernels, read (uniformly) by the
+// per-point kernels.  Plain POD; lives in the context's workspace.
+struct IcpState {
+  float R[9];        // current pose, column-major (what the points see)
+  float t[3];
+  float smean[3];    // source centroid (P2POINT_REF)
+  float mu;          // annealing parameter for the next iteration
+  int32_t iter;      // iterations completed
+  int32_t done;      // P2PLANE converged / failed flag
+  float last_cost;   // sum d2 of the last iteration (as float)
+  float pad0;
+  double Rd[9];      // P2PLANE high-precision pose
+  double td[3];
+  double last_xi;    // |xi| of the last P2PLANE step
+  double last_cnt;   // accepted correspondences of the last step
+  double last_d2;    // sum d2 of the last step
+  int32_t fail;      // P2PLANE: singular system / too few points
+  int32_t pad1;
+};
+
+struct IcpParams {
+  int64_t n;           // total source points (all shards)
+  int32_t anneal_every;
+  float anneal_div;
+  float p2plane_eps;
+  float p2plane_mu;
+  float p2plane_max_d2;
+  int32_t max_iter;
+};
+
+}  // namespace rst
+
+// ---- public opaque objects ------------------------------------------------
+struct rst_ctx {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  // workspaces (grow-only)
+  void* ws = nullptr;
+  size_t ws_bytes = 0;
+  void* pinned = nullptr;
+  size_t pinned_bytes = 0;
+  rst::IcpState* d_state = nullptr;
+  rst::IcpState* h_state = nullptr;   // pinned mirror
+  double* d_slab = nullptr;           // per-block partial sums
+  size_t slab_bytes = 0;
+  // timing of the dominant per-iteration kernel
+  bool timing = false;
+  std::vector<hipEvent_t> ev;
+  float last_kernel_ms = 0.f;
+  int32_t last_kernel_launches = 0;
+};
+
+struct rst_target {
+  rst_ctx* ctx = nullptr;
+  int64_t m = 0;
+  int32_t nleaves = 0;
+  float4* pts = nullptr;        // [m] Morton-sorted (x,y,z,orig idx bits)
+  float4* nodes = nullptr;      // [2 * 2*nleaves]
+  int32_t* leaf_start = nullptr;// [nleaves+1]
+  float4* nrm = nullptr;        // [m] normals in sorted order (optional)
+  float bbox[6] = {0, 0, 0, 0, 0, 0};
+  int32_t pos0 = 0;             // sorted position of original point 0
+  bool has_bvh = false;
+};
+
+namespace rst {
+
+// workspace helpers (implemented in capi.hip)
+int ctx_workspace(rst_ctx* ctx, size_t bytes, void** out);
+int ctx_pinned(rst_ctx* ctx, size_t bytes, void** out);
+int ctx_slab(rst_ctx* ctx, size_t bytes, double** out);
+
+// target build (build.hip)
+int target_build_device(rst_ctx* ctx, const float* d_xyz, int64_t m,
+                        bool with_bvh, rst_target** out);
+size_t target_index_bytes(const rst_target* t);
+
+// NN queries (query.hip)
+int query_nn_device(rst_ctx* ctx, const rst_target* tgt, const float* d_q,
+                    int64_t nq, int32_t* d_idx, float* d_d2);
+int query_knn_device(rst_ctx* ctx, const rst_target* tgt, const float* d_q,
+                     int64_t nq, int k, int32_t* d_idx, float* d_d2);
+int compute_normals(rst_ctx* ctx, rst_target* tgt, int k, const float vp[3]);
+
+// ICP (icp.hip)
+int icp_align_prepared(rst_ctx* ctx, const rst_target* src,
+                       const rst_target* tgt, const rst_icp_opts* opts,
+                       float pose_inout[16], float* mean_cost,
+                       int32_t* iters_run, rst_comm* comm);
+int centroid_device(rst_ctx* ctx, const float4* d_pts, int64_t n,
+                    double* d_out3);
+int kabsch_device(rst_ctx* ctx, const double cov[9], const float smean[3],
+                  const float dmean[3], float pose_out[16]);
+
+// unprojection (unproject.hip)
+int unproject_device(rst_ctx* ctx, const uint16_t* d_depth,
+                     const rst_intrinsics* K, int keep_invalid,
+                     float* d_xyz, int64_t* n_out);
+
+// RCCL (comm.hip)
+int comm_allreduce_sum_f64(rst_comm* comm, double* d_buf, size_t count,
+                           hipStream_t stream);
+int comm_size(const rst_comm* comm);
+
+}  // namespace rst

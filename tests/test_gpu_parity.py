@@ -1,0 +1,308 @@
+"""GPU parity: the HIP path through the C ABI against the oracle.
+
+Bars (DESIGN.md "Parity"):
+  * NN (idx, d2), unprojection, kNN: bit-exact;
+  * Kabsch solve on given sums: <= 1 float ulp per pose coefficient;
+  * AlignIcp3d vs the oracle with fp64 sums (the GPU's reduction
+    arithmetic): <= 2e-5 rad / m;
+  * AlignIcp3d vs the oracle with the reference's fp32 sequential sums:
+    <= max(1e-4, 2 x the reference's own fp32-vs-fp64 sensitivity);
+  * P2PLANE vs its CPU restatement: <= 1e-4 (normals computed independently).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN_NAMES, PAIR_NAMES, load_golden
+from oracle import oracle as O
+from posemetric import pose_err
+from realsensetracker_amd import _lib as L
+from realsensetracker_amd import align as A
+from realsensetracker_amd import driver
+
+pytestmark = pytest.mark.gpu
+FMAX = np.finfo(np.float32).max
+
+
+# ---- nearest neighbour ----------------------------------------------------------
+@pytest.mark.parametrize("name", GOLDEN_NAMES)
+def test_nn_bitexact_golden(ctx, name):
+    g = load_golden(name)
+    t = A.Target.build(g["dst"], ctx)
+    idx, d2 = t.query(g["src"])  # iteration 0 runs at the identity pose
+    assert np.array_equal(idx, g["nn_idx0"])
+    assert np.array_equal(d2, g["nn_d20"])
+
+
+def test_nn_bitexact_ties_duplicates_random(ctx):
+    rng = np.random.default_rng(0)
+    lat = np.stack(np.meshgrid(*[np.arange(10, dtype=np.float32) * 0.1] * 3), -1).reshape(-1, 3)
+    dst = np.concatenate([lat, lat[::7], rng.normal(size=(3000, 3)).astype(np.float32)])
+    q = np.concatenate([lat + np.float32(0.05), lat[:100],
+                        rng.normal(size=(5000, 3)).astype(np.float32) * 3])
+    t = A.Target.build(dst, ctx)
+    gi, gd = t.query(q)
+    oi, od = O.nn_bruteforce(dst, q)
+    assert np.array_equal(gi, oi) and np.array_equal(gd, od)
+
+
+@pytest.mark.parametrize("m", [1, 2, 3, 15, 16, 17, 31, 33, 100, 1000])
+def test_nn_small_targets(ctx, m):
+    rng = np.random.default_rng(m)
+    dst = rng.uniform(-1, 1, size=(m, 3)).astype(np.float32)
+    q = rng.uniform(-2, 2, size=(257, 3)).astype(np.float32)
+    gi, gd = A.Target.build(dst, ctx).query(q)
+    oi, od = O.nn_bruteforce(dst, q)
+    assert np.array_equal(gi, oi) and np.array_equal(gd, od)
+
+
+def test_nn_nonfinite_queries_and_empty_target(ctx):
+    dst = np.random.default_rng(1).normal(size=(500, 3)).astype(np.float32)
+    q = np.array([[np.nan, 0, 0], [0, np.inf, 0], [0, 0, -np.inf], [0.1, 0.2, 0.3]], np.float32)
+    gi, gd = A.Target.build(dst, ctx).query(q)
+    assert list(gi[:3]) == [0, 0, 0] and np.all(gd[:3] == FMAX)
+    oi, od = O.nn_bruteforce(dst, q)
+    assert gi[3] == oi[3] and gd[3] == od[3]
+    ei, ed = A.Target.build(np.zeros((0, 3), np.float32), ctx).query(q)
+    assert np.all(ei == 0) and np.all(ed == FMAX)
+
+
+@pytest.mark.parametrize("k", [4, 8, 16, 32])
+def test_knn_bitexact(ctx, k):
+    rng = np.random.default_rng(k)
+    dst = rng.uniform(-1, 1, size=(5000, 3)).astype(np.float32)
+    dst[100:200] = dst[:100]  # duplicates -> exact ties
+    q = rng.uniform(-1.1, 1.1, size=(700, 3)).astype(np.float32)
+    gi, gd = A.Target.build(dst, ctx).query(q, k)
+    oi, od = O.KDTree(dst).query(q, k)
+    assert np.array_equal(gi, oi) and np.array_equal(gd, od)
+
+
+# ---- Kabsch solve --------------------------------------------------------------------
+def test_kabsch_device_vs_oracle(ctx):
+    rng = np.random.default_rng(3)
+    diffs = []
+    for name in PAIR_NAMES:
+        g = load_golden(name)
+        for cov in (g["cov0"], g["cov1"]):
+            sm = O.centroid(g["src"])
+            dm = g["dmean0"]
+            ref = O.kabsch_pose(cov, sm, dm)
+            out = np.zeros(16, np.float32)
+            c = np.ascontiguousarray(cov.T).reshape(9)
+            L.check(L.lib().rst_kabsch_solve(ctx.handle, c.ctypes.data_as(C.POINTER(C.c_double)),
+                                             L.fptr(sm), L.fptr(dm), L.fptr(out)), "kabsch")
+            diffs.append(np.abs(L.cm_to_pose(out) - ref).max())
+    for _ in range(200):
+        cov = rng.normal(size=(3, 3)) * 10 ** rng.uniform(-2, 4)
+        sm = rng.normal(size=3).astype(np.float32)
+        dm = rng.normal(size=3).astype(np.float32)
+        ref = O.kabsch_pose(cov, sm, dm)
+        out = np.zeros(16, np.float32)
+        c = np.ascontiguousarray(cov.T).reshape(9)
+        L.check(L.lib().rst_kabsch_solve(ctx.handle, c.ctypes.data_as(C.POINTER(C.c_double)),
+                                         L.fptr(sm), L.fptr(dm), L.fptr(out)), "kabsch")
+        diffs.append(np.abs(L.cm_to_pose(out) - ref).max())
+    diffs = np.array(diffs)
+    assert diffs.max() <= 6e-7, diffs.max()      # <= ~1 ulp of |coef| <= 4
+    assert np.mean(diffs == 0) > 0.8
+
+
+# ---- ICP (P2POINT_REF) ----------------------------------------------------------------
+@pytest.mark.parametrize("name", GOLDEN_NAMES)
+def test_icp_matches_oracle_fp64_sums(ctx, name):
+    g = load_golden(name)
+    t = A.Target.build(g["dst"], ctx)
+    T = np.eye(4, dtype=np.float32)
+    ok = A.AlignIcp3d(g["src"], g["dst"], t, int(g["max_iter"]), T)
+    assert ok == bool(g["ok"])
+    e = pose_err(T, g["pose_final_fp64"])
+    assert max(e) <= 2e-5, e
+
+
+@pytest.mark.parametrize("name", GOLDEN_NAMES)
+def test_icp_matches_reference_arithmetic(ctx, name):
+    g = load_golden(name)
+    T = np.eye(4, dtype=np.float32)
+    ok = A.AlignIcp3d(g["src"], g["dst"], int(g["max_iter"]), T)  # 4-arg overload
+    assert ok == bool(g["ok"])
+    self_sens = max(pose_err(g["pose_final"], g["pose_final_fp64"]))
+    tol = max(1e-4, 2 * self_sens)
+    e = pose_err(T, g["pose_final"])
+    assert max(e) <= tol, (e, self_sens)
+
+
+def test_icp_first_iterations_track_oracle(ctx):
+    g = load_golden("pair_160x120_s2")
+    for it, key in ((1, "pose1"), (8, "pose8")):
+        T = np.eye(4, dtype=np.float32)
+        assert A.AlignIcp3d(g["src"], g["dst"], it, T)
+        _, To, _, _ = O.align_icp(g["src"], g["dst"], it, sum_mode=1)
+        assert max(pose_err(T, To)) <= 2e-6
+        assert max(pose_err(T, g[key])) <= 1e-4  # reference fp32 sums
+
+
+def test_icp_deterministic(ctx):
+    g = load_golden("pair_120x90_s1")
+    t = A.Target.build(g["dst"], ctx)
+    outs = []
+    for _ in range(3):
+        T = np.eye(4, dtype=np.float32)
+        A.AlignIcp3d(g["src"], g["dst"], t, 64, T)
+        outs.append(T)
+    assert all(np.array_equal(outs[0], o) for o in outs[1:])
+
+
+def test_icp_early_false_return(ctx):
+    T0 = np.eye(4, dtype=np.float32)
+    T0[1, 3] = 0.25
+    T = T0.copy()
+    assert not A.AlignIcp3d(np.zeros((2, 3), np.float32), np.ones((50, 3), np.float32), 128, T)
+    assert np.array_equal(T, T0)
+    assert not A.AlignIcp3d(np.ones((50, 3), np.float32), np.zeros((2, 3), np.float32), 128, T)
+    assert np.array_equal(T, T0)
+
+
+def test_icp_zero_iterations(ctx):
+    g = load_golden("random_128")
+    T = np.eye(4, dtype=np.float32)
+    T[0, 3] = 0.1
+    T0 = T.copy()
+    assert A.AlignIcp3d(g["src"], g["dst"], 0, T)
+    assert np.array_equal(T, T0)
+
+
+def test_icp_exact_recovery_property_full_size(ctx):
+    """640x480-sized identical clouds under a known motion: the loop must
+    recover it (size-independent property at the bench size)."""
+    K = driver.intrinsics(640, 480)
+    sc = driver.SyntheticScene(4)
+    da = sc.render(np.eye(4, dtype=np.float32), K, noise_seed=9)
+    pa = driver.unproject(da, K, ctx=ctx)
+    rng = np.random.default_rng(4)
+    D = driver.random_offset(rng)
+    Di = np.linalg.inv(D)
+    pb = (pa.astype(np.float64) @ Di[:3, :3].T + Di[:3, 3]).astype(np.float32)
+    t = A.Target.build(pa, ctx)
+    T = np.eye(4, dtype=np.float32)
+    assert A.AlignIcp3d(pb, pa, t, 128, T)
+    ang, tr = pose_err(T, D)
+    assert ang < 1e-5 and tr < 1e-5, (ang, tr)
+
+
+def test_icp_full_size_tracks_oracle_fp64(ctx):
+    """640x480 pair, 12 iterations: GPU vs the fp64-sum oracle."""
+    K = driver.intrinsics(640, 480)
+    sc = driver.SyntheticScene(5)
+    da, db, D = driver.make_pair(sc, K, seed=21)
+    pa = driver.unproject(da, K, ctx=ctx)
+    pb = driver.unproject(db, K, ctx=ctx)
+    t = A.Target.build(pa, ctx)
+    T = np.eye(4, dtype=np.float32)
+    A.AlignIcp3d(pb, pa, t, 12, T)
+    _, To, _, _ = O.align_icp(pb, pa, 12, sum_mode=1)
+    assert max(pose_err(T, To)) <= 2e-5
+    # NN at the final pose on a sample of queries, bit-exact vs brute force
+    q = O.transform_points(T, pb[:: max(1, len(pb) // 1500)])
+    gi, gd = t.query(q)
+    oi, od = O.nn_bruteforce(pa, q)
+    assert np.array_equal(gi, oi) and np.array_equal(gd, od)
+
+
+def test_device_resident_path(ctx):
+    torch = pytest.importorskip("torch")
+    g = load_golden("pair_120x90_s1")
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    try:
+        ds = torch.from_numpy(g["src"]).cuda()
+        dd = torch.from_numpy(g["dst"]).cuda()
+        t = A.Target.build_device(dd.data_ptr(), dd.shape[0], ctx)
+        buf = L.pose_to_cm(np.eye(4))
+        mc = C.c_float(0)
+        o = L.default_opts()
+        st = L.lib().rst_icp_align_device(ctx.handle, C.c_void_p(ds.data_ptr()), ds.shape[0],
+                                          t.handle, C.byref(o), L.fptr(buf), C.byref(mc))
+        assert st == 0
+        T = np.eye(4, dtype=np.float32)
+        A.AlignIcp3d(g["src"], g["dst"], t, 128, T)
+        assert np.array_equal(L.cm_to_pose(buf), T)
+    finally:
+        ctx.set_stream(None)
+
+
+def test_sharded_single_rank_equals_unsharded(ctx):
+    torch = pytest.importorskip("torch")
+    g = load_golden("pair_80x60_s0")
+    uid = C.create_string_buffer(L.COMM_ID_BYTES)
+    L.check(L.lib().rst_comm_get_unique_id(uid), "uid")
+    comm = C.c_void_p()
+    L.check(L.lib().rst_comm_create(ctx.handle, uid, 1, 0, C.byref(comm)), "comm")
+    try:
+        t = A.Target.build(g["dst"], ctx)
+        ds = torch.from_numpy(g["src"]).cuda()
+        torch.cuda.synchronize()
+        buf = L.pose_to_cm(np.eye(4))
+        mc = C.c_float(0)
+        o = L.default_opts()
+        st = L.lib().rst_icp_align_sharded_device(ctx.handle, comm, C.c_void_p(ds.data_ptr()),
+                                                  ds.shape[0], t.handle, C.byref(o),
+                                                  L.fptr(buf), C.byref(mc))
+        assert st == 0
+        T = np.eye(4, dtype=np.float32)
+        A.AlignIcp3d(g["src"], g["dst"], t, 128, T)
+        assert np.array_equal(L.cm_to_pose(buf), T)
+    finally:
+        L.lib().rst_comm_destroy(comm)
+
+
+# ---- depth -> xyz, normals, P2PLANE ---------------------------------------------------------
+@pytest.mark.parametrize("name", PAIR_NAMES)
+def test_unproject_bitexact(ctx, name):
+    g = load_golden(name)
+    h, w = g["depth_a"].shape
+    K4 = g["K4"]
+    K = driver.intrinsics(w, h, fx=K4[0], fy=K4[1], cx=K4[2], cy=K4[3], min_depth=0, max_depth=0)
+    pts = driver.unproject(g["depth_a"], K, ctx=ctx)
+    assert np.array_equal(pts, g["dst"])
+    full = driver.unproject(g["depth_a"], K, keep_invalid=True, ctx=ctx)
+    assert np.array_equal(full, O.unproject(g["depth_a"], K4, keep_invalid=True))
+
+
+@pytest.mark.parametrize("name", PAIR_NAMES)
+def test_normals_match_oracle(ctx, name):
+    g = load_golden(name)
+    t = A.Target.build(g["dst"], ctx)
+    n = A.ComputeNormals(g["dst"], t, 16)
+    cos = np.sum(n * g["normals_dst"], axis=1)
+    assert np.mean(cos > 1 - 1e-4) > 0.995, np.mean(cos > 1 - 1e-4)
+    assert np.mean(cos > 0) > 0.999
+
+
+@pytest.mark.parametrize("name", PAIR_NAMES)
+def test_p2plane_matches_restatement(ctx, name):
+    g = load_golden(name)
+    t = A.Target.build(g["dst"], ctx)
+    t.compute_normals(16)
+    s = A.Target.build(g["src"], ctx)
+    r = A.align_prepared(s, t, None, L.default_opts(mode=L.RST_P2PLANE, max_iter=30))
+    assert r.ok
+    e = pose_err(r.pose, g["p2plane_pose"])
+    assert max(e) <= 1e-4, e
+    assert max(pose_err(r.pose, g["T_gt"])) <= 3e-3
+
+
+def test_frame_prepare_device(ctx):
+    torch = pytest.importorskip("torch")
+    g = load_golden("pair_120x90_s1")
+    h, w = g["depth_a"].shape
+    K4 = g["K4"]
+    K = driver.intrinsics(w, h, fx=K4[0], fy=K4[1], cx=K4[2], cy=K4[3], min_depth=0, max_depth=0)
+    d = torch.from_numpy(g["depth_a"].astype(np.int16)).cuda()
+    torch.cuda.synchronize()
+    t = A.Target.from_depth_device(d.data_ptr(), K, normals_k=16, ctx=ctx)
+    assert len(t) == len(g["dst"])
+    idx, d2 = t.query(g["src"])
+    assert np.array_equal(idx, g["nn_idx0"]) and np.array_equal(d2, g["nn_d20"])

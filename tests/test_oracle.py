@@ -1,0 +1,164 @@
+"""CPU: the oracle against the golden vectors, the independent numpy
+restatement, brute force and hand-checkable cases."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+import np_restate as NPR
+from conftest import GOLDEN_NAMES, PAIR_NAMES, load_golden
+from oracle import oracle as O
+from posemetric import pose_err
+
+
+@pytest.mark.parametrize("name", GOLDEN_NAMES)
+def test_oracle_reproduces_golden(name):
+    g = load_golden(name)
+    it = int(g["max_iter"])
+    ok, T, mc, tr = O.align_icp(g["src"], g["dst"], it, trace=True)
+    assert np.array_equal(tr["nn_idx0"], g["nn_idx0"])
+    assert np.array_equal(tr["nn_d20"], g["nn_d20"])
+    np.testing.assert_array_equal(tr["cov"][0], g["cov0"])
+    np.testing.assert_array_equal(tr["cov"][1], g["cov1"])
+    np.testing.assert_array_equal(tr["pose"][0], g["pose1"])
+    np.testing.assert_array_equal(tr["pose"][7], g["pose8"])
+    np.testing.assert_array_equal(T, g["pose_final"])
+    assert ok == bool(g["ok"]) and np.float32(mc) == g["mean_cost"]
+    _, T64, _, _ = O.align_icp(g["src"], g["dst"], it, sum_mode=1)
+    np.testing.assert_array_equal(T64, g["pose_final_fp64"])
+
+
+@pytest.mark.parametrize("name", ["random_128", "pair_80x60_s0"])
+def test_numpy_restatement_matches_golden(name):
+    g = load_golden(name)
+    ok, T, mc, tr = NPR.align_icp(g["src"], g["dst"], int(g["max_iter"]), trace=True)
+    assert np.array_equal(tr["nn_idx0"], g["nn_idx0"])
+    assert np.array_equal(tr["nn_d20"], g["nn_d20"])
+    np.testing.assert_allclose(tr["cov"][0], g["cov0"], rtol=1e-9, atol=1e-12)
+    assert max(pose_err(T, g["pose_final"])) <= 2e-6
+
+
+@pytest.mark.parametrize("name", ["random_128", "random_2048"])
+def test_random_source_recovers_known_motion(name):
+    """Identical point sets under a known rigid motion: the reference loop
+    converges to it (to float precision)."""
+    g = load_golden(name)
+    ang, tr = pose_err(g["pose_final"], g["T_gt"])
+    assert ang < 1e-6 and tr < 1e-6
+
+
+def test_kdtree_equals_bruteforce_with_ties():
+    rng = np.random.default_rng(0)
+    # a lattice (massive exact ties) plus duplicated points plus noise
+    g = np.stack(np.meshgrid(*[np.arange(8, dtype=np.float32) * 0.25] * 3), -1).reshape(-1, 3)
+    dst = np.concatenate([g, g[:50], rng.normal(size=(300, 3)).astype(np.float32)])
+    q = np.concatenate([g + 0.125, rng.normal(size=(500, 3)).astype(np.float32), g[:20]])
+    t = O.KDTree(dst, 16)
+    i1, d1 = t.query(q)
+    i2, d2 = O.nn_bruteforce(dst, q)
+    assert np.array_equal(i1, i2) and np.array_equal(d1, d2)
+    # lowest index wins every tie
+    for k in range(len(q)):
+        dd = NPR.d2_ref(q[k][None], dst)
+        assert i1[k] == np.nonzero(dd == dd.min())[0][0]
+
+
+def test_knn_sorted_and_exact():
+    rng = np.random.default_rng(1)
+    dst = rng.uniform(-1, 1, size=(2000, 3)).astype(np.float32)
+    q = rng.uniform(-1.2, 1.2, size=(200, 3)).astype(np.float32)
+    idx, d2 = O.KDTree(dst).query(q, 16)
+    for k in range(len(q)):
+        dd = NPR.d2_ref(q[k][None], dst)
+        order = np.lexsort((np.arange(len(dst)), dd))[:16]
+        assert np.array_equal(idx[k], order) and np.array_equal(d2[k], dd[order])
+
+
+def test_nonfinite_query_keeps_reference_outparams():
+    dst = np.random.default_rng(2).normal(size=(100, 3)).astype(np.float32)
+    q = np.array([[np.nan, 0, 0], [np.inf, 1, 1], [0, 0, 0]], np.float32)
+    idx, d2 = O.KDTree(dst).query(q)
+    assert idx[0] == 0 and d2[0] == np.finfo(np.float32).max
+    assert idx[1] == 0 and d2[1] == np.finfo(np.float32).max
+    assert d2[2] < 10
+
+
+def test_centroid_is_fp32_sequential():
+    rng = np.random.default_rng(3)
+    c = rng.uniform(0, 5, size=(100003, 3)).astype(np.float32)
+    np.testing.assert_array_equal(O.centroid(c), NPR.centroid(c))
+
+
+def test_jacobi_svd_reconstructs():
+    rng = np.random.default_rng(4)
+    for _ in range(50):
+        A = rng.normal(size=(3, 3)) * rng.uniform(1e-3, 1e4)
+        U, S, V = O.jacobi_svd3(A)
+        np.testing.assert_allclose(U @ np.diag(S) @ V.T, A, atol=1e-12 * np.abs(A).max() * 10)
+        np.testing.assert_allclose(U.T @ U, np.eye(3), atol=1e-13)
+        np.testing.assert_allclose(V.T @ V, np.eye(3), atol=1e-13)
+        assert np.all(np.diff(S) <= 0)
+        np.testing.assert_allclose(S, np.linalg.svd(A)[1], rtol=1e-12)
+
+
+def test_kabsch_matches_numpy_restatement():
+    rng = np.random.default_rng(5)
+    for _ in range(50):
+        cov = rng.normal(size=(3, 3)) * 100
+        sm = rng.normal(size=3).astype(np.float32)
+        dm = rng.normal(size=3).astype(np.float32)
+        a = O.kabsch_pose(cov, sm, dm)
+        b = NPR.kabsch_pose(cov, sm, dm)
+        assert max(pose_err(a, b)) < 1e-6
+
+
+def test_early_false_return_leaves_pose():
+    T0 = np.diag([1, 1, 1, 1]).astype(np.float32)
+    T0[0, 3] = 0.5
+    ok, T, mc, _ = O.align_icp(np.zeros((2, 3), np.float32), np.zeros((10, 3), np.float32), 128, T0)
+    assert not ok and np.array_equal(T, T0)
+    ok, T, _, _ = O.align_icp(np.zeros((10, 3), np.float32), np.zeros((2, 3), np.float32), 128, T0)
+    assert not ok and np.array_equal(T, T0)
+
+
+def test_zero_iterations_is_identity_true():
+    g = load_golden("random_128")
+    ok, T, mc, _ = O.align_icp(g["src"], g["dst"], 0)
+    assert ok and mc == 0.0 and np.array_equal(T, np.eye(4, dtype=np.float32))
+
+
+def test_mu_schedule():
+    g = load_golden("random_128")
+    mu = g["mu"]
+    exp = np.float32(1.0)
+    for it in range(len(mu)):
+        if it > 0 and it % 8 == 0:
+            exp = np.float32(exp / np.float32(1.4))
+        assert mu[it] == exp
+
+
+@pytest.mark.parametrize("name", PAIR_NAMES)
+def test_unproject_oracle_is_pinhole(name):
+    g = load_golden(name)
+    K4 = g["K4"]
+    pts = O.unproject(g["depth_a"], K4)
+    np.testing.assert_array_equal(pts, g["dst"])
+    v, u = np.nonzero(g["depth_a"])
+    z = np.float32(0.001) * g["depth_a"][v, u].astype(np.float32)
+    x = ((u.astype(np.float32) - K4[2]) / K4[0]).astype(np.float32)
+    np.testing.assert_array_equal(pts[:, 0], z * x)
+
+
+@pytest.mark.parametrize("name", PAIR_NAMES)
+def test_p2plane_oracle_converges_to_ground_truth(name):
+    g = load_golden(name)
+    ang, tr = pose_err(g["p2plane_pose"], g["T_gt"])
+    assert ang < 2e-3 and tr < 3e-3, (ang, tr)
+    assert 1 <= int(g["p2plane_iters"]) <= 30
+
+
+def test_normals_oracle_unit_and_oriented():
+    g = load_golden("pair_80x60_s0")
+    n = g["normals_dst"]
+    np.testing.assert_allclose(np.linalg.norm(n, axis=1), 1.0, atol=1e-5)
+    assert np.all(np.sum(g["dst"] * n, axis=1) <= 0)  # face the viewpoint (origin)
