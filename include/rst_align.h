@@ -122,6 +122,14 @@ int rst_target_query_nn(rst_ctx* ctx, const rst_target* tgt, const float* q,
 int rst_target_query_nn_device(rst_ctx* ctx, const rst_target* tgt,
                                const float* d_q, int64_t nq, int32_t* d_idx,
                                float* d_d2);
+/* The same exact 1-NN, for spatially coherent query batches (e.g. one
+ * frame's points in scan order) with optional warm candidates: warm[i] =
+ * a target index believed close to q[i] (the previous frame's answer), <0
+ * = none; warm may be NULL.  Runs the ICP loop's wave-cooperative search;
+ * results are identical to rst_target_query_nn for any input. */
+int rst_target_query_nn_warm(rst_ctx* ctx, const rst_target* tgt, const float* q,
+                             int64_t nq, const int32_t* warm, int32_t* idx,
+                             float* d2);
 /* Exact k-NN (k <= 32), results sorted by (d2, idx). */
 int rst_target_query_knn(rst_ctx* ctx, const rst_target* tgt, const float* q,
                          int64_t nq, int k, int32_t* idx, float* d2);

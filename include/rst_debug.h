@@ -1,0 +1,25 @@
+/*
+ * rst_debug.h -- diagnostics of the MI355X ICP library (not part of the
+ * drop-in boundary; used by scripts/ and tests/ to explain performance).
+ */
+#ifndef RST_DEBUG_H_
+#define RST_DEBUG_H_
+
+#include "rst_align.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* rst_target_query_nn_warm plus per-wavefront search statistics: stats
+ * receives 8 int32 per 64 queries (staging rounds, nodes tested, leaves
+ * staged, leaves scanned, flushes, active lanes, lanes without a finite
+ * starting bound, region extent in micrometres). */
+int rst_debug_query_nn_warm_stats(rst_ctx* ctx, const rst_target* tgt, const float* q,
+                                  int64_t nq, const int32_t* warm, int32_t* idx, float* d2,
+                                  int32_t* stats);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RST_DEBUG_H_ */

@@ -59,6 +59,8 @@ PROTOTYPES = {
     "rst_target_get_normals": (C.c_int, [_P, _P, c_float_p]),
     "rst_target_query_nn": (C.c_int, [_P, _P, c_float_p, C.c_int64, c_int32_p, c_float_p]),
     "rst_target_query_nn_device": (C.c_int, [_P, _P, _P, C.c_int64, _P, _P]),
+    "rst_target_query_nn_warm": (C.c_int, [_P, _P, c_float_p, C.c_int64, c_int32_p, c_int32_p,
+                                           c_float_p]),
     "rst_target_query_knn": (C.c_int, [_P, _P, c_float_p, C.c_int64, C.c_int, c_int32_p,
                                        c_float_p]),
     "rst_icp_align": (C.c_int, [_P, c_float_p, C.c_int64, _P, C.POINTER(IcpOpts), c_float_p,
@@ -92,10 +94,28 @@ PROTOTYPES = {
 _lib = None
 
 
+def _share_torch_runtime() -> None:
+    """One HIP runtime per process.  The torch wheel bundles its own
+    libamdhip64 / libhsa-runtime64 / librccl with the same sonames as
+    /opt/rocm's; whichever is mapped first satisfies our library's NEEDED
+    entries.  If ours were loaded first, a later `import torch` would map a
+    second runtime and the two tear each other down at exit ("free():
+    invalid pointer").  So when torch is importable it is imported first and
+    our library binds to its runtime; without torch, /opt/rocm's is used.
+    RST_NO_TORCH=1 skips this (pure C-ABI processes)."""
+    if os.environ.get("RST_NO_TORCH") == "1":
+        return
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
+
+
 def lib() -> C.CDLL:
     """Load librst_align.so (raises if it is absent: no fallback path)."""
     global _lib
     if _lib is None:
+        _share_torch_runtime()
         if not LIB_PATH.exists():
             raise ImportError(
                 f"realsensetracker_amd: HIP library not built ({LIB_PATH}); run "

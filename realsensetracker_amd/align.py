@@ -137,6 +137,23 @@ class Target:
                                              num_closest, L.iptr(idx), L.fptr(d2)), "query_knn")
         return idx, d2
 
+    def query_warm(self, points, warm=None):
+        """Exact 1-NN of a spatially coherent batch, optionally seeded with
+        warm candidate indices (e.g. the previous frame's answer)."""
+        q = L.as_cloud(points)
+        n = q.shape[0]
+        idx = np.zeros(n, np.int32)
+        d2 = np.zeros(n, np.float32)
+        w = None
+        if warm is not None:
+            w = np.ascontiguousarray(np.asarray(warm, np.int32))
+            if w.shape != (n,):
+                raise ValueError("warm must have one entry per query")
+        L.check(L.lib().rst_target_query_nn_warm(self.ctx.handle, self._h, L.fptr(q), n,
+                                                 L.iptr(w) if w is not None else None,
+                                                 L.iptr(idx), L.fptr(d2)), "query_nn_warm")
+        return idx, d2
+
     def compute_normals(self, k: int = 16, viewpoint=(0.0, 0.0, 0.0)):
         vp = np.asarray(viewpoint, np.float32)
         L.check(L.lib().rst_target_compute_normals(self.ctx.handle, self._h, k, L.fptr(vp)),

@@ -28,7 +28,7 @@ ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 ARCH = os.environ.get("RST_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = ["build.hip", "query.hip", "icp.hip", "capi.hip", "unproject.hip", "comm.hip", "synth.cpp"]
-HEADERS = ["rst_internal.hpp", "rst_device.hpp"]
+HEADERS = ["rst_internal.hpp", "rst_device.hpp", "rst_bvh.hpp"]
 LIB_NAME = "librst_align.so"
 
 # -ffp-contract=off: reference-exact rounding of the transform / distance /

@@ -224,6 +224,13 @@ __global__ __launch_bounds__(kBS) void k_gather(const float* __restrict__ xyz,
                        xyz[3 * (int64_t)j + 2], __int_as_float((int)j));
 }
 
+// inverse permutation: inv[original index] = sorted position
+__global__ __launch_bounds__(kBS) void k_inverse(const uint32_t* __restrict__ perm, int64_t m,
+                                                 int32_t* __restrict__ inv) {
+  const int64_t i = blockIdx.x * (int64_t)kBS + threadIdx.x;
+  if (i < m) inv[perm[i]] = (int32_t)i;
+}
+
 // sorted position of original index 0 (the reference's dst.GetPoint(0)
 // when nanoflann returns no neighbour)
 __global__ __launch_bounds__(kBS) void k_find_pos0(const uint32_t* __restrict__ perm, int64_t m,
@@ -232,63 +239,9 @@ __global__ __launch_bounds__(kBS) void k_find_pos0(const uint32_t* __restrict__ 
   if (i < m && perm[i] == 0u) *out = (int32_t)i;
 }
 
-__global__ __launch_bounds__(kBS) void k_leaf_start(int32_t* __restrict__ ls,
-                                                    int64_t m, int nleaves) {
-  const int64_t L = blockIdx.x * (int64_t)kBS + threadIdx.x;
-  if (L > nleaves) return;
-  ls[L] = (int32_t)(L * m / nleaves);
-}
-
-__global__ __launch_bounds__(kBS) void k_leaf_boxes(const float4* __restrict__ pts,
-                                                    const int32_t* __restrict__ ls,
-                                                    int nleaves,
-                                                    float4* __restrict__ nodes) {
+__global__ __launch_bounds__(kBS) void k_leaf_boxes(BvhView bv, float4* __restrict__ nodes) {
   const int L = blockIdx.x * kBS + threadIdx.x;
-  if (L >= nleaves) return;
-  float4 lo = make_float4(INFINITY, INFINITY, INFINITY, 0.0f);
-  float4 hi = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.0f);
-  for (int i = ls[L]; i < ls[L + 1]; ++i) {
-    const float4 p = pts[i];
-    if (!(__builtin_isfinite(p.x) && __builtin_isfinite(p.y) && __builtin_isfinite(p.z)))
-      continue;
-    lo.x = fminf(lo.x, p.x); lo.y = fminf(lo.y, p.y); lo.z = fminf(lo.z, p.z);
-    hi.x = fmaxf(hi.x, p.x); hi.y = fmaxf(hi.y, p.y); hi.z = fmaxf(hi.z, p.z);
-  }
-  const int k = nleaves + L;
-  nodes[2 * k] = lo;
-  nodes[2 * k + 1] = hi;
-}
-
-__device__ __forceinline__ void make_internal(float4* __restrict__ nodes, int k) {
-  const float4 l0 = nodes[2 * (2 * k)], h0 = nodes[2 * (2 * k) + 1];
-  const float4 l1 = nodes[2 * (2 * k + 1)], h1 = nodes[2 * (2 * k + 1) + 1];
-  float4 lo, hi;
-  lo.x = fminf(l0.x, l1.x); lo.y = fminf(l0.y, l1.y); lo.z = fminf(l0.z, l1.z);
-  hi.x = fmaxf(h0.x, h1.x); hi.y = fmaxf(h0.y, h1.y); hi.z = fmaxf(h0.z, h1.z);
-  const bool e0 = !(l0.x <= h0.x), e1 = !(l1.x <= h1.x);  // empty children
-  float split;
-  int ab;
-  if (e0 || e1) {
-    // near child = the non-empty one: left if right is empty
-    ab = 0;
-    split = e1 ? INFINITY : -INFINITY;
-  } else {
-    const float c0[3] = {0.5f * (l0.x + h0.x), 0.5f * (l0.y + h0.y), 0.5f * (l0.z + h0.z)};
-    const float c1[3] = {0.5f * (l1.x + h1.x), 0.5f * (l1.y + h1.y), 0.5f * (l1.z + h1.z)};
-    int ax = 0;
-    float best = fabsf(c1[0] - c0[0]);
-    for (int a = 1; a < 3; ++a)
-      if (fabsf(c1[a] - c0[a]) > best) {
-        best = fabsf(c1[a] - c0[a]);
-        ax = a;
-      }
-    split = 0.5f * (c0[ax] + c1[ax]);
-    ab = ax | (c0[ax] <= c1[ax] ? 0 : 4);
-  }
-  lo.w = split;
-  hi.w = __int_as_float(ab);
-  nodes[2 * k] = lo;
-  nodes[2 * k + 1] = hi;
+  if (L < bv.nleaves) make_leaf(bv, nodes, L);
 }
 
 __global__ __launch_bounds__(kBS) void k_level(float4* __restrict__ nodes, int lo_k,
@@ -332,7 +285,18 @@ int radix_sort_pairs(rst_ctx* ctx, uint32_t* keys, uint32_t* vals, uint32_t* ktm
 
 size_t target_index_bytes(const rst_target* t) {
   if (!t->has_bvh) return 0;
-  return (size_t)4 * t->nleaves * sizeof(float4) + (size_t)(t->nleaves + 1) * 4;
+  return (size_t)4 * t->nleaves * sizeof(float4);
+}
+
+BvhView view_of(const rst_target* t) {
+  BvhView v;
+  v.pts = t->pts;
+  v.nodes = t->nodes;
+  v.m = (int32_t)t->m;
+  v.nleaves = t->nleaves;
+  v.lg = t->lg;
+  v.pad = 0;
+  return v;
 }
 
 int target_build_device(rst_ctx* ctx, const float* d_xyz, int64_t m, bool with_bvh,
@@ -344,16 +308,22 @@ int target_build_device(rst_ctx* ctx, const float* d_xyz, int64_t m, bool with_b
   t->m = m;
   hipStream_t st = ctx->stream;
   int64_t nl = 1;
-  while (nl * kLeafTarget < m) nl <<= 1;
+  int lg = 0;
+  while (nl * kLeafTarget < m) {
+    nl <<= 1;
+    ++lg;
+  }
   t->nleaves = (int32_t)nl;
+  t->lg = lg;
   const int64_t mp = std::max<int64_t>(m, 1);
-  if (hipMalloc(&t->pts, sizeof(float4) * mp) != hipSuccess) {
+  if (hipMalloc(&t->pts, sizeof(float4) * mp) != hipSuccess ||
+      hipMalloc(&t->inv, sizeof(int32_t) * mp) != hipSuccess) {
+    if (t->pts) hipFree(t->pts);
     delete t;
     return RST_E_NOMEM;
   }
   if (with_bvh) {
-    if (hipMalloc(&t->nodes, sizeof(float4) * 4 * nl) != hipSuccess ||
-        hipMalloc(&t->leaf_start, sizeof(int32_t) * (nl + 1)) != hipSuccess) {
+    if (hipMalloc(&t->nodes, sizeof(float4) * 4 * nl) != hipSuccess) {
       rst_target_free(t);
       return RST_E_NOMEM;
     }
@@ -401,9 +371,9 @@ int target_build_device(rst_ctx* ctx, const float* d_xyz, int64_t m, bool with_b
   }
   k_gather<<<blocks_for(m), kBS, 0, st>>>(d_xyz, vals, m, t->pts);
   k_find_pos0<<<blocks_for(m), kBS, 0, st>>>(vals, m, (int32_t*)(bbox + 6));
+  k_inverse<<<blocks_for(m), kBS, 0, st>>>(vals, m, t->inv);
   if (with_bvh) {
-    k_leaf_start<<<blocks_for(nl + 1), kBS, 0, st>>>(t->leaf_start, m, (int)nl);
-    k_leaf_boxes<<<blocks_for(nl), kBS, 0, st>>>(t->pts, t->leaf_start, (int)nl, t->nodes);
+    k_leaf_boxes<<<blocks_for(nl), kBS, 0, st>>>(view_of(t), t->nodes);
     int64_t cnt = nl / 2;
     while (cnt >= 2 * kBS) {
       k_level<<<blocks_for(cnt), kBS, 0, st>>>(t->nodes, (int)cnt, (int)cnt);

@@ -99,6 +99,8 @@ static int upload_xyz(rst_ctx* ctx, const float* h, int64_t n, float** d_out) {
 
 using namespace rst;
 
+#include "rst_debug.h"
+
 extern "C" {
 
 int rst_abi_version(void) { return RST_ABI_VERSION; }
@@ -222,8 +224,8 @@ int rst_target_free(rst_target* t) {
   // touch its context, which may already be gone
   if (t->pts) hipFree(t->pts);
   if (t->nodes) hipFree(t->nodes);
-  if (t->leaf_start) hipFree(t->leaf_start);
   if (t->nrm) hipFree(t->nrm);
+  if (t->inv) hipFree(t->inv);
   delete t;
   return RST_OK;
 }
@@ -275,6 +277,47 @@ int rst_target_query_nn(rst_ctx* ctx, const rst_target* t, const float* q, int64
   void* dout = nullptr;
   int s = ctx_workspace(ctx, (sizeof(int32_t) + sizeof(float)) * nq, &dout);
   if (s >= 0) s = query_nn_device(ctx, t, dq, nq, (int32_t*)dout, (float*)((int32_t*)dout + nq));
+  if (s >= 0) {
+    if (hipMemcpyAsync(idx, dout, sizeof(int32_t) * nq, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+        hipMemcpyAsync(d2, (int32_t*)dout + nq, sizeof(float) * nq, hipMemcpyDeviceToHost,
+                       ctx->stream) != hipSuccess ||
+        hipStreamSynchronize(ctx->stream) != hipSuccess)
+      s = RST_E_HIP;
+  }
+  hipStreamSynchronize(ctx->stream);
+  hipFree(dq);
+  return s < 0 ? s : RST_OK;
+}
+
+int rst_target_query_nn_warm(rst_ctx* ctx, const rst_target* t, const float* q, int64_t nq,
+                             const int32_t* warm, int32_t* idx, float* d2) {
+  return rst_debug_query_nn_warm_stats(ctx, t, q, nq, warm, idx, d2, nullptr);
+}
+
+int rst_debug_query_nn_warm_stats(rst_ctx* ctx, const rst_target* t, const float* q, int64_t nq,
+                                  const int32_t* warm, int32_t* idx, float* d2, int32_t* stats) {
+  if (!ctx || !t || nq < 0 || (nq > 0 && (!q || !idx || !d2))) return RST_E_ARG;
+  if (nq == 0) return RST_OK;
+  RST_HIP(hipSetDevice(ctx->device));
+  float* dq = nullptr;
+  RST_CHECK(upload_xyz(ctx, q, nq, &dq));
+  void* dout = nullptr;
+  const int64_t nwav = (nq + 63) / 64;
+  int s = ctx_workspace(ctx, (2 * sizeof(int32_t) + sizeof(float)) * nq + 32 * nwav + 256, &dout);
+  int32_t* dwarm = nullptr;
+  int* dstats = stats ? (int*)((int32_t*)dout + 3 * nq + 16) : nullptr;
+  if (s >= 0 && warm) {
+    dwarm = (int32_t*)dout + 2 * nq;
+    if (hipMemcpyAsync(dwarm, warm, sizeof(int32_t) * nq, hipMemcpyHostToDevice, ctx->stream) !=
+        hipSuccess)
+      s = RST_E_HIP;
+  }
+  if (s >= 0)
+    s = query_nn_warm_device(ctx, t, dq, nq, dwarm, (int32_t*)dout, (float*)((int32_t*)dout + nq),
+                             dstats);
+  if (s >= 0 && stats &&
+      hipMemcpyAsync(stats, dstats, 32 * nwav, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess)
+    s = RST_E_HIP;
   if (s >= 0) {
     if (hipMemcpyAsync(idx, dout, sizeof(int32_t) * nq, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
         hipMemcpyAsync(d2, (int32_t*)dout + nq, sizeof(float) * nq, hipMemcpyDeviceToHost,

@@ -18,6 +18,7 @@
 #include <cstring>
 
 #include "rst_device.hpp"
+#include "rst_wave_nn.hpp"
 #include "rst_internal.hpp"
 
 namespace rst {
@@ -34,6 +35,21 @@ __device__ __forceinline__ Pose3 load_pose(const IcpState* __restrict__ st) {
 #pragma unroll
   for (int k = 0; k < 3; ++k) P.t[k] = st->t[k];
   return P;
+}
+
+// Exact 1-NN of one query per lane, seeded by a warm candidate (sorted
+// target position, -1 = cold): the candidate's own d2 is the lane's first
+// bound, then the wave-cooperative search of rst_wave_nn.hpp.
+__device__ __forceinline__ Best1 nn_seeded(const BvhView& bv, bool act, int warm, float qx,
+                                           float qy, float qz, WnnScratch& ws) {
+  Best1 r;
+  r.init();
+  if (act && warm >= 0) {
+    const float4 p = bv.pts[warm];
+    r.offer(d2_ref(qx, qy, qz, p.x, p.y, p.z), f2i(p.w), warm);
+  }
+  nn_wave_region(bv, act, qx, qy, qz, r, ws);
+  return r;
 }
 
 // ---- centroid ------------------------------------------------------------------
@@ -148,12 +164,12 @@ __global__ __launch_bounds__(kBS) void k_p2point(BvhView bv, const float4* __res
   const float4 s = act ? src[i] : make_float4(0.f, 0.f, 0.f, 0.f);
   float px, py, pz;
   xform(P, s.x, s.y, s.z, px, py, pz);  // :107
-  float bd;
-  int bi, bp;
-  // :112 exact 1-NN: warm-started from the previous iteration's neighbour,
-  // then one cooperative BVH walk per wave
-  nn_warm(bv, act ? nnpos[i] : -1, px, py, pz, bd, bi, bp);
-  nn_wave(bv, act, px, py, pz, bd, bi, bp);
+  // :112 exact 1-NN: the wave's 64 queries search together, each lane
+  // seeded with its previous neighbour
+  __shared__ WnnScratch wsc[kBS / kWave];
+  const Best1 r = nn_seeded(bv, act, act ? nnpos[i] : -1, px, py, pz, wsc[threadIdx.x / kWave]);
+  const float bd = r.d;
+  const int bp = r.pos;
   if (act) {
     nnpos[i] = bp;
     const float l = mu / (bd + mu);         // :116-117
@@ -268,10 +284,10 @@ __global__ __launch_bounds__(kBS) void k_p2plane(BvhView bv, const float4* __res
   const float4 s = act ? src[i] : make_float4(0.f, 0.f, 0.f, 0.f);
   float px, py, pz;
   xform(P, s.x, s.y, s.z, px, py, pz);
-  float bd;
-  int bi, bp;
-  nn_warm(bv, act ? nnpos[i] : -1, px, py, pz, bd, bi, bp);
-  nn_wave(bv, act, px, py, pz, bd, bi, bp);
+  __shared__ WnnScratch wsc[kBS / kWave];
+  const Best1 r = nn_seeded(bv, act, act ? nnpos[i] : -1, px, py, pz, wsc[threadIdx.x / kWave]);
+  const float bd = r.d;
+  const int bp = r.pos;
   if (act) {
     nnpos[i] = bp;
     if (bp >= 0 && bd <= max_d2) {
@@ -529,11 +545,7 @@ int icp_align_prepared(rst_ctx* ctx, const rst_target* src, const rst_target* tg
                                                  : FLT_MAX;
   prm.max_iter = opts.max_iter;
 
-  BvhView bv;
-  bv.pts = tgt->pts;
-  bv.nodes = tgt->nodes;
-  bv.leaf_start = tgt->leaf_start;
-  bv.nleaves = tgt->nleaves;
+  const BvhView bv = view_of(tgt);
 
   const bool timing = ctx->timing && opts.max_iter > 0;
   if (timing) {

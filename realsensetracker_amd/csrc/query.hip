@@ -12,6 +12,7 @@
 #include <cmath>
 
 #include "rst_device.hpp"
+#include "rst_wave_nn.hpp"
 #include "rst_internal.hpp"
 
 namespace rst {
@@ -19,93 +20,49 @@ namespace {
 
 constexpr int kBS = 256;
 
-__global__ __launch_bounds__(kBS) void k_query_nn(BvhView bv,
-                                                  const float* __restrict__ q,
-                                                  int64_t nq,
-                                                  int32_t* __restrict__ idx,
+// One query per lane, top-down from the root (no warm candidate).
+__global__ __launch_bounds__(kBS) void k_query_nn(BvhView bv, const float* __restrict__ q,
+                                                  int64_t nq, int32_t* __restrict__ idx,
                                                   float* __restrict__ d2) {
   const int64_t i = blockIdx.x * (int64_t)kBS + threadIdx.x;
   if (i >= nq) return;
-  float bd;
-  int bi, bp;
-  nn_exact(bv, q[3 * i], q[3 * i + 1], q[3 * i + 2], bd, bi, bp);
-  idx[i] = bi;
-  d2[i] = bd;
+  Best1 r;
+  r.init();
+  search(bv, -1, q[3 * i], q[3 * i + 1], q[3 * i + 2], r);
+  idx[i] = r.id;
+  d2[i] = r.d;
 }
 
-// Sorted (d2, idx) list of K candidates kept in registers; branch-free
-// insertion (static indices only, no scratch).
-template <int K>
-struct KnnList {
-  float d[K];
-  int id[K];
-  int pos[K];
-  __device__ __forceinline__ void init() {
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-      d[j] = FLT_MAX;
-      id[j] = 0x7fffffff;
-      pos[j] = -1;
+// Coherent queries with warm candidates (original target indices, <0 or
+// out of range = none): the wave-cooperative search the ICP loop uses.
+__global__ __launch_bounds__(kBS) void k_query_nn_warm(BvhView bv, const int32_t* __restrict__ inv,
+                                                       const float* __restrict__ q, int64_t nq,
+                                                       const int32_t* __restrict__ warm,
+                                                       int32_t* __restrict__ idx,
+                                                       float* __restrict__ d2,
+                                                       int* __restrict__ stats) {
+  __shared__ WnnScratch wsc[kBS / kWave];
+  const int64_t i = blockIdx.x * (int64_t)kBS + threadIdx.x;
+  const bool act = i < nq;
+  float qx = 0.f, qy = 0.f, qz = 0.f;
+  Best1 r;
+  r.init();
+  if (act) {
+    qx = q[3 * i];
+    qy = q[3 * i + 1];
+    qz = q[3 * i + 2];
+    const int w = warm ? warm[i] : -1;
+    if (w >= 0 && w < bv.m) {
+      const int pos = inv[w];
+      const float4 p = bv.pts[pos];
+      r.offer(d2_ref(qx, qy, qz, p.x, p.y, p.z), f2i(p.w), pos);
     }
   }
-  __device__ __forceinline__ static bool better(float a, int ia, float b, int ib) {
-    return (a < b) || ((a == b) && (ia < ib));
-  }
-  __device__ __forceinline__ float worst() const { return d[K - 1]; }
-  __device__ __forceinline__ void insert(float nd, int nid, int np) {
-    if (!(nd < FLT_MAX) || !better(nd, nid, d[K - 1], id[K - 1])) return;
-#pragma unroll
-    for (int j = K - 1; j >= 1; --j) {
-      const bool shift = better(nd, nid, d[j - 1], id[j - 1]);
-      const bool here = !shift && better(nd, nid, d[j], id[j]);
-      d[j] = shift ? d[j - 1] : (here ? nd : d[j]);
-      id[j] = shift ? id[j - 1] : (here ? nid : id[j]);
-      pos[j] = shift ? pos[j - 1] : (here ? np : pos[j]);
-    }
-    if (better(nd, nid, d[0], id[0])) {
-      d[0] = nd;
-      id[0] = nid;
-      pos[0] = np;
-    }
-  }
-};
-
-// Exact kNN by the same stackless traversal as nn_exact; prune bound is the
-// K-th best d2 (FLT_MAX until K points are held).
-template <int K>
-__device__ __forceinline__ void knn_exact(const BvhView& bv, float qx, float qy,
-                                          float qz, KnnList<K>& L) {
-  L.init();
-  if (!(__builtin_isfinite(qx) && __builtin_isfinite(qy) && __builtin_isfinite(qz)))
-    return;
-  const int nl = bv.nleaves;
-  int cur = 1, prev = 0;
-  while (cur != 0) {
-    const int parent = cur >> 1;
-    const float4 lo = bv.nodes[2 * cur];
-    const float4 hi = bv.nodes[2 * cur + 1];
-    int next;
-    if (prev == parent) {
-      const float bd = box_d2(qx, qy, qz, lo, hi);
-      if (bd > L.worst()) {
-        next = parent;
-      } else if (cur >= nl) {
-        const int Lf = cur - nl;
-        const int b = bv.leaf_start[Lf], e = bv.leaf_start[Lf + 1];
-        for (int i = b; i < e; ++i) {
-          const float4 p = bv.pts[i];
-          L.insert(d2_ref(qx, qy, qz, p.x, p.y, p.z), __float_as_int(p.w), i);
-        }
-        next = parent;
-      } else {
-        next = near_child(cur, lo, hi, qx, qy, qz);
-      }
-    } else {
-      const int nc = near_child(cur, lo, hi, qx, qy, qz);
-      next = (prev == nc) ? (prev ^ 1) : parent;
-    }
-    prev = cur;
-    cur = next;
+  nn_wave_region(bv, act, qx, qy, qz, r, wsc[threadIdx.x / kWave],
+                 stats ? stats + 8 * (int64_t)(i / kWave) : nullptr);
+  if (act) {
+    idx[i] = r.id;
+    d2[i] = r.d;
   }
 }
 
@@ -116,8 +73,9 @@ __global__ __launch_bounds__(kBS) void k_query_knn(BvhView bv, const float* __re
                                                    float* __restrict__ d2) {
   const int64_t i = blockIdx.x * (int64_t)kBS + threadIdx.x;
   if (i >= nq) return;
-  KnnList<K> L;
-  knn_exact<K>(bv, q[3 * i], q[3 * i + 1], q[3 * i + 2], L);
+  BestK<K> L;
+  L.init();
+  search(bv, -1, q[3 * i], q[3 * i + 1], q[3 * i + 2], L);
 #pragma unroll
   for (int j = 0; j < K; ++j) {
     if (j < k) {
@@ -185,8 +143,10 @@ __global__ __launch_bounds__(kBS) void k_normals(BvhView bv, int64_t m, float vx
   const int64_t i = blockIdx.x * (int64_t)kBS + threadIdx.x;
   if (i >= m) return;
   const float4 p = bv.pts[i];
-  KnnList<K> L;
-  knn_exact<K>(bv, p.x, p.y, p.z, L);
+  // the query is target point i itself: bottom-up from its own leaf
+  BestK<K> L;
+  L.init();
+  search(bv, (int)i, p.x, p.y, p.z, L);
   // centroid in result order, fp32 (point_cloud_utils.cpp:186-191)
   float cx = 0.f, cy = 0.f, cz = 0.f;
 #pragma unroll
@@ -226,15 +186,6 @@ __global__ __launch_bounds__(kBS) void k_normals(BvhView bv, int64_t m, float vx
 
 inline int blocks_for(int64_t n) { return (int)std::max<int64_t>(1, (n + kBS - 1) / kBS); }
 
-BvhView view_of(const rst_target* t) {
-  BvhView v;
-  v.pts = t->pts;
-  v.nodes = t->nodes;
-  v.leaf_start = t->leaf_start;
-  v.nleaves = t->nleaves;
-  return v;
-}
-
 }  // namespace
 
 int query_nn_device(rst_ctx* ctx, const rst_target* tgt, const float* d_q, int64_t nq,
@@ -251,6 +202,17 @@ int query_nn_device(rst_ctx* ctx, const rst_target* tgt, const float* d_q, int64
     return RST_OK;
   }
   k_query_nn<<<blocks_for(nq), kBS, 0, ctx->stream>>>(view_of(tgt), d_q, nq, d_idx, d_d2);
+  RST_HIP(hipGetLastError());
+  return RST_OK;
+}
+
+int query_nn_warm_device(rst_ctx* ctx, const rst_target* tgt, const float* d_q, int64_t nq,
+                         const int32_t* d_warm, int32_t* d_idx, float* d_d2, int* d_stats) {
+  if (!ctx || !tgt || nq < 0 || !tgt->has_bvh) return RST_E_ARG;
+  if (nq == 0) return RST_OK;
+  if (tgt->m == 0) return query_nn_device(ctx, tgt, d_q, nq, d_idx, d_d2);
+  k_query_nn_warm<<<blocks_for(nq), kBS, 0, ctx->stream>>>(view_of(tgt), tgt->inv, d_q, nq, d_warm,
+                                                           d_idx, d_d2, d_stats);
   RST_HIP(hipGetLastError());
   return RST_OK;
 }

@@ -11,6 +11,8 @@
 #include <cfloat>
 #include <cstdint>
 
+#include "rst_bvh.hpp"
+
 namespace rst {
 
 constexpr int kWave = 64;
@@ -38,186 +40,6 @@ __device__ __forceinline__ void xform(const Pose3& P, float sx, float sy,
   px = P.t[0] + mv_row(P.r, 0, sx, sy, sz);
   py = P.t[1] + mv_row(P.r, 1, sx, sy, sz);
   pz = P.t[2] + mv_row(P.r, 2, sx, sy, sz);
-}
-
-// nanoflann L2_Adaptor::evalMetric for DIM=3: ((dx*dx + dy*dy) + dz*dz),
-// d = query - point (kdtree.hpp:51-57).
-__device__ __forceinline__ float d2_ref(float qx, float qy, float qz,
-                                        float px, float py, float pz) {
-  const float dx = qx - px;
-  const float dy = qy - py;
-  const float dz = qz - pz;
-  float r = dx * dx;
-  r = r + dy * dy;
-  r = r + dz * dz;
-  return r;
-}
-
-// Lower bound of d2_ref over every point of an AABB: per-axis gaps are
-// monotone in float, so this never exceeds any contained point's d2_ref.
-__device__ __forceinline__ float box_d2(float qx, float qy, float qz,
-                                        const float4& lo, const float4& hi) {
-  const float ex = fmaxf(fmaxf(lo.x - qx, qx - hi.x), 0.0f);
-  const float ey = fmaxf(fmaxf(lo.y - qy, qy - hi.y), 0.0f);
-  const float ez = fmaxf(fmaxf(lo.z - qz, qz - hi.z), 0.0f);
-  float r = ex * ex;
-  r = r + ey * ey;
-  r = r + ez * ez;
-  return r;
-}
-
-// ---- BVH view ---------------------------------------------------------------
-struct BvhView {
-  const float4* __restrict__ pts;      // sorted points, .w = orig idx bits
-  const float4* __restrict__ nodes;    // 2 float4 per heap node
-  const int32_t* __restrict__ leaf_start;
-  int32_t nleaves;
-};
-
-__device__ __forceinline__ int near_child(int k, const float4& lo,
-                                          const float4& hi, float qx,
-                                          float qy, float qz) {
-  const int ab = __float_as_int(hi.w);
-  const int ax = ab & 3;
-  const float qa = ax == 0 ? qx : (ax == 1 ? qy : qz);
-  const bool q_low = qa < lo.w;
-  const bool left_low = (ab & 4) == 0;
-  return (q_low == left_low) ? (2 * k) : (2 * k + 1);
-}
-
-// Exact 1-NN by stackless depth-first traversal of the heap BVH (near child
-// first, parent recovered as k>>1).  Result = lexicographic min of
-// (d2, orig idx) over points with d2 < FLT_MAX; nothing found -> (0,FLT_MAX),
-// which is what the reference's out-params hold when nanoflann adds no
-// point (align_icp.cpp:110-112, KNNResultSet::init).
-__device__ __forceinline__ void nn_exact(const BvhView& bv, float qx,
-                                         float qy, float qz, float& best_d2,
-                                         int& best_idx, int& best_pos) {
-  best_d2 = FLT_MAX;
-  best_idx = 0;
-  best_pos = -1;
-  if (!(__builtin_isfinite(qx) && __builtin_isfinite(qy) &&
-        __builtin_isfinite(qz)))
-    return;
-  const int nl = bv.nleaves;
-  int cur = 1, prev = 0;
-  while (cur != 0) {
-    const int parent = cur >> 1;
-    const float4 lo = bv.nodes[2 * cur];
-    const float4 hi = bv.nodes[2 * cur + 1];
-    int next;
-    if (prev == parent) {
-      const float bd = box_d2(qx, qy, qz, lo, hi);
-      if (bd > best_d2) {
-        next = parent;
-      } else if (cur >= nl) {
-        const int L = cur - nl;
-        const int b = bv.leaf_start[L];
-        const int e = bv.leaf_start[L + 1];
-        for (int i = b; i < e; ++i) {
-          const float4 p = bv.pts[i];
-          const float d2 = d2_ref(qx, qy, qz, p.x, p.y, p.z);
-          const int id = __float_as_int(p.w);
-          const bool better =
-              (d2 < best_d2) || ((d2 == best_d2) && (id < best_idx));
-          if (better) {
-            best_d2 = d2;
-            best_idx = id;
-            best_pos = i;
-          }
-        }
-        next = parent;
-      } else {
-        next = near_child(cur, lo, hi, qx, qy, qz);
-      }
-    } else {
-      const int nc = near_child(cur, lo, hi, qx, qy, qz);
-      next = (prev == nc) ? (prev ^ 1) : parent;
-    }
-    prev = cur;
-    cur = next;
-  }
-}
-
-// Wave-cooperative exact 1-NN for 64 spatially coherent queries (the source
-// is Morton-sorted, so a wave holds one compact patch).  The wave walks the
-// BVH once: node boxes and leaf points are read with wave-uniform addresses
-// (scalar loads, no per-lane gather); a subtree is entered when ANY lane's
-// box lower bound is <= that lane's current best (ballot), so every lane's
-// result is the same exact lexicographic (d2, idx) minimum nn_exact returns.
-// best_* may arrive warm (a real candidate, e.g. the previous ICP
-// iteration's neighbour) -- that only tightens the pruning.
-__device__ __forceinline__ void nn_wave(const BvhView& bv, bool active, float qx, float qy,
-                                        float qz, float& best_d2, int& best_idx,
-                                        int& best_pos) {
-  const bool live = active && __builtin_isfinite(qx) && __builtin_isfinite(qy) &&
-                    __builtin_isfinite(qz);
-  const uint64_t lm = __ballot(live);
-  if (lm == 0) return;
-  // representative query (first live lane) steers the near-child order
-  const int rl = __ffsll((unsigned long long)lm) - 1;
-  const float rx = __shfl(qx, rl, kWave);
-  const float ry = __shfl(qy, rl, kWave);
-  const float rz = __shfl(qz, rl, kWave);
-  const int nl = bv.nleaves;
-  int cur = 1, prev = 0;
-  while (cur != 0) {
-    // the walk state is wave-uniform by construction; say so, so node and
-    // point addresses become scalar loads
-    cur = __builtin_amdgcn_readfirstlane(cur);
-    prev = __builtin_amdgcn_readfirstlane(prev);
-    const int parent = cur >> 1;
-    const float4 lo = bv.nodes[2 * cur];
-    const float4 hi = bv.nodes[2 * cur + 1];
-    int next;
-    if (prev == parent) {
-      const float bd = box_d2(qx, qy, qz, lo, hi);
-      const bool want = live && (bd <= best_d2);
-      if (__ballot(want) == 0) {
-        next = parent;
-      } else if (cur >= nl) {
-        const int L = cur - nl;
-        const int b = __builtin_amdgcn_readfirstlane(bv.leaf_start[L]);
-        const int e = __builtin_amdgcn_readfirstlane(bv.leaf_start[L + 1]);
-        for (int i = b; i < e; ++i) {
-          const float4 p = bv.pts[i];
-          const float d2 = d2_ref(qx, qy, qz, p.x, p.y, p.z);
-          const int id = __float_as_int(p.w);
-          const bool better = (d2 < best_d2) || ((d2 == best_d2) && (id < best_idx));
-          best_d2 = better ? d2 : best_d2;
-          best_idx = better ? id : best_idx;
-          best_pos = better ? i : best_pos;
-        }
-        next = parent;
-      } else {
-        next = near_child(cur, lo, hi, rx, ry, rz);
-      }
-    } else {
-      const int nc = near_child(cur, lo, hi, rx, ry, rz);
-      next = (prev == nc) ? (prev ^ 1) : parent;
-    }
-    prev = cur;
-    cur = next;
-  }
-}
-
-// Warm start from a known candidate (sorted position pos): its own exact
-// d2_ref becomes the initial bound.  Lanes with pos < 0 start cold.
-__device__ __forceinline__ void nn_warm(const BvhView& bv, int pos, float qx, float qy,
-                                        float qz, float& best_d2, int& best_idx,
-                                        int& best_pos) {
-  best_d2 = FLT_MAX;
-  best_idx = 0;
-  best_pos = -1;
-  if (pos >= 0) {
-    const float4 p = bv.pts[pos];
-    const float d2 = d2_ref(qx, qy, qz, p.x, p.y, p.z);
-    if (d2 < FLT_MAX) {  // the reference only ever adds points with d2 < FLT_MAX
-      best_d2 = d2;
-      best_idx = __float_as_int(p.w);
-      best_pos = pos;
-    }
-  }
 }
 
 // ---- wave / block reductions ------------------------------------------------

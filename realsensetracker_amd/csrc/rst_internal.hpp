@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "rst_align.h"
+#include "rst_bvh.hpp"
 
 namespace rst {
 
@@ -36,12 +37,7 @@ namespace rst {
 void set_last_error(hipError_t e, const char* what, const char* file,
                     int line);
 
-// ---- geometry of the BVH --------------------------------------------------
-// Heap-ordered complete binary tree, root = 1, children 2k / 2k+1, leaves
-// [nleaves, 2*nleaves).  Node k = two float4: lo (x,y,z,split) and
-// hi (x,y,z,axis-bits).  Leaf L holds sorted points
-// [leaf_start[L], leaf_start[L+1]) = [L*m/nleaves, (L+1)*m/nleaves).
-constexpr int kLeafTarget = 16;   // nanoflann leaf_max_size at align_icp.cpp:165
+// BVH geometry: rst_bvh.hpp.
 
 // ---- device-resident state of one ICP solve --------------------------------
 // Written only by the single-block solve kernels, read (uniformly) by the
@@ -101,9 +97,10 @@ struct rst_target {
   rst_ctx* ctx = nullptr;
   int64_t m = 0;
   int32_t nleaves = 0;
+  int32_t lg = 0;               // nleaves = 1 << lg
   float4* pts = nullptr;        // [m] Morton-sorted (x,y,z,orig idx bits)
   float4* nodes = nullptr;      // [2 * 2*nleaves]
-  int32_t* leaf_start = nullptr;// [nleaves+1]
+  int32_t* inv = nullptr;       // [m] original index -> sorted position
   float4* nrm = nullptr;        // [m] normals in sorted order (optional)
   float bbox[6] = {0, 0, 0, 0, 0, 0};
   int32_t pos0 = 0;             // sorted position of original point 0
@@ -121,10 +118,14 @@ int ctx_slab(rst_ctx* ctx, size_t bytes, double** out);
 int target_build_device(rst_ctx* ctx, const float* d_xyz, int64_t m,
                         bool with_bvh, rst_target** out);
 size_t target_index_bytes(const rst_target* t);
+BvhView view_of(const rst_target* t);
 
 // NN queries (query.hip)
 int query_nn_device(rst_ctx* ctx, const rst_target* tgt, const float* d_q,
                     int64_t nq, int32_t* d_idx, float* d_d2);
+int query_nn_warm_device(rst_ctx* ctx, const rst_target* tgt, const float* d_q, int64_t nq,
+                         const int32_t* d_warm, int32_t* d_idx, float* d_d2,
+                         int* d_stats = nullptr);
 int query_knn_device(rst_ctx* ctx, const rst_target* tgt, const float* d_q,
                      int64_t nq, int k, int32_t* d_idx, float* d_d2);
 int compute_normals(rst_ctx* ctx, rst_target* tgt, int k, const float vp[3]);

@@ -1,0 +1,185 @@
+// bvh_selftest.cpp -- CPU check of the exact searches in rst_bvh.hpp.
+//
+// The product runs these searches on the GPU; they are written
+// __host__ __device__, so the very same code is exercised here on the CPU
+// against brute force (lexicographic (d2, index) minimum, the contract of
+// rst_target_query_nn).  A CPU build of the index mirrors build.hip's
+// pipeline (Morton order, fixed-size leaves, make_leaf / make_internal).
+//
+// Usage: bvh_selftest [seed]   -- exit 0 on success, prints a summary.
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <random>
+#include <vector>
+
+#include "rst_bvh.hpp"
+
+using namespace rst;
+
+namespace {
+
+uint32_t spread10(uint32_t v) {
+  v &= 0x3ffu;
+  v = (v | (v << 16)) & 0x030000FFu;
+  v = (v | (v << 8)) & 0x0300F00Fu;
+  v = (v | (v << 4)) & 0x030C30C3u;
+  v = (v | (v << 2)) & 0x09249249u;
+  return v;
+}
+
+struct Index {
+  std::vector<float4> pts;
+  std::vector<float4> nodes;
+  BvhView bv;
+};
+
+Index build(const std::vector<float>& xyz) {
+  Index ix;
+  const int m = (int)(xyz.size() / 3);
+  float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+  for (int i = 0; i < m; ++i)
+    if (finite3(xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2]))
+      for (int d = 0; d < 3; ++d) {
+        lo[d] = std::min(lo[d], xyz[3 * i + d]);
+        hi[d] = std::max(hi[d], xyz[3 * i + d]);
+      }
+  const float ext = std::max(std::max(hi[0] - lo[0], hi[1] - lo[1]), hi[2] - lo[2]);
+  const float sc = ext > 0 ? 1023.0f / ext : 0.0f;
+  std::vector<std::pair<uint32_t, int>> kv(m);
+  for (int i = 0; i < m; ++i) {
+    const float x = xyz[3 * i], y = xyz[3 * i + 1], z = xyz[3 * i + 2];
+    uint32_t code = 0x3fffffffu;
+    if (finite3(x, y, z)) {
+      auto q = [&](float v, float l) { return (uint32_t)std::min(std::max((v - l) * sc, 0.0f), 1023.0f); };
+      code = (spread10(q(x, lo[0])) << 2) | (spread10(q(y, lo[1])) << 1) | spread10(q(z, lo[2]));
+    }
+    kv[i] = {code, i};
+  }
+  std::stable_sort(kv.begin(), kv.end(),
+                   [](const auto& a, const auto& b) { return a.first < b.first; });
+  ix.pts.resize(std::max(m, 1));
+  for (int i = 0; i < m; ++i) {
+    const int j = kv[i].second;
+    ix.pts[i] = make_float4(xyz[3 * j], xyz[3 * j + 1], xyz[3 * j + 2], i2f(j));
+  }
+  int nl = 1, lg = 0;
+  while ((int64_t)nl * kLeafTarget < m) {
+    nl <<= 1;
+    ++lg;
+  }
+  ix.nodes.resize(4 * (size_t)nl);
+  ix.bv.pts = ix.pts.data();
+  ix.bv.nodes = ix.nodes.data();
+  ix.bv.m = m;
+  ix.bv.nleaves = nl;
+  ix.bv.lg = lg;
+  ix.bv.pad = 0;
+  for (int L = 0; L < nl; ++L) make_leaf(ix.bv, ix.nodes.data(), L);
+  for (int k = nl - 1; k >= 1; --k) make_internal(ix.nodes.data(), k);
+  return ix;
+}
+
+template <int K>
+void brute(const std::vector<float>& xyz, float qx, float qy, float qz, BestK<K>& r) {
+  r.init();
+  if (!finite3(qx, qy, qz)) return;
+  const int m = (int)(xyz.size() / 3);
+  for (int j = 0; j < m; ++j)
+    r.offer(d2_ref(qx, qy, qz, xyz[3 * j], xyz[3 * j + 1], xyz[3 * j + 2]), j, j);
+}
+
+int g_fail = 0;
+long g_checks = 0;
+
+void check(bool ok, const char* what, int m, int q) {
+  ++g_checks;
+  if (!ok && g_fail++ < 20) fprintf(stderr, "FAIL %s m=%d query=%d\n", what, m, q);
+}
+
+// sorted position of original index j
+int pos_of(const Index& ix, int j) {
+  for (int i = 0; i < ix.bv.m; ++i)
+    if (f2i(ix.pts[i].w) == j) return i;
+  return -1;
+}
+
+void run_case(std::mt19937_64& rng, int m, int nq, int mode) {
+  std::uniform_real_distribution<float> U(-1.0f, 1.0f);
+  std::vector<float> xyz(3 * (size_t)m);
+  for (int i = 0; i < m; ++i) {
+    if (mode == 1) {  // coarse lattice: many exact ties and duplicates
+      for (int d = 0; d < 3; ++d) xyz[3 * i + d] = std::floor(U(rng) * 4.0f) * 0.25f;
+    } else if (mode == 2) {  // surface-like: a wavy sheet, dense
+      const float u = U(rng), v = U(rng);
+      xyz[3 * i] = u;
+      xyz[3 * i + 1] = v;
+      xyz[3 * i + 2] = 0.1f * std::sin(6.0f * u) * std::cos(5.0f * v) + 0.002f * U(rng);
+    } else {
+      for (int d = 0; d < 3; ++d) xyz[3 * i + d] = U(rng);
+    }
+  }
+  if (mode == 3 && m > 4) {  // a few non-finite target points
+    xyz[0] = NAN;
+    xyz[4] = INFINITY;
+  }
+  const Index ix = build(xyz);
+  std::uniform_int_distribution<int> P(0, std::max(m - 1, 0));
+  for (int q = 0; q < nq; ++q) {
+    float qx, qy, qz;
+    if (q % 3 == 0 && m > 0) {  // near an existing point (tight searches)
+      const int j = P(rng);
+      qx = xyz[3 * j] + 0.01f * U(rng);
+      qy = xyz[3 * j + 1] + 0.01f * U(rng);
+      qz = xyz[3 * j + 2] + 0.01f * U(rng);
+    } else {
+      qx = 1.5f * U(rng);
+      qy = 1.5f * U(rng);
+      qz = 1.5f * U(rng);
+    }
+    if (q == 7) qx = NAN;
+    BestK<1> b1;
+    brute(xyz, qx, qy, qz, b1);
+    BestK<4> b4;
+    brute(xyz, qx, qy, qz, b4);
+    // cold top-down
+    Best1 r;
+    r.init();
+    search(ix.bv, -1, qx, qy, qz, r);
+    check(r.d == b1.d[0] && (r.pos < 0 ? b1.pos[0] < 0 : r.id == b1.id[0]), "nn cold", m, q);
+    // warm: from a random start, from the answer, seeded with the start's d2
+    for (int w = 0; w < 2 && m > 0; ++w) {
+      const int start = w == 0 ? P(rng) : (b1.pos[0] >= 0 ? pos_of(ix, b1.id[0]) : P(rng));
+      Best1 s;
+      s.init();
+      const float4 p = ix.pts[start];
+      if (finite3(qx, qy, qz)) s.offer(d2_ref(qx, qy, qz, p.x, p.y, p.z), f2i(p.w), start);
+      search(ix.bv, start, qx, qy, qz, s);
+      check(s.d == b1.d[0] && (s.pos < 0 ? b1.pos[0] < 0 : s.id == b1.id[0]), "nn warm", m, q);
+      if (s.pos >= 0) check(f2i(ix.pts[s.pos].w) == s.id, "nn pos", m, q);
+    }
+    // k = 4, bottom-up from a random leaf
+    if (m > 0) {
+      BestK<4> k4;
+      k4.init();
+      search(ix.bv, P(rng), qx, qy, qz, k4);
+      bool ok = true;
+      for (int j = 0; j < 4; ++j) ok &= k4.d[j] == b4.d[j] && k4.id[j] == b4.id[j];
+      check(ok, "knn4 warm", m, q);
+    }
+  }
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  const uint64_t seed = argc > 1 ? strtoull(argv[1], nullptr, 10) : 1;
+  std::mt19937_64 rng(seed);
+  const int sizes[] = {0, 1, 2, 3, 7, 16, 17, 33, 100, 257, 1000, 4099, 20000};
+  for (int m : sizes)
+    for (int mode = 0; mode < 4; ++mode) run_case(rng, m, m >= 4099 ? 300 : 120, mode);
+  printf("bvh_selftest: %ld checks, %d failures\n", g_checks, g_fail);
+  return g_fail == 0 ? 0 : 1;
+}

@@ -49,6 +49,57 @@ def test_nn_bitexact_ties_duplicates_random(ctx):
     assert np.array_equal(gi, oi) and np.array_equal(gd, od)
 
 
+def _warm_cases(n, m, oi, rng):
+    """cold, the exact answer, a random (bad) candidate, out-of-range."""
+    return {"none": None, "cold": np.full(n, -1, np.int32), "exact": oi.astype(np.int32),
+            "random": rng.integers(0, m, size=n).astype(np.int32),
+            "oob": np.full(n, m + 5, np.int32)}
+
+
+@pytest.mark.parametrize("name", GOLDEN_NAMES)
+def test_nn_warm_coherent_bitexact_golden(ctx, name):
+    """The ICP loop's wave-cooperative search through rst_target_query_nn_warm:
+    identical (idx, d2) for every kind of seed."""
+    g = load_golden(name)
+    t = A.Target.build(g["dst"], ctx)
+    q = g["src"]
+    oi, od = O.nn_bruteforce(g["dst"], q) if len(g["dst"]) * len(q) < 4e8 else (g["nn_idx0"], g["nn_d20"])
+    rng = np.random.default_rng(1)
+    for kind, w in _warm_cases(len(q), len(g["dst"]), oi, rng).items():
+        gi, gd = t.query_warm(q, w)
+        assert np.array_equal(gi, oi), kind
+        assert np.array_equal(gd, od), kind
+
+
+def test_nn_warm_ties_duplicates_incoherent(ctx):
+    rng = np.random.default_rng(3)
+    lat = np.stack(np.meshgrid(*[np.arange(10, dtype=np.float32) * 0.1] * 3), -1).reshape(-1, 3)
+    dst = np.concatenate([lat, lat[::7], rng.normal(size=(3000, 3)).astype(np.float32)])
+    q = np.concatenate([lat + np.float32(0.05), lat[:100],
+                        rng.normal(size=(5000, 3)).astype(np.float32) * 3])
+    q[17] = np.nan
+    q[18, 1] = np.inf
+    rng.shuffle(q[200:])  # incoherent tail: wide wave regions, still exact
+    t = A.Target.build(dst, ctx)
+    oi, od = O.nn_bruteforce(dst, q)
+    for kind, w in _warm_cases(len(q), len(dst), oi, rng).items():
+        gi, gd = t.query_warm(q, w)
+        assert np.array_equal(gi, oi), kind
+        assert np.array_equal(gd, od), kind
+
+
+@pytest.mark.parametrize("m", [1, 2, 3, 17, 100, 1000])
+def test_nn_warm_small_targets(ctx, m):
+    rng = np.random.default_rng(100 + m)
+    dst = rng.uniform(-1, 1, size=(m, 3)).astype(np.float32)
+    q = rng.uniform(-2, 2, size=(300, 3)).astype(np.float32)
+    oi, od = O.nn_bruteforce(dst, q)
+    t = A.Target.build(dst, ctx)
+    for kind, w in _warm_cases(len(q), m, oi, rng).items():
+        gi, gd = t.query_warm(q, w)
+        assert np.array_equal(gi, oi) and np.array_equal(gd, od), kind
+
+
 @pytest.mark.parametrize("m", [1, 2, 3, 15, 16, 17, 31, 33, 100, 1000])
 def test_nn_small_targets(ctx, m):
     rng = np.random.default_rng(m)
