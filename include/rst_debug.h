@@ -19,6 +19,10 @@ int rst_debug_query_nn_warm_stats(rst_ctx* ctx, const rst_target* tgt, const flo
                                   int64_t nq, const int32_t* warm, int32_t* idx, float* d2,
                                   int32_t* stats);
 
+/* Fallback-queue length (queries the leaf adjacency could not certify) of
+ * each iteration of the last align call on ctx (first n <= 256). */
+int rst_debug_queue_trace(rst_ctx* ctx, int32_t* out, int32_t n);
+
 #ifdef __cplusplus
 }
 #endif

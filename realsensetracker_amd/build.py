@@ -28,7 +28,6 @@ ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 ARCH = os.environ.get("RST_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = ["build.hip", "query.hip", "icp.hip", "capi.hip", "unproject.hip", "comm.hip", "synth.cpp"]
-HEADERS = ["rst_internal.hpp", "rst_device.hpp", "rst_bvh.hpp"]
 LIB_NAME = "librst_align.so"
 
 # -ffp-contract=off: reference-exact rounding of the transform / distance /
@@ -44,7 +43,8 @@ def _hipcc() -> str:
 
 def _stamp(src: Path) -> str:
     h = hashlib.sha1()
-    for p in [src] + [CSRC / x for x in HEADERS] + [INCLUDE / "rst_align.h"]:
+    # every header can reach every source: hash them all
+    for p in [src] + sorted(CSRC.glob("*.hpp")) + sorted(INCLUDE.glob("*.h")):
         h.update(p.read_bytes())
     h.update(" ".join(CFLAGS).encode())
     return h.hexdigest()[:16]

@@ -15,6 +15,7 @@
 #include <cmath>
 
 #include "rst_device.hpp"
+#include "rst_wave_nn.hpp"
 #include "rst_internal.hpp"
 
 namespace rst {
@@ -79,15 +80,6 @@ __global__ __launch_bounds__(kBS) void k_bbox_final(const float* __restrict__ pa
 }
 
 // ---- Morton keys ---------------------------------------------------------------
-__device__ __forceinline__ uint32_t spread10(uint32_t v) {
-  v &= 0x3ffu;
-  v = (v | (v << 16)) & 0x030000FFu;
-  v = (v | (v << 8)) & 0x0300F00Fu;
-  v = (v | (v << 4)) & 0x030C30C3u;
-  v = (v | (v << 2)) & 0x09249249u;
-  return v;
-}
-
 __global__ __launch_bounds__(kBS) void k_morton(const float* __restrict__ xyz,
                                                 int64_t m,
                                                 const float* __restrict__ bbox,
@@ -95,20 +87,7 @@ __global__ __launch_bounds__(kBS) void k_morton(const float* __restrict__ xyz,
                                                 uint32_t* __restrict__ vals) {
   const int64_t i = blockIdx.x * (int64_t)kBS + threadIdx.x;
   if (i >= m) return;
-  const float lx = bbox[0], ly = bbox[1], lz = bbox[2];
-  const float ext = fmaxf(fmaxf(bbox[3] - lx, bbox[4] - ly), bbox[5] - lz);
-  const float sc = ext > 0.0f ? 1023.0f / ext : 0.0f;
-  const float x = xyz[3 * i], y = xyz[3 * i + 1], z = xyz[3 * i + 2];
-  uint32_t code;
-  if (__builtin_isfinite(x) && __builtin_isfinite(y) && __builtin_isfinite(z)) {
-    const uint32_t qx = (uint32_t)fminf(fmaxf((x - lx) * sc, 0.0f), 1023.0f);
-    const uint32_t qy = (uint32_t)fminf(fmaxf((y - ly) * sc, 0.0f), 1023.0f);
-    const uint32_t qz = (uint32_t)fminf(fmaxf((z - lz) * sc, 0.0f), 1023.0f);
-    code = (spread10(qx) << 2) | (spread10(qy) << 1) | spread10(qz);
-  } else {
-    code = 0x3fffffffu;  // non-finite points sort last
-  }
-  keys[i] = code;
+  keys[i] = morton_code(xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2], bbox);
   vals[i] = (uint32_t)i;
 }
 
@@ -244,6 +223,14 @@ __global__ __launch_bounds__(kBS) void k_leaf_boxes(BvhView bv, float4* __restri
   if (L < bv.nleaves) make_leaf(bv, nodes, L);
 }
 
+// leaf adjacency (the tracking index, rst_bvh.hpp): one wavefront per leaf
+__global__ __launch_bounds__(kBS) void k_leaf_adj(BvhView bv, float4* __restrict__ ent,
+                                                  float* __restrict__ reach) {
+  __shared__ WnnScratch wsc[kBS / kWave];
+  const int L = blockIdx.x * (kBS / kWave) + threadIdx.x / kWave;
+  if (L < bv.nleaves) leaf_adj_wave(bv, L, ent, reach, wsc[threadIdx.x / kWave]);
+}
+
 __global__ __launch_bounds__(kBS) void k_level(float4* __restrict__ nodes, int lo_k,
                                                int count) {
   const int i = blockIdx.x * kBS + threadIdx.x;
@@ -283,6 +270,13 @@ int radix_sort_pairs(rst_ctx* ctx, uint32_t* keys, uint32_t* vals, uint32_t* ktm
   return RST_OK;  // 4 passes: result back in keys/vals
 }
 
+AdjView adj_of(const rst_target* t) {
+  AdjView a;
+  a.ent = t->adj;
+  a.reach = t->reach;
+  return a;
+}
+
 size_t target_index_bytes(const rst_target* t) {
   if (!t->has_bvh) return 0;
   return (size_t)4 * t->nleaves * sizeof(float4);
@@ -292,6 +286,8 @@ BvhView view_of(const rst_target* t) {
   BvhView v;
   v.pts = t->pts;
   v.nodes = t->nodes;
+  v.codes = t->codes;
+  v.bbox = t->codes ? (const float*)(t->codes + std::max<int64_t>(t->m, 1)) : nullptr;
   v.m = (int32_t)t->m;
   v.nleaves = t->nleaves;
   v.lg = t->lg;
@@ -317,13 +313,17 @@ int target_build_device(rst_ctx* ctx, const float* d_xyz, int64_t m, bool with_b
   t->lg = lg;
   const int64_t mp = std::max<int64_t>(m, 1);
   if (hipMalloc(&t->pts, sizeof(float4) * mp) != hipSuccess ||
-      hipMalloc(&t->inv, sizeof(int32_t) * mp) != hipSuccess) {
+      hipMalloc(&t->inv, sizeof(int32_t) * mp) != hipSuccess ||
+      hipMalloc(&t->codes, sizeof(uint32_t) * mp + sizeof(float) * 8) != hipSuccess) {
     if (t->pts) hipFree(t->pts);
+    if (t->inv) hipFree(t->inv);
     delete t;
     return RST_E_NOMEM;
   }
   if (with_bvh) {
-    if (hipMalloc(&t->nodes, sizeof(float4) * 4 * nl) != hipSuccess) {
+    if (hipMalloc(&t->nodes, sizeof(float4) * 4 * nl) != hipSuccess ||
+        hipMalloc(&t->adj, sizeof(float4) * 2 * kAdjK * nl) != hipSuccess ||
+        hipMalloc(&t->reach, sizeof(float) * nl) != hipSuccess) {
       rst_target_free(t);
       return RST_E_NOMEM;
     }
@@ -369,6 +369,14 @@ int target_build_device(rst_ctx* ctx, const float* d_xyz, int64_t m, bool with_b
     rst_target_free(t);
     return s;
   }
+  // sorted codes + their box stay with the target (cold-start seeds)
+  if (hipMemcpyAsync(t->codes, keys, sizeof(uint32_t) * m, hipMemcpyDeviceToDevice, st) !=
+          hipSuccess ||
+      hipMemcpyAsync(t->codes + mp, bbox, sizeof(float) * 6, hipMemcpyDeviceToDevice, st) !=
+          hipSuccess) {
+    rst_target_free(t);
+    return RST_E_HIP;
+  }
   k_gather<<<blocks_for(m), kBS, 0, st>>>(d_xyz, vals, m, t->pts);
   k_find_pos0<<<blocks_for(m), kBS, 0, st>>>(vals, m, (int32_t*)(bbox + 6));
   k_inverse<<<blocks_for(m), kBS, 0, st>>>(vals, m, t->inv);
@@ -380,6 +388,7 @@ int target_build_device(rst_ctx* ctx, const float* d_xyz, int64_t m, bool with_b
       cnt >>= 1;
     }
     if (cnt >= 1) k_levels_top<<<1, kBS, 0, st>>>(t->nodes, (int)cnt);
+    k_leaf_adj<<<blocks_for(nl, kBS / kWave), kBS, 0, st>>>(view_of(t), t->adj, t->reach);
   }
   if (hipGetLastError() != hipSuccess ||
       hipMemcpyAsync(t->bbox, bbox, sizeof(float) * 6, hipMemcpyDeviceToHost, st) != hipSuccess ||

@@ -226,6 +226,9 @@ int rst_target_free(rst_target* t) {
   if (t->nodes) hipFree(t->nodes);
   if (t->nrm) hipFree(t->nrm);
   if (t->inv) hipFree(t->inv);
+  if (t->codes) hipFree(t->codes);
+  if (t->adj) hipFree(t->adj);
+  if (t->reach) hipFree(t->reach);
   delete t;
   return RST_OK;
 }
@@ -312,9 +315,13 @@ int rst_debug_query_nn_warm_stats(rst_ctx* ctx, const rst_target* t, const float
         hipSuccess)
       s = RST_E_HIP;
   }
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (stats && (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess)) s = RST_E_HIP;
+  if (s >= 0 && e0) s = hipEventRecord(e0, ctx->stream) == hipSuccess ? s : RST_E_HIP;
   if (s >= 0)
     s = query_nn_warm_device(ctx, t, dq, nq, dwarm, (int32_t*)dout, (float*)((int32_t*)dout + nq),
                              dstats);
+  if (s >= 0 && e1) s = hipEventRecord(e1, ctx->stream) == hipSuccess ? s : RST_E_HIP;
   if (s >= 0 && stats &&
       hipMemcpyAsync(stats, dstats, 32 * nwav, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess)
     s = RST_E_HIP;
@@ -326,8 +333,23 @@ int rst_debug_query_nn_warm_stats(rst_ctx* ctx, const rst_target* t, const float
       s = RST_E_HIP;
   }
   hipStreamSynchronize(ctx->stream);
+  if (e0 && e1 && s >= 0) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, e0, e1) == hipSuccess) {
+      ctx->last_kernel_ms = ms;
+      ctx->last_kernel_launches = 1;
+    }
+  }
+  if (e0) hipEventDestroy(e0);
+  if (e1) hipEventDestroy(e1);
   hipFree(dq);
   return s < 0 ? s : RST_OK;
+}
+
+int rst_debug_queue_trace(rst_ctx* ctx, int32_t* out, int32_t n) {
+  if (!ctx || !out || n < 0) return RST_E_ARG;
+  for (int i = 0; i < n && i < kQTrace; ++i) out[i] = ctx->h_state->qlen[i];
+  return RST_OK;
 }
 
 int rst_target_query_knn(rst_ctx* ctx, const rst_target* t, const float* q, int64_t nq, int k,

@@ -1,15 +1,18 @@
 // icp.hip -- the ICP loop of AlignIcp3d (align_icp.cpp:73-167) on MI355X.
 //
-// Per iteration two launches on one stream, no host round trip:
-//   k_p2point / k_p2plane : one source point per thread -- transform,
-//       exact NN (BVH), robust weight, fp64 partial sums, wave-shuffle +
-//       LDS block reduction -> one slab row per block;
-//   k_solve_*            : one block -- fixed-order reduction of the slab
-//       (bitwise reproducible), then thread 0 solves the 3x3 Kabsch
-//       (P2POINT_REF) or 6x6 normal equations (P2PLANE) and writes the next
-//       pose into the device-resident IcpState.
-// Multi-GPU: the slab is first reduced to one row, all-reduced over RCCL,
-// and every rank solves the same pose (DESIGN.md "Multi-GPU").
+// Per iteration three launches on one stream, no host round trip:
+//   k_icp_nn<Acc>  one source point per thread: transform, exact NN through
+//       the leaf adjacency of last iteration's neighbour (rst_bvh.hpp
+//       adj_search; cold lanes start from a Morton-code seed), robust
+//       weight, fp64 partial sums -> one slab row per block.  Lanes the
+//       adjacency cannot certify are queued (per-block segment, in order);
+//   k_icp_fb<Acc>  one wavefront per queued query: the cooperative exact
+//       search of rst_wave_nn.hpp, partial sums -> one slab row per block;
+//   k_solve_*      one block: fixed-order reduction of both slabs (bitwise
+//       reproducible), then thread 0 solves the 3x3 Kabsch (P2POINT_REF)
+//       or 6x6 normal equations (P2PLANE) into the device-resident IcpState.
+// Multi-GPU: both slabs are first reduced to one row, all-reduced over
+// RCCL, and every rank solves the same pose (DESIGN.md "Multi-GPU").
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -27,6 +30,7 @@ namespace {
 constexpr int kBS = 256;
 constexpr int kNP2Point = 16;  // sum w q u^T (9), sum w u (3), sum q (3), sum d2
 constexpr int kNP2Plane = 30;  // A (21), b (6), sum w r^2, count, sum d2
+constexpr int kFbBlocks = 512;  // fixed grid of the fallback kernel (2048 waves)
 
 __device__ __forceinline__ Pose3 load_pose(const IcpState* __restrict__ st) {
   Pose3 P;
@@ -35,21 +39,6 @@ __device__ __forceinline__ Pose3 load_pose(const IcpState* __restrict__ st) {
 #pragma unroll
   for (int k = 0; k < 3; ++k) P.t[k] = st->t[k];
   return P;
-}
-
-// Exact 1-NN of one query per lane, seeded by a warm candidate (sorted
-// target position, -1 = cold): the candidate's own d2 is the lane's first
-// bound, then the wave-cooperative search of rst_wave_nn.hpp.
-__device__ __forceinline__ Best1 nn_seeded(const BvhView& bv, bool act, int warm, float qx,
-                                           float qy, float qz, WnnScratch& ws) {
-  Best1 r;
-  r.init();
-  if (act && warm >= 0) {
-    const float4 p = bv.pts[warm];
-    r.offer(d2_ref(qx, qy, qz, p.x, p.y, p.z), f2i(p.w), warm);
-  }
-  nn_wave_region(bv, act, qx, qy, qz, r, ws);
-  return r;
 }
 
 // ---- centroid ------------------------------------------------------------------
@@ -69,17 +58,20 @@ __global__ __launch_bounds__(kBS) void k_centroid_partial(const float4* __restri
   block_sum_to_slab<4, kBS>(v, lds, slab + blockIdx.x * 4);
 }
 
-// Reduce `rows` slab rows of NV doubles into out[NV] (fixed order).
+// Reduce slab rows (rows1 of slab1, then rows2 of slab2; NV doubles each)
+// into out[NV], in a fixed order.
 template <int NV>
-__device__ __forceinline__ void reduce_slab_rows(const double* __restrict__ slab, int rows,
+__device__ __forceinline__ void reduce_slab_rows(const double* __restrict__ slab1, int rows1,
+                                                 const double* __restrict__ slab2, int rows2,
                                                  double* __restrict__ red /*[NV][kBS]*/,
                                                  double* __restrict__ out) {
   double acc[NV];
 #pragma unroll
   for (int k = 0; k < NV; ++k) acc[k] = 0.0;
-  for (int b = threadIdx.x; b < rows; b += kBS) {
+  for (int b = threadIdx.x; b < rows1 + rows2; b += kBS) {
+    const double* row = b < rows1 ? slab1 + (int64_t)b * NV : slab2 + (int64_t)(b - rows1) * NV;
 #pragma unroll
-    for (int k = 0; k < NV; ++k) acc[k] += slab[(int64_t)b * NV + k];
+    for (int k = 0; k < NV; ++k) acc[k] += row[k];
   }
 #pragma unroll
   for (int k = 0; k < NV; ++k) red[k * kBS + threadIdx.x] = acc[k];
@@ -97,10 +89,11 @@ __device__ __forceinline__ void reduce_slab_rows(const double* __restrict__ slab
 }
 
 template <int NV>
-__global__ __launch_bounds__(kBS) void k_slab_reduce(const double* __restrict__ slab, int rows,
+__global__ __launch_bounds__(kBS) void k_slab_reduce(const double* __restrict__ slab1, int rows1,
+                                                     const double* __restrict__ slab2, int rows2,
                                                      double* __restrict__ out) {
   __shared__ double red[NV * kBS];
-  reduce_slab_rows<NV>(slab, rows, red, out);
+  reduce_slab_rows<NV>(slab1, rows1, slab2, rows2, red, out);
 }
 
 struct InitArgs {
@@ -116,7 +109,7 @@ __global__ __launch_bounds__(kBS) void k_init_state(const double* __restrict__ c
                                                     InitArgs a, IcpState* __restrict__ st) {
   __shared__ double red[4 * kBS];
   __shared__ double tot[4];
-  if (a.need_centroid) reduce_slab_rows<4>(cslab, rows, red, tot);
+  if (a.need_centroid) reduce_slab_rows<4>(cslab, rows, cslab, 0, red, tot);
   if (threadIdx.x == 0) {
     for (int c = 0; c < 3; ++c)
       for (int r = 0; r < 3; ++r) {
@@ -144,48 +137,226 @@ __global__ __launch_bounds__(kBS) void k_init_state(const double* __restrict__ c
   }
 }
 
-// ---- P2POINT_REF -----------------------------------------------------------------
-// Single pass over the correspondences with the source centroid known:
-//   cov = sum w (q - dbar)(s - sbar)^T = sum w q u^T - dbar (sum w u)^T,
-// u = s - sbar in float as at align_icp.cpp:129, dbar = sum q / n.
-__global__ __launch_bounds__(kBS) void k_p2point(BvhView bv, const float4* __restrict__ src,
-                                                 int64_t n, const IcpState* __restrict__ st,
-                                                 int32_t pos0, int32_t* __restrict__ nnpos,
-                                                 double* __restrict__ slab) {
-  __shared__ double lds[(kBS / kWave) * kNP2Point];
-  const Pose3 P = load_pose(st);
-  const float mu = st->mu;
-  const float sm0 = st->smean[0], sm1 = st->smean[1], sm2 = st->smean[2];
-  double v[kNP2Point];
+// ---- per-point accumulation policies ---------------------------------------------
+struct Uni {  // uniform per-iteration values of the device state
+  Pose3 P;
+  float mu;
+  float sm0, sm1, sm2;
+};
+
+__device__ __forceinline__ Uni load_uni(const IcpState* __restrict__ st) {
+  Uni u;
+  u.P = load_pose(st);
+  u.mu = st->mu;
+  u.sm0 = st->smean[0];
+  u.sm1 = st->smean[1];
+  u.sm2 = st->smean[2];
+  return u;
+}
+
+struct AccArgs {
+  const float4* __restrict__ nrm;  // P2PLANE: target normals, sorted order
+  float pmu;                       // P2PLANE: Geman-McClure scale on r^2
+  float max_d2;                    // P2PLANE: correspondence rejection
+  int32_t pos0;                    // sorted position of dst[0]
+};
+
+// P2POINT_REF.  Single pass over the correspondences with the source
+// centroid known:  cov = sum w (q - dbar)(s - sbar)^T
+//                      = sum w q u^T - dbar (sum w u)^T,
+// u = s - sbar in float as at align_icp.cpp:129, dbar = sum q / n (:120-122);
+// no neighbour -> q = dst[0], d2 = FLT_MAX (the query's untouched outputs).
+struct P2PointAcc {
+  static constexpr int NV = kNP2Point;  // sum w q u^T (9), sum w u (3), sum q (3), sum d2
+  static constexpr bool kCanFinish = false;
+  __device__ static void add(double (&v)[NV], const BvhView& bv, const AccArgs& a, const Uni& u,
+                             const float4& s, float px, float py, float pz, float bd, int bp) {
+    (void)px; (void)py; (void)pz;
+    const float l = u.mu / (bd + u.mu);  // :116-117
+    const float w = l * l;
+    const float4 q = bv.pts[bp >= 0 ? bp : a.pos0];
+    const float u0 = s.x - u.sm0, u1 = s.y - u.sm1, u2 = s.z - u.sm2;
+    const double dw = (double)w;
+    const double wq0 = dw * (double)q.x, wq1 = dw * (double)q.y, wq2 = dw * (double)q.z;
+    v[0] += wq0 * u0; v[1] += wq0 * u1; v[2] += wq0 * u2;
+    v[3] += wq1 * u0; v[4] += wq1 * u1; v[5] += wq1 * u2;
+    v[6] += wq2 * u0; v[7] += wq2 * u1; v[8] += wq2 * u2;
+    v[9] += dw * u0; v[10] += dw * u1; v[11] += dw * u2;
+    v[12] += q.x; v[13] += q.y; v[14] += q.z;
+    v[15] += bd;
+  }
+};
+
+// P2PLANE (build's own mode): r = n.(p - q), w = (mu/(r^2+mu))^2,
+// J = [p x n ; n]; 21 + 6 + 3 sums.
+struct P2PlaneAcc {
+  static constexpr int NV = kNP2Plane;  // A (21), b (6), sum w r^2, count, sum d2
+  static constexpr bool kCanFinish = true;
+  __device__ static void add(double (&v)[NV], const BvhView& bv, const AccArgs& a, const Uni& u,
+                             const float4& s, float px, float py, float pz, float bd, int bp) {
+    (void)u; (void)s;
+    if (bp < 0 || !(bd <= a.max_d2)) return;
+    const float4 q = bv.pts[bp];
+    const float4 nn = a.nrm[bp];
+    const float e0 = px - q.x, e1 = py - q.y, e2 = pz - q.z;
+    const float r = (nn.x * e0 + nn.y * e1) + nn.z * e2;
+    const double dr = (double)r;
+    const double l = (double)a.pmu / (dr * dr + (double)a.pmu);
+    const double w = l * l;
+    const double X = px, Y = py, Z = pz, NX = nn.x, NY = nn.y, NZ = nn.z;
+    const double J[6] = {Y * NZ - Z * NY, Z * NX - X * NZ, X * NY - Y * NX, NX, NY, NZ};
+    int k = 0;
 #pragma unroll
-  for (int k = 0; k < kNP2Point; ++k) v[k] = 0.0;
+    for (int i = 0; i < 6; ++i) {
+      const double wa = w * J[i];
+#pragma unroll
+      for (int c = 0; c <= i; ++c) v[k++] += wa * J[c];
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) v[21 + i] += w * J[i] * dr;
+    v[27] += w * dr * dr;
+    v[28] += 1.0;
+    v[29] += bd;
+  }
+};
+
+// ---- kernel 1: adjacency search, one point per thread ----------------------------------
+template <class Acc>
+__global__ __launch_bounds__(kBS) void k_icp_nn(BvhView bv, AdjView av, AccArgs aa,
+                                                const float4* __restrict__ src, int64_t n,
+                                                const IcpState* __restrict__ st,
+                                                int32_t* __restrict__ nnpos,
+                                                int32_t* __restrict__ qbuf,
+                                                int32_t* __restrict__ qcnt,
+                                                double* __restrict__ slab) {
+  __shared__ double lds[(kBS / kWave) * Acc::NV];
+  __shared__ int wq[kBS / kWave];
+  if (Acc::kCanFinish && st->done) {  // converged: uniform early exit
+    if (threadIdx.x == 0) qcnt[blockIdx.x] = 0;
+    return;
+  }
+  const Uni u = load_uni(st);
+  double v[Acc::NV];
+#pragma unroll
+  for (int k = 0; k < Acc::NV; ++k) v[k] = 0.0;
   const int64_t i = blockIdx.x * (int64_t)kBS + threadIdx.x;
   const bool act = i < n;
   const float4 s = act ? src[i] : make_float4(0.f, 0.f, 0.f, 0.f);
   float px, py, pz;
-  xform(P, s.x, s.y, s.z, px, py, pz);  // :107
-  // :112 exact 1-NN: the wave's 64 queries search together, each lane
-  // seeded with its previous neighbour
-  __shared__ WnnScratch wsc[kBS / kWave];
-  const Best1 r = nn_seeded(bv, act, act ? nnpos[i] : -1, px, py, pz, wsc[threadIdx.x / kWave]);
-  const float bd = r.d;
-  const int bp = r.pos;
-  if (act) {
-    nnpos[i] = bp;
-    const float l = mu / (bd + mu);         // :116-117
-    const float w = l * l;
-    const float4 q = bv.pts[bp >= 0 ? bp : pos0];  // no neighbour -> dst[0]
-    const float u0 = s.x - sm0, u1 = s.y - sm1, u2 = s.z - sm2;
-    const double dw = (double)w;
-    const double wq0 = dw * (double)q.x, wq1 = dw * (double)q.y, wq2 = dw * (double)q.z;
-    v[0] = wq0 * u0; v[1] = wq0 * u1; v[2] = wq0 * u2;
-    v[3] = wq1 * u0; v[4] = wq1 * u1; v[5] = wq1 * u2;
-    v[6] = wq2 * u0; v[7] = wq2 * u1; v[8] = wq2 * u2;
-    v[9] = dw * u0; v[10] = dw * u1; v[11] = dw * u2;
-    v[12] = q.x; v[13] = q.y; v[14] = q.z;
-    v[15] = bd;
+  xform(u.P, s.x, s.y, s.z, px, py, pz);  // align_icp.cpp:107
+  const bool fin = finite3(px, py, pz);
+  // :112 exact 1-NN, starting from last iteration's neighbour
+  int warm = act ? nnpos[i] : -1;
+  if (act && fin && warm < 0) warm = morton_seed(bv, px, py, pz);
+  Best1 r;
+  r.init();
+  if (act && fin) {
+    const float4 w = bv.pts[warm];
+    r.offer(d2_ref(px, py, pz, w.x, w.y, w.z), f2i(w.w), warm);
   }
-  block_sum_to_slab<kNP2Point, kBS>(v, lds, slab + (int64_t)blockIdx.x * kNP2Point);
+  const bool done = act && (!fin || adj_search_wide(bv, av, warm, px, py, pz, r));
+  // lanes the adjacency could not certify go to the fallback queue, in
+  // point order within the block's segment
+  const bool need = act && !done;
+  const uint64_t bm = __ballot(need);
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+  if (lane == 0) wq[wid] = __popcll(bm);
+  __syncthreads();
+  int before = 0, total = 0;
+#pragma unroll
+  for (int w = 0; w < kBS / kWave; ++w) {
+    before += w < wid ? wq[w] : 0;
+    total += wq[w];
+  }
+  if (need) qbuf[blockIdx.x * (int64_t)kBS + before + __popcll(bm & ((1ull << lane) - 1ull))] = (int)i;
+  if (threadIdx.x == 0) qcnt[blockIdx.x] = total;
+  if (done) {
+    nnpos[i] = r.pos;
+    Acc::add(v, bv, aa, u, s, px, py, pz, r.d, r.pos);
+  }
+  block_sum_to_slab<Acc::NV, kBS>(v, lds, slab + (int64_t)blockIdx.x * Acc::NV);
+}
+
+// ---- kernel 2: the queued queries, one wavefront each --------------------------------
+// Queue entry e (global order: block segments in block order) is handled by
+// wave e mod W of this fixed grid; each wave adds its entries in increasing
+// e, so the slab is reproducible.
+template <class Acc>
+__global__ __launch_bounds__(kBS) void k_icp_fb(BvhView bv, AccArgs aa,
+                                                const float4* __restrict__ src,
+                                                IcpState* __restrict__ st,
+                                                int32_t* __restrict__ nnpos,
+                                                const int32_t* __restrict__ qbuf,
+                                                const int32_t* __restrict__ qcnt, int nb1,
+                                                double* __restrict__ slab2) {
+  extern __shared__ int pref[];  // [nb1 + 1]
+  __shared__ double lds[(kBS / kWave) * Acc::NV];
+  __shared__ WnnScratch wsc[kBS / kWave];
+  __shared__ int part[kBS + 1];
+  double v[Acc::NV];
+#pragma unroll
+  for (int k = 0; k < Acc::NV; ++k) v[k] = 0.0;
+  if (Acc::kCanFinish && st->done) return;  // the solve ignores the slab then
+  // exclusive prefix of the per-block queue counts
+  const int per = (nb1 + kBS - 1) / kBS;
+  const int b0 = threadIdx.x * per;
+  int sum = 0;
+  for (int b = b0; b < b0 + per && b < nb1; ++b) sum += qcnt[b];
+  part[threadIdx.x] = sum;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int t = 0; t < kBS; ++t) {
+      const int x = part[t];
+      part[t] = acc;
+      acc += x;
+    }
+    part[kBS] = acc;
+  }
+  __syncthreads();
+  {
+    int acc = part[threadIdx.x];
+    for (int b = b0; b < b0 + per && b < nb1; ++b) {
+      pref[b] = acc;
+      acc += qcnt[b];
+    }
+    if (threadIdx.x == 0) pref[nb1] = part[kBS];
+  }
+  __syncthreads();
+  const int E = pref[nb1];
+  if (blockIdx.x == 0 && threadIdx.x == 0 && st->iter < kQTrace) st->qlen[st->iter] = E;
+  const Uni u = load_uni(st);
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+  const int W = gridDim.x * (kBS / kWave);
+  for (int e = blockIdx.x * (kBS / kWave) + wid; e < E; e += W) {
+    int lo = 0, hi = nb1 - 1;  // block segment holding entry e
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (pref[mid] <= e)
+        lo = mid;
+      else
+        hi = mid - 1;
+    }
+    const int i = qbuf[lo * (int64_t)kBS + (e - pref[lo])];
+    const float4 s = src[i];
+    float px, py, pz;
+    xform(u.P, s.x, s.y, s.z, px, py, pz);
+    const bool fin = finite3(px, py, pz);
+    int warm = nnpos[i];
+    if (fin && warm < 0) warm = morton_seed(bv, px, py, pz);
+    Best1 r;
+    r.init();
+    if (fin) {
+      const float4 w = bv.pts[warm];
+      r.offer(d2_ref(px, py, pz, w.x, w.y, w.z), f2i(w.w), warm);
+    }
+    nn_wave_one(bv, warm, px, py, pz, r, wsc[wid]);
+    if (lane == 0) {
+      nnpos[i] = r.pos;
+      Acc::add(v, bv, aa, u, s, px, py, pz, r.d, r.pos);
+    }
+  }
+  block_sum_to_slab<Acc::NV, kBS>(v, lds, slab2 + (int64_t)blockIdx.x * Acc::NV);
 }
 
 // Kabsch solve (align_icp.cpp:139-151; SolveKabsch :58-69): fp64 SVD,
@@ -257,64 +428,14 @@ __device__ void p2point_update(const double* tot, const IcpParams& prm, IcpState
   if (next > 0 && prm.anneal_every > 0 && next % prm.anneal_every == 0) st->mu = st->mu / prm.anneal_div;
 }
 
-__global__ __launch_bounds__(kBS) void k_solve_p2point(const double* __restrict__ slab, int rows,
+__global__ __launch_bounds__(kBS) void k_solve_p2point(const double* __restrict__ slab1, int rows1,
+                                                       const double* __restrict__ slab2, int rows2,
                                                        IcpParams prm, IcpState* __restrict__ st,
                                                        float* __restrict__ trace) {
   __shared__ double red[kNP2Point * kBS];
   __shared__ double tot[kNP2Point];
-  reduce_slab_rows<kNP2Point>(slab, rows, red, tot);
+  reduce_slab_rows<kNP2Point>(slab1, rows1, slab2, rows2, red, tot);
   if (threadIdx.x == 0) p2point_update(tot, prm, st, trace);
-}
-
-// ---- P2PLANE (build's own mode) -----------------------------------------------------
-// r = n.(p - q), w = (mu/(r^2+mu))^2, J = [p x n ; n]; 21 + 6 + 3 sums.
-__global__ __launch_bounds__(kBS) void k_p2plane(BvhView bv, const float4* __restrict__ nrm,
-                                                 const float4* __restrict__ src, int64_t n,
-                                                 const IcpState* __restrict__ st, float pmu,
-                                                 float max_d2, int32_t* __restrict__ nnpos,
-                                                 double* __restrict__ slab) {
-  __shared__ double lds[(kBS / kWave) * kNP2Plane];
-  if (st->done) return;  // converged: uniform early exit, slab unused
-  const Pose3 P = load_pose(st);
-  double v[kNP2Plane];
-#pragma unroll
-  for (int k = 0; k < kNP2Plane; ++k) v[k] = 0.0;
-  const int64_t i = blockIdx.x * (int64_t)kBS + threadIdx.x;
-  const bool act = i < n;
-  const float4 s = act ? src[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-  float px, py, pz;
-  xform(P, s.x, s.y, s.z, px, py, pz);
-  __shared__ WnnScratch wsc[kBS / kWave];
-  const Best1 r = nn_seeded(bv, act, act ? nnpos[i] : -1, px, py, pz, wsc[threadIdx.x / kWave]);
-  const float bd = r.d;
-  const int bp = r.pos;
-  if (act) {
-    nnpos[i] = bp;
-    if (bp >= 0 && bd <= max_d2) {
-      const float4 q = bv.pts[bp];
-      const float4 nn = nrm[bp];
-      const float e0 = px - q.x, e1 = py - q.y, e2 = pz - q.z;
-      const float r = (nn.x * e0 + nn.y * e1) + nn.z * e2;
-      const double dr = (double)r;
-      const double l = (double)pmu / (dr * dr + (double)pmu);
-      const double w = l * l;
-      const double X = px, Y = py, Z = pz, NX = nn.x, NY = nn.y, NZ = nn.z;
-      const double J[6] = {Y * NZ - Z * NY, Z * NX - X * NZ, X * NY - Y * NX, NX, NY, NZ};
-      int k = 0;
-#pragma unroll
-      for (int a = 0; a < 6; ++a) {
-        const double wa = w * J[a];
-#pragma unroll
-        for (int c = 0; c <= a; ++c) v[k++] = wa * J[c];
-      }
-#pragma unroll
-      for (int a = 0; a < 6; ++a) v[21 + a] = w * J[a] * dr;
-      v[27] = w * dr * dr;
-      v[28] = 1.0;
-      v[29] = bd;
-    }
-  }
-  block_sum_to_slab<kNP2Plane, kBS>(v, lds, slab + (int64_t)blockIdx.x * kNP2Plane);
 }
 
 __device__ bool chol6_solve(const double* Ap /*packed lower 21*/, const double* rhs, double* x) {
@@ -424,13 +545,14 @@ __device__ void p2plane_update(const double* tot, const IcpParams& prm, IcpState
   if (nx < (double)prm.p2plane_eps) st->done = 1;
 }
 
-__global__ __launch_bounds__(kBS) void k_solve_p2plane(const double* __restrict__ slab, int rows,
+__global__ __launch_bounds__(kBS) void k_solve_p2plane(const double* __restrict__ slab1, int rows1,
+                                                       const double* __restrict__ slab2, int rows2,
                                                        IcpParams prm, IcpState* __restrict__ st,
                                                        float* __restrict__ trace) {
   __shared__ double red[kNP2Plane * kBS];
   __shared__ double tot[kNP2Plane];
   if (st->done) return;
-  reduce_slab_rows<kNP2Plane>(slab, rows, red, tot);
+  reduce_slab_rows<kNP2Plane>(slab1, rows1, slab2, rows2, red, tot);
   if (threadIdx.x == 0) p2plane_update(tot, prm, st, trace);
 }
 
@@ -481,14 +603,16 @@ int icp_align_prepared(rst_ctx* ctx, const rst_target* src, const rst_target* tg
   const int64_t n_local = src->m;
   int64_t n_total = n_local;
   hipStream_t st = ctx->stream;
-  // one scratch buffer: [centroid slab | per-iteration slab | totals | pos0]
+  // one scratch buffer: [centroid / kernel-1 slab | kernel-2 slab | totals]
   const int nblk = blocks_for(n_local);
   const int NV = p2plane ? kNP2Plane : kNP2Point;
   const int ncb = std::min(1024, blocks_for(n_local));
-  const size_t slab_doubles = (size_t)std::max(nblk * NV, ncb * 4) + 64;
+  const size_t rows1 = (size_t)std::max(nblk * NV, ncb * 4);
+  const size_t slab_doubles = rows1 + (size_t)kFbBlocks * NV + 64;
   double* slab = nullptr;
   RST_CHECK(ctx_slab(ctx, sizeof(double) * slab_doubles, &slab));
-  double* totals = slab + (size_t)std::max(nblk * NV, ncb * 4);  // 64 doubles
+  double* slab2 = slab + rows1;
+  double* totals = slab2 + (size_t)kFbBlocks * NV;  // 64 doubles
 
   // n_total and the centroid are global quantities under sharding
   if (comm) {
@@ -515,7 +639,7 @@ int icp_align_prepared(rst_ctx* ctx, const rst_target* src, const rst_target* tg
       if (crows < 0) return crows;
     }
     if (comm) {
-      k_slab_reduce<4><<<1, kBS, 0, st>>>(slab, crows, totals);
+      k_slab_reduce<4><<<1, kBS, 0, st>>>(slab, crows, slab, 0, totals);
       RST_CHECK(comm_allreduce_sum_f64(comm, totals, 4, st));
       k_init_state<<<1, kBS, 0, st>>>(totals, 1, ia, ctx->d_state);
     } else {
@@ -524,16 +648,27 @@ int icp_align_prepared(rst_ctx* ctx, const rst_target* src, const rst_target* tg
   } else {
     k_init_state<<<1, kBS, 0, st>>>(slab, 0, ia, ctx->d_state);
   }
-  const int32_t pos0 = tgt->pos0;
   // per source point: sorted target position of its last neighbour (warm
-  // start of the next iteration's exact search); -1 = cold
-  int32_t* nnpos = nullptr;
+  // start of the next iteration's exact search; -1 = cold); the fallback
+  // queue (one kBS segment per kernel-1 block) and its per-block counts
+  int32_t *nnpos = nullptr, *qbuf = nullptr, *qcnt = nullptr;
   {
+    const size_t np = (size_t)std::max<int64_t>(n_local, 1);
+    const size_t nq = (size_t)nblk * kBS;
     void* w = nullptr;
-    RST_CHECK(ctx_workspace(ctx, sizeof(int32_t) * (size_t)std::max<int64_t>(n_local, 1), &w));
+    RST_CHECK(ctx_workspace(ctx, sizeof(int32_t) * (np + nq + nblk + 64), &w));
     nnpos = (int32_t*)w;
-    RST_HIP(hipMemsetAsync(nnpos, 0xff, sizeof(int32_t) * (size_t)std::max<int64_t>(n_local, 1), st));
+    qbuf = nnpos + np;
+    qcnt = qbuf + nq;
+    RST_HIP(hipMemsetAsync(nnpos, 0xff, sizeof(int32_t) * np, st));
   }
+  AccArgs aa;
+  aa.nrm = tgt->nrm;
+  aa.pmu = opts.p2plane_mu;
+  aa.max_d2 = opts.p2plane_max_dist > 0 ? opts.p2plane_max_dist * opts.p2plane_max_dist : FLT_MAX;
+  aa.pos0 = tgt->pos0;
+  const AdjView av = adj_of(tgt);
+  const size_t fb_lds = sizeof(int) * ((size_t)nblk + 1);
 
   IcpParams prm;
   prm.n = n_total;
@@ -559,30 +694,39 @@ int icp_align_prepared(rst_ctx* ctx, const rst_target* src, const rst_target* tg
   for (int it = 0; it < opts.max_iter; ++it) {
     if (timing) RST_HIP(hipEventRecord(ctx->ev[2 * it], st));
     if (n_local > 0) {
-      if (p2plane)
-        k_p2plane<<<nblk, kBS, 0, st>>>(bv, tgt->nrm, src->pts, n_local, ctx->d_state,
-                                        opts.p2plane_mu, prm.p2plane_max_d2, nnpos, slab);
-      else
-        k_p2point<<<nblk, kBS, 0, st>>>(bv, src->pts, n_local, ctx->d_state, pos0, nnpos,
-                                        slab);
+      if (p2plane) {
+        k_icp_nn<P2PlaneAcc><<<nblk, kBS, 0, st>>>(bv, av, aa, src->pts, n_local, ctx->d_state,
+                                                   nnpos, qbuf, qcnt, slab);
+        if (timing) RST_HIP(hipEventRecord(ctx->ev[2 * it + 1], st));
+        k_icp_fb<P2PlaneAcc><<<kFbBlocks, kBS, fb_lds, st>>>(bv, aa, src->pts, ctx->d_state, nnpos,
+                                                             qbuf, qcnt, nblk, slab2);
+      } else {
+        k_icp_nn<P2PointAcc><<<nblk, kBS, 0, st>>>(bv, av, aa, src->pts, n_local, ctx->d_state,
+                                                   nnpos, qbuf, qcnt, slab);
+        if (timing) RST_HIP(hipEventRecord(ctx->ev[2 * it + 1], st));
+        k_icp_fb<P2PointAcc><<<kFbBlocks, kBS, fb_lds, st>>>(bv, aa, src->pts, ctx->d_state, nnpos,
+                                                             qbuf, qcnt, nblk, slab2);
+      }
+    } else if (timing) {
+      RST_HIP(hipEventRecord(ctx->ev[2 * it + 1], st));
     }
-    if (timing) RST_HIP(hipEventRecord(ctx->ev[2 * it + 1], st));
     const int rows = n_local > 0 ? nblk : 0;
+    const int rows2 = n_local > 0 ? kFbBlocks : 0;
     if (comm) {
       if (p2plane) {
-        k_slab_reduce<kNP2Plane><<<1, kBS, 0, st>>>(slab, rows, totals);
+        k_slab_reduce<kNP2Plane><<<1, kBS, 0, st>>>(slab, rows, slab2, rows2, totals);
         RST_CHECK(comm_allreduce_sum_f64(comm, totals, kNP2Plane, st));
-        k_solve_p2plane<<<1, kBS, 0, st>>>(totals, 1, prm, ctx->d_state, nullptr);
+        k_solve_p2plane<<<1, kBS, 0, st>>>(totals, 1, totals, 0, prm, ctx->d_state, nullptr);
       } else {
-        k_slab_reduce<kNP2Point><<<1, kBS, 0, st>>>(slab, rows, totals);
+        k_slab_reduce<kNP2Point><<<1, kBS, 0, st>>>(slab, rows, slab2, rows2, totals);
         RST_CHECK(comm_allreduce_sum_f64(comm, totals, kNP2Point, st));
-        k_solve_p2point<<<1, kBS, 0, st>>>(totals, 1, prm, ctx->d_state, nullptr);
+        k_solve_p2point<<<1, kBS, 0, st>>>(totals, 1, totals, 0, prm, ctx->d_state, nullptr);
       }
     } else {
       if (p2plane)
-        k_solve_p2plane<<<1, kBS, 0, st>>>(slab, rows, prm, ctx->d_state, nullptr);
+        k_solve_p2plane<<<1, kBS, 0, st>>>(slab, rows, slab2, rows2, prm, ctx->d_state, nullptr);
       else
-        k_solve_p2point<<<1, kBS, 0, st>>>(slab, rows, prm, ctx->d_state, nullptr);
+        k_solve_p2point<<<1, kBS, 0, st>>>(slab, rows, slab2, rows2, prm, ctx->d_state, nullptr);
     }
   }
   RST_HIP(hipGetLastError());

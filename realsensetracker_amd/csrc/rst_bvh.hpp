@@ -70,11 +70,52 @@ RST_HD float box_d2(float qx, float qy, float qz, const float4& lo, const float4
 struct BvhView {
   const float4* __restrict__ pts;    // [m] sorted points, .w = original index bits
   const float4* __restrict__ nodes;  // [2 * 2nl]
+  const uint32_t* __restrict__ codes;  // [m] sorted Morton codes (may be null)
+  const float* __restrict__ bbox;    // [6] the codes' quantisation box (may be null)
   int32_t m;
   int32_t nleaves;
   int32_t lg;                        // nleaves = 1 << lg
   int32_t pad;
 };
+
+// ---- Morton order ------------------------------------------------------------------
+RST_HD uint32_t spread10(uint32_t v) {
+  v &= 0x3ffu;
+  v = (v | (v << 16)) & 0x030000FFu;
+  v = (v | (v << 8)) & 0x0300F00Fu;
+  v = (v | (v << 4)) & 0x030C30C3u;
+  v = (v | (v << 2)) & 0x09249249u;
+  return v;
+}
+
+// 30-bit code of a point quantised to 1024^3 cells over the cube of side
+// max extent at bbox lo; non-finite points sort last.
+RST_HD uint32_t morton_code(float x, float y, float z, const float* bbox) {
+  const float lx = bbox[0], ly = bbox[1], lz = bbox[2];
+  const float ext = fmaxf(fmaxf(bbox[3] - lx, bbox[4] - ly), bbox[5] - lz);
+  const float sc = ext > 0.0f ? 1023.0f / ext : 0.0f;
+  if (!finite3(x, y, z)) return 0x3fffffffu;
+  const uint32_t qx = (uint32_t)fminf(fmaxf((x - lx) * sc, 0.0f), 1023.0f);
+  const uint32_t qy = (uint32_t)fminf(fmaxf((y - ly) * sc, 0.0f), 1023.0f);
+  const uint32_t qz = (uint32_t)fminf(fmaxf((z - lz) * sc, 0.0f), 1023.0f);
+  return (spread10(qx) << 2) | (spread10(qy) << 1) | spread10(qz);
+}
+
+// Cold start: the sorted position whose Morton code is nearest to the
+// query's (lower bound, clamped) -- usually a point of the same small cell,
+// a cheap first bound for the exact searches.
+RST_HD int morton_seed(const BvhView& bv, float qx, float qy, float qz) {
+  const uint32_t c = morton_code(qx, qy, qz, bv.bbox);
+  int lo = 0, hi = bv.m;  // first code >= c in [lo, hi]
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (bv.codes[mid] < c)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return lo < bv.m ? lo : bv.m - 1;
+}
 
 RST_HD int leaf_begin(const BvhView& bv, int L) { return (int)(((int64_t)L * bv.m) >> bv.lg); }
 
@@ -100,7 +141,7 @@ RST_HD int near_child(int k, const float4& lo, const float4& hi, float qx, float
 // Lexicographic (d2, id) order; only d2 < FLT_MAX is ever admitted (what
 // nanoflann's KNNResultSet does with its FLT_MAX-initialised slots).
 RST_HD bool lex_less(float a, int ia, float b, int ib) {
-  return (a < b) || ((a == b) && (ia < ib));
+  return (a < b) | ((a == b) & (ia < ib));  // bitwise: no branches on the GPU
 }
 
 struct Best1 {
@@ -219,6 +260,129 @@ RST_HD void search(const BvhView& bv, int warm, float qx, float qy, float qz, R&
     search_from(bv, warm, qx, qy, qz, res);
   else
     descend(bv, 1, qx, qy, qz, res);
+}
+
+// ---- leaf adjacency: the tracking index ----------------------------------------------
+// ICP queries move little between iterations, so a lane's last neighbour is
+// a good start and the exact answer lies in a small ball around the query.
+// For every leaf L the build stores up to kAdjK nearby leaves by box-to-box
+// distance (ascending, L itself first), each entry carrying that leaf's
+// box, and reach[L] such that every leaf NOT listed has bbd >= reach[L].  A
+// query whose ball (radius sqrt(bound)) satisfies
+//     dist(q, box(L)) + sqrt(bound) < reach[L]
+// is then answered exactly by the listed leaves alone (any point within
+// the ball lies in a leaf whose box is closer to box(L) than reach[L]), and
+// the scan stops at the first entry with bbd - dist(q, box(L)) > sqrt(bound)
+// (entries are sorted, so no later box can touch the ball either).
+constexpr int kAdjK = 24;
+
+struct AdjView {
+  // [nl * kAdjK * 2]: entry = (lo.xyz, bbd) (hi.xyz, leaf index bits); leaf -1 = none
+  const float4* __restrict__ ent;
+  const float* __restrict__ reach;  // [nl]
+};
+
+// Box-to-box distance squared (0 when they overlap; +inf when either box
+// is empty, i.e. lo > hi).
+RST_HD float bbd2(const float4& l1, const float4& h1, const float4& l2, const float4& h2) {
+  const float ex = fmaxf(fmaxf(l2.x - h1.x, l1.x - h2.x), 0.0f);
+  const float ey = fmaxf(fmaxf(l2.y - h1.y, l1.y - h2.y), 0.0f);
+  const float ez = fmaxf(fmaxf(l2.z - h1.z, l1.z - h2.z), 0.0f);
+  float r = ex * ex;
+  r = r + ey * ey;
+  r = r + ez * ez;
+  return r;
+}
+
+RST_HD void adj_put(float4* ent, int L, int k, int X, float bbd, const float4& lo,
+                    const float4& hi) {
+  float4* e = ent + ((int64_t)L * kAdjK + k) * 2;
+  e[0] = make_float4(lo.x, lo.y, lo.z, bbd);
+  e[1] = make_float4(hi.x, hi.y, hi.z, i2f(X));
+}
+
+// The K nearest leaves of leaf L by bbd2 (items = leaves, id = leaf index):
+// bottom-up from L like search_from, pruning subtrees by bbd2 to their box.
+// (Reference builder for tests; the GPU builds with rst_wave_nn.hpp.)
+template <class R>
+RST_HD void leaf_descend(const BvhView& bv, int root, const float4& ql, const float4& qh, R& res) {
+  const int nl = bv.nleaves;
+  const int top = root >> 1;
+  const float cx = 0.5f * (ql.x + qh.x), cy = 0.5f * (ql.y + qh.y), cz = 0.5f * (ql.z + qh.z);
+  int cur = root, prev = top;
+  do {
+    const int parent = cur >> 1;
+    const float4 lo = bv.nodes[2 * cur];
+    const float4 hi = bv.nodes[2 * cur + 1];
+    int next;
+    if (prev == parent) {
+      const float b = bbd2(ql, qh, lo, hi);
+      if (b > res.bound()) {
+        next = parent;
+      } else if (cur >= nl) {
+        res.offer(b, cur - nl, cur - nl);
+        next = parent;
+      } else {
+        next = near_child(cur, lo, hi, cx, cy, cz);
+      }
+    } else {
+      const int nc = near_child(cur, lo, hi, cx, cy, cz);
+      next = (prev == nc) ? (prev ^ 1) : parent;
+    }
+    prev = cur;
+    cur = next;
+  } while (cur != top);
+}
+
+template <class R>
+RST_HD void leaf_knn(const BvhView& bv, int L, R& res) {
+  const int nl = bv.nleaves;
+  int node = nl + L;
+  const float4 ql = bv.nodes[2 * node], qh = bv.nodes[2 * node + 1];
+  res.offer(bbd2(ql, qh, ql, qh), L, L);
+  while (node > 1) {
+    leaf_descend(bv, node ^ 1, ql, qh, res);
+    node >>= 1;
+  }
+}
+
+// Adjacency record of leaf L from its K+1 nearest (sorted) leaves.
+template <int K1>
+RST_HD void adj_store(const BvhView& bv, const BestK<K1>& r, int L, float4* ent, float* reach) {
+  static_assert(K1 == kAdjK + 1, "list length");
+  const int nl = bv.nleaves;
+  for (int j = 0; j < kAdjK; ++j) {
+    const int X = r.pos[j] >= 0 ? r.id[j] : -1;
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    adj_put(ent, L, j, X, X >= 0 ? sqrtf(r.d[j]) : INFINITY, X >= 0 ? bv.nodes[2 * (nl + X)] : z,
+            X >= 0 ? bv.nodes[2 * (nl + X) + 1] : z);
+  }
+  reach[L] = r.pos[kAdjK] >= 0 ? sqrtf(r.d[kAdjK]) : INFINITY;
+}
+
+// Exact search through the adjacency of the leaf holding sorted position
+// `start` (res already holds at least that point's offer, or a smaller
+// bound).  Returns false, having offered nothing, when the query ball is
+// not covered -- the caller then needs a full search.
+template <class R>
+RST_HD bool adj_search(const BvhView& bv, const AdjView& av, int start, float qx, float qy,
+                       float qz, R& res) {
+  const int nl = bv.nleaves;
+  const int L = leaf_of(bv, start);
+  const float4 lo = bv.nodes[2 * (nl + L)], hi = bv.nodes[2 * (nl + L) + 1];
+  // margins cover float rounding of every distance below (relative 1e-5)
+  const float dl = sqrtf(box_d2(qx, qy, qz, lo, hi)) * 1.00001f;
+  const float rb = sqrtf(res.bound()) * 1.00001f + 1e-30f;
+  if (!(dl + rb < av.reach[L] * 0.99999f)) return false;
+  const float4* e = av.ent + (int64_t)L * kAdjK * 2;
+  for (int k = 0; k < kAdjK; ++k) {
+    const float4 l = e[2 * k], h = e[2 * k + 1];
+    const int X = f2i(h.w);
+    if (X < 0) break;
+    if (l.w * 0.99999f - dl > sqrtf(res.bound()) * 1.00001f + 1e-30f) break;
+    if (box_d2(qx, qy, qz, l, h) <= res.bound()) scan_leaf(bv, X, qx, qy, qz, res);
+  }
+  return true;
 }
 
 // ---- build: internal node from its two children ------------------------------------

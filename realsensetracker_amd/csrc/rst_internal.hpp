@@ -42,6 +42,8 @@ void set_last_error(hipError_t e, const char* what, const char* file,
 // ---- device-resident state of one ICP solve --------------------------------
 // Written only by the single-block solve kernels, read (uniformly) by the
 // per-point kernels.  Plain POD; lives in the context's workspace.
+constexpr int kQTrace = 256;
+
 struct IcpState {
   float R[9];        // current pose, column-major (what the points see)
   float t[3];
@@ -58,6 +60,7 @@ struct IcpState {
   double last_d2;    // sum d2 of the last step
   int32_t fail;      // P2PLANE: singular system / too few points
   int32_t pad1;
+  int32_t qlen[kQTrace];  // fallback-queue length per iteration (diagnostics)
 };
 
 struct IcpParams {
@@ -101,6 +104,9 @@ struct rst_target {
   float4* pts = nullptr;        // [m] Morton-sorted (x,y,z,orig idx bits)
   float4* nodes = nullptr;      // [2 * 2*nleaves]
   int32_t* inv = nullptr;       // [m] original index -> sorted position
+  uint32_t* codes = nullptr;    // [m] sorted Morton codes, then 6 floats: their box
+  float4* adj = nullptr;        // [nleaves * kAdjK * 2] leaf adjacency (rst_bvh.hpp)
+  float* reach = nullptr;       // [nleaves]
   float4* nrm = nullptr;        // [m] normals in sorted order (optional)
   float bbox[6] = {0, 0, 0, 0, 0, 0};
   int32_t pos0 = 0;             // sorted position of original point 0
@@ -119,6 +125,7 @@ int target_build_device(rst_ctx* ctx, const float* d_xyz, int64_t m,
                         bool with_bvh, rst_target** out);
 size_t target_index_bytes(const rst_target* t);
 BvhView view_of(const rst_target* t);
+AdjView adj_of(const rst_target* t);
 
 // NN queries (query.hip)
 int query_nn_device(rst_ctx* ctx, const rst_target* tgt, const float* d_q,

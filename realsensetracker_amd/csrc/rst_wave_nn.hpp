@@ -11,10 +11,11 @@
 //   1. every lane has a bound: the d2 of its warm candidate (last
 //      iteration's neighbour; cold lanes take the best point of the leaf a
 //      greedy near-child descent reaches);
-//   2. region = AABB of all lanes' balls (radius sqrt(bound), inflated);
-//   3. staging walk: LIFO stack of node ids in LDS, popped up to 32 at a
+//   2. regions = AABB of the balls (radius sqrt(bound), inflated) of each
+//      8-lane group, and their union;
+//   3. staging walk: LIFO stack of node ids in LDS, popped up to 64 at a
 //      time -- lane t loads node t's box (one coalesced load per round, all
-//      in flight together), keeps it if it meets the region; internal nodes
+//      in flight together), keeps it if it meets a group region; internal nodes
 //      push both children, leaves are staged (box + id) in LDS.  The walk
 //      starts at the lowest common ancestor of the lanes' start leaves plus
 //      the sibling of every ancestor, i.e. still the whole tree;
@@ -25,8 +26,8 @@
 //      offers it to its own lexicographic (d2, index) minimum.  The region
 //      shrinks after every flush as the bounds tighten.
 //
-// Exactness: a node is dropped only if its box misses the region, i.e. for
-// every lane its box_d2 exceeds that lane's bound; a staged leaf is skipped
+// Exactness: a node is dropped only if its box misses every group region,
+// i.e. for every lane its box_d2 exceeds that lane's bound; a staged leaf is skipped
 // only if no lane's box_d2 <= bound.  Bounds only decrease, so every point
 // not offered is strictly worse than the final answer (same argument as the
 // tree walks of rst_bvh.hpp, which tests/cpp/bvh_selftest.cpp checks).
@@ -41,14 +42,34 @@
 namespace rst {
 
 constexpr int kWnnStack = 512;   // node ids per wave (see the overflow rule)
-constexpr int kWnnLeaves = 64;   // staged leaves per flush
-constexpr int kWnnPop = 32;      // nodes tested per staging round
+constexpr int kWnnLeaves = 128;  // staged leaves per flush
+constexpr int kWnnPop = 64;      // nodes tested per staging round
+constexpr int kWnnGroups = 8;    // lane groups with their own region (8 lanes each)
+// Work cap of the shared walk: a wave whose regions stage more leaves than
+// this (a cold start with poor seeds, a cluster of far outliers) finishes
+// with per-lane bottom-up searches instead (rst_bvh.hpp search_from: exact
+// from any starting bound; divergent gathers, but a bounded latency chain).
+constexpr int kWnnCap = 256;
 
-struct WnnScratch {              // per-wave LDS (4 KB)
+struct WnnScratch {              // per-wave LDS (6.6 KB)
   int stack[kWnnStack];
   float4 leaf_lo[kWnnLeaves];    // .w = leaf index bits
-  float4 leaf_hi[kWnnLeaves];    // .w = point count bits
+  float4 leaf_hi[kWnnLeaves];
+  float4 greg_lo[2 * kWnnGroups];  // AABBs of the group's ordinary balls (2 runs)
+  float4 greg_hi[2 * kWnnGroups];
+  float4 gsph[kWnnGroups];       // sphere around the group's big balls (xyz, R^2)
 };
+
+// A lane whose bound exceeds this radius (metres) is "big": its ball joins
+// its group's bounding sphere instead of the group's AABB.  An off-surface
+// query (frame border, occlusion) has a large ball that touches the target
+// surface only near its neighbour; the ball's AABB would take in a whole
+// square of surface, a sphere test does not.
+constexpr float kWnnBigR = 0.012f;
+// A group whose largest step between consecutive queries exceeds this
+// (metres) straddles a jump of the Morton curve (e.g. far wall -> near
+// object): its ordinary balls get one AABB per side of the jump.
+constexpr float kWnnJump = 0.05f;
 
 __device__ __forceinline__ float wnn_rl(float v, int l) {
   return i2f(__builtin_amdgcn_readlane(f2i(v), l));
@@ -94,18 +115,106 @@ struct WnnRegion {
   }
 };
 
-__device__ __forceinline__ WnnRegion wnn_region(bool act, float qx, float qy, float qz,
-                                                float bound) {
+// min / max over the 8 lanes of a group (xor 1, 2, 4 stays in the group)
+__device__ __forceinline__ float wnn_gmin(float v) {
+#pragma unroll
+  for (int o = 1; o < 8; o <<= 1) v = fminf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ float wnn_gmax(float v) {
+#pragma unroll
+  for (int o = 1; o < 8; o <<= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Regions of the current bounds, per 8-lane group (in LDS): the AABB of the
+// ordinary balls -- two AABBs, one per side, when the group straddles a
+// jump of the Morton curve -- and a sphere holding the big balls (a far
+// outlier only widens its own group's sphere); the union AABB is returned.
+__device__ __forceinline__ WnnRegion wnn_regions(bool act, float qx, float qy, float qz,
+                                                 float bound, WnnScratch& ws) {
   // inflate so float rounding can never drop a node some lane needs
   const float rad = act ? sqrtf(bound) * 1.0001f + 1e-20f : 0.0f;
-  WnnRegion g;
-  g.lx = wnn_min_f(act ? qx - rad : FLT_MAX);
-  g.ly = wnn_min_f(act ? qy - rad : FLT_MAX);
-  g.lz = wnn_min_f(act ? qz - rad : FLT_MAX);
-  g.hx = wnn_max_f(act ? qx + rad : -FLT_MAX);
-  g.hy = wnn_max_f(act ? qy + rad : -FLT_MAX);
-  g.hz = wnn_max_f(act ? qz + rad : -FLT_MAX);
-  return g;
+  const bool big = act && rad > kWnnBigR;
+  const bool ord = act && !big;
+  const int lane = __lane_id();
+  const int gl = lane & 7;
+  // largest step to the previous query inside the group -> run split point
+  const float px = __shfl(qx, lane - 1, 64), py = __shfl(qy, lane - 1, 64),
+              pz = __shfl(qz, lane - 1, 64);
+  const bool pact = __shfl((int)act, lane - 1, 64) != 0;
+  float gap = -1.f;
+  if (gl > 0 && act && pact) {
+    const float ex = qx - px, ey = qy - py, ez = qz - pz;
+    gap = ex * ex + ey * ey + ez * ez;
+  }
+  float gbest = gap;
+  int gk = gl;
+#pragma unroll
+  for (int o = 1; o < 8; o <<= 1) {
+    const float og = __shfl_xor(gbest, o, 64);
+    const int ok = __shfl_xor(gk, o, 64);
+    const bool take = (og > gbest) | ((og == gbest) & (ok < gk));
+    gbest = take ? og : gbest;
+    gk = take ? ok : gk;
+  }
+  const int run = (gbest > kWnnJump * kWnnJump && gl >= gk) ? 1 : 0;
+  float lx[2], ly[2], lz[2], hx[2], hy[2], hz[2];
+#pragma unroll
+  for (int sub = 0; sub < 2; ++sub) {
+    const bool in = ord && run == sub;
+    lx[sub] = wnn_gmin(in ? qx - rad : FLT_MAX);
+    ly[sub] = wnn_gmin(in ? qy - rad : FLT_MAX);
+    lz[sub] = wnn_gmin(in ? qz - rad : FLT_MAX);
+    hx[sub] = wnn_gmax(in ? qx + rad : -FLT_MAX);
+    hy[sub] = wnn_gmax(in ? qy + rad : -FLT_MAX);
+    hz[sub] = wnn_gmax(in ? qz + rad : -FLT_MAX);
+  }
+  // big balls: centre = middle of their centres, R = max |q - c| + r
+  const float bx0 = wnn_gmin(big ? qx : FLT_MAX), bx1 = wnn_gmax(big ? qx : -FLT_MAX);
+  const float by0 = wnn_gmin(big ? qy : FLT_MAX), by1 = wnn_gmax(big ? qy : -FLT_MAX);
+  const float bz0 = wnn_gmin(big ? qz : FLT_MAX), bz1 = wnn_gmax(big ? qz : -FLT_MAX);
+  const bool anybig = bx0 <= bx1;
+  const float cx = anybig ? 0.5f * (bx0 + bx1) : 0.f;
+  const float cy = anybig ? 0.5f * (by0 + by1) : 0.f;
+  const float cz = anybig ? 0.5f * (bz0 + bz1) : 0.f;
+  const float dx = qx - cx, dy = qy - cy, dz = qz - cz;
+  const float R = wnn_gmax(big ? (sqrtf(dx * dx + dy * dy + dz * dz) + rad) * 1.0001f + 1e-20f
+                               : 0.f);
+  if (gl == 0) {
+    const int g = lane >> 3;
+    ws.greg_lo[2 * g] = make_float4(lx[0], ly[0], lz[0], 0.f);
+    ws.greg_hi[2 * g] = make_float4(hx[0], hy[0], hz[0], 0.f);
+    ws.greg_lo[2 * g + 1] = make_float4(lx[1], ly[1], lz[1], 0.f);
+    ws.greg_hi[2 * g + 1] = make_float4(hx[1], hy[1], hz[1], 0.f);
+    ws.gsph[g] = make_float4(cx, cy, cz, anybig ? R * R * 1.0001f : -1.f);
+  }
+  WnnRegion u;
+  u.lx = wnn_min_f(fminf(fminf(lx[0], lx[1]), anybig ? cx - R : FLT_MAX));
+  u.ly = wnn_min_f(fminf(fminf(ly[0], ly[1]), anybig ? cy - R : FLT_MAX));
+  u.lz = wnn_min_f(fminf(fminf(lz[0], lz[1]), anybig ? cz - R : FLT_MAX));
+  u.hx = wnn_max_f(fmaxf(fmaxf(hx[0], hx[1]), anybig ? cx + R : -FLT_MAX));
+  u.hy = wnn_max_f(fmaxf(fmaxf(hy[0], hy[1]), anybig ? cy + R : -FLT_MAX));
+  u.hz = wnn_max_f(fmaxf(fmaxf(hz[0], hz[1]), anybig ? cz + R : -FLT_MAX));
+  __builtin_amdgcn_wave_barrier();
+  return u;
+}
+
+__device__ __forceinline__ bool wnn_meets_group(const WnnScratch& ws, const float4& lo,
+                                                const float4& hi) {
+  bool m = false;
+#pragma unroll
+  for (int k = 0; k < 2 * kWnnGroups; ++k) {
+    const float4 a = ws.greg_lo[k], b = ws.greg_hi[k];
+    m |= (lo.x <= b.x) & (hi.x >= a.x) & (lo.y <= b.y) & (hi.y >= a.y) & (lo.z <= b.z) &
+         (hi.z >= a.z);
+  }
+#pragma unroll
+  for (int g = 0; g < kWnnGroups; ++g) {
+    const float4 c = ws.gsph[g];
+    m |= box_d2(c.x, c.y, c.z, lo, hi) <= c.w;
+  }
+  return m;
 }
 
 // Offer the staged leaves [0, ns) to every active lane.  Four leaves per
@@ -147,13 +256,15 @@ __device__ __forceinline__ int wnn_flush(const BvhView& bv, const WnnScratch& ws
 // r arrives holding the warm candidate (or empty) and leaves with the exact
 // lexicographic (d2, index) minimum; non-finite queries find nothing.
 // stats (diagnostics, may be null): per wave, 8 ints at stats[8 * wave]:
-// staging rounds, nodes tested, leaves staged, leaves scanned, flushes,
-// active lanes, lanes with no finite bound, region extent (um, max axis).
+// staging rounds, nodes tested, leaves staged, leaves scanned, wave time
+// (s_memrealtime ticks, 10 ns), active lanes, lanes with no finite bound,
+// region extent (um, max axis).
 __device__ __forceinline__ void nn_wave_region(const BvhView& bv, bool act, float qx, float qy,
                                             float qz, Best1& r, WnnScratch& ws,
                                             int* stats = nullptr) {
   const int lane = __lane_id();
   const int nl = bv.nleaves;
+  const uint64_t t_start = stats ? __builtin_amdgcn_s_memrealtime() : 0;
   act = act && bv.m > 0 && finite3(qx, qy, qz);
   if (act && r.pos < 0) wnn_seed(bv, qx, qy, qz, r);
   if (__ballot(act) == 0) return;
@@ -173,7 +284,7 @@ __device__ __forceinline__ void nn_wave_region(const BvhView& bv, bool act, floa
   if (lane == 0) ws.stack[depth] = (int)lca;
   int sp = depth + 1;
   __builtin_amdgcn_wave_barrier();
-  WnnRegion reg = wnn_region(act, qx, qy, qz, r.d);
+  WnnRegion reg = wnn_regions(act, qx, qy, qz, r.d, ws);
   int ns = 0;
   int st_rounds = 0, st_nodes = 0, st_staged = 0, st_scanned = 0, st_flush = 0;
   if (stats) {
@@ -191,7 +302,9 @@ __device__ __forceinline__ void nn_wave_region(const BvhView& bv, bool act, floa
     if (sp > 0) {
       // overflow rule: above the high-water mark pop one node at a time
       // (pure DFS grows the stack by at most the tree depth)
-      const int k = sp > kWnnStack - 64 ? 1 : min(kWnnPop, sp);
+      // overflow rule: pops shrink as the stack fills, down to one node at
+      // a time (pure DFS then grows the stack by at most the tree depth)
+      const int k = min(min(kWnnPop, sp), max(1, (kWnnStack - 48 - sp) / 2));
       ++st_rounds;
       st_nodes += k;
       int node = 0;
@@ -203,7 +316,7 @@ __device__ __forceinline__ void nn_wave_region(const BvhView& bv, bool act, floa
       if (lane < k) {
         lo = bv.nodes[2 * node];
         hi = bv.nodes[2 * node + 1];
-        pass = reg.meets(lo, hi);
+        pass = reg.meets(lo, hi) && wnn_meets_group(ws, lo, hi);
       }
       const bool isleaf = node >= nl;
       const uint64_t im = __ballot(pass && !isleaf);
@@ -227,12 +340,23 @@ __device__ __forceinline__ void nn_wave_region(const BvhView& bv, bool act, floa
       st_staged += __popcll(lm);
       __builtin_amdgcn_wave_barrier();
     }
-    if (ns > kWnnLeaves - kWnnPop || (sp == 0 && ns > 0)) {
+    const bool over = st_staged > kWnnCap;
+    if (ns > kWnnLeaves - kWnnPop || (ns > 0 && (sp == 0 || over))) {
       st_scanned += wnn_flush(bv, ws, ns, act, qx, qy, qz, r);
       ++st_flush;
       ns = 0;
-      reg = wnn_region(act, qx, qy, qz, r.d);
-      __builtin_amdgcn_wave_barrier();
+      reg = wnn_regions(act, qx, qy, qz, r.d, ws);
+    }
+    if (over) {
+      // fallback: every lane finishes on its own (exact from its bound)
+      if (act) {
+        if (r.pos >= 0)
+          search_from(bv, r.pos, qx, qy, qz, r);
+        else
+          descend(bv, 1, qx, qy, qz, r);
+      }
+      st_flush = -1;
+      break;
     }
   }
   if (stats && lane == 0) {
@@ -240,8 +364,292 @@ __device__ __forceinline__ void nn_wave_region(const BvhView& bv, bool act, floa
     stats[1] = st_nodes;
     stats[2] = st_staged;
     stats[3] = st_scanned;
-    stats[4] = st_flush;
+    stats[4] = (int)(__builtin_amdgcn_s_memrealtime() - t_start);
+    if (st_flush < 0) stats[5] = -stats[5];  // marks a capped wave
   }
+}
+
+}  // namespace rst
+
+namespace rst {
+
+// ---- one query, a whole wavefront ------------------------------------------------
+// The fallback of the ICP search (queries the leaf adjacency cannot cover:
+// cold starts with poor seeds, far outliers at frame borders and
+// occlusions).  All 64 lanes work on the same query q: the staging walk
+// tests up to 64 nodes per round exactly (box_d2 <= bound), starting at the
+// warm leaf and the siblings of its ancestors; staged leaves are scanned 64
+// points per step, one point per lane, and a lexicographic wave minimum
+// after every flush tightens the shared bound.  Latency ~ the depth of the
+// subtrees the ball touches, not the number of points in it.
+__device__ __forceinline__ Best1 wave_lex_min(Best1 b) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float od = __shfl_xor(b.d, o, 64);
+    const int oid = __shfl_xor(b.id, o, 64);
+    const int op = __shfl_xor(b.pos, o, 64);
+    const bool t = lex_less(od, oid, b.d, b.id) | ((od == b.d) & (oid == b.id) & (op > b.pos));
+    b.d = t ? od : b.d;
+    b.id = t ? oid : b.id;
+    b.pos = t ? op : b.pos;
+  }
+  return b;
+}
+
+// r: uniform across the wave (the warm offer, or empty); returns the exact
+// answer, uniform.  warm: sorted position to start from (-1: the root).
+__device__ __forceinline__ void nn_wave_one(const BvhView& bv, int warm, float qx, float qy,
+                                            float qz, Best1& r, WnnScratch& ws) {
+  const int lane = __lane_id();
+  const int nl = bv.nleaves;
+  if (bv.m <= 0 || !finite3(qx, qy, qz)) return;
+  Best1 mine = r;
+  const unsigned start = (warm >= 0 && warm < bv.m) ? (unsigned)(nl + leaf_of(bv, warm)) : 1u;
+  const int depth = 31 - __clz(start);
+  if (lane < depth) ws.stack[lane] = (int)((start >> (depth - 1 - lane)) ^ 1u);
+  if (lane == 0) ws.stack[depth] = (int)start;
+  int sp = depth + 1;
+  int ns = 0;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  __builtin_amdgcn_wave_barrier();
+  while (sp > 0 || ns > 0) {
+    if (sp > 0) {
+      const int k = min(min(kWnnPop, sp), max(1, (kWnnStack - 48 - sp) / 2));
+      int node = 0;
+      if (lane < k) node = ws.stack[sp - 1 - lane];
+      sp -= k;
+      __builtin_amdgcn_wave_barrier();
+      bool pass = false;
+      float4 lo = make_float4(0.f, 0.f, 0.f, 0.f), hi = lo;
+      float bd = 0.f;
+      if (lane < k) {
+        lo = bv.nodes[2 * node];
+        hi = bv.nodes[2 * node + 1];
+        bd = box_d2(qx, qy, qz, lo, hi);
+        pass = bd <= r.d;
+      }
+      const bool isleaf = node >= nl;
+      const uint64_t im = __ballot(pass && !isleaf);
+      const uint64_t lm = __ballot(pass && isleaf);
+      if (pass && !isleaf) {
+        const int rk = __popcll(im & lt);
+        const int nc = near_child(node, lo, hi, qx, qy, qz);
+        ws.stack[sp + 2 * rk] = nc ^ 1;
+        ws.stack[sp + 2 * rk + 1] = nc;
+      }
+      if (pass && isleaf) {
+        const int rk = __popcll(lm & lt);
+        ws.leaf_lo[ns + rk] = make_float4(bd, 0.f, 0.f, i2f(node - nl));
+      }
+      sp += 2 * __popcll(im);
+      ns += __popcll(lm);
+      __builtin_amdgcn_wave_barrier();
+    }
+    if (ns > kWnnLeaves - kWnnPop || (sp == 0 && ns > 0)) {
+      // four leaves per step: lanes 16g..16g+15 take leaf s+g's points
+      const int g = lane >> 4, o = lane & 15;
+      for (int s = 0; s < ns; s += 4) {
+        if (s + g < ns) {
+          const float4 e = ws.leaf_lo[s + g];
+          if (e.x <= r.d) {
+            const int L = f2i(e.w);
+            const int b = leaf_begin(bv, L);
+            if (o < leaf_begin(bv, L + 1) - b) {
+              const float4 p = bv.pts[b + o];
+              mine.offer(d2_ref(qx, qy, qz, p.x, p.y, p.z), f2i(p.w), b + o);
+            }
+          }
+        }
+      }
+      r = wave_lex_min(mine);
+      ns = 0;
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+}
+
+}  // namespace rst
+
+namespace rst {
+
+// ---- per-lane search through the leaf adjacency (the ICP fast path) ------------
+// rst_bvh.hpp adj_search with every load issued early: adjacency entries
+// four at a time (each entry carries its leaf's box, so a test needs no
+// further gather) and leaf points eight at a time, unconditionally (index
+// clamped), so a lane's dependent chain is warm point -> entries -> points.
+__device__ __forceinline__ void scan_leaf_wide(const BvhView& bv, int X, float qx, float qy,
+                                               float qz, Best1& r) {
+  const int b = leaf_begin(bv, X), n = leaf_begin(bv, X + 1) - b;
+  const int last = bv.m - 1;
+  for (int j0 = 0; j0 < n; j0 += 8) {
+    float4 p[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) p[j] = bv.pts[min(b + j0 + j, last)];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (j0 + j < n) r.offer(d2_ref(qx, qy, qz, p[j].x, p[j].y, p[j].z), f2i(p[j].w), b + j0 + j);
+  }
+}
+
+// When the ball is not covered (the query moved away from its last
+// neighbour, early ICP iterations), the warm candidate is first walked
+// through the adjacency: the listed leaf whose box is nearest to the query
+// is scanned and the best point found becomes the new start, up to
+// kWalkSteps times.  Walking only lowers the bound; exactness still comes
+// from the coverage test of the final leaf.
+constexpr int kWalkSteps = 3;
+
+__device__ __forceinline__ bool adj_search_wide(const BvhView& bv, const AdjView& av, int start,
+                                                float qx, float qy, float qz, Best1& r) {
+  const int nl = bv.nleaves;
+  int L = leaf_of(bv, start);
+  float dl;
+  for (int step = 0;; ++step) {
+    const float4 lo = bv.nodes[2 * (nl + L)], hi = bv.nodes[2 * (nl + L) + 1];
+    const float reach = av.reach[L];
+    // same margins as rst_bvh.hpp adj_search
+    dl = sqrtf(box_d2(qx, qy, qz, lo, hi)) * 1.00001f;
+    if (dl + sqrtf(r.d) * 1.00001f + 1e-30f < reach * 0.99999f) break;
+    if (step == kWalkSteps) return false;
+    // walk: scan the listed leaf nearest to the query (other than L)
+    const float4* e = av.ent + (int64_t)L * kAdjK * 2;
+    float bb = FLT_MAX;
+    int bx = -1;
+    for (int k = 1; k < kAdjK; ++k) {
+      const float4 l = e[2 * k], h = e[2 * k + 1];
+      const int X = f2i(h.w);
+      const float b = box_d2(qx, qy, qz, l, h);
+      const bool t = X >= 0 && b < bb;
+      bb = t ? b : bb;
+      bx = t ? X : bx;
+    }
+    if (bx < 0 || !(bb < r.d)) return false;
+    scan_leaf_wide(bv, bx, qx, qy, qz, r);
+    L = leaf_of(bv, r.pos);
+  }
+  const float4* e = av.ent + (int64_t)L * kAdjK * 2;
+  for (int k0 = 0; k0 < kAdjK; k0 += 4) {
+    float4 l[4], h[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      l[j] = e[2 * (k0 + j)];
+      h[j] = e[2 * (k0 + j) + 1];
+    }
+    bool stop = false;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (stop) break;
+      const int X = f2i(h[j].w);
+      if (X < 0 || l[j].w * 0.99999f - dl > sqrtf(r.d) * 1.00001f + 1e-30f) {
+        stop = true;
+      } else if (box_d2(qx, qy, qz, l[j], h[j]) <= r.d) {
+        scan_leaf_wide(bv, X, qx, qy, qz, r);
+      }
+    }
+    if (stop) break;
+  }
+  return true;
+}
+
+// ---- adjacency build: one wavefront per leaf -------------------------------------
+// Range query around box(L) with radius D0 = 2 x its diagonal (halved while
+// more than kWnnLeaves leaves fall inside), then the kAdjK nearest of the
+// collected leaves by rank.  reach[L] = the (kAdjK+1)-th distance when more
+// were collected, else sqrt(D0^2): every leaf not listed is at least that
+// far (non-collected leaves have bbd2 > D0^2).  Degenerate cases (empty box,
+// persistent overflow) get reach 0: such a leaf never certifies a query.
+__device__ __forceinline__ void leaf_adj_wave(const BvhView& bv, int L, float4* __restrict__ ent,
+                                              float* __restrict__ reach, WnnScratch& ws) {
+  const int lane = __lane_id();
+  const int nl = bv.nleaves;
+  const float4 ql = bv.nodes[2 * (nl + L)], qh = bv.nodes[2 * (nl + L) + 1];
+  const float dx = qh.x - ql.x, dy = qh.y - ql.y, dz = qh.z - ql.z;
+  const float diag2 = dx * dx + dy * dy + dz * dz;
+  float D2 = 4.0f * diag2;
+  int ns = 0;
+  bool overflow = !(ql.x <= qh.x) || !(diag2 < FLT_MAX);
+  for (int attempt = 0; attempt < 6 && !(!(ql.x <= qh.x) || !(diag2 < FLT_MAX)); ++attempt) {
+    const unsigned start = (unsigned)(nl + L);
+    const int depth = 31 - __clz(start);
+    if (lane < depth) ws.stack[lane] = (int)((start >> (depth - 1 - lane)) ^ 1u);
+    if (lane == 0) ws.stack[depth] = (int)start;
+    int sp = depth + 1;
+    ns = 0;
+    overflow = false;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    __builtin_amdgcn_wave_barrier();
+    while (sp > 0 && !overflow) {
+      const int k = min(min(kWnnPop, sp), max(1, (kWnnStack - 48 - sp) / 2));
+      int node = 0;
+      if (lane < k) node = ws.stack[sp - 1 - lane];
+      sp -= k;
+      __builtin_amdgcn_wave_barrier();
+      bool pass = false;
+      float b2 = 0.f;
+      if (lane < k) {
+        b2 = bbd2(ql, qh, bv.nodes[2 * node], bv.nodes[2 * node + 1]);
+        pass = b2 <= D2;
+      }
+      const bool isleaf = node >= nl;
+      const uint64_t im = __ballot(pass && !isleaf);
+      const uint64_t lm = __ballot(pass && isleaf);
+      if (ns + __popcll(lm) > kWnnLeaves) {
+        overflow = true;
+        break;
+      }
+      if (pass && !isleaf) {
+        const int rk = __popcll(im & lt);
+        ws.stack[sp + 2 * rk] = 2 * node + 1;
+        ws.stack[sp + 2 * rk + 1] = 2 * node;
+      }
+      if (pass && isleaf) ws.leaf_lo[ns + __popcll(lm & lt)] = make_float4(b2, 0.f, 0.f, i2f(node - nl));
+      sp += 2 * __popcll(im);
+      ns += __popcll(lm);
+      __builtin_amdgcn_wave_barrier();
+    }
+    if (!overflow) break;
+    D2 *= 0.25f;
+  }
+  float4* e = ent + (int64_t)L * kAdjK * 2;
+  if (overflow) {
+    if (lane < kAdjK) {
+      e[2 * lane] = make_float4(0.f, 0.f, 0.f, INFINITY);
+      e[2 * lane + 1] = make_float4(0.f, 0.f, 0.f, i2f(-1));
+    }
+    if (lane == 0) reach[L] = 0.0f;
+    return;
+  }
+  __builtin_amdgcn_wave_barrier();
+  // rank of each collected leaf in (bbd2, index) order
+  float rk_b2 = -1.f;  // bbd2 of the element ranked kAdjK (the reach)
+  for (int s = lane; s < kWnnLeaves; s += 64) {
+    int rank = 1 << 30;
+    float mb = 0.f;
+    int mid = 0;
+    if (s < ns) {
+      const float4 me = ws.leaf_lo[s];
+      mb = me.x;
+      mid = f2i(me.w);
+      rank = 0;
+      for (int t = 0; t < ns; ++t) {
+        const float4 o = ws.leaf_lo[t];
+        rank += lex_less(o.x, f2i(o.w), mb, mid) ? 1 : 0;
+      }
+    }
+    if (rank < kAdjK) {
+      e[2 * rank] = make_float4(bv.nodes[2 * (nl + mid)].x, bv.nodes[2 * (nl + mid)].y,
+                                bv.nodes[2 * (nl + mid)].z, sqrtf(mb));
+      const float4 h = bv.nodes[2 * (nl + mid) + 1];
+      e[2 * rank + 1] = make_float4(h.x, h.y, h.z, i2f(mid));
+    }
+    if (rank == kAdjK) rk_b2 = mb;
+  }
+  if (lane >= ns && lane < kAdjK) {
+    e[2 * lane] = make_float4(0.f, 0.f, 0.f, INFINITY);
+    e[2 * lane + 1] = make_float4(0.f, 0.f, 0.f, i2f(-1));
+  }
+  const float kth = wnn_max_f(rk_b2);
+  if (lane == 0) reach[L] = ns > kAdjK ? sqrtf(kth) : sqrtf(D2);
 }
 
 }  // namespace rst

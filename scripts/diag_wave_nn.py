@@ -64,12 +64,18 @@ def main():
                   L.iptr(idx), L.fptr(d2), L.iptr(st)), "stats")
         dt = time.perf_counter() - t0
         st = st.reshape(-1, 8)
-        names = ["rounds", "nodes", "staged", "scanned", "flushes", "active", "nobound", "ext_um"]
-        print(f"--- {label}: wall {dt*1e3:.1f} ms (incl. upload)")
+        names = ["rounds", "nodes", "staged", "scanned", "wave_us", "active", "nobound", "ext_um"]
+        st = st.astype(np.float64)
+        st[:, 4] *= 0.01
+        print(f"--- {label}: wall {dt*1e3:.1f} ms (incl. upload), kernel {ctx.last_kernel_time()[0]*1e3:.1f} us")
         for k, nm in enumerate(names):
             v = st[:, k].astype(np.float64)
             print(f"  {nm:8s} mean {v.mean():10.1f}  p50 {np.percentile(v,50):10.1f}  "
                   f"p90 {np.percentile(v,90):10.1f}  p99 {np.percentile(v,99):10.1f}  max {v.max():10.0f}")
+        print("  capped waves:", int((st[:, 5] < 0).sum()), "of", len(st))
+        slow = np.argsort(st[:, 4])[-5:]
+        for w in slow:
+            print("   slow wave", w, " ".join(f"{nm}={st[w,k]:.0f}" for k, nm in enumerate(names)))
         return idx, d2, q
 
     idx0, _, q0 = stats_for(np.eye(4, dtype=np.float32), None, "identity pose, cold")

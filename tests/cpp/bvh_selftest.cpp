@@ -21,19 +21,15 @@ using namespace rst;
 
 namespace {
 
-uint32_t spread10(uint32_t v) {
-  v &= 0x3ffu;
-  v = (v | (v << 16)) & 0x030000FFu;
-  v = (v | (v << 8)) & 0x0300F00Fu;
-  v = (v | (v << 4)) & 0x030C30C3u;
-  v = (v | (v << 2)) & 0x09249249u;
-  return v;
-}
+void check(bool ok, const char* what, int m, int q);
 
 struct Index {
   std::vector<float4> pts;
   std::vector<float4> nodes;
+  std::vector<float4> adj;
+  std::vector<float> reach;
   BvhView bv;
+  AdjView av;
 };
 
 Index build(const std::vector<float>& xyz) {
@@ -71,6 +67,8 @@ Index build(const std::vector<float>& xyz) {
     ++lg;
   }
   ix.nodes.resize(4 * (size_t)nl);
+  ix.bv.codes = nullptr;
+  ix.bv.bbox = nullptr;
   ix.bv.pts = ix.pts.data();
   ix.bv.nodes = ix.nodes.data();
   ix.bv.m = m;
@@ -79,7 +77,41 @@ Index build(const std::vector<float>& xyz) {
   ix.bv.pad = 0;
   for (int L = 0; L < nl; ++L) make_leaf(ix.bv, ix.nodes.data(), L);
   for (int k = nl - 1; k >= 1; --k) make_internal(ix.nodes.data(), k);
+  ix.adj.resize((size_t)nl * kAdjK * 2);
+  ix.reach.resize(nl);
+  if (m > 0)
+    for (int L = 0; L < nl; ++L) {
+      BestK<kAdjK + 1> r;
+      r.init();
+      leaf_knn(ix.bv, L, r);
+      adj_store(ix.bv, r, L, ix.adj.data(), ix.reach.data());
+    }
+  ix.av.ent = ix.adj.data();
+  ix.av.reach = ix.reach.data();
   return ix;
+}
+
+// leaf_knn against brute force over all leaf boxes
+void check_adjacency(const Index& ix) {
+  const int nl = ix.bv.nleaves;
+  if (ix.bv.m <= 0) return;
+  for (int L = 0; L < nl; L += std::max(1, nl / 64)) {
+    std::vector<float> d;
+    for (int X = 0; X < nl; ++X) {
+      const float b = bbd2(ix.nodes[2 * (nl + L)], ix.nodes[2 * (nl + L) + 1],
+                           ix.nodes[2 * (nl + X)], ix.nodes[2 * (nl + X) + 1]);
+      if (b < FLT_MAX) d.push_back(b);
+    }
+    std::sort(d.begin(), d.end());
+    bool ok = true;
+    for (int j = 0; j < kAdjK; ++j) {
+      const float4 a = ix.adj[((size_t)L * kAdjK + j) * 2];
+      const float want = j < (int)d.size() ? sqrtf(d[j]) : INFINITY;
+      ok &= a.w == want;
+    }
+    ok &= ix.reach[L] == (kAdjK < (int)d.size() ? sqrtf(d[kAdjK]) : INFINITY);
+    check(ok, "adjacency", ix.bv.m, L);
+  }
 }
 
 template <int K>
@@ -93,6 +125,7 @@ void brute(const std::vector<float>& xyz, float qx, float qy, float qz, BestK<K>
 
 int g_fail = 0;
 long g_checks = 0;
+long g_covered = 0, g_adj_tries = 0;
 
 void check(bool ok, const char* what, int m, int q) {
   ++g_checks;
@@ -126,6 +159,7 @@ void run_case(std::mt19937_64& rng, int m, int nq, int mode) {
     xyz[4] = INFINITY;
   }
   const Index ix = build(xyz);
+  check_adjacency(ix);
   std::uniform_int_distribution<int> P(0, std::max(m - 1, 0));
   for (int q = 0; q < nq; ++q) {
     float qx, qy, qz;
@@ -160,6 +194,19 @@ void run_case(std::mt19937_64& rng, int m, int nq, int mode) {
       check(s.d == b1.d[0] && (s.pos < 0 ? b1.pos[0] < 0 : s.id == b1.id[0]), "nn warm", m, q);
       if (s.pos >= 0) check(f2i(ix.pts[s.pos].w) == s.id, "nn pos", m, q);
     }
+    // adjacency search from a warm candidate near the answer
+    if (m > 0 && finite3(qx, qy, qz)) {
+      const int start = b1.pos[0] >= 0 && (q & 1) ? pos_of(ix, b1.id[0]) : P(rng);
+      Best1 s;
+      s.init();
+      const float4 p = ix.pts[start];
+      s.offer(d2_ref(qx, qy, qz, p.x, p.y, p.z), f2i(p.w), start);
+      ++g_adj_tries;
+      if (adj_search(ix.bv, ix.av, start, qx, qy, qz, s)) {
+        ++g_covered;
+        check(s.d == b1.d[0] && (s.pos < 0 ? b1.pos[0] < 0 : s.id == b1.id[0]), "adj", m, q);
+      }
+    }
     // k = 4, bottom-up from a random leaf
     if (m > 0) {
       BestK<4> k4;
@@ -180,6 +227,7 @@ int main(int argc, char** argv) {
   const int sizes[] = {0, 1, 2, 3, 7, 16, 17, 33, 100, 257, 1000, 4099, 20000};
   for (int m : sizes)
     for (int mode = 0; mode < 4; ++mode) run_case(rng, m, m >= 4099 ? 300 : 120, mode);
-  printf("bvh_selftest: %ld checks, %d failures\n", g_checks, g_fail);
+  printf("bvh_selftest: %ld checks, %d failures (adjacency covered %ld of %ld warm queries)\n",
+         g_checks, g_fail, g_covered, g_adj_tries);
   return g_fail == 0 ? 0 : 1;
 }
