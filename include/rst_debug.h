@@ -19,8 +19,9 @@ int rst_debug_query_nn_warm_stats(rst_ctx* ctx, const rst_target* tgt, const flo
                                   int64_t nq, const int32_t* warm, int32_t* idx, float* d2,
                                   int32_t* stats);
 
-/* Fallback-queue length (queries the leaf adjacency could not certify) of
- * each iteration of the last align call on ctx (first n <= 256). */
+/* Per iteration of the last align call on ctx (first n <= 256), 5 int32:
+ * fallback-queue length (queries no adjacency level certified), then the
+ * lanes certified at level 1 without / after a walk, at level 2, level 3. */
 int rst_debug_queue_trace(rst_ctx* ctx, int32_t* out, int32_t n);
 
 #ifdef __cplusplus

@@ -112,29 +112,83 @@ __global__ __launch_bounds__(kBS) void k_rs_hist(const uint32_t* __restrict__ ke
   hist[(int64_t)threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
 }
 
-// Exclusive scan of `total` u32 in place by one 1024-thread block.
-__global__ __launch_bounds__(1024) void k_scan_single(uint32_t* __restrict__ a,
-                                                      int64_t total) {
-  __shared__ uint32_t s[1024];
-  const int64_t per = (total + 1023) / 1024;
-  const int64_t b = threadIdx.x * per;
-  const int64_t e = b + per < total ? b + per : total;
-  uint32_t sum = 0;
-  for (int64_t i = b; i < e; ++i) sum += a[i];
-  s[threadIdx.x] = sum;
+// ---- device-wide int32 scans (add or max; inclusive or exclusive) ----------------
+// Three launches: per-tile scan (1024 items, 4 per thread) + tile totals;
+// one block scans the totals (any count, 256 at a time with a carry); every
+// tile then folds in its prefix.
+constexpr int kScanItems = 4;
+constexpr int kScanTile = kBS * kScanItems;
+
+template <bool Max>
+__device__ __forceinline__ int32_t sop(int32_t a, int32_t b) {
+  return Max ? (a > b ? a : b) : a + b;
+}
+
+template <bool Max, bool Excl>
+__global__ __launch_bounds__(kBS) void k_scan_tile(const int32_t* __restrict__ in,
+                                                   int32_t* __restrict__ out, int64_t n,
+                                                   int32_t* __restrict__ tot) {
+  __shared__ int32_t sh[kBS];
+  const int32_t ident = Max ? INT32_MIN : 0;
+  const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
+  int32_t v[kScanItems];
+  int32_t acc = ident;
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) {
+    v[k] = base + k < n ? in[base + k] : ident;
+    acc = sop<Max>(acc, v[k]);
+  }
+  sh[threadIdx.x] = acc;
   __syncthreads();
-  for (int off = 1; off < 1024; off <<= 1) {
-    uint32_t v = threadIdx.x >= off ? s[threadIdx.x - off] : 0u;
+  for (int off = 1; off < kBS; off <<= 1) {
+    const int32_t o = threadIdx.x >= off ? sh[threadIdx.x - off] : ident;
     __syncthreads();
-    s[threadIdx.x] += v;
+    sh[threadIdx.x] = sop<Max>(sh[threadIdx.x], o);
     __syncthreads();
   }
-  uint32_t run = s[threadIdx.x] - sum;  // exclusive prefix of this chunk
-  for (int64_t i = b; i < e; ++i) {
-    const uint32_t v = a[i];
-    a[i] = run;
-    run += v;
+  int32_t run = threadIdx.x > 0 ? sh[threadIdx.x - 1] : ident;
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) {
+    const int32_t before = run;
+    run = sop<Max>(run, v[k]);
+    if (base + k < n) out[base + k] = Excl ? before : run;
   }
+  if (threadIdx.x == kBS - 1) tot[blockIdx.x] = sh[kBS - 1];
+}
+
+// exclusive prefix of the tile totals, in place
+template <bool Max>
+__global__ __launch_bounds__(kBS) void k_scan_top(int32_t* __restrict__ tot, int ntiles) {
+  __shared__ int32_t sh[kBS];
+  const int32_t ident = Max ? INT32_MIN : 0;
+  int32_t carry = ident;
+  for (int c = 0; c < ntiles; c += kBS) {
+    const int i = c + threadIdx.x;
+    const int32_t x = i < ntiles ? tot[i] : ident;
+    sh[threadIdx.x] = x;
+    __syncthreads();
+    for (int off = 1; off < kBS; off <<= 1) {
+      const int32_t o = threadIdx.x >= off ? sh[threadIdx.x - off] : ident;
+      __syncthreads();
+      sh[threadIdx.x] = sop<Max>(sh[threadIdx.x], o);
+      __syncthreads();
+    }
+    const int32_t excl = threadIdx.x > 0 ? sh[threadIdx.x - 1] : ident;
+    if (i < ntiles) tot[i] = sop<Max>(carry, excl);
+    carry = sop<Max>(carry, sh[kBS - 1]);
+    __syncthreads();
+  }
+}
+
+template <bool Max>
+__global__ __launch_bounds__(kBS) void k_scan_fix(int32_t* __restrict__ out, int64_t n,
+                                                  const int32_t* __restrict__ tot) {
+  if (blockIdx.x == 0) return;
+  const int32_t p = tot[blockIdx.x];
+  const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k)
+    if (base + k < n) out[base + k] = sop<Max>(p, out[base + k]);
 }
 
 __global__ __launch_bounds__(kBS) void k_rs_scatter(
@@ -223,12 +277,47 @@ __global__ __launch_bounds__(kBS) void k_leaf_boxes(BvhView bv, float4* __restri
   if (L < bv.nleaves) make_leaf(bv, nodes, L);
 }
 
+// ---- compact leaves (rst_bvh.hpp leaf_cut) ---------------------------------------
+// seg[i] = i where i starts a block of the code grid, else -1 (then a max
+// scan turns it into each point's block start)
+__global__ __launch_bounds__(kBS) void k_leaf_seg(const uint32_t* __restrict__ codes, int64_t m,
+                                                  int32_t* __restrict__ seg) {
+  const int64_t i = blockIdx.x * (int64_t)kBS + threadIdx.x;
+  if (i >= m) return;
+  seg[i] = (i == 0 || (codes[i] >> kLeafCellShift) != (codes[i - 1] >> kLeafCellShift)) ? (int)i
+                                                                                         : -1;
+}
+
+__global__ __launch_bounds__(kBS) void k_leaf_cutflag(const uint32_t* __restrict__ codes,
+                                                      const int32_t* __restrict__ seg, int64_t m,
+                                                      int32_t* __restrict__ cut) {
+  const int64_t i = blockIdx.x * (int64_t)kBS + threadIdx.x;
+  if (i >= m) return;
+  cut[i] = leaf_cut(codes, (int)i, seg[i]) ? 1 : 0;
+}
+
+// pleaf = inclusive count of cuts - 1; the cut positions are the leaf starts
+__global__ __launch_bounds__(kBS) void k_leaf_start(int32_t* __restrict__ pleaf, int64_t m,
+                                                    int32_t* __restrict__ lstart) {
+  const int64_t i = blockIdx.x * (int64_t)kBS + threadIdx.x;
+  if (i >= m) return;
+  const int32_t c = pleaf[i];
+  if (i == 0 || pleaf[i - 1] != c) lstart[c - 1] = (int32_t)i;
+  pleaf[i] = c - 1;
+}
+
+__global__ __launch_bounds__(kBS) void k_leaf_tail(int32_t* __restrict__ lstart, int nl0, int nl,
+                                                   int32_t m) {
+  const int L = nl0 + blockIdx.x * kBS + threadIdx.x;
+  if (L <= nl) lstart[L] = m;
+}
+
 // leaf adjacency (the tracking index, rst_bvh.hpp): one wavefront per leaf
-__global__ __launch_bounds__(kBS) void k_leaf_adj(BvhView bv, float4* __restrict__ ent,
+__global__ __launch_bounds__(kBS) void k_leaf_adj(BvhView bv, int first, float4* __restrict__ ent,
                                                   float* __restrict__ reach) {
   __shared__ WnnScratch wsc[kBS / kWave];
   const int L = blockIdx.x * (kBS / kWave) + threadIdx.x / kWave;
-  if (L < bv.nleaves) leaf_adj_wave(bv, L, ent, reach, wsc[threadIdx.x / kWave]);
+  if (L < first) leaf_adj_wave(bv, first, L, ent, reach, wsc[threadIdx.x / kWave]);
 }
 
 __global__ __launch_bounds__(kBS) void k_level(float4* __restrict__ nodes, int lo_k,
@@ -252,8 +341,16 @@ inline int blocks_for(int64_t n, int per = kBS) {
 
 }  // namespace
 
+template <bool Max, bool Excl>
+void scan_i32(hipStream_t st, const int32_t* in, int32_t* out, int64_t n, int32_t* tot) {
+  const int nt = (int)std::max<int64_t>(1, (n + kScanTile - 1) / kScanTile);
+  k_scan_tile<Max, Excl><<<nt, kBS, 0, st>>>(in, out, n, tot);
+  k_scan_top<Max><<<1, kBS, 0, st>>>(tot, nt);
+  k_scan_fix<Max><<<nt, kBS, 0, st>>>(out, n, tot);
+}
+
 int radix_sort_pairs(rst_ctx* ctx, uint32_t* keys, uint32_t* vals, uint32_t* ktmp,
-                     uint32_t* vtmp, uint32_t* hist, int64_t n) {
+                     uint32_t* vtmp, uint32_t* hist, int32_t* stot, int64_t n) {
   hipStream_t st = ctx->stream;
   const int nb = blocks_for(n, kRsTile);
   const int shifts[4] = {0, 8, 16, 24};
@@ -261,7 +358,7 @@ int radix_sort_pairs(rst_ctx* ctx, uint32_t* keys, uint32_t* vals, uint32_t* ktm
   uint32_t *ka = keys, *va = vals, *kb = ktmp, *vb = vtmp;
   for (int p = 0; p < 4; ++p) {
     k_rs_hist<<<nb, kBS, 0, st>>>(ka, n, shifts[p], masks[p], nb, hist);
-    k_scan_single<<<1, 1024, 0, st>>>(hist, (int64_t)256 * nb);
+    scan_i32<false, true>(st, (const int32_t*)hist, (int32_t*)hist, (int64_t)256 * nb, stot);
     k_rs_scatter<<<nb, kBS, 0, st>>>(ka, va, kb, vb, n, shifts[p], masks[p], nb, hist);
     std::swap(ka, kb);
     std::swap(va, vb);
@@ -273,6 +370,10 @@ int radix_sort_pairs(rst_ctx* ctx, uint32_t* keys, uint32_t* vals, uint32_t* ktm
 AdjView adj_of(const rst_target* t) {
   AdjView a;
   a.ent = t->adj;
+  a.ent2 = t->adj2;
+  a.reach2 = t->reach2;
+  a.ent3 = t->adj3;
+  a.reach3 = t->reach3;
   a.reach = t->reach;
   return a;
 }
@@ -286,6 +387,8 @@ BvhView view_of(const rst_target* t) {
   BvhView v;
   v.pts = t->pts;
   v.nodes = t->nodes;
+  v.lstart = t->lstart;
+  v.pleaf = t->pleaf;
   v.codes = t->codes;
   v.bbox = t->codes ? (const float*)(t->codes + std::max<int64_t>(t->m, 1)) : nullptr;
   v.m = (int32_t)t->m;
@@ -298,42 +401,72 @@ BvhView view_of(const rst_target* t) {
 int target_build_device(rst_ctx* ctx, const float* d_xyz, int64_t m, bool with_bvh,
                         rst_target** out) {
   if (!ctx || !out || m < 0 || (m > 0 && !d_xyz)) return RST_E_ARG;
-  if (m >= (int64_t)1 << 31) return RST_E_ARG;
+  // leaf-range tags of the adjacency pack begin * 32 (rst_bvh.hpp leaf_tag)
+  if (m >= (int64_t)1 << 26) return RST_E_ARG;
   rst_target* t = new rst_target();
   t->ctx = ctx;
   t->m = m;
   hipStream_t st = ctx->stream;
-  int64_t nl = 1;
-  int lg = 0;
-  while (nl * kLeafTarget < m) {
-    nl <<= 1;
-    ++lg;
-  }
-  t->nleaves = (int32_t)nl;
-  t->lg = lg;
   const int64_t mp = std::max<int64_t>(m, 1);
   if (hipMalloc(&t->pts, sizeof(float4) * mp) != hipSuccess ||
       hipMalloc(&t->inv, sizeof(int32_t) * mp) != hipSuccess ||
+      hipMalloc(&t->pleaf, sizeof(int32_t) * mp) != hipSuccess ||
       hipMalloc(&t->codes, sizeof(uint32_t) * mp + sizeof(float) * 8) != hipSuccess) {
-    if (t->pts) hipFree(t->pts);
-    if (t->inv) hipFree(t->inv);
-    delete t;
+    rst_target_free(t);
     return RST_E_NOMEM;
   }
-  if (with_bvh) {
-    if (hipMalloc(&t->nodes, sizeof(float4) * 4 * nl) != hipSuccess ||
-        hipMalloc(&t->adj, sizeof(float4) * 2 * kAdjK * nl) != hipSuccess ||
-        hipMalloc(&t->reach, sizeof(float) * nl) != hipSuccess) {
-      rst_target_free(t);
-      return RST_E_NOMEM;
+  // leaves: how many is known only after the sort (an empty cloud: one
+  // empty leaf)
+  auto alloc_tree = [&](int64_t NL) -> int {
+    int64_t nl = 1;
+    int lg = 0;
+    while (nl < NL) {
+      nl <<= 1;
+      ++lg;
     }
+    t->nleaves = (int32_t)nl;
+    t->lg = lg;
+    if (hipMalloc(&t->nodes, sizeof(float4) * 4 * nl) != hipSuccess ||
+        hipMalloc(&t->lstart, sizeof(int32_t) * (nl + 1)) != hipSuccess ||
+        hipMalloc(&t->adj, sizeof(float4) * 2 * kAdjK * nl) != hipSuccess ||
+        hipMalloc(&t->reach, sizeof(float) * nl) != hipSuccess ||
+        hipMalloc(&t->adj2, sizeof(float4) * 2 * kAdjK * std::max<int64_t>(nl >> kAdj2Shift, 1)) !=
+            hipSuccess ||
+        hipMalloc(&t->reach2, sizeof(float) * std::max<int64_t>(nl >> kAdj2Shift, 1)) !=
+            hipSuccess)
+      return RST_E_NOMEM;
+    if (hipMalloc(&t->adj3, sizeof(float4) * 2 * kAdjK * std::max<int64_t>(nl >> kAdj3Shift, 1)) !=
+            hipSuccess ||
+        hipMalloc(&t->reach3, sizeof(float) * std::max<int64_t>(nl >> kAdj3Shift, 1)) !=
+            hipSuccess)
+      return RST_E_NOMEM;
+    if (nl < (1 << kAdj2Shift) && hipMemsetAsync(t->reach2, 0, sizeof(float), st) != hipSuccess)
+      return RST_E_HIP;
+    if (nl < (1 << kAdj3Shift) && hipMemsetAsync(t->reach3, 0, sizeof(float), st) != hipSuccess)
+      return RST_E_HIP;
     t->has_bvh = true;
-  }
+    return RST_OK;
+  };
   if (m == 0) {
+    int s = with_bvh ? alloc_tree(1) : RST_OK;
+    if (s >= 0 && with_bvh) {
+      // one empty leaf: lstart = {0, 0}, empty box, no adjacency
+      const float4 e[2] = {make_float4(INFINITY, INFINITY, INFINITY, 0.f),
+                           make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f)};
+      const int32_t z[2] = {0, 0};
+      if (hipMemcpyAsync(t->nodes + 2, e, sizeof(e), hipMemcpyHostToDevice, st) != hipSuccess ||
+          hipMemcpyAsync(t->lstart, z, sizeof(z), hipMemcpyHostToDevice, st) != hipSuccess ||
+          hipStreamSynchronize(st) != hipSuccess)
+        s = RST_E_HIP;
+    }
+    if (s < 0) {
+      rst_target_free(t);
+      return s;
+    }
     *out = t;
     return RST_OK;
   }
-  // workspace: bbox partials | bbox | keys | vals | ktmp | vtmp | hist
+  // workspace: bbox partials | bbox | keys | vals | ktmp | vtmp | hist | scan tiles
   const int nbb = std::min(1024, blocks_for(m));
   const int nb = blocks_for(m, kRsTile);
   size_t off = 0;
@@ -349,6 +482,7 @@ int target_build_device(rst_ctx* ctx, const float* d_xyz, int64_t m, bool with_b
   const size_t o_kt = carve(sizeof(uint32_t) * m);
   const size_t o_vt = carve(sizeof(uint32_t) * m);
   const size_t o_h = carve(sizeof(uint32_t) * 256 * (size_t)nb);
+  const size_t o_tot = carve(sizeof(int32_t) * (256 * (size_t)nb / kScanTile + m / kScanTile + 64));
   void* ws = nullptr;
   int s = ctx_workspace(ctx, off, &ws);
   if (s < 0) {
@@ -360,11 +494,12 @@ int target_build_device(rst_ctx* ctx, const float* d_xyz, int64_t m, bool with_b
   float* bbox = (float*)(w + o_bbox);
   uint32_t* keys = (uint32_t*)(w + o_k);
   uint32_t* vals = (uint32_t*)(w + o_v);
+  int32_t* tot = (int32_t*)(w + o_tot);
   k_bbox_partial<<<nbb, kBS, 0, st>>>(d_xyz, m, part);
   k_bbox_final<<<1, kBS, 0, st>>>(part, nbb, bbox);
   k_morton<<<blocks_for(m), kBS, 0, st>>>(d_xyz, m, bbox, keys, vals);
   s = radix_sort_pairs(ctx, keys, vals, (uint32_t*)(w + o_kt), (uint32_t*)(w + o_vt),
-                       (uint32_t*)(w + o_h), m);
+                       (uint32_t*)(w + o_h), tot, m);
   if (s < 0) {
     rst_target_free(t);
     return s;
@@ -380,7 +515,28 @@ int target_build_device(rst_ctx* ctx, const float* d_xyz, int64_t m, bool with_b
   k_gather<<<blocks_for(m), kBS, 0, st>>>(d_xyz, vals, m, t->pts);
   k_find_pos0<<<blocks_for(m), kBS, 0, st>>>(vals, m, (int32_t*)(bbox + 6));
   k_inverse<<<blocks_for(m), kBS, 0, st>>>(vals, m, t->inv);
+  int32_t NL = 0;
   if (with_bvh) {
+    // compact leaves: block starts (max scan), cut flags, leaf ids (add scan)
+    int32_t* seg = (int32_t*)(w + o_kt);
+    k_leaf_seg<<<blocks_for(m), kBS, 0, st>>>(t->codes, m, seg);
+    scan_i32<true, false>(st, seg, seg, m, tot);
+    k_leaf_cutflag<<<blocks_for(m), kBS, 0, st>>>(t->codes, seg, m, t->pleaf);
+    scan_i32<false, false>(st, t->pleaf, t->pleaf, m, tot);
+    if (hipMemcpyAsync(&NL, t->pleaf + (m - 1), sizeof(int32_t), hipMemcpyDeviceToHost, st) !=
+            hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess) {
+      rst_target_free(t);
+      return RST_E_HIP;
+    }
+    s = alloc_tree(std::max<int32_t>(NL, 1));
+    if (s < 0) {
+      rst_target_free(t);
+      return s;
+    }
+    const int nl = t->nleaves;
+    k_leaf_start<<<blocks_for(m), kBS, 0, st>>>(t->pleaf, m, t->lstart);
+    k_leaf_tail<<<blocks_for(nl + 1 - NL), kBS, 0, st>>>(t->lstart, NL, nl, (int32_t)m);
     k_leaf_boxes<<<blocks_for(nl), kBS, 0, st>>>(view_of(t), t->nodes);
     int64_t cnt = nl / 2;
     while (cnt >= 2 * kBS) {
@@ -388,7 +544,13 @@ int target_build_device(rst_ctx* ctx, const float* d_xyz, int64_t m, bool with_b
       cnt >>= 1;
     }
     if (cnt >= 1) k_levels_top<<<1, kBS, 0, st>>>(t->nodes, (int)cnt);
-    k_leaf_adj<<<blocks_for(nl, kBS / kWave), kBS, 0, st>>>(view_of(t), t->adj, t->reach);
+    k_leaf_adj<<<blocks_for(nl, kBS / kWave), kBS, 0, st>>>(view_of(t), nl, t->adj, t->reach);
+    if (nl >= (1 << kAdj2Shift))
+      k_leaf_adj<<<blocks_for(nl >> kAdj2Shift, kBS / kWave), kBS, 0, st>>>(
+          view_of(t), nl >> kAdj2Shift, t->adj2, t->reach2);
+    if (nl >= (1 << kAdj3Shift))
+      k_leaf_adj<<<blocks_for(nl >> kAdj3Shift, kBS / kWave), kBS, 0, st>>>(
+          view_of(t), nl >> kAdj3Shift, t->adj3, t->reach3);
   }
   if (hipGetLastError() != hipSuccess ||
       hipMemcpyAsync(t->bbox, bbox, sizeof(float) * 6, hipMemcpyDeviceToHost, st) != hipSuccess ||

@@ -227,8 +227,14 @@ int rst_target_free(rst_target* t) {
   if (t->nrm) hipFree(t->nrm);
   if (t->inv) hipFree(t->inv);
   if (t->codes) hipFree(t->codes);
+  if (t->lstart) hipFree(t->lstart);
+  if (t->pleaf) hipFree(t->pleaf);
   if (t->adj) hipFree(t->adj);
   if (t->reach) hipFree(t->reach);
+  if (t->adj2) hipFree(t->adj2);
+  if (t->reach2) hipFree(t->reach2);
+  if (t->adj3) hipFree(t->adj3);
+  if (t->reach3) hipFree(t->reach3);
   delete t;
   return RST_OK;
 }
@@ -348,7 +354,10 @@ int rst_debug_query_nn_warm_stats(rst_ctx* ctx, const rst_target* t, const float
 
 int rst_debug_queue_trace(rst_ctx* ctx, int32_t* out, int32_t n) {
   if (!ctx || !out || n < 0) return RST_E_ARG;
-  for (int i = 0; i < n && i < kQTrace; ++i) out[i] = ctx->h_state->qlen[i];
+  for (int i = 0; i < n && i < kQTrace; ++i) {
+    out[5 * i] = ctx->h_state->qlen[i];
+    for (int j = 0; j < 4; ++j) out[5 * i + 1 + j] = ctx->h_state->path[i][j];
+  }
   return RST_OK;
 }
 

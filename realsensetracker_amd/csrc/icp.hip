@@ -30,7 +30,8 @@ namespace {
 constexpr int kBS = 256;
 constexpr int kNP2Point = 16;  // sum w q u^T (9), sum w u (3), sum q (3), sum d2
 constexpr int kNP2Plane = 30;  // A (21), b (6), sum w r^2, count, sum d2
-constexpr int kFbBlocks = 512;  // fixed grid of the fallback kernel (2048 waves)
+constexpr int kFbBlocks = 2048;  // fixed grid of the fallback kernel (8192 waves)
+constexpr bool kL2InNn = false;  // kernel 1 also tries the level-2 adjacency
 
 __device__ __forceinline__ Pose3 load_pose(const IcpState* __restrict__ st) {
   Pose3 P;
@@ -59,41 +60,49 @@ __global__ __launch_bounds__(kBS) void k_centroid_partial(const float4* __restri
 }
 
 // Reduce slab rows (rows1 of slab1, then rows2 of slab2; NV doubles each)
-// into out[NV], in a fixed order.
+// into out[NV] in a fixed order (bitwise reproducible): each thread sums a
+// strided set of rows, then wave shuffles and one LDS pass.  When fb_e is
+// given, slab2 holds rows only for the first ceil(*fb_e / waves-per-block)
+// fallback blocks (the others had no queue entries).
+constexpr int kRedBS = 1024;
 template <int NV>
 __device__ __forceinline__ void reduce_slab_rows(const double* __restrict__ slab1, int rows1,
                                                  const double* __restrict__ slab2, int rows2,
-                                                 double* __restrict__ red /*[NV][kBS]*/,
+                                                 const int32_t* __restrict__ fb_e,
+                                                 double* __restrict__ red /*[kRedBS/64][NV]*/,
                                                  double* __restrict__ out) {
+  if (fb_e) rows2 = min(rows2, (*fb_e + kBS / kWave - 1) / (kBS / kWave));
   double acc[NV];
 #pragma unroll
   for (int k = 0; k < NV; ++k) acc[k] = 0.0;
-  for (int b = threadIdx.x; b < rows1 + rows2; b += kBS) {
+  for (int b = threadIdx.x; b < rows1 + rows2; b += blockDim.x) {
     const double* row = b < rows1 ? slab1 + (int64_t)b * NV : slab2 + (int64_t)(b - rows1) * NV;
 #pragma unroll
     for (int k = 0; k < NV; ++k) acc[k] += row[k];
   }
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
 #pragma unroll
-  for (int k = 0; k < NV; ++k) red[k * kBS + threadIdx.x] = acc[k];
-  __syncthreads();
-  for (int s = kBS / 2; s > 0; s >>= 1) {
-    if (threadIdx.x < s) {
+  for (int k = 0; k < NV; ++k) acc[k] = wave_sum(acc[k]);
+  if (lane == 0) {
 #pragma unroll
-      for (int k = 0; k < NV; ++k)
-        red[k * kBS + threadIdx.x] += red[k * kBS + threadIdx.x + s];
-    }
-    __syncthreads();
+    for (int k = 0; k < NV; ++k) red[wid * NV + k] = acc[k];
   }
-  if (threadIdx.x < NV) out[threadIdx.x] = red[threadIdx.x * kBS];
+  __syncthreads();
+  if (threadIdx.x < NV) {
+    double t = 0.0;
+    for (int w = 0; w < (int)blockDim.x / kWave; ++w) t += red[w * NV + threadIdx.x];
+    out[threadIdx.x] = t;
+  }
   __syncthreads();
 }
 
 template <int NV>
-__global__ __launch_bounds__(kBS) void k_slab_reduce(const double* __restrict__ slab1, int rows1,
-                                                     const double* __restrict__ slab2, int rows2,
-                                                     double* __restrict__ out) {
-  __shared__ double red[NV * kBS];
-  reduce_slab_rows<NV>(slab1, rows1, slab2, rows2, red, out);
+__global__ __launch_bounds__(kRedBS) void k_slab_reduce(const double* __restrict__ slab1, int rows1,
+                                                        const double* __restrict__ slab2, int rows2,
+                                                        const int32_t* __restrict__ fb_e,
+                                                        double* __restrict__ out) {
+  __shared__ double red[(kRedBS / kWave) * NV];
+  reduce_slab_rows<NV>(slab1, rows1, slab2, rows2, fb_e, red, out);
 }
 
 struct InitArgs {
@@ -107,9 +116,9 @@ struct InitArgs {
 // point_cloud_utils.cpp:92-98; DESIGN.md "Numerics").
 __global__ __launch_bounds__(kBS) void k_init_state(const double* __restrict__ cslab, int rows,
                                                     InitArgs a, IcpState* __restrict__ st) {
-  __shared__ double red[4 * kBS];
+  __shared__ double red[(kBS / kWave) * 4];
   __shared__ double tot[4];
-  if (a.need_centroid) reduce_slab_rows<4>(cslab, rows, cslab, 0, red, tot);
+  if (a.need_centroid) reduce_slab_rows<4>(cslab, rows, cslab, 0, nullptr, red, tot);
   if (threadIdx.x == 0) {
     for (int c = 0; c < 3; ++c)
       for (int r = 0; r < 3; ++r) {
@@ -128,6 +137,10 @@ __global__ __launch_bounds__(kBS) void k_init_state(const double* __restrict__ c
     }
     st->mu = a.mu0;
     st->iter = 0;
+    for (int k = 0; k < kQTrace; ++k) {
+      st->qlen[k] = 0;
+      for (int j = 0; j < 4; ++j) st->path[k][j] = 0;
+    }
     st->done = 0;
     st->fail = 0;
     st->last_cost = 0.f;
@@ -254,7 +267,8 @@ __global__ __launch_bounds__(kBS) void k_icp_nn(BvhView bv, AdjView av, AccArgs 
     const float4 w = bv.pts[warm];
     r.offer(d2_ref(px, py, pz, w.x, w.y, w.z), f2i(w.w), warm);
   }
-  const bool done = act && (!fin || adj_search_wide(bv, av, warm, px, py, pz, r));
+  bool done = act && (!fin || adj_search_wide(bv, av, warm, px, py, pz, r));
+  if (kL2InNn && act && !done) done = adj2_search(bv, av, r.pos >= 0 ? r.pos : warm, px, py, pz, r);
   // lanes the adjacency could not certify go to the fallback queue, in
   // point order within the block's segment
   const bool need = act && !done;
@@ -324,7 +338,10 @@ __global__ __launch_bounds__(kBS) void k_icp_fb(BvhView bv, AccArgs aa,
   }
   __syncthreads();
   const int E = pref[nb1];
-  if (blockIdx.x == 0 && threadIdx.x == 0 && st->iter < kQTrace) st->qlen[st->iter] = E;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    st->fb_e = E;  // the solve reads only the slab rows of blocks with entries
+    if (st->iter < kQTrace) st->qlen[st->iter] = E;
+  }
   const Uni u = load_uni(st);
   const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
   const int W = gridDim.x * (kBS / kWave);
@@ -363,16 +380,22 @@ __global__ __launch_bounds__(kBS) void k_icp_fb(BvhView bv, AccArgs aa,
 // R = float(U V^T), reflection fix, t = dmean - R smean, quaternion trip.
 __device__ void kabsch_solve(const double* cov, const float* smean, const float* dmean,
                              float* Rq, float* t) {
-  double U[9], S[3], V[9];
-  svd3_jacobi(cov, U, S, V);
+  // R = U V^T: the polar factor (cheap, nonsingular cov), else Jacobi SVD
+  double P[9];
   float R[9];
-  for (int r = 0; r < 3; ++r)
-    for (int c = 0; c < 3; ++c) {
-      const double a0 = RST_M3(U, r, 0) * RST_M3(V, c, 0);
-      const double a1 = RST_M3(U, r, 1) * RST_M3(V, c, 1);
-      const double a2 = RST_M3(U, r, 2) * RST_M3(V, c, 2);
-      RST_M3(R, r, c) = (float)(a0 + (a1 + a2));
-    }
+  if (polar3(cov, P)) {
+    for (int k = 0; k < 9; ++k) R[k] = (float)P[k];
+  } else {
+    double U[9], S[3], V[9];
+    svd3_jacobi(cov, U, S, V);
+    for (int r = 0; r < 3; ++r)
+      for (int c = 0; c < 3; ++c) {
+        const double a0 = RST_M3(U, r, 0) * RST_M3(V, c, 0);
+        const double a1 = RST_M3(U, r, 1) * RST_M3(V, c, 1);
+        const double a2 = RST_M3(U, r, 2) * RST_M3(V, c, 2);
+        RST_M3(R, r, c) = (float)(a0 + (a1 + a2));
+      }
+  }
   if (det3f(R) < 0) {  // :143-145 (non-standard fix kept on purpose)
     for (int r = 0; r < 3; ++r) RST_M3(R, r, 2) *= -1.0f;
   }
@@ -428,13 +451,15 @@ __device__ void p2point_update(const double* tot, const IcpParams& prm, IcpState
   if (next > 0 && prm.anneal_every > 0 && next % prm.anneal_every == 0) st->mu = st->mu / prm.anneal_div;
 }
 
-__global__ __launch_bounds__(kBS) void k_solve_p2point(const double* __restrict__ slab1, int rows1,
-                                                       const double* __restrict__ slab2, int rows2,
-                                                       IcpParams prm, IcpState* __restrict__ st,
-                                                       float* __restrict__ trace) {
-  __shared__ double red[kNP2Point * kBS];
+__global__ __launch_bounds__(kRedBS) void k_solve_p2point(const double* __restrict__ slab1,
+                                                          int rows1,
+                                                          const double* __restrict__ slab2,
+                                                          int rows2, IcpParams prm,
+                                                          IcpState* __restrict__ st,
+                                                          float* __restrict__ trace) {
+  __shared__ double red[(kRedBS / kWave) * kNP2Point];
   __shared__ double tot[kNP2Point];
-  reduce_slab_rows<kNP2Point>(slab1, rows1, slab2, rows2, red, tot);
+  reduce_slab_rows<kNP2Point>(slab1, rows1, slab2, rows2, &st->fb_e, red, tot);
   if (threadIdx.x == 0) p2point_update(tot, prm, st, trace);
 }
 
@@ -545,14 +570,16 @@ __device__ void p2plane_update(const double* tot, const IcpParams& prm, IcpState
   if (nx < (double)prm.p2plane_eps) st->done = 1;
 }
 
-__global__ __launch_bounds__(kBS) void k_solve_p2plane(const double* __restrict__ slab1, int rows1,
-                                                       const double* __restrict__ slab2, int rows2,
-                                                       IcpParams prm, IcpState* __restrict__ st,
-                                                       float* __restrict__ trace) {
-  __shared__ double red[kNP2Plane * kBS];
+__global__ __launch_bounds__(kRedBS) void k_solve_p2plane(const double* __restrict__ slab1,
+                                                          int rows1,
+                                                          const double* __restrict__ slab2,
+                                                          int rows2, IcpParams prm,
+                                                          IcpState* __restrict__ st,
+                                                          float* __restrict__ trace) {
+  __shared__ double red[(kRedBS / kWave) * kNP2Plane];
   __shared__ double tot[kNP2Plane];
   if (st->done) return;
-  reduce_slab_rows<kNP2Plane>(slab1, rows1, slab2, rows2, red, tot);
+  reduce_slab_rows<kNP2Plane>(slab1, rows1, slab2, rows2, &st->fb_e, red, tot);
   if (threadIdx.x == 0) p2plane_update(tot, prm, st, trace);
 }
 
@@ -639,7 +666,7 @@ int icp_align_prepared(rst_ctx* ctx, const rst_target* src, const rst_target* tg
       if (crows < 0) return crows;
     }
     if (comm) {
-      k_slab_reduce<4><<<1, kBS, 0, st>>>(slab, crows, slab, 0, totals);
+      k_slab_reduce<4><<<1, kRedBS, 0, st>>>(slab, crows, slab, 0, nullptr, totals);
       RST_CHECK(comm_allreduce_sum_f64(comm, totals, 4, st));
       k_init_state<<<1, kBS, 0, st>>>(totals, 1, ia, ctx->d_state);
     } else {
@@ -714,19 +741,19 @@ int icp_align_prepared(rst_ctx* ctx, const rst_target* src, const rst_target* tg
     const int rows2 = n_local > 0 ? kFbBlocks : 0;
     if (comm) {
       if (p2plane) {
-        k_slab_reduce<kNP2Plane><<<1, kBS, 0, st>>>(slab, rows, slab2, rows2, totals);
+        k_slab_reduce<kNP2Plane><<<1, kRedBS, 0, st>>>(slab, rows, slab2, rows2, &ctx->d_state->fb_e, totals);
         RST_CHECK(comm_allreduce_sum_f64(comm, totals, kNP2Plane, st));
-        k_solve_p2plane<<<1, kBS, 0, st>>>(totals, 1, totals, 0, prm, ctx->d_state, nullptr);
+        k_solve_p2plane<<<1, kRedBS, 0, st>>>(totals, 1, totals, 0, prm, ctx->d_state, nullptr);
       } else {
-        k_slab_reduce<kNP2Point><<<1, kBS, 0, st>>>(slab, rows, slab2, rows2, totals);
+        k_slab_reduce<kNP2Point><<<1, kRedBS, 0, st>>>(slab, rows, slab2, rows2, &ctx->d_state->fb_e, totals);
         RST_CHECK(comm_allreduce_sum_f64(comm, totals, kNP2Point, st));
-        k_solve_p2point<<<1, kBS, 0, st>>>(totals, 1, totals, 0, prm, ctx->d_state, nullptr);
+        k_solve_p2point<<<1, kRedBS, 0, st>>>(totals, 1, totals, 0, prm, ctx->d_state, nullptr);
       }
     } else {
       if (p2plane)
-        k_solve_p2plane<<<1, kBS, 0, st>>>(slab, rows, slab2, rows2, prm, ctx->d_state, nullptr);
+        k_solve_p2plane<<<1, kRedBS, 0, st>>>(slab, rows, slab2, rows2, prm, ctx->d_state, nullptr);
       else
-        k_solve_p2point<<<1, kBS, 0, st>>>(slab, rows, slab2, rows2, prm, ctx->d_state, nullptr);
+        k_solve_p2point<<<1, kRedBS, 0, st>>>(slab, rows, slab2, rows2, prm, ctx->d_state, nullptr);
     }
   }
   RST_HIP(hipGetLastError());

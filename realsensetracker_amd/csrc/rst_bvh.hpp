@@ -5,7 +5,11 @@
 // heap BVH over the Morton-sorted target points:
 //   root = node 1, children 2k / 2k+1, leaves = nodes [nl, 2nl), nl = 2^lg;
 //   node k = two float4: lo (x, y, z, split) and hi (x, y, z, axis bits);
-//   leaf L holds sorted points [L*m >> lg, (L+1)*m >> lg)  (8..16 points).
+//   leaf L holds sorted points [lstart[L], lstart[L+1]) (1..16 points;
+//   leaves past the last are empty).  Leaves are compact: the Morton order
+//   is cut wherever it leaves a 4x4x4-cell block of the code grid (the
+//   Z-curve jumps across space there on a 2.5D surface) and every run is
+//   chopped into <= 16-point pieces -- see leaf_cut().
 //
 // Every search here is EXACT: the result is the lexicographic minimum of
 // (d2, original index) over all points with d2 < FLT_MAX, where d2 is
@@ -71,6 +75,8 @@ struct BvhView {
   const float4* __restrict__ pts;    // [m] sorted points, .w = original index bits
   const float4* __restrict__ nodes;  // [2 * 2nl]
   const uint32_t* __restrict__ codes;  // [m] sorted Morton codes (may be null)
+  const int32_t* __restrict__ lstart;  // [nl + 1] first point of each leaf
+  const int32_t* __restrict__ pleaf;   // [m] leaf of each sorted point
   const float* __restrict__ bbox;    // [6] the codes' quantisation box (may be null)
   int32_t m;
   int32_t nleaves;
@@ -117,15 +123,17 @@ RST_HD int morton_seed(const BvhView& bv, float qx, float qy, float qz) {
   return lo < bv.m ? lo : bv.m - 1;
 }
 
-RST_HD int leaf_begin(const BvhView& bv, int L) { return (int)(((int64_t)L * bv.m) >> bv.lg); }
+RST_HD int leaf_begin(const BvhView& bv, int L) { return bv.lstart[L]; }
+RST_HD int leaf_of(const BvhView& bv, int p) { return bv.pleaf[p]; }
 
-// Leaf holding sorted position p: the largest L with leaf_begin(L) <= p.
-RST_HD int leaf_of(const BvhView& bv, int p) {
-  int L = (int)((((double)p + 1.0) * (double)bv.nleaves - 1.0) / (double)bv.m);
-  L = L < 0 ? 0 : (L >= bv.nleaves ? bv.nleaves - 1 : L);
-  while (L > 0 && leaf_begin(bv, L) > p) --L;
-  while (L + 1 < bv.nleaves && leaf_begin(bv, L + 1) <= p) ++L;
-  return L;
+// Leaf layout rule: a leaf starts at sorted position i when i begins a new
+// block of the code grid (code >> kLeafCellShift differs from i-1's) or
+// when kLeafTarget points of the current block have been taken.
+// seg = first position of i's block.
+constexpr int kLeafCellShift = 9;
+RST_HD bool leaf_cut(const uint32_t* codes, int i, int seg) {
+  return i == 0 || (codes[i] >> kLeafCellShift) != (codes[i - 1] >> kLeafCellShift) ||
+         ((i - seg) % kLeafTarget) == 0;
 }
 
 RST_HD int near_child(int k, const float4& lo, const float4& hi, float qx, float qy, float qz) {
@@ -251,6 +259,31 @@ RST_HD void search_from(const BvhView& bv, int start, float qx, float qy, float 
   }
 }
 
+// search_from with every ancestor's sibling box loaded up front (the loads
+// are independent, so one latency instead of one per level); only the
+// siblings whose box is within the bound -- usually a few low ones -- are
+// then walked.  Same result as search_from.
+constexpr int kMaxDepth = 28;
+template <class R>
+RST_HD void search_from_fast(const BvhView& bv, int start, float qx, float qy, float qz, R& res) {
+  const int nl = bv.nleaves;
+  const int leafnode = nl + leaf_of(bv, start);
+  scan_leaf(bv, leafnode - nl, qx, qy, qz, res);
+  const int depth = 31 - __builtin_clz((unsigned)leafnode);
+  float sb[kMaxDepth];
+#pragma unroll
+  for (int k = 0; k < kMaxDepth; ++k) {
+    sb[k] = FLT_MAX;
+    if (k < depth) {
+      const int sib = (leafnode >> k) ^ 1;
+      sb[k] = box_d2(qx, qy, qz, bv.nodes[2 * sib], bv.nodes[2 * sib + 1]);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kMaxDepth; ++k)
+    if (k < depth && sb[k] <= res.bound()) descend(bv, (leafnode >> k) ^ 1, qx, qy, qz, res);
+}
+
 // Exact search of the whole index: bottom-up from `warm` when given (>= 0),
 // else top-down from the root.  Non-finite queries find nothing.
 template <class R>
@@ -276,10 +309,22 @@ RST_HD void search(const BvhView& bv, int warm, float qx, float qy, float qz, R&
 // (entries are sorted, so no later box can touch the ball either).
 constexpr int kAdjK = 24;
 
+// The same index one level up (items = nodes of 2^kAdj2Shift leaves) gives
+// the far queries (frame borders, occlusions, early iterations) a reach
+// several times larger.
+// Level 3 (items = nodes of 2^kAdj3Shift leaves) covers what is left:
+// first iterations from a poor pose and the farthest outliers.
+constexpr int kAdj2Shift = 3;
+constexpr int kAdj3Shift = 6;
+
 struct AdjView {
   // [nl * kAdjK * 2]: entry = (lo.xyz, bbd) (hi.xyz, leaf index bits); leaf -1 = none
   const float4* __restrict__ ent;
-  const float* __restrict__ reach;  // [nl]
+  const float* __restrict__ reach;   // [nl]
+  const float4* __restrict__ ent2;   // [(nl >> kAdj2Shift) * kAdjK * 2]
+  const float* __restrict__ reach2;  // [nl >> kAdj2Shift] (0 when nl is too small)
+  const float4* __restrict__ ent3;   // [(nl >> kAdj3Shift) * kAdjK * 2]
+  const float* __restrict__ reach3;  // [nl >> kAdj3Shift] (0 when nl is too small)
 };
 
 // Box-to-box distance squared (0 when they overlap; +inf when either box
@@ -294,19 +339,37 @@ RST_HD float bbd2(const float4& l1, const float4& h1, const float4& l2, const fl
   return r;
 }
 
-RST_HD void adj_put(float4* ent, int L, int k, int X, float bbd, const float4& lo,
+// Entry tag (hi.w bits): at the leaf level the listed leaf's point range,
+// begin * 32 + count (count <= 16; begin < 2^26), so a scan needs no further
+// lookup; at levels 2/3 the item index.  -1 = no entry.
+RST_HD int leaf_tag(const BvhView& bv, int X) {
+  const int b = leaf_begin(bv, X);
+  return b * 32 + (leaf_begin(bv, X + 1) - b);
+}
+
+RST_HD void adj_put(float4* ent, int L, int k, int tag, float bbd, const float4& lo,
                     const float4& hi) {
   float4* e = ent + ((int64_t)L * kAdjK + k) * 2;
   e[0] = make_float4(lo.x, lo.y, lo.z, bbd);
-  e[1] = make_float4(hi.x, hi.y, hi.z, i2f(X));
+  e[1] = make_float4(hi.x, hi.y, hi.z, i2f(tag));
+}
+
+// Offer the sorted points [b, b + n) (one leaf).
+template <class R>
+RST_HD void scan_range(const BvhView& bv, int b, int n, float qx, float qy, float qz, R& res) {
+  for (int i = b; i < b + n; ++i) {
+    const float4 p = bv.pts[i];
+    res.offer(d2_ref(qx, qy, qz, p.x, p.y, p.z), f2i(p.w), i);
+  }
 }
 
 // The K nearest leaves of leaf L by bbd2 (items = leaves, id = leaf index):
 // bottom-up from L like search_from, pruning subtrees by bbd2 to their box.
 // (Reference builder for tests; the GPU builds with rst_wave_nn.hpp.)
 template <class R>
-RST_HD void leaf_descend(const BvhView& bv, int root, const float4& ql, const float4& qh, R& res) {
-  const int nl = bv.nleaves;
+RST_HD void leaf_descend(const BvhView& bv, int first, int root, const float4& ql, const float4& qh,
+                         R& res) {
+  const int nl = first;
   const int top = root >> 1;
   const float cx = 0.5f * (ql.x + qh.x), cy = 0.5f * (ql.y + qh.y), cz = 0.5f * (ql.z + qh.z);
   int cur = root, prev = top;
@@ -334,27 +397,29 @@ RST_HD void leaf_descend(const BvhView& bv, int root, const float4& ql, const fl
   } while (cur != top);
 }
 
+// items = nodes [first, 2 first) (first = nleaves: the leaves)
 template <class R>
-RST_HD void leaf_knn(const BvhView& bv, int L, R& res) {
-  const int nl = bv.nleaves;
-  int node = nl + L;
+RST_HD void leaf_knn(const BvhView& bv, int first, int L, R& res) {
+  int node = first + L;
   const float4 ql = bv.nodes[2 * node], qh = bv.nodes[2 * node + 1];
   res.offer(bbd2(ql, qh, ql, qh), L, L);
   while (node > 1) {
-    leaf_descend(bv, node ^ 1, ql, qh, res);
+    leaf_descend(bv, first, node ^ 1, ql, qh, res);
     node >>= 1;
   }
 }
 
 // Adjacency record of leaf L from its K+1 nearest (sorted) leaves.
 template <int K1>
-RST_HD void adj_store(const BvhView& bv, const BestK<K1>& r, int L, float4* ent, float* reach) {
+RST_HD void adj_store(const BvhView& bv, int first, const BestK<K1>& r, int L, float4* ent,
+                      float* reach) {
   static_assert(K1 == kAdjK + 1, "list length");
-  const int nl = bv.nleaves;
+  const int nl = first;
   for (int j = 0; j < kAdjK; ++j) {
     const int X = r.pos[j] >= 0 ? r.id[j] : -1;
     const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-    adj_put(ent, L, j, X, X >= 0 ? sqrtf(r.d[j]) : INFINITY, X >= 0 ? bv.nodes[2 * (nl + X)] : z,
+    const int tag = X < 0 ? -1 : (first == bv.nleaves ? leaf_tag(bv, X) : X);
+    adj_put(ent, L, j, tag, X >= 0 ? sqrtf(r.d[j]) : INFINITY, X >= 0 ? bv.nodes[2 * (nl + X)] : z,
             X >= 0 ? bv.nodes[2 * (nl + X) + 1] : z);
   }
   reach[L] = r.pos[kAdjK] >= 0 ? sqrtf(r.d[kAdjK]) : INFINITY;
@@ -377,10 +442,65 @@ RST_HD bool adj_search(const BvhView& bv, const AdjView& av, int start, float qx
   const float4* e = av.ent + (int64_t)L * kAdjK * 2;
   for (int k = 0; k < kAdjK; ++k) {
     const float4 l = e[2 * k], h = e[2 * k + 1];
+    const int tag = f2i(h.w);
+    if (tag < 0) break;
+    if (l.w * 0.99999f - dl > sqrtf(res.bound()) * 1.00001f + 1e-30f) break;
+    if (box_d2(qx, qy, qz, l, h) <= res.bound()) scan_range(bv, tag >> 5, tag & 31, qx, qy, qz, res);
+  }
+  return true;
+}
+
+// The same through the level-2 index: entries are nodes of 2^kAdj2Shift
+// leaves; a listed node touching the ball has each of its leaves box-tested
+// and scanned.  Level-2 nodes partition the leaves, so the coverage argument
+// is unchanged.
+template <class R>
+RST_HD bool adj2_search(const BvhView& bv, const AdjView& av, int start, float qx, float qy,
+                        float qz, R& res) {
+  const int nl = bv.nleaves;
+  if (nl < (1 << kAdj2Shift)) return false;
+  const int first = nl >> kAdj2Shift;
+  const int N = (nl + leaf_of(bv, start)) >> kAdj2Shift;
+  const float4 lo = bv.nodes[2 * N], hi = bv.nodes[2 * N + 1];
+  const float dl = sqrtf(box_d2(qx, qy, qz, lo, hi)) * 1.00001f;
+  const float rb = sqrtf(res.bound()) * 1.00001f + 1e-30f;
+  if (!(dl + rb < av.reach2[N - first] * 0.99999f)) return false;
+  const float4* e = av.ent2 + (int64_t)(N - first) * kAdjK * 2;
+  for (int k = 0; k < kAdjK; ++k) {
+    const float4 l = e[2 * k], h = e[2 * k + 1];
     const int X = f2i(h.w);
     if (X < 0) break;
     if (l.w * 0.99999f - dl > sqrtf(res.bound()) * 1.00001f + 1e-30f) break;
-    if (box_d2(qx, qy, qz, l, h) <= res.bound()) scan_leaf(bv, X, qx, qy, qz, res);
+    if (!(box_d2(qx, qy, qz, l, h) <= res.bound())) continue;
+    const int leaf0 = ((first + X) << kAdj2Shift) - nl;
+    for (int j = 0; j < (1 << kAdj2Shift); ++j) {
+      const int Lj = leaf0 + j;
+      if (box_d2(qx, qy, qz, bv.nodes[2 * (nl + Lj)], bv.nodes[2 * (nl + Lj) + 1]) <= res.bound())
+        scan_leaf(bv, Lj, qx, qy, qz, res);
+    }
+  }
+  return true;
+}
+
+// Level 3: listed nodes touching the ball are walked exactly (descend).
+template <class R>
+RST_HD bool adj3_search(const BvhView& bv, const AdjView& av, int start, float qx, float qy,
+                        float qz, R& res) {
+  const int nl = bv.nleaves;
+  if (nl < (1 << kAdj3Shift)) return false;
+  const int first = nl >> kAdj3Shift;
+  const int N = (nl + leaf_of(bv, start)) >> kAdj3Shift;
+  const float4 lo = bv.nodes[2 * N], hi = bv.nodes[2 * N + 1];
+  const float dl = sqrtf(box_d2(qx, qy, qz, lo, hi)) * 1.00001f;
+  const float rb = sqrtf(res.bound()) * 1.00001f + 1e-30f;
+  if (!(dl + rb < av.reach3[N - first] * 0.99999f)) return false;
+  const float4* e = av.ent3 + (int64_t)(N - first) * kAdjK * 2;
+  for (int k = 0; k < kAdjK; ++k) {
+    const float4 l = e[2 * k], h = e[2 * k + 1];
+    const int X = f2i(h.w);
+    if (X < 0) break;
+    if (l.w * 0.99999f - dl > sqrtf(res.bound()) * 1.00001f + 1e-30f) break;
+    if (box_d2(qx, qy, qz, l, h) <= res.bound()) descend(bv, first + X, qx, qy, qz, res);
   }
   return true;
 }

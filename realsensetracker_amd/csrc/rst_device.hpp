@@ -179,6 +179,68 @@ __device__ inline void svd3_jacobi(const double* a_in, double* U, double* S,
   }
 }
 
+// Orthogonal polar factor Q of a nonsingular 3x3 a (column-major), i.e.
+// U V^T of its SVD, by scaled Newton iteration X <- (g X + X^-T / g) / 2
+// (Higham; g = sqrt(|X^-1|_F / |X|_F) while far from convergence, then 1
+// for the quadratic tail).  For nonsingular a the polar factor is unique, so
+// this is the same rotation JacobiSVD's U V^T gives (align_icp.cpp:139-141)
+// at ~1e-16 relative; a few dozen fp64 flops per step instead of Jacobi
+// sweeps.  Returns false (the caller falls back to svd3_jacobi) when a is
+// numerically singular or the iteration does not settle.
+__device__ inline bool polar3(const double* a, double* Q) {
+  double X[9];
+  double nx = 0.0;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    X[i] = a[i];
+    nx += a[i] * a[i];
+  }
+  nx = sqrt(nx);
+  if (!(nx > 0.0) || !(nx < 1e300)) return false;
+  for (int it = 0; it < 40; ++it) {
+    // cofactor matrix C (column-major): X^-T = C / det
+    double C[9];
+    RST_M3(C, 0, 0) = RST_M3(X, 1, 1) * RST_M3(X, 2, 2) - RST_M3(X, 1, 2) * RST_M3(X, 2, 1);
+    RST_M3(C, 0, 1) = RST_M3(X, 1, 2) * RST_M3(X, 2, 0) - RST_M3(X, 1, 0) * RST_M3(X, 2, 2);
+    RST_M3(C, 0, 2) = RST_M3(X, 1, 0) * RST_M3(X, 2, 1) - RST_M3(X, 1, 1) * RST_M3(X, 2, 0);
+    RST_M3(C, 1, 0) = RST_M3(X, 0, 2) * RST_M3(X, 2, 1) - RST_M3(X, 0, 1) * RST_M3(X, 2, 2);
+    RST_M3(C, 1, 1) = RST_M3(X, 0, 0) * RST_M3(X, 2, 2) - RST_M3(X, 0, 2) * RST_M3(X, 2, 0);
+    RST_M3(C, 1, 2) = RST_M3(X, 0, 1) * RST_M3(X, 2, 0) - RST_M3(X, 0, 0) * RST_M3(X, 2, 1);
+    RST_M3(C, 2, 0) = RST_M3(X, 0, 1) * RST_M3(X, 1, 2) - RST_M3(X, 0, 2) * RST_M3(X, 1, 1);
+    RST_M3(C, 2, 1) = RST_M3(X, 0, 2) * RST_M3(X, 1, 0) - RST_M3(X, 0, 0) * RST_M3(X, 1, 2);
+    RST_M3(C, 2, 2) = RST_M3(X, 0, 0) * RST_M3(X, 1, 1) - RST_M3(X, 0, 1) * RST_M3(X, 1, 0);
+    const double det = RST_M3(X, 0, 0) * RST_M3(C, 0, 0) + RST_M3(X, 0, 1) * RST_M3(C, 0, 1) +
+                       RST_M3(X, 0, 2) * RST_M3(C, 0, 2);
+    double n2 = 0.0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) n2 += X[i] * X[i];
+    const double nX = sqrt(n2);
+    // numerically singular (condition ~ nX^3 / |det| beyond ~1e12)
+    if (!(fabs(det) > 1e-12 * nX * nX * nX)) return false;
+    const double id = 1.0 / det;
+    double ni2 = 0.0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      C[i] *= id;
+      ni2 += C[i] * C[i];
+    }
+    const double g = it < 6 ? sqrt(sqrt(ni2) / nX) : 1.0;
+    double diff = 0.0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      const double xn = 0.5 * (g * X[i] + C[i] / g);
+      diff += (xn - X[i]) * (xn - X[i]);
+      X[i] = xn;
+    }
+    if (it >= 6 && diff <= 1e-30 * 3.0) {
+#pragma unroll
+      for (int i = 0; i < 9; ++i) Q[i] = X[i];
+      return true;
+    }
+  }
+  return false;
+}
+
 // Matrix3f::determinant (Eigen bruteforce_det3_helper order).
 __device__ __forceinline__ float det3f(const float* m) {
   const float d0 = RST_M3(m, 0, 0) * (RST_M3(m, 1, 1) * RST_M3(m, 2, 2) - RST_M3(m, 1, 2) * RST_M3(m, 2, 1));

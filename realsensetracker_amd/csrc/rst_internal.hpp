@@ -59,8 +59,10 @@ struct IcpState {
   double last_cnt;   // accepted correspondences of the last step
   double last_d2;    // sum d2 of the last step
   int32_t fail;      // P2PLANE: singular system / too few points
-  int32_t pad1;
+  int32_t fb_e;      // fallback-queue entries of the current iteration
   int32_t qlen[kQTrace];  // fallback-queue length per iteration (diagnostics)
+  int32_t path[kQTrace][4];  // lanes certified at adjacency level 1 (no walk) /
+                             // level 1 after a walk / level 2 / level 3
 };
 
 struct IcpParams {
@@ -103,10 +105,16 @@ struct rst_target {
   int32_t lg = 0;               // nleaves = 1 << lg
   float4* pts = nullptr;        // [m] Morton-sorted (x,y,z,orig idx bits)
   float4* nodes = nullptr;      // [2 * 2*nleaves]
+  int32_t* lstart = nullptr;    // [nleaves + 1] leaf ranges (rst_bvh.hpp)
+  int32_t* pleaf = nullptr;     // [m] leaf of each sorted point
   int32_t* inv = nullptr;       // [m] original index -> sorted position
   uint32_t* codes = nullptr;    // [m] sorted Morton codes, then 6 floats: their box
   float4* adj = nullptr;        // [nleaves * kAdjK * 2] leaf adjacency (rst_bvh.hpp)
   float* reach = nullptr;       // [nleaves]
+  float4* adj2 = nullptr;       // the same over the nodes of 8 leaves
+  float* reach2 = nullptr;
+  float4* adj3 = nullptr;       // ... and over the nodes of 64 leaves
+  float* reach3 = nullptr;
   float4* nrm = nullptr;        // [m] normals in sorted order (optional)
   float bbox[6] = {0, 0, 0, 0, 0, 0};
   int32_t pos0 = 0;             // sorted position of original point 0

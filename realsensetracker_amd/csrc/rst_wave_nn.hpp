@@ -477,9 +477,8 @@ namespace rst {
 // four at a time (each entry carries its leaf's box, so a test needs no
 // further gather) and leaf points eight at a time, unconditionally (index
 // clamped), so a lane's dependent chain is warm point -> entries -> points.
-__device__ __forceinline__ void scan_leaf_wide(const BvhView& bv, int X, float qx, float qy,
-                                               float qz, Best1& r) {
-  const int b = leaf_begin(bv, X), n = leaf_begin(bv, X + 1) - b;
+__device__ __forceinline__ void scan_range_wide(const BvhView& bv, int b, int n, float qx,
+                                                float qy, float qz, Best1& r) {
   const int last = bv.m - 1;
   for (int j0 = 0; j0 < n; j0 += 8) {
     float4 p[8];
@@ -497,10 +496,11 @@ __device__ __forceinline__ void scan_leaf_wide(const BvhView& bv, int X, float q
 // is scanned and the best point found becomes the new start, up to
 // kWalkSteps times.  Walking only lowers the bound; exactness still comes
 // from the coverage test of the final leaf.
-constexpr int kWalkSteps = 3;
+constexpr int kWalkSteps = 1;
 
 __device__ __forceinline__ bool adj_search_wide(const BvhView& bv, const AdjView& av, int start,
-                                                float qx, float qy, float qz, Best1& r) {
+                                                float qx, float qy, float qz, Best1& r,
+                                                int* walked = nullptr) {
   const int nl = bv.nleaves;
   int L = leaf_of(bv, start);
   float dl;
@@ -510,6 +510,7 @@ __device__ __forceinline__ bool adj_search_wide(const BvhView& bv, const AdjView
     // same margins as rst_bvh.hpp adj_search
     dl = sqrtf(box_d2(qx, qy, qz, lo, hi)) * 1.00001f;
     if (dl + sqrtf(r.d) * 1.00001f + 1e-30f < reach * 0.99999f) break;
+    if (walked) *walked = step + 1;
     if (step == kWalkSteps) return false;
     // walk: scan the listed leaf nearest to the query (other than L)
     const float4* e = av.ent + (int64_t)L * kAdjK * 2;
@@ -517,14 +518,14 @@ __device__ __forceinline__ bool adj_search_wide(const BvhView& bv, const AdjView
     int bx = -1;
     for (int k = 1; k < kAdjK; ++k) {
       const float4 l = e[2 * k], h = e[2 * k + 1];
-      const int X = f2i(h.w);
+      const int tag = f2i(h.w);
       const float b = box_d2(qx, qy, qz, l, h);
-      const bool t = X >= 0 && b < bb;
+      const bool t = tag >= 0 && b < bb;
       bb = t ? b : bb;
-      bx = t ? X : bx;
+      bx = t ? tag : bx;
     }
     if (bx < 0 || !(bb < r.d)) return false;
-    scan_leaf_wide(bv, bx, qx, qy, qz, r);
+    scan_range_wide(bv, bx >> 5, bx & 31, qx, qy, qz, r);
     L = leaf_of(bv, r.pos);
   }
   const float4* e = av.ent + (int64_t)L * kAdjK * 2;
@@ -539,11 +540,11 @@ __device__ __forceinline__ bool adj_search_wide(const BvhView& bv, const AdjView
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       if (stop) break;
-      const int X = f2i(h[j].w);
-      if (X < 0 || l[j].w * 0.99999f - dl > sqrtf(r.d) * 1.00001f + 1e-30f) {
+      const int tag = f2i(h[j].w);
+      if (tag < 0 || l[j].w * 0.99999f - dl > sqrtf(r.d) * 1.00001f + 1e-30f) {
         stop = true;
       } else if (box_d2(qx, qy, qz, l[j], h[j]) <= r.d) {
-        scan_leaf_wide(bv, X, qx, qy, qz, r);
+        scan_range_wide(bv, tag >> 5, tag & 31, qx, qy, qz, r);
       }
     }
     if (stop) break;
@@ -552,20 +553,23 @@ __device__ __forceinline__ bool adj_search_wide(const BvhView& bv, const AdjView
 }
 
 // ---- adjacency build: one wavefront per leaf -------------------------------------
-// Range query around box(L) with radius D0 = 2 x its diagonal (halved while
+// Range query around box(L) with radius D0 = 3 x its diagonal (halved while
 // more than kWnnLeaves leaves fall inside), then the kAdjK nearest of the
 // collected leaves by rank.  reach[L] = the (kAdjK+1)-th distance when more
 // were collected, else sqrt(D0^2): every leaf not listed is at least that
 // far (non-collected leaves have bbd2 > D0^2).  Degenerate cases (empty box,
 // persistent overflow) get reach 0: such a leaf never certifies a query.
-__device__ __forceinline__ void leaf_adj_wave(const BvhView& bv, int L, float4* __restrict__ ent,
-                                              float* __restrict__ reach, WnnScratch& ws) {
+// Items = the tree nodes [first, 2 first) of one level (first = nleaves:
+// the leaves; first = nleaves >> 3: nodes of 8 leaves), L = item index.
+__device__ __forceinline__ void leaf_adj_wave(const BvhView& bv, int first, int L,
+                                              float4* __restrict__ ent, float* __restrict__ reach,
+                                              WnnScratch& ws) {
   const int lane = __lane_id();
-  const int nl = bv.nleaves;
+  const int nl = first;
   const float4 ql = bv.nodes[2 * (nl + L)], qh = bv.nodes[2 * (nl + L) + 1];
   const float dx = qh.x - ql.x, dy = qh.y - ql.y, dz = qh.z - ql.z;
   const float diag2 = dx * dx + dy * dy + dz * dz;
-  float D2 = 4.0f * diag2;
+  float D2 = 9.0f * diag2;  // radius 3 x the item's diagonal, halved on overflow
   int ns = 0;
   bool overflow = !(ql.x <= qh.x) || !(diag2 < FLT_MAX);
   for (int attempt = 0; attempt < 6 && !(!(ql.x <= qh.x) || !(diag2 < FLT_MAX)); ++attempt) {
@@ -640,7 +644,8 @@ __device__ __forceinline__ void leaf_adj_wave(const BvhView& bv, int L, float4* 
       e[2 * rank] = make_float4(bv.nodes[2 * (nl + mid)].x, bv.nodes[2 * (nl + mid)].y,
                                 bv.nodes[2 * (nl + mid)].z, sqrtf(mb));
       const float4 h = bv.nodes[2 * (nl + mid) + 1];
-      e[2 * rank + 1] = make_float4(h.x, h.y, h.z, i2f(mid));
+      const int tag = first == bv.nleaves ? leaf_tag(bv, mid) : mid;
+      e[2 * rank + 1] = make_float4(h.x, h.y, h.z, i2f(tag));
     }
     if (rank == kAdjK) rk_b2 = mb;
   }

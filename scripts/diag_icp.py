@@ -40,11 +40,13 @@ def main():
             t2 = time.perf_counter()
             r = A.align_prepared(tb, ta, None, L.default_opts(mode=mode, max_iter=it))
             t3 = time.perf_counter()
-            q = np.zeros(256, np.int32)
+            q = np.zeros((256, 5), np.int32)
             qt(ctx.handle, L.iptr(q), 256)
             print(f"pair {pair} mode {mode}: n={len(pb)} build {1e3*(t1-t0):.2f} ms  align "
                   f"{1e3*(t3-t2):.2f} ms  iters {r.iterations} ok {r.ok}")
-            print("  queue per iter:", " ".join(str(x) for x in q[:r.iterations]))
+            print("  iter: queue | L1 L1walk L2 L3")
+            for i in list(range(min(8, r.iterations))) + list(range(16, r.iterations, 16)):
+                print(f"  {i:3d}: {q[i,0]:6d} | {q[i,1]:6d} {q[i,2]:6d} {q[i,3]:6d} {q[i,4]:6d}")
 
 
 if __name__ == "__main__":

@@ -25,9 +25,11 @@ void check(bool ok, const char* what, int m, int q);
 
 struct Index {
   std::vector<float4> pts;
+  std::vector<uint32_t> codes;
+  std::vector<int32_t> lstart, pleaf;
   std::vector<float4> nodes;
-  std::vector<float4> adj;
-  std::vector<float> reach;
+  std::vector<float4> adj, adj2, adj3;
+  std::vector<float> reach, reach2, reach3;
   BvhView bv;
   AdjView av;
 };
@@ -57,18 +59,33 @@ Index build(const std::vector<float>& xyz) {
   std::stable_sort(kv.begin(), kv.end(),
                    [](const auto& a, const auto& b) { return a.first < b.first; });
   ix.pts.resize(std::max(m, 1));
+  ix.codes.resize(std::max(m, 1));
   for (int i = 0; i < m; ++i) {
     const int j = kv[i].second;
     ix.pts[i] = make_float4(xyz[3 * j], xyz[3 * j + 1], xyz[3 * j + 2], i2f(j));
+    ix.codes[i] = kv[i].first;
   }
+  // compact leaves (rst_bvh.hpp leaf_cut)
+  ix.pleaf.assign(std::max(m, 1), 0);
+  ix.lstart.clear();
+  int seg = 0;
+  for (int i = 0; i < m; ++i) {
+    if (i == 0 || (ix.codes[i] >> kLeafCellShift) != (ix.codes[i - 1] >> kLeafCellShift)) seg = i;
+    if (leaf_cut(ix.codes.data(), i, seg)) ix.lstart.push_back(i);
+    ix.pleaf[i] = (int)ix.lstart.size() - 1;
+  }
+  const int NL = std::max((int)ix.lstart.size(), 1);
   int nl = 1, lg = 0;
-  while ((int64_t)nl * kLeafTarget < m) {
+  while (nl < NL) {
     nl <<= 1;
     ++lg;
   }
+  while ((int)ix.lstart.size() <= nl) ix.lstart.push_back(m);
   ix.nodes.resize(4 * (size_t)nl);
-  ix.bv.codes = nullptr;
+  ix.bv.codes = ix.codes.data();
   ix.bv.bbox = nullptr;
+  ix.bv.lstart = ix.lstart.data();
+  ix.bv.pleaf = ix.pleaf.data();
   ix.bv.pts = ix.pts.data();
   ix.bv.nodes = ix.nodes.data();
   ix.bv.m = m;
@@ -83,11 +100,35 @@ Index build(const std::vector<float>& xyz) {
     for (int L = 0; L < nl; ++L) {
       BestK<kAdjK + 1> r;
       r.init();
-      leaf_knn(ix.bv, L, r);
-      adj_store(ix.bv, r, L, ix.adj.data(), ix.reach.data());
+      leaf_knn(ix.bv, nl, L, r);
+      adj_store(ix.bv, nl, r, L, ix.adj.data(), ix.reach.data());
     }
+  const int n2 = std::max(nl >> kAdj2Shift, 1);
+  ix.adj2.resize((size_t)n2 * kAdjK * 2);
+  ix.reach2.assign(n2, 0.0f);
+  if (m > 0 && nl >= (1 << kAdj2Shift))
+    for (int L = 0; L < n2; ++L) {
+      BestK<kAdjK + 1> r;
+      r.init();
+      leaf_knn(ix.bv, n2, L, r);
+      adj_store(ix.bv, n2, r, L, ix.adj2.data(), ix.reach2.data());
+    }
+  const int n3 = std::max(nl >> kAdj3Shift, 1);
+  ix.adj3.resize((size_t)n3 * kAdjK * 2);
+  ix.reach3.assign(n3, 0.0f);
+  if (m > 0 && nl >= (1 << kAdj3Shift))
+    for (int L = 0; L < n3; ++L) {
+      BestK<kAdjK + 1> r;
+      r.init();
+      leaf_knn(ix.bv, n3, L, r);
+      adj_store(ix.bv, n3, r, L, ix.adj3.data(), ix.reach3.data());
+    }
+  ix.av.ent3 = ix.adj3.data();
+  ix.av.reach3 = ix.reach3.data();
   ix.av.ent = ix.adj.data();
   ix.av.reach = ix.reach.data();
+  ix.av.ent2 = ix.adj2.data();
+  ix.av.reach2 = ix.reach2.data();
   return ix;
 }
 
@@ -125,7 +166,7 @@ void brute(const std::vector<float>& xyz, float qx, float qy, float qz, BestK<K>
 
 int g_fail = 0;
 long g_checks = 0;
-long g_covered = 0, g_adj_tries = 0;
+long g_covered = 0, g_covered2 = 0, g_covered3 = 0, g_adj_tries = 0;
 
 void check(bool ok, const char* what, int m, int q) {
   ++g_checks;
@@ -190,8 +231,13 @@ void run_case(std::mt19937_64& rng, int m, int nq, int mode) {
       s.init();
       const float4 p = ix.pts[start];
       if (finite3(qx, qy, qz)) s.offer(d2_ref(qx, qy, qz, p.x, p.y, p.z), f2i(p.w), start);
+      Best1 s2 = s;
       search(ix.bv, start, qx, qy, qz, s);
       check(s.d == b1.d[0] && (s.pos < 0 ? b1.pos[0] < 0 : s.id == b1.id[0]), "nn warm", m, q);
+      if (finite3(qx, qy, qz)) {
+        search_from_fast(ix.bv, start, qx, qy, qz, s2);
+        check(s2.d == b1.d[0] && (s2.pos < 0 ? b1.pos[0] < 0 : s2.id == b1.id[0]), "nn fast", m, q);
+      }
       if (s.pos >= 0) check(f2i(ix.pts[s.pos].w) == s.id, "nn pos", m, q);
     }
     // adjacency search from a warm candidate near the answer
@@ -202,9 +248,19 @@ void run_case(std::mt19937_64& rng, int m, int nq, int mode) {
       const float4 p = ix.pts[start];
       s.offer(d2_ref(qx, qy, qz, p.x, p.y, p.z), f2i(p.w), start);
       ++g_adj_tries;
+      Best1 s2 = s;
       if (adj_search(ix.bv, ix.av, start, qx, qy, qz, s)) {
         ++g_covered;
         check(s.d == b1.d[0] && (s.pos < 0 ? b1.pos[0] < 0 : s.id == b1.id[0]), "adj", m, q);
+      }
+      Best1 s3 = s2;
+      if (adj3_search(ix.bv, ix.av, start, qx, qy, qz, s3)) {
+        ++g_covered3;
+        check(s3.d == b1.d[0] && (s3.pos < 0 ? b1.pos[0] < 0 : s3.id == b1.id[0]), "adj3", m, q);
+      }
+      if (adj2_search(ix.bv, ix.av, start, qx, qy, qz, s2)) {
+        ++g_covered2;
+        check(s2.d == b1.d[0] && (s2.pos < 0 ? b1.pos[0] < 0 : s2.id == b1.id[0]), "adj2", m, q);
       }
     }
     // k = 4, bottom-up from a random leaf
@@ -227,7 +283,8 @@ int main(int argc, char** argv) {
   const int sizes[] = {0, 1, 2, 3, 7, 16, 17, 33, 100, 257, 1000, 4099, 20000};
   for (int m : sizes)
     for (int mode = 0; mode < 4; ++mode) run_case(rng, m, m >= 4099 ? 300 : 120, mode);
-  printf("bvh_selftest: %ld checks, %d failures (adjacency covered %ld of %ld warm queries)\n",
-         g_checks, g_fail, g_covered, g_adj_tries);
+  printf("bvh_selftest: %ld checks, %d failures (adjacency covered %ld / level 2 %ld / level 3 "
+         "%ld of %ld warm queries)\n", g_checks, g_fail, g_covered, g_covered2, g_covered3,
+         g_adj_tries);
   return g_fail == 0 ? 0 : 1;
 }
