@@ -164,6 +164,16 @@ int rst_icp_align_prepared(rst_ctx* ctx, const rst_target* src,
 int rst_kabsch_solve(rst_ctx* ctx, const double cov[9], const float smean[3],
                      const float dmean[3], float pose_out[16]);
 
+/* SolveKabsch (align_icp.cpp:18-71, declared align_icp.hpp:14-17): weighted
+ * Kabsch over k correspondences pairs[2c] = src index, pairs[2c+1] = dst
+ * index; weights may be NULL (unweighted branch, :38-45).  Means and the
+ * fp64 covariance are computed on the device, then the same solve as
+ * rst_kabsch_solve.  RST_FALSE when n < 3 or m < 3 (pose untouched, :22-24);
+ * RST_E_ARG for k < 1 or an index out of range. */
+int rst_solve_kabsch(rst_ctx* ctx, const float* src, int64_t n,
+                     const float* dst, int64_t m, const int32_t* pairs,
+                     const float* weights, int64_t k, float pose_out[16]);
+
 /* ComputeCentroid (point_cloud_utils.cpp:92-98), fp64 accumulation. */
 int rst_compute_centroid(rst_ctx* ctx, const float* xyz, int64_t n,
                          float out[3]);

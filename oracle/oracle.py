@@ -48,6 +48,8 @@ def lib():
         L.orc_transform_points.argtypes = [_f, _f, C.c_int64, _f]
         L.orc_jacobi_svd3.argtypes = [_d, _d, _d, _d]
         L.orc_kabsch_pose.argtypes = [_d, _f, _f, _f]
+        L.orc_solve_kabsch.restype = C.c_int
+        L.orc_solve_kabsch.argtypes = [_f, C.c_int64, _f, C.c_int64, _i, _f, C.c_int64, _f]
         L.orc_align_icp.restype = C.c_int
         L.orc_align_icp.argtypes = [_f, C.c_int64, _f, C.c_int64, P, C.c_int, _f, _f,
                                     C.POINTER(_Trace)]
@@ -148,6 +150,19 @@ def kabsch_pose(cov, smean, dmean):
     lib().orc_kabsch_pose(c.ctypes.data_as(_d), _fp(np.asarray(smean, np.float32)),
                           _fp(np.asarray(dmean, np.float32)), _fp(out))
     return _uncm(out)
+
+
+def solve_kabsch(src, dst, pairs, weights=None, T=None):
+    """SolveKabsch (align_icp.cpp:18-71).  pairs: (k, 2) int (src, dst).
+    Returns (ok, pose); pose = T (untouched) when ok is False."""
+    src, dst = _cloud(src), _cloud(dst)
+    p = np.ascontiguousarray(np.asarray(pairs, np.int32).reshape(-1, 2))
+    w = None if weights is None else np.ascontiguousarray(np.asarray(weights, np.float32))
+    T0 = np.eye(4, dtype=np.float32) if T is None else np.asarray(T, np.float32)
+    out = _cm(T0)
+    ok = lib().orc_solve_kabsch(_fp(src), len(src), _fp(dst), len(dst), p.ctypes.data_as(_i),
+                                None if w is None else _fp(w), len(p), _fp(out))
+    return bool(ok), _uncm(out)
 
 
 def align_icp(src, dst, max_iter=128, T=None, tree: KDTree | None = None, trace=False,

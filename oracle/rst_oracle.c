@@ -655,6 +655,39 @@ void orc_kabsch_pose(const double cov[9], const float smean[3],
 }
 
 /* ------------------------------------------------------------------------ */
+/* SolveKabsch (align_icp.cpp:18-71): fp32 sequential means over the pairs
+ * (:27-34), cov += w * double(float((q - dbar)(s - sbar)^T)) (:36-54), then
+ * the Kabsch of :58-69 (same as the ICP's :139-151). */
+int orc_solve_kabsch(const float* src, int64_t n, const float* dst, int64_t m,
+                     const int32_t* pairs, const float* weights, int64_t k,
+                     float pose_out[16]) {
+  if (n < 3 || m < 3) return 0; /* :22-24 */
+  float sm[3] = {0.f, 0.f, 0.f}, dm[3] = {0.f, 0.f, 0.f};
+  for (int64_t c = 0; c < k; ++c)
+    for (int a = 0; a < 3; ++a) {
+      sm[a] += src[3 * (int64_t)pairs[2 * c] + a];
+      dm[a] += dst[3 * (int64_t)pairs[2 * c + 1] + a];
+    }
+  const float fk = (float)k; /* Vector3f /= size_t */
+  for (int a = 0; a < 3; ++a) {
+    sm[a] /= fk;
+    dm[a] /= fk;
+  }
+  double cov[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  for (int64_t c = 0; c < k; ++c) {
+    const float* s = src + 3 * (int64_t)pairs[2 * c];
+    const float* q = dst + 3 * (int64_t)pairs[2 * c + 1];
+    const float u[3] = {s[0] - sm[0], s[1] - sm[1], s[2] - sm[2]};
+    const float v[3] = {q[0] - dm[0], q[1] - dm[1], q[2] - dm[2]};
+    const double w = weights ? (double)weights[c] : 1.0;
+    for (int r = 0; r < 3; ++r)
+      for (int cc = 0; cc < 3; ++cc) A3(cov, r, cc) += w * (double)(v[r] * u[cc]);
+  }
+  orc_kabsch_pose(cov, sm, dm, pose_out);
+  return 1;
+}
+
+/* ------------------------------------------------------------------------ */
 /* AlignIcp3d (align_icp.cpp:73-161; 4-arg overload :163-167) */
 int orc_align_icp(const float* src, int64_t n, const float* dst, int64_t m,
                   const orc_kdtree* tree, int max_iter, float pose_inout[16],

@@ -56,6 +56,13 @@ void orc_nn_batch(const orc_kdtree* t, const float* q, int64_t nq,
 void orc_nn_bruteforce(const float* xyz, int64_t m, const float* q,
                        int64_t nq, int32_t* idx, float* d2);
 
+/* ---- align/SolveKabsch (align_icp.cpp:18-71) ----------------------------- */
+/* pairs[2c] = src index, pairs[2c+1] = dst index; weights may be NULL.
+ * Returns 0 (pose untouched) when n < 3 or m < 3. */
+int orc_solve_kabsch(const float* src, int64_t n, const float* dst, int64_t m,
+                     const int32_t* pairs, const float* weights, int64_t k,
+                     float pose_out[16]);
+
 /* ---- common/centroid (point_cloud_utils.cpp:92-98) ---------------------- */
 void orc_centroid(const float* xyz, int64_t n, float out[3]);
 

@@ -71,6 +71,8 @@ PROTOTYPES = {
                                        c_float_p]),
     "rst_icp_align_prepared": (C.c_int, [_P, _P, _P, C.POINTER(IcpOpts), c_float_p, c_float_p,
                                          c_int32_p]),
+    "rst_solve_kabsch": (C.c_int, [_P, c_float_p, C.c_int64, c_float_p, C.c_int64, c_int32_p,
+                                   c_float_p, C.c_int64, c_float_p]),
     "rst_compute_centroid": (C.c_int, [_P, c_float_p, C.c_int64, c_float_p]),
     "rst_kabsch_solve": (C.c_int, [_P, C.POINTER(C.c_double), c_float_p, c_float_p, c_float_p]),
     "rst_unproject": (C.c_int, [_P, c_u16_p, C.POINTER(Intrinsics), C.c_int, c_float_p,

@@ -8,6 +8,7 @@ the MI355X C ABI (include/rst_align.h):
     AlignIcp3d(src, dst, max_iter, T)            -> bool  (T updated in place)
     AlignIcp3d(src, dst, dst_tree, max_iter, T)  -> bool
     KDTree3f(dst, leaf_max_size=16).query(p, k)  -> (indices, sq_dists)
+    SolveKabsch(src, dst, indices, weights, T)   -> bool  (T updated in place)
     ComputeCentroid(cloud)                       -> (3,) float32
     ComputeNormals(cloud, tree, k)               -> (n, 3) float32
     OrientNormals(cloud, viewpoint, normals)     (in place)
@@ -256,6 +257,31 @@ def AlignIcp3d(src, dst, *args, opts: "L.IcpOpts | None" = None) -> bool:
                      "rst_icp_align")
     if len(s) >= 3 and len(dst) >= 3:
         T[...] = L.cm_to_pose(buf)
+    return st == L.RST_OK
+
+
+def SolveKabsch(src, dst, indices, weights, xfm: np.ndarray, ctx: Context | None = None) -> bool:
+    """SolveKabsch(src, dst, indices, weights, &xfm) (align_icp.cpp:18-71) on the GPU.
+
+    indices: (k, 2) int pairs (src index, dst index); weights: (k,) or
+    empty/None for the unweighted branch.  xfm (4x4 float32) is written in
+    place; untouched when the reference returns false (< 3 points)."""
+    if not (isinstance(xfm, np.ndarray) and xfm.shape == (4, 4) and xfm.dtype == np.float32):
+        raise TypeError("xfm must be a (4, 4) float32 ndarray (updated in place)")
+    ctx = ctx or get_context()
+    s, d = L.as_cloud(src), L.as_cloud(dst)
+    p = np.ascontiguousarray(np.asarray(indices, np.int32).reshape(-1, 2))
+    w = None
+    if weights is not None and len(weights) > 0:
+        w = np.ascontiguousarray(np.asarray(weights, np.float32))
+        if len(w) != len(p):
+            raise ValueError("weights must match indices")
+    buf = L.pose_to_cm(xfm)
+    st = L.check(L.lib().rst_solve_kabsch(ctx.handle, L.fptr(s), len(s), L.fptr(d), len(d),
+                                          L.iptr(p), None if w is None else L.fptr(w), len(p),
+                                          L.fptr(buf)), "rst_solve_kabsch")
+    if st == L.RST_OK:
+        xfm[...] = L.cm_to_pose(buf)
     return st == L.RST_OK
 
 

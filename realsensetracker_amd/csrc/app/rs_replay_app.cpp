@@ -1,0 +1,142 @@
+// rs_replay_app -- the reference's frame-to-frame replay loop
+// (rs_tracker/app/src/rs_replay_app.cpp:211-270) as host C++ over the
+// MI355X align module, with the synthetic frame source in place of the
+// recorded .pb sequence (driver decoupled from the camera):
+//
+//   for each frame: depth -> cloud (rst_unproject; RemoveNans = drop invalid)
+//     xfm = Identity; ok = AlignIcp3d(curr, prev, 128, &xfm)      (:235,251)
+//     if ok: total_xfm = total_xfm * xfm; prev = curr              (:266-270)
+//
+// Voxel downsampling (:246-247) is SURVEY.md §8f row f1 and not applied.
+// Prints per-frame timing and drift against the scene's ground truth.
+//
+//   rs_replay_app [--frames N] [--width W] [--height H] [--iters K] [--seed S]
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "rs_tracker/align/align_icp.hpp"
+
+namespace {
+
+struct Args {
+  int frames = 10, width = 640, height = 480, iters = 128;
+  uint64_t seed = 0;
+};
+
+Args Parse(int argc, char** argv) {
+  Args a;
+  for (int i = 1; i + 1 < argc; i += 2) {
+    const std::string k = argv[i];
+    const long v = std::strtol(argv[i + 1], nullptr, 10);
+    if (k == "--frames") a.frames = (int)v;
+    else if (k == "--width") a.width = (int)v;
+    else if (k == "--height") a.height = (int)v;
+    else if (k == "--iters") a.iters = (int)v;
+    else if (k == "--seed") a.seed = (uint64_t)v;
+    else { std::fprintf(stderr, "unknown flag %s\n", k.c_str()); std::exit(2); }
+  }
+  return a;
+}
+
+// inverse of a rigid 4x4 column-major transform
+void RigidInverse(const float* T, float* out) {
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < 3; ++c) out[c * 4 + r] = T[r * 4 + c];
+  for (int r = 0; r < 3; ++r) {
+    float s = 0.f;
+    for (int k = 0; k < 3; ++k) s += out[k * 4 + r] * T[12 + k];
+    out[12 + r] = -s;
+  }
+  out[3] = out[7] = out[11] = 0.f;
+  out[15] = 1.f;
+}
+
+void Mul(const float* A, const float* B, float* out) {
+  for (int r = 0; r < 4; ++r)
+    for (int c = 0; c < 4; ++c) {
+      float s = 0.f;
+      for (int k = 0; k < 4; ++k) s += A[k * 4 + r] * B[c * 4 + k];
+      out[c * 4 + r] = s;
+    }
+}
+
+void PoseError(const float* T, const float* G, double* ang, double* tr) {
+  double tr3 = 0.0;  // trace(R_T R_G^T)
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < 3; ++c) tr3 += (double)T[c * 4 + r] * G[c * 4 + r];
+  *ang = std::acos(std::fmax(-1.0, std::fmin(1.0, (tr3 - 1.0) / 2.0)));
+  double s = 0.0;
+  for (int r = 0; r < 3; ++r) s += (double)(T[12 + r] - G[12 + r]) * (T[12 + r] - G[12 + r]);
+  *tr = std::sqrt(s);
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  using rs_tracker::gpu::Check;
+  const Args a = Parse(argc, argv);
+  rst_scene* scene = nullptr;
+  Check(rst_scene_create(a.seed, &scene), "rst_scene_create");
+  rst_intrinsics K{};
+  K.width = a.width;
+  K.height = a.height;
+  K.fx = K.fy = 385.0f * (float)a.width / 640.0f;
+  K.cx = 0.5f * (float)a.width;
+  K.cy = 0.5f * (float)a.height;
+  K.depth_scale = 0.001f;
+  K.min_depth = 0.3f;
+  K.max_depth = 5.0f;
+  rs_tracker::gpu::Context& ctx = rs_tracker::gpu::DefaultContext();
+
+  std::vector<uint16_t> depth((size_t)a.width * a.height);
+  std::vector<float> xyz(3 * depth.size());
+  auto grab = [&](int f, float* T_wc) {
+    Check(rst_scene_trajectory(scene, f, T_wc), "trajectory");
+    Check(rst_scene_render_depth(scene, T_wc, &K, 1000u + (uint64_t)f, 0.001f, 0.03f, depth.data()),
+          "render");
+    int64_t n = 0;
+    Check(rst_unproject(ctx.get(), depth.data(), &K, 0, xyz.data(), &n), "rst_unproject");
+    return rs_tracker::Cloud3f(xyz.data(), n);
+  };
+
+  float T0[16], T0inv[16], Tf[16];
+  rs_tracker::Cloud3f prev = grab(0, T0);
+  RigidInverse(T0, T0inv);
+  rs_tracker::Isometry3f total_xfm = rs_tracker::Isometry3f::Identity();
+  double worst_ang = 0.0, worst_tr = 0.0, total_ms = 0.0;
+  int ok_count = 0;
+  for (int f = 1; f < a.frames; ++f) {
+    rs_tracker::Cloud3f cloud = grab(f, Tf);
+    rs_tracker::Isometry3f xfm = rs_tracker::Isometry3f::Identity();
+    const auto t0 = std::chrono::steady_clock::now();
+    const bool suc = rs_tracker::AlignIcp3d(cloud, prev, a.iters, &xfm);
+    const double ms =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    total_ms += ms;
+    if (suc) {
+      total_xfm = total_xfm * xfm;
+      prev = std::move(cloud);
+      ++ok_count;
+    } else {
+      std::printf("ALIGNMENT FAILED!!\n");
+    }
+    float tot[16], gt[16];
+    rs_tracker::ToColMajor(total_xfm, tot);
+    Mul(T0inv, Tf, gt);
+    double ang, tr;
+    PoseError(tot, gt, &ang, &tr);
+    worst_ang = std::fmax(worst_ang, ang);
+    worst_tr = std::fmax(worst_tr, tr);
+    std::printf("frame %3d  n=%7lld  align %8.2f ms  drift %.2e rad %.2e m\n", f,
+                (long long)prev.cols(), ms, ang, tr);
+  }
+  std::printf("frames %d  aligned %d  mean align %.2f ms  worst drift %.2e rad %.2e m\n",
+              a.frames - 1, ok_count, total_ms / std::max(1, a.frames - 1), worst_ang, worst_tr);
+  rst_scene_destroy(scene);
+  return ok_count == a.frames - 1 ? 0 : 1;
+}

@@ -84,6 +84,11 @@ static int upload_xyz(rst_ctx* ctx, const float* h, int64_t n, float** d_out) {
       hipFree(d);
       return s;
     }
+    // the staging buffer may still feed an earlier async copy
+    if (hipStreamSynchronize(ctx->stream) != hipSuccess) {
+      hipFree(d);
+      return RST_E_HIP;
+    }
     memcpy(pin, h, sizeof(float) * 3 * n);
     if (hipMemcpyAsync(d, pin, sizeof(float) * 3 * n, hipMemcpyHostToDevice, ctx->stream) !=
         hipSuccess) {
@@ -437,6 +442,37 @@ int rst_kabsch_solve(rst_ctx* ctx, const double cov[9], const float smean[3],
   if (!ctx || !cov || !smean || !dmean || !pose_out) return RST_E_ARG;
   RST_HIP(hipSetDevice(ctx->device));
   return kabsch_device(ctx, cov, smean, dmean, pose_out);
+}
+
+int rst_solve_kabsch(rst_ctx* ctx, const float* src, int64_t n, const float* dst, int64_t m,
+                     const int32_t* pairs, const float* weights, int64_t k, float pose_out[16]) {
+  if (!ctx || !pose_out || n < 0 || m < 0 || k < 0 || (n > 0 && !src) || (m > 0 && !dst) ||
+      (k > 0 && !pairs))
+    return RST_E_ARG;
+  if (n < 3 || m < 3) return RST_FALSE;  // align_icp.cpp:22-24, pose untouched
+  if (k < 1) return RST_E_ARG;           // reference: 0/0 means (NaN pose)
+  for (int64_t c = 0; c < k; ++c)        // host-side bounds check before any launch
+    if (pairs[2 * c] < 0 || pairs[2 * c] >= n || pairs[2 * c + 1] < 0 || pairs[2 * c + 1] >= m)
+      return RST_E_ARG;
+  RST_HIP(hipSetDevice(ctx->device));
+  float *ds = nullptr, *dd = nullptr;
+  void* dp = nullptr;
+  RST_CHECK(upload_xyz(ctx, src, n, &ds));
+  int r = upload_xyz(ctx, dst, m, &dd);
+  const size_t pb = sizeof(int32_t) * 2 * (size_t)k, wb = weights ? sizeof(float) * (size_t)k : 0;
+  if (r >= 0 && hipMalloc(&dp, pb + wb) != hipSuccess) r = RST_E_NOMEM;
+  if (r >= 0 && (hipMemcpyAsync(dp, pairs, pb, hipMemcpyHostToDevice, ctx->stream) != hipSuccess ||
+                 (weights && hipMemcpyAsync((char*)dp + pb, weights, wb, hipMemcpyHostToDevice,
+                                            ctx->stream) != hipSuccess)))
+    r = RST_E_HIP;
+  if (r >= 0)
+    r = solve_kabsch_device(ctx, ds, dd, (const int32_t*)dp,
+                            weights ? (const float*)((char*)dp + pb) : nullptr, k, pose_out);
+  hipStreamSynchronize(ctx->stream);
+  if (dp) hipFree(dp);
+  if (dd) hipFree(dd);
+  hipFree(ds);
+  return r;
 }
 
 int rst_compute_centroid(rst_ctx* ctx, const float* xyz, int64_t n, float out[3]) {

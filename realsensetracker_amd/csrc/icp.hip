@@ -420,6 +420,51 @@ __global__ void k_kabsch(const double* __restrict__ in /*cov[9] smean[3] dmean[3
   out[15] = 1.f;
 }
 
+// ---- SolveKabsch (align_icp.cpp:18-71): correspondences -> pose ----------------------
+// Pass 1: fp64 sums of src[pairs.first] and dst[pairs.second] (6 per block).
+__global__ __launch_bounds__(kBS) void k_pairs_sum(const float* __restrict__ src,
+                                                   const float* __restrict__ dst,
+                                                   const int32_t* __restrict__ pairs, int64_t k,
+                                                   double* __restrict__ slab) {
+  __shared__ double lds[(kBS / kWave) * 6];
+  double v[6] = {0, 0, 0, 0, 0, 0};
+  for (int64_t c = blockIdx.x * (int64_t)kBS + threadIdx.x; c < k;
+       c += (int64_t)gridDim.x * kBS) {
+    const int64_t i = pairs[2 * c], j = pairs[2 * c + 1];
+    v[0] += src[3 * i]; v[1] += src[3 * i + 1]; v[2] += src[3 * i + 2];
+    v[3] += dst[3 * j]; v[4] += dst[3 * j + 1]; v[5] += dst[3 * j + 2];
+  }
+  block_sum_to_slab<6, kBS>(v, lds, slab + blockIdx.x * 6);
+}
+
+// Pass 2: the means (float, as src_mean /= indices.size() at :33-34), then
+// cov += w * double(float((q - dbar)(s - sbar)^T)) (:36-54) in fp64.
+__global__ __launch_bounds__(kBS) void k_pairs_cov(const float* __restrict__ src,
+                                                   const float* __restrict__ dst,
+                                                   const int32_t* __restrict__ pairs,
+                                                   const float* __restrict__ weights, int64_t k,
+                                                   const double* __restrict__ tot6,
+                                                   double* __restrict__ slab) {
+  __shared__ double lds[(kBS / kWave) * 9];
+  const float sm0 = (float)(tot6[0] / (double)k), sm1 = (float)(tot6[1] / (double)k),
+              sm2 = (float)(tot6[2] / (double)k);
+  const float dm0 = (float)(tot6[3] / (double)k), dm1 = (float)(tot6[4] / (double)k),
+              dm2 = (float)(tot6[5] / (double)k);
+  double v[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  for (int64_t c = blockIdx.x * (int64_t)kBS + threadIdx.x; c < k;
+       c += (int64_t)gridDim.x * kBS) {
+    const int64_t i = pairs[2 * c], j = pairs[2 * c + 1];
+    const float u[3] = {src[3 * i] - sm0, src[3 * i + 1] - sm1, src[3 * i + 2] - sm2};
+    const float q[3] = {dst[3 * j] - dm0, dst[3 * j + 1] - dm1, dst[3 * j + 2] - dm2};
+    const double w = weights ? (double)weights[c] : 1.0;
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int cc = 0; cc < 3; ++cc) v[r * 3 + cc] += w * (double)(q[r] * u[cc]);
+  }
+  block_sum_to_slab<9, kBS>(v, lds, slab + blockIdx.x * 9);
+}
+
 // Kabsch on the reduced sums (align_icp.cpp:122, 139-151).
 __device__ void p2point_update(const double* tot, const IcpParams& prm, IcpState* st,
                                float* trace) {
@@ -602,6 +647,37 @@ int kabsch_device(rst_ctx* ctx, const double cov[9], const float smean[3], const
   k_kabsch<<<1, 64, 0, st>>>(buf, (float*)(buf + 16));
   RST_HIP(hipGetLastError());
   RST_HIP(hipMemcpyAsync(pose_out, buf + 16, sizeof(float) * 16, hipMemcpyDeviceToHost, st));
+  RST_HIP(hipStreamSynchronize(st));
+  return RST_OK;
+}
+
+// cov (row-major sums from k_pairs_cov) + means -> k_kabsch's input layout
+__global__ void k_pairs_pack(const double* __restrict__ tot6, const double* __restrict__ tot9,
+                             int64_t k, double* __restrict__ out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < 3; ++c) RST_M3(out, r, c) = tot9[r * 3 + c];
+  for (int a = 0; a < 6; ++a) out[9 + a] = (double)(float)(tot6[a] / (double)k);
+}
+
+int solve_kabsch_device(rst_ctx* ctx, const float* d_src, const float* d_dst,
+                        const int32_t* d_pairs, const float* d_w, int64_t k,
+                        float pose_out[16]) {
+  const int nb = std::min(1024, blocks_for(k));
+  double* slab = nullptr;
+  RST_CHECK(ctx_slab(ctx, sizeof(double) * (9 * (size_t)nb + 64), &slab));
+  double* tot6 = slab + 9 * (size_t)nb;
+  double* tot9 = tot6 + 8;
+  double* packed = tot9 + 16;  // 15 in, 16 floats out
+  hipStream_t st = ctx->stream;
+  k_pairs_sum<<<nb, kBS, 0, st>>>(d_src, d_dst, d_pairs, k, slab);
+  k_slab_reduce<6><<<1, kRedBS, 0, st>>>(slab, nb, slab, 0, nullptr, tot6);
+  k_pairs_cov<<<nb, kBS, 0, st>>>(d_src, d_dst, d_pairs, d_w, k, tot6, slab);
+  k_slab_reduce<9><<<1, kRedBS, 0, st>>>(slab, nb, slab, 0, nullptr, tot9);
+  k_pairs_pack<<<1, 64, 0, st>>>(tot6, tot9, k, packed);
+  k_kabsch<<<1, 64, 0, st>>>(packed, (float*)(packed + 16));
+  RST_HIP(hipGetLastError());
+  RST_HIP(hipMemcpyAsync(pose_out, packed + 16, sizeof(float) * 16, hipMemcpyDeviceToHost, st));
   RST_HIP(hipStreamSynchronize(st));
   return RST_OK;
 }

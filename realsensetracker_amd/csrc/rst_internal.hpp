@@ -150,6 +150,8 @@ int icp_align_prepared(rst_ctx* ctx, const rst_target* src,
                        const rst_target* tgt, const rst_icp_opts* opts,
                        float pose_inout[16], float* mean_cost,
                        int32_t* iters_run, rst_comm* comm);
+int solve_kabsch_device(rst_ctx* ctx, const float* d_src, const float* d_dst,
+                        const int32_t* d_pairs, const float* d_w, int64_t k, float pose_out[16]);
 int centroid_device(rst_ctx* ctx, const float4* d_pts, int64_t n,
                     double* d_out3);
 int kabsch_device(rst_ctx* ctx, const double cov[9], const float smean[3],

@@ -1,0 +1,83 @@
+"""Multi-GPU ICP: the source cloud sharded across ranks (one process per GPU).
+
+The reference has no distribution; this is the build's
+scaling of AlignIcp3d (align_icp.cpp:92-153) to one node:
+
+* the target index is replicated (every rank builds it from the same frame);
+* the source splits into contiguous shards, ``shard_bounds``;
+* per iteration every rank reduces its 16 (P2POINT_REF) / 30 (P2PLANE) fp64
+  partial sums to one row and ONE RCCL all-reduce over xGMI makes them
+  global; every rank then solves the same pose (no broadcast).
+
+Host logic only: the RCCL communicator is created from a unique id that
+rank 0 draws and ``torch.distributed`` broadcasts (any backend; gloo in the
+CPU tests).  The per-iteration exchange is inside librst_align.so
+(``rst_icp_align_sharded_device``).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib as L
+
+
+def shard_bounds(n: int, world: int, rank: int) -> tuple[int, int]:
+    """Contiguous [lo, hi) of n source points for `rank`; shard sizes differ
+    by at most one and the shards tile [0, n) in rank order."""
+    if world < 1 or not 0 <= rank < world or n < 0:
+        raise ValueError("bad shard spec")
+    base, extra = divmod(n, world)
+    lo = rank * base + min(rank, extra)
+    return lo, lo + base + (1 if rank < extra else 0)
+
+
+def exchange_unique_id(group=None) -> bytes:
+    """Rank 0 draws the RCCL unique id; every rank returns the same bytes."""
+    import torch.distributed as dist
+    buf = [None]
+    if dist.get_rank(group) == 0:
+        raw = C.create_string_buffer(L.COMM_ID_BYTES)
+        L.check(L.lib().rst_comm_get_unique_id(raw), "rst_comm_get_unique_id")
+        buf[0] = raw.raw
+    dist.broadcast_object_list(buf, src=0, group=group)
+    assert isinstance(buf[0], bytes) and len(buf[0]) == L.COMM_ID_BYTES
+    return buf[0]
+
+
+class ShardedAligner:
+    """One rank's side of the sharded ICP.  Every rank calls ``align`` with
+    its own shard (device pointer, see ``shard_bounds``) and the replicated
+    target; all ranks return the same pose."""
+
+    def __init__(self, ctx, group=None):
+        import torch.distributed as dist
+        self.ctx = ctx
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        uid = exchange_unique_id(group)
+        self._comm = C.c_void_p()
+        L.check(L.lib().rst_comm_create(ctx.handle, uid, self.world, self.rank,
+                                        C.byref(self._comm)), "rst_comm_create")
+
+    def align(self, d_src_shard: int, n_shard: int, target, opts=None, pose=None):
+        pose = np.eye(4, dtype=np.float32) if pose is None else np.asarray(pose, np.float32)
+        buf = L.pose_to_cm(pose)
+        mc = C.c_float(0)
+        o = opts if opts is not None else L.default_opts()
+        st = L.check(L.lib().rst_icp_align_sharded_device(
+            self.ctx.handle, self._comm, C.c_void_p(d_src_shard), int(n_shard), target.handle,
+            C.byref(o), L.fptr(buf), C.byref(mc)), "rst_icp_align_sharded_device")
+        return st == L.RST_OK, L.cm_to_pose(buf), float(mc.value)
+
+    def close(self):
+        if self._comm:
+            L.lib().rst_comm_destroy(self._comm)
+            self._comm = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

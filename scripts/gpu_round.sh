@@ -12,7 +12,7 @@ step() {  # name, limit, command...
   echo "$name rc=$rc"; tail -5 gpurun_out/$name.log
   [ $rc -eq 0 ] || exit $rc
 }
-step pytest_gpu 600 python -m pytest tests/ -x -q -m gpu
+step pytest_gpu 600 python -u -m pytest tests/ -x -v -m gpu --timeout 120 --timeout-method thread
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 600 python bench.py
 step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${TAG} -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu

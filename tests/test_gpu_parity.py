@@ -357,3 +357,29 @@ def test_frame_prepare_device(ctx):
     assert len(t) == len(g["dst"])
     idx, d2 = t.query(g["src"])
     assert np.array_equal(idx, g["nn_idx0"]) and np.array_equal(d2, g["nn_d20"])
+
+
+# ---- SolveKabsch (align_icp.cpp:18-71) -------------------------------------------------
+@pytest.mark.parametrize("weighted", [False, True])
+def test_solve_kabsch_device_vs_oracle(ctx, weighted):
+    g = load_golden("pair_120x90_s1")
+    src, dst = g["src"], g["dst"]
+    pairs = np.stack([np.arange(len(src)), g["nn_idx0"]], 1).astype(np.int32)
+    rng = np.random.default_rng(5)
+    w = rng.uniform(0.0, 1.0, len(src)).astype(np.float32) if weighted else None
+    ok_o, To = O.solve_kabsch(src, dst, pairs, w)
+    T = np.eye(4, dtype=np.float32)
+    assert A.SolveKabsch(src, dst, pairs, w, T) == ok_o
+    # means: fp64 device sums vs the reference's fp32 sequential sums
+    assert max(pose_err(T, To)) <= 1e-5
+
+
+def test_solve_kabsch_device_contract(ctx):
+    T0 = np.eye(4, dtype=np.float32)
+    T0[2, 3] = 0.3
+    T = T0.copy()
+    assert not A.SolveKabsch(np.zeros((2, 3), np.float32), np.ones((9, 3), np.float32),
+                             [[0, 0]], None, T)
+    assert np.array_equal(T, T0)
+    with pytest.raises(L.RstError):
+        A.SolveKabsch(np.ones((9, 3), np.float32), np.ones((9, 3), np.float32), [[0, 9]], None, T)

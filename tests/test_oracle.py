@@ -162,3 +162,40 @@ def test_normals_oracle_unit_and_oriented():
     n = g["normals_dst"]
     np.testing.assert_allclose(np.linalg.norm(n, axis=1), 1.0, atol=1e-5)
     assert np.all(np.sum(g["dst"] * n, axis=1) <= 0)  # face the viewpoint (origin)
+
+
+def test_solve_kabsch_oracle_recovers_motion_and_matches_numpy():
+    """SolveKabsch (align_icp.cpp:18-71): exact correspondences under a known
+    rigid motion give that motion; weights enter the covariance linearly."""
+    from realsensetracker_amd import driver
+    rng = np.random.default_rng(7)
+    src = rng.uniform(-1, 1, size=(500, 3)).astype(np.float32)
+    D = driver.random_offset(rng, deg=(5.0, 10.0), cm=(5.0, 10.0))
+    dst = (src.astype(np.float64) @ D[:3, :3].T + D[:3, 3]).astype(np.float32)
+    perm = rng.permutation(500)
+    dst_p = dst[perm]
+    inv = np.argsort(perm)
+    pairs = np.stack([np.arange(500), inv], 1)
+    ok, T = O.solve_kabsch(src, dst_p, pairs)
+    assert ok
+    assert max(pose_err(T, D)) < 2e-6
+    w = rng.uniform(0.1, 1.0, 500).astype(np.float32)
+    ok, Tw = O.solve_kabsch(src, dst_p, pairs, w)
+    assert ok and max(pose_err(Tw, D)) < 2e-6
+    # the weighted covariance in numpy -> the same Kabsch
+    sm = np.cumsum(src[pairs[:, 0]], 0, dtype=np.float32)[-1] / np.float32(500)
+    dm = np.cumsum(dst_p[pairs[:, 1]], 0, dtype=np.float32)[-1] / np.float32(500)
+    u = src[pairs[:, 0]] - sm
+    v = dst_p[pairs[:, 1]] - dm
+    cov = (w[:, None, None].astype(np.float64) *
+           (v[:, :, None] * u[:, None, :]).astype(np.float64)).sum(0)
+    Tn = O.kabsch_pose(cov, sm, dm)
+    assert max(pose_err(Tw, Tn)) < 1e-6
+
+
+def test_solve_kabsch_oracle_too_few_points():
+    T0 = np.eye(4, dtype=np.float32)
+    T0[0, 3] = 0.5
+    ok, T = O.solve_kabsch(np.zeros((2, 3), np.float32), np.zeros((10, 3), np.float32),
+                           [[0, 0], [1, 1]], T=T0)
+    assert not ok and np.array_equal(T, T0)
