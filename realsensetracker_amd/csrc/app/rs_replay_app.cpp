@@ -11,6 +11,7 @@
 // Prints per-frame timing and drift against the scene's ground truth.
 //
 //   rs_replay_app [--frames N] [--width W] [--height H] [--iters K] [--seed S]
+//                 [--dump FILE]   (per-frame xfm, one line of 16 col-major floats)
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -26,6 +27,7 @@ namespace {
 struct Args {
   int frames = 10, width = 640, height = 480, iters = 128;
   uint64_t seed = 0;
+  const char* dump = nullptr;  // write each frame's xfm (16 floats, col-major)
 };
 
 Args Parse(int argc, char** argv) {
@@ -38,6 +40,7 @@ Args Parse(int argc, char** argv) {
     else if (k == "--height") a.height = (int)v;
     else if (k == "--iters") a.iters = (int)v;
     else if (k == "--seed") a.seed = (uint64_t)v;
+    else if (k == "--dump") a.dump = argv[i + 1];
     else { std::fprintf(stderr, "unknown flag %s\n", k.c_str()); std::exit(2); }
   }
   return a;
@@ -110,6 +113,7 @@ int main(int argc, char** argv) {
   rs_tracker::Isometry3f total_xfm = rs_tracker::Isometry3f::Identity();
   double worst_ang = 0.0, worst_tr = 0.0, total_ms = 0.0;
   int ok_count = 0;
+  FILE* dump = a.dump ? std::fopen(a.dump, "w") : nullptr;
   for (int f = 1; f < a.frames; ++f) {
     rs_tracker::Cloud3f cloud = grab(f, Tf);
     rs_tracker::Isometry3f xfm = rs_tracker::Isometry3f::Identity();
@@ -118,6 +122,11 @@ int main(int argc, char** argv) {
     const double ms =
         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     total_ms += ms;
+    if (dump) {
+      float x[16];
+      rs_tracker::ToColMajor(xfm, x);
+      for (int k = 0; k < 16; ++k) std::fprintf(dump, "%.9g%c", x[k], k == 15 ? '\n' : ' ');
+    }
     if (suc) {
       total_xfm = total_xfm * xfm;
       prev = std::move(cloud);
@@ -137,6 +146,7 @@ int main(int argc, char** argv) {
   }
   std::printf("frames %d  aligned %d  mean align %.2f ms  worst drift %.2e rad %.2e m\n",
               a.frames - 1, ok_count, total_ms / std::max(1, a.frames - 1), worst_ang, worst_tr);
+  if (dump) std::fclose(dump);
   rst_scene_destroy(scene);
   return ok_count == a.frames - 1 ? 0 : 1;
 }
