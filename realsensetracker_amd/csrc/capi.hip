@@ -357,6 +357,40 @@ int rst_debug_query_nn_warm_stats(rst_ctx* ctx, const rst_target* t, const float
   return s < 0 ? s : RST_OK;
 }
 
+int rst_debug_query_nn_fallback(rst_ctx* ctx, const rst_target* t, const float* q, int64_t nq,
+                                const int32_t* warm, int mode, int32_t* idx, float* d2,
+                                int32_t* path) {
+  if (!ctx || !t || nq < 0 || (nq > 0 && (!q || !idx || !d2 || !path))) return RST_E_ARG;
+  if (mode != 0 && mode != 2 && mode != 3 && mode != 23) return RST_E_ARG;
+  if (nq == 0) return RST_OK;
+  if (t->m == 0) return RST_E_ARG;
+  RST_HIP(hipSetDevice(ctx->device));
+  float* dq = nullptr;
+  RST_CHECK(upload_xyz(ctx, q, nq, &dq));
+  void* dout = nullptr;
+  int s = ctx_workspace(ctx, (3 * sizeof(int32_t) + sizeof(float)) * nq + 256, &dout);
+  int32_t* dwarm = nullptr;
+  int32_t* di = (int32_t*)dout;
+  float* dd = (float*)(di + nq);
+  int32_t* dp = (int32_t*)(dd + nq);
+  if (s >= 0 && warm) {
+    dwarm = dp + nq;
+    if (hipMemcpyAsync(dwarm, warm, sizeof(int32_t) * nq, hipMemcpyHostToDevice, ctx->stream) !=
+        hipSuccess)
+      s = RST_E_HIP;
+  }
+  if (s >= 0) s = query_nn_fallback_device(ctx, t, dq, nq, dwarm, mode, di, dd, dp);
+  if (s >= 0 &&
+      (hipMemcpyAsync(idx, di, sizeof(int32_t) * nq, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+       hipMemcpyAsync(d2, dd, sizeof(float) * nq, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+       hipMemcpyAsync(path, dp, sizeof(int32_t) * nq, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+       hipStreamSynchronize(ctx->stream) != hipSuccess))
+    s = RST_E_HIP;
+  hipStreamSynchronize(ctx->stream);
+  hipFree(dq);
+  return s < 0 ? s : RST_OK;
+}
+
 int rst_debug_queue_trace(rst_ctx* ctx, int32_t* out, int32_t n) {
   if (!ctx || !out || n < 0) return RST_E_ARG;
   for (int i = 0; i < n && i < kQTrace; ++i) {

@@ -31,7 +31,6 @@ constexpr int kBS = 256;
 constexpr int kNP2Point = 16;  // sum w q u^T (9), sum w u (3), sum q (3), sum d2
 constexpr int kNP2Plane = 30;  // A (21), b (6), sum w r^2, count, sum d2
 constexpr int kFbBlocks = 2048;  // fixed grid of the fallback kernel (8192 waves)
-constexpr bool kL2InNn = false;  // kernel 1 also tries the level-2 adjacency
 
 __device__ __forceinline__ Pose3 load_pose(const IcpState* __restrict__ st) {
   Pose3 P;
@@ -181,6 +180,7 @@ struct AccArgs {
 // no neighbour -> q = dst[0], d2 = FLT_MAX (the query's untouched outputs).
 struct P2PointAcc {
   static constexpr int NV = kNP2Point;  // sum w q u^T (9), sum w u (3), sum q (3), sum d2
+  static constexpr int RS = 16;         // slab row stride (doubles; divides kRedBS)
   static constexpr bool kCanFinish = false;
   __device__ static void add(double (&v)[NV], const BvhView& bv, const AccArgs& a, const Uni& u,
                              const float4& s, float px, float py, float pz, float bd, int bp) {
@@ -204,6 +204,7 @@ struct P2PointAcc {
 // J = [p x n ; n]; 21 + 6 + 3 sums.
 struct P2PlaneAcc {
   static constexpr int NV = kNP2Plane;  // A (21), b (6), sum w r^2, count, sum d2
+  static constexpr int RS = 32;
   static constexpr bool kCanFinish = true;
   __device__ static void add(double (&v)[NV], const BvhView& bv, const AccArgs& a, const Uni& u,
                              const float4& s, float px, float py, float pz, float bd, int bp) {
@@ -234,6 +235,53 @@ struct P2PlaneAcc {
 };
 
 // ---- kernel 1: adjacency search, one point per thread ----------------------------------
+// Exclusive prefix of the per-block queue counts (one block, kBS threads):
+// pref[b] = entries before block b's segment, pref[nb] = E.
+__device__ void queue_prefix(const int32_t* __restrict__ qcnt, int nb, int32_t* __restrict__ pref,
+                             IcpState* __restrict__ st) {
+  __shared__ int part[kBS + 1];
+  const int per = (nb + kBS - 1) / kBS;
+  const int b0 = threadIdx.x * per;
+  int sum = 0;
+  for (int b = b0; b < b0 + per && b < nb; ++b) sum += __builtin_nontemporal_load(qcnt + b);
+  part[threadIdx.x] = sum;
+  __syncthreads();
+  if (threadIdx.x < kWave) {  // one wave scans the kBS partials, 4 per lane
+    const int l = threadIdx.x;
+    int a[kBS / kWave], t = 0;
+#pragma unroll
+    for (int k = 0; k < kBS / kWave; ++k) {
+      a[k] = part[l * (kBS / kWave) + k];
+      t += a[k];
+    }
+    int inc = t;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+      const int y = __shfl_up(inc, o, kWave);
+      if (l >= o) inc += y;
+    }
+    int acc = inc - t;
+#pragma unroll
+    for (int k = 0; k < kBS / kWave; ++k) {
+      part[l * (kBS / kWave) + k] = acc;
+      acc += a[k];
+    }
+    if (l == kWave - 1) part[kBS] = inc;
+  }
+  __syncthreads();
+  int acc = part[threadIdx.x];
+  for (int b = b0; b < b0 + per && b < nb; ++b) {
+    pref[b] = acc;
+    acc += __builtin_nontemporal_load(qcnt + b);
+  }
+  if (threadIdx.x == 0) {
+    const int E = part[kBS];
+    pref[nb] = E;
+    st->fb_e = E;
+    if (st->iter < kQTrace) st->qlen[st->iter] = E;
+  }
+}
+
 template <class Acc>
 __global__ __launch_bounds__(kBS) void k_icp_nn(BvhView bv, AdjView av, AccArgs aa,
                                                 const float4* __restrict__ src, int64_t n,
@@ -267,8 +315,7 @@ __global__ __launch_bounds__(kBS) void k_icp_nn(BvhView bv, AdjView av, AccArgs 
     const float4 w = bv.pts[warm];
     r.offer(d2_ref(px, py, pz, w.x, w.y, w.z), f2i(w.w), warm);
   }
-  bool done = act && (!fin || adj_search_wide(bv, av, warm, px, py, pz, r));
-  if (kL2InNn && act && !done) done = adj2_search(bv, av, r.pos >= 0 ? r.pos : warm, px, py, pz, r);
+  const bool done = act && (!fin || adj_search_wide(bv, av, warm, px, py, pz, r));
   // lanes the adjacency could not certify go to the fallback queue, in
   // point order within the block's segment
   const bool need = act && !done;
@@ -288,92 +335,16 @@ __global__ __launch_bounds__(kBS) void k_icp_nn(BvhView bv, AdjView av, AccArgs 
     nnpos[i] = r.pos;
     Acc::add(v, bv, aa, u, s, px, py, pz, r.d, r.pos);
   }
-  block_sum_to_slab<Acc::NV, kBS>(v, lds, slab + (int64_t)blockIdx.x * Acc::NV);
+  block_sum_to_slab<Acc::NV, kBS>(v, lds, slab + (int64_t)blockIdx.x * Acc::RS);
 }
 
-// ---- kernel 2: the queued queries, one wavefront each --------------------------------
-// Queue entry e (global order: block segments in block order) is handled by
-// wave e mod W of this fixed grid; each wave adds its entries in increasing
-// e, so the slab is reproducible.
-template <class Acc>
-__global__ __launch_bounds__(kBS) void k_icp_fb(BvhView bv, AccArgs aa,
-                                                const float4* __restrict__ src,
-                                                IcpState* __restrict__ st,
-                                                int32_t* __restrict__ nnpos,
-                                                const int32_t* __restrict__ qbuf,
-                                                const int32_t* __restrict__ qcnt, int nb1,
-                                                double* __restrict__ slab2) {
-  extern __shared__ int pref[];  // [nb1 + 1]
-  __shared__ double lds[(kBS / kWave) * Acc::NV];
-  __shared__ WnnScratch wsc[kBS / kWave];
-  __shared__ int part[kBS + 1];
-  double v[Acc::NV];
-#pragma unroll
-  for (int k = 0; k < Acc::NV; ++k) v[k] = 0.0;
-  if (Acc::kCanFinish && st->done) return;  // the solve ignores the slab then
-  // exclusive prefix of the per-block queue counts
-  const int per = (nb1 + kBS - 1) / kBS;
-  const int b0 = threadIdx.x * per;
-  int sum = 0;
-  for (int b = b0; b < b0 + per && b < nb1; ++b) sum += qcnt[b];
-  part[threadIdx.x] = sum;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int acc = 0;
-    for (int t = 0; t < kBS; ++t) {
-      const int x = part[t];
-      part[t] = acc;
-      acc += x;
-    }
-    part[kBS] = acc;
-  }
-  __syncthreads();
-  {
-    int acc = part[threadIdx.x];
-    for (int b = b0; b < b0 + per && b < nb1; ++b) {
-      pref[b] = acc;
-      acc += qcnt[b];
-    }
-    if (threadIdx.x == 0) pref[nb1] = part[kBS];
-  }
-  __syncthreads();
-  const int E = pref[nb1];
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    st->fb_e = E;  // the solve reads only the slab rows of blocks with entries
-    if (st->iter < kQTrace) st->qlen[st->iter] = E;
-  }
-  const Uni u = load_uni(st);
-  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
-  const int W = gridDim.x * (kBS / kWave);
-  for (int e = blockIdx.x * (kBS / kWave) + wid; e < E; e += W) {
-    int lo = 0, hi = nb1 - 1;  // block segment holding entry e
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (pref[mid] <= e)
-        lo = mid;
-      else
-        hi = mid - 1;
-    }
-    const int i = qbuf[lo * (int64_t)kBS + (e - pref[lo])];
-    const float4 s = src[i];
-    float px, py, pz;
-    xform(u.P, s.x, s.y, s.z, px, py, pz);
-    const bool fin = finite3(px, py, pz);
-    int warm = nnpos[i];
-    if (fin && warm < 0) warm = morton_seed(bv, px, py, pz);
-    Best1 r;
-    r.init();
-    if (fin) {
-      const float4 w = bv.pts[warm];
-      r.offer(d2_ref(px, py, pz, w.x, w.y, w.z), f2i(w.w), warm);
-    }
-    nn_wave_one(bv, warm, px, py, pz, r, wsc[wid]);
-    if (lane == 0) {
-      nnpos[i] = r.pos;
-      Acc::add(v, bv, aa, u, s, px, py, pz, r.d, r.pos);
-    }
-  }
-  block_sum_to_slab<Acc::NV, kBS>(v, lds, slab2 + (int64_t)blockIdx.x * Acc::NV);
+// One block: the exclusive prefix of kernel 1's per-block queue counts and
+// the queue length E (st->fb_e) for kernel 2.
+__global__ __launch_bounds__(kBS) void k_queue_prefix(const int32_t* __restrict__ qcnt, int nb,
+                                                      int32_t* __restrict__ pref,
+                                                      IcpState* __restrict__ st) {
+  if (st->done) return;
+  queue_prefix(qcnt, nb, pref, st);
 }
 
 // Kabsch solve (align_icp.cpp:139-151; SolveKabsch :58-69): fp64 SVD,
@@ -466,8 +437,7 @@ __global__ __launch_bounds__(kBS) void k_pairs_cov(const float* __restrict__ src
 }
 
 // Kabsch on the reduced sums (align_icp.cpp:122, 139-151).
-__device__ void p2point_update(const double* tot, const IcpParams& prm, IcpState* st,
-                               float* trace) {
+__device__ void p2point_update(const double* tot, const IcpParams& prm, IcpCore* st) {
   const double n = (double)prm.n;
   float dmean[3];
   for (int r = 0; r < 3; ++r) dmean[r] = (float)(tot[12 + r] / n);
@@ -481,31 +451,10 @@ __device__ void p2point_update(const double* tot, const IcpParams& prm, IcpState
   for (int k = 0; k < 3; ++k) st->t[k] = t[k];
   st->last_cost = (float)tot[15];
   const int it = st->iter;
-  if (trace) {
-    float* tp = trace + (int64_t)it * 16;
-    for (int c = 0; c < 3; ++c) {
-      for (int r = 0; r < 3; ++r) tp[c * 4 + r] = Rq[c * 3 + r];
-      tp[c * 4 + 3] = 0.f;
-    }
-    for (int r = 0; r < 3; ++r) tp[12 + r] = t[r];
-    tp[15] = 1.f;
-  }
   const int next = it + 1;
   st->iter = next;
   // :96-98 -- mu for iteration `next`
   if (next > 0 && prm.anneal_every > 0 && next % prm.anneal_every == 0) st->mu = st->mu / prm.anneal_div;
-}
-
-__global__ __launch_bounds__(kRedBS) void k_solve_p2point(const double* __restrict__ slab1,
-                                                          int rows1,
-                                                          const double* __restrict__ slab2,
-                                                          int rows2, IcpParams prm,
-                                                          IcpState* __restrict__ st,
-                                                          float* __restrict__ trace) {
-  __shared__ double red[(kRedBS / kWave) * kNP2Point];
-  __shared__ double tot[kNP2Point];
-  reduce_slab_rows<kNP2Point>(slab1, rows1, slab2, rows2, &st->fb_e, red, tot);
-  if (threadIdx.x == 0) p2point_update(tot, prm, st, trace);
 }
 
 __device__ bool chol6_solve(const double* Ap /*packed lower 21*/, const double* rhs, double* x) {
@@ -544,8 +493,7 @@ __device__ bool chol6_solve(const double* Ap /*packed lower 21*/, const double* 
   return true;
 }
 
-__device__ void p2plane_update(const double* tot, const IcpParams& prm, IcpState* st,
-                               float* trace) {
+__device__ void p2plane_update(const double* tot, const IcpParams& prm, IcpCore* st) {
   if (st->done) return;
   const double cnt = tot[28];
   double xi[6];
@@ -602,30 +550,153 @@ __device__ void p2plane_update(const double* tot, const IcpParams& prm, IcpState
   st->last_cnt = cnt;
   st->last_d2 = tot[29];
   const int it = st->iter;
-  if (trace) {
-    float* tp = trace + (int64_t)it * 16;
-    for (int c = 0; c < 3; ++c) {
-      for (int r = 0; r < 3; ++r) tp[c * 4 + r] = st->R[c * 3 + r];
-      tp[c * 4 + 3] = 0.f;
-    }
-    for (int r = 0; r < 3; ++r) tp[12 + r] = st->t[r];
-    tp[15] = 1.f;
-  }
   st->iter = it + 1;
   if (nx < (double)prm.p2plane_eps) st->done = 1;
 }
 
-__global__ __launch_bounds__(kRedBS) void k_solve_p2plane(const double* __restrict__ slab1,
-                                                          int rows1,
-                                                          const double* __restrict__ slab2,
-                                                          int rows2, IcpParams prm,
-                                                          IcpState* __restrict__ st,
-                                                          float* __restrict__ trace) {
-  __shared__ double red[(kRedBS / kWave) * kNP2Plane];
-  __shared__ double tot[kNP2Plane];
-  if (st->done) return;
-  reduce_slab_rows<kNP2Plane>(slab1, rows1, slab2, rows2, &st->fb_e, red, tot);
-  if (threadIdx.x == 0) p2plane_update(tot, prm, st, trace);
+template <class Acc>
+__device__ __forceinline__ void acc_update(const double* tot, const IcpParams& prm, IcpCore* st) {
+  if constexpr (Acc::NV == kNP2Point)
+    p2point_update(tot, prm, st);
+  else
+    p2plane_update(tot, prm, st);
+}
+
+// ---- kernel 3: fixed-order reduction of both slabs + the solve ----------------------
+// Rows of Acc::RS doubles (RS divides kRedBS): thread t sums column t % RS
+// of rows t / RS, t / RS + kRedBS / RS, ... -- coalesced loads, all in
+// flight together -- then per column a fixed-order sum over the kRedBS / RS
+// partials.  Bitwise reproducible.  slab2 holds rows for the first
+// ceil(E / waves-per-block) fallback blocks only.  Single GPU: thread 0
+// solves (align_icp.cpp:122-151); multi-GPU: the row goes to `totals` for
+// the RCCL all-reduce and k_solve_only follows.
+template <class Acc>
+__global__ __launch_bounds__(kRedBS) void k_reduce_solve(const double* __restrict__ slab1,
+                                                         int rows1,
+                                                         const double* __restrict__ slab2,
+                                                         int rows2max, IcpParams prm,
+                                                         IcpState* __restrict__ st,
+                                                         double* __restrict__ totals) {
+  constexpr int RS = Acc::RS, PER = kRedBS / RS;
+  __shared__ double red[kRedBS];
+  __shared__ double tot[RS];
+  if (Acc::kCanFinish && st->done) return;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  IcpCore core;
+  if (threadIdx.x == 0 && !totals) core = *static_cast<const IcpCore*>(st);  // loads in flight
+  const int E = st->fb_e;
+  const int rows2 = max(1, min(rows2max, (E + kBS / kWave - 1) / (kBS / kWave)));
+  const int t = threadIdx.x, col = t % RS;
+  // unrolled so a thread's loads are all in flight before the first add
+  // waits (a rolled loop pays one memory latency per row)
+  double acc = 0.0;
+#pragma unroll 16
+  for (int r = t / RS; r < rows1; r += PER) acc += __builtin_nontemporal_load(slab1 + (int64_t)r * RS + col);
+#pragma unroll 8
+  for (int r = t / RS; r < rows2; r += PER) acc += __builtin_nontemporal_load(slab2 + (int64_t)r * RS + col);
+  red[t] = acc;
+  __syncthreads();
+  if (t < RS) {
+    double x = 0.0;
+    for (int j = 0; j < PER; ++j) x += red[j * RS + t];
+    tot[t] = x;
+  }
+  __syncthreads();
+  if (totals) {
+    if (t < Acc::NV) totals[t] = tot[t];
+  } else if (t == 0) {
+    const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+    const int it = core.iter;
+    acc_update<Acc>(tot, prm, &core);
+    *static_cast<IcpCore*>(st) = core;
+    const uint64_t t2 = __builtin_amdgcn_s_memrealtime();
+    if (it < kQTrace) {  // diagnostics (rst_debug_queue_trace): 10 ns ticks
+      st->path[it][1] = (int)(t1 - t0);
+      st->path[it][2] = (int)(t2 - t1);
+    }
+  }
+}
+
+// Multi-GPU: the all-reduced row -> the same solve on every rank.
+template <class Acc>
+__global__ void k_solve_only(const double* __restrict__ totals, IcpParams prm,
+                             IcpState* __restrict__ st) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  IcpCore core = *static_cast<const IcpCore*>(st);
+  if (Acc::kCanFinish && core.done) return;
+  double tot[Acc::NV];
+  for (int k = 0; k < Acc::NV; ++k) tot[k] = totals[k];
+  acc_update<Acc>(tot, prm, &core);
+  *static_cast<IcpCore*>(st) = core;
+}
+
+// ---- kernel 2: the queued queries, one wavefront each --------------------------------
+// Queue entry e (global order: block segments in block order, prefix from
+// kernel 1's tail) is handled by wave e mod W of this fixed grid; each wave
+// adds its entries in increasing e, so the slab is reproducible.  Only the
+// first nw = max(1, ceil(E / waves-per-block)) blocks have work; the others
+// exit at once.  The last of the nw blocks to finish reduces both slabs in a
+// fixed order and, single-GPU, solves the pose (align_icp.cpp:122-151);
+// multi-GPU it leaves the reduced row in `totals` for the RCCL all-reduce.
+template <class Acc>
+__global__ __launch_bounds__(kBS) void k_icp_fb(BvhView bv, AdjView av, AccArgs aa,
+                                                const float4* __restrict__ src,
+                                                IcpState* __restrict__ st,
+                                                int32_t* __restrict__ nnpos,
+                                                const int32_t* __restrict__ qbuf,
+                                                const int32_t* __restrict__ gpref, int nb1,
+                                                double* __restrict__ slab2) {
+  extern __shared__ int pref[];  // [nb1 + 1]
+  __shared__ double lds[(kBS / kWave) * Acc::NV];
+  __shared__ WnnScratch wsc[kBS / kWave];
+  if (Acc::kCanFinish && st->done) return;  // converged: nothing reads the slabs
+  const int E = st->fb_e;
+  const int nw = max(1, min((int)gridDim.x, (E + kBS / kWave - 1) / (kBS / kWave)));
+  if ((int)blockIdx.x >= nw) return;
+  double v[Acc::NV];
+#pragma unroll
+  for (int k = 0; k < Acc::NV; ++k) v[k] = 0.0;
+  if (E > 0) {
+    for (int b = threadIdx.x; b <= nb1; b += kBS) pref[b] = gpref[b];
+    __syncthreads();
+    const Uni u = load_uni(st);
+    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+    const int W = gridDim.x * (kBS / kWave);
+    for (int e = blockIdx.x * (kBS / kWave) + wid; e < E; e += W) {
+      int lo = 0, hi = nb1 - 1;  // block segment holding entry e
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (pref[mid] <= e)
+          lo = mid;
+        else
+          hi = mid - 1;
+      }
+      const int i = qbuf[lo * (int64_t)kBS + (e - pref[lo])];
+      const float4 s = src[i];
+      float px, py, pz;
+      xform(u.P, s.x, s.y, s.z, px, py, pz);
+      const bool fin = finite3(px, py, pz);
+      int warm = nnpos[i];
+      if (fin && warm < 0) warm = morton_seed(bv, px, py, pz);
+      Best1 r;
+      r.init();
+      if (fin) {
+        const float4 w = bv.pts[warm];
+        r.offer(d2_ref(px, py, pz, w.x, w.y, w.z), f2i(w.w), warm);
+      }
+      // the level-2 and level-3 adjacency cover most far queries in a few
+      // memory round trips; the full walk from the warm leaf is exact for
+      // anything else
+      if (!nn_wave_adj(bv, av, kAdj2Shift, warm, px, py, pz, r, wsc[wid]) &&
+          !nn_wave_adj(bv, av, kAdj3Shift, warm, px, py, pz, r, wsc[wid]))
+        nn_wave_one(bv, warm, px, py, pz, r, wsc[wid]);
+      if (lane == 0) {
+        nnpos[i] = r.pos;
+        Acc::add(v, bv, aa, u, s, px, py, pz, r.d, r.pos);
+      }
+    }
+  }
+  block_sum_to_slab<Acc::NV, kBS>(v, lds, slab2 + (int64_t)blockIdx.x * Acc::RS);
 }
 
 inline int blocks_for(int64_t n) { return (int)std::max<int64_t>(1, (n + kBS - 1) / kBS); }
@@ -709,13 +780,14 @@ int icp_align_prepared(rst_ctx* ctx, const rst_target* src, const rst_target* tg
   // one scratch buffer: [centroid / kernel-1 slab | kernel-2 slab | totals]
   const int nblk = blocks_for(n_local);
   const int NV = p2plane ? kNP2Plane : kNP2Point;
+  const int RS = p2plane ? P2PlaneAcc::RS : P2PointAcc::RS;
   const int ncb = std::min(1024, blocks_for(n_local));
-  const size_t rows1 = (size_t)std::max(nblk * NV, ncb * 4);
-  const size_t slab_doubles = rows1 + (size_t)kFbBlocks * NV + 64;
+  const size_t rows1 = (size_t)std::max(nblk * RS, ncb * 4);
+  const size_t slab_doubles = rows1 + (size_t)kFbBlocks * RS + 64;
   double* slab = nullptr;
   RST_CHECK(ctx_slab(ctx, sizeof(double) * slab_doubles, &slab));
   double* slab2 = slab + rows1;
-  double* totals = slab2 + (size_t)kFbBlocks * NV;  // 64 doubles
+  double* totals = slab2 + (size_t)kFbBlocks * RS;  // 64 doubles
 
   // n_total and the centroid are global quantities under sharding
   if (comm) {
@@ -754,15 +826,16 @@ int icp_align_prepared(rst_ctx* ctx, const rst_target* src, const rst_target* tg
   // per source point: sorted target position of its last neighbour (warm
   // start of the next iteration's exact search; -1 = cold); the fallback
   // queue (one kBS segment per kernel-1 block) and its per-block counts
-  int32_t *nnpos = nullptr, *qbuf = nullptr, *qcnt = nullptr;
+  int32_t *nnpos = nullptr, *qbuf = nullptr, *qcnt = nullptr, *pref = nullptr;
   {
     const size_t np = (size_t)std::max<int64_t>(n_local, 1);
     const size_t nq = (size_t)nblk * kBS;
     void* w = nullptr;
-    RST_CHECK(ctx_workspace(ctx, sizeof(int32_t) * (np + nq + nblk + 64), &w));
+    RST_CHECK(ctx_workspace(ctx, sizeof(int32_t) * (np + nq + 2 * nblk + 64), &w));
     nnpos = (int32_t*)w;
     qbuf = nnpos + np;
     qcnt = qbuf + nq;
+    pref = qcnt + nblk;
     RST_HIP(hipMemsetAsync(nnpos, 0xff, sizeof(int32_t) * np, st));
   }
   AccArgs aa;
@@ -794,6 +867,7 @@ int icp_align_prepared(rst_ctx* ctx, const rst_target* src, const rst_target* tg
       ctx->ev.push_back(e);
     }
   }
+  double* red_out = comm ? totals : nullptr;  // multi-GPU: reduce only
   for (int it = 0; it < opts.max_iter; ++it) {
     if (timing) RST_HIP(hipEventRecord(ctx->ev[2 * it], st));
     if (n_local > 0) {
@@ -801,35 +875,32 @@ int icp_align_prepared(rst_ctx* ctx, const rst_target* src, const rst_target* tg
         k_icp_nn<P2PlaneAcc><<<nblk, kBS, 0, st>>>(bv, av, aa, src->pts, n_local, ctx->d_state,
                                                    nnpos, qbuf, qcnt, slab);
         if (timing) RST_HIP(hipEventRecord(ctx->ev[2 * it + 1], st));
-        k_icp_fb<P2PlaneAcc><<<kFbBlocks, kBS, fb_lds, st>>>(bv, aa, src->pts, ctx->d_state, nnpos,
-                                                             qbuf, qcnt, nblk, slab2);
+        k_queue_prefix<<<1, kBS, 0, st>>>(qcnt, nblk, pref, ctx->d_state);
+        k_icp_fb<P2PlaneAcc><<<kFbBlocks, kBS, fb_lds, st>>>(bv, av, aa, src->pts, ctx->d_state, nnpos,
+                                                             qbuf, pref, nblk, slab2);
+        k_reduce_solve<P2PlaneAcc><<<1, kRedBS, 0, st>>>(slab, nblk, slab2, kFbBlocks, prm,
+                                                         ctx->d_state, red_out);
       } else {
         k_icp_nn<P2PointAcc><<<nblk, kBS, 0, st>>>(bv, av, aa, src->pts, n_local, ctx->d_state,
                                                    nnpos, qbuf, qcnt, slab);
         if (timing) RST_HIP(hipEventRecord(ctx->ev[2 * it + 1], st));
-        k_icp_fb<P2PointAcc><<<kFbBlocks, kBS, fb_lds, st>>>(bv, aa, src->pts, ctx->d_state, nnpos,
-                                                             qbuf, qcnt, nblk, slab2);
-      }
-    } else if (timing) {
-      RST_HIP(hipEventRecord(ctx->ev[2 * it + 1], st));
-    }
-    const int rows = n_local > 0 ? nblk : 0;
-    const int rows2 = n_local > 0 ? kFbBlocks : 0;
-    if (comm) {
-      if (p2plane) {
-        k_slab_reduce<kNP2Plane><<<1, kRedBS, 0, st>>>(slab, rows, slab2, rows2, &ctx->d_state->fb_e, totals);
-        RST_CHECK(comm_allreduce_sum_f64(comm, totals, kNP2Plane, st));
-        k_solve_p2plane<<<1, kRedBS, 0, st>>>(totals, 1, totals, 0, prm, ctx->d_state, nullptr);
-      } else {
-        k_slab_reduce<kNP2Point><<<1, kRedBS, 0, st>>>(slab, rows, slab2, rows2, &ctx->d_state->fb_e, totals);
-        RST_CHECK(comm_allreduce_sum_f64(comm, totals, kNP2Point, st));
-        k_solve_p2point<<<1, kRedBS, 0, st>>>(totals, 1, totals, 0, prm, ctx->d_state, nullptr);
+        k_queue_prefix<<<1, kBS, 0, st>>>(qcnt, nblk, pref, ctx->d_state);
+        k_icp_fb<P2PointAcc><<<kFbBlocks, kBS, fb_lds, st>>>(bv, av, aa, src->pts, ctx->d_state, nnpos,
+                                                             qbuf, pref, nblk, slab2);
+        k_reduce_solve<P2PointAcc><<<1, kRedBS, 0, st>>>(slab, nblk, slab2, kFbBlocks, prm,
+                                                         ctx->d_state, red_out);
       }
     } else {
+      if (timing) RST_HIP(hipEventRecord(ctx->ev[2 * it + 1], st));
+      // an empty shard still joins the all-reduce with zero partial sums
+      RST_HIP(hipMemsetAsync(totals, 0, sizeof(double) * NV, st));
+    }
+    if (comm) {
+      RST_CHECK(comm_allreduce_sum_f64(comm, totals, NV, st));
       if (p2plane)
-        k_solve_p2plane<<<1, kRedBS, 0, st>>>(slab, rows, slab2, rows2, prm, ctx->d_state, nullptr);
+        k_solve_only<P2PlaneAcc><<<1, 64, 0, st>>>(totals, prm, ctx->d_state);
       else
-        k_solve_p2point<<<1, kRedBS, 0, st>>>(slab, rows, slab2, rows2, prm, ctx->d_state, nullptr);
+        k_solve_only<P2PointAcc><<<1, 64, 0, st>>>(totals, prm, ctx->d_state);
     }
   }
   RST_HIP(hipGetLastError());

@@ -66,6 +66,48 @@ __global__ __launch_bounds__(kBS) void k_query_nn_warm(BvhView bv, const int32_t
   }
 }
 
+// The ICP fallback's per-query searches (icp.hip k_icp_fb), one wavefront
+// per query, for testing: mode 0 = the full walk from the warm leaf; 2 / 3 =
+// the level-2 / level-3 adjacency first (then the walk when not covered);
+// 23 = level 2, then 3, then the walk (what the ICP loop does).  path[i] =
+// the strategy that answered (2, 3 or 0).
+__global__ __launch_bounds__(kBS) void k_query_nn_fallback(BvhView bv, AdjView av,
+                                                           const int32_t* __restrict__ inv,
+                                                           const float* __restrict__ q,
+                                                           int64_t nq,
+                                                           const int32_t* __restrict__ warm,
+                                                           int mode, int32_t* __restrict__ idx,
+                                                           float* __restrict__ d2,
+                                                           int32_t* __restrict__ path) {
+  __shared__ WnnScratch wsc[kBS / kWave];
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+  const int64_t i = blockIdx.x * (int64_t)(kBS / kWave) + wid;
+  if (i >= nq) return;  // wave-uniform
+  const float qx = q[3 * i], qy = q[3 * i + 1], qz = q[3 * i + 2];
+  Best1 r;
+  r.init();
+  int start = -1;
+  const int w = warm ? warm[i] : -1;
+  if (w >= 0 && w < bv.m && finite3(qx, qy, qz)) {
+    start = inv[w];
+    const float4 p = bv.pts[start];
+    r.offer(d2_ref(qx, qy, qz, p.x, p.y, p.z), f2i(p.w), start);
+  }
+  int how = 0;
+  if ((mode == 2 || mode == 23) && nn_wave_adj(bv, av, kAdj2Shift, start, qx, qy, qz, r, wsc[wid]))
+    how = 2;
+  else if ((mode == 3 || mode == 23) &&
+           nn_wave_adj(bv, av, kAdj3Shift, start, qx, qy, qz, r, wsc[wid]))
+    how = 3;
+  else
+    nn_wave_one(bv, start, qx, qy, qz, r, wsc[wid]);
+  if (lane == 0) {
+    idx[i] = r.pos >= 0 ? r.id : 0;
+    d2[i] = r.d;
+    path[i] = how;
+  }
+}
+
 template <int K>
 __global__ __launch_bounds__(kBS) void k_query_knn(BvhView bv, const float* __restrict__ q,
                                                    int64_t nq, int k,
@@ -213,6 +255,19 @@ int query_nn_warm_device(rst_ctx* ctx, const rst_target* tgt, const float* d_q, 
   if (tgt->m == 0) return query_nn_device(ctx, tgt, d_q, nq, d_idx, d_d2);
   k_query_nn_warm<<<blocks_for(nq), kBS, 0, ctx->stream>>>(view_of(tgt), tgt->inv, d_q, nq, d_warm,
                                                            d_idx, d_d2, d_stats);
+  RST_HIP(hipGetLastError());
+  return RST_OK;
+}
+
+int query_nn_fallback_device(rst_ctx* ctx, const rst_target* tgt, const float* d_q, int64_t nq,
+                             const int32_t* d_warm, int mode, int32_t* d_idx, float* d_d2,
+                             int32_t* d_path) {
+  if (!ctx || !tgt || nq < 0 || !tgt->has_bvh) return RST_E_ARG;
+  if (nq == 0) return RST_OK;
+  const int64_t nb = (nq + kBS / kWave - 1) / (kBS / kWave);
+  k_query_nn_fallback<<<(unsigned)nb, kBS, 0, ctx->stream>>>(view_of(tgt), adj_of(tgt), tgt->inv,
+                                                             d_q, nq, d_warm, mode, d_idx, d_d2,
+                                                             d_path);
   RST_HIP(hipGetLastError());
   return RST_OK;
 }

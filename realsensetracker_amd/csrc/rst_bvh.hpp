@@ -162,6 +162,7 @@ struct Best1 {
     pos = -1;
   }
   RST_HD float bound() const { return d; }
+  RST_HD float radius() const { return sqrtf(d); }
   RST_HD void offer(float d2, int id_, int pos_) {
     const bool b = lex_less(d2, id_, d, id);
     d = b ? d2 : d;

@@ -161,13 +161,19 @@ __device__ inline void svd3_jacobi(const double* a_in, double* U, double* S,
 #pragma unroll
     for (int i = 0; i < 9; ++i) U[i] = V[i];
   } else if (nz == 2) {
-    const int c0 = zc == 0 ? 1 : 0;
-    const int c1 = zc == 2 ? 1 : 2;
-    // u_z = u_c0 x u_c1, in the cyclic orientation of (c0, c1, zc)
+    // u_z = u_c0 x u_c1, in the cyclic orientation of (c0, c1, zc), with
+    // c0 = first and c1 = second non-zero column (selects, not indices:
+    // every array index stays static, so nothing lands in scratch memory)
+    double a[3], b[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      a[r] = zc == 0 ? RST_M3(U, r, 1) : RST_M3(U, r, 0);
+      b[r] = zc == 2 ? RST_M3(U, r, 1) : RST_M3(U, r, 2);
+    }
     double x[3];
-    x[0] = RST_M3(U, 1, c0) * RST_M3(U, 2, c1) - RST_M3(U, 2, c0) * RST_M3(U, 1, c1);
-    x[1] = RST_M3(U, 2, c0) * RST_M3(U, 0, c1) - RST_M3(U, 0, c0) * RST_M3(U, 2, c1);
-    x[2] = RST_M3(U, 0, c0) * RST_M3(U, 1, c1) - RST_M3(U, 1, c0) * RST_M3(U, 0, c1);
+    x[0] = a[1] * b[2] - a[2] * b[1];
+    x[1] = a[2] * b[0] - a[0] * b[2];
+    x[2] = a[0] * b[1] - a[1] * b[0];
     const double sg = (zc == 1) ? -1.0 : 1.0;  // (0,2,1) is an odd order
     // keep det(U) == det(V) so U V^T is a proper rotation
     double dv = RST_M3(V, 0, 0) * (RST_M3(V, 1, 1) * RST_M3(V, 2, 2) - RST_M3(V, 1, 2) * RST_M3(V, 2, 1)) -
@@ -175,7 +181,10 @@ __device__ inline void svd3_jacobi(const double* a_in, double* U, double* S,
                 RST_M3(V, 0, 2) * (RST_M3(V, 1, 0) * RST_M3(V, 2, 1) - RST_M3(V, 1, 1) * RST_M3(V, 2, 0));
     const double sd = dv < 0 ? -1.0 : 1.0;
 #pragma unroll
-    for (int r = 0; r < 3; ++r) RST_M3(U, r, zc) = sg * sd * x[r];
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+        if (c == zc) RST_M3(U, r, c) = sg * sd * x[r];
   }
 }
 
@@ -225,10 +234,11 @@ __device__ inline bool polar3(const double* a, double* Q) {
       ni2 += C[i] * C[i];
     }
     const double g = it < 6 ? sqrt(sqrt(ni2) / nX) : 1.0;
+    const double ig = 1.0 / g;
     double diff = 0.0;
 #pragma unroll
     for (int i = 0; i < 9; ++i) {
-      const double xn = 0.5 * (g * X[i] + C[i] / g);
+      const double xn = 0.5 * (g * X[i] + C[i] * ig);
       diff += (xn - X[i]) * (xn - X[i]);
       X[i] = xn;
     }
@@ -262,17 +272,33 @@ __device__ inline void quat_roundtrip(const float* R, float* Rq) {
     q[1] = (RST_M3(R, 0, 2) - RST_M3(R, 2, 0)) * t;
     q[2] = (RST_M3(R, 1, 0) - RST_M3(R, 0, 1)) * t;
   } else {
+    // i = argmax diagonal, j = i+1, k = i+2 (mod 3), spelled out per i so
+    // every index is static (no scratch memory on the GPU)
     int i = 0;
     if (RST_M3(R, 1, 1) > RST_M3(R, 0, 0)) i = 1;
-    if (RST_M3(R, 2, 2) > RST_M3(R, i, i)) i = 2;
-    const int j = (i + 1) % 3;
-    const int k = (j + 1) % 3;
-    float t = sqrtf(RST_M3(R, i, i) - RST_M3(R, j, j) - RST_M3(R, k, k) + 1.0f);
-    q[i] = 0.5f * t;
-    t = 0.5f / t;
-    q[3] = (RST_M3(R, k, j) - RST_M3(R, j, k)) * t;
-    q[j] = (RST_M3(R, j, i) + RST_M3(R, i, j)) * t;
-    q[k] = (RST_M3(R, k, i) + RST_M3(R, i, k)) * t;
+    if (RST_M3(R, 2, 2) > (i == 0 ? RST_M3(R, 0, 0) : RST_M3(R, 1, 1))) i = 2;
+    if (i == 0) {
+      float t = sqrtf(RST_M3(R, 0, 0) - RST_M3(R, 1, 1) - RST_M3(R, 2, 2) + 1.0f);
+      q[0] = 0.5f * t;
+      t = 0.5f / t;
+      q[3] = (RST_M3(R, 2, 1) - RST_M3(R, 1, 2)) * t;
+      q[1] = (RST_M3(R, 1, 0) + RST_M3(R, 0, 1)) * t;
+      q[2] = (RST_M3(R, 2, 0) + RST_M3(R, 0, 2)) * t;
+    } else if (i == 1) {
+      float t = sqrtf(RST_M3(R, 1, 1) - RST_M3(R, 2, 2) - RST_M3(R, 0, 0) + 1.0f);
+      q[1] = 0.5f * t;
+      t = 0.5f / t;
+      q[3] = (RST_M3(R, 0, 2) - RST_M3(R, 2, 0)) * t;
+      q[2] = (RST_M3(R, 2, 1) + RST_M3(R, 1, 2)) * t;
+      q[0] = (RST_M3(R, 0, 1) + RST_M3(R, 1, 0)) * t;
+    } else {
+      float t = sqrtf(RST_M3(R, 2, 2) - RST_M3(R, 0, 0) - RST_M3(R, 1, 1) + 1.0f);
+      q[2] = 0.5f * t;
+      t = 0.5f / t;
+      q[3] = (RST_M3(R, 1, 0) - RST_M3(R, 0, 1)) * t;
+      q[0] = (RST_M3(R, 0, 2) + RST_M3(R, 2, 0)) * t;
+      q[1] = (RST_M3(R, 1, 2) + RST_M3(R, 2, 1)) * t;
+    }
   }
   const float x = q[0], y = q[1], z = q[2], w = q[3];
   const float tx = 2.0f * x, ty = 2.0f * y, tz = 2.0f * z;

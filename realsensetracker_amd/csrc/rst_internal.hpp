@@ -44,7 +44,10 @@ void set_last_error(hipError_t e, const char* what, const char* file,
 // per-point kernels.  Plain POD; lives in the context's workspace.
 constexpr int kQTrace = 256;
 
-struct IcpState {
+// The part of the state the solve reads and writes: copied to registers at
+// the start of the solve kernel (its loads overlap the slab reduction) and
+// written back at the end.
+struct IcpCore {
   float R[9];        // current pose, column-major (what the points see)
   float t[3];
   float smean[3];    // source centroid (P2POINT_REF)
@@ -60,9 +63,11 @@ struct IcpState {
   double last_d2;    // sum d2 of the last step
   int32_t fail;      // P2PLANE: singular system / too few points
   int32_t fb_e;      // fallback-queue entries of the current iteration
+};
+
+struct IcpState : IcpCore {
   int32_t qlen[kQTrace];  // fallback-queue length per iteration (diagnostics)
-  int32_t path[kQTrace][4];  // lanes certified at adjacency level 1 (no walk) /
-                             // level 1 after a walk / level 2 / level 3
+  int32_t path[kQTrace][4];  // per-iteration diagnostics (rst_debug_queue_trace)
 };
 
 struct IcpParams {
@@ -141,6 +146,9 @@ int query_nn_device(rst_ctx* ctx, const rst_target* tgt, const float* d_q,
 int query_nn_warm_device(rst_ctx* ctx, const rst_target* tgt, const float* d_q, int64_t nq,
                          const int32_t* d_warm, int32_t* d_idx, float* d_d2,
                          int* d_stats = nullptr);
+int query_nn_fallback_device(rst_ctx* ctx, const rst_target* tgt, const float* d_q, int64_t nq,
+                             const int32_t* d_warm, int mode, int32_t* d_idx, float* d_d2,
+                             int32_t* d_path);
 int query_knn_device(rst_ctx* ctx, const rst_target* tgt, const float* d_q,
                      int64_t nq, int k, int32_t* d_idx, float* d_d2);
 int compute_normals(rst_ctx* ctx, rst_target* tgt, int k, const float vp[3]);

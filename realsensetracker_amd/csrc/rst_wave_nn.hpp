@@ -51,6 +51,17 @@ constexpr int kWnnGroups = 8;    // lane groups with their own region (8 lanes e
 // from any starting bound; divergent gathers, but a bounded latency chain).
 constexpr int kWnnCap = 256;
 
+// Lanes of one wavefront hand data to each other through LDS (WnnScratch)
+// between these points.  The hardware executes a wave's LDS accesses in
+// order, but the compiler may move memory operations across a bare
+// wave_barrier; the wavefront-scope fences make the hand-off an ordering
+// point for the compiler too (they emit no cache maintenance).
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 struct WnnScratch {              // per-wave LDS (6.6 KB)
   int stack[kWnnStack];
   float4 leaf_lo[kWnnLeaves];    // .w = leaf index bits
@@ -196,7 +207,7 @@ __device__ __forceinline__ WnnRegion wnn_regions(bool act, float qx, float qy, f
   u.hx = wnn_max_f(fmaxf(fmaxf(hx[0], hx[1]), anybig ? cx + R : -FLT_MAX));
   u.hy = wnn_max_f(fmaxf(fmaxf(hy[0], hy[1]), anybig ? cy + R : -FLT_MAX));
   u.hz = wnn_max_f(fmaxf(fmaxf(hz[0], hz[1]), anybig ? cz + R : -FLT_MAX));
-  __builtin_amdgcn_wave_barrier();
+  wave_sync();
   return u;
 }
 
@@ -283,7 +294,7 @@ __device__ __forceinline__ void nn_wave_region(const BvhView& bv, bool act, floa
   if (lane < depth) ws.stack[lane] = (int)((lca >> (depth - 1 - lane)) ^ 1u);
   if (lane == 0) ws.stack[depth] = (int)lca;
   int sp = depth + 1;
-  __builtin_amdgcn_wave_barrier();
+  wave_sync();
   WnnRegion reg = wnn_regions(act, qx, qy, qz, r.d, ws);
   int ns = 0;
   int st_rounds = 0, st_nodes = 0, st_staged = 0, st_scanned = 0, st_flush = 0;
@@ -310,7 +321,7 @@ __device__ __forceinline__ void nn_wave_region(const BvhView& bv, bool act, floa
       int node = 0;
       if (lane < k) node = ws.stack[sp - 1 - lane];
       sp -= k;
-      __builtin_amdgcn_wave_barrier();
+      wave_sync();
       bool pass = false;
       float4 lo = make_float4(0.f, 0.f, 0.f, 0.f), hi = lo;
       if (lane < k) {
@@ -338,7 +349,7 @@ __device__ __forceinline__ void nn_wave_region(const BvhView& bv, bool act, floa
       sp += 2 * __popcll(im);
       ns += __popcll(lm);
       st_staged += __popcll(lm);
-      __builtin_amdgcn_wave_barrier();
+      wave_sync();
     }
     const bool over = st_staged > kWnnCap;
     if (ns > kWnnLeaves - kWnnPop || (ns > 0 && (sp == 0 || over))) {
@@ -396,29 +407,70 @@ __device__ __forceinline__ Best1 wave_lex_min(Best1 b) {
   return b;
 }
 
-// r: uniform across the wave (the warm offer, or empty); returns the exact
-// answer, uniform.  warm: sorted position to start from (-1: the root).
-__device__ __forceinline__ void nn_wave_one(const BvhView& bv, int warm, float qx, float qy,
-                                            float qz, Best1& r, WnnScratch& ws) {
+// Scan the staged leaves [0, ns) (ws.leaf_lo[s] = (box_d2, -, -, leaf bits))
+// for one query: leaf ranges first (one load per leaf, all lanes), then the
+// points 32 leaves at a time -- lanes 16g..16g+15 take leaf s+g's points,
+// eight leaf groups' loads in flight per lane before any offer -- so a flush
+// costs a couple of memory latencies, not one per four leaves.  Leaves whose
+// box_d2 exceeds the current (uniform) bound are skipped.  r <- the wave
+// minimum of every lane's offers.
+template <class R>
+__device__ __forceinline__ void wnn_flush_one(const BvhView& bv, WnnScratch& ws, int ns, float qx,
+                                              float qy, float qz, R& mine, R& r) {
+  const int lane = __lane_id();
+  for (int s = lane; s < ns; s += kWave) {
+    const int L = f2i(ws.leaf_lo[s].w);
+    const int b = leaf_begin(bv, L);
+    const int e = leaf_begin(bv, L + 1);
+    ws.leaf_hi[s] = make_float4(0.f, 0.f, i2f(b), i2f(e - b));
+  }
+  wave_sync();
+  const int g = lane >> 4, o = lane & 15;
+  const float bnd = r.bound();
+  const int last = bv.m - 1;
+  for (int s0 = 0; s0 < ns; s0 += 32) {
+    float4 p[8];
+    int pos[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int s = s0 + 4 * k + g;
+      pos[k] = -1;
+      if (s < ns) {
+        const float bd = ws.leaf_lo[s].x;
+        const float4 rg = ws.leaf_hi[s];
+        if (bd <= bnd && o < f2i(rg.w)) pos[k] = f2i(rg.z) + o;
+      }
+      p[k] = bv.pts[pos[k] >= 0 ? pos[k] : last];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (pos[k] >= 0) mine.offer(d2_ref(qx, qy, qz, p[k].x, p[k].y, p[k].z), f2i(p[k].w), pos[k]);
+  }
+  r = wave_lex_min(mine);
+  wave_sync();
+}
+
+// The staging walk of one query from the sp node ids on ws.stack: up to 64
+// nodes tested per round (one coalesced load each, all in flight), internal
+// nodes whose box meets the ball push both children, leaves are staged and
+// scanned in flushes that tighten the (uniform) bound.  Exact over the
+// subtrees on the initial stack.
+template <class R>
+__device__ __forceinline__ void nn_wave_walk(const BvhView& bv, int sp, float qx, float qy,
+                                             float qz, R& r, WnnScratch& ws) {
   const int lane = __lane_id();
   const int nl = bv.nleaves;
-  if (bv.m <= 0 || !finite3(qx, qy, qz)) return;
-  Best1 mine = r;
-  const unsigned start = (warm >= 0 && warm < bv.m) ? (unsigned)(nl + leaf_of(bv, warm)) : 1u;
-  const int depth = 31 - __clz(start);
-  if (lane < depth) ws.stack[lane] = (int)((start >> (depth - 1 - lane)) ^ 1u);
-  if (lane == 0) ws.stack[depth] = (int)start;
-  int sp = depth + 1;
+  R mine = r;
   int ns = 0;
   const uint64_t lt = (1ull << lane) - 1ull;
-  __builtin_amdgcn_wave_barrier();
+  wave_sync();
   while (sp > 0 || ns > 0) {
     if (sp > 0) {
       const int k = min(min(kWnnPop, sp), max(1, (kWnnStack - 48 - sp) / 2));
       int node = 0;
       if (lane < k) node = ws.stack[sp - 1 - lane];
       sp -= k;
-      __builtin_amdgcn_wave_barrier();
+      wave_sync();
       bool pass = false;
       float4 lo = make_float4(0.f, 0.f, 0.f, 0.f), hi = lo;
       float bd = 0.f;
@@ -426,7 +478,7 @@ __device__ __forceinline__ void nn_wave_one(const BvhView& bv, int warm, float q
         lo = bv.nodes[2 * node];
         hi = bv.nodes[2 * node + 1];
         bd = box_d2(qx, qy, qz, lo, hi);
-        pass = bd <= r.d;
+        pass = bd <= r.bound();
       }
       const bool isleaf = node >= nl;
       const uint64_t im = __ballot(pass && !isleaf);
@@ -443,29 +495,101 @@ __device__ __forceinline__ void nn_wave_one(const BvhView& bv, int warm, float q
       }
       sp += 2 * __popcll(im);
       ns += __popcll(lm);
-      __builtin_amdgcn_wave_barrier();
+      wave_sync();
     }
     if (ns > kWnnLeaves - kWnnPop || (sp == 0 && ns > 0)) {
-      // four leaves per step: lanes 16g..16g+15 take leaf s+g's points
-      const int g = lane >> 4, o = lane & 15;
-      for (int s = 0; s < ns; s += 4) {
-        if (s + g < ns) {
-          const float4 e = ws.leaf_lo[s + g];
-          if (e.x <= r.d) {
-            const int L = f2i(e.w);
-            const int b = leaf_begin(bv, L);
-            if (o < leaf_begin(bv, L + 1) - b) {
-              const float4 p = bv.pts[b + o];
-              mine.offer(d2_ref(qx, qy, qz, p.x, p.y, p.z), f2i(p.w), b + o);
-            }
-          }
-        }
-      }
-      r = wave_lex_min(mine);
+      wnn_flush_one(bv, ws, ns, qx, qy, qz, mine, r);
       ns = 0;
-      __builtin_amdgcn_wave_barrier();
     }
   }
+}
+
+// r: uniform across the wave (the warm offer, or empty); returns the exact
+// answer, uniform.  warm: sorted position to start from (-1: the root).
+// The walk starts at the warm leaf and the sibling of every ancestor (a
+// partition of the tree).
+template <class R>
+__device__ __forceinline__ void nn_wave_one(const BvhView& bv, int warm, float qx, float qy,
+                                            float qz, R& r, WnnScratch& ws) {
+  const int lane = __lane_id();
+  const int nl = bv.nleaves;
+  if (bv.m <= 0 || !finite3(qx, qy, qz)) return;
+  const unsigned start = (warm >= 0 && warm < bv.m) ? (unsigned)(nl + leaf_of(bv, warm)) : 1u;
+  const int depth = 31 - __clz(start);
+  if (lane < depth) ws.stack[lane] = (int)((start >> (depth - 1 - lane)) ^ 1u);
+  if (lane == 0) ws.stack[depth] = (int)start;
+  nn_wave_walk(bv, depth + 1, qx, qy, qz, r, ws);
+}
+
+// Exact 1-NN of one query through the level-2 (shift = kAdj2Shift: items =
+// nodes of 8 leaves) or level-3 (kAdj3Shift: nodes of 64 leaves) adjacency
+// of the warm point's item, whole wave: the same coverage argument as
+// rst_bvh.hpp adj2_search / adj3_search, with the 24 entries tested by 24
+// lanes at once.  Level 2 stages the candidate nodes' leaves directly (one
+// round of box loads); level 3 seeds the staging walk with the candidate
+// nodes.  Returns false, having offered nothing, when the ball is not
+// covered.  r uniform in and out.
+template <class R>
+__device__ __forceinline__ bool nn_wave_adj(const BvhView& bv, const AdjView& av, int shift,
+                                            int warm, float qx, float qy, float qz, R& r,
+                                            WnnScratch& ws) {
+  const int lane = __lane_id();
+  const int nl = bv.nleaves;
+  if (nl < (1 << shift) || warm < 0 || warm >= bv.m || !finite3(qx, qy, qz)) return false;
+  const float4* ent = shift == kAdj2Shift ? av.ent2 : av.ent3;
+  const float* reach = shift == kAdj2Shift ? av.reach2 : av.reach3;
+  const int first = nl >> shift;
+  const int N = (nl + leaf_of(bv, warm)) >> shift;
+  float4 l = make_float4(0.f, 0.f, 0.f, 0.f), h = l;
+  int X = -1;
+  if (lane < kAdjK) {
+    l = ent[((int64_t)(N - first) * kAdjK + lane) * 2];
+    h = ent[((int64_t)(N - first) * kAdjK + lane) * 2 + 1];
+    X = f2i(h.w);
+  }
+  const float4 nlo = bv.nodes[2 * N], nhi = bv.nodes[2 * N + 1];
+  const float rch = reach[N - first];
+  // margins cover float rounding of every distance (rst_bvh.hpp adj_search)
+  const float dl = sqrtf(box_d2(qx, qy, qz, nlo, nhi)) * 1.00001f;
+  const float rb = sqrtf(r.bound()) * 1.00001f + 1e-30f;
+  if (!(dl + rb < rch * 0.99999f)) return false;
+  // entries are sorted by box distance: the early exit of the sequential
+  // scan is the same per-entry test
+  const bool cand = X >= 0 && !(l.w * 0.99999f - dl > rb) && box_d2(qx, qy, qz, l, h) <= r.bound();
+  const uint64_t cm = __ballot(cand);
+  const uint64_t lt = (1ull << lane) - 1ull;
+  const int nc = __popcll(cm);
+  if (cand) ws.stack[__popcll(cm & lt)] = first + X;
+  wave_sync();
+  if (shift != kAdj2Shift) {
+    nn_wave_walk(bv, nc, qx, qy, qz, r, ws);
+    return true;
+  }
+  // level 2: the candidate nodes' 8 leaves each, boxes tested by the wave
+  R mine = r;
+  int ns = 0;
+  const int total = nc << kAdj2Shift;
+  for (int i0 = 0; i0 < total; i0 += kWave) {
+    const int idx = i0 + lane;
+    bool pass = false;
+    float bd = 0.f;
+    int L = 0;
+    if (idx < total) {
+      const int node = ws.stack[idx >> kAdj2Shift];
+      L = (node << kAdj2Shift) - nl + (idx & ((1 << kAdj2Shift) - 1));
+      bd = box_d2(qx, qy, qz, bv.nodes[2 * (nl + L)], bv.nodes[2 * (nl + L) + 1]);
+      pass = bd <= r.bound();
+    }
+    const uint64_t lm = __ballot(pass);
+    if (pass) ws.leaf_lo[ns + __popcll(lm & lt)] = make_float4(bd, 0.f, 0.f, i2f(L));
+    ns += __popcll(lm);
+    wave_sync();
+    if (ns > kWnnLeaves - kWave || (i0 + kWave >= total && ns > 0)) {
+      wnn_flush_one(bv, ws, ns, qx, qy, qz, mine, r);
+      ns = 0;
+    }
+  }
+  return true;
 }
 
 }  // namespace rst
@@ -477,8 +601,9 @@ namespace rst {
 // four at a time (each entry carries its leaf's box, so a test needs no
 // further gather) and leaf points eight at a time, unconditionally (index
 // clamped), so a lane's dependent chain is warm point -> entries -> points.
-__device__ __forceinline__ void scan_range_wide(const BvhView& bv, int b, int n, float qx,
-                                                float qy, float qz, Best1& r) {
+template <class R>
+RST_HD void scan_range_wide(const BvhView& bv, int b, int n, float qx,
+                                                float qy, float qz, R& r) {
   const int last = bv.m - 1;
   for (int j0 = 0; j0 < n; j0 += 8) {
     float4 p[8];
@@ -498,8 +623,9 @@ __device__ __forceinline__ void scan_range_wide(const BvhView& bv, int b, int n,
 // from the coverage test of the final leaf.
 constexpr int kWalkSteps = 1;
 
-__device__ __forceinline__ bool adj_search_wide(const BvhView& bv, const AdjView& av, int start,
-                                                float qx, float qy, float qz, Best1& r,
+template <class R>
+RST_HD bool adj_search_wide(const BvhView& bv, const AdjView& av, int start,
+                                                float qx, float qy, float qz, R& r,
                                                 int* walked = nullptr) {
   const int nl = bv.nleaves;
   int L = leaf_of(bv, start);
@@ -509,7 +635,7 @@ __device__ __forceinline__ bool adj_search_wide(const BvhView& bv, const AdjView
     const float reach = av.reach[L];
     // same margins as rst_bvh.hpp adj_search
     dl = sqrtf(box_d2(qx, qy, qz, lo, hi)) * 1.00001f;
-    if (dl + sqrtf(r.d) * 1.00001f + 1e-30f < reach * 0.99999f) break;
+    if (dl + r.radius() * 1.00001f + 1e-30f < reach * 0.99999f) break;
     if (walked) *walked = step + 1;
     if (step == kWalkSteps) return false;
     // walk: scan the listed leaf nearest to the query (other than L)
@@ -541,9 +667,9 @@ __device__ __forceinline__ bool adj_search_wide(const BvhView& bv, const AdjView
     for (int j = 0; j < 4; ++j) {
       if (stop) break;
       const int tag = f2i(h[j].w);
-      if (tag < 0 || l[j].w * 0.99999f - dl > sqrtf(r.d) * 1.00001f + 1e-30f) {
+      if (tag < 0 || l[j].w * 0.99999f - dl > r.radius() * 1.00001f + 1e-30f) {
         stop = true;
-      } else if (box_d2(qx, qy, qz, l[j], h[j]) <= r.d) {
+      } else if (box_d2(qx, qy, qz, l[j], h[j]) <= r.bound()) {
         scan_range_wide(bv, tag >> 5, tag & 31, qx, qy, qz, r);
       }
     }
@@ -581,13 +707,13 @@ __device__ __forceinline__ void leaf_adj_wave(const BvhView& bv, int first, int 
     ns = 0;
     overflow = false;
     const uint64_t lt = (1ull << lane) - 1ull;
-    __builtin_amdgcn_wave_barrier();
+    wave_sync();
     while (sp > 0 && !overflow) {
       const int k = min(min(kWnnPop, sp), max(1, (kWnnStack - 48 - sp) / 2));
       int node = 0;
       if (lane < k) node = ws.stack[sp - 1 - lane];
       sp -= k;
-      __builtin_amdgcn_wave_barrier();
+      wave_sync();
       bool pass = false;
       float b2 = 0.f;
       if (lane < k) {
@@ -609,7 +735,7 @@ __device__ __forceinline__ void leaf_adj_wave(const BvhView& bv, int first, int 
       if (pass && isleaf) ws.leaf_lo[ns + __popcll(lm & lt)] = make_float4(b2, 0.f, 0.f, i2f(node - nl));
       sp += 2 * __popcll(im);
       ns += __popcll(lm);
-      __builtin_amdgcn_wave_barrier();
+      wave_sync();
     }
     if (!overflow) break;
     D2 *= 0.25f;
@@ -623,7 +749,7 @@ __device__ __forceinline__ void leaf_adj_wave(const BvhView& bv, int first, int 
     if (lane == 0) reach[L] = 0.0f;
     return;
   }
-  __builtin_amdgcn_wave_barrier();
+  wave_sync();
   // rank of each collected leaf in (bbd2, index) order
   float rk_b2 = -1.f;  // bbd2 of the element ranked kAdjK (the reach)
   for (int s = lane; s < kWnnLeaves; s += 64) {

@@ -44,9 +44,8 @@ def main():
             qt(ctx.handle, L.iptr(q), 256)
             print(f"pair {pair} mode {mode}: n={len(pb)} build {1e3*(t1-t0):.2f} ms  align "
                   f"{1e3*(t3-t2):.2f} ms  iters {r.iterations} ok {r.ok}")
-            print("  iter: queue | L1 L1walk L2 L3")
-            for i in list(range(min(8, r.iterations))) + list(range(16, r.iterations, 16)):
-                print(f"  {i:3d}: {q[i,0]:6d} | {q[i,1]:6d} {q[i,2]:6d} {q[i,3]:6d} {q[i,4]:6d}")
+            print("  fallback queue per iteration:", " ".join(str(x) for x in q[:r.iterations, 0]))
+            print("  solve kernel: reduce / solve (x10 ns):", " ".join(f"{a}/{b}" for a, b in q[:min(r.iterations, 24), 1:3]))
 
 
 if __name__ == "__main__":

@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "rst_bvh.hpp"
+#include "rst_wave_nn.hpp"
 
 using namespace rst;
 
@@ -167,6 +168,7 @@ void brute(const std::vector<float>& xyz, float qx, float qy, float qz, BestK<K>
 int g_fail = 0;
 long g_checks = 0;
 long g_covered = 0, g_covered2 = 0, g_covered3 = 0, g_adj_tries = 0;
+long g_wide = 0;
 
 void check(bool ok, const char* what, int m, int q) {
   ++g_checks;
@@ -263,6 +265,18 @@ void run_case(std::mt19937_64& rng, int m, int nq, int mode) {
         check(s2.d == b1.d[0] && (s2.pos < 0 ? b1.pos[0] < 0 : s2.id == b1.id[0]), "adj2", m, q);
       }
     }
+    // the ICP kernel's adjacency search (rst_wave_nn.hpp adj_search_wide)
+    if (m > 0 && finite3(qx, qy, qz)) {
+      const int start = b1.pos[0] >= 0 && (q & 2) ? pos_of(ix, b1.id[0]) : P(rng);
+      Best1 s;
+      s.init();
+      const float4 p = ix.pts[start];
+      s.offer(d2_ref(qx, qy, qz, p.x, p.y, p.z), f2i(p.w), start);
+      if (adj_search_wide(ix.bv, ix.av, start, qx, qy, qz, s)) {
+        ++g_wide;
+        check(s.d == b1.d[0] && s.id == b1.id[0], "adj wide", m, q);
+      }
+    }
     // k = 4, bottom-up from a random leaf
     if (m > 0) {
       BestK<4> k4;
@@ -284,7 +298,7 @@ int main(int argc, char** argv) {
   for (int m : sizes)
     for (int mode = 0; mode < 4; ++mode) run_case(rng, m, m >= 4099 ? 300 : 120, mode);
   printf("bvh_selftest: %ld checks, %d failures (adjacency covered %ld / level 2 %ld / level 3 "
-         "%ld of %ld warm queries)\n", g_checks, g_fail, g_covered, g_covered2, g_covered3,
-         g_adj_tries);
+         "%ld of %ld warm queries; wide %ld)\n", g_checks, g_fail, g_covered, g_covered2,
+         g_covered3, g_adj_tries, g_wide);
   return g_fail == 0 ? 0 : 1;
 }

@@ -391,3 +391,52 @@ def test_solve_kabsch_device_contract(ctx):
     assert np.array_equal(T, T0)
     with pytest.raises(L.RstError):
         A.SolveKabsch(np.ones((9, 3), np.float32), np.ones((9, 3), np.float32), [[0, 9]], None, T)
+
+
+# ---- the ICP fallback search (k_icp_fb's per-query strategies) ------------------------
+def _fallback(ctx, t, q, warm, mode):
+    n = len(q)
+    idx = np.zeros(n, np.int32)
+    d2 = np.zeros(n, np.float32)
+    path = np.zeros(n, np.int32)
+    f = L.lib().rst_debug_query_nn_fallback
+    f.restype = C.c_int
+    f.argtypes = [C.c_void_p, C.c_void_p, L.c_float_p, C.c_int64, L.c_int32_p, C.c_int,
+                  L.c_int32_p, L.c_float_p, L.c_int32_p]
+    q = np.ascontiguousarray(q, np.float32)
+    w = None if warm is None else np.ascontiguousarray(warm, np.int32)
+    L.check(f(ctx.handle, t.handle, L.fptr(q), n, None if w is None else L.iptr(w), mode,
+              L.iptr(idx), L.fptr(d2), L.iptr(path)), "fallback")
+    return idx, d2, path
+
+
+@pytest.fixture(scope="module")
+def frame_640(ctx):
+    K = driver.intrinsics(640, 480)
+    sc = driver.SyntheticScene(3)
+    da, db, _ = driver.make_pair(sc, K, seed=31)
+    pa = driver.unproject(da, K, ctx=ctx)
+    pb = driver.unproject(db, K, ctx=ctx)
+    return pa, pb, A.Target.build(pa, ctx), O.KDTree(pa)
+
+
+@pytest.mark.parametrize("mode", [0, 2, 3, 23])
+def test_icp_fallback_search_bitexact(ctx, frame_640, mode):
+    """Near and far (1 mm .. 50 cm off the surface) queries, good / poor /
+    missing warm candidates: every strategy returns the exact (d2, index)."""
+    pa, pb, t, tree = frame_640
+    rng = np.random.default_rng(mode)
+    sel = rng.choice(len(pb), 3000, replace=False)
+    off = rng.normal(size=(3000, 3)).astype(np.float32)
+    off *= (10 ** rng.uniform(-3, np.log10(0.5), 3000)).astype(np.float32)[:, None] / np.linalg.norm(off, axis=1, keepdims=True)
+    q = (pb[sel] + off).astype(np.float32)
+    oi, od = tree.query(q)
+    gi0, _ = tree.query(pb[sel])
+    paths = []
+    for warm in (gi0.astype(np.int32), rng.integers(0, len(pa), 3000).astype(np.int32), None):
+        gi, gd, path = _fallback(ctx, t, q, warm, mode)
+        assert np.array_equal(gd, od)
+        assert np.array_equal(gi, oi)
+        paths.append(path)
+    if mode in (2, 23):  # with a good warm point the level-2 index answers many
+        assert np.mean(paths[0] == 2) > 0.2
