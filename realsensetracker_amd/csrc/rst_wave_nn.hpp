@@ -38,6 +38,7 @@
 #include <climits>
 
 #include "rst_bvh.hpp"
+#include "rst_device.hpp"
 
 namespace rst {
 
