@@ -54,13 +54,16 @@ constexpr int kWnnCap = 256;
 
 // Lanes of one wavefront hand data to each other through LDS (WnnScratch)
 // between these points.  The hardware executes a wave's LDS accesses in
-// order, but the compiler may move memory operations across a bare
-// wave_barrier; the wavefront-scope fences make the hand-off an ordering
-// point for the compiler too (they emit no cache maintenance).
+// order, but the compiler may move plain memory operations across a bare
+// wave_barrier (and across wavefront-scope fences, which order atomics
+// only); the asm memory clobber pins them.  No cache maintenance.
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // a full compiler barrier for plain (non-atomic) LDS accesses too, and
+  // every LDS access of this wave retired before the next one issues
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
 struct WnnScratch {              // per-wave LDS (6.6 KB)
