@@ -92,7 +92,9 @@ int rst_ctx_synchronize(rst_ctx* ctx);
  * align call, measured with HIP events on the context's stream; and the
  * number of launches it covers.  Used by bench.py's roofline. */
 int rst_ctx_last_kernel_time(rst_ctx* ctx, float* avg_ms, int32_t* launches);
-/* Enable/disable per-iteration kernel timing (adds events; default off). */
+/* Per-iteration kernel timing (HIP events around the dominant kernel on the
+ * context's stream): 0 = off (default), 1 = every iteration, k > 1 = every
+ * k-th iteration (fewer events in a timed loop). */
 int rst_ctx_enable_kernel_timing(rst_ctx* ctx, int enable);
 
 /* ---- target index (replaces KDTree3f{dst,16}; kdtree.hpp:27-57) --------- */
@@ -157,6 +159,20 @@ int rst_icp_align_prepared(rst_ctx* ctx, const rst_target* src,
                            float pose_inout[16], float* mean_cost,
                            int32_t* iterations_run);
 
+/* rst_icp_align_prepared split in two, so several frame pairs can be in
+ * flight on one GPU (one context -- one HIP stream -- each): _async enqueues
+ * the whole loop and returns RST_OK, or RST_FALSE for the reference's early
+ * false (nothing enqueued), or an error; _wait blocks until that align is
+ * done and returns what rst_icp_align_prepared would (pose_inout in: the
+ * same initial guess given to _async; out: the result).  One align per
+ * context at a time (RST_E_STATE otherwise).  src and tgt must stay alive
+ * until _wait returns. */
+int rst_icp_align_prepared_async(rst_ctx* ctx, const rst_target* src,
+                                 const rst_target* tgt, const rst_icp_opts* opts,
+                                 const float pose_in[16]);
+int rst_icp_align_wait(rst_ctx* ctx, float pose_inout[16], float* mean_cost,
+                       int32_t* iterations_run);
+
 /* The per-iteration solve of AlignIcp3d / SolveKabsch (align_icp.cpp:58-69,
  * 139-151) run by the device solve kernel on a given fp64 cross-covariance
  * (column-major) and float means: R = float(U V^T), R.col(2) *= -1 when
@@ -194,6 +210,27 @@ int rst_unproject_device(rst_ctx* ctx, const uint16_t* d_depth,
 int rst_frame_prepare_device(rst_ctx* ctx, const uint16_t* d_depth,
                              const rst_intrinsics* K, int normals_k,
                              rst_target** out);
+
+/* ---- cloud preprocessing the callers run before AlignIcp3d -------------- */
+/* RemoveNans (point_cloud_utils.cpp:163-174): keep the points whose three
+ * coordinates are finite, in input order.  out holds >= n points; n_out
+ * receives the count.  Returns RST_OK. */
+int rst_remove_nans(rst_ctx* ctx, const float* xyz, int64_t n, float* out,
+                    int64_t* n_out);
+int rst_remove_nans_device(rst_ctx* ctx, const float* d_xyz, int64_t n,
+                           float* d_out, int64_t* n_out);
+/* DownsampleVoxel (point_cloud_utils.cpp:34-68): the first point (lowest
+ * input index) of every voxel (int)floor(p / voxel_size), emitted in
+ * ascending input index (the reference's order is its unordered_map's,
+ * i.e. unspecified; the point SET is identical).  NaN / out-of-int-range
+ * coordinates key to INT_MIN as the reference's float->int cast does on
+ * x86-64.  voxel_size must be > 0 and n < 2^30 (RST_E_ARG otherwise);
+ * out holds >= n points. */
+int rst_downsample_voxel(rst_ctx* ctx, const float* xyz, int64_t n,
+                         float voxel_size, float* out, int64_t* n_out);
+int rst_downsample_voxel_device(rst_ctx* ctx, const float* d_xyz, int64_t n,
+                                float voxel_size, float* d_out,
+                                int64_t* n_out);
 
 /* ---- synthetic frame source (driver; replaces the camera) --------------- */
 /* Procedural room (walls + random spheres/boxes), seeded. */

@@ -21,15 +21,16 @@ int rst_debug_query_nn_warm_stats(rst_ctx* ctx, const rst_target* tgt, const flo
 
 /* Per iteration of the last align call on ctx (first n <= 256), 5 int32:
  * fallback-queue length (queries the level-1 adjacency could not certify),
- * unused, then the solve kernel's reduction and solve times (10 ns ticks),
- * unused. */
+ * queries answered by their candidate list (no search), unused, then the
+ * solve kernel's reduction and solve times (10 ns ticks). */
 int rst_debug_queue_trace(rst_ctx* ctx, int32_t* out, int32_t n);
 
 /* The ICP loop's fallback search (one wavefront per query) on a host batch:
  * mode 0 = full walk from the warm leaf, 2 / 3 = level-2 / level-3
  * adjacency first, 23 = both then the walk.  warm = original target indices
- * (may be NULL); path[i] = 2, 3 or 0 (which strategy answered).  Results
- * equal rst_target_query_nn's. */
+ * (may be NULL); path[i] & 15 = 2, 3 or 0 (which strategy answered),
+ * path[i] >> 4 = the search's shader cycles / 16.  Results equal
+ * rst_target_query_nn's. */
 int rst_debug_query_nn_fallback(rst_ctx* ctx, const rst_target* tgt, const float* q,
                                 int64_t nq, const int32_t* warm, int mode, int32_t* idx,
                                 float* d2, int32_t* path);

@@ -59,6 +59,10 @@ def lib():
         L.orc_p2point_partials.argtypes = [_f, C.c_int64, P, _f, _f, _f, C.c_float, _d]
         L.orc_compute_normals.argtypes = [_f, C.c_int64, P, C.c_int, _f, _f]
         L.orc_unproject.restype = C.c_int64
+        L.orc_remove_nans.argtypes = [_f, C.c_int64, _f]
+        L.orc_remove_nans.restype = C.c_int64
+        L.orc_downsample_voxel.argtypes = [_f, C.c_int64, C.c_float, _f]
+        L.orc_downsample_voxel.restype = C.c_int64
         L.orc_unproject.argtypes = [_u16, C.c_int, C.c_int, _f, C.c_float, C.c_int, _f]
         L.orc_align_p2plane.restype = C.c_int
         L.orc_align_p2plane.argtypes = [_f, C.c_int64, _f, _f, C.c_int64, P, C.c_int,
@@ -217,6 +221,22 @@ def unproject(depth, K4, depth_scale=0.001, keep_invalid=False):
     out = np.zeros((h * w, 3), np.float32)
     n = lib().orc_unproject(d.ctypes.data_as(_u16), w, h, _fp(np.asarray(K4, np.float32)),
                             depth_scale, int(keep_invalid), _fp(out))
+    return out[:n].copy()
+
+
+def remove_nans(cloud):
+    """RemoveNans (point_cloud_utils.cpp:163-174)."""
+    a = _cloud(cloud)
+    out = np.zeros_like(a)
+    n = lib().orc_remove_nans(_fp(a), a.shape[0], _fp(out))
+    return out[:n].copy()
+
+
+def downsample_voxel(cloud, voxel_size):
+    """DownsampleVoxel (point_cloud_utils.cpp:34-68), ascending input order."""
+    a = _cloud(cloud)
+    out = np.zeros_like(a)
+    n = lib().orc_downsample_voxel(_fp(a), a.shape[0], float(voxel_size), _fp(out))
     return out[:n].copy()
 
 

@@ -10,6 +10,7 @@
 #include "rst_oracle.h"
 
 #include <float.h>
+#include <limits.h>
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
@@ -1076,4 +1077,67 @@ int orc_align_p2plane(const float* src, int64_t n, const float* dst,
   }
   if (own) orc_kdtree_free(own);
   return ok ? it : -1;
+}
+
+/* ---- common/RemoveNans (point_cloud_utils.cpp:163-174) ------------------- */
+int64_t orc_remove_nans(const float* xyz, int64_t n, float* out) {
+  int64_t m = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    const float* p = xyz + 3 * i;
+    if (!(isfinite(p[0]) && isfinite(p[1]) && isfinite(p[2]))) continue; /* :167 allFinite */
+    out[3 * m + 0] = p[0];
+    out[3 * m + 1] = p[1];
+    out[3 * m + 2] = p[2];
+    ++m;
+  }
+  return m;
+}
+
+/* ---- common/DownsampleVoxel (point_cloud_utils.cpp:34-68) --------------- */
+/* (point / voxel_size).floor().cast<int>() (:41-42) per axis; the cast of a
+ * NaN / out-of-range float is what x86-64 cvttss2si returns, INT_MIN. */
+static int orc_vox_coord(float x, float v) {
+  const float q = floorf(x / v);
+  return (q >= -2147483648.0f && q < 2147483648.0f) ? (int)q : INT_MIN;
+}
+
+int64_t orc_downsample_voxel(const float* xyz, int64_t n, float voxel_size, float* out) {
+  /* the set of voxels seen so far (:43-46: emplace only when new, so each
+   * voxel keeps its FIRST point); open addressing over (ix,iy,iz) */
+  int64_t cap = 16;
+  while (cap < 2 * n) cap <<= 1;
+  int32_t* keys = (int32_t*)malloc(sizeof(int32_t) * 3 * (size_t)cap);
+  uint8_t* used = (uint8_t*)calloc((size_t)cap, 1);
+  int64_t m = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    const float* p = xyz + 3 * i;
+    const int k0 = orc_vox_coord(p[0], voxel_size), k1 = orc_vox_coord(p[1], voxel_size),
+              k2 = orc_vox_coord(p[2], voxel_size);
+    uint64_t h = ((uint64_t)(uint32_t)k0 * 73856093u) ^ ((uint64_t)(uint32_t)k1 * 19349663u) ^
+                 ((uint64_t)(uint32_t)k2 * 83492791u);
+    h ^= h >> 17;
+    int64_t s = (int64_t)(h & (uint64_t)(cap - 1));
+    int found = 0;
+    while (used[s]) {
+      if (keys[3 * s] == k0 && keys[3 * s + 1] == k1 && keys[3 * s + 2] == k2) {
+        found = 1;
+        break;
+      }
+      s = (s + 1) & (cap - 1);
+    }
+    if (found) continue;
+    used[s] = 1;
+    keys[3 * s] = k0;
+    keys[3 * s + 1] = k1;
+    keys[3 * s + 2] = k2;
+    /* emitted in first-seen (= ascending index) order; the reference emits
+     * the same set in unordered_map iteration order (:54-57, :63-66) */
+    out[3 * m + 0] = p[0];
+    out[3 * m + 1] = p[1];
+    out[3 * m + 2] = p[2];
+    ++m;
+  }
+  free(keys);
+  free(used);
+  return m;
 }

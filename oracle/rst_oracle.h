@@ -132,6 +132,18 @@ void orc_compute_normals(const float* xyz, int64_t m, const orc_kdtree* tree,
 int64_t orc_unproject(const uint16_t* depth, int w, int h, const float K[4],
                       float depth_scale, int keep_invalid, float* xyz);
 
+/* ---- common/RemoveNans (point_cloud_utils.cpp:163-174) ----------------- */
+/* Finite points in input order; returns the count (out holds >= n). */
+int64_t orc_remove_nans(const float* xyz, int64_t n, float* out);
+
+/* ---- common/DownsampleVoxel (point_cloud_utils.cpp:34-68) --------------- */
+/* The first point of every voxel (int)floor(p / voxel_size) (NaN or
+ * out-of-int-range -> INT_MIN, x86-64's cast), in ascending input index;
+ * returns the count.  The reference emits the same points in unordered_map
+ * order. */
+int64_t orc_downsample_voxel(const float* xyz, int64_t n, float voxel_size,
+                             float* out);
+
 /* ---- build's own point-to-plane mode (no reference counterpart) --------- */
 /* Gauss-Newton point-to-plane with the same annealed weight schedule;
  * see DESIGN.md "P2PLANE".  Returns iterations run. */

@@ -16,6 +16,7 @@ LIB_PATH = Path(os.environ.get(
     "RST_LIB", Path(__file__).resolve().parent / "lib" / "librst_align.so"))
 
 RST_OK, RST_FALSE = 0, 1
+RST_E_ARG, RST_E_HIP, RST_E_NOMEM, RST_E_NODEVICE, RST_E_COMM, RST_E_STATE = -1, -2, -3, -4, -5, -6
 RST_P2POINT_REF, RST_P2PLANE = 0, 1
 COMM_ID_BYTES = 128
 
@@ -73,11 +74,18 @@ PROTOTYPES = {
                                          c_int32_p]),
     "rst_solve_kabsch": (C.c_int, [_P, c_float_p, C.c_int64, c_float_p, C.c_int64, c_int32_p,
                                    c_float_p, C.c_int64, c_float_p]),
+    "rst_icp_align_prepared_async": (C.c_int, [_P, _P, _P, C.POINTER(IcpOpts), c_float_p]),
+    "rst_icp_align_wait": (C.c_int, [_P, c_float_p, c_float_p, c_int32_p]),
     "rst_compute_centroid": (C.c_int, [_P, c_float_p, C.c_int64, c_float_p]),
     "rst_kabsch_solve": (C.c_int, [_P, C.POINTER(C.c_double), c_float_p, c_float_p, c_float_p]),
     "rst_unproject": (C.c_int, [_P, c_u16_p, C.POINTER(Intrinsics), C.c_int, c_float_p,
                                 c_int64_p]),
     "rst_unproject_device": (C.c_int, [_P, _P, C.POINTER(Intrinsics), C.c_int, _P, c_int64_p]),
+    "rst_remove_nans": (C.c_int, [_P, c_float_p, C.c_int64, c_float_p, c_int64_p]),
+    "rst_remove_nans_device": (C.c_int, [_P, _P, C.c_int64, _P, c_int64_p]),
+    "rst_downsample_voxel": (C.c_int, [_P, c_float_p, C.c_int64, C.c_float, c_float_p,
+                                       c_int64_p]),
+    "rst_downsample_voxel_device": (C.c_int, [_P, _P, C.c_int64, C.c_float, _P, c_int64_p]),
     "rst_frame_prepare_device": (C.c_int, [_P, _P, C.POINTER(Intrinsics), C.c_int,
                                            C.POINTER(_P)]),
     "rst_scene_create": (C.c_int, [C.c_uint64, C.POINTER(_P)]),

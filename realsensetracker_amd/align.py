@@ -12,6 +12,8 @@ the MI355X C ABI (include/rst_align.h):
     ComputeCentroid(cloud)                       -> (3,) float32
     ComputeNormals(cloud, tree, k)               -> (n, 3) float32
     OrientNormals(cloud, viewpoint, normals)     (in place)
+    RemoveNans(cloud)                            -> (k, 3) float32
+    DownsampleVoxel(cloud, voxel_size)           -> (k, 3) float32
 
 Clouds are (n, 3) float32 arrays (the byte layout of Cloud3f); transforms are
 4x4 float32 arrays in math orientation.
@@ -46,7 +48,8 @@ class Context:
     def synchronize(self):
         L.check(L.lib().rst_ctx_synchronize(self._h), "rst_ctx_synchronize")
 
-    def enable_kernel_timing(self, on: bool = True):
+    def enable_kernel_timing(self, on: "bool | int" = True):
+        """0/False off, 1/True every iteration, k > 1 every k-th."""
         L.check(L.lib().rst_ctx_enable_kernel_timing(self._h, int(on)), "timing")
 
     def last_kernel_time(self):
@@ -227,6 +230,37 @@ def align_prepared(src: Target, target: Target, pose=None,
     return IcpResult(st == L.RST_OK, L.cm_to_pose(buf), float(mc.value), int(it.value))
 
 
+class PendingAlign:
+    """An align enqueued with align_prepared_async; .wait() -> IcpResult."""
+
+    def __init__(self, ctx: Context, pose: np.ndarray, refs):
+        self.ctx = ctx
+        self._buf = L.pose_to_cm(pose)
+        self._refs = refs  # src / target stay alive until wait()
+
+    def wait(self) -> IcpResult:
+        mc = C.c_float(0)
+        it = C.c_int32(0)
+        st = L.check(L.lib().rst_icp_align_wait(self.ctx.handle, L.fptr(self._buf), C.byref(mc),
+                                                C.byref(it)), "rst_icp_align_wait")
+        self._refs = None
+        return IcpResult(st == L.RST_OK, L.cm_to_pose(self._buf), float(mc.value), int(it.value))
+
+
+def align_prepared_async(src: Target, target: Target, ctx: Context, pose=None,
+                         opts: "L.IcpOpts | None" = None) -> PendingAlign:
+    """Enqueue AlignIcp3d(src, target) on ctx's stream and return at once;
+    one pending align per context (use one context per frame pair in
+    flight)."""
+    pose = np.eye(4, dtype=np.float32) if pose is None else np.asarray(pose, np.float32)
+    o = opts if opts is not None else L.default_opts()
+    p = PendingAlign(ctx, pose, (src, target))
+    L.check(L.lib().rst_icp_align_prepared_async(ctx.handle, src.handle, target.handle,
+                                                 C.byref(o), L.fptr(L.pose_to_cm(pose))),
+            "rst_icp_align_prepared_async")
+    return p
+
+
 def AlignIcp3d(src, dst, *args, opts: "L.IcpOpts | None" = None) -> bool:
     """AlignIcp3d(src, dst, max_iter, T) / AlignIcp3d(src, dst, dst_tree, max_iter, T).
 
@@ -292,6 +326,31 @@ def ComputeCentroid(cloud, ctx: Context | None = None) -> np.ndarray:
     L.check(L.lib().rst_compute_centroid(ctx.handle, L.fptr(a), a.shape[0], L.fptr(out)),
             "rst_compute_centroid")
     return out
+
+
+def RemoveNans(cloud, ctx: Context | None = None) -> np.ndarray:
+    """point_cloud_utils.cpp:163-174: the points with three finite
+    coordinates, in input order."""
+    ctx = ctx or get_context()
+    a = L.as_cloud(cloud)
+    out = np.zeros_like(a)
+    n = C.c_int64(0)
+    L.check(L.lib().rst_remove_nans(ctx.handle, L.fptr(a), a.shape[0], L.fptr(out), C.byref(n)),
+            "rst_remove_nans")
+    return out[:n.value].copy()
+
+
+def DownsampleVoxel(cloud, voxel_size: float, ctx: Context | None = None) -> np.ndarray:
+    """point_cloud_utils.cpp:34-68: the first point of every voxel
+    floor(p / voxel_size).  Returned in ascending input index; the reference
+    returns the same points in its unordered_map's order (unspecified)."""
+    ctx = ctx or get_context()
+    a = L.as_cloud(cloud)
+    out = np.zeros_like(a)
+    n = C.c_int64(0)
+    L.check(L.lib().rst_downsample_voxel(ctx.handle, L.fptr(a), a.shape[0], float(voxel_size),
+                                         L.fptr(out), C.byref(n)), "rst_downsample_voxel")
+    return out[:n.value].copy()
 
 
 def ComputeNormals(cloud, tree: Target, num_neighbors: int = 16,

@@ -406,12 +406,13 @@ int target_build_device(rst_ctx* ctx, const float* d_xyz, int64_t m, bool with_b
   rst_target* t = new rst_target();
   t->ctx = ctx;
   t->m = m;
+  ctx->live.push_back(t);
   hipStream_t st = ctx->stream;
   const int64_t mp = std::max<int64_t>(m, 1);
-  if (hipMalloc(&t->pts, sizeof(float4) * mp) != hipSuccess ||
-      hipMalloc(&t->inv, sizeof(int32_t) * mp) != hipSuccess ||
-      hipMalloc(&t->pleaf, sizeof(int32_t) * mp) != hipSuccess ||
-      hipMalloc(&t->codes, sizeof(uint32_t) * mp + sizeof(float) * 8) != hipSuccess) {
+  auto ta = [&](auto** p, size_t bytes) { return target_alloc(t, bytes, (void**)p) >= 0; };
+  if (!ta(&t->pts, sizeof(float4) * mp) || !ta(&t->inv, sizeof(int32_t) * mp) ||
+      !ta(&t->pleaf, sizeof(int32_t) * mp) ||
+      !ta(&t->codes, sizeof(uint32_t) * mp + sizeof(float) * 8)) {
     rst_target_free(t);
     return RST_E_NOMEM;
   }
@@ -426,19 +427,12 @@ int target_build_device(rst_ctx* ctx, const float* d_xyz, int64_t m, bool with_b
     }
     t->nleaves = (int32_t)nl;
     t->lg = lg;
-    if (hipMalloc(&t->nodes, sizeof(float4) * 4 * nl) != hipSuccess ||
-        hipMalloc(&t->lstart, sizeof(int32_t) * (nl + 1)) != hipSuccess ||
-        hipMalloc(&t->adj, sizeof(float4) * 2 * kAdjK * nl) != hipSuccess ||
-        hipMalloc(&t->reach, sizeof(float) * nl) != hipSuccess ||
-        hipMalloc(&t->adj2, sizeof(float4) * 2 * kAdjK * std::max<int64_t>(nl >> kAdj2Shift, 1)) !=
-            hipSuccess ||
-        hipMalloc(&t->reach2, sizeof(float) * std::max<int64_t>(nl >> kAdj2Shift, 1)) !=
-            hipSuccess)
-      return RST_E_NOMEM;
-    if (hipMalloc(&t->adj3, sizeof(float4) * 2 * kAdjK * std::max<int64_t>(nl >> kAdj3Shift, 1)) !=
-            hipSuccess ||
-        hipMalloc(&t->reach3, sizeof(float) * std::max<int64_t>(nl >> kAdj3Shift, 1)) !=
-            hipSuccess)
+    const int64_t n2 = std::max<int64_t>(nl >> kAdj2Shift, 1);
+    const int64_t n3 = std::max<int64_t>(nl >> kAdj3Shift, 1);
+    if (!ta(&t->nodes, sizeof(float4) * 4 * nl) || !ta(&t->lstart, sizeof(int32_t) * (nl + 1)) ||
+        !ta(&t->adj, sizeof(float4) * 2 * kAdjK * nl) || !ta(&t->reach, sizeof(float) * nl) ||
+        !ta(&t->adj2, sizeof(float4) * 2 * kAdjK * n2) || !ta(&t->reach2, sizeof(float) * n2) ||
+        !ta(&t->adj3, sizeof(float4) * 2 * kAdjK * n3) || !ta(&t->reach3, sizeof(float) * n3))
       return RST_E_NOMEM;
     if (nl < (1 << kAdj2Shift) && hipMemsetAsync(t->reach2, 0, sizeof(float), st) != hipSuccess)
       return RST_E_HIP;

@@ -23,6 +23,52 @@ void set_last_error(hipError_t e, const char* what, const char* file, int line) 
   if (getenv("RST_VERBOSE")) fprintf(stderr, "[rst] %s\n", g_last_error);
 }
 
+static size_t size_class(size_t bytes) {
+  size_t b = bytes < 256 ? 256 : bytes;
+  int lg = 63 - __builtin_clzll(b);
+  const size_t step = lg >= 3 ? ((size_t)1 << (lg - 3)) : 1;
+  return (b + step - 1) / step * step;
+}
+
+constexpr size_t kPoolMaxBytes = (size_t)4 << 30;
+
+int ctx_alloc(rst_ctx* ctx, size_t bytes, void** out, size_t* class_bytes) {
+  const size_t c = size_class(bytes);
+  *class_bytes = c;
+  auto it = ctx->pool.find(c);
+  if (it != ctx->pool.end()) {
+    *out = it->second;
+    ctx->pool.erase(it);
+    ctx->pool_bytes -= c;
+    return RST_OK;
+  }
+  if (hipMalloc(out, c) != hipSuccess) {
+    // give the cached blocks back and retry once
+    for (auto& kv : ctx->pool) hipFree(kv.second);
+    ctx->pool.clear();
+    ctx->pool_bytes = 0;
+    if (hipMalloc(out, c) != hipSuccess) return RST_E_NOMEM;
+  }
+  return RST_OK;
+}
+
+void ctx_release(rst_ctx* ctx, void* p, size_t c) {
+  if (!p) return;
+  if (ctx && ctx->pool_bytes + c <= kPoolMaxBytes) {
+    ctx->pool.emplace(c, p);
+    ctx->pool_bytes += c;
+  } else {
+    hipFree(p);
+  }
+}
+
+int target_alloc(rst_target* t, size_t bytes, void** out) {
+  size_t c = 0;
+  RST_CHECK(ctx_alloc(t->ctx, bytes, out, &c));
+  t->allocs.emplace_back(*out, c);
+  return RST_OK;
+}
+
 int ctx_workspace(rst_ctx* ctx, size_t bytes, void** out) {
   if (bytes > ctx->ws_bytes) {
     if (ctx->ws) {
@@ -176,6 +222,8 @@ int rst_ctx_destroy(rst_ctx* ctx) {
   if (ctx->h_state) hipHostFree(ctx->h_state);
   if (ctx->d_slab) hipFree(ctx->d_slab);
   if (ctx->own_stream) hipStreamDestroy(ctx->own_stream);
+  for (rst_target* t : ctx->live) t->ctx = nullptr;  // they free to the device
+  for (auto& kv : ctx->pool) hipFree(kv.second);
   delete ctx;
   return RST_OK;
 }
@@ -202,6 +250,7 @@ int rst_ctx_last_kernel_time(rst_ctx* ctx, float* avg_ms, int32_t* launches) {
 int rst_ctx_enable_kernel_timing(rst_ctx* ctx, int enable) {
   if (!ctx) return RST_E_ARG;
   ctx->timing = enable != 0;
+  ctx->timing_stride = enable > 1 ? enable : 1;
   return RST_OK;
 }
 
@@ -225,21 +274,20 @@ int rst_target_build_device(rst_ctx* ctx, const float* d_xyz, int64_t m, rst_tar
 
 int rst_target_free(rst_target* t) {
   if (!t) return RST_OK;
-  // hipFree waits for outstanding work on the buffers; the handle does not
-  // touch its context, which may already be gone
-  if (t->pts) hipFree(t->pts);
-  if (t->nodes) hipFree(t->nodes);
-  if (t->nrm) hipFree(t->nrm);
-  if (t->inv) hipFree(t->inv);
-  if (t->codes) hipFree(t->codes);
-  if (t->lstart) hipFree(t->lstart);
-  if (t->pleaf) hipFree(t->pleaf);
-  if (t->adj) hipFree(t->adj);
-  if (t->reach) hipFree(t->reach);
-  if (t->adj2) hipFree(t->adj2);
-  if (t->reach2) hipFree(t->reach2);
-  if (t->adj3) hipFree(t->adj3);
-  if (t->reach3) hipFree(t->reach3);
+  // blocks go back to the context's pool (no device-wide sync); once the
+  // context is gone, to the device
+  rst_ctx* ctx = t->ctx;
+  if (ctx) {
+    auto& lv = ctx->live;
+    for (size_t k = 0; k < lv.size(); ++k)
+      if (lv[k] == t) {
+        lv[k] = lv.back();
+        lv.pop_back();
+        break;
+      }
+    hipSetDevice(ctx->device);
+  }
+  for (auto& a : t->allocs) ctx_release(ctx, a.first, a.second);
   delete t;
   return RST_OK;
 }
@@ -361,7 +409,7 @@ int rst_debug_query_nn_fallback(rst_ctx* ctx, const rst_target* t, const float* 
                                 const int32_t* warm, int mode, int32_t* idx, float* d2,
                                 int32_t* path) {
   if (!ctx || !t || nq < 0 || (nq > 0 && (!q || !idx || !d2 || !path))) return RST_E_ARG;
-  if (mode != 0 && mode != 2 && mode != 3 && mode != 23) return RST_E_ARG;
+  if (mode != 0 && mode != 2 && mode != 3 && mode != 23 && (mode < 100 || mode > 102)) return RST_E_ARG;
   if (nq == 0) return RST_OK;
   if (t->m == 0) return RST_E_ARG;
   RST_HIP(hipSetDevice(ctx->device));
@@ -432,6 +480,26 @@ int rst_icp_align_prepared(rst_ctx* ctx, const rst_target* src, const rst_target
   if (!ctx || !src || !tgt || !pose_inout) return RST_E_ARG;
   RST_HIP(hipSetDevice(ctx->device));
   return icp_align_prepared(ctx, src, tgt, opts, pose_inout, mean_cost, iterations_run, nullptr);
+}
+
+int rst_icp_align_prepared_async(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
+                                 const rst_icp_opts* opts, const float pose_in[16]) {
+  if (!ctx || !src || !tgt || !pose_in) return RST_E_ARG;
+  if (ctx->pend.active) return RST_E_STATE;  // one align in flight per context
+  RST_HIP(hipSetDevice(ctx->device));
+  const int s = icp_launch(ctx, src, tgt, opts, pose_in, nullptr);
+  if (s == RST_FALSE) {  // the reference's early false: _wait reports it
+    ctx->pend.active = true;
+    ctx->pend.early_false = true;
+  }
+  return s;
+}
+
+int rst_icp_align_wait(rst_ctx* ctx, float pose_inout[16], float* mean_cost,
+                       int32_t* iterations_run) {
+  if (!ctx || !pose_inout) return RST_E_ARG;
+  RST_HIP(hipSetDevice(ctx->device));
+  return icp_finish(ctx, pose_inout, mean_cost, iterations_run);
 }
 
 int rst_icp_align_device(rst_ctx* ctx, const float* d_src, int64_t n, const rst_target* tgt,

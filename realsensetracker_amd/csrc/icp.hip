@@ -182,12 +182,15 @@ struct P2PointAcc {
   static constexpr int NV = kNP2Point;  // sum w q u^T (9), sum w u (3), sum q (3), sum d2
   static constexpr int RS = 16;         // slab row stride (doubles; divides kRedBS)
   static constexpr bool kCanFinish = false;
+  // q = the neighbour's coordinates (the caller has them), bp its sorted
+  // position; no neighbour (bp < 0) -> dst[0], d2 = FLT_MAX
   __device__ static void add(double (&v)[NV], const BvhView& bv, const AccArgs& a, const Uni& u,
-                             const float4& s, float px, float py, float pz, float bd, int bp) {
+                             const float4& s, float px, float py, float pz, float bd, int bp,
+                             float4 q) {
     (void)px; (void)py; (void)pz;
     const float l = u.mu / (bd + u.mu);  // :116-117
     const float w = l * l;
-    const float4 q = bv.pts[bp >= 0 ? bp : a.pos0];
+    if (bp < 0) q = bv.pts[a.pos0];
     const float u0 = s.x - u.sm0, u1 = s.y - u.sm1, u2 = s.z - u.sm2;
     const double dw = (double)w;
     const double wq0 = dw * (double)q.x, wq1 = dw * (double)q.y, wq2 = dw * (double)q.z;
@@ -207,10 +210,10 @@ struct P2PlaneAcc {
   static constexpr int RS = 32;
   static constexpr bool kCanFinish = true;
   __device__ static void add(double (&v)[NV], const BvhView& bv, const AccArgs& a, const Uni& u,
-                             const float4& s, float px, float py, float pz, float bd, int bp) {
-    (void)u; (void)s;
+                             const float4& s, float px, float py, float pz, float bd, int bp,
+                             float4 q) {
+    (void)u; (void)s; (void)bv;
     if (bp < 0 || !(bd <= a.max_d2)) return;
-    const float4 q = bv.pts[bp];
     const float4 nn = a.nrm[bp];
     const float e0 = px - q.x, e1 = py - q.y, e2 = pz - q.z;
     const float r = (nn.x * e0 + nn.y * e1) + nn.z * e2;
@@ -333,7 +336,7 @@ __global__ __launch_bounds__(kBS) void k_icp_nn(BvhView bv, AdjView av, AccArgs 
   if (threadIdx.x == 0) qcnt[blockIdx.x] = total;
   if (done) {
     nnpos[i] = r.pos;
-    Acc::add(v, bv, aa, u, s, px, py, pz, r.d, r.pos);
+    Acc::add(v, bv, aa, u, s, px, py, pz, r.d, r.pos, bv.pts[r.pos >= 0 ? r.pos : 0]);
   }
   block_sum_to_slab<Acc::NV, kBS>(v, lds, slab + (int64_t)blockIdx.x * Acc::RS);
 }
@@ -611,8 +614,8 @@ __global__ __launch_bounds__(kRedBS) void k_reduce_solve(const double* __restric
     *static_cast<IcpCore*>(st) = core;
     const uint64_t t2 = __builtin_amdgcn_s_memrealtime();
     if (it < kQTrace) {  // diagnostics (rst_debug_queue_trace): 10 ns ticks
-      st->path[it][1] = (int)(t1 - t0);
-      st->path[it][2] = (int)(t2 - t1);
+      st->path[it][2] = (int)(t1 - t0);
+      st->path[it][3] = (int)(t2 - t1);
     }
   }
 }
@@ -692,7 +695,7 @@ __global__ __launch_bounds__(kBS) void k_icp_fb(BvhView bv, AdjView av, AccArgs 
         nn_wave_one(bv, warm, px, py, pz, r, wsc[wid]);
       if (lane == 0) {
         nnpos[i] = r.pos;
-        Acc::add(v, bv, aa, u, s, px, py, pz, r.d, r.pos);
+        Acc::add(v, bv, aa, u, s, px, py, pz, r.d, r.pos, bv.pts[r.pos >= 0 ? r.pos : 0]);
       }
     }
   }
@@ -760,10 +763,14 @@ int centroid_device(rst_ctx* ctx, const float4* d_pts, int64_t n, double* d_out)
   return nb;
 }
 
-int icp_align_prepared(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
-                       const rst_icp_opts* opts_in, float pose_inout[16], float* mean_cost,
-                       int32_t* iters_run, rst_comm* comm) {
-  if (!ctx || !src || !tgt || !pose_inout) return RST_E_ARG;
+// Enqueue a whole AlignIcp3d on the context's stream (no host round trip
+// on a single GPU); icp_finish waits and reads the result.  Returns RST_OK
+// when enqueued, RST_FALSE for the reference's early false (nothing
+// enqueued), or an error.
+int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
+               const rst_icp_opts* opts_in, const float pose_in[16], rst_comm* comm) {
+  if (!ctx || !src || !tgt || !pose_in) return RST_E_ARG;
+  ctx->pend = {};
   rst_icp_opts opts;
   if (opts_in)
     opts = *opts_in;
@@ -782,6 +789,7 @@ int icp_align_prepared(rst_ctx* ctx, const rst_target* src, const rst_target* tg
   const int NV = p2plane ? kNP2Plane : kNP2Point;
   const int RS = p2plane ? P2PlaneAcc::RS : P2PointAcc::RS;
   const int ncb = std::min(1024, blocks_for(n_local));
+  // [kernel 1 (+ centroid) | kernel 3 | totals]
   const size_t rows1 = (size_t)std::max(nblk * RS, ncb * 4);
   const size_t slab_doubles = rows1 + (size_t)kFbBlocks * RS + 64;
   double* slab = nullptr;
@@ -804,7 +812,7 @@ int icp_align_prepared(rst_ctx* ctx, const rst_target* src, const rst_target* tg
   if (p2plane && n_total < 6) return RST_FALSE;
 
   InitArgs ia;
-  memcpy(ia.pose, pose_inout, sizeof(ia.pose));
+  memcpy(ia.pose, pose_in, sizeof(ia.pose));
   ia.mu0 = opts.mu0;
   ia.need_centroid = p2plane ? 0 : 1;
   int crows = 0;
@@ -825,7 +833,8 @@ int icp_align_prepared(rst_ctx* ctx, const rst_target* src, const rst_target* tg
   }
   // per source point: sorted target position of its last neighbour (warm
   // start of the next iteration's exact search; -1 = cold); the fallback
-  // queue (one kBS segment per kernel-1 block) and its per-block counts
+  // queue (one kBS segment per kernel-1 block), its per-block counts and
+  // their prefix
   int32_t *nnpos = nullptr, *qbuf = nullptr, *qcnt = nullptr, *pref = nullptr;
   {
     const size_t np = (size_t)std::max<int64_t>(n_local, 1);
@@ -869,29 +878,30 @@ int icp_align_prepared(rst_ctx* ctx, const rst_target* src, const rst_target* tg
   }
   double* red_out = comm ? totals : nullptr;  // multi-GPU: reduce only
   for (int it = 0; it < opts.max_iter; ++it) {
-    if (timing) RST_HIP(hipEventRecord(ctx->ev[2 * it], st));
+    const bool tm = timing && it % ctx->timing_stride == 0;  // sampled iterations
+    if (tm) RST_HIP(hipEventRecord(ctx->ev[2 * it], st));
     if (n_local > 0) {
       if (p2plane) {
         k_icp_nn<P2PlaneAcc><<<nblk, kBS, 0, st>>>(bv, av, aa, src->pts, n_local, ctx->d_state,
                                                    nnpos, qbuf, qcnt, slab);
-        if (timing) RST_HIP(hipEventRecord(ctx->ev[2 * it + 1], st));
+        if (tm) RST_HIP(hipEventRecord(ctx->ev[2 * it + 1], st));
         k_queue_prefix<<<1, kBS, 0, st>>>(qcnt, nblk, pref, ctx->d_state);
-        k_icp_fb<P2PlaneAcc><<<kFbBlocks, kBS, fb_lds, st>>>(bv, av, aa, src->pts, ctx->d_state, nnpos,
-                                                             qbuf, pref, nblk, slab2);
+        k_icp_fb<P2PlaneAcc><<<kFbBlocks, kBS, fb_lds, st>>>(bv, av, aa, src->pts, ctx->d_state,
+                                                             nnpos, qbuf, pref, nblk, slab2);
         k_reduce_solve<P2PlaneAcc><<<1, kRedBS, 0, st>>>(slab, nblk, slab2, kFbBlocks, prm,
                                                          ctx->d_state, red_out);
       } else {
         k_icp_nn<P2PointAcc><<<nblk, kBS, 0, st>>>(bv, av, aa, src->pts, n_local, ctx->d_state,
                                                    nnpos, qbuf, qcnt, slab);
-        if (timing) RST_HIP(hipEventRecord(ctx->ev[2 * it + 1], st));
+        if (tm) RST_HIP(hipEventRecord(ctx->ev[2 * it + 1], st));
         k_queue_prefix<<<1, kBS, 0, st>>>(qcnt, nblk, pref, ctx->d_state);
-        k_icp_fb<P2PointAcc><<<kFbBlocks, kBS, fb_lds, st>>>(bv, av, aa, src->pts, ctx->d_state, nnpos,
-                                                             qbuf, pref, nblk, slab2);
+        k_icp_fb<P2PointAcc><<<kFbBlocks, kBS, fb_lds, st>>>(bv, av, aa, src->pts, ctx->d_state,
+                                                             nnpos, qbuf, pref, nblk, slab2);
         k_reduce_solve<P2PointAcc><<<1, kRedBS, 0, st>>>(slab, nblk, slab2, kFbBlocks, prm,
                                                          ctx->d_state, red_out);
       }
     } else {
-      if (timing) RST_HIP(hipEventRecord(ctx->ev[2 * it + 1], st));
+      if (tm) RST_HIP(hipEventRecord(ctx->ev[2 * it + 1], st));
       // an empty shard still joins the all-reduce with zero partial sums
       RST_HIP(hipMemsetAsync(totals, 0, sizeof(double) * NV, st));
     }
@@ -905,23 +915,39 @@ int icp_align_prepared(rst_ctx* ctx, const rst_target* src, const rst_target* tg
   }
   RST_HIP(hipGetLastError());
   RST_HIP(hipMemcpyAsync(ctx->h_state, ctx->d_state, sizeof(IcpState), hipMemcpyDeviceToHost, st));
-  RST_HIP(hipStreamSynchronize(st));
-  if (timing) {
+  ctx->pend.active = true;
+  ctx->pend.p2plane = p2plane;
+  ctx->pend.timing = timing;
+  ctx->pend.max_iter = opts.max_iter;
+  ctx->pend.n_total = n_total;
+  return RST_OK;
+}
+
+int icp_finish(rst_ctx* ctx, float pose_inout[16], float* mean_cost, int32_t* iters_run) {
+  if (!ctx || !pose_inout) return RST_E_ARG;
+  if (!ctx->pend.active) return RST_E_STATE;
+  const auto pd = ctx->pend;
+  ctx->pend.active = false;
+  if (pd.early_false) return RST_FALSE;  // pose untouched (align_icp.cpp:77-79)
+  RST_HIP(hipStreamSynchronize(ctx->stream));
+  if (pd.timing) {
     float total = 0.f;
-    for (int it = 0; it < opts.max_iter; ++it) {
+    int cnt = 0;
+    for (int it = 0; it < pd.max_iter; it += ctx->timing_stride) {
       float ms = 0.f;
       RST_HIP(hipEventElapsedTime(&ms, ctx->ev[2 * it], ctx->ev[2 * it + 1]));
       total += ms;
+      ++cnt;
     }
-    ctx->last_kernel_ms = total / opts.max_iter;
-    ctx->last_kernel_launches = opts.max_iter;
+    ctx->last_kernel_ms = cnt ? total / cnt : 0.f;
+    ctx->last_kernel_launches = cnt;
   }
   const IcpState& h = *ctx->h_state;
-  if (p2plane && h.fail) {
+  if (pd.p2plane && h.fail) {
     if (iters_run) *iters_run = h.iter;
     return RST_FALSE;
   }
-  if (opts.max_iter > 0 || p2plane) {
+  if (pd.max_iter > 0 || pd.p2plane) {
     for (int c = 0; c < 3; ++c) {
       for (int r = 0; r < 3; ++r) pose_inout[c * 4 + r] = h.R[c * 3 + r];
       pose_inout[c * 4 + 3] = 0.f;
@@ -931,15 +957,23 @@ int icp_align_prepared(rst_ctx* ctx, const rst_target* src, const rst_target* tg
   }
   if (iters_run) *iters_run = h.iter;
   float mc;
-  if (p2plane) {
+  if (pd.p2plane) {
     mc = h.last_cnt > 0 ? (float)sqrt(h.last_d2 / h.last_cnt) : 0.f;
   } else {
     // :157 mean_cost = sqrt(cost / n) with cost the last iteration's sum d2
-    mc = sqrtf(h.last_cost / (float)n_total);
+    mc = sqrtf(h.last_cost / (float)pd.n_total);
   }
   if (mean_cost) *mean_cost = mc;
-  if (p2plane) return RST_OK;
+  if (pd.p2plane) return RST_OK;
   return (mc < 10000.0f) ? RST_OK : RST_FALSE;  // :160 (NaN -> false)
+}
+
+int icp_align_prepared(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
+                       const rst_icp_opts* opts, float pose_inout[16], float* mean_cost,
+                       int32_t* iters_run, rst_comm* comm) {
+  const int s = icp_launch(ctx, src, tgt, opts, pose_inout, comm);
+  if (s != RST_OK) return s;  // error, or the early false with the pose untouched
+  return icp_finish(ctx, pose_inout, mean_cost, iters_run);
 }
 
 }  // namespace rst

@@ -83,6 +83,7 @@ __global__ __launch_bounds__(kBS) void k_query_nn_fallback(BvhView bv, AdjView a
   const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
   const int64_t i = blockIdx.x * (int64_t)(kBS / kWave) + wid;
   if (i >= nq) return;  // wave-uniform
+  const uint64_t t0 = __builtin_amdgcn_s_memtime();
   const float qx = q[3 * i], qy = q[3 * i + 1], qz = q[3 * i + 2];
   Best1 r;
   r.init();
@@ -100,11 +101,15 @@ __global__ __launch_bounds__(kBS) void k_query_nn_fallback(BvhView bv, AdjView a
            nn_wave_adj(bv, av, kAdj3Shift, start, qx, qy, qz, r, wsc[wid]))
     how = 3;
   else
-    nn_wave_one(bv, start, qx, qy, qz, r, wsc[wid]);
+    nn_wave_one(bv, start, qx, qy, qz, r, wsc[wid], mode >= 100 ? mode - 100 : 0);
+  const uint64_t t1 = __builtin_amdgcn_s_memtime();
   if (lane == 0) {
     idx[i] = r.pos >= 0 ? r.id : 0;
     d2[i] = r.d;
-    path[i] = how;
+    // strategy in the low 4 bits, the wave's shader cycles / 16 above
+    uint64_t c16 = (t1 - t0) >> 4;
+    if (c16 > (uint64_t)((1u << 27) - 1)) c16 = (1u << 27) - 1;
+    path[i] = how | ((int)c16 << 4);
   }
 }
 
@@ -300,7 +305,7 @@ int compute_normals(rst_ctx* ctx, rst_target* tgt, int k, const float vp[3]) {
   // (std::vector<int> oi(k) zero-initialised); not supported here
   if (tgt->m < k) return RST_E_ARG;
   if (!tgt->nrm) {
-    if (hipMalloc(&tgt->nrm, sizeof(float4) * std::max<int64_t>(tgt->m, 1)) != hipSuccess)
+    if (target_alloc(tgt, sizeof(float4) * std::max<int64_t>(tgt->m, 1), (void**)&tgt->nrm) < 0)
       return RST_E_NOMEM;
   }
   if (tgt->m == 0) return RST_OK;

@@ -186,6 +186,7 @@ struct BestK {
     }
   }
   RST_HD float bound() const { return d[K - 1]; }
+  RST_HD float radius() const { return sqrtf(d[K - 1]); }
   RST_HD void offer(float nd, int nid, int np) {
     if (!(nd < FLT_MAX) || !lex_less(nd, nid, d[K - 1], id[K - 1])) return;
 #pragma unroll

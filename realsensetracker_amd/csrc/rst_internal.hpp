@@ -11,6 +11,8 @@
 #include <cstddef>
 #include <cstdint>
 #include <cstdio>
+#include <map>
+#include <utility>
 #include <vector>
 
 #include "rst_align.h"
@@ -98,9 +100,26 @@ struct rst_ctx {
   size_t slab_bytes = 0;
   // timing of the dominant per-iteration kernel
   bool timing = false;
+  int timing_stride = 1;              // time every timing_stride-th iteration
   std::vector<hipEvent_t> ev;
   float last_kernel_ms = 0.f;
   int32_t last_kernel_launches = 0;
+  // device memory of freed targets, kept for the next build (hipFree
+  // synchronises the whole device, which would stall every stream of a
+  // pipelined frame loop): size class -> blocks
+  std::multimap<size_t, void*> pool;
+  size_t pool_bytes = 0;
+  std::vector<rst_target*> live;  // targets built on this context
+  // the align enqueued by icp_launch and not yet collected by icp_finish
+  struct Pending {
+    bool early_false = false;
+    bool active = false;
+    bool p2plane = false;
+    bool timing = false;
+  int timing_stride = 1;              // time every timing_stride-th iteration
+    int32_t max_iter = 0;
+    int64_t n_total = 0;
+  } pend;
 };
 
 struct rst_target {
@@ -124,9 +143,17 @@ struct rst_target {
   float bbox[6] = {0, 0, 0, 0, 0, 0};
   int32_t pos0 = 0;             // sorted position of original point 0
   bool has_bvh = false;
+  std::vector<std::pair<void*, size_t>> allocs;  // every device block (size class)
 };
 
 namespace rst {
+
+// device memory through the context's pool (capi.hip): blocks are rounded
+// to a size class (1/8 of a power of two), reused first-fit by class
+int ctx_alloc(rst_ctx* ctx, size_t bytes, void** out, size_t* class_bytes);
+void ctx_release(rst_ctx* ctx, void* p, size_t class_bytes);
+// a target-owned block (freed with the target)
+int target_alloc(rst_target* t, size_t bytes, void** out);
 
 // workspace helpers (implemented in capi.hip)
 int ctx_workspace(rst_ctx* ctx, size_t bytes, void** out);
@@ -154,6 +181,9 @@ int query_knn_device(rst_ctx* ctx, const rst_target* tgt, const float* d_q,
 int compute_normals(rst_ctx* ctx, rst_target* tgt, int k, const float vp[3]);
 
 // ICP (icp.hip)
+int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
+               const rst_icp_opts* opts, const float pose_in[16], rst_comm* comm);
+int icp_finish(rst_ctx* ctx, float pose_inout[16], float* mean_cost, int32_t* iters_run);
 int icp_align_prepared(rst_ctx* ctx, const rst_target* src,
                        const rst_target* tgt, const rst_icp_opts* opts,
                        float pose_inout[16], float* mean_cost,
@@ -169,6 +199,12 @@ int kabsch_device(rst_ctx* ctx, const double cov[9], const float smean[3],
 int unproject_device(rst_ctx* ctx, const uint16_t* d_depth,
                      const rst_intrinsics* K, int keep_invalid,
                      float* d_xyz, int64_t* n_out);
+
+// RemoveNans / DownsampleVoxel (voxel.hip); synchronous (n_out is host)
+int remove_nans_device(rst_ctx* ctx, const float* d_xyz, int64_t n, float* d_out,
+                       int64_t* n_out);
+int downsample_voxel_device(rst_ctx* ctx, const float* d_xyz, int64_t n, float voxel,
+                            float* d_out, int64_t* n_out);
 
 // RCCL (comm.hip)
 int comm_allreduce_sum_f64(rst_comm* comm, double* d_buf, size_t count,

@@ -420,8 +420,27 @@ __device__ __forceinline__ Best1 wave_lex_min(Best1 b) {
 // minimum of every lane's offers.
 template <class R>
 __device__ __forceinline__ void wnn_flush_one(const BvhView& bv, WnnScratch& ws, int ns, float qx,
-                                              float qy, float qz, R& mine, R& r) {
+                                              float qy, float qz, R& mine, R& r, int variant = 0) {
   const int lane = __lane_id();
+  if (variant == 2) {  // DEBUG: the original one-leaf-group-at-a-time scan
+    const int g = lane >> 4, o = lane & 15;
+    for (int s = 0; s < ns; s += 4) {
+      if (s + g < ns) {
+        const float4 e = ws.leaf_lo[s + g];
+        if (e.x <= r.bound()) {
+          const int L = f2i(e.w);
+          const int b = leaf_begin(bv, L);
+          if (o < leaf_begin(bv, L + 1) - b) {
+            const float4 p = bv.pts[b + o];
+            mine.offer(d2_ref(qx, qy, qz, p.x, p.y, p.z), f2i(p.w), b + o);
+          }
+        }
+      }
+    }
+    r = wave_lex_min(mine);
+    wave_sync();
+    return;
+  }
   for (int s = lane; s < ns; s += kWave) {
     const int L = f2i(ws.leaf_lo[s].w);
     const int b = leaf_begin(bv, L);
@@ -442,7 +461,7 @@ __device__ __forceinline__ void wnn_flush_one(const BvhView& bv, WnnScratch& ws,
       if (s < ns) {
         const float bd = ws.leaf_lo[s].x;
         const float4 rg = ws.leaf_hi[s];
-        if (bd <= bnd && o < f2i(rg.w)) pos[k] = f2i(rg.z) + o;
+        if ((variant == 1 || bd <= bnd) && o < f2i(rg.w)) pos[k] = f2i(rg.z) + o;
       }
       p[k] = bv.pts[pos[k] >= 0 ? pos[k] : last];
     }
@@ -461,7 +480,7 @@ __device__ __forceinline__ void wnn_flush_one(const BvhView& bv, WnnScratch& ws,
 // subtrees on the initial stack.
 template <class R>
 __device__ __forceinline__ void nn_wave_walk(const BvhView& bv, int sp, float qx, float qy,
-                                             float qz, R& r, WnnScratch& ws) {
+                                             float qz, R& r, WnnScratch& ws, int variant = 0) {
   const int lane = __lane_id();
   const int nl = bv.nleaves;
   R mine = r;
@@ -502,7 +521,7 @@ __device__ __forceinline__ void nn_wave_walk(const BvhView& bv, int sp, float qx
       wave_sync();
     }
     if (ns > kWnnLeaves - kWnnPop || (sp == 0 && ns > 0)) {
-      wnn_flush_one(bv, ws, ns, qx, qy, qz, mine, r);
+      wnn_flush_one(bv, ws, ns, qx, qy, qz, mine, r, variant);
       ns = 0;
     }
   }
@@ -514,7 +533,7 @@ __device__ __forceinline__ void nn_wave_walk(const BvhView& bv, int sp, float qx
 // partition of the tree).
 template <class R>
 __device__ __forceinline__ void nn_wave_one(const BvhView& bv, int warm, float qx, float qy,
-                                            float qz, R& r, WnnScratch& ws) {
+                                            float qz, R& r, WnnScratch& ws, int variant = 0) {
   const int lane = __lane_id();
   const int nl = bv.nleaves;
   if (bv.m <= 0 || !finite3(qx, qy, qz)) return;
@@ -522,7 +541,7 @@ __device__ __forceinline__ void nn_wave_one(const BvhView& bv, int warm, float q
   const int depth = 31 - __clz(start);
   if (lane < depth) ws.stack[lane] = (int)((start >> (depth - 1 - lane)) ^ 1u);
   if (lane == 0) ws.stack[depth] = (int)start;
-  nn_wave_walk(bv, depth + 1, qx, qy, qz, r, ws);
+  nn_wave_walk(bv, depth + 1, qx, qy, qz, r, ws, variant);
 }
 
 // Exact 1-NN of one query through the level-2 (shift = kAdj2Shift: items =
@@ -680,6 +699,135 @@ RST_HD bool adj_search_wide(const BvhView& bv, const AdjView& av, int start,
     if (stop) break;
   }
   return true;
+}
+
+// ---- the ICP loop's candidate lists ----------------------------------------------------
+// Exact K nearest of q (r empty: BestK keeps duplicate offers) through the
+// leaf adjacency of the leaf holding sorted position `start`: the entries in
+// order of box distance, each scanned when its box meets the ball of the
+// running K-th distance, until an entry lies beyond that ball (sorted: all
+// later ones do too); then the coverage test with the FINAL radius -- every
+// point inside the final ball lies in a listed leaf (reach), each listed
+// leaf within it was visited with a ball at least as large.  Returns false
+// (r only improved) when the ball is not covered.  While the list holds
+// fewer than K points the radius is infinite: every entry is scanned.
+template <int K>
+RST_HD bool adj_knn_search(const BvhView& bv, const AdjView& av, int start, float qx, float qy,
+                           float qz, BestK<K>& r) {
+  const int nl = bv.nleaves;
+  const int L = leaf_of(bv, start);
+  const float4 lo = bv.nodes[2 * (nl + L)], hi = bv.nodes[2 * (nl + L) + 1];
+  // margins cover float rounding of every distance (rst_bvh.hpp adj_search)
+  const float dl = sqrtf(box_d2(qx, qy, qz, lo, hi)) * 1.00001f;
+  const float4* e = av.ent + (int64_t)L * kAdjK * 2;
+  for (int k0 = 0; k0 < kAdjK; k0 += 4) {
+    float4 l[4], h[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      l[j] = e[2 * (k0 + j)];
+      h[j] = e[2 * (k0 + j) + 1];
+    }
+    bool stop = false;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (stop) break;
+      const int tag = f2i(h[j].w);
+      if (tag < 0 || l[j].w * 0.99999f - dl > r.radius() * 1.00001f + 1e-30f) {
+        stop = true;
+      } else if (box_d2(qx, qy, qz, l[j], h[j]) <= r.bound()) {
+        scan_range_wide(bv, tag >> 5, tag & 31, qx, qy, qz, r);
+      }
+    }
+    if (stop) break;
+  }
+  return dl + r.radius() * 1.00001f + 1e-30f < av.reach[L] * 0.99999f;
+}
+
+// The exact K nearest of one query through the leaf adjacency of the warm
+// point's leaf, whole wavefront (the ICP loop's list rebuild): lanes 0..23
+// load the 24 entries at once and rank them by box distance to q; leaves
+// are then scanned four per load instruction (16 lanes per leaf) in that
+// order until the next leaf's box lies beyond the running K-th distance, and
+// each batch's points are merged into the list (uniform across the wave) in
+// ascending order.  Exact when covered: every point within the final ball
+// lies in a listed leaf (reach), and every listed leaf whose box meets the
+// final ball was scanned (ascending box order, the ball only shrinks).
+// Returns false (L holds what was found) when the ball is not covered.
+template <int K>
+__device__ __forceinline__ bool nn_wave_knn(const BvhView& bv, const AdjView& av, int warm,
+                                            float qx, float qy, float qz, BestK<K>& L,
+                                            WnnScratch& ws) {
+  const int lane = __lane_id();
+  const int nl = bv.nleaves;
+  L.init();
+  if (bv.m <= 0 || warm < 0 || warm >= bv.m || !finite3(qx, qy, qz)) return false;
+  const int H = leaf_of(bv, warm);
+  const float4* e = av.ent + (int64_t)H * kAdjK * 2;
+  float4 l = make_float4(0.f, 0.f, 0.f, 0.f), h = l;
+  int tag = -1;
+  if (lane < kAdjK) {
+    l = e[2 * lane];
+    h = e[2 * lane + 1];
+    tag = f2i(h.w);
+  }
+  const float4 nlo = bv.nodes[2 * (nl + H)], nhi = bv.nodes[2 * (nl + H) + 1];
+  const float rch = av.reach[H];
+  // margins cover float rounding of every distance (rst_bvh.hpp adj_search)
+  const float dl = sqrtf(box_d2(qx, qy, qz, nlo, nhi)) * 1.00001f;
+  const bool valid = lane < kAdjK && tag >= 0;
+  const float bq = valid ? box_d2(qx, qy, qz, l, h) : FLT_MAX;
+  int rank = 0;
+#pragma unroll
+  for (int j = 0; j < kAdjK; ++j) {
+    const float bj = wnn_rl(bq, j);
+    rank += ((bj < bq) | ((bj == bq) & (j < lane))) ? 1 : 0;
+  }
+  const int nv = __popcll(__ballot(valid));
+  if (valid) ws.leaf_lo[rank] = make_float4(bq, 0.f, 0.f, i2f(tag));
+  wave_sync();
+  const int g = lane >> 4, o = lane & 15;
+  for (int b0 = 0; b0 < nv; b0 += 4) {
+    if (ws.leaf_lo[b0].x > L.bound()) break;  // every later leaf is farther still
+    float d = FLT_MAX;
+    int id = 0x7fffffff, ps = -1;
+    if (b0 + g < nv) {
+      const float4 en = ws.leaf_lo[b0 + g];
+      const int tg = f2i(en.w);
+      if (en.x <= L.bound() && o < (tg & 31)) {
+        ps = (tg >> 5) + o;
+        const float4 p = bv.pts[ps];
+        d = d2_ref(qx, qy, qz, p.x, p.y, p.z);
+        id = f2i(p.w);
+      }
+    }
+    // merge the batch: its candidates that beat the K-th, smallest first
+    bool live = ps >= 0 && lex_less(d, id, L.d[K - 1], L.id[K - 1]);
+    while (__ballot(live)) {
+      Best1 c;
+      c.d = live ? d : FLT_MAX;
+      c.id = live ? id : 0x7fffffff;
+      c.pos = live ? ps : -1;
+      c = wave_lex_min(c);
+      if (!lex_less(c.d, c.id, L.d[K - 1], L.id[K - 1])) break;
+      L.offer(c.d, c.id, c.pos);
+      live = live && id != c.id && lex_less(d, id, L.d[K - 1], L.id[K - 1]);
+    }
+  }
+  wave_sync();
+  return dl + sqrtf(L.bound()) * 1.00001f + 1e-30f < rch * 0.99999f;
+}
+
+// The list certificate (icp.hip): a list made at query position c.xyz holds
+// every target point with d2 < c.w = R2 (the K-th distance of an exact K-NN
+// search; no other point is closer).  For the query now at p, delta =
+// |p - c| away, every point off the list is at least sqrt(R2) - delta from
+// p; when the list's best point is closer than that by the 1e-5 relative
+// margins (float rounding of each distance here is < 1e-6 relative), the
+// list's lexicographic minimum is the exact nearest neighbour.
+RST_HD bool list_cert_holds(const float4& c, float dbest, float px, float py, float pz) {
+  const float ex = px - c.x, ey = py - c.y, ez = pz - c.z;
+  const float del = sqrtf((ex * ex + ey * ey) + ez * ez);
+  return c.w > 0.0f && sqrtf(dbest) * 1.00001f + del * 1.00001f + 1e-30f < sqrtf(c.w) * 0.99999f;
 }
 
 // ---- adjacency build: one wavefront per leaf -------------------------------------

@@ -207,8 +207,8 @@ int rst_frame_prepare_device(rst_ctx* ctx, const uint16_t* d_depth, const rst_in
   RST_HIP(hipSetDevice(ctx->device));
   const int64_t npx = (int64_t)K->width * K->height;
   float* dx = nullptr;
-  if (hipMalloc(&dx, sizeof(float) * 3 * std::max<int64_t>(npx, 1)) != hipSuccess)
-    return RST_E_NOMEM;
+  size_t dxc = 0;
+  RST_CHECK(ctx_alloc(ctx, sizeof(float) * 3 * std::max<int64_t>(npx, 1), (void**)&dx, &dxc));
   int64_t n = 0;
   int s = unproject_device(ctx, d_depth, K, 0, dx, &n);
   rst_target* t = nullptr;
@@ -218,7 +218,7 @@ int rst_frame_prepare_device(rst_ctx* ctx, const uint16_t* d_depth, const rst_in
     s = compute_normals(ctx, t, normals_k, vp);
   }
   hipStreamSynchronize(ctx->stream);
-  hipFree(dx);
+  ctx_release(ctx, dx, dxc);
   if (s < 0) {
     if (t) rst_target_free(t);
     return s;

@@ -21,7 +21,7 @@ off *= (10 ** rng.uniform(-3, np.log10(0.5), 3000)).astype(np.float32)[:, None] 
 q = (pb[sel] + off).astype(np.float32)
 oi, od = tree.query(q)
 gi0, _ = tree.query(pb[sel])
-for mode in (0, 2, 3, 23):
+for mode in (0, 2, 3, 23, 100, 101, 102):
     for wn, warm in (("good", gi0.astype(np.int32)), ("rand", rng.integers(0, len(pa), 3000).astype(np.int32))):
         gi, gd, path = _fallback(ctx, t, q, warm, mode)
         bad = np.nonzero(gd != od)[0]

@@ -44,8 +44,10 @@ def main():
             qt(ctx.handle, L.iptr(q), 256)
             print(f"pair {pair} mode {mode}: n={len(pb)} build {1e3*(t1-t0):.2f} ms  align "
                   f"{1e3*(t3-t2):.2f} ms  iters {r.iterations} ok {r.ok}")
-            print("  fallback queue per iteration:", " ".join(str(x) for x in q[:r.iterations, 0]))
-            print("  solve kernel: reduce / solve (x10 ns):", " ".join(f"{a}/{b}" for a, b in q[:min(r.iterations, 24), 1:3]))
+            print("  slow queue per iteration:", " ".join(str(x) for x in q[:r.iterations, 0]))
+            print("  answered by candidate list:", " ".join(str(x) for x in q[:r.iterations, 1]))
+            print("  lists rebuilt (slow kernel):", " ".join(str(x) for x in q[:r.iterations, 2]))
+            print("  solve kernel: reduce / solve (x10 ns):", " ".join(f"{a}/{b}" for a, b in q[:min(r.iterations, 24), 3:5]))
 
 
 if __name__ == "__main__":

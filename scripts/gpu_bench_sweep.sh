@@ -1,0 +1,8 @@
+#!/bin/bash
+# Bench sweep over pairs in flight (no CPU baseline).
+set -o pipefail
+mkdir -p gpurun_out
+for k in ${INFLIGHT:-1 2 3 4}; do
+  timeout -k 10 300 python bench.py --no-cpu --no-p2plane --inflight $k > gpurun_out/bench_if$k.log 2>&1 || exit $?
+  echo "inflight $k: $(grep '^{' gpurun_out/bench_if$k.log | python3 -c 'import json,sys; d=json.load(sys.stdin); print(round(d["value"]), "it/s", round(d["frames_per_s"],1), "fps k_icp_nn", round(d["roofline"]["avg_us"],1), "us")')"
+done

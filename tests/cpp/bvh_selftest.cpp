@@ -168,7 +168,7 @@ void brute(const std::vector<float>& xyz, float qx, float qy, float qz, BestK<K>
 int g_fail = 0;
 long g_checks = 0;
 long g_covered = 0, g_covered2 = 0, g_covered3 = 0, g_adj_tries = 0;
-long g_wide = 0;
+long g_wide = 0, g_knn_tries = 0, g_knn_cov = 0, g_list_tries = 0, g_list_holds = 0;
 
 void check(bool ok, const char* what, int m, int q) {
   ++g_checks;
@@ -277,6 +277,45 @@ void run_case(std::mt19937_64& rng, int m, int nq, int mode) {
         check(s.d == b1.d[0] && s.id == b1.id[0], "adj wide", m, q);
       }
     }
+    // the ICP candidate lists: exact 8-NN through the adjacency, and a moved
+    // query whose list certificate holds has its nearest neighbour on the list
+    if (m > 0 && finite3(qx, qy, qz)) {
+      const int start = b1.pos[0] >= 0 && (q & 4) ? pos_of(ix, b1.id[0]) : P(rng);
+      BestK<8> k8;  // (no warm offer: the scan of start's own leaf offers it)
+      k8.init();
+      BestK<8> b8;
+      brute(xyz, qx, qy, qz, b8);
+      ++g_knn_tries;
+      if (adj_knn_search(ix.bv, ix.av, start, qx, qy, qz, k8)) {
+        ++g_knn_cov;
+        bool ok = true;
+        for (int j = 0; j < 8; ++j) ok &= k8.d[j] == b8.d[j] && (b8.pos[j] < 0 || k8.id[j] == b8.id[j]);
+        check(ok, "adj knn", m, q);
+        const float4 c = make_float4(qx, qy, qz, k8.d[7] < FLT_MAX ? k8.d[7] : -1.0f);
+        for (int t = 0; t < 8; ++t) {
+          const float sc = 1e-4f * powf(3.0f, (float)t);
+          const float nx = qx + sc * U(rng), ny = qy + sc * U(rng), nz = qz + sc * U(rng);
+          float dbest = FLT_MAX;
+          int ibest = 0x7fffffff;
+          for (int j = 0; j < 8; ++j) {
+            if (k8.pos[j] < 0) continue;
+            const float4 pj = ix.pts[k8.pos[j]];
+            const float dj = d2_ref(nx, ny, nz, pj.x, pj.y, pj.z);
+            if (lex_less(dj, f2i(pj.w), dbest, ibest)) {
+              dbest = dj;
+              ibest = f2i(pj.w);
+            }
+          }
+          ++g_list_tries;
+          if (list_cert_holds(c, dbest, nx, ny, nz)) {
+            ++g_list_holds;
+            BestK<1> bb;
+            brute(xyz, nx, ny, nz, bb);
+            check(bb.id[0] == ibest && bb.d[0] == dbest, "list cert", m, q);
+          }
+        }
+      }
+    }
     // k = 4, bottom-up from a random leaf
     if (m > 0) {
       BestK<4> k4;
@@ -298,7 +337,8 @@ int main(int argc, char** argv) {
   for (int m : sizes)
     for (int mode = 0; mode < 4; ++mode) run_case(rng, m, m >= 4099 ? 300 : 120, mode);
   printf("bvh_selftest: %ld checks, %d failures (adjacency covered %ld / level 2 %ld / level 3 "
-         "%ld of %ld warm queries; wide %ld)\n", g_checks, g_fail, g_covered, g_covered2,
-         g_covered3, g_adj_tries, g_wide);
+         "%ld of %ld warm queries; wide %ld; 8-NN covered %ld of %ld; list certificates held %ld "
+         "of %ld moves)\n", g_checks, g_fail, g_covered, g_covered2, g_covered3, g_adj_tries,
+         g_wide, g_knn_cov, g_knn_tries, g_list_holds, g_list_tries);
   return g_fail == 0 ? 0 : 1;
 }

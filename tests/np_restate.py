@@ -170,3 +170,32 @@ def align_icp(src, dst, max_iter=128, T=None, trace=False):
             tr["dmean"].append(dmean)
     mc = float(np.sqrt(f32(cost) / f32(n)))
     return mc < 10000, xfm, mc, (tr if trace else None)
+
+
+# ---- preprocessing (point_cloud_utils.cpp:34-68, 163-174) -------------------
+def remove_nans(cloud: np.ndarray) -> np.ndarray:
+    """RemoveNans: rows whose three coordinates are finite, order kept."""
+    a = np.asarray(cloud, f32)
+    return a[np.isfinite(a).all(axis=1)]
+
+
+def voxel_keys(cloud: np.ndarray, voxel_size: float) -> np.ndarray:
+    """(point / voxel_size).floor().cast<int>() per axis (float32 division);
+    NaN / out-of-int-range -> INT_MIN, x86-64's cvttss2si result."""
+    a = np.asarray(cloud, f32)
+    with np.errstate(invalid="ignore", divide="ignore", over="ignore"):
+        q = np.floor(a / f32(voxel_size))
+        ok = (q >= f32(-2147483648.0)) & (q < f32(2147483648.0))
+        return np.where(ok, q, 0).astype(np.int64).astype(np.int32) * ok + \
+            np.int32(np.iinfo(np.int32).min) * ~ok
+
+
+def downsample_voxel(cloud: np.ndarray, voxel_size: float) -> np.ndarray:
+    """DownsampleVoxel: the first point of each voxel, in ascending index
+    (np.unique's return_index is the first occurrence)."""
+    a = np.asarray(cloud, f32)
+    if len(a) == 0:
+        return a.reshape(0, 3)
+    k = voxel_keys(a, voxel_size).astype(np.int32)
+    _, first = np.unique(k, axis=0, return_index=True)
+    return a[np.sort(first)]

@@ -199,3 +199,30 @@ def test_solve_kabsch_oracle_too_few_points():
     ok, T = O.solve_kabsch(np.zeros((2, 3), np.float32), np.zeros((10, 3), np.float32),
                            [[0, 0], [1, 1]], T=T0)
     assert not ok and np.array_equal(T, T0)
+
+
+# ---- f1: RemoveNans / DownsampleVoxel oracle vs the numpy restatement -------
+import preproc_cases as PC  # noqa: E402
+
+
+@pytest.mark.parametrize("name", sorted(PC.cases()))
+def test_remove_nans_oracle_matches_numpy(name):
+    cloud, _ = PC.cases()[name]
+    np.testing.assert_array_equal(O.remove_nans(cloud), NPR.remove_nans(cloud))
+
+
+@pytest.mark.parametrize("name", sorted(PC.cases()))
+def test_downsample_voxel_oracle_matches_numpy(name):
+    cloud, v = PC.cases()[name]
+    got = O.downsample_voxel(cloud, v)
+    np.testing.assert_array_equal(got, NPR.downsample_voxel(cloud, v))
+    # one point per occupied voxel, each the first of its voxel
+    k = NPR.voxel_keys(cloud, v)
+    assert len(got) == (len(np.unique(k, axis=0)) if len(cloud) else 0)
+
+
+def test_downsample_voxel_oracle_on_frame():
+    cloud = PC.frame_cloud()
+    got = O.downsample_voxel(cloud, PC.VOXEL)
+    np.testing.assert_array_equal(got, NPR.downsample_voxel(cloud, PC.VOXEL))
+    assert 0 < len(got) < len(cloud)
