@@ -6,9 +6,19 @@ One step = one incoming frame of the stream, fully on the GPU:
     (the frame's index, reused as the next pair's target)
     -> AlignIcp3d(curr, prev) with the reference's P2POINT_REF loop,
        128 fixed iterations (rs_replay_app.cpp:246-251).
-value = ICP iterations/s over all ranks (steps * 128 / time).  A second timed
-loop runs the build's point-to-plane mode on the same frames (reported as
-extra fields).  Multi-GPU: one process per GPU, each rank tracks its own
+value = ICP iterations/s over all ranks (steps * 128 / time).  Frame
+preparation runs on its own HIP stream and --inflight frame pairs (default 2)
+are aligned concurrently, each on its own context/stream: one pair's
+iteration chain is launch/latency-bound, so independent pairs overlap on the
+GPU.  A second timed loop runs the build's point-to-plane mode on the same
+frames (reported as extra fields).
+
+roofline: the dominant kernel k_icp_nn (transform + exact NN + weighted
+partial sums of one ICP iteration), algorithmic bytes per launch
+12 n + 12 m + S_idx, over its average duration from HIP
+events on the aligning stream (every 8th iteration), vs 8 TB/s.  traffic =
+HBM bytes per launch from the committed PMC pass (profiles/pmc_*.json:
+FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE).  Multi-GPU: one process per GPU, each rank tracks its own
 stream (frame pairs are independent; no data-path collective) -> weak
 scaling; barrier + max-over-ranks timing.
 
@@ -86,7 +96,7 @@ def load_traffic():
         return None
     try:
         d = json.loads(files[-1].read_text())
-        return d.get("k_p2point_bytes_per_launch")
+        return d.get("k_icp_nn_bytes_per_launch")
     except Exception:
         return None
 
@@ -104,7 +114,7 @@ def main():
     ap.add_argument("--no-p2plane", action="store_true")
     ap.add_argument("--cpu-iters", type=int, default=24)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--inflight", type=int, default=3,
+    ap.add_argument("--inflight", type=int, default=2,
                     help="frame pairs in flight per GPU (one HIP stream each)")
     a = ap.parse_args()
 

@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 #include "rst_device.hpp"
@@ -239,8 +240,10 @@ struct P2PlaneAcc {
 
 // ---- kernel 1: adjacency search, one point per thread ----------------------------------
 // Exclusive prefix of the per-block queue counts (one block, kBS threads):
-// pref[b] = entries before block b's segment, pref[nb] = E.
-__device__ void queue_prefix(const int32_t* __restrict__ qcnt, int nb, int32_t* __restrict__ pref,
+// pref[b] = entries before block b's segment, pref[nb] = E.  pref may be
+// LDS (every fallback block scans the counts itself); st, when given,
+// receives E (fb_e) and the queue trace.
+__device__ void queue_prefix(const int32_t* __restrict__ qcnt, int nb, int32_t* pref,
                              IcpState* __restrict__ st) {
   __shared__ int part[kBS + 1];
   const int per = (nb + kBS - 1) / kBS;
@@ -280,8 +283,10 @@ __device__ void queue_prefix(const int32_t* __restrict__ qcnt, int nb, int32_t* 
   if (threadIdx.x == 0) {
     const int E = part[kBS];
     pref[nb] = E;
-    st->fb_e = E;
-    if (st->iter < kQTrace) st->qlen[st->iter] = E;
+    if (st) {
+      st->fb_e = E;
+      if (st->iter < kQTrace) st->qlen[st->iter] = E;
+    }
   }
 }
 
@@ -339,15 +344,6 @@ __global__ __launch_bounds__(kBS) void k_icp_nn(BvhView bv, AdjView av, AccArgs 
     Acc::add(v, bv, aa, u, s, px, py, pz, r.d, r.pos, bv.pts[r.pos >= 0 ? r.pos : 0]);
   }
   block_sum_to_slab<Acc::NV, kBS>(v, lds, slab + (int64_t)blockIdx.x * Acc::RS);
-}
-
-// One block: the exclusive prefix of kernel 1's per-block queue counts and
-// the queue length E (st->fb_e) for kernel 2.
-__global__ __launch_bounds__(kBS) void k_queue_prefix(const int32_t* __restrict__ qcnt, int nb,
-                                                      int32_t* __restrict__ pref,
-                                                      IcpState* __restrict__ st) {
-  if (st->done) return;
-  queue_prefix(qcnt, nb, pref, st);
 }
 
 // Kabsch solve (align_icp.cpp:139-151; SolveKabsch :58-69): fp64 SVD,
@@ -585,8 +581,6 @@ __global__ __launch_bounds__(kRedBS) void k_reduce_solve(const double* __restric
   __shared__ double tot[RS];
   if (Acc::kCanFinish && st->done) return;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  IcpCore core;
-  if (threadIdx.x == 0 && !totals) core = *static_cast<const IcpCore*>(st);  // loads in flight
   const int E = st->fb_e;
   const int rows2 = max(1, min(rows2max, (E + kBS / kWave - 1) / (kBS / kWave)));
   const int t = threadIdx.x, col = t % RS;
@@ -608,6 +602,9 @@ __global__ __launch_bounds__(kRedBS) void k_reduce_solve(const double* __restric
   if (totals) {
     if (t < Acc::NV) totals[t] = tot[t];
   } else if (t == 0) {
+    // (loaded here, not before the reduction: held across it, the state
+    // would be spilled to scratch and reloaded anyway)
+    IcpCore core = *static_cast<const IcpCore*>(st);
     const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
     const int it = core.iter;
     acc_update<Acc>(tot, prm, &core);
@@ -647,21 +644,24 @@ __global__ __launch_bounds__(kBS) void k_icp_fb(BvhView bv, AdjView av, AccArgs 
                                                 IcpState* __restrict__ st,
                                                 int32_t* __restrict__ nnpos,
                                                 const int32_t* __restrict__ qbuf,
-                                                const int32_t* __restrict__ gpref, int nb1,
+                                                const int32_t* __restrict__ qcnt, int nb1,
                                                 double* __restrict__ slab2) {
   extern __shared__ int pref[];  // [nb1 + 1]
   __shared__ double lds[(kBS / kWave) * Acc::NV];
   __shared__ WnnScratch wsc[kBS / kWave];
   if (Acc::kCanFinish && st->done) return;  // converged: nothing reads the slabs
-  const int E = st->fb_e;
+  // every block scans kernel 1's per-block queue counts into LDS (a few KB
+  // of L2 reads; cheaper than a separate prefix launch); block 0 publishes
+  // the queue length for the reduction
+  queue_prefix(qcnt, nb1, pref, blockIdx.x == 0 ? st : nullptr);
+  __syncthreads();
+  const int E = pref[nb1];
   const int nw = max(1, min((int)gridDim.x, (E + kBS / kWave - 1) / (kBS / kWave)));
   if ((int)blockIdx.x >= nw) return;
   double v[Acc::NV];
 #pragma unroll
   for (int k = 0; k < Acc::NV; ++k) v[k] = 0.0;
   if (E > 0) {
-    for (int b = threadIdx.x; b <= nb1; b += kBS) pref[b] = gpref[b];
-    __syncthreads();
     const Uni u = load_uni(st);
     const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
     const int W = gridDim.x * (kBS / kWave);
@@ -833,9 +833,8 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
   }
   // per source point: sorted target position of its last neighbour (warm
   // start of the next iteration's exact search; -1 = cold); the fallback
-  // queue (one kBS segment per kernel-1 block), its per-block counts and
-  // their prefix
-  int32_t *nnpos = nullptr, *qbuf = nullptr, *qcnt = nullptr, *pref = nullptr;
+  // queue (one kBS segment per kernel-1 block) and its per-block counts
+  int32_t *nnpos = nullptr, *qbuf = nullptr, *qcnt = nullptr;
   {
     const size_t np = (size_t)std::max<int64_t>(n_local, 1);
     const size_t nq = (size_t)nblk * kBS;
@@ -844,7 +843,6 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
     nnpos = (int32_t*)w;
     qbuf = nnpos + np;
     qcnt = qbuf + nq;
-    pref = qcnt + nblk;
     RST_HIP(hipMemsetAsync(nnpos, 0xff, sizeof(int32_t) * np, st));
   }
   AccArgs aa;
@@ -885,18 +883,16 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
         k_icp_nn<P2PlaneAcc><<<nblk, kBS, 0, st>>>(bv, av, aa, src->pts, n_local, ctx->d_state,
                                                    nnpos, qbuf, qcnt, slab);
         if (tm) RST_HIP(hipEventRecord(ctx->ev[2 * it + 1], st));
-        k_queue_prefix<<<1, kBS, 0, st>>>(qcnt, nblk, pref, ctx->d_state);
         k_icp_fb<P2PlaneAcc><<<kFbBlocks, kBS, fb_lds, st>>>(bv, av, aa, src->pts, ctx->d_state,
-                                                             nnpos, qbuf, pref, nblk, slab2);
+                                                             nnpos, qbuf, qcnt, nblk, slab2);
         k_reduce_solve<P2PlaneAcc><<<1, kRedBS, 0, st>>>(slab, nblk, slab2, kFbBlocks, prm,
                                                          ctx->d_state, red_out);
       } else {
         k_icp_nn<P2PointAcc><<<nblk, kBS, 0, st>>>(bv, av, aa, src->pts, n_local, ctx->d_state,
                                                    nnpos, qbuf, qcnt, slab);
         if (tm) RST_HIP(hipEventRecord(ctx->ev[2 * it + 1], st));
-        k_queue_prefix<<<1, kBS, 0, st>>>(qcnt, nblk, pref, ctx->d_state);
         k_icp_fb<P2PointAcc><<<kFbBlocks, kBS, fb_lds, st>>>(bv, av, aa, src->pts, ctx->d_state,
-                                                             nnpos, qbuf, pref, nblk, slab2);
+                                                             nnpos, qbuf, qcnt, nblk, slab2);
         k_reduce_solve<P2PointAcc><<<1, kRedBS, 0, st>>>(slab, nblk, slab2, kFbBlocks, prm,
                                                          ctx->d_state, red_out);
       }
