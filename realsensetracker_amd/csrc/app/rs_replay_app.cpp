@@ -3,14 +3,17 @@
 // MI355X align module, with the synthetic frame source in place of the
 // recorded .pb sequence (driver decoupled from the camera):
 //
-//   for each frame: depth -> cloud (rst_unproject; RemoveNans = drop invalid)
-//     xfm = Identity; ok = AlignIcp3d(curr, prev, 128, &xfm)      (:235,251)
-//     if ok: total_xfm = total_xfm * xfm; prev = curr              (:266-270)
+//   for each frame: depth -> cloud_raw (rst_unproject, invalid pixels dropped)
+//     RemoveNans(cloud_raw, &cloud)                                 (:229)
+//     DownsampleVoxel(cloud, v, &curr_down), (prev, v, &prev_down)  (:246-247)
+//     xfm = Identity; ok = AlignIcp3d(curr_down, prev_down, 128, &xfm) (:235,251)
+//     if ok: total_xfm = total_xfm * xfm; prev = cloud               (:266-270)
 //
-// Voxel downsampling (:246-247) is SURVEY.md §8f row f1 and not applied.
 // Prints per-frame timing and drift against the scene's ground truth.
 //
 //   rs_replay_app [--frames N] [--width W] [--height H] [--iters K] [--seed S]
+//                 [--voxel-mm V]  (voxel edge in mm, default 50 as the
+//                                  reference; 0 = align the full clouds)
 //                 [--dump FILE]   (per-frame xfm, one line of 16 col-major floats)
 #include <chrono>
 #include <cmath>
@@ -21,11 +24,12 @@
 #include <vector>
 
 #include "rs_tracker/align/align_icp.hpp"
+#include "rs_tracker/common/point_cloud_utils.hpp"
 
 namespace {
 
 struct Args {
-  int frames = 10, width = 640, height = 480, iters = 128;
+  int frames = 10, width = 640, height = 480, iters = 128, voxel_mm = 50;
   uint64_t seed = 0;
   const char* dump = nullptr;  // write each frame's xfm (16 floats, col-major)
 };
@@ -41,6 +45,7 @@ Args Parse(int argc, char** argv) {
     else if (k == "--iters") a.iters = (int)v;
     else if (k == "--seed") a.seed = (uint64_t)v;
     else if (k == "--dump") a.dump = argv[i + 1];
+    else if (k == "--voxel-mm") a.voxel_mm = (int)v;
     else { std::fprintf(stderr, "unknown flag %s\n", k.c_str()); std::exit(2); }
   }
   return a;
@@ -104,8 +109,12 @@ int main(int argc, char** argv) {
           "render");
     int64_t n = 0;
     Check(rst_unproject(ctx.get(), depth.data(), &K, 0, xyz.data(), &n), "rst_unproject");
-    return rs_tracker::Cloud3f(xyz.data(), n);
+    const rs_tracker::Cloud3f cloud_raw(xyz.data(), n);
+    rs_tracker::Cloud3f cloud;
+    rs_tracker::RemoveNans(cloud_raw, &cloud);  // (:229)
+    return cloud;
   };
+  const float voxel = (float)a.voxel_mm / 1000.0f;  // 50 -> 0.05f exactly as the reference
 
   float T0[16], T0inv[16], Tf[16];
   rs_tracker::Cloud3f prev = grab(0, T0);
@@ -118,7 +127,15 @@ int main(int argc, char** argv) {
     rs_tracker::Cloud3f cloud = grab(f, Tf);
     rs_tracker::Isometry3f xfm = rs_tracker::Isometry3f::Identity();
     const auto t0 = std::chrono::steady_clock::now();
-    const bool suc = rs_tracker::AlignIcp3d(cloud, prev, a.iters, &xfm);
+    bool suc;
+    if (voxel > 0.f) {  // (:245-251)
+      rs_tracker::Cloud3f curr_cloud_down, prev_cloud_down;
+      rs_tracker::DownsampleVoxel(cloud, voxel, &curr_cloud_down);
+      rs_tracker::DownsampleVoxel(prev, voxel, &prev_cloud_down);
+      suc = rs_tracker::AlignIcp3d(curr_cloud_down, prev_cloud_down, a.iters, &xfm);
+    } else {
+      suc = rs_tracker::AlignIcp3d(cloud, prev, a.iters, &xfm);
+    }
     const double ms =
         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     total_ms += ms;
