@@ -61,8 +61,22 @@ def cpu_model() -> str:
 
 
 def render_frames(seed: int, n: int, K, stride: int):
+    """n consecutive frames of the seeded trajectory (the renderer is C++
+    behind ctypes, which drops the GIL: a thread pool renders in parallel)."""
+    from concurrent.futures import ThreadPoolExecutor
     sc = driver.SyntheticScene(seed)
-    return [sc.render(sc.trajectory(i * stride), K, noise_seed=1000 * seed + i) for i in range(n)]
+    with ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
+        return list(ex.map(lambda i: sc.render(sc.trajectory(i * stride), K,
+                                               noise_seed=1000 * seed + i), range(n)))
+
+
+def pingpong(k: int, n: int) -> int:
+    """Frame index k of a stream that runs 0..n-1 and back, so every pair
+    is two consecutive trajectory frames (no artificial wrap-around jump)."""
+    if n < 2:
+        return 0
+    p = k % (2 * n - 2)
+    return p if p < n else 2 * n - 2 - p
 
 
 def cpu_baseline(width: int, height: int, iters: int):
@@ -108,7 +122,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--width", type=int, default=640)
     ap.add_argument("--height", type=int, default=480)
-    ap.add_argument("--frames", type=int, default=8, help="distinct frames cycled per rank")
+    ap.add_argument("--frames", type=int, default=0,
+                    help="distinct frames per rank (0: one per step, at most 512)")
     ap.add_argument("--stride", type=int, default=1, help="trajectory frames between frames")
     ap.add_argument("--iters", type=int, default=128)
     ap.add_argument("--no-p2plane", action="store_true")
@@ -147,7 +162,7 @@ def main():
         return float(t.item())
 
     K = driver.intrinsics(a.width, a.height)
-    nfr = max(2, a.frames)
+    nfr = max(2, a.frames if a.frames > 0 else min(512, max(a.steps, a.warmup) + 1))
     frames = render_frames(seed=rank, n=nfr, K=K, stride=a.stride)
     # depth frames resident in HBM before timing (hipMalloc'd via ctypes)
     hip = C.CDLL("libamdhip64.so")
@@ -187,7 +202,7 @@ def main():
         prev = A.Target.from_depth_device(d_depth[0].value, K, normals_k, pctx)
         k = 1
         for s in range(nsteps):
-            cur = A.Target.from_depth_device(d_depth[k % nfr].value, K, normals_k, pctx)
+            cur = A.Target.from_depth_device(d_depth[pingpong(k, nfr)].value, K, normals_k, pctx)
             if len(pending) == len(actx):
                 finish_one()
             c = actx[s % len(actx)]
