@@ -6,9 +6,10 @@
 //       adj_search; cold lanes start from a Morton-code seed), robust
 //       weight, fp64 partial sums -> one slab row per block.  Lanes the
 //       adjacency cannot certify are queued (per-block segment, in order);
-//   k_icp_fb<Acc>  one wavefront per queued query: the cooperative exact
-//       search of rst_wave_nn.hpp, partial sums -> one slab row per block;
-//   k_solve_*      one block: fixed-order reduction of both slabs (bitwise
+//   k_icp_fb<Acc>  every block scans the per-block queue counts into LDS,
+//       then one wavefront per queued query: the cooperative exact search
+//       of rst_wave_nn.hpp, partial sums -> one slab row per block;
+//   k_reduce_solve<Acc>  one block: fixed-order reduction of both slabs (bitwise
 //       reproducible), then thread 0 solves the 3x3 Kabsch (P2POINT_REF)
 //       or 6x6 normal equations (P2PLANE) into the device-resident IcpState.
 // Multi-GPU: both slabs are first reduced to one row, all-reduced over
@@ -631,13 +632,12 @@ __global__ void k_solve_only(const double* __restrict__ totals, IcpParams prm,
 }
 
 // ---- kernel 2: the queued queries, one wavefront each --------------------------------
-// Queue entry e (global order: block segments in block order, prefix from
-// kernel 1's tail) is handled by wave e mod W of this fixed grid; each wave
-// adds its entries in increasing e, so the slab is reproducible.  Only the
-// first nw = max(1, ceil(E / waves-per-block)) blocks have work; the others
-// exit at once.  The last of the nw blocks to finish reduces both slabs in a
-// fixed order and, single-GPU, solves the pose (align_icp.cpp:122-151);
-// multi-GPU it leaves the reduced row in `totals` for the RCCL all-reduce.
+// Queue entry e (global order: kernel 1's block segments in block order;
+// every block rebuilds their prefix in LDS from the per-block counts) is
+// handled by wave e mod W of this fixed grid; each wave adds its entries in
+// increasing e, so the slab is reproducible.  Only the first
+// nw = max(1, ceil(E / waves-per-block)) blocks have work; the others exit
+// after the scan.  Block 0 publishes E for k_reduce_solve.
 template <class Acc>
 __global__ __launch_bounds__(kBS) void k_icp_fb(BvhView bv, AdjView av, AccArgs aa,
                                                 const float4* __restrict__ src,
