@@ -410,7 +410,7 @@ int target_build_device(rst_ctx* ctx, const float* d_xyz, int64_t m, bool with_b
   hipStream_t st = ctx->stream;
   const int64_t mp = std::max<int64_t>(m, 1);
   auto ta = [&](auto** p, size_t bytes) { return target_alloc(t, bytes, (void**)p) >= 0; };
-  if (!ta(&t->pts, sizeof(float4) * mp) || !ta(&t->inv, sizeof(int32_t) * mp) ||
+  if (!ta(&t->pts, sizeof(float4) * (mp + kPtsPad)) || !ta(&t->inv, sizeof(int32_t) * mp) ||
       !ta(&t->pleaf, sizeof(int32_t) * mp) ||
       !ta(&t->codes, sizeof(uint32_t) * mp + sizeof(float) * 8)) {
     rst_target_free(t);

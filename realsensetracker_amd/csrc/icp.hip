@@ -183,6 +183,7 @@ struct AccArgs {
 struct P2PointAcc {
   static constexpr int NV = kNP2Point;  // sum w q u^T (9), sum w u (3), sum q (3), sum d2
   static constexpr int RS = 16;         // slab row stride (doubles; divides kRedBS)
+  static constexpr int kMinWaves = 5;   // k_icp_nn occupancy (waves/SIMD): one round of waves
   static constexpr bool kCanFinish = false;
   // q = the neighbour's coordinates (the caller has them), bp its sorted
   // position; no neighbour (bp < 0) -> dst[0], d2 = FLT_MAX
@@ -210,6 +211,7 @@ struct P2PointAcc {
 struct P2PlaneAcc {
   static constexpr int NV = kNP2Plane;  // A (21), b (6), sum w r^2, count, sum d2
   static constexpr int RS = 32;
+  static constexpr int kMinWaves = 4;
   static constexpr bool kCanFinish = true;
   __device__ static void add(double (&v)[NV], const BvhView& bv, const AccArgs& a, const Uni& u,
                              const float4& s, float px, float py, float pz, float bd, int bp,
@@ -292,7 +294,7 @@ __device__ void queue_prefix(const int32_t* __restrict__ qcnt, int nb, int32_t* 
 }
 
 template <class Acc>
-__global__ __launch_bounds__(kBS) void k_icp_nn(BvhView bv, AdjView av, AccArgs aa,
+__global__ __launch_bounds__(kBS, Acc::kMinWaves) void k_icp_nn(BvhView bv, AdjView av, AccArgs aa,
                                                 const float4* __restrict__ src, int64_t n,
                                                 const IcpState* __restrict__ st,
                                                 int32_t* __restrict__ nnpos,

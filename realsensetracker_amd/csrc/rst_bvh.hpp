@@ -71,6 +71,10 @@ RST_HD float box_d2(float qx, float qy, float qz, const float4& lo, const float4
   return r;
 }
 
+// Sorted point arrays carry kPtsPad float4 of padding past m, so a leaf scan
+// may load a full batch from one base address without clamping indices.
+constexpr int kPtsPad = 16;
+
 struct BvhView {
   const float4* __restrict__ pts;    // [m] sorted points, .w = original index bits
   const float4* __restrict__ nodes;  // [2 * 2nl]

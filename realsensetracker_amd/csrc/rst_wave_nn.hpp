@@ -638,6 +638,43 @@ RST_HD void scan_range_wide(const BvhView& bv, int b, int n, float qx,
   }
 }
 
+// Best1 form (the ICP fast path): the batch loaded from one base address
+// (immediate offsets; kPtsPad covers the overrun), the distance with packed
+// (x, y) arithmetic (the roundings of d2_ref: ((dx*dx + dy*dy) + dz*dz), no
+// contraction), and lex_less as one unsigned 64-bit compare of (d2 bits,
+// id): d2 >= 0 orders like its bits, and NaN / inf keys never beat the
+// FLT_MAX start, as with the float compare.
+typedef float rst_f2 __attribute__((ext_vector_type(2)));
+template <>
+RST_HD void scan_range_wide<Best1>(const BvhView& bv, int b, int n, float qx, float qy, float qz,
+                                   Best1& r) {
+  const rst_f2 qxy = {qx, qy};
+  uint64_t best = ((uint64_t)(uint32_t)f2i(r.d) << 32) | (uint32_t)r.id;
+  int bj = -1;  // offset in the range of the best point so far (uniform candidates)
+  for (int j0 = 0; j0 < n; j0 += 8) {
+    const float4* base = bv.pts + b + j0;
+    float4 p[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) p[j] = base[j];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const rst_f2 pxy = {p[j].x, p[j].y};
+      const rst_f2 dxy = qxy - pxy;
+      const rst_f2 sq = dxy * dxy;
+      const float dz = qz - p[j].z;
+      float d2 = sq.x + sq.y;
+      d2 = d2 + dz * dz;
+      const uint64_t key = ((uint64_t)(uint32_t)f2i(d2) << 32) | (uint32_t)f2i(p[j].w);
+      const bool t = (j0 + j < n) & (key < best);
+      best = t ? key : best;
+      bj = t ? j0 + j : bj;
+    }
+  }
+  r.d = i2f((int)(uint32_t)(best >> 32));
+  r.id = (int)(uint32_t)best;
+  r.pos = bj >= 0 ? b + bj : r.pos;
+}
+
 // When the ball is not covered (the query moved away from its last
 // neighbour, early ICP iterations), the warm candidate is first walked
 // through the adjacency: the listed leaf whose box is nearest to the query

@@ -59,7 +59,7 @@ Index build(const std::vector<float>& xyz) {
   }
   std::stable_sort(kv.begin(), kv.end(),
                    [](const auto& a, const auto& b) { return a.first < b.first; });
-  ix.pts.resize(std::max(m, 1));
+  ix.pts.resize(std::max(m, 1) + kPtsPad);
   ix.codes.resize(std::max(m, 1));
   for (int i = 0; i < m; ++i) {
     const int j = kv[i].second;
