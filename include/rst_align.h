@@ -232,6 +232,34 @@ int rst_downsample_voxel_device(rst_ctx* ctx, const float* d_xyz, int64_t n,
                                 float voxel_size, float* d_out,
                                 int64_t* n_out);
 
+/* ---- GICP, the align module's second path -------- */
+/* ComputeCovariances(tree, cloud, covs, use_gicp) (point_cloud_utils.cpp:
+ * 100-161) on a prepared cloud: per point the 32 nearest others (33-NN,
+ * self first), fp32 centroid and sum of outer products / 31; use_gicp:
+ * U diag(1, 1, 1e-2) U^T.  covs_out: m x 9 floats (3x3 column-major, as
+ * Eigen::Matrix3f), original point order. */
+int rst_compute_covariances(rst_ctx* ctx, const rst_target* tgt, int use_gicp,
+                            float* covs_out);
+/* ComputeAlignment(src, dst, src_covs, dst_covs, dst_indices, seed, &T)
+ * (align_gicp.cpp:41-103): minimises 1/2 sum Huber_0.5(|C_i^-1/2 (R s_i +
+ * t - d_j)|^2), C_i = S_d + R S_s R^T (gicp_cost.hpp:40-73), from seed, by
+ * Levenberg-Marquardt (fp64, at most max_iter cost evaluations; the Ceres
+ * solver it replaces is not reproduced step by step, only its objective).
+ * pose_out col-major 4x4; cost_out = the final cost (Ceres final_cost);
+ * RST_FALSE when the pose is not finite. */
+int rst_gicp_solve(rst_ctx* ctx, const float* src, int64_t n, const float* dst,
+                   int64_t m, const float* src_covs, const float* dst_covs,
+                   const int32_t* dst_idx, const float seed[16], int max_iter,
+                   float pose_out[16], double* cost_out, int32_t* iters_out);
+/* ComputeAlignment(src, dst, &T) (align_gicp.cpp:105-163): covariances of
+ * both clouds (k = 32, use_gicp = false), estimate = Identity (the
+ * reference ignores T's value), outer_iters (reference: 16) x {exact 1-NN
+ * of estimate * src in dst; the solve above seeded at estimate}.
+ * RST_FALSE (cost = inf) when the result is not finite (:145-150). */
+int rst_gicp_align(rst_ctx* ctx, const float* src, int64_t n, const float* dst,
+                   int64_t m, int outer_iters, int max_inner, float pose_out[16],
+                   double* cost_out);
+
 /* ---- synthetic frame source (driver; replaces the camera) --------------- */
 /* Procedural room (walls + random spheres/boxes), seeded. */
 int rst_scene_create(uint64_t seed, rst_scene** out);

@@ -63,6 +63,14 @@ def lib():
         L.orc_remove_nans.restype = C.c_int64
         L.orc_downsample_voxel.argtypes = [_f, C.c_int64, C.c_float, _f]
         L.orc_downsample_voxel.restype = C.c_int64
+        L.orc_compute_covariances.argtypes = [_f, C.c_int64, P, C.c_int, _f]
+        L.orc_gicp_eval.restype = C.c_double
+        L.orc_gicp_eval.argtypes = [_f, C.c_int64, _f, _f, _f, _i, _d, _d, _d, _d]
+        L.orc_gicp_solve.restype = C.c_double
+        L.orc_gicp_solve.argtypes = [_f, C.c_int64, _f, _f, _f, _i, _f, C.c_int, _f,
+                                     C.POINTER(C.c_int)]
+        L.orc_gicp_align.restype = C.c_double
+        L.orc_gicp_align.argtypes = [_f, C.c_int64, _f, C.c_int64, C.c_int, C.c_int, _f]
         L.orc_unproject.argtypes = [_u16, C.c_int, C.c_int, _f, C.c_float, C.c_int, _f]
         L.orc_align_p2plane.restype = C.c_int
         L.orc_align_p2plane.argtypes = [_f, C.c_int64, _f, _f, C.c_int64, P, C.c_int,
@@ -238,6 +246,57 @@ def downsample_voxel(cloud, voxel_size):
     out = np.zeros_like(a)
     n = lib().orc_downsample_voxel(_fp(a), a.shape[0], float(voxel_size), _fp(out))
     return out[:n].copy()
+
+
+def compute_covariances(cloud, use_gicp=False, tree: KDTree | None = None):
+    """ComputeCovariances (point_cloud_utils.cpp:100-161): (n, 3, 3) float32."""
+    a = _cloud(cloud)
+    t = tree or KDTree(a, 16)
+    out = np.zeros((a.shape[0], 9), np.float32)
+    lib().orc_compute_covariances(_fp(a), a.shape[0], t.h, int(use_gicp), _fp(out))
+    return out.reshape(-1, 3, 3).transpose(0, 2, 1).copy()  # col-major -> (r, c)
+
+
+def _covs_cm(covs):
+    c = np.ascontiguousarray(np.asarray(covs, np.float32).transpose(0, 2, 1))
+    return c.reshape(-1, 9)
+
+
+def gicp_eval(src, dst, src_covs, dst_covs, idx, R, t):
+    """(F, H (6x6), g (6)) of the GICP cost at (R, t) (fp64)."""
+    s, d = _cloud(src), _cloud(dst)
+    cs, cd = _covs_cm(src_covs), _covs_cm(dst_covs)
+    ii = np.ascontiguousarray(idx, np.int32)
+    Rr = np.ascontiguousarray(R, np.float64).reshape(9)
+    tt = np.ascontiguousarray(t, np.float64).reshape(3)
+    H = np.zeros(36)
+    g = np.zeros(6)
+    F = lib().orc_gicp_eval(_fp(s), s.shape[0], _fp(d), _fp(cs), _fp(cd), ii.ctypes.data_as(_i),
+                            Rr.ctypes.data_as(_d), tt.ctypes.data_as(_d), H.ctypes.data_as(_d),
+                            g.ctypes.data_as(_d))
+    return F, H.reshape(6, 6), g
+
+
+def gicp_solve(src, dst, src_covs, dst_covs, idx, seed=None, max_iter=64):
+    """Inner ComputeAlignment (align_gicp.cpp:41-103): (cost, pose, evaluations)."""
+    s, d = _cloud(src), _cloud(dst)
+    cs, cd = _covs_cm(src_covs), _covs_cm(dst_covs)
+    ii = np.ascontiguousarray(idx, np.int32)
+    sd = _cm(np.eye(4) if seed is None else seed)
+    out = np.zeros(16, np.float32)
+    its = C.c_int(0)
+    F = lib().orc_gicp_solve(_fp(s), s.shape[0], _fp(d), _fp(cs), _fp(cd), ii.ctypes.data_as(_i),
+                             _fp(sd), max_iter, _fp(out), C.byref(its))
+    return F, _uncm(out), its.value
+
+
+def gicp_align(src, dst, outer_iters=16, max_inner=64):
+    """ComputeAlignment(src, dst, &T) (align_gicp.cpp:105-163): (cost, pose)."""
+    s, d = _cloud(src), _cloud(dst)
+    out = np.zeros(16, np.float32)
+    F = lib().orc_gicp_align(_fp(s), s.shape[0], _fp(d), d.shape[0], outer_iters, max_inner,
+                             _fp(out))
+    return F, _uncm(out)
 
 
 def align_p2plane(src, dst, dst_normals, max_iter=30, eps=1e-6, mu=4e-4, max_dist=0.0, T=None,

@@ -1141,3 +1141,363 @@ int64_t orc_downsample_voxel(const float* xyz, int64_t n, float voxel_size, floa
   free(used);
   return m;
 }
+
+/* ==== f2: GICP (point_cloud_utils.cpp:100-161, align_gicp.cpp:41-163) ===== */
+
+/* ComputeCovariances: 33-NN (self included, first result dropped), fp32
+ * centroid of the 32 neighbours in result order, fp32 sum of outer
+ * products, / 31 (:117-159); use_gicp: cov <- U diag(1, 1, 1e-2) U^T with U
+ * the singular vectors of cov (:139-155), here I - (1 - 1e-2) u3 u3^T in
+ * fp64 (u3 = the smallest singular vector; independent of U's signs). */
+void orc_compute_covariances(const float* xyz, int64_t n, const orc_kdtree* tree,
+                             int use_gicp, float* covs) {
+  int32_t idx[33];
+  float d2[33];
+  for (int64_t i = 0; i < n; ++i) {
+    orc_kdtree_knn(tree, xyz + 3 * i, 33, idx, d2);
+    float c[3] = {0.f, 0.f, 0.f};
+    for (int j = 1; j < 33; ++j)
+      for (int r = 0; r < 3; ++r) c[r] += xyz[3 * (int64_t)idx[j] + r];
+    for (int r = 0; r < 3; ++r) c[r] /= 32.0f;
+    float cov[9] = {0};
+    for (int j = 1; j < 33; ++j) {
+      float dl[3];
+      for (int r = 0; r < 3; ++r) dl[r] = xyz[3 * (int64_t)idx[j] + r] - c[r];
+      for (int cc = 0; cc < 3; ++cc)
+        for (int r = 0; r < 3; ++r) cov[cc * 3 + r] += dl[r] * dl[cc];
+    }
+    float* o = covs + 9 * i;
+    if (use_gicp) {
+      double a[9], u[9], s[3], v[9];
+      for (int k = 0; k < 9; ++k) a[k] = cov[k];
+      orc_jacobi_svd3(a, u, s, v);
+      const double* u3 = u + 6; /* column 2: smallest singular value */
+      for (int cc = 0; cc < 3; ++cc)
+        for (int r = 0; r < 3; ++r)
+          o[cc * 3 + r] = (float)((r == cc ? 1.0 : 0.0) - (1.0 - 1e-2) * u3[r] * u3[cc]);
+    } else {
+      for (int k = 0; k < 9; ++k) o[k] = cov[k] / 31.0f;
+    }
+  }
+}
+
+/* symmetric 3x3 eigen-decomposition, cyclic Jacobi (fp64); a row-major
+ * scalars, V columns = eigenvectors */
+static void gicp_sym_eig3(const double A[9], double lam[3], double V[9]) {
+  double a[3][3];
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < 3; ++c) a[r][c] = A[3 * r + c];
+  double v[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
+  static const int P[3] = {0, 0, 1}, Q[3] = {1, 2, 2};
+  for (int sweep = 0; sweep < 12; ++sweep) {
+    const double off = a[0][1] * a[0][1] + a[0][2] * a[0][2] + a[1][2] * a[1][2];
+    const double dg = a[0][0] * a[0][0] + a[1][1] * a[1][1] + a[2][2] * a[2][2];
+    if (!(off > 1e-32 * dg)) break;
+    for (int k = 0; k < 3; ++k) {
+      const int p = P[k], q = Q[k];
+      const double apq = a[p][q];
+      if (apq == 0.0) continue;
+      const double th = (a[q][q] - a[p][p]) / (2.0 * apq);
+      const double t = (th >= 0 ? 1.0 : -1.0) / (fabs(th) + sqrt(th * th + 1.0));
+      const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+      for (int r = 0; r < 3; ++r) { /* A <- A J (columns p, q) */
+        const double arp = a[r][p], arq = a[r][q];
+        a[r][p] = c * arp - s * arq;
+        a[r][q] = s * arp + c * arq;
+      }
+      for (int r = 0; r < 3; ++r) { /* A <- J^T A (rows p, q) */
+        const double apr = a[p][r], aqr = a[q][r];
+        a[p][r] = c * apr - s * aqr;
+        a[q][r] = s * apr + c * aqr;
+      }
+      for (int r = 0; r < 3; ++r) {
+        const double vrp = v[r][p], vrq = v[r][q];
+        v[r][p] = c * vrp - s * vrq;
+        v[r][q] = s * vrp + c * vrq;
+      }
+    }
+  }
+  for (int k = 0; k < 3; ++k) lam[k] = a[k][k];
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < 3; ++c) V[3 * r + c] = v[r][c];
+}
+
+/* One GICP evaluation at (R, t): F = 1/2 sum rho(|r_i|^2) with Huber(0.5)
+ * (align_gicp.cpp:70), r_i = C_i^{-1/2} (R s_i + t - d_i),
+ * C_i = S_d + R S_s R^T (gicp_cost.hpp:50-69), and the Gauss-Newton
+ * quantities of Ceres' robust corrector for a loss with rho'' <= 0
+ * (J~ = sqrt(rho') J): H = sum rho' J^T J, g = sum rho' J^T r, J the exact
+ * Jacobian w.r.t. (w, t), R(w) = exp([w]x) R, including the dependence of
+ * C_i^{-1/2} on R (derivative of the inverse square root through the
+ * eigen-decomposition).  H row-major 6x6. */
+double orc_gicp_eval(const float* src, int64_t n, const float* dst, const float* src_covs,
+                     const float* dst_covs, const int32_t* dst_idx, const double R[9],
+                     const double t[3], double H[36], double g[6]) {
+  double F = 0.0;
+  if (H) memset(H, 0, sizeof(double) * 36);
+  if (g) memset(g, 0, sizeof(double) * 6);
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t j = dst_idx[i];
+    const float* Ss = src_covs + 9 * i; /* col-major (Eigen) = symmetric anyway */
+    const float* Sd = dst_covs + 9 * j;
+    double A[9], C[9], RS[9];
+    for (int r = 0; r < 3; ++r)
+      for (int c = 0; c < 3; ++c) {
+        double s = 0;
+        for (int k = 0; k < 3; ++k) s += R[3 * r + k] * (double)Ss[3 * c + k];
+        RS[3 * r + c] = s;
+      }
+    for (int r = 0; r < 3; ++r)
+      for (int c = 0; c < 3; ++c) {
+        double s = 0;
+        for (int k = 0; k < 3; ++k) s += RS[3 * r + k] * R[3 * c + k];
+        A[3 * r + c] = s;
+      }
+    for (int r = 0; r < 3; ++r)
+      for (int c = 0; c < 3; ++c) C[3 * r + c] = (double)Sd[3 * c + r] + A[3 * r + c];
+    /* symmetrise (rounding) */
+    for (int r = 0; r < 3; ++r)
+      for (int c = r + 1; c < 3; ++c) {
+        const double m = 0.5 * (C[3 * r + c] + C[3 * c + r]);
+        C[3 * r + c] = C[3 * c + r] = m;
+      }
+    double lam[3], V[9];
+    gicp_sym_eig3(C, lam, V);
+    double is[3];
+    for (int k = 0; k < 3; ++k) is[k] = 1.0 / sqrt(lam[k] > 1e-30 ? lam[k] : 1e-30);
+    double M[9];
+    for (int r = 0; r < 3; ++r)
+      for (int c = 0; c < 3; ++c) {
+        double s = 0;
+        for (int k = 0; k < 3; ++k) s += V[3 * r + k] * is[k] * V[3 * c + k];
+        M[3 * r + c] = s;
+      }
+    double Rs[3], dl[3];
+    for (int r = 0; r < 3; ++r) {
+      Rs[r] = R[3 * r] * src[3 * i] + R[3 * r + 1] * src[3 * i + 1] + R[3 * r + 2] * src[3 * i + 2];
+      dl[r] = Rs[r] + t[r] - (double)dst[3 * j + r];
+    }
+    double res[3];
+    for (int r = 0; r < 3; ++r) res[r] = M[3 * r] * dl[0] + M[3 * r + 1] * dl[1] + M[3 * r + 2] * dl[2];
+    const double s2 = res[0] * res[0] + res[1] * res[1] + res[2] * res[2];
+    const double rho = s2 <= 0.25 ? s2 : sqrt(s2) - 0.25;
+    const double rho1 = s2 <= 0.25 ? 1.0 : 0.5 / sqrt(s2);
+    F += 0.5 * rho;
+    if (!H) continue;
+    /* Daleckii-Krein weights of X -> X^{-1/2} */
+    double W[9];
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b) {
+        const double la = lam[a] > 1e-30 ? lam[a] : 1e-30, lb = lam[b] > 1e-30 ? lam[b] : 1e-30;
+        W[3 * a + b] = fabs(la - lb) > 1e-12 * (la + lb) ? (is[a] - is[b]) / (la - lb)
+                                                         : -0.5 * is[a] / la;
+      }
+    double J[3][6];
+    for (int k = 0; k < 3; ++k) {
+      /* E = G_k A - A G_k, G_k = [e_k]x */
+      double G[9] = {0};
+      if (k == 0) { G[5] = -1; G[7] = 1; }
+      if (k == 1) { G[2] = 1; G[6] = -1; }
+      if (k == 2) { G[1] = -1; G[3] = 1; }
+      double E[9];
+      for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) {
+          double s = 0;
+          for (int q = 0; q < 3; ++q) s += G[3 * r + q] * A[3 * q + c] - A[3 * r + q] * G[3 * q + c];
+          E[3 * r + c] = s;
+        }
+      double B[9], T[9], dM[9];
+      for (int a = 0; a < 3; ++a) /* B = V^T E V */
+        for (int b = 0; b < 3; ++b) {
+          double s = 0;
+          for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) s += V[3 * r + a] * E[3 * r + c] * V[3 * c + b];
+          B[3 * a + b] = s * W[3 * a + b];
+        }
+      for (int r = 0; r < 3; ++r) /* dM = V B V^T */
+        for (int b = 0; b < 3; ++b) {
+          double s = 0;
+          for (int a = 0; a < 3; ++a) s += V[3 * r + a] * B[3 * a + b];
+          T[3 * r + b] = s;
+        }
+      for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) {
+          double s = 0;
+          for (int b = 0; b < 3; ++b) s += T[3 * r + b] * V[3 * c + b];
+          dM[3 * r + c] = s;
+        }
+      /* d(delta)/dw_k = e_k x (R s) */
+      double ex[3] = {0, 0, 0};
+      if (k == 0) { ex[1] = -Rs[2]; ex[2] = Rs[1]; }
+      if (k == 1) { ex[0] = Rs[2]; ex[2] = -Rs[0]; }
+      if (k == 2) { ex[0] = -Rs[1]; ex[1] = Rs[0]; }
+      for (int r = 0; r < 3; ++r)
+        J[r][k] = dM[3 * r] * dl[0] + dM[3 * r + 1] * dl[1] + dM[3 * r + 2] * dl[2] +
+                  M[3 * r] * ex[0] + M[3 * r + 1] * ex[1] + M[3 * r + 2] * ex[2];
+    }
+    for (int r = 0; r < 3; ++r)
+      for (int c = 0; c < 3; ++c) J[r][3 + c] = M[3 * r + c];
+    for (int a = 0; a < 6; ++a) {
+      double ga = 0;
+      for (int r = 0; r < 3; ++r) ga += J[r][a] * res[r];
+      g[a] += rho1 * ga;
+      for (int b = 0; b < 6; ++b) {
+        double h = 0;
+        for (int r = 0; r < 3; ++r) h += J[r][a] * J[r][b];
+        H[6 * a + b] += rho1 * h;
+      }
+    }
+  }
+  return F;
+}
+
+static void gicp_rodrigues(const double w[3], double E[9]) {
+  const double th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+  const double th = sqrt(th2);
+  double a, b;
+  if (th < 1e-8) {
+    a = 1.0 - th2 / 6.0;
+    b = 0.5 - th2 / 24.0;
+  } else {
+    a = sin(th) / th;
+    b = (1.0 - cos(th)) / th2;
+  }
+  const double K[9] = {0, -w[2], w[1], w[2], 0, -w[0], -w[1], w[0], 0};
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < 3; ++c) {
+      double kk = 0;
+      for (int q = 0; q < 3; ++q) kk += K[3 * r + q] * K[3 * q + c];
+      E[3 * r + c] = (r == c ? 1.0 : 0.0) + a * K[3 * r + c] + b * kk;
+    }
+}
+
+/* (H + lambda diag(H)) x = -g by Cholesky; 0 when not positive definite */
+static int gicp_lm_step(const double H[36], const double g[6], double lambda, double x[6]) {
+  double L[36];
+  for (int a = 0; a < 6; ++a)
+    for (int b = 0; b < 6; ++b) L[6 * a + b] = H[6 * a + b] + (a == b ? lambda * H[6 * a + a] : 0.0);
+  for (int j = 0; j < 6; ++j) {
+    double s = L[6 * j + j];
+    for (int k = 0; k < j; ++k) s -= L[6 * j + k] * L[6 * j + k];
+    if (!(s > 0)) return 0;
+    L[6 * j + j] = sqrt(s);
+    for (int i = j + 1; i < 6; ++i) {
+      double u = L[6 * i + j];
+      for (int k = 0; k < j; ++k) u -= L[6 * i + k] * L[6 * j + k];
+      L[6 * i + j] = u / L[6 * j + j];
+    }
+  }
+  double y[6];
+  for (int i = 0; i < 6; ++i) {
+    double s = -g[i];
+    for (int k = 0; k < i; ++k) s -= L[6 * i + k] * y[k];
+    y[i] = s / L[6 * i + i];
+  }
+  for (int i = 5; i >= 0; --i) {
+    double s = y[i];
+    for (int k = i + 1; k < 6; ++k) s -= L[6 * k + i] * x[k];
+    x[i] = s / L[6 * i + i];
+  }
+  return 1;
+}
+
+/* ComputeAlignment with given covariances and correspondences
+ * (align_gicp.cpp:41-103): Ceres' Levenberg-Marquardt restated as the
+ * build's own LM (DESIGN.md "GICP"): evaluate the candidate; accept when F
+ * drops (lambda /= 3, floor 1e-12) else lambda *= 4; stop when the step norm
+ * < 1e-10, the relative drop < 1e-12, lambda > 1e10, or after max_iter
+ * evaluations.  Returns the final F (Ceres' final_cost); pose_out 4x4
+ * col-major float (R from the fp64 rotation, as q.toRotationMatrix()). */
+double orc_gicp_solve(const float* src, int64_t n, const float* dst, const float* src_covs,
+                      const float* dst_covs, const int32_t* dst_idx, const float seed[16],
+                      int max_iter, float pose_out[16], int* iters_out) {
+  double R[9], t[3];
+  for (int r = 0; r < 3; ++r) {
+    for (int c = 0; c < 3; ++c) R[3 * r + c] = seed[4 * c + r];
+    t[r] = seed[12 + r];
+  }
+  double H[36], g[6];
+  double F = orc_gicp_eval(src, n, dst, src_covs, dst_covs, dst_idx, R, t, H, g);
+  double lambda = 1e-4;
+  int it = 1;
+  while (it < max_iter) {
+    double x[6] = {0, 0, 0, 0, 0, 0};
+    if (!gicp_lm_step(H, g, lambda, x)) {
+      lambda *= 4.0;
+      if (lambda > 1e10) break;
+      continue;
+    }
+    const double nx = sqrt(x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3] + x[4] * x[4] + x[5] * x[5]);
+    if (nx < 1e-10) break;
+    double E[9], R2[9], t2[3];
+    gicp_rodrigues(x, E);
+    for (int r = 0; r < 3; ++r)
+      for (int c = 0; c < 3; ++c) {
+        double s = 0;
+        for (int q = 0; q < 3; ++q) s += E[3 * r + q] * R[3 * q + c];
+        R2[3 * r + c] = s;
+      }
+    for (int r = 0; r < 3; ++r) t2[r] = t[r] + x[3 + r];
+    double H2[36], g2[6];
+    const double F2 = orc_gicp_eval(src, n, dst, src_covs, dst_covs, dst_idx, R2, t2, H2, g2);
+    ++it;
+    if (F2 < F) {
+      const double drop = (F - F2) / (F > 0 ? F : 1.0);
+      memcpy(R, R2, sizeof(R));
+      memcpy(t, t2, sizeof(t));
+      memcpy(H, H2, sizeof(H));
+      memcpy(g, g2, sizeof(g));
+      F = F2;
+      lambda = lambda / 3.0 > 1e-12 ? lambda / 3.0 : 1e-12;
+      if (drop < 1e-12) break;
+    } else {
+      lambda *= 4.0;
+      if (lambda > 1e10) break;
+    }
+  }
+  for (int c = 0; c < 3; ++c) {
+    for (int r = 0; r < 3; ++r) pose_out[4 * c + r] = (float)R[3 * r + c];
+    pose_out[4 * c + 3] = 0.f;
+  }
+  for (int r = 0; r < 3; ++r) pose_out[12 + r] = (float)t[r];
+  pose_out[15] = 1.f;
+  if (iters_out) *iters_out = it;
+  return F;
+}
+
+/* ComputeAlignment(src, dst, &T) (align_gicp.cpp:105-163): covariances of
+ * both clouds (k = 32, use_gicp = false), estimate = Identity (the
+ * reference ignores T's value), 16 x { correspondences = exact 1-NN of
+ * estimate * src in dst; estimate = LM solve seeded at estimate }.  Returns
+ * the last solve's cost; T = estimate. */
+double orc_gicp_align(const float* src, int64_t n, const float* dst, int64_t m,
+                      int outer_iters, int max_inner, float pose_out[16]) {
+  orc_kdtree* ts = orc_kdtree_build(src, n, 16);
+  orc_kdtree* td = orc_kdtree_build(dst, m, 16);
+  float* cs = (float*)malloc(sizeof(float) * 9 * (size_t)n);
+  float* cd = (float*)malloc(sizeof(float) * 9 * (size_t)m);
+  orc_compute_covariances(src, n, ts, 0, cs);
+  orc_compute_covariances(dst, m, td, 0, cd);
+  float est[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+  float* tmp = (float*)malloc(sizeof(float) * 3 * (size_t)n);
+  int32_t* nn = (int32_t*)malloc(sizeof(int32_t) * (size_t)n);
+  double cost = 0.0;
+  for (int o = 0; o < outer_iters; ++o) {
+    orc_transform_points(est, src, n, tmp);
+    for (int64_t i = 0; i < n; ++i) {
+      float d2;
+      orc_kdtree_knn(td, tmp + 3 * i, 1, nn + i, &d2);
+    }
+    float next[16];
+    cost = orc_gicp_solve(src, n, dst, cs, cd, nn, est, max_inner, next, NULL);
+    memcpy(est, next, sizeof(est));
+  }
+  memcpy(pose_out, est, sizeof(est));
+  free(cs);
+  free(cd);
+  free(tmp);
+  free(nn);
+  orc_kdtree_free(ts);
+  orc_kdtree_free(td);
+  return cost;
+}

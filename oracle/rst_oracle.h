@@ -144,6 +144,23 @@ int64_t orc_remove_nans(const float* xyz, int64_t n, float* out);
 int64_t orc_downsample_voxel(const float* xyz, int64_t n, float voxel_size,
                              float* out);
 
+/* ---- f2: GICP (point_cloud_utils.cpp:100-161, align_gicp.cpp:41-163) ---- */
+/* ComputeCovariances: covs n x 9 (3x3 col-major each). */
+void orc_compute_covariances(const float* xyz, int64_t n, const orc_kdtree* tree,
+                             int use_gicp, float* covs);
+/* F, and when H/g are non-NULL the robust Gauss-Newton quantities, at the
+ * pose (R row-major 3x3, t). */
+double orc_gicp_eval(const float* src, int64_t n, const float* dst, const float* src_covs,
+                     const float* dst_covs, const int32_t* dst_idx, const double R[9],
+                     const double t[3], double H[36], double g[6]);
+/* the inner ComputeAlignment (given covariances / correspondences) */
+double orc_gicp_solve(const float* src, int64_t n, const float* dst, const float* src_covs,
+                      const float* dst_covs, const int32_t* dst_idx, const float seed[16],
+                      int max_iter, float pose_out[16], int* iters_out);
+/* the 3-argument ComputeAlignment(src, dst, &T) */
+double orc_gicp_align(const float* src, int64_t n, const float* dst, int64_t m,
+                      int outer_iters, int max_inner, float pose_out[16]);
+
 /* ---- build's own point-to-plane mode (no reference counterpart) --------- */
 /* Gauss-Newton point-to-plane with the same annealed weight schedule;
  * see DESIGN.md "P2PLANE".  Returns iterations run. */

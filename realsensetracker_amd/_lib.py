@@ -86,6 +86,12 @@ PROTOTYPES = {
     "rst_downsample_voxel": (C.c_int, [_P, c_float_p, C.c_int64, C.c_float, c_float_p,
                                        c_int64_p]),
     "rst_downsample_voxel_device": (C.c_int, [_P, _P, C.c_int64, C.c_float, _P, c_int64_p]),
+    "rst_compute_covariances": (C.c_int, [_P, _P, C.c_int, c_float_p]),
+    "rst_gicp_solve": (C.c_int, [_P, c_float_p, C.c_int64, c_float_p, C.c_int64, c_float_p,
+                                 c_float_p, c_int32_p, c_float_p, C.c_int, c_float_p,
+                                 C.POINTER(C.c_double), c_int32_p]),
+    "rst_gicp_align": (C.c_int, [_P, c_float_p, C.c_int64, c_float_p, C.c_int64, C.c_int,
+                                 C.c_int, c_float_p, C.POINTER(C.c_double)]),
     "rst_frame_prepare_device": (C.c_int, [_P, _P, C.POINTER(Intrinsics), C.c_int,
                                            C.POINTER(_P)]),
     "rst_scene_create": (C.c_int, [C.c_uint64, C.POINTER(_P)]),

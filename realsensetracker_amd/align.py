@@ -353,6 +353,58 @@ def DownsampleVoxel(cloud, voxel_size: float, ctx: Context | None = None) -> np.
     return out[:n.value].copy()
 
 
+def ComputeCovariances(tree: Target, cloud=None, use_gicp: bool = False) -> np.ndarray:
+    """point_cloud_utils.cpp:100-161 on `tree`'s cloud (the reference passes
+    the tree and the cloud it indexes; `cloud` is accepted for that shape and
+    must be the same points): (m, 3, 3) float32 per point, original order."""
+    m = len(tree)
+    if cloud is not None and len(L.as_cloud(cloud)) != m:
+        raise ValueError("cloud must be the tree's cloud")
+    out = np.zeros((m, 9), np.float32)
+    L.check(L.lib().rst_compute_covariances(tree.ctx.handle, tree.handle, int(bool(use_gicp)),
+                                            L.fptr(out)), "rst_compute_covariances")
+    return out.reshape(-1, 3, 3).transpose(0, 2, 1).copy()  # col-major -> [r, c]
+
+
+def _covs_cm(covs) -> np.ndarray:
+    c = np.asarray(covs, np.float32).reshape(-1, 3, 3)
+    return np.ascontiguousarray(c.transpose(0, 2, 1)).reshape(-1, 9)
+
+
+def ComputeAlignment(src, dst, *args, max_iter: int = 64, outer_iters: int = 16,
+                     ctx: Context | None = None) -> float:
+    """GICP (align_gicp.cpp): ComputeAlignment(src, dst, T) or
+    ComputeAlignment(src, dst, src_covs, dst_covs, dst_indices, seed, T).
+    T (4x4 float32) receives the result; returns the final cost (inf, T
+    untouched, when the solve produced a non-finite pose)."""
+    ctx = ctx or get_context()
+    s, d = L.as_cloud(src), L.as_cloud(dst)
+    cost = C.c_double(0.0)
+    out = np.zeros(16, np.float32)
+    if len(args) == 1:
+        (T,) = args
+        st = L.check(L.lib().rst_gicp_align(ctx.handle, L.fptr(s), len(s), L.fptr(d), len(d),
+                                            int(outer_iters), int(max_iter), L.fptr(out),
+                                            C.byref(cost)), "rst_gicp_align")
+    elif len(args) == 5:
+        src_covs, dst_covs, idx, seed, T = args
+        cs, cd = _covs_cm(src_covs), _covs_cm(dst_covs)
+        ii = np.ascontiguousarray(idx, np.int32)
+        sd = L.pose_to_cm(seed)
+        its = C.c_int32(0)
+        st = L.check(L.lib().rst_gicp_solve(ctx.handle, L.fptr(s), len(s), L.fptr(d), len(d),
+                                            L.fptr(cs), L.fptr(cd), L.iptr(ii), L.fptr(sd),
+                                            int(max_iter), L.fptr(out), C.byref(cost),
+                                            C.byref(its)), "rst_gicp_solve")
+    else:
+        raise TypeError("ComputeAlignment(src, dst, T) or "
+                        "ComputeAlignment(src, dst, src_covs, dst_covs, dst_indices, seed, T)")
+    if st != L.RST_OK:
+        return float("inf")
+    T[...] = L.cm_to_pose(out)
+    return float(cost.value)
+
+
 def ComputeNormals(cloud, tree: Target, num_neighbors: int = 16,
                    viewpoint=(0.0, 0.0, 0.0)) -> np.ndarray:
     """kNN-PCA normals of `tree`'s cloud, oriented toward `viewpoint`

@@ -206,6 +206,10 @@ int remove_nans_device(rst_ctx* ctx, const float* d_xyz, int64_t n, float* d_out
 int downsample_voxel_device(rst_ctx* ctx, const float* d_xyz, int64_t n, float voxel,
                             float* d_out, int64_t* n_out);
 
+// GICP covariances (gicp.hip): d_covs m x 9, original order, col-major 3x3
+int compute_covariances_device(rst_ctx* ctx, const rst_target* tgt, int use_gicp,
+                               float* d_covs);
+
 // RCCL (comm.hip)
 int comm_allreduce_sum_f64(rst_comm* comm, double* d_buf, size_t count,
                            hipStream_t stream);

@@ -543,3 +543,65 @@ def test_preprocess_contract(ctx):
         assert L.lib().rst_downsample_voxel(ctx.handle, L.fptr(a), 4, bad, L.fptr(out),
                                             C.byref(n)) == L.RST_E_ARG
     assert L.lib().rst_remove_nans(ctx.handle, L.fptr(a), -1, L.fptr(out), C.byref(n)) == L.RST_E_ARG
+
+
+# ---- f2: GICP (point_cloud_utils.cpp:100-161, align_gicp.cpp:41-163) -----------
+def _gicp_pair(name="pair_160x120_s2", voxel=0.1):
+    g = load_golden(name)
+    return O.downsample_voxel(g["src"], voxel), O.downsample_voxel(g["dst"], voxel), g["T_gt"]
+
+
+@pytest.mark.parametrize("use_gicp", [False, True])
+def test_covariances_match_oracle(ctx, use_gicp):
+    src, _, _ = _gicp_pair()
+    t = A.Target.build(src, ctx)
+    got = A.ComputeCovariances(t, src, use_gicp=use_gicp)
+    want = O.compute_covariances(src, use_gicp=use_gicp)
+    if use_gicp:  # fp64 SVD on both sides, different Jacobi orders: float noise
+        np.testing.assert_allclose(got, want, atol=2e-6)
+    else:  # same neighbours, same fp32 sums in the same order
+        np.testing.assert_allclose(got, want, rtol=1e-6, atol=1e-12)
+
+
+def test_gicp_solve_matches_oracle(ctx):
+    src, dst, T = _gicp_pair()
+    cs, cd = O.compute_covariances(src), O.compute_covariances(dst)
+    idx, _ = O.KDTree(dst).query(src)
+    Tg = np.eye(4, dtype=np.float32)
+    cost = A.ComputeAlignment(src, dst, cs, cd, idx, np.eye(4, dtype=np.float32), Tg, ctx=ctx)
+    F, P, its = O.gicp_solve(src, dst, cs, cd, idx, max_iter=64)
+    # same LM decisions; fp64 sums in a different order
+    assert max(pose_err(Tg, P)) <= 1e-5
+    assert abs(cost - F) <= 1e-6 * F
+
+
+def test_gicp_align_matches_oracle_and_motion(ctx):
+    src, dst, T = _gicp_pair()
+    Tg = np.eye(4, dtype=np.float32)
+    cost = A.ComputeAlignment(src, dst, Tg, ctx=ctx)
+    F, P = O.gicp_align(src, dst)
+    # 16 outer rounds of (exact NN of the float estimate, LM): identical
+    # correspondences every round, so the fp64 summation order is the only
+    # difference (measured: identical poses); a flipped correspondence
+    # would compound, hence the margin
+    assert max(pose_err(Tg, P)) <= 1e-5
+    assert abs(cost - F) <= 1e-6 * F
+    ang, tr = pose_err(Tg, T)
+    assert ang < 1e-3 and tr < 3e-3
+    assert np.isfinite(cost)
+
+
+def test_gicp_contract(ctx):
+    src, dst, _ = _gicp_pair()
+    cs = np.zeros((len(src), 9), np.float32)
+    cd = np.zeros((len(dst), 9), np.float32)
+    bad = np.full(len(src), len(dst), np.int32)
+    out = np.zeros(16, np.float32)
+    seed = np.eye(4, dtype=np.float32).reshape(16)
+    c = C.c_double(0)
+    it = C.c_int32(0)
+    assert L.lib().rst_gicp_solve(ctx.handle, L.fptr(src), len(src), L.fptr(dst), len(dst),
+                                  L.fptr(cs), L.fptr(cd), L.iptr(bad), L.fptr(seed), 8,
+                                  L.fptr(out), C.byref(c), C.byref(it)) == L.RST_E_ARG
+    assert L.lib().rst_gicp_align(ctx.handle, L.fptr(src), 0, L.fptr(dst), len(dst), 16, 8,
+                                  L.fptr(out), C.byref(c)) == L.RST_E_ARG

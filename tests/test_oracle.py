@@ -226,3 +226,61 @@ def test_downsample_voxel_oracle_on_frame():
     got = O.downsample_voxel(cloud, PC.VOXEL)
     np.testing.assert_array_equal(got, NPR.downsample_voxel(cloud, PC.VOXEL))
     assert 0 < len(got) < len(cloud)
+
+
+# ---- f2: GICP oracle (point_cloud_utils.cpp:100-161, align_gicp.cpp:41-163) ----
+def _gicp_pair():
+    g = load_golden("pair_160x120_s2")
+    return (O.downsample_voxel(g["src"], 0.1), O.downsample_voxel(g["dst"], 0.1), g["T_gt"])
+
+
+def test_covariances_oracle_matches_numpy():
+    from scipy.spatial import cKDTree
+    src, _, _ = _gicp_pair()
+    cov = O.compute_covariances(src)
+    _, ii = cKDTree(src.astype(np.float64)).query(src, 33)
+    for k in range(0, len(src), max(1, len(src) // 50)):
+        nb = src[ii[k, 1:]].astype(np.float64)
+        c = nb - nb.mean(0)
+        np.testing.assert_allclose(cov[k], c.T @ c / 31, rtol=1e-4, atol=1e-8)
+    # use_gicp: eigenvalues (1, 1, 1e-2), the last along the smallest direction
+    cg = O.compute_covariances(src, use_gicp=True)
+    for k in range(0, len(src), max(1, len(src) // 20)):
+        w = np.linalg.eigvalsh(cg[k].astype(np.float64))
+        np.testing.assert_allclose(w, [1e-2, 1, 1], atol=1e-5)
+
+
+def test_gicp_gradient_matches_finite_differences():
+    src, dst, T = _gicp_pair()
+    cs, cd = O.compute_covariances(src), O.compute_covariances(dst)
+    idx, _ = O.KDTree(dst).query(src)
+
+    def rod(w):
+        th = np.linalg.norm(w)
+        K = np.array([[0, -w[2], w[1]], [w[2], 0, -w[0]], [-w[1], w[0], 0]])
+        if th < 1e-12:
+            return np.eye(3) + K
+        return np.eye(3) + np.sin(th) / th * K + (1 - np.cos(th)) / th ** 2 * K @ K
+
+    # a pose near (not at) the optimum, so the gradient is well away from 0
+    R = rod(np.array([0.01, -0.02, 0.005])) @ T[:3, :3].astype(np.float64)
+    t = T[:3, 3].astype(np.float64) + 0.003
+
+    F, H, g = O.gicp_eval(src, dst, cs, cd, idx, R, t)
+    num = np.zeros(6)
+    for k in range(6):
+        dx = np.zeros(6)
+        dx[k] = 1e-6
+        fp = O.gicp_eval(src, dst, cs, cd, idx, rod(dx[:3]) @ R, t + dx[3:])[0]
+        fm = O.gicp_eval(src, dst, cs, cd, idx, rod(-dx[:3]) @ R, t - dx[3:])[0]
+        num[k] = (fp - fm) / 2e-6
+    assert np.abs(g - num).max() <= 1e-4 * np.abs(num).max()
+    assert np.all(np.linalg.eigvalsh(H) > 0)
+
+
+def test_gicp_align_oracle_recovers_motion():
+    src, dst, T = _gicp_pair()
+    cost, P = O.gicp_align(src, dst)
+    ang, tr = pose_err(P, T)
+    assert ang < 1e-3 and tr < 3e-3, (ang, tr)
+    assert np.isfinite(cost) and cost > 0
