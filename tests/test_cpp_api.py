@@ -19,6 +19,7 @@ PROBE = r"""
 #include <cstdio>
 #include "rs_tracker/align/align_icp.hpp"
 #include "rs_tracker/common/point_cloud_utils.hpp"
+#include "rs_tracker/align/align_gicp.hpp"
 int main() {
   using namespace rs_tracker;
   Cloud3f two(2), many(50);
@@ -29,6 +30,8 @@ int main() {
   if (AlignIcp3d(two, many, 128, &T)) return 10;
   if (AlignIcp3d(many, two, 128, &T)) return 11;
   if (SolveKabsch(two, many, {{0, 0}}, {}, &T)) return 12;
+  Cloud3f none;
+  if (ComputeAlignment(none, many, &T) != std::numeric_limits<float>::infinity()) return 15;
   ToColMajor(T, after);
   for (int k = 0; k < 16; ++k) if (before[k] != after[k]) return 13;
   try {
