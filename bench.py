@@ -130,6 +130,7 @@ def main():
     ap.add_argument("--cpu-iters", type=int, default=24)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-host-api", action="store_true")
+    ap.add_argument("--no-gicp", action="store_true")
     ap.add_argument("--inflight", type=int, default=2,
                     help="frame pairs in flight per GPU (one HIP stream each)")
     a = ap.parse_args()
@@ -276,6 +277,27 @@ def main():
                 "note": "AlignIcp3d(src, dst, 128, T) with host clouds, one pair at a time: "
                         "PCIe-inclusive (upload, index build, ICP, readback)"}
 
+    # ---- the tracker's GICP loop (rs_tracker.cpp:79-87; extra fields) ------------
+    # per frame: DownsampleVoxel(curr, 0.1); ComputeAlignment(prev, curr, &T)
+    # (16 rounds of exact NN + LM), host clouds, one pair at a time
+    gicp = None
+    if not a.no_gicp:
+        clouds = [A.DownsampleVoxel(driver.unproject(frames[pingpong(k, nfr)], K), 0.1)
+                  for k in range(4)]
+        T = np.eye(4, dtype=np.float32)
+        A.ComputeAlignment(clouds[0], clouds[1], T)  # warm-up
+        t3 = time.perf_counter()
+        costs = []
+        for k in range(1, 4):
+            T = np.eye(4, dtype=np.float32)
+            costs.append(A.ComputeAlignment(clouds[k - 1], clouds[k], T))
+        dtg = (time.perf_counter() - t3) / 3
+        gicp = {"ms_per_pair": 1000.0 * dtg, "pairs_per_s": 1.0 / dtg,
+                "points_per_cloud": int(np.mean([len(c) for c in clouds])),
+                "all_finite": bool(np.all(np.isfinite(costs))),
+                "note": "rs_tracker.cpp loop: DownsampleVoxel(0.1) + GICP ComputeAlignment "
+                        "(covariances k=32, 16 x {exact NN, fp64 LM <= 64 evaluations})"}
+
     # ---- roofline of the dominant kernel (k_p2point, HIP events) --------------------
     avg_ms = st["kernel_ms"] / max(1, st["launches"])
     n_avg = st["n"] / max(1, a.steps)
@@ -321,6 +343,8 @@ def main():
         out["p2plane"] = pl
     if host is not None:
         out["host_api"] = host
+    if gicp is not None:
+        out["gicp"] = gicp
     if cpu is not None:
         out["speedup_vs_cpu_baseline"] = value / cpu["value"]
     print(json.dumps(out))

@@ -5,6 +5,6 @@ set -o pipefail
 mkdir -p gpurun_out
 for k in ${INFLIGHT:-1 2}; do
   f=gpurun_out/bench_if$k.log
-  timeout -k 10 300 python bench.py --no-cpu --no-p2plane --no-host-api --inflight $k > $f 2>&1 || exit $?
+  timeout -k 10 300 python bench.py --no-cpu --no-p2plane --no-host-api --no-gicp --inflight $k > $f 2>&1 || exit $?
   echo "inflight $k: $(grep '^{' $f | python3 -c 'import json,sys; d=json.load(sys.stdin); print(round(d["value"]), "it/s", round(d["frames_per_s"],1), "fps k_icp_nn", round(d["roofline"]["avg_us"],1), "us")')"
 done
