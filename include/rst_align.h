@@ -232,6 +232,22 @@ int rst_downsample_voxel_device(rst_ctx* ctx, const float* d_xyz, int64_t n,
                                 float voxel_size, float* d_out,
                                 int64_t* n_out);
 
+/* ---- CloudAccumulator (rs_replay_app.cpp:76-129) -- */
+/* A voxel map on the device: AddCloud(xfm, cloud) inserts xfm * p for
+ * every point whose voxel (int)(p * inv) -- inv = float(1.0 / voxel_size),
+ * truncation, NaN / out-of-range -> INT_MIN -- is new; the first point added
+ * to a voxel stays.  Extract returns the points in insertion order (the
+ * reference returns them in unordered_map order: same set). */
+typedef struct rst_accum rst_accum;
+int rst_accum_create(rst_ctx* ctx, float voxel_size, rst_accum** out);
+int rst_accum_destroy(rst_accum* a);
+int rst_accum_add(rst_accum* a, const float pose[16], const float* xyz, int64_t n);
+int rst_accum_add_device(rst_accum* a, const float pose[16], const float* d_xyz,
+                         int64_t n);
+int rst_accum_size(const rst_accum* a, int64_t* n);
+/* out holds >= size points */
+int rst_accum_extract(rst_accum* a, float* out, int64_t* n_out);
+
 /* ---- GICP, the align module's second path -------- */
 /* ComputeCovariances(tree, cloud, covs, use_gicp) (point_cloud_utils.cpp:
  * 100-161) on a prepared cloud: per point the 32 nearest others (33-NN,

@@ -71,6 +71,12 @@ def lib():
                                      C.POINTER(C.c_int)]
         L.orc_gicp_align.restype = C.c_double
         L.orc_gicp_align.argtypes = [_f, C.c_int64, _f, C.c_int64, C.c_int, C.c_int, _f]
+        L.orc_accum_create.restype = P
+        L.orc_accum_create.argtypes = [C.c_float]
+        L.orc_accum_free.argtypes = [P]
+        L.orc_accum_add.argtypes = [P, _f, _f, C.c_int64]
+        L.orc_accum_extract.restype = C.c_int64
+        L.orc_accum_extract.argtypes = [P, _f]
         L.orc_unproject.argtypes = [_u16, C.c_int, C.c_int, _f, C.c_float, C.c_int, _f]
         L.orc_align_p2plane.restype = C.c_int
         L.orc_align_p2plane.argtypes = [_f, C.c_int64, _f, _f, C.c_int64, P, C.c_int,
@@ -297,6 +303,29 @@ def gicp_align(src, dst, outer_iters=16, max_inner=64):
     F = lib().orc_gicp_align(_fp(s), s.shape[0], _fp(d), d.shape[0], outer_iters, max_inner,
                              _fp(out))
     return F, _uncm(out)
+
+
+class Accumulator:
+    """CloudAccumulator (rs_replay_app.cpp:76-129), insertion order."""
+
+    def __init__(self, voxel_size=0.05):
+        self.h = lib().orc_accum_create(float(voxel_size))
+
+    def add(self, T, cloud):
+        a = _cloud(cloud)
+        lib().orc_accum_add(self.h, _fp(_cm(T)), _fp(a), a.shape[0])
+
+    def extract(self):
+        n = lib().orc_accum_extract(self.h, None)
+        out = np.zeros((n, 3), np.float32)
+        lib().orc_accum_extract(self.h, _fp(out))
+        return out
+
+    def __del__(self):
+        try:
+            lib().orc_accum_free(self.h)
+        except Exception:
+            pass
 
 
 def align_p2plane(src, dst, dst_normals, max_iter=30, eps=1e-6, mu=4e-4, max_dist=0.0, T=None,

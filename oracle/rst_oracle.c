@@ -1501,3 +1501,99 @@ double orc_gicp_align(const float* src, int64_t n, const float* dst, int64_t m,
   orc_kdtree_free(td);
   return cost;
 }
+
+/* ==== f4: CloudAccumulator (rs_replay_app.cpp:76-129) ======================== */
+struct orc_accum {
+  float inv;
+  int64_t cap, used, count, list_cap;
+  int32_t* keys; /* 3 per slot */
+  uint8_t* used_flag;
+  float* list;
+};
+
+static int orc_trunc_key(float x, float inv) {
+  const float q = x * inv;
+  return (q >= -2147483648.0f && q < 2147483648.0f) ? (int)q : INT_MIN;
+}
+
+orc_accum* orc_accum_create(float voxel_size) {
+  orc_accum* a = (orc_accum*)calloc(1, sizeof(orc_accum));
+  a->inv = (float)(1.0 / (double)voxel_size); /* :91-92 */
+  return a;
+}
+
+void orc_accum_free(orc_accum* a) {
+  if (!a) return;
+  free(a->keys);
+  free(a->used_flag);
+  free(a->list);
+  free(a);
+}
+
+static uint64_t orc_key_hash(int x, int y, int z) {
+  uint64_t h = ((uint64_t)(uint32_t)x * 73856093u) ^ ((uint64_t)(uint32_t)y * 19349663u) ^
+               ((uint64_t)(uint32_t)z * 83492791u);
+  return h ^ (h >> 17);
+}
+
+static void orc_accum_rehash(orc_accum* a, int64_t need) {
+  int64_t cap = a->cap ? a->cap : 1024;
+  while (cap < 2 * need) cap <<= 1;
+  if (cap == a->cap) return;
+  free(a->keys);
+  free(a->used_flag);
+  a->keys = (int32_t*)malloc(sizeof(int32_t) * 3 * (size_t)cap);
+  a->used_flag = (uint8_t*)calloc((size_t)cap, 1);
+  a->cap = cap;
+  for (int64_t j = 0; j < a->count; ++j) {
+    const float* p = a->list + 3 * j;
+    const int k0 = orc_trunc_key(p[0], a->inv), k1 = orc_trunc_key(p[1], a->inv),
+              k2 = orc_trunc_key(p[2], a->inv);
+    int64_t s = (int64_t)(orc_key_hash(k0, k1, k2) & (uint64_t)(cap - 1));
+    while (a->used_flag[s]) s = (s + 1) & (cap - 1);
+    a->used_flag[s] = 1;
+    a->keys[3 * s] = k0;
+    a->keys[3 * s + 1] = k1;
+    a->keys[3 * s + 2] = k2;
+  }
+}
+
+/* AddCloud (:95-106): p = xfm * point (:98), key = (p * inv).cast<int>()
+ * (:108-110), emplace only when new */
+void orc_accum_add(orc_accum* a, const float pose[16], const float* xyz, int64_t n) {
+  orc_accum_rehash(a, a->count + n);
+  if (a->list_cap < a->count + n) {
+    int64_t c = a->list_cap ? a->list_cap : 1024;
+    while (c < a->count + n) c *= 2;
+    a->list = (float*)realloc(a->list, sizeof(float) * 3 * (size_t)c);
+    a->list_cap = c;
+  }
+  for (int64_t i = 0; i < n; ++i) {
+    float p[3];
+    orc_transform_points(pose, xyz + 3 * i, 1, p);
+    const int k0 = orc_trunc_key(p[0], a->inv), k1 = orc_trunc_key(p[1], a->inv),
+              k2 = orc_trunc_key(p[2], a->inv);
+    int64_t s = (int64_t)(orc_key_hash(k0, k1, k2) & (uint64_t)(a->cap - 1));
+    int found = 0;
+    while (a->used_flag[s]) {
+      if (a->keys[3 * s] == k0 && a->keys[3 * s + 1] == k1 && a->keys[3 * s + 2] == k2) {
+        found = 1;
+        break;
+      }
+      s = (s + 1) & (a->cap - 1);
+    }
+    if (found) continue;
+    a->used_flag[s] = 1;
+    a->keys[3 * s] = k0;
+    a->keys[3 * s + 1] = k1;
+    a->keys[3 * s + 2] = k2;
+    memcpy(a->list + 3 * a->count, p, sizeof(p));
+    ++a->count;
+  }
+}
+
+/* ExtractPointCloud (:112-121), insertion order; returns the count */
+int64_t orc_accum_extract(const orc_accum* a, float* out) {
+  if (out && a->count) memcpy(out, a->list, sizeof(float) * 3 * (size_t)a->count);
+  return a->count;
+}

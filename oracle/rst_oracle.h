@@ -161,6 +161,13 @@ double orc_gicp_solve(const float* src, int64_t n, const float* dst, const float
 double orc_gicp_align(const float* src, int64_t n, const float* dst, int64_t m,
                       int outer_iters, int max_inner, float pose_out[16]);
 
+/* ---- f4: CloudAccumulator (rs_replay_app.cpp:76-129) ------------------- */
+typedef struct orc_accum orc_accum;
+orc_accum* orc_accum_create(float voxel_size);
+void orc_accum_free(orc_accum* a);
+void orc_accum_add(orc_accum* a, const float pose[16], const float* xyz, int64_t n);
+int64_t orc_accum_extract(const orc_accum* a, float* out);
+
 /* ---- build's own point-to-plane mode (no reference counterpart) --------- */
 /* Gauss-Newton point-to-plane with the same annealed weight schedule;
  * see DESIGN.md "P2PLANE".  Returns iterations run. */

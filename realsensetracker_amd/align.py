@@ -14,6 +14,10 @@ the MI355X C ABI (include/rst_align.h):
     OrientNormals(cloud, viewpoint, normals)     (in place)
     RemoveNans(cloud)                            -> (k, 3) float32
     DownsampleVoxel(cloud, voxel_size)           -> (k, 3) float32
+    ComputeCovariances(tree, cloud, use_gicp)    -> (n, 3, 3) float32
+    ComputeAlignment(src, dst, T) / (src, dst, src_covs, dst_covs, idx, seed, T)
+                                                 -> cost (GICP; T updated)
+    CloudAccumulator(voxel).AddCloud(xfm, cloud) / .ExtractPointCloud()
 
 Clouds are (n, 3) float32 arrays (the byte layout of Cloud3f); transforms are
 4x4 float32 arrays in math orientation.
@@ -351,6 +355,45 @@ def DownsampleVoxel(cloud, voxel_size: float, ctx: Context | None = None) -> np.
     L.check(L.lib().rst_downsample_voxel(ctx.handle, L.fptr(a), a.shape[0], float(voxel_size),
                                          L.fptr(out), C.byref(n)), "rst_downsample_voxel")
     return out[:n.value].copy()
+
+
+class CloudAccumulator:
+    """rs_replay_app.cpp:76-129 on the device: AddCloud(xfm, cloud) keeps
+    the first point (after xfm) of every voxel (int)(p / voxel_size);
+    ExtractPointCloud() returns them in insertion order (the reference's
+    order is its unordered_map's: same set)."""
+
+    def __init__(self, voxel_size: float = 0.05, ctx: Context | None = None):
+        self.ctx = ctx or get_context()
+        self._h = C.c_void_p()
+        L.check(L.lib().rst_accum_create(self.ctx.handle, float(voxel_size), C.byref(self._h)),
+                "rst_accum_create")
+
+    def AddCloud(self, xfm, cloud) -> None:
+        a = L.as_cloud(cloud)
+        L.check(L.lib().rst_accum_add(self._h, L.fptr(L.pose_to_cm(xfm)), L.fptr(a), len(a)),
+                "rst_accum_add")
+
+    def __len__(self) -> int:
+        n = C.c_int64(0)
+        L.check(L.lib().rst_accum_size(self._h, C.byref(n)), "rst_accum_size")
+        return n.value
+
+    def ExtractPointCloud(self) -> np.ndarray:
+        out = np.zeros((len(self), 3), np.float32)
+        n = C.c_int64(0)
+        L.check(L.lib().rst_accum_extract(self._h, L.fptr(out), C.byref(n)), "rst_accum_extract")
+        return out[:n.value]
+
+    def __del__(self):
+        if sys.is_finalizing():
+            return
+        try:
+            if self._h:
+                L.lib().rst_accum_destroy(self._h)
+                self._h = C.c_void_p()
+        except Exception:
+            pass
 
 
 def ComputeCovariances(tree: Target, cloud=None, use_gicp: bool = False) -> np.ndarray:

@@ -1,30 +1,44 @@
 // rs_replay_app -- the reference's frame-to-frame replay loop
 // (rs_tracker/app/src/rs_replay_app.cpp:211-270) as host C++ over the
-// MI355X align module, with the synthetic frame source in place of the
-// recorded .pb sequence (driver decoupled from the camera):
+// MI355X align module.  Frames come from a directory of recorded RSTC
+// records (include/rs_tracker/driver/cloud_record.hpp; the reference replays
+// a glob of protobuf records) or from the synthetic scene (driver decoupled
+// from the camera):
 //
-//   for each frame: depth -> cloud_raw (rst_unproject, invalid pixels dropped)
+//   for each frame: cloud_raw (record, or depth -> rst_unproject)
 //     RemoveNans(cloud_raw, &cloud)                                 (:229)
+//     first frame: prev = cloud; acc.AddCloud(total_xfm, prev)       (:237-241)
 //     DownsampleVoxel(cloud, v, &curr_down), (prev, v, &prev_down)  (:246-247)
 //     xfm = Identity; ok = AlignIcp3d(curr_down, prev_down, 128, &xfm) (:235,251)
-//     if ok: total_xfm = total_xfm * xfm; prev = cloud               (:266-270)
+//     if ok: total_xfm = total_xfm * xfm; acc.AddCloud(total_xfm, cloud);
+//            prev = cloud                                            (:264-269)
 //
-// Prints per-frame timing and drift against the scene's ground truth.
+// Prints per-frame timing and, for the synthetic scene, drift against the
+// ground truth.
 //
 //   rs_replay_app [--frames N] [--width W] [--height H] [--iters K] [--seed S]
 //                 [--voxel-mm V]  (voxel edge in mm, default 50 as the
 //                                  reference; 0 = align the full clouds)
 //                 [--dump FILE]   (per-frame xfm, one line of 16 col-major floats)
+//                 [--records DIR] (replay DIR/*.rstc in name order)
+//                 [--write-records DIR] (record the synthetic stream's raw clouds)
+//                 [--accum-mm V --map-out FILE] (CloudAccumulator voxel, written
+//                                  as one record at the end)
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <filesystem>
+#include <memory>
 #include <string>
 #include <vector>
 
 #include "rs_tracker/align/align_icp.hpp"
+#include "rs_tracker/common/cloud_accumulator.hpp"
 #include "rs_tracker/common/point_cloud_utils.hpp"
+#include "rs_tracker/driver/cloud_record.hpp"
 
 namespace {
 
@@ -32,6 +46,10 @@ struct Args {
   int frames = 10, width = 640, height = 480, iters = 128, voxel_mm = 50;
   uint64_t seed = 0;
   const char* dump = nullptr;  // write each frame's xfm (16 floats, col-major)
+  const char* records = nullptr;
+  const char* write_records = nullptr;
+  int accum_mm = 0;
+  const char* map_out = nullptr;
 };
 
 Args Parse(int argc, char** argv) {
@@ -46,6 +64,10 @@ Args Parse(int argc, char** argv) {
     else if (k == "--seed") a.seed = (uint64_t)v;
     else if (k == "--dump") a.dump = argv[i + 1];
     else if (k == "--voxel-mm") a.voxel_mm = (int)v;
+    else if (k == "--records") a.records = argv[i + 1];
+    else if (k == "--write-records") a.write_records = argv[i + 1];
+    else if (k == "--accum-mm") a.accum_mm = (int)v;
+    else if (k == "--map-out") a.map_out = argv[i + 1];
     else { std::fprintf(stderr, "unknown flag %s\n", k.c_str()); std::exit(2); }
   }
   return a;
@@ -87,7 +109,19 @@ void PoseError(const float* T, const float* G, double* ang, double* tr) {
 
 int main(int argc, char** argv) {
   using rs_tracker::gpu::Check;
-  const Args a = Parse(argc, argv);
+  Args a = Parse(argc, argv);
+  std::vector<std::string> files;
+  if (a.records) {
+    for (const auto& e : std::filesystem::directory_iterator(a.records))
+      if (e.path().extension() == ".rstc") files.push_back(e.path().string());
+    std::sort(files.begin(), files.end());
+    a.frames = (int)files.size();
+    if (a.frames < 1) {
+      std::fprintf(stderr, "no .rstc records in %s\n", a.records);
+      return 2;
+    }
+  }
+  if (a.write_records) std::filesystem::create_directories(a.write_records);
   rst_scene* scene = nullptr;
   Check(rst_scene_create(a.seed, &scene), "rst_scene_create");
   rst_intrinsics K{};
@@ -104,12 +138,28 @@ int main(int argc, char** argv) {
   std::vector<uint16_t> depth((size_t)a.width * a.height);
   std::vector<float> xyz(3 * depth.size());
   auto grab = [&](int f, float* T_wc) {
+    if (!files.empty()) {  // a recorded frame (:221-225)
+      rs_tracker::Cloud3f cloud_raw, cloud;
+      if (!rs_tracker::ReadCloudRecord(files[f], &cloud_raw)) {
+        std::fprintf(stderr, "bad record %s\n", files[f].c_str());
+        std::exit(2);
+      }
+      for (int k = 0; k < 16; ++k) T_wc[k] = (k % 5 == 0) ? 1.f : 0.f;
+      rs_tracker::RemoveNans(cloud_raw, &cloud);  // (:229)
+      return cloud;
+    }
     Check(rst_scene_trajectory(scene, f, T_wc), "trajectory");
     Check(rst_scene_render_depth(scene, T_wc, &K, 1000u + (uint64_t)f, 0.001f, 0.03f, depth.data()),
           "render");
     int64_t n = 0;
     Check(rst_unproject(ctx.get(), depth.data(), &K, 0, xyz.data(), &n), "rst_unproject");
     const rs_tracker::Cloud3f cloud_raw(xyz.data(), n);
+    if (a.write_records) {
+      char name[64];
+      std::snprintf(name, sizeof(name), "/frame_%05d.rstc", f);
+      if (!rs_tracker::WriteCloudRecord(std::string(a.write_records) + name, cloud_raw, f / 30.0))
+        std::exit(3);
+    }
     rs_tracker::Cloud3f cloud;
     rs_tracker::RemoveNans(cloud_raw, &cloud);  // (:229)
     return cloud;
@@ -120,6 +170,11 @@ int main(int argc, char** argv) {
   rs_tracker::Cloud3f prev = grab(0, T0);
   RigidInverse(T0, T0inv);
   rs_tracker::Isometry3f total_xfm = rs_tracker::Isometry3f::Identity();
+  std::unique_ptr<rs_tracker::CloudAccumulator> acc;
+  if (a.accum_mm > 0) {
+    acc.reset(new rs_tracker::CloudAccumulator((float)a.accum_mm / 1000.0f));
+    acc->AddCloud(total_xfm, prev);  // (:240)
+  }
   double worst_ang = 0.0, worst_tr = 0.0, total_ms = 0.0;
   int ok_count = 0;
   FILE* dump = a.dump ? std::fopen(a.dump, "w") : nullptr;
@@ -146,6 +201,7 @@ int main(int argc, char** argv) {
     }
     if (suc) {
       total_xfm = total_xfm * xfm;
+      if (acc) acc->AddCloud(total_xfm, cloud);  // (:266)
       prev = std::move(cloud);
       ++ok_count;
     } else {
@@ -154,16 +210,23 @@ int main(int argc, char** argv) {
     float tot[16], gt[16];
     rs_tracker::ToColMajor(total_xfm, tot);
     Mul(T0inv, Tf, gt);
-    double ang, tr;
-    PoseError(tot, gt, &ang, &tr);
-    worst_ang = std::fmax(worst_ang, ang);
-    worst_tr = std::fmax(worst_tr, tr);
+    double ang = 0.0, tr = 0.0;
+    if (files.empty()) {  // ground truth only for the synthetic scene
+      PoseError(tot, gt, &ang, &tr);
+      worst_ang = std::fmax(worst_ang, ang);
+      worst_tr = std::fmax(worst_tr, tr);
+    }
     std::printf("frame %3d  n=%7lld  align %8.2f ms  drift %.2e rad %.2e m\n", f,
                 (long long)prev.cols(), ms, ang, tr);
   }
   std::printf("frames %d  aligned %d  mean align %.2f ms  worst drift %.2e rad %.2e m\n",
               a.frames - 1, ok_count, total_ms / std::max(1, a.frames - 1), worst_ang, worst_tr);
   if (dump) std::fclose(dump);
+  if (acc) {
+    const rs_tracker::Cloud3f map = acc->ExtractPointCloud();
+    std::printf("map points %lld\n", (long long)map.cols());
+    if (a.map_out && !rs_tracker::WriteCloudRecord(a.map_out, map)) return 3;
+  }
   rst_scene_destroy(scene);
   return ok_count == a.frames - 1 ? 0 : 1;
 }

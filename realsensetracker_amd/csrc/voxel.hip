@@ -43,9 +43,12 @@ __device__ __forceinline__ bool finite_pt(const float* __restrict__ xyz, int64_t
          __builtin_isfinite(xyz[3 * i + 2]);
 }
 
-// (int)floor(x / v) with x86-64 cvttss2si semantics outside int range / NaN
-__device__ __forceinline__ int vox_coord(float x, float v) {
-  const float q = floorf(x / v);
+// Voxel keys with x86-64 cvttss2si semantics outside int range / NaN:
+//   kind 0 (DownsampleVoxel, point_cloud_utils.cpp:41-42): (int)floor(x / v);
+//   kind 1 (CloudAccumulator::GetVoxelIndex, rs_replay_app.cpp:108-110):
+//           (int)(x * v), v = the float inverse voxel size (truncation).
+__device__ __forceinline__ int vox_coord(float x, float v, int kind) {
+  const float q = kind == 0 ? floorf(x / v) : x * v;
   return (q >= -2147483648.0f && q < 2147483648.0f) ? (int)q : INT_MIN;
 }
 
@@ -53,9 +56,10 @@ struct Vox {
   int x, y, z;
 };
 
-__device__ __forceinline__ Vox vox_of(const float* __restrict__ xyz, int64_t i, float v) {
-  return Vox{vox_coord(xyz[3 * i], v), vox_coord(xyz[3 * i + 1], v),
-             vox_coord(xyz[3 * i + 2], v)};
+__device__ __forceinline__ Vox vox_of(const float* __restrict__ xyz, int64_t i, float v,
+                                      int kind = 0) {
+  return Vox{vox_coord(xyz[3 * i], v, kind), vox_coord(xyz[3 * i + 1], v, kind),
+             vox_coord(xyz[3 * i + 2], v, kind)};
 }
 
 __device__ __forceinline__ uint32_t vox_hash(const Vox& k) {
@@ -157,11 +161,11 @@ __global__ __launch_bounds__(kBS) void k_keep_write(const float* __restrict__ xy
 // 1. claim the slot of i's voxel: the first empty slot on its probe sequence
 //    (CAS), or the slot whose representative point lies in the same voxel
 __global__ __launch_bounds__(kBS) void k_vox_claim(const float* __restrict__ xyz, int64_t n,
-                                                   float v, int32_t* __restrict__ rep,
+                                                   float v, int kind, int32_t* __restrict__ rep,
                                                    uint32_t mask, int32_t* __restrict__ slot_of) {
   const int64_t i = blockIdx.x * (int64_t)kBS + threadIdx.x;
   if (i >= n) return;
-  const Vox k = vox_of(xyz, i, v);
+  const Vox k = vox_of(xyz, i, v, kind);
   uint32_t h = vox_hash(k) & mask;
   for (uint32_t probe = 0; probe <= mask; ++probe) {
     int32_t cur = __hip_atomic_load(&rep[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -173,7 +177,7 @@ __global__ __launch_bounds__(kBS) void k_vox_claim(const float* __restrict__ xyz
       }
       cur = prev;
     }
-    const Vox o = vox_of(xyz, cur, v);
+    const Vox o = vox_of(xyz, cur, v, kind);
     if (o.x == k.x && o.y == k.y && o.z == k.z) {
       slot_of[i] = (int32_t)h;
       return;
@@ -236,12 +240,16 @@ int remove_nans_device(rst_ctx* ctx, const float* d_xyz, int64_t n, float* d_out
   return compact(ctx, d_xyz, n, 0, nullptr, counts, counts + nb + 16, d_out, n_out);
 }
 
-int downsample_voxel_device(rst_ctx* ctx, const float* d_xyz, int64_t n, float voxel,
-                            float* d_out, int64_t* n_out) {
-  if (n == 0) {
-    *n_out = 0;
-    return RST_OK;
-  }
+// flag[i] = 1 iff point i is the first (lowest index) of its voxel; the
+// workspace layout is returned so the caller can reuse its count buffer
+struct VoxWs {
+  uint8_t* flag;
+  uint32_t* counts;
+  int nb;
+};
+
+int first_per_voxel(rst_ctx* ctx, const float* d_xyz, int64_t n, float v, int kind,
+                    VoxWs* out) {
   uint32_t slots = 1024;
   while ((int64_t)slots < 2 * n) slots <<= 1;
   const int nb = blocks_for(n, kTile);
@@ -256,16 +264,111 @@ int downsample_voxel_device(rst_ctx* ctx, const float* d_xyz, int64_t n, float v
   int32_t* rep = (int32_t*)w;
   int32_t* minidx = (int32_t*)(w + o_min);
   int32_t* slot_of = (int32_t*)(w + o_slot);
-  uint8_t* flag = (uint8_t*)(w + o_flag);
-  uint32_t* counts = (uint32_t*)(w + o_cnt);
+  out->flag = (uint8_t*)(w + o_flag);
+  out->counts = (uint32_t*)(w + o_cnt);
+  out->nb = nb;
   hipStream_t st = ctx->stream;
   RST_HIP(hipMemsetAsync(rep, 0xff, sizeof(int32_t) * slots, st));     // -1: empty
   RST_HIP(hipMemsetAsync(minidx, 0x7f, sizeof(int32_t) * slots, st));  // > any index
-  k_vox_claim<<<blocks_for(n), kBS, 0, st>>>(d_xyz, n, voxel, rep, slots - 1, slot_of);
+  k_vox_claim<<<blocks_for(n), kBS, 0, st>>>(d_xyz, n, v, kind, rep, slots - 1, slot_of);
   k_vox_min<<<blocks_for(n), kBS, 0, st>>>(n, slot_of, minidx);
-  k_vox_flag<<<blocks_for(n), kBS, 0, st>>>(n, slot_of, minidx, flag);
+  k_vox_flag<<<blocks_for(n), kBS, 0, st>>>(n, slot_of, minidx, out->flag);
   RST_HIP(hipGetLastError());
-  return compact(ctx, d_xyz, n, 1, flag, counts, counts + nb + 16, d_out, n_out);
+  return RST_OK;
+}
+
+int downsample_voxel_device(rst_ctx* ctx, const float* d_xyz, int64_t n, float voxel,
+                            float* d_out, int64_t* n_out) {
+  if (n == 0) {
+    *n_out = 0;
+    return RST_OK;
+  }
+  VoxWs w;
+  RST_CHECK(first_per_voxel(ctx, d_xyz, n, voxel, 0, &w));
+  return compact(ctx, d_xyz, n, 1, w.flag, w.counts, w.counts + w.nb + 16, d_out, n_out);
+}
+
+// ---- CloudAccumulator (rs_replay_app.cpp:76-129) --------------------------------------
+// A persistent voxel map: the first point ever added to each voxel, kept in
+// insertion order.  Per AddCloud: transform (xfm * p, align_icp.cpp:107's
+// order), the first point per voxel within the cloud (first_per_voxel,
+// kind 1), then those representatives -- distinct keys -- are inserted into
+// the persistent table (64-bit owner word per slot: cloud number << 32 |
+// index; a slot owned by the current cloud holds a different key, one owned
+// by an earlier cloud has its key visible and is compared), and the inserted
+// ones are appended to the point list with an order-preserving compaction.
+// The table is rebuilt from the list when it passes half full.
+constexpr uint64_t kAccEmpty = ~0ull;
+constexpr uint32_t kAccRebuilt = 0xFFFFFFFEu;
+
+__global__ __launch_bounds__(kBS) void k_acc_xform(const float* __restrict__ xyz, int64_t n,
+                                                   Pose3 P, float* __restrict__ out) {
+  const int64_t i = blockIdx.x * (int64_t)kBS + threadIdx.x;
+  if (i >= n) return;
+  float x, y, z;
+  xform(P, xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2], x, y, z);
+  out[3 * i] = x;
+  out[3 * i + 1] = y;
+  out[3 * i + 2] = z;
+}
+
+__global__ __launch_bounds__(kBS) void k_acc_insert(const float* __restrict__ xyz, int64_t n,
+                                                    const uint8_t* __restrict__ first, float inv,
+                                                    uint64_t* __restrict__ owner,
+                                                    int32_t* __restrict__ keys, uint32_t mask,
+                                                    uint32_t cloud, uint8_t* __restrict__ ins) {
+  const int64_t i = blockIdx.x * (int64_t)kBS + threadIdx.x;
+  if (i >= n) return;
+  if (!first[i]) {
+    ins[i] = 0;
+    return;
+  }
+  const Vox k = vox_of(xyz, i, inv, 1);
+  const uint64_t mine = ((uint64_t)cloud << 32) | (uint64_t)(uint32_t)i;
+  uint32_t h = vox_hash(k) & mask;
+  for (uint32_t probe = 0; probe <= mask; ++probe) {
+    uint64_t o = __hip_atomic_load(&owner[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (o == kAccEmpty) {
+      const uint64_t prev = atomicCAS((unsigned long long*)&owner[h], kAccEmpty, mine);
+      if (prev == kAccEmpty) {
+        keys[3 * h] = k.x;
+        keys[3 * h + 1] = k.y;
+        keys[3 * h + 2] = k.z;
+        ins[i] = 1;
+        return;
+      }
+      o = prev;
+    }
+    // a slot taken in this launch holds another key (the representatives'
+    // keys are distinct); earlier slots' keys are visible: compare
+    if ((uint32_t)(o >> 32) != cloud && keys[3 * h] == k.x && keys[3 * h + 1] == k.y &&
+        keys[3 * h + 2] == k.z) {
+      ins[i] = 0;  // the voxel already has its point (emplace only when new)
+      return;
+    }
+    h = (h + 1) & mask;
+  }
+  ins[i] = 0;  // unreachable: the table stays at most half full
+}
+
+// re-insert every list point (distinct keys by construction)
+__global__ __launch_bounds__(kBS) void k_acc_rebuild(const float* __restrict__ list, int64_t n,
+                                                     float inv, uint64_t* __restrict__ owner,
+                                                     int32_t* __restrict__ keys, uint32_t mask) {
+  const int64_t i = blockIdx.x * (int64_t)kBS + threadIdx.x;
+  if (i >= n) return;
+  const Vox k = vox_of(list, i, inv, 1);
+  const uint64_t mine = ((uint64_t)kAccRebuilt << 32) | (uint64_t)(uint32_t)i;
+  uint32_t h = vox_hash(k) & mask;
+  for (uint32_t probe = 0; probe <= mask; ++probe) {
+    if (atomicCAS((unsigned long long*)&owner[h], kAccEmpty, mine) == kAccEmpty) {
+      keys[3 * h] = k.x;
+      keys[3 * h + 1] = k.y;
+      keys[3 * h + 2] = k.z;
+      return;
+    }
+    h = (h + 1) & mask;
+  }
 }
 
 }  // namespace rst
@@ -337,6 +440,164 @@ int rst_downsample_voxel(rst_ctx* ctx, const float* xyz, int64_t n, float voxel_
   return run_host(ctx, xyz, n, out, n_out, [&](const float* din, float* dout) {
     return downsample_voxel_device(ctx, din, n, voxel_size, dout, n_out);
   });
+}
+
+}  // extern "C"
+
+// ---- CloudAccumulator handle ----------------------------------------------------------
+struct rst_accum {
+  rst_ctx* ctx = nullptr;
+  float voxel = 0.f, inv = 0.f;
+  uint32_t cap = 0;        // table slots (power of two)
+  uint64_t* owner = nullptr;
+  int32_t* keys = nullptr;  // 3 per slot
+  float* list = nullptr;    // accumulated points, insertion order
+  int64_t count = 0, list_cap = 0;
+  uint32_t cloud = 0;       // AddCloud calls so far
+};
+
+namespace {
+
+int accum_grow_table(rst_accum* a, int64_t need) {
+  uint32_t cap = a->cap ? a->cap : 1u << 16;
+  while ((int64_t)cap < 2 * need) cap <<= 1;
+  if (cap == a->cap && a->owner) return RST_OK;
+  hipStream_t st = a->ctx->stream;
+  RST_HIP(hipStreamSynchronize(st));
+  if (a->owner) hipFree(a->owner);
+  if (a->keys) hipFree(a->keys);
+  a->owner = nullptr;
+  a->keys = nullptr;
+  if (hipMalloc(&a->owner, sizeof(uint64_t) * cap) != hipSuccess ||
+      hipMalloc(&a->keys, sizeof(int32_t) * 3 * cap) != hipSuccess)
+    return RST_E_NOMEM;
+  a->cap = cap;
+  RST_HIP(hipMemsetAsync(a->owner, 0xff, sizeof(uint64_t) * cap, st));
+  if (a->count > 0) {
+    k_acc_rebuild<<<(unsigned)((a->count + kBS - 1) / kBS), kBS, 0, st>>>(
+        a->list, a->count, a->inv, a->owner, a->keys, cap - 1);
+    RST_HIP(hipGetLastError());
+  }
+  return RST_OK;
+}
+
+int accum_grow_list(rst_accum* a, int64_t need) {
+  if (need <= a->list_cap) return RST_OK;
+  int64_t cap = a->list_cap ? a->list_cap : 1 << 16;
+  while (cap < need) cap *= 2;
+  float* nl = nullptr;
+  if (hipMalloc(&nl, sizeof(float) * 3 * cap) != hipSuccess) return RST_E_NOMEM;
+  if (a->count > 0)
+    RST_HIP(hipMemcpyAsync(nl, a->list, sizeof(float) * 3 * a->count, hipMemcpyDeviceToDevice,
+                           a->ctx->stream));
+  RST_HIP(hipStreamSynchronize(a->ctx->stream));
+  if (a->list) hipFree(a->list);
+  a->list = nl;
+  a->list_cap = cap;
+  return RST_OK;
+}
+
+int accum_add_device(rst_accum* a, const float pose[16], const float* d_xyz, int64_t n) {
+  if (n == 0) return RST_OK;
+  rst_ctx* ctx = a->ctx;
+  hipStream_t st = ctx->stream;
+  RST_CHECK(accum_grow_table(a, a->count + n));
+  RST_CHECK(accum_grow_list(a, a->count + n));
+  float* tmp = nullptr;
+  uint8_t* ins = nullptr;
+  size_t ct = 0, ci = 0;
+  RST_CHECK(ctx_alloc(ctx, sizeof(float) * 3 * n, (void**)&tmp, &ct));
+  int s = ctx_alloc(ctx, (size_t)n, (void**)&ins, &ci);
+  if (s >= 0) {
+    Pose3 P;
+    for (int c = 0; c < 3; ++c)
+      for (int r = 0; r < 3; ++r) P.r[3 * c + r] = pose[4 * c + r];  // column-major
+    for (int r = 0; r < 3; ++r) P.t[r] = pose[12 + r];
+    k_acc_xform<<<blocks_for(n), kBS, 0, st>>>(d_xyz, n, P, tmp);
+    VoxWs w;
+    s = first_per_voxel(ctx, tmp, n, a->inv, 1, &w);
+    if (s >= 0) {
+      k_acc_insert<<<blocks_for(n), kBS, 0, st>>>(tmp, n, w.flag, a->inv, a->owner, a->keys,
+                                                  a->cap - 1, a->cloud, ins);
+      int64_t added = 0;
+      s = compact(ctx, tmp, n, 1, ins, w.counts, w.counts + w.nb + 16, a->list + 3 * a->count,
+                  &added);
+      if (s >= 0) {
+        a->count += added;
+        a->cloud = a->cloud + 1 >= kAccRebuilt ? 0 : a->cloud + 1;
+      }
+    }
+  }
+  hipStreamSynchronize(st);
+  ctx_release(ctx, tmp, ct);
+  if (ins) ctx_release(ctx, ins, ci);
+  return s < 0 ? s : RST_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rst_accum_create(rst_ctx* ctx, float voxel_size, rst_accum** out) {
+  if (!ctx || !out || !(voxel_size > 0.f)) return RST_E_ARG;
+  RST_HIP(hipSetDevice(ctx->device));
+  rst_accum* a = new rst_accum();
+  a->ctx = ctx;
+  a->voxel = voxel_size;
+  a->inv = (float)(1.0 / (double)voxel_size);  // voxel_size_inv_(1.0 / voxel_size_)
+  *out = a;
+  return RST_OK;
+}
+
+int rst_accum_destroy(rst_accum* a) {
+  if (!a) return RST_OK;
+  if (a->ctx) hipStreamSynchronize(a->ctx->stream);
+  if (a->owner) hipFree(a->owner);
+  if (a->keys) hipFree(a->keys);
+  if (a->list) hipFree(a->list);
+  delete a;
+  return RST_OK;
+}
+
+int rst_accum_add_device(rst_accum* a, const float pose[16], const float* d_xyz, int64_t n) {
+  if (!a || !pose || n < 0 || (n > 0 && !d_xyz) || n >= ((int64_t)1 << 30)) return RST_E_ARG;
+  RST_HIP(hipSetDevice(a->ctx->device));
+  return accum_add_device(a, pose, d_xyz, n);
+}
+
+int rst_accum_add(rst_accum* a, const float pose[16], const float* xyz, int64_t n) {
+  if (!a || !pose || n < 0 || (n > 0 && !xyz) || n >= ((int64_t)1 << 30)) return RST_E_ARG;
+  RST_HIP(hipSetDevice(a->ctx->device));
+  if (n == 0) return RST_OK;
+  float* d = nullptr;
+  size_t c = 0;
+  RST_CHECK(ctx_alloc(a->ctx, sizeof(float) * 3 * n, (void**)&d, &c));
+  int s = hipMemcpyAsync(d, xyz, sizeof(float) * 3 * n, hipMemcpyHostToDevice, a->ctx->stream) ==
+                  hipSuccess
+              ? RST_OK
+              : RST_E_HIP;
+  if (s >= 0) s = accum_add_device(a, pose, d, n);
+  hipStreamSynchronize(a->ctx->stream);
+  ctx_release(a->ctx, d, c);
+  return s;
+}
+
+int rst_accum_size(const rst_accum* a, int64_t* n) {
+  if (!a || !n) return RST_E_ARG;
+  *n = a->count;
+  return RST_OK;
+}
+
+int rst_accum_extract(rst_accum* a, float* out, int64_t* n_out) {
+  if (!a || !n_out || (a->count > 0 && !out)) return RST_E_ARG;
+  RST_HIP(hipSetDevice(a->ctx->device));
+  if (a->count > 0) {
+    RST_HIP(hipMemcpyAsync(out, a->list, sizeof(float) * 3 * a->count, hipMemcpyDeviceToHost,
+                           a->ctx->stream));
+    RST_HIP(hipStreamSynchronize(a->ctx->stream));
+  }
+  *n_out = a->count;
+  return RST_OK;
 }
 
 }  // extern "C"

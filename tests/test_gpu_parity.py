@@ -605,3 +605,38 @@ def test_gicp_contract(ctx):
                                   L.fptr(out), C.byref(c), C.byref(it)) == L.RST_E_ARG
     assert L.lib().rst_gicp_align(ctx.handle, L.fptr(src), 0, L.fptr(dst), len(dst), 16, 8,
                                   L.fptr(out), C.byref(c)) == L.RST_E_ARG
+
+
+# ---- f4: CloudAccumulator (rs_replay_app.cpp:76-129) ---------------------------
+def test_accumulator_matches_oracle(ctx):
+    g = load_golden("pair_160x120_s2")
+    rng = np.random.default_rng(9)
+    extra = rng.uniform(-3, 3, (2000, 3)).astype(np.float32)
+    extra[:7] = np.nan
+    extra[7:9] = 1e30  # out of int range: the INT_MIN voxel
+    T2 = g["T_gt"].astype(np.float32)
+    seq = [(np.eye(4, dtype=np.float32), g["src"]), (T2, g["dst"]),
+           (np.eye(4, dtype=np.float32), extra), (T2, g["src"]), (T2, np.zeros((0, 3), np.float32))]
+    acc = A.CloudAccumulator(0.05, ctx)
+    ref = O.Accumulator(0.05)
+    for T, c in seq:
+        acc.AddCloud(T, c)
+        ref.add(T, c)
+        np.testing.assert_array_equal(acc.ExtractPointCloud(), ref.extract())
+
+
+def test_accumulator_full_frames_grow(ctx):
+    # three 640x480 frames along the trajectory: the device table grows and
+    # is rebuilt from the point list on the way
+    K = driver.intrinsics(640, 480)
+    sc = driver.SyntheticScene(4)
+    acc = A.CloudAccumulator(0.02, ctx)
+    ref = O.Accumulator(0.02)
+    for f in range(3):
+        T = sc.trajectory(f).astype(np.float32)
+        c = driver.unproject(sc.render(sc.trajectory(f), K, noise_seed=f), K, ctx=ctx)
+        acc.AddCloud(T, c)
+        ref.add(T, c)
+    got = acc.ExtractPointCloud()
+    assert len(got) > 100000
+    np.testing.assert_array_equal(got, ref.extract())

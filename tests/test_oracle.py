@@ -284,3 +284,35 @@ def test_gicp_align_oracle_recovers_motion():
     ang, tr = pose_err(P, T)
     assert ang < 1e-3 and tr < 3e-3, (ang, tr)
     assert np.isfinite(cost) and cost > 0
+
+
+# ---- f4: CloudAccumulator oracle (rs_replay_app.cpp:76-129) -------------------
+def _accum_numpy(clouds_poses, voxel):
+    inv = np.float32(1.0 / voxel)
+    seen, out = set(), []
+    for T, cloud in clouds_poses:
+        p = NPR.transform(T, cloud)
+        with np.errstate(invalid="ignore", over="ignore"):
+            q = p * inv
+        ok = (q >= np.float32(-2147483648.0)) & (q < np.float32(2147483648.0))
+        k = np.where(ok, np.trunc(np.where(ok, q, 0)), -2147483648).astype(np.int64)
+        for i in range(len(p)):
+            key = tuple(k[i])
+            if key not in seen:
+                seen.add(key)
+                out.append(p[i])
+    return np.array(out, np.float32).reshape(-1, 3)
+
+
+def test_accumulator_oracle_matches_numpy():
+    g = load_golden("pair_80x60_s0")
+    rng = np.random.default_rng(5)
+    T1 = np.eye(4, dtype=np.float32)
+    T2 = g["T_gt"].astype(np.float32)
+    extra = rng.uniform(-3, 3, (500, 3)).astype(np.float32)
+    extra[:5] = np.nan
+    seq = [(T1, g["src"]), (T2, g["dst"]), (T1, extra), (T2, g["src"])]
+    acc = O.Accumulator(0.05)
+    for T, c in seq:
+        acc.add(T, c)
+    np.testing.assert_array_equal(acc.extract(), _accum_numpy(seq, 0.05))
