@@ -232,6 +232,24 @@ int rst_downsample_voxel_device(rst_ctx* ctx, const float* d_xyz, int64_t n,
                                 float voxel_size, float* d_out,
                                 int64_t* n_out);
 
+/* ---- FPFH global initialisation ------------------ */
+/* ComputeFpfh(cloud, viewpoint, normal_k, feature_radius, &fpfh)
+ * (fpfh.cpp:248-262): index, kNN-PCA normals oriented to the viewpoint
+ * (normal_k in {8, 16, 32}, n >= normal_k), SPFH over the radius neighbours
+ * (|p - q|^2 < r^2), FPFH = sum over neighbours but self of spfh / dist,
+ * each 11-bin histogram normalised (fpfh.cpp:114-165).  fpfh_out: n x 33
+ * floats, input order. */
+int rst_compute_fpfh(rst_ctx* ctx, const float* xyz, int64_t n,
+                     const float viewpoint[3], int normal_k, float radius,
+                     float* fpfh_out);
+/* ComputeMatches(src, dst, k) (fpfh.cpp:285-300): the exact k (1 or 2)
+ * nearest dst features of every src feature (33-D, nanoflann metric_L2
+ * arithmetic, ties to the lower index); idx_out n x k, d2_out (optional)
+ * n x k. */
+int rst_compute_matches(rst_ctx* ctx, const float* src_feat, int64_t n,
+                        const float* dst_feat, int64_t m, int k,
+                        int32_t* idx_out, float* d2_out);
+
 /* ---- CloudAccumulator (rs_replay_app.cpp:76-129) -- */
 /* A voxel map on the device: AddCloud(xfm, cloud) inserts xfm * p for
  * every point whose voxel (int)(p * inv) -- inv = float(1.0 / voxel_size),

@@ -71,6 +71,8 @@ def lib():
                                      C.POINTER(C.c_int)]
         L.orc_gicp_align.restype = C.c_double
         L.orc_gicp_align.argtypes = [_f, C.c_int64, _f, C.c_int64, C.c_int, C.c_int, _f]
+        L.orc_compute_fpfh.argtypes = [_f, C.c_int64, _f, C.c_int, C.c_float, _f]
+        L.orc_compute_matches.argtypes = [_f, C.c_int64, _f, C.c_int64, C.c_int, _i, _f]
         L.orc_accum_create.restype = P
         L.orc_accum_create.argtypes = [C.c_float]
         L.orc_accum_free.argtypes = [P]
@@ -303,6 +305,26 @@ def gicp_align(src, dst, outer_iters=16, max_inner=64):
     F = lib().orc_gicp_align(_fp(s), s.shape[0], _fp(d), d.shape[0], outer_iters, max_inner,
                              _fp(out))
     return F, _uncm(out)
+
+
+def compute_fpfh(cloud, viewpoint=(0, 0, 0), normal_k=16, radius=0.5):
+    """ComputeFpfh (fpfh.cpp:248-262): (n, 33) float32."""
+    a = _cloud(cloud)
+    out = np.zeros((a.shape[0], 33), np.float32)
+    lib().orc_compute_fpfh(_fp(a), a.shape[0], _fp(np.asarray(viewpoint, np.float32)),
+                           int(normal_k), float(radius), _fp(out))
+    return out
+
+
+def compute_matches(src_feat, dst_feat, k=2):
+    """ComputeMatches (fpfh.cpp:285-300): (idx (n, k), d2 (n, k))."""
+    s = np.ascontiguousarray(np.asarray(src_feat, np.float32).reshape(-1, 33))
+    d = np.ascontiguousarray(np.asarray(dst_feat, np.float32).reshape(-1, 33))
+    idx = np.zeros((len(s), k), np.int32)
+    d2 = np.zeros((len(s), k), np.float32)
+    lib().orc_compute_matches(_fp(s), len(s), _fp(d), len(d), int(k), idx.ctypes.data_as(_i),
+                              _fp(d2))
+    return idx, d2
 
 
 class Accumulator:

@@ -161,6 +161,14 @@ double orc_gicp_solve(const float* src, int64_t n, const float* dst, const float
 double orc_gicp_align(const float* src, int64_t n, const float* dst, int64_t m,
                       int outer_iters, int max_inner, float pose_out[16]);
 
+/* ---- f3: FPFH (fpfh.cpp:20-165,248-300; rst_oracle_fpfh.c) ------------- */
+/* ComputeFpfh: out n x 33, input order (normal_k as orc_compute_normals) */
+void orc_compute_fpfh(const float* xyz, int64_t n, const float viewpoint[3], int normal_k,
+                      float radius, float* out);
+/* ComputeMatches: idx n x k (k = 1 or 2), d2 optional */
+void orc_compute_matches(const float* src, int64_t n, const float* dst, int64_t m, int k,
+                         int32_t* idx, float* d2);
+
 /* ---- f4: CloudAccumulator (rs_replay_app.cpp:76-129) ------------------- */
 typedef struct orc_accum orc_accum;
 orc_accum* orc_accum_create(float voxel_size);

@@ -86,6 +86,10 @@ PROTOTYPES = {
     "rst_downsample_voxel": (C.c_int, [_P, c_float_p, C.c_int64, C.c_float, c_float_p,
                                        c_int64_p]),
     "rst_downsample_voxel_device": (C.c_int, [_P, _P, C.c_int64, C.c_float, _P, c_int64_p]),
+    "rst_compute_fpfh": (C.c_int, [_P, c_float_p, C.c_int64, c_float_p, C.c_int, C.c_float,
+                                   c_float_p]),
+    "rst_compute_matches": (C.c_int, [_P, c_float_p, C.c_int64, c_float_p, C.c_int64, C.c_int,
+                                      c_int32_p, c_float_p]),
     "rst_accum_create": (C.c_int, [_P, C.c_float, C.POINTER(_P)]),
     "rst_accum_destroy": (C.c_int, [_P]),
     "rst_accum_add": (C.c_int, [_P, c_float_p, c_float_p, C.c_int64]),

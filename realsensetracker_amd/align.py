@@ -18,6 +18,9 @@ the MI355X C ABI (include/rst_align.h):
     ComputeAlignment(src, dst, T) / (src, dst, src_covs, dst_covs, idx, seed, T)
                                                  -> cost (GICP; T updated)
     CloudAccumulator(voxel).AddCloud(xfm, cloud) / .ExtractPointCloud()
+    ComputeFpfh(cloud, viewpoint, normal_k, radius) -> (n, 33) float32
+    ComputeMatches(src_fpfh, dst_fpfh, 2)        -> (n, 2) int32
+    PruneMatchesLowe(matches, src_fpfh, dst_fpfh, ratio) -> (pairs, weights)
 
 Clouds are (n, 3) float32 arrays (the byte layout of Cloud3f); transforms are
 4x4 float32 arrays in math orientation.
@@ -355,6 +358,60 @@ def DownsampleVoxel(cloud, voxel_size: float, ctx: Context | None = None) -> np.
     L.check(L.lib().rst_downsample_voxel(ctx.handle, L.fptr(a), a.shape[0], float(voxel_size),
                                          L.fptr(out), C.byref(n)), "rst_downsample_voxel")
     return out[:n.value].copy()
+
+
+def ComputeFpfh(cloud, viewpoint=(0.0, 0.0, 0.0), normal_k: int = 16,
+                feature_radius: float = 0.5, ctx: Context | None = None) -> np.ndarray:
+    """fpfh.cpp:248-262: (n, 33) float32 FPFH features (rs_align_app's
+    defaults: normal_k 16, radius 0.5)."""
+    ctx = ctx or get_context()
+    a = L.as_cloud(cloud)
+    out = np.zeros((len(a), 33), np.float32)
+    vp = np.asarray(viewpoint, np.float32)
+    L.check(L.lib().rst_compute_fpfh(ctx.handle, L.fptr(a), len(a), L.fptr(vp), int(normal_k),
+                                     float(feature_radius), L.fptr(out)), "rst_compute_fpfh")
+    return out
+
+
+def ComputeMatches(src_fpfh, dst_fpfh, num_matches: int = 2,
+                   ctx: Context | None = None) -> np.ndarray:
+    """fpfh.cpp:285-300: (n, num_matches) int32 indices of the nearest dst
+    features (num_matches 1 or 2)."""
+    ctx = ctx or get_context()
+    s = np.ascontiguousarray(np.asarray(src_fpfh, np.float32).reshape(-1, 33))
+    d = np.ascontiguousarray(np.asarray(dst_fpfh, np.float32).reshape(-1, 33))
+    out = np.zeros((len(s), num_matches), np.int32)
+    L.check(L.lib().rst_compute_matches(ctx.handle, L.fptr(s), len(s), L.fptr(d), len(d),
+                                        int(num_matches), L.iptr(out), None),
+            "rst_compute_matches")
+    return out
+
+
+def PruneMatchesLowe(matches, src_fpfh, dst_fpfh, lowe_ratio: float = 0.9):
+    """rs_align_app.cpp:177-217 (the caller's host code): keep (i, j0) when
+    d0 < lowe_ratio * d1 (or (i, j1) symmetrically), weight exp(-d / 0.0625)
+    with d the squared feature distance.  Returns (pairs (k, 2) int32,
+    weights (k,) float32)."""
+    m = np.asarray(matches, np.int64)
+    s = np.asarray(src_fpfh, np.float32)
+    d = np.asarray(dst_fpfh, np.float32)
+    r = np.float32(lowe_ratio)
+    kvar = np.float32(0.25 * 0.25)
+    pairs, w = [], []
+    for i in range(len(m)):
+        j0, j1 = int(m[i, 0]), int(m[i, 1])
+        e0 = s[i] - d[j0]
+        e1 = s[i] - d[j1]
+        d0 = np.float32(np.sum(e0 * e0, dtype=np.float32))
+        d1 = np.float32(np.sum(e1 * e1, dtype=np.float32))
+        if d0 < d1:
+            if d0 < r * d1:
+                pairs.append((i, j0))
+                w.append(np.exp(-d0 / kvar))
+        elif d1 < r * d0:
+            pairs.append((i, j1))
+            w.append(np.exp(-d1 / kvar))
+    return (np.asarray(pairs, np.int32).reshape(-1, 2), np.asarray(w, np.float32))
 
 
 class CloudAccumulator:

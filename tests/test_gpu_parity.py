@@ -640,3 +640,64 @@ def test_accumulator_full_frames_grow(ctx):
     got = acc.ExtractPointCloud()
     assert len(got) > 100000
     np.testing.assert_array_equal(got, ref.extract())
+
+
+# ---- f3: FPFH global initialisation (fpfh.cpp, rs_align_app.cpp:272-295) --------
+@pytest.mark.parametrize("radius", [0.25, 0.5])
+def test_fpfh_matches_oracle(ctx, radius):
+    src, _, _ = _gicp_pair()
+    got = A.ComputeFpfh(src, (0, 0, 0), 16, radius, ctx=ctx)
+    want = O.compute_fpfh(src, (0, 0, 0), 16, radius)
+    # SPFH: the same bins (order-free sums); FPFH: the same neighbours summed
+    # in BVH vs index order -> float rounding only
+    err = np.abs(got - want).max(axis=1)
+    assert np.mean(err <= 1e-5) >= 0.999, np.sort(err)[-10:]
+    assert err.max() <= 0.05
+
+
+@pytest.mark.parametrize("k", [1, 2])
+def test_feature_matches_bitexact(ctx, k):
+    src, dst, _ = _gicp_pair()
+    fs = O.compute_fpfh(src, radius=0.5)
+    fd = O.compute_fpfh(dst, radius=0.5)
+    fd[10] = fd[20]  # an exact tie: the lower index wins
+    got = A.ComputeMatches(fs, fd, k, ctx=ctx)
+    want, _ = O.compute_matches(fs, fd, k)
+    assert np.array_equal(got, want)
+
+
+def test_fpfh_init_pipeline_matches_oracle(ctx):
+    """rs_align_app.cpp:272-295: FPFH both clouds, 2-NN matches, Lowe 0.9,
+    weighted Kabsch -- on the GPU vs on the oracle's features."""
+    src, dst, _ = _gicp_pair()
+    fs, fd = A.ComputeFpfh(src, ctx=ctx), A.ComputeFpfh(dst, ctx=ctx)
+    m = A.ComputeMatches(fs, fd, 2, ctx=ctx)
+    ofs, ofd = O.compute_fpfh(src), O.compute_fpfh(dst)
+    om, _ = O.compute_matches(ofs, ofd, 2)
+    # features equal to float rounding; a 33-D nearest neighbour among the
+    # near-identical features of a repetitive room flips for a few points
+    assert np.mean(m[:, 0] == om[:, 0]) >= 0.95
+    pairs, w = A.PruneMatchesLowe(m, fs, fd, 0.9)
+    T = np.eye(4, dtype=np.float32)
+    assert A.SolveKabsch(src, dst, pairs, w, T, ctx=ctx)
+    assert np.all(np.isfinite(T)) and abs(np.linalg.det(T[:3, :3]) - 1) < 1e-4
+    # on the same pruned correspondences the device Kabsch equals the oracle's
+    opairs, ow = A.PruneMatchesLowe(om, ofs, ofd, 0.9)
+    T2 = np.eye(4, dtype=np.float32)
+    assert A.SolveKabsch(src, dst, opairs, ow, T2, ctx=ctx)
+    ok, To = O.solve_kabsch(src, dst, opairs, ow)
+    assert ok
+    assert max(pose_err(T2, To)) <= 1e-4
+
+
+def test_fpfh_contract(ctx):
+    a = np.random.default_rng(0).normal(size=(100, 3)).astype(np.float32)
+    out = np.zeros((100, 33), np.float32)
+    vp = np.zeros(3, np.float32)
+    assert L.lib().rst_compute_fpfh(ctx.handle, L.fptr(a), 100, L.fptr(vp), 12, 0.5,
+                                    L.fptr(out)) == L.RST_E_ARG
+    assert L.lib().rst_compute_fpfh(ctx.handle, L.fptr(a), 100, L.fptr(vp), 16, 0.0,
+                                    L.fptr(out)) == L.RST_E_ARG
+    idx = np.zeros((100, 3), np.int32)
+    assert L.lib().rst_compute_matches(ctx.handle, L.fptr(out), 100, L.fptr(out), 100, 3,
+                                       L.iptr(idx), None) == L.RST_E_ARG

@@ -316,3 +316,23 @@ def test_accumulator_oracle_matches_numpy():
     for T, c in seq:
         acc.add(T, c)
     np.testing.assert_array_equal(acc.extract(), _accum_numpy(seq, 0.05))
+
+
+# ---- f3: FPFH oracle (fpfh.cpp:20-165,248-300) ----------------------------------
+def test_fpfh_oracle_histograms_and_matches():
+    src, dst, _ = _gicp_pair()
+    fs = O.compute_fpfh(src, radius=0.5)
+    h = fs.reshape(-1, 3, 11)
+    s = h.sum(-1)
+    # every point has neighbours at 0.5 m here: each histogram sums to 1
+    np.testing.assert_allclose(s, 1.0, atol=1e-5)
+    assert np.all(fs >= 0)
+    fd = O.compute_fpfh(dst, radius=0.5)
+    idx, d2 = O.compute_matches(fs, fd, 2)
+    # brute force in float64 agrees on the nearest (no near-ties at this size)
+    sub = fs[:200].astype(np.float64)
+    full = ((sub[:, None, :] - fd[None, :, :].astype(np.float64)) ** 2).sum(-1)
+    order = np.argsort(full, axis=1, kind="stable")[:, :2]
+    agree = np.mean(order[:, 0] == idx[:200, 0])
+    assert agree > 0.99
+    assert np.all(d2[:, 0] <= d2[:, 1])
