@@ -20,6 +20,8 @@ PROBE = r"""
 #include "rs_tracker/align/align_icp.hpp"
 #include "rs_tracker/common/point_cloud_utils.hpp"
 #include "rs_tracker/align/align_gicp.hpp"
+#include "rs_tracker/common/cloud_accumulator.hpp"
+#include "rs_tracker/common/fpfh.hpp"
 int main() {
   using namespace rs_tracker;
   Cloud3f two(2), many(50);
