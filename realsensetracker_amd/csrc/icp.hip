@@ -33,6 +33,18 @@ constexpr int kBS = 256;
 constexpr int kNP2Point = 16;  // sum w q u^T (9), sum w u (3), sum q (3), sum d2
 constexpr int kNP2Plane = 30;  // A (21), b (6), sum w r^2, count, sum d2
 constexpr int kFbBlocks = 2048;  // fixed grid of the fallback kernel (8192 waves)
+// From a queue of lane_min entries (IcpParams; 3/4 of the source points: the
+// cold first iteration, where most lanes' warm balls are not covered) the
+// fallback kernel gives every queued query one lane instead of one
+// wavefront: the per-lane exact search (rst_bvh.hpp search_from) issues 64x
+// fewer instructions per query.  Shorter queues hold the far points, whose
+// per-lane searches are long chains: the wave search wins there (measured).
+// Blocks of the fallback grid that hold queue entries (k_icp_fb writes their
+// slab rows, k_reduce_solve reads them):
+__device__ __forceinline__ int fb_blocks(int E, int grid, int lane_min) {
+  const int per = E >= lane_min ? kBS : kBS / kWave;
+  return max(1, min(grid, (E + per - 1) / per));
+}
 
 __device__ __forceinline__ Pose3 load_pose(const IcpState* __restrict__ st) {
   Pose3 P;
@@ -585,7 +597,7 @@ __global__ __launch_bounds__(kRedBS) void k_reduce_solve(const double* __restric
   if (Acc::kCanFinish && st->done) return;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   const int E = st->fb_e;
-  const int rows2 = max(1, min(rows2max, (E + kBS / kWave - 1) / (kBS / kWave)));
+  const int rows2 = fb_blocks(E, rows2max, prm.lane_min);
   const int t = threadIdx.x, col = t % RS;
   // unrolled so a thread's loads are all in flight before the first add
   // waits (a rolled loop pays one memory latency per row)
@@ -647,7 +659,7 @@ __global__ __launch_bounds__(kBS) void k_icp_fb(BvhView bv, AdjView av, AccArgs 
                                                 int32_t* __restrict__ nnpos,
                                                 const int32_t* __restrict__ qbuf,
                                                 const int32_t* __restrict__ qcnt, int nb1,
-                                                double* __restrict__ slab2) {
+                                                int lane_min, double* __restrict__ slab2) {
   extern __shared__ int pref[];  // [nb1 + 1]
   __shared__ double lds[(kBS / kWave) * Acc::NV];
   __shared__ WnnScratch wsc[kBS / kWave];
@@ -658,12 +670,40 @@ __global__ __launch_bounds__(kBS) void k_icp_fb(BvhView bv, AdjView av, AccArgs 
   queue_prefix(qcnt, nb1, pref, blockIdx.x == 0 ? st : nullptr);
   __syncthreads();
   const int E = pref[nb1];
-  const int nw = max(1, min((int)gridDim.x, (E + kBS / kWave - 1) / (kBS / kWave)));
-  if ((int)blockIdx.x >= nw) return;
+  if ((int)blockIdx.x >= fb_blocks(E, gridDim.x, lane_min)) return;
   double v[Acc::NV];
 #pragma unroll
   for (int k = 0; k < Acc::NV; ++k) v[k] = 0.0;
-  if (E > 0) {
+  if (E >= lane_min) {  // uniform: one lane per query, entries in order
+    const Uni u = load_uni(st);
+    const int T = gridDim.x * kBS;
+    for (int e = blockIdx.x * kBS + threadIdx.x; e < E; e += T) {
+      int lo = 0, hi = nb1 - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (pref[mid] <= e)
+          lo = mid;
+        else
+          hi = mid - 1;
+      }
+      const int i = qbuf[lo * (int64_t)kBS + (e - pref[lo])];
+      const float4 s = src[i];
+      float px, py, pz;
+      xform(u.P, s.x, s.y, s.z, px, py, pz);
+      const bool fin = finite3(px, py, pz);
+      int warm = nnpos[i];
+      if (fin && warm < 0) warm = morton_seed(bv, px, py, pz);
+      Best1 r;
+      r.init();
+      if (fin) {
+        const float4 w = bv.pts[warm];
+        r.offer(d2_ref(px, py, pz, w.x, w.y, w.z), f2i(w.w), warm);
+        search(bv, warm, px, py, pz, r);  // exact: warm leaf, then each ancestor's sibling
+      }
+      nnpos[i] = r.pos;
+      Acc::add(v, bv, aa, u, s, px, py, pz, r.d, r.pos, bv.pts[r.pos >= 0 ? r.pos : 0]);
+    }
+  } else if (E > 0) {
     const Uni u = load_uni(st);
     const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
     const int W = gridDim.x * (kBS / kWave);
@@ -864,6 +904,7 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
   prm.p2plane_max_d2 = opts.p2plane_max_dist > 0 ? opts.p2plane_max_dist * opts.p2plane_max_dist
                                                  : FLT_MAX;
   prm.max_iter = opts.max_iter;
+  prm.lane_min = (int)std::max<int64_t>(16384, (3 * n_local) / 4);
 
   const BvhView bv = view_of(tgt);
 
@@ -886,7 +927,8 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
                                                    nnpos, qbuf, qcnt, slab);
         if (tm) RST_HIP(hipEventRecord(ctx->ev[2 * it + 1], st));
         k_icp_fb<P2PlaneAcc><<<kFbBlocks, kBS, fb_lds, st>>>(bv, av, aa, src->pts, ctx->d_state,
-                                                             nnpos, qbuf, qcnt, nblk, slab2);
+                                                             nnpos, qbuf, qcnt, nblk,
+                                                             prm.lane_min, slab2);
         k_reduce_solve<P2PlaneAcc><<<1, kRedBS, 0, st>>>(slab, nblk, slab2, kFbBlocks, prm,
                                                          ctx->d_state, red_out);
       } else {
@@ -894,7 +936,8 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
                                                    nnpos, qbuf, qcnt, slab);
         if (tm) RST_HIP(hipEventRecord(ctx->ev[2 * it + 1], st));
         k_icp_fb<P2PointAcc><<<kFbBlocks, kBS, fb_lds, st>>>(bv, av, aa, src->pts, ctx->d_state,
-                                                             nnpos, qbuf, qcnt, nblk, slab2);
+                                                             nnpos, qbuf, qcnt, nblk,
+                                                             prm.lane_min, slab2);
         k_reduce_solve<P2PointAcc><<<1, kRedBS, 0, st>>>(slab, nblk, slab2, kFbBlocks, prm,
                                                          ctx->d_state, red_out);
       }

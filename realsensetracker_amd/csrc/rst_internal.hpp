@@ -80,6 +80,7 @@ struct IcpParams {
   float p2plane_mu;
   float p2plane_max_d2;
   int32_t max_iter;
+  int32_t lane_min;    // fallback queue length from which it runs one lane per query
 };
 
 }  // namespace rst
