@@ -683,6 +683,18 @@ RST_HD void scan_range_wide<Best1>(const BvhView& bv, int b, int n, float qx, fl
 // from the coverage test of the final leaf.
 constexpr int kWalkSteps = 1;
 
+// sqrt for the coverage / stop tests: the hardware v_sqrt_f32 (about 1 ulp)
+// on the device; every use carries the 1.00001 / 0.99999 margins of
+// rst_bvh.hpp adj_search, far wider than its error, so the tests stay
+// conservative (the correctly rounded sqrtf costs ~15 instructions per call)
+RST_HD float margin_sqrt(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_sqrtf(x);
+#else
+  return sqrtf(x);
+#endif
+}
+
 template <class R>
 RST_HD bool adj_search_wide(const BvhView& bv, const AdjView& av, int start,
                                                 float qx, float qy, float qz, R& r,
@@ -694,8 +706,8 @@ RST_HD bool adj_search_wide(const BvhView& bv, const AdjView& av, int start,
     const float4 lo = bv.nodes[2 * (nl + L)], hi = bv.nodes[2 * (nl + L) + 1];
     const float reach = av.reach[L];
     // same margins as rst_bvh.hpp adj_search
-    dl = sqrtf(box_d2(qx, qy, qz, lo, hi)) * 1.00001f;
-    if (dl + r.radius() * 1.00001f + 1e-30f < reach * 0.99999f) break;
+    dl = margin_sqrt(box_d2(qx, qy, qz, lo, hi)) * 1.00001f;
+    if (dl + margin_sqrt(r.bound()) * 1.00001f + 1e-30f < reach * 0.99999f) break;
     if (walked) *walked = step + 1;
     if (step == kWalkSteps) return false;
     // walk: scan the listed leaf nearest to the query (other than L)
@@ -723,11 +735,14 @@ RST_HD bool adj_search_wide(const BvhView& bv, const AdjView& av, int start,
       h[j] = e[2 * (k0 + j) + 1];
     }
     bool stop = false;
+    // the batch's stop radius from the bound at its start: the bound only
+    // shrinks, so a later entry tested against it stops no earlier (exact)
+    const float rad = margin_sqrt(r.bound()) * 1.00001f + 1e-30f;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       if (stop) break;
       const int tag = f2i(h[j].w);
-      if (tag < 0 || l[j].w * 0.99999f - dl > r.radius() * 1.00001f + 1e-30f) {
+      if (tag < 0 || l[j].w * 0.99999f - dl > rad) {
         stop = true;
       } else if (box_d2(qx, qy, qz, l[j], h[j]) <= r.bound()) {
         scan_range_wide(bv, tag >> 5, tag & 31, qx, qy, qz, r);
