@@ -22,6 +22,14 @@ FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE).  Multi-GPU: one process per GP
 stream (frame pairs are independent; no data-path collective) -> weak
 scaling; barrier + max-over-ranks timing.
 
+Other BASELINE configs (extra bench lines, same JSON contract):
+    --width 1280 --height 720     configs[2]: the stream at 720p
+    --workload pyramid            configs[4]: 3-level coarse-to-fine ICP on a
+                                  1280x720 stream, pose chained on the device
+    --workload sharded            configs[3]: a 1000x1000 (~1M-point) pair, the
+                                  source sharded over the ranks, one RCCL
+                                  all-reduce per iteration (strong scaling)
+
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
 """
@@ -47,6 +55,8 @@ from realsensetracker_amd import align as A  # noqa: E402
 from realsensetracker_amd import driver  # noqa: E402
 
 METRIC = "ICP iterations/sec + frames/sec, 640×480 RGB-D, 1/2/4/8 MI355X"
+# workload -> default frame size (BASELINE.json configs[1] / [4] / [3])
+WORKLOADS = {"stream": (640, 480), "pyramid": (1280, 720), "sharded": (1000, 1000)}
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
@@ -115,13 +125,107 @@ def load_traffic():
         return None
 
 
+def p2point_alg_bytes(n: float, m: float) -> float:
+    """SURVEY.md §8d fused P2POINT iteration: 12 n + 12 m + S_idx, S_idx =
+    leaf boxes (64 B) + leaf ranges (4 B) of the power-of-two leaf count."""
+    nleaves = 1
+    while nleaves * 16 < m:
+        nleaves *= 2
+    return 12 * n + 12 * m + 64 * nleaves + 4 * (nleaves + 1)
+
+
+def run_sharded(a, K, frames, d_depth, hip, world, rank, local, dist, barrier, max_over_ranks):
+    """configs[3]: one large scan pair (default 1000x1000 depth, ~1M points),
+    the source sharded across the ranks (contiguous point ranges), the target
+    index replicated; per iteration one RCCL all-reduce of the 16 fp64
+    partial sums over xGMI (rst_icp_align_sharded_device).  A step = one
+    AlignIcp3d of the pair (128 iterations); total work is fixed as N grows
+    (strong scaling), value = the pair's ICP iterations/s."""
+    from realsensetracker_amd.shard import ShardedAligner, shard_bounds
+    ctx = A.Context(local)
+    tgt = A.Target.from_depth_device(d_depth[0].value, K, 0, ctx)
+    npx = a.width * a.height
+    d_src = C.c_void_p()
+    assert hip.hipMalloc(C.byref(d_src), C.c_size_t(12 * npx)) == 0
+    n = C.c_int64(0)
+    L.check(L.lib().rst_unproject_device(ctx.handle, d_depth[1], C.byref(K), 0, d_src,
+                                         C.byref(n)), "rst_unproject_device")
+    lo, hi = shard_bounds(n.value, world, rank)
+    sh = ShardedAligner(ctx) if dist is not None else ShardedAligner(ctx, world=1, rank=0)
+    opts = L.default_opts(max_iter=a.iters)
+    ptr = d_src.value + 12 * lo
+
+    def step():
+        ok, pose, _ = sh.align(ptr, hi - lo, tgt, opts)
+        return ok, pose
+
+    for _ in range(a.warmup):
+        step()
+    ctx.enable_kernel_timing(8)
+    kms, kl, oks = 0.0, 0, 0
+    barrier()
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        ok, pose = step()
+        oks += int(ok)
+        ms, nl = ctx.last_kernel_time()
+        kms += ms * nl
+        kl += nl
+    ctx.synchronize()
+    barrier()
+    dt = max_over_ranks(time.perf_counter() - t0)
+    ctx.enable_kernel_timing(0)
+    avg_ms = kms / max(1, kl)
+    alg = p2point_alg_bytes(hi - lo, len(tgt))
+    achieved = alg / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    if rank == 0:
+        cpu = None if a.no_cpu or world > 1 else cpu_baseline(a.width, a.height, a.cpu_iters)
+        value = a.steps * a.iters / dt
+        out = {
+            "metric": METRIC, "value": value, "unit": "ICP iterations/s", "n_gpus": world,
+            "steps": a.steps, "warmup": a.warmup, "ms_per_step": 1000.0 * dt / a.steps,
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (seeded procedural room, ray-cast u16 depth, 1 mm noise, "
+                    "~3% invalid)",
+            "config": {"workload": f"{a.width}x{a.height} scan pair ({n.value} source points), "
+                                   f"AlignIcp3d P2POINT_REF {a.iters} iters, source sharded "
+                                   f"over {world} rank(s), one RCCL all-reduce of 16 fp64 "
+                                   f"per iteration",
+                       "width": a.width, "height": a.height, "iters_per_pair": a.iters,
+                       "points_per_frame": n.value, "target_points": len(tgt),
+                       "accumulation": "fp64 partial sums", "parallelism": f"shard{world}"},
+            "frames_per_s": a.steps / dt, "pairs_ok": oks,
+            "final_pose_t": [float(x) for x in pose[:3, 3]],
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "k_icp_nn", "avg_us": 1000.0 * avg_ms,
+                         "alg_bytes_per_launch": alg},
+            "cpu_baseline": cpu,
+        }
+        if cpu is not None:
+            out["speedup_vs_cpu_baseline"] = value / cpu["value"]
+        print(json.dumps(out))
+    sh.close()
+    tgt.free()
+    hip.hipFree(d_src)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--width", type=int, default=640)
-    ap.add_argument("--height", type=int, default=480)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="stream",
+                    help="stream: configs[1] (configs[2] with --width 1280 --height 720); "
+                         "pyramid: configs[4]; sharded: configs[3]")
+    ap.add_argument("--width", type=int, default=0, help="0: the workload's default")
+    ap.add_argument("--height", type=int, default=0)
+    ap.add_argument("--levels", type=int, default=3, help="pyramid levels (stride 2^l)")
+    ap.add_argument("--pyr-iters", default="32,32,64",
+                    help="pyramid: P2POINT_REF iterations per level, finest first")
     ap.add_argument("--frames", type=int, default=0,
                     help="distinct frames per rank (0: one per step, at most 512)")
     ap.add_argument("--stride", type=int, default=1, help="trajectory frames between frames")
@@ -134,6 +238,12 @@ def main():
     ap.add_argument("--inflight", type=int, default=2,
                     help="frame pairs in flight per GPU (one HIP stream each)")
     a = ap.parse_args()
+    dw, dh = WORKLOADS[a.workload]
+    a.width, a.height = a.width or dw, a.height or dh
+    pyr = a.workload == "pyramid"
+    pyr_iters = [int(x) for x in a.pyr_iters.split(",")] if pyr else [a.iters]
+    if pyr and len(pyr_iters) != a.levels:
+        ap.error("--pyr-iters needs one count per level")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -165,6 +275,8 @@ def main():
 
     K = driver.intrinsics(a.width, a.height)
     nfr = max(2, a.frames if a.frames > 0 else min(512, max(a.steps, a.warmup) + 1))
+    if a.workload == "sharded":
+        nfr = 2  # one pair, aligned every step
     frames = render_frames(seed=rank, n=nfr, K=K, stride=a.stride)
     # depth frames resident in HBM before timing (hipMalloc'd via ctypes)
     hip = C.CDLL("libamdhip64.so")
@@ -177,6 +289,10 @@ def main():
         assert hip.hipMemcpy(p, f.ctypes.data_as(C.c_void_p), C.c_size_t(2 * npx), 1) == 0
         d_depth.append(p)
 
+    if a.workload == "sharded":
+        return run_sharded(a, K, frames, d_depth, hip, world, rank, local, dist, barrier,
+                           max_over_ranks)
+
     opts_ref = L.default_opts(max_iter=a.iters)
     opts_pl = L.default_opts(mode=L.RST_P2PLANE, max_iter=30)
     # frame preparation on its own context (stream); each frame pair in
@@ -188,33 +304,48 @@ def main():
     def run(nsteps: int, opts, normals_k: int, stats: dict | None):
         pending = deque()
 
+        def prep(f):  # frame -> its level targets (one level unless pyramid)
+            if pyr:
+                return A.Target.pyramid_from_depth_device(d_depth[f].value, K, a.levels,
+                                                          normals_k, pctx)
+            return [A.Target.from_depth_device(d_depth[f].value, K, normals_k, pctx)]
+
         def finish_one():
             pa, c, cur, tgt = pending.popleft()
             r = pa.wait()
             if stats is not None:
-                stats["iters"] += r.iterations
-                stats["n"] += len(cur)
-                stats["m"] += len(tgt)
+                # pyramid P2POINT_REF: every level runs its fixed count
+                stats["iters"] += r.iterations + (sum(lv_iters[1:]) if pyr and
+                                                  opts.mode == L.RST_P2POINT_REF else 0)
+                stats["n"] += len(cur[0])
+                stats["m"] += len(tgt[0])
                 stats["ok"] += int(r.ok)
                 ms, nl = c.last_kernel_time()
                 stats["kernel_ms"] += ms * nl
                 stats["launches"] += nl
-            tgt.free()  # frame f: target of pair f, source of pair f-1 (done)
+            for t in tgt:  # frame f: target of pair f, source of pair f-1 (done)
+                t.free()
 
-        prev = A.Target.from_depth_device(d_depth[0].value, K, normals_k, pctx)
+        lv_iters = pyr_iters if opts.mode == L.RST_P2POINT_REF else [opts.max_iter] * a.levels
+        prev = prep(0)
         k = 1
         for s in range(nsteps):
-            cur = A.Target.from_depth_device(d_depth[pingpong(k, nfr)].value, K, normals_k, pctx)
+            cur = prep(pingpong(k, nfr))
             if len(pending) == len(actx):
                 finish_one()
             c = actx[s % len(actx)]
             # AlignIcp3d(curr, prev, 128, &xfm), xfm = Identity (rs_replay_app.cpp:235,251)
-            pending.append((A.align_prepared_async(cur, prev, c, None, opts), c, cur, prev))
+            if pyr:
+                pa = A.align_pyramid_async(cur, prev, c, lv_iters, None, opts)
+            else:
+                pa = A.align_prepared_async(cur[0], prev[0], c, None, opts)
+            pending.append((pa, c, cur, prev))
             prev = cur
             k += 1
         while pending:
             finish_one()
-        prev.free()
+        for t in prev:
+            t.free()
 
     def timing(on: bool):
         for c in actx:  # HIP events around k_icp_nn on every 8th iteration
@@ -263,7 +394,7 @@ def main():
     # AlignIcp3d(src, dst, 128, &T) on host clouds, one pair at a time: PCIe
     # upload of both clouds + index build + 128 iterations + pose readback
     host = None
-    if not a.no_host_api:
+    if not a.no_host_api and not pyr:
         clouds = [driver.unproject(frames[pingpong(k, nfr)], K) for k in range(4)]
         T = np.eye(4, dtype=np.float32)
         A.AlignIcp3d(clouds[1], clouds[0], a.iters, T)  # warm the context's pools
@@ -281,7 +412,7 @@ def main():
     # per frame: DownsampleVoxel(curr, 0.1); ComputeAlignment(prev, curr, &T)
     # (16 rounds of exact NN + LM), host clouds, one pair at a time
     gicp = None
-    if not a.no_gicp:
+    if not a.no_gicp and not pyr:
         clouds = [A.DownsampleVoxel(driver.unproject(frames[pingpong(k, nfr)], K), 0.1)
                   for k in range(4)]
         T = np.eye(4, dtype=np.float32)
@@ -302,13 +433,10 @@ def main():
     avg_ms = st["kernel_ms"] / max(1, st["launches"])
     n_avg = st["n"] / max(1, a.steps)
     m_avg = st["m"] / max(1, a.steps)
-    nleaves = 1
-    while nleaves * 16 < m_avg:
-        nleaves *= 2
-    s_idx = 64 * nleaves + 4 * (nleaves + 1)
-    alg_bytes = 12 * n_avg + 12 * m_avg + s_idx  # SURVEY.md §8d fused P2POINT iteration
+    alg_bytes = p2point_alg_bytes(n_avg, m_avg)
     achieved = alg_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-    traffic = load_traffic()
+    # the committed PMC pass is of the default workload only
+    traffic = load_traffic() if (a.workload, a.width, a.height) == ("stream", 640, 480) else None
 
     if rank != 0:
         if dist is not None:
@@ -324,10 +452,16 @@ def main():
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic (seeded procedural RGB-D room, ray-cast u16 depth, 1 mm noise, "
                 "~3% invalid)",
-        "config": {"workload": f"{a.width}x{a.height} synthetic RGB-D stream, per frame: "
-                               f"unproject + index build + AlignIcp3d P2POINT_REF "
-                               f"{a.iters} iters (reference loop)",
-                   "width": a.width, "height": a.height, "iters_per_pair": a.iters,
+        "config": {"workload": (f"{a.width}x{a.height} synthetic RGB-D stream, per frame: "
+                                f"{a.levels}-level pyramid (stride 2^l) unproject + index "
+                                f"builds, coarse-to-fine P2POINT_REF ICP, iterations per "
+                                f"level {pyr_iters} (finest first), pose chained on the device"
+                                if pyr else
+                                f"{a.width}x{a.height} synthetic RGB-D stream, per frame: "
+                                f"unproject + index build + AlignIcp3d P2POINT_REF "
+                                f"{a.iters} iters (reference loop)"),
+                   "width": a.width, "height": a.height,
+                   "iters_per_pair": sum(pyr_iters) if pyr else a.iters,
                    "points_per_frame": round(n_avg), "frames_cycled": nfr,
                    "accumulation": "fp64 partial sums", "parallelism": f"replica{world}",
                    "pairs_in_flight_per_gpu": len(actx)},

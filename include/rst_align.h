@@ -173,6 +173,22 @@ int rst_icp_align_prepared_async(rst_ctx* ctx, const rst_target* src,
 int rst_icp_align_wait(rst_ctx* ctx, float pose_inout[16], float* mean_cost,
                        int32_t* iterations_run);
 
+/* Coarse-to-fine ICP over pyramid levels (BASELINE configs[4]; the
+ * reference has no pyramid): level 0 is the finest, nlevels-1 the coarsest.
+ * Runs levels nlevels-1 .. 0, iters[l] iterations each, every level starting
+ * from the previous level's pose -- chained on the device, so the whole
+ * pyramid is enqueued at once.  Equivalent to calling
+ * rst_icp_align_prepared(src[l], tgt[l], opts{max_iter = iters[l]}, pose)
+ * coarsest first with one pose array (a level whose early false leaves the
+ * pose untouched is skipped the same way).  RST_FALSE, nothing enqueued,
+ * when level 0 has < 3 source or target points (< 6 source points for
+ * RST_P2PLANE); _wait then reports it too.  Finish with rst_icp_align_wait
+ * (level 0's result; iterations_run = level 0's). */
+int rst_icp_align_pyramid_async(rst_ctx* ctx, const rst_target* const* src,
+                                const rst_target* const* tgt, int nlevels,
+                                const int32_t* iters, const rst_icp_opts* opts,
+                                const float pose_in[16]);
+
 /* The per-iteration solve of AlignIcp3d / SolveKabsch (align_icp.cpp:58-69,
  * 139-151) run by the device solve kernel on a given fp64 cross-covariance
  * (column-major) and float means: R = float(U V^T), R.col(2) *= -1 when
@@ -210,6 +226,21 @@ int rst_unproject_device(rst_ctx* ctx, const uint16_t* d_depth,
 int rst_frame_prepare_device(rst_ctx* ctx, const uint16_t* d_depth,
                              const rst_intrinsics* K, int normals_k,
                              rst_target** out);
+/* Decimated deprojection (coarse-to-fine pyramid, BASELINE configs[4]; no
+ * reference counterpart): every stride-th pixel of every stride-th row,
+ * i.e. pixel (stride*ul, stride*vl) deprojected with the full image's
+ * intrinsics K, so the points are exactly the level-0 points of those
+ * pixels.  stride 1 = rst_unproject_device. */
+int rst_unproject_strided_device(rst_ctx* ctx, const uint16_t* d_depth,
+                                 const rst_intrinsics* K, int stride,
+                                 int keep_invalid, float* d_xyz_out,
+                                 int64_t* n_out);
+/* rst_frame_prepare_device for levels 0..nlevels-1 (stride 2^l) of one
+ * depth frame: out_levels[l] receives level l's target handle (all freed
+ * and NULL on error). */
+int rst_frame_prepare_pyramid_device(rst_ctx* ctx, const uint16_t* d_depth,
+                                     const rst_intrinsics* K, int nlevels,
+                                     int normals_k, rst_target** out_levels);
 
 /* ---- cloud preprocessing the callers run before AlignIcp3d -------------- */
 /* RemoveNans (point_cloud_utils.cpp:163-174): keep the points whose three

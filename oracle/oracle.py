@@ -59,6 +59,7 @@ def lib():
         L.orc_p2point_partials.argtypes = [_f, C.c_int64, P, _f, _f, _f, C.c_float, _d]
         L.orc_compute_normals.argtypes = [_f, C.c_int64, P, C.c_int, _f, _f]
         L.orc_unproject.restype = C.c_int64
+        L.orc_unproject_strided.restype = C.c_int64
         L.orc_remove_nans.argtypes = [_f, C.c_int64, _f]
         L.orc_remove_nans.restype = C.c_int64
         L.orc_downsample_voxel.argtypes = [_f, C.c_int64, C.c_float, _f]
@@ -80,6 +81,8 @@ def lib():
         L.orc_accum_extract.restype = C.c_int64
         L.orc_accum_extract.argtypes = [P, _f]
         L.orc_unproject.argtypes = [_u16, C.c_int, C.c_int, _f, C.c_float, C.c_int, _f]
+        L.orc_unproject_strided.argtypes = [_u16, C.c_int, C.c_int, C.c_int, _f, C.c_float,
+                                            C.c_int, _f]
         L.orc_align_p2plane.restype = C.c_int
         L.orc_align_p2plane.argtypes = [_f, C.c_int64, _f, _f, C.c_int64, P, C.c_int,
                                         C.c_float, C.c_float, C.c_float, _f, _f]
@@ -231,13 +234,30 @@ def compute_normals(cloud, k=16, viewpoint=(0, 0, 0), tree: KDTree | None = None
     return out
 
 
-def unproject(depth, K4, depth_scale=0.001, keep_invalid=False):
+def unproject(depth, K4, depth_scale=0.001, keep_invalid=False, stride=1):
+    """Pinhole deprojection; stride > 1 = pyramid level (every stride-th
+    pixel of every stride-th row, full-image intrinsics)."""
     d = np.ascontiguousarray(depth, np.uint16)
     h, w = d.shape
     out = np.zeros((h * w, 3), np.float32)
-    n = lib().orc_unproject(d.ctypes.data_as(_u16), w, h, _fp(np.asarray(K4, np.float32)),
-                            depth_scale, int(keep_invalid), _fp(out))
+    n = lib().orc_unproject_strided(d.ctypes.data_as(_u16), w, h, int(stride),
+                                    _fp(np.asarray(K4, np.float32)), C.c_float(depth_scale),
+                                    int(keep_invalid), _fp(out))
     return out[:n].copy()
+
+
+def align_icp_pyramid(src_levels, dst_levels, iters, T=None, sum_mode: int = 0):
+    """Coarse-to-fine chain of the AlignIcp3d restatement (BASELINE
+    configs[4]; the reference has no pyramid): levels finest first, run
+    coarsest first, one pose array passed through every level (a level's
+    early false leaves it untouched).  Returns (ok, pose, mean_cost) of
+    level 0."""
+    T = np.eye(4, dtype=np.float32) if T is None else np.asarray(T, np.float32)
+    ok, mc = False, 0.0
+    for lv in reversed(range(len(src_levels))):
+        ok, T, mc, _ = align_icp(src_levels[lv], dst_levels[lv], iters[lv], T=T,
+                                 sum_mode=sum_mode)
+    return ok, T, mc
 
 
 def remove_nans(cloud):

@@ -916,10 +916,18 @@ void orc_compute_normals(const float* xyz, int64_t m, const orc_kdtree* tree,
  *   x = (u - ppx)/fx; y = (v - ppy)/fy; P = (z*x, z*y, z), z = scale*d. */
 int64_t orc_unproject(const uint16_t* depth, int w, int h, const float K[4],
                       float depth_scale, int keep_invalid, float* xyz) {
+  return orc_unproject_strided(depth, w, h, 1, K, depth_scale, keep_invalid, xyz);
+}
+
+/* Pyramid level of stride s (BASELINE configs[4]; no reference
+ * counterpart): pixels (u, v) with u % s == 0 and v % s == 0, row-major,
+ * deprojected with the full image's intrinsics. */
+int64_t orc_unproject_strided(const uint16_t* depth, int w, int h, int s, const float K[4],
+                              float depth_scale, int keep_invalid, float* xyz) {
   const float fx = K[0], fy = K[1], cx = K[2], cy = K[3];
   int64_t k = 0;
-  for (int v = 0; v < h; ++v)
-    for (int u = 0; u < w; ++u) {
+  for (int v = 0; v < h; v += s)
+    for (int u = 0; u < w; u += s) {
       const uint16_t d = depth[(int64_t)v * w + u];
       if (d == 0 && !keep_invalid) continue;
       const float z = depth_scale * (float)d;

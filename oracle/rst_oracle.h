@@ -131,6 +131,8 @@ void orc_compute_normals(const float* xyz, int64_t m, const orc_kdtree* tree,
  * NaN->0 mapping) when keep_invalid, else dropped.  Returns point count. */
 int64_t orc_unproject(const uint16_t* depth, int w, int h, const float K[4],
                       float depth_scale, int keep_invalid, float* xyz);
+int64_t orc_unproject_strided(const uint16_t* depth, int w, int h, int s, const float K[4],
+                              float depth_scale, int keep_invalid, float* xyz);
 
 /* ---- common/RemoveNans (point_cloud_utils.cpp:163-174) ----------------- */
 /* Finite points in input order; returns the count (out holds >= n). */

@@ -76,11 +76,15 @@ PROTOTYPES = {
                                    c_float_p, C.c_int64, c_float_p]),
     "rst_icp_align_prepared_async": (C.c_int, [_P, _P, _P, C.POINTER(IcpOpts), c_float_p]),
     "rst_icp_align_wait": (C.c_int, [_P, c_float_p, c_float_p, c_int32_p]),
+    "rst_icp_align_pyramid_async": (C.c_int, [_P, C.POINTER(_P), C.POINTER(_P), C.c_int,
+                                              c_int32_p, C.POINTER(IcpOpts), c_float_p]),
     "rst_compute_centroid": (C.c_int, [_P, c_float_p, C.c_int64, c_float_p]),
     "rst_kabsch_solve": (C.c_int, [_P, C.POINTER(C.c_double), c_float_p, c_float_p, c_float_p]),
     "rst_unproject": (C.c_int, [_P, c_u16_p, C.POINTER(Intrinsics), C.c_int, c_float_p,
                                 c_int64_p]),
     "rst_unproject_device": (C.c_int, [_P, _P, C.POINTER(Intrinsics), C.c_int, _P, c_int64_p]),
+    "rst_unproject_strided_device": (C.c_int, [_P, _P, C.POINTER(Intrinsics), C.c_int, C.c_int,
+                                               _P, c_int64_p]),
     "rst_remove_nans": (C.c_int, [_P, c_float_p, C.c_int64, c_float_p, c_int64_p]),
     "rst_remove_nans_device": (C.c_int, [_P, _P, C.c_int64, _P, c_int64_p]),
     "rst_downsample_voxel": (C.c_int, [_P, c_float_p, C.c_int64, C.c_float, c_float_p,
@@ -104,6 +108,8 @@ PROTOTYPES = {
                                  C.c_int, c_float_p, C.POINTER(C.c_double)]),
     "rst_frame_prepare_device": (C.c_int, [_P, _P, C.POINTER(Intrinsics), C.c_int,
                                            C.POINTER(_P)]),
+    "rst_frame_prepare_pyramid_device": (C.c_int, [_P, _P, C.POINTER(Intrinsics), C.c_int,
+                                                   C.c_int, C.POINTER(_P)]),
     "rst_scene_create": (C.c_int, [C.c_uint64, C.POINTER(_P)]),
     "rst_scene_destroy": (C.c_int, [_P]),
     "rst_scene_render_depth": (C.c_int, [_P, c_float_p, C.POINTER(Intrinsics), C.c_uint64,

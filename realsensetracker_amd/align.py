@@ -125,6 +125,19 @@ class Target:
                 "rst_frame_prepare_device")
         return cls(h, ctx)
 
+    @classmethod
+    def pyramid_from_depth_device(cls, d_depth_ptr: int, K: "L.Intrinsics", nlevels: int,
+                                  normals_k: int = 0,
+                                  ctx: Context | None = None) -> "list[Target]":
+        """Targets of pyramid levels 0..nlevels-1 of one depth frame (level l:
+        every 2^l-th pixel of every 2^l-th row, full-image intrinsics)."""
+        ctx = ctx or get_context()
+        hs = (C.c_void_p * nlevels)()
+        L.check(L.lib().rst_frame_prepare_pyramid_device(ctx.handle, C.c_void_p(d_depth_ptr),
+                                                         C.byref(K), nlevels, normals_k, hs),
+                "rst_frame_prepare_pyramid_device")
+        return [cls(C.c_void_p(hs[l]), ctx) for l in range(nlevels)]
+
     @property
     def handle(self):
         return self._h
@@ -266,6 +279,34 @@ def align_prepared_async(src: Target, target: Target, ctx: Context, pose=None,
                                                  C.byref(o), L.fptr(L.pose_to_cm(pose))),
             "rst_icp_align_prepared_async")
     return p
+
+
+def align_pyramid_async(src_levels, tgt_levels, ctx: Context, iters, pose=None,
+                        opts: "L.IcpOpts | None" = None) -> PendingAlign:
+    """Enqueue the coarse-to-fine ICP (rst_icp_align_pyramid_async): levels
+    are finest first; runs coarsest -> finest, iters[l] iterations at level
+    l, the pose chained on the device.  .wait() -> level 0's IcpResult."""
+    nl = len(src_levels)
+    if len(tgt_levels) != nl or len(iters) != nl or nl < 1:
+        raise ValueError("src_levels, tgt_levels and iters need one entry per level")
+    pose = np.eye(4, dtype=np.float32) if pose is None else np.asarray(pose, np.float32)
+    o = opts if opts is not None else L.default_opts()
+    sh = (C.c_void_p * nl)(*[t.handle.value for t in src_levels])
+    th = (C.c_void_p * nl)(*[t.handle.value for t in tgt_levels])
+    it = np.ascontiguousarray(iters, np.int32)
+    p = PendingAlign(ctx, pose, (list(src_levels), list(tgt_levels)))
+    L.check(L.lib().rst_icp_align_pyramid_async(ctx.handle, sh, th, nl,
+                                                it.ctypes.data_as(L.c_int32_p), C.byref(o),
+                                                L.fptr(L.pose_to_cm(pose))),
+            "rst_icp_align_pyramid_async")
+    return p
+
+
+def align_pyramid(src_levels, tgt_levels, iters, pose=None,
+                  opts: "L.IcpOpts | None" = None) -> IcpResult:
+    """Blocking align_pyramid_async on the targets' context."""
+    return align_pyramid_async(src_levels, tgt_levels, tgt_levels[0].ctx, iters, pose,
+                               opts).wait()
 
 
 def AlignIcp3d(src, dst, *args, opts: "L.IcpOpts | None" = None) -> bool:

@@ -495,6 +495,43 @@ int rst_icp_align_prepared_async(rst_ctx* ctx, const rst_target* src, const rst_
   return s;
 }
 
+int rst_icp_align_pyramid_async(rst_ctx* ctx, const rst_target* const* src,
+                                const rst_target* const* tgt, int nlevels, const int32_t* iters,
+                                const rst_icp_opts* opts, const float pose_in[16]) {
+  if (!ctx || !src || !tgt || !iters || !pose_in || nlevels < 1 || nlevels > 16) return RST_E_ARG;
+  for (int l = 0; l < nlevels; ++l)
+    if (!src[l] || !tgt[l] || iters[l] < 0) return RST_E_ARG;
+  if (ctx->pend.active) return RST_E_STATE;
+  RST_HIP(hipSetDevice(ctx->device));
+  rst_icp_opts o;
+  if (opts)
+    o = *opts;
+  else
+    rst_icp_opts_default(&o);
+  // level 0 decides the result: its early false (align_icp.cpp:77-79) means
+  // nothing to run; _wait reports it with the pose untouched
+  if (src[0]->m < 3 || tgt[0]->m < 3 || (o.mode == RST_P2PLANE && src[0]->m < 6)) {
+    ctx->pend = {};
+    ctx->pend.active = true;
+    ctx->pend.early_false = true;
+    return RST_FALSE;
+  }
+  bool chained = false;  // a solve has been enqueued on the context's state
+  for (int l = nlevels - 1; l >= 0; --l) {
+    o.max_iter = iters[l];
+    const int s = icp_launch(ctx, src[l], tgt[l], &o, pose_in, nullptr, chained);
+    if (s == RST_FALSE) continue;  // early false: the pose passes through (level 0 excluded above)
+    if (s != RST_OK) {
+      ctx->pend = {};
+      hipStreamSynchronize(ctx->stream);
+      return s;
+    }
+    chained = true;
+  }
+  ctx->pend.pyramid = true;
+  return RST_OK;
+}
+
 int rst_icp_align_wait(rst_ctx* ctx, float pose_inout[16], float* mean_cost,
                        int32_t* iterations_run) {
   if (!ctx || !pose_inout) return RST_E_ARG;

@@ -122,9 +122,12 @@ struct InitArgs {
   float pose[16];
   float mu0;
   int32_t need_centroid;
+  int32_t chain;  // pyramid: start from the pose the previous solve on this state left
 };
 
-// State initialisation: pose from the caller, mu0, centroid = fp64 sum / n
+// State initialisation: pose from the caller (or, chained, the previous
+// solve's result: its pose, or its initial pose when it failed -- what
+// icp_finish would hand back), mu0, centroid = fp64 sum / n
 // rounded to float (reference: fp32 sequential sum * float(1.0/n),
 // point_cloud_utils.cpp:92-98; DESIGN.md "Numerics").
 __global__ __launch_bounds__(kBS) void k_init_state(const double* __restrict__ cslab, int rows,
@@ -133,14 +136,23 @@ __global__ __launch_bounds__(kBS) void k_init_state(const double* __restrict__ c
   __shared__ double tot[4];
   if (a.need_centroid) reduce_slab_rows<4>(cslab, rows, cslab, 0, nullptr, red, tot);
   if (threadIdx.x == 0) {
+    float P[12];  // R col-major, t
     for (int c = 0; c < 3; ++c)
-      for (int r = 0; r < 3; ++r) {
-        st->R[c * 3 + r] = a.pose[c * 4 + r];
-        st->Rd[c * 3 + r] = a.pose[c * 4 + r];
-      }
+      for (int r = 0; r < 3; ++r) P[c * 3 + r] = a.pose[c * 4 + r];
+    for (int r = 0; r < 3; ++r) P[9 + r] = a.pose[12 + r];
+    if (a.chain) {
+      const bool failed = st->fail != 0;
+      for (int k = 0; k < 9; ++k) P[k] = failed ? st->in_pose[k] : st->R[k];
+      for (int k = 0; k < 3; ++k) P[9 + k] = failed ? st->in_pose[9 + k] : st->t[k];
+    }
+    for (int k = 0; k < 12; ++k) st->in_pose[k] = P[k];
+    for (int k = 0; k < 9; ++k) {
+      st->R[k] = P[k];
+      st->Rd[k] = P[k];
+    }
     for (int r = 0; r < 3; ++r) {
-      st->t[r] = a.pose[12 + r];
-      st->td[r] = a.pose[12 + r];
+      st->t[r] = P[9 + r];
+      st->td[r] = P[9 + r];
     }
     if (a.need_centroid) {
       const double n = tot[3] > 0 ? tot[3] : 1.0;
@@ -810,7 +822,8 @@ int centroid_device(rst_ctx* ctx, const float4* d_pts, int64_t n, double* d_out)
 // when enqueued, RST_FALSE for the reference's early false (nothing
 // enqueued), or an error.
 int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
-               const rst_icp_opts* opts_in, const float pose_in[16], rst_comm* comm) {
+               const rst_icp_opts* opts_in, const float pose_in[16], rst_comm* comm,
+               bool chain) {
   if (!ctx || !src || !tgt || !pose_in) return RST_E_ARG;
   ctx->pend = {};
   rst_icp_opts opts;
@@ -857,6 +870,7 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
   memcpy(ia.pose, pose_in, sizeof(ia.pose));
   ia.mu0 = opts.mu0;
   ia.need_centroid = p2plane ? 0 : 1;
+  ia.chain = chain ? 1 : 0;
   int crows = 0;
   if (!p2plane) {
     if (n_local > 0) {
@@ -986,9 +1000,17 @@ int icp_finish(rst_ctx* ctx, float pose_inout[16], float* mean_cost, int32_t* it
   const IcpState& h = *ctx->h_state;
   if (pd.p2plane && h.fail) {
     if (iters_run) *iters_run = h.iter;
+    if (pd.pyramid) {  // the pose level 0 started from (the coarser levels' result)
+      for (int c = 0; c < 3; ++c) {
+        for (int r = 0; r < 3; ++r) pose_inout[c * 4 + r] = h.in_pose[c * 3 + r];
+        pose_inout[c * 4 + 3] = 0.f;
+      }
+      for (int r = 0; r < 3; ++r) pose_inout[12 + r] = h.in_pose[9 + r];
+      pose_inout[15] = 1.f;
+    }
     return RST_FALSE;
   }
-  if (pd.max_iter > 0 || pd.p2plane) {
+  if (pd.max_iter > 0 || pd.p2plane || pd.pyramid) {  // (a pyramid's coarse levels moved it)
     for (int c = 0; c < 3; ++c) {
       for (int r = 0; r < 3; ++r) pose_inout[c * 4 + r] = h.R[c * 3 + r];
       pose_inout[c * 4 + 3] = 0.f;

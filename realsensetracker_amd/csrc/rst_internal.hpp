@@ -68,6 +68,8 @@ struct IcpCore {
 };
 
 struct IcpState : IcpCore {
+  float in_pose[12];      // the solve's initial pose (R col-major, t): a pyramid
+                          // level that fails chains this on (host semantics)
   int32_t qlen[kQTrace];  // fallback-queue length per iteration (diagnostics)
   int32_t path[kQTrace][4];  // per-iteration diagnostics (rst_debug_queue_trace)
 };
@@ -117,7 +119,7 @@ struct rst_ctx {
     bool active = false;
     bool p2plane = false;
     bool timing = false;
-  int timing_stride = 1;              // time every timing_stride-th iteration
+    bool pyramid = false;  // rst_icp_align_pyramid_async: a failed level 0 hands back its input
     int32_t max_iter = 0;
     int64_t n_total = 0;
   } pend;
@@ -183,7 +185,8 @@ int compute_normals(rst_ctx* ctx, rst_target* tgt, int k, const float vp[3]);
 
 // ICP (icp.hip)
 int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
-               const rst_icp_opts* opts, const float pose_in[16], rst_comm* comm);
+               const rst_icp_opts* opts, const float pose_in[16], rst_comm* comm,
+               bool chain = false);
 int icp_finish(rst_ctx* ctx, float pose_inout[16], float* mean_cost, int32_t* iters_run);
 int icp_align_prepared(rst_ctx* ctx, const rst_target* src,
                        const rst_target* tgt, const rst_icp_opts* opts,
@@ -199,7 +202,7 @@ int kabsch_device(rst_ctx* ctx, const double cov[9], const float smean[3],
 // unprojection (unproject.hip)
 int unproject_device(rst_ctx* ctx, const uint16_t* d_depth,
                      const rst_intrinsics* K, int keep_invalid,
-                     float* d_xyz, int64_t* n_out);
+                     float* d_xyz, int64_t* n_out, int stride = 1);
 
 // RemoveNans / DownsampleVoxel (voxel.hip); synchronous (n_out is host)
 int remove_nans_device(rst_ctx* ctx, const float* d_xyz, int64_t n, float* d_out,

@@ -7,6 +7,11 @@
 // Pinhole deprojection with rs2_deproject_pixel_to_point's op order (no
 // distortion):  x = (u - ppx)/fx,  y = (v - ppy)/fy,  P = (z*x, z*y, z).
 // HBM traffic: 2 B/px in, 12 B/valid px out (+ 4 B per 1024-px tile count).
+//
+// Pyramid levels (BASELINE configs[4]): level l reads every s = 2^l-th pixel
+// of every s-th row -- pixel (u, v) = (s*ul, s*vl) of the full image with
+// the full image's intrinsics, so a level's points are exactly a subset of
+// the level-0 points (2 B / s^2 px in).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -23,8 +28,15 @@ constexpr int kTile = kBS * kRounds;
 
 struct Cam {
   float fx, fy, cx, cy, scale, zmin, zmax;
-  int w;
+  int w;       // width of the (decimated) pixel grid
+  int s;       // decimation stride (1 = full resolution)
+  int64_t ws;  // row pitch of the depth image (pixels)
 };
+
+// depth index of grid pixel p
+__device__ __forceinline__ int64_t src_px(int64_t p, const Cam& c) {
+  return (p / c.w) * c.s * c.ws + (p % c.w) * c.s;
+}
 
 __device__ __forceinline__ bool valid_px(uint16_t d, const Cam& c, float& z) {
   z = c.scale * (float)d;
@@ -40,7 +52,7 @@ __global__ __launch_bounds__(kBS) void k_count(const uint16_t* __restrict__ dept
   for (int r = 0; r < kRounds; ++r) {
     const int64_t p = base + r * kBS + threadIdx.x;
     float z;
-    if (p < npx && valid_px(depth[p], c, z)) ++cnt;
+    if (p < npx && valid_px(depth[src_px(p, c)], c, z)) ++cnt;
   }
   // wave + block sum
 #pragma unroll
@@ -66,10 +78,10 @@ __global__ __launch_bounds__(kBS) void k_write(const uint16_t* __restrict__ dept
   for (int r = 0; r < kRounds; ++r) {
     const int64_t p = base + r * kBS + threadIdx.x;
     const bool inb = p < npx;
-    const uint16_t d = inb ? depth[p] : (uint16_t)0;
+    const uint16_t d = inb ? depth[src_px(p, c)] : (uint16_t)0;
     float z;
     const bool ok = inb && valid_px(d, c, z);
-    const int u = (int)(p % c.w), v = (int)(p / c.w);
+    const int u = (int)(p % c.w) * c.s, v = (int)(p / c.w) * c.s;
     const float x = ((float)u - c.cx) / c.fx;
     const float y = ((float)v - c.cy) / c.fy;
     if (keep_invalid) {
@@ -128,11 +140,14 @@ __global__ __launch_bounds__(1024) void k_scan_small(uint32_t* __restrict__ a, i
 }  // namespace
 
 int unproject_device(rst_ctx* ctx, const uint16_t* d_depth, const rst_intrinsics* K,
-                     int keep_invalid, float* d_xyz, int64_t* n_out) {
+                     int keep_invalid, float* d_xyz, int64_t* n_out, int stride) {
   if (!ctx || !d_depth || !K || !d_xyz || !n_out) return RST_E_ARG;
   if (K->width <= 0 || K->height <= 0 || !(K->fx != 0.f) || !(K->fy != 0.f)) return RST_E_ARG;
-  const int64_t npx = (int64_t)K->width * K->height;
-  Cam c{K->fx, K->fy, K->cx, K->cy, K->depth_scale, K->min_depth, K->max_depth, K->width};
+  if (stride < 1 || stride > 1024) return RST_E_ARG;
+  const int wl = (K->width + stride - 1) / stride, hl = (K->height + stride - 1) / stride;
+  const int64_t npx = (int64_t)wl * hl;
+  Cam c{K->fx, K->fy, K->cx, K->cy, K->depth_scale, K->min_depth, K->max_depth, wl, stride,
+        (int64_t)K->width};
   const int nb = (int)((npx + kTile - 1) / kTile);
   hipStream_t st = ctx->stream;
   if (keep_invalid) {
@@ -166,7 +181,14 @@ int rst_unproject_device(rst_ctx* ctx, const uint16_t* d_depth, const rst_intrin
                          int keep_invalid, float* d_xyz_out, int64_t* n_out) {
   if (!ctx) return RST_E_ARG;
   RST_HIP(hipSetDevice(ctx->device));
-  return unproject_device(ctx, d_depth, K, keep_invalid, d_xyz_out, n_out);
+  return unproject_device(ctx, d_depth, K, keep_invalid, d_xyz_out, n_out, 1);
+}
+
+int rst_unproject_strided_device(rst_ctx* ctx, const uint16_t* d_depth, const rst_intrinsics* K,
+                                 int stride, int keep_invalid, float* d_xyz_out, int64_t* n_out) {
+  if (!ctx) return RST_E_ARG;
+  RST_HIP(hipSetDevice(ctx->device));
+  return unproject_device(ctx, d_depth, K, keep_invalid, d_xyz_out, n_out, stride);
 }
 
 int rst_unproject(rst_ctx* ctx, const uint16_t* depth, const rst_intrinsics* K, int keep_invalid,
@@ -187,7 +209,7 @@ int rst_unproject(rst_ctx* ctx, const uint16_t* depth, const rst_intrinsics* K, 
       hipSuccess)
     s = RST_E_HIP;
   int64_t n = 0;
-  if (s >= 0) s = unproject_device(ctx, dd, K, keep_invalid, dx, &n);
+  if (s >= 0) s = unproject_device(ctx, dd, K, keep_invalid, dx, &n, 1);
   if (s >= 0) {
     if (hipMemcpyAsync(xyz_out, dx, sizeof(float) * 3 * n, hipMemcpyDeviceToHost, ctx->stream) !=
             hipSuccess ||
@@ -201,16 +223,19 @@ int rst_unproject(rst_ctx* ctx, const uint16_t* depth, const rst_intrinsics* K, 
   return s;
 }
 
-int rst_frame_prepare_device(rst_ctx* ctx, const uint16_t* d_depth, const rst_intrinsics* K,
-                             int normals_k, rst_target** out) {
-  if (!ctx || !d_depth || !K || !out) return RST_E_ARG;
-  RST_HIP(hipSetDevice(ctx->device));
+}  // extern "C"
+
+namespace rst {
+// depth (device) -> points of pyramid level `stride` -> target handle
+// (+ normals when normals_k > 0)
+static int frame_prepare(rst_ctx* ctx, const uint16_t* d_depth, const rst_intrinsics* K,
+                         int stride, int normals_k, rst_target** out) {
   const int64_t npx = (int64_t)K->width * K->height;
   float* dx = nullptr;
   size_t dxc = 0;
   RST_CHECK(ctx_alloc(ctx, sizeof(float) * 3 * std::max<int64_t>(npx, 1), (void**)&dx, &dxc));
   int64_t n = 0;
-  int s = unproject_device(ctx, d_depth, K, 0, dx, &n);
+  int s = unproject_device(ctx, d_depth, K, 0, dx, &n, stride);
   rst_target* t = nullptr;
   if (s >= 0) s = target_build_device(ctx, dx, n, true, &t);
   if (s >= 0 && normals_k > 0) {
@@ -224,6 +249,35 @@ int rst_frame_prepare_device(rst_ctx* ctx, const uint16_t* d_depth, const rst_in
     return s;
   }
   *out = t;
+  return RST_OK;
+}
+}  // namespace rst
+
+extern "C" {
+
+int rst_frame_prepare_device(rst_ctx* ctx, const uint16_t* d_depth, const rst_intrinsics* K,
+                             int normals_k, rst_target** out) {
+  if (!ctx || !d_depth || !K || !out) return RST_E_ARG;
+  RST_HIP(hipSetDevice(ctx->device));
+  return frame_prepare(ctx, d_depth, K, 1, normals_k, out);
+}
+
+int rst_frame_prepare_pyramid_device(rst_ctx* ctx, const uint16_t* d_depth,
+                                     const rst_intrinsics* K, int nlevels, int normals_k,
+                                     rst_target** out_levels) {
+  if (!ctx || !d_depth || !K || !out_levels || nlevels < 1 || nlevels > 10) return RST_E_ARG;
+  RST_HIP(hipSetDevice(ctx->device));
+  for (int l = 0; l < nlevels; ++l) out_levels[l] = nullptr;
+  for (int l = 0; l < nlevels; ++l) {
+    const int s = frame_prepare(ctx, d_depth, K, 1 << l, normals_k, &out_levels[l]);
+    if (s < 0) {
+      for (int k = 0; k < l; ++k) {
+        rst_target_free(out_levels[k]);
+        out_levels[k] = nullptr;
+      }
+      return s;
+    }
+  }
   return RST_OK;
 }
 

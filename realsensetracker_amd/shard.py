@@ -51,12 +51,25 @@ class ShardedAligner:
     its own shard (device pointer, see ``shard_bounds``) and the replicated
     target; all ranks return the same pose."""
 
-    def __init__(self, ctx, group=None):
-        import torch.distributed as dist
+    def __init__(self, ctx, group=None, world: int | None = None, rank: int | None = None,
+                 uid: bytes | None = None):
+        """Ranks from ``torch.distributed`` (the default), or given
+        explicitly with the RCCL unique id (e.g. world 1 without a process
+        group: the id is drawn locally)."""
         self.ctx = ctx
-        self.rank = dist.get_rank(group)
-        self.world = dist.get_world_size(group)
-        uid = exchange_unique_id(group)
+        if world is None:
+            import torch.distributed as dist
+            self.rank = dist.get_rank(group)
+            self.world = dist.get_world_size(group)
+            uid = exchange_unique_id(group)
+        else:
+            self.world, self.rank = int(world), int(rank or 0)
+            if uid is None:
+                if self.world != 1:
+                    raise ValueError("world > 1 needs the shared unique id")
+                raw = C.create_string_buffer(L.COMM_ID_BYTES)
+                L.check(L.lib().rst_comm_get_unique_id(raw), "rst_comm_get_unique_id")
+                uid = raw.raw
         self._comm = C.c_void_p()
         L.check(L.lib().rst_comm_create(ctx.handle, uid, self.world, self.rank,
                                         C.byref(self._comm)), "rst_comm_create")

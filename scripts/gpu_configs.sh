@@ -1,0 +1,19 @@
+#!/bin/bash
+# GPU parity tests + bench lines of the other BASELINE configs (720p stream,
+# pyramid, sharded 1M pair).  Each GPU step has its own limit; the chain
+# stops at the first failure.   TAG=r01g bash scripts/gpu_configs.sh
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+TAG=${TAG:-r01}
+step() {  # name, limit, command...
+  local name=$1 lim=$2; shift 2
+  timeout -k 10 "$lim" "$@" > gpurun_out/${TAG}_$name.log 2>&1
+  local rc=$?
+  echo "$name rc=$rc"; tail -3 gpurun_out/${TAG}_$name.log
+  [ $rc -eq 0 ] || exit $rc
+}
+step pytest_gpu 600 python -u -m pytest tests/ -x -v -m gpu --timeout 120 --timeout-method thread
+step bench_pyramid 300 python bench.py --workload pyramid --no-p2plane
+step bench_sharded 300 python bench.py --workload sharded --steps 5 --warmup 1
+step bench_720p 300 python bench.py --width 1280 --height 720 --no-host-api --no-gicp

@@ -701,3 +701,112 @@ def test_fpfh_contract(ctx):
     idx = np.zeros((100, 3), np.int32)
     assert L.lib().rst_compute_matches(ctx.handle, L.fptr(out), 100, L.fptr(out), 100, 3,
                                        L.iptr(idx), None) == L.RST_E_ARG
+
+
+# ---- coarse-to-fine pyramid (BASELINE configs[4]) ----------------------------------------
+def _pair_intrinsics(g):
+    h, w = g["depth_a"].shape
+    K4 = g["K4"]
+    return driver.intrinsics(w, h, fx=K4[0], fy=K4[1], cx=K4[2], cy=K4[3], min_depth=0,
+                             max_depth=0), K4
+
+
+@pytest.mark.parametrize("stride", [1, 2, 3, 4, 8])
+def test_unproject_strided_bitexact(ctx, stride):
+    torch = pytest.importorskip("torch")
+    g = load_golden("pair_160x120_s2")
+    K, K4 = _pair_intrinsics(g)
+    d = torch.from_numpy(g["depth_a"].astype(np.int16)).cuda()
+    out = torch.zeros((d.numel(), 3), dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    for keep in (0, 1):
+        n = C.c_int64(0)
+        L.check(L.lib().rst_unproject_strided_device(ctx.handle, C.c_void_p(d.data_ptr()),
+                                                     C.byref(K), stride, keep,
+                                                     C.c_void_p(out.data_ptr()), C.byref(n)),
+                "rst_unproject_strided_device")
+        got = out[: n.value].cpu().numpy()
+        assert np.array_equal(got, O.unproject(g["depth_a"], K4, keep_invalid=bool(keep),
+                                               stride=stride)), (stride, keep)
+    bad = C.c_int64(0)
+    assert L.lib().rst_unproject_strided_device(ctx.handle, C.c_void_p(d.data_ptr()), C.byref(K),
+                                                0, 0, C.c_void_p(out.data_ptr()),
+                                                C.byref(bad)) == L.RST_E_ARG
+
+
+def _pyramid(ctx, g, nlev, normals_k=0):
+    torch = pytest.importorskip("torch")
+    K, K4 = _pair_intrinsics(g)
+    da = torch.from_numpy(g["depth_a"].astype(np.int16)).cuda()
+    db = torch.from_numpy(g["depth_b"].astype(np.int16)).cuda()
+    torch.cuda.synchronize()
+    tl = A.Target.pyramid_from_depth_device(da.data_ptr(), K, nlev, normals_k, ctx)
+    sl = A.Target.pyramid_from_depth_device(db.data_ptr(), K, nlev, normals_k, ctx)
+    pa = [O.unproject(g["depth_a"], K4, stride=1 << lv) for lv in range(nlev)]
+    pb = [O.unproject(g["depth_b"], K4, stride=1 << lv) for lv in range(nlev)]
+    return sl, tl, pb, pa
+
+
+def test_pyramid_levels_are_strided_frames(ctx):
+    g = load_golden("pair_160x120_s2")
+    sl, tl, pb, pa = _pyramid(ctx, g, 3)
+    for lv in range(3):
+        assert len(tl[lv]) == len(pa[lv]) and len(sl[lv]) == len(pb[lv])
+        _, d2 = tl[lv].query(pa[lv])  # every oracle point of the level is in the index
+        assert np.all(d2 == 0)
+
+
+@pytest.mark.parametrize("name", PAIR_NAMES)
+def test_pyramid_matches_oracle_chain(ctx, name):
+    """3-level coarse-to-fine P2POINT_REF: the device-chained pyramid equals
+    the same levels aligned one call at a time with one pose (bit-exact),
+    and the oracle's chain with fp64 sums within the ICP gate."""
+    g = load_golden(name)
+    sl, tl, pb, pa = _pyramid(ctx, g, 3)
+    iters = [16, 24, 32]  # finest first
+    r = A.align_pyramid(sl, tl, iters)
+    T = np.eye(4, dtype=np.float32)
+    for lv in (2, 1, 0):
+        rl = A.align_prepared(sl[lv], tl[lv], T, L.default_opts(max_iter=iters[lv]))
+        T = rl.pose
+    assert np.array_equal(r.pose, T)
+    assert r.ok == rl.ok and r.iterations == iters[0]
+    ok, To, _ = O.align_icp_pyramid(pb, pa, iters, sum_mode=1)
+    assert ok == r.ok
+    assert max(pose_err(r.pose, To)) <= 2e-5, pose_err(r.pose, To)
+
+
+def test_pyramid_p2plane_matches_chained_calls(ctx):
+    g = load_golden("pair_160x120_s2")
+    sl, tl, _, _ = _pyramid(ctx, g, 3, normals_k=16)
+    o = L.default_opts(mode=L.RST_P2PLANE, max_iter=30)
+    r = A.align_pyramid(sl, tl, [30, 30, 30], None, o)
+    T = np.eye(4, dtype=np.float32)
+    for lv in (2, 1, 0):
+        rl = A.align_prepared(sl[lv], tl[lv], T, o)
+        if rl.ok:
+            T = rl.pose
+    assert r.ok and np.array_equal(r.pose, T)
+    assert max(pose_err(r.pose, g["T_gt"])) <= 3e-3
+
+
+def test_pyramid_contract(ctx):
+    g = load_golden("pair_80x60_s0")
+    sl, tl, _, _ = _pyramid(ctx, g, 2)
+    tiny = A.Target.build(g["src"][:2], ctx)
+    T0 = np.eye(4, dtype=np.float32)
+    T0[0, 3] = 0.01
+    # level 0 with < 3 points: the reference's early false, pose untouched
+    r = A.align_pyramid([tiny, sl[1]], tl, [8, 8], T0)
+    assert not r.ok and np.array_equal(r.pose, T0)
+    # a coarse level with < 3 points is skipped: = level 0 alone
+    r = A.align_pyramid([sl[0], tiny], tl, [8, 8], T0)
+    r0 = A.align_prepared(sl[0], tl[0], T0, L.default_opts(max_iter=8))
+    assert np.array_equal(r.pose, r0.pose) and r.ok == r0.ok
+    # one level = the plain prepared align; zero iterations pass the pose through
+    r = A.align_pyramid([sl[0]], [tl[0]], [8], T0)
+    assert np.array_equal(r.pose, r0.pose)
+    r = A.align_pyramid(sl, tl, [0, 0], T0)
+    assert np.array_equal(r.pose, T0)
+    with pytest.raises(ValueError):
+        A.align_pyramid(sl, tl, [8])

@@ -149,6 +149,45 @@ def test_unproject_oracle_is_pinhole(name):
     np.testing.assert_array_equal(pts[:, 0], z * x)
 
 
+@pytest.mark.parametrize("stride", [1, 2, 3, 4])
+def test_unproject_strided_oracle_is_pinhole_subsample(stride):
+    """Pyramid level (BASELINE configs[4]): the pixels (s*ul, s*vl), full
+    intrinsics -- numpy restatement, and exactly a subset of level 0."""
+    g = load_golden("pair_160x120_s2")
+    K4 = g["K4"]
+    d = g["depth_a"]
+    pts = O.unproject(d, K4, stride=stride)
+    v, u = np.nonzero(d[::stride, ::stride])
+    v, u = v * stride, u * stride
+    z = np.float32(0.001) * d[v, u].astype(np.float32)
+    x = ((u.astype(np.float32) - K4[2]) / K4[0]).astype(np.float32)
+    y = ((v.astype(np.float32) - K4[3]) / K4[1]).astype(np.float32)
+    np.testing.assert_array_equal(pts, np.stack([z * x, z * y, z], 1))
+    full = O.unproject(d, K4)
+    keep = (np.nonzero(d.ravel())[0])
+    sel = np.isin(keep, (v * d.shape[1] + u))
+    np.testing.assert_array_equal(pts, full[sel])
+    assert len(O.unproject(d, K4, keep_invalid=True, stride=stride)) == \
+        d[::stride, ::stride].size
+
+
+def test_pyramid_oracle_chain():
+    g = load_golden("pair_160x120_s2")
+    K4 = g["K4"]
+    src = [O.unproject(g["depth_b"], K4, stride=1 << lv) for lv in range(3)]
+    dst = [O.unproject(g["depth_a"], K4, stride=1 << lv) for lv in range(3)]
+    # one level = AlignIcp3d
+    ok1, T1, mc1 = O.align_icp_pyramid(src[:1], dst[:1], [16])
+    ok, T, mc, _ = O.align_icp(src[0], dst[0], 16)
+    assert ok1 == ok and np.array_equal(T1, T) and mc1 == mc
+    # coarse-to-fine: the chain of calls with one pose
+    okp, Tp, _ = O.align_icp_pyramid(src, dst, [16, 16, 32], sum_mode=1)
+    Tc = np.eye(4, dtype=np.float32)
+    for lv, it in ((2, 32), (1, 16), (0, 16)):
+        _, Tc, _, _ = O.align_icp(src[lv], dst[lv], it, T=Tc, sum_mode=1)
+    assert okp and np.array_equal(Tp, Tc)
+
+
 @pytest.mark.parametrize("name", PAIR_NAMES)
 def test_p2plane_oracle_converges_to_ground_truth(name):
     g = load_golden(name)
