@@ -32,7 +32,8 @@ namespace {
 constexpr int kBS = 256;
 constexpr int kNP2Point = 16;  // sum w q u^T (9), sum w u (3), sum q (3), sum d2
 constexpr int kNP2Plane = 30;  // A (21), b (6), sum w r^2, count, sum d2
-constexpr int kFbBlocks = 2048;  // fixed grid of the fallback kernel (8192 waves)
+constexpr int kFbBlocks = 2048;  // largest fallback grid (RST_FB_BLOCKS)
+constexpr int kFbDefault = 1024;  // fallback grid (4096 waves; r01g sweep: 2048 / 512 lose)
 // From a queue of lane_min entries (IcpParams; 3/4 of the source points: the
 // cold first iteration, where most lanes' warm balls are not covered) the
 // fallback kernel gives every queued query one lane instead of one
@@ -592,8 +593,9 @@ __device__ __forceinline__ void acc_update(const double* tot, const IcpParams& p
 // Rows of Acc::RS doubles (RS divides kRedBS): thread t sums column t % RS
 // of rows t / RS, t / RS + kRedBS / RS, ... -- coalesced loads, all in
 // flight together -- then per column a fixed-order sum over the kRedBS / RS
-// partials.  Bitwise reproducible.  slab2 holds rows for the first
-// ceil(E / waves-per-block) fallback blocks only.  Single GPU: thread 0
+// partials.  Bitwise reproducible.  The ICP loop passes rows1 = 0: every
+// fallback block's row already holds its share of kernel 1's rows
+// (k_icp_fb).  Single GPU: thread 0
 // solves (align_icp.cpp:122-151); multi-GPU: the row goes to `totals` for
 // the RCCL all-reduce and k_solve_only follows.
 template <class Acc>
@@ -608,15 +610,14 @@ __global__ __launch_bounds__(kRedBS) void k_reduce_solve(const double* __restric
   __shared__ double tot[RS];
   if (Acc::kCanFinish && st->done) return;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  const int E = st->fb_e;
-  const int rows2 = fb_blocks(E, rows2max, prm.lane_min);
+  const int rows2 = rows2max;  // every fallback block writes its row (kernel 1's folded in)
   const int t = threadIdx.x, col = t % RS;
   // unrolled so a thread's loads are all in flight before the first add
   // waits (a rolled loop pays one memory latency per row)
   double acc = 0.0;
 #pragma unroll 16
   for (int r = t / RS; r < rows1; r += PER) acc += __builtin_nontemporal_load(slab1 + (int64_t)r * RS + col);
-#pragma unroll 8
+#pragma unroll 16
   for (int r = t / RS; r < rows2; r += PER) acc += __builtin_nontemporal_load(slab2 + (int64_t)r * RS + col);
   red[t] = acc;
   __syncthreads();
@@ -662,8 +663,9 @@ __global__ void k_solve_only(const double* __restrict__ totals, IcpParams prm,
 // every block rebuilds their prefix in LDS from the per-block counts) is
 // handled by wave e mod W of this fixed grid; each wave adds its entries in
 // increasing e, so the slab is reproducible.  Only the first
-// nw = max(1, ceil(E / waves-per-block)) blocks have work; the others exit
-// after the scan.  Block 0 publishes E for k_reduce_solve.
+// nw = max(1, ceil(E / waves-per-block)) blocks have queries.  Every block
+// then folds kernel 1's slab rows b, b + G, ... into its own row, so the
+// solve kernel reduces G rows, not nb1 + G.  Block 0 publishes E.
 template <class Acc>
 __global__ __launch_bounds__(kBS) void k_icp_fb(BvhView bv, AdjView av, AccArgs aa,
                                                 const float4* __restrict__ src,
@@ -671,7 +673,8 @@ __global__ __launch_bounds__(kBS) void k_icp_fb(BvhView bv, AdjView av, AccArgs 
                                                 int32_t* __restrict__ nnpos,
                                                 const int32_t* __restrict__ qbuf,
                                                 const int32_t* __restrict__ qcnt, int nb1,
-                                                int lane_min, double* __restrict__ slab2) {
+                                                int lane_min, const double* __restrict__ slab1,
+                                                double* __restrict__ slab2) {
   extern __shared__ int pref[];  // [nb1 + 1]
   __shared__ double lds[(kBS / kWave) * Acc::NV];
   __shared__ WnnScratch wsc[kBS / kWave];
@@ -682,11 +685,13 @@ __global__ __launch_bounds__(kBS) void k_icp_fb(BvhView bv, AdjView av, AccArgs 
   queue_prefix(qcnt, nb1, pref, blockIdx.x == 0 ? st : nullptr);
   __syncthreads();
   const int E = pref[nb1];
-  if ((int)blockIdx.x >= fb_blocks(E, gridDim.x, lane_min)) return;
+  const bool work = (int)blockIdx.x < fb_blocks(E, gridDim.x, lane_min);
   double v[Acc::NV];
 #pragma unroll
   for (int k = 0; k < Acc::NV; ++k) v[k] = 0.0;
-  if (E >= lane_min) {  // uniform: one lane per query, entries in order
+  if (!work) {
+    // no queries: the fold of kernel 1's rows only
+  } else if (E >= lane_min) {  // uniform: one lane per query, entries in order
     const Uni u = load_uni(st);
     const int T = gridDim.x * kBS;
     for (int e = blockIdx.x * kBS + threadIdx.x; e < E; e += T) {
@@ -753,7 +758,8 @@ __global__ __launch_bounds__(kBS) void k_icp_fb(BvhView bv, AdjView av, AccArgs 
       }
     }
   }
-  block_sum_to_slab<Acc::NV, kBS>(v, lds, slab2 + (int64_t)blockIdx.x * Acc::RS);
+  block_sum_to_slab_fold<Acc::NV, kBS>(v, lds, slab2 + (int64_t)blockIdx.x * Acc::RS, slab1, nb1,
+                                       Acc::RS, blockIdx.x, gridDim.x);
 }
 
 inline int blocks_for(int64_t n) { return (int)std::max<int64_t>(1, (n + kBS - 1) / kBS); }
@@ -908,6 +914,12 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
   aa.pos0 = tgt->pos0;
   const AdjView av = adj_of(tgt);
   const size_t fb_lds = sizeof(int) * ((size_t)nblk + 1);
+  // fallback grid (RST_FB_BLOCKS: tuning knob, <= kFbBlocks)
+  static const int fb_grid = [] {
+    const char* e = getenv("RST_FB_BLOCKS");
+    const int v = e ? atoi(e) : kFbDefault;
+    return (v >= 1 && v <= kFbBlocks) ? v : kFbBlocks;
+  }();
 
   IcpParams prm;
   prm.n = n_total;
@@ -940,19 +952,19 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
         k_icp_nn<P2PlaneAcc><<<nblk, kBS, 0, st>>>(bv, av, aa, src->pts, n_local, ctx->d_state,
                                                    nnpos, qbuf, qcnt, slab);
         if (tm) RST_HIP(hipEventRecord(ctx->ev[2 * it + 1], st));
-        k_icp_fb<P2PlaneAcc><<<kFbBlocks, kBS, fb_lds, st>>>(bv, av, aa, src->pts, ctx->d_state,
+        k_icp_fb<P2PlaneAcc><<<fb_grid, kBS, fb_lds, st>>>(bv, av, aa, src->pts, ctx->d_state,
                                                              nnpos, qbuf, qcnt, nblk,
-                                                             prm.lane_min, slab2);
-        k_reduce_solve<P2PlaneAcc><<<1, kRedBS, 0, st>>>(slab, nblk, slab2, kFbBlocks, prm,
+                                                             prm.lane_min, slab, slab2);
+        k_reduce_solve<P2PlaneAcc><<<1, kRedBS, 0, st>>>(slab, 0, slab2, fb_grid, prm,
                                                          ctx->d_state, red_out);
       } else {
         k_icp_nn<P2PointAcc><<<nblk, kBS, 0, st>>>(bv, av, aa, src->pts, n_local, ctx->d_state,
                                                    nnpos, qbuf, qcnt, slab);
         if (tm) RST_HIP(hipEventRecord(ctx->ev[2 * it + 1], st));
-        k_icp_fb<P2PointAcc><<<kFbBlocks, kBS, fb_lds, st>>>(bv, av, aa, src->pts, ctx->d_state,
+        k_icp_fb<P2PointAcc><<<fb_grid, kBS, fb_lds, st>>>(bv, av, aa, src->pts, ctx->d_state,
                                                              nnpos, qbuf, qcnt, nblk,
-                                                             prm.lane_min, slab2);
-        k_reduce_solve<P2PointAcc><<<1, kRedBS, 0, st>>>(slab, nblk, slab2, kFbBlocks, prm,
+                                                             prm.lane_min, slab, slab2);
+        k_reduce_solve<P2PointAcc><<<1, kRedBS, 0, st>>>(slab, 0, slab2, fb_grid, prm,
                                                          ctx->d_state, red_out);
       }
     } else {

@@ -84,6 +84,34 @@ __device__ __forceinline__ void block_sum_to_slab(double (&v)[NV],
   }
 }
 
+// block_sum_to_slab, then rows blk, blk + step, ... (< rows) of another slab
+// (row stride `stride`) added in increasing order: a grid of G blocks folds
+// an earlier kernel's rows into its own G, fixed order (reproducible).
+template <int NV, int BS>
+__device__ __forceinline__ void block_sum_to_slab_fold(double (&v)[NV], double* lds,
+                                                       double* slab_row,
+                                                       const double* __restrict__ other,
+                                                       int rows, int stride, int blk, int step) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wid = threadIdx.x / kWave;
+  double ex = 0.0;  // loads issued before the wave sums (latency overlap)
+  if (threadIdx.x < NV)
+    for (int r = blk; r < rows; r += step) ex += other[(int64_t)r * stride + threadIdx.x];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) v[k] = wave_sum(v[k]);
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) lds[wid * NV + k] = v[k];
+  }
+  __syncthreads();
+  if (threadIdx.x < NV) {
+    double s = 0.0;
+#pragma unroll
+    for (int w = 0; w < BS / kWave; ++w) s += lds[w * NV + threadIdx.x];
+    slab_row[threadIdx.x] = s + ex;
+  }
+}
+
 // ---- 3x3 linear algebra (single thread) -------------------------------------
 #define RST_M3(m, r, c) (m)[(c) * 3 + (r)]
 
