@@ -235,6 +235,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-host-api", action="store_true")
     ap.add_argument("--no-gicp", action="store_true")
+    ap.add_argument("--graphs", action="store_true",
+                    help="replay each align's iteration loop as a hipGraph (no kernel timing)")
     ap.add_argument("--inflight", type=int, default=2,
                     help="frame pairs in flight per GPU (one HIP stream each)")
     a = ap.parse_args()
@@ -347,9 +349,13 @@ def main():
         for t in prev:
             t.free()
 
+    if a.graphs:
+        for c in actx:
+            c.enable_graphs(True)
+
     def timing(on: bool):
         for c in actx:  # HIP events around k_icp_nn on every 8th iteration
-            c.enable_kernel_timing(8 if on else 0)
+            c.enable_kernel_timing(8 if on and not a.graphs else 0)
 
     def sync_all():
         for c in [pctx] + actx:
@@ -464,7 +470,7 @@ def main():
                    "iters_per_pair": sum(pyr_iters) if pyr else a.iters,
                    "points_per_frame": round(n_avg), "frames_cycled": nfr,
                    "accumulation": "fp64 partial sums", "parallelism": f"replica{world}",
-                   "pairs_in_flight_per_gpu": len(actx)},
+                   "pairs_in_flight_per_gpu": len(actx), "hipgraph": bool(a.graphs)},
         "frames_per_s": frames_all / dt,
         "pairs_ok": st["ok"],
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

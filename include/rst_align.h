@@ -92,6 +92,12 @@ int rst_ctx_synchronize(rst_ctx* ctx);
  * align call, measured with HIP events on the context's stream; and the
  * number of launches it covers.  Used by bench.py's roofline. */
 int rst_ctx_last_kernel_time(rst_ctx* ctx, float* avg_ms, int32_t* launches);
+/* hipGraph mode (BASELINE configs[4]): each align's iteration loop is
+ * captured and replayed as one graph (the executable for a given iteration
+ * count and mode is kept on the context and updated in place with the next
+ * align's arguments).  Same results; not used by the sharded (RCCL) align or
+ * while kernel timing is on.  0 = off (default). */
+int rst_ctx_enable_graphs(rst_ctx* ctx, int enable);
 /* Per-iteration kernel timing (HIP events around the dominant kernel on the
  * context's stream): 0 = off (default), 1 = every iteration, k > 1 = every
  * k-th iteration (fewer events in a timed loop). */

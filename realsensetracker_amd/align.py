@@ -59,6 +59,10 @@ class Context:
         """0/False off, 1/True every iteration, k > 1 every k-th."""
         L.check(L.lib().rst_ctx_enable_kernel_timing(self._h, int(on)), "timing")
 
+    def enable_graphs(self, on: bool = True):
+        """Replay each align's iteration loop as one hipGraph."""
+        L.check(L.lib().rst_ctx_enable_graphs(self._h, int(on)), "rst_ctx_enable_graphs")
+
     def last_kernel_time(self):
         ms = C.c_float(0)
         n = C.c_int32(0)

@@ -216,6 +216,7 @@ int rst_ctx_destroy(rst_ctx* ctx) {
   hipSetDevice(ctx->device);
   if (ctx->stream) hipStreamSynchronize(ctx->stream);
   for (hipEvent_t e : ctx->ev) hipEventDestroy(e);
+  for (auto& kv : ctx->gexec) hipGraphExecDestroy(kv.second);
   if (ctx->ws) hipFree(ctx->ws);
   if (ctx->pinned) hipHostFree(ctx->pinned);
   if (ctx->d_state) hipFree(ctx->d_state);
@@ -244,6 +245,12 @@ int rst_ctx_last_kernel_time(rst_ctx* ctx, float* avg_ms, int32_t* launches) {
   if (!ctx) return RST_E_ARG;
   if (avg_ms) *avg_ms = ctx->last_kernel_ms;
   if (launches) *launches = ctx->last_kernel_launches;
+  return RST_OK;
+}
+
+int rst_ctx_enable_graphs(rst_ctx* ctx, int enable) {
+  if (!ctx) return RST_E_ARG;
+  ctx->graphs = enable != 0;
   return RST_OK;
 }
 

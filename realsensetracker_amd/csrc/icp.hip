@@ -944,6 +944,12 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
     }
   }
   double* red_out = comm ? totals : nullptr;  // multi-GPU: reduce only
+  // hipGraph mode: the iteration loop (+ the state readback) is captured and
+  // replayed as one graph; the executable per (iterations, mode) is updated
+  // in place with this align's arguments (same topology).  Not with RCCL in
+  // the loop or per-iteration events.
+  const bool graph = ctx->graphs && !comm && !timing && n_local > 0 && opts.max_iter > 0;
+  if (graph) RST_HIP(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
   for (int it = 0; it < opts.max_iter; ++it) {
     const bool tm = timing && it % ctx->timing_stride == 0;  // sampled iterations
     if (tm) RST_HIP(hipEventRecord(ctx->ev[2 * it], st));
@@ -982,6 +988,28 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
   }
   RST_HIP(hipGetLastError());
   RST_HIP(hipMemcpyAsync(ctx->h_state, ctx->d_state, sizeof(IcpState), hipMemcpyDeviceToHost, st));
+  if (graph) {
+    hipGraph_t g = nullptr;
+    RST_HIP(hipStreamEndCapture(st, &g));
+    hipGraphExec_t& ex = ctx->gexec[{opts.max_iter, (int)p2plane}];
+    if (ex) {
+      hipGraphNode_t err_node = nullptr;
+      hipGraphExecUpdateResult ur;
+      if (hipGraphExecUpdate(ex, g, &err_node, &ur) != hipSuccess ||
+          ur != hipGraphExecUpdateSuccess) {
+        (void)hipGetLastError();
+        hipGraphExecDestroy(ex);
+        ex = nullptr;
+      }
+    }
+    if (!ex && hipGraphInstantiate(&ex, g, nullptr, nullptr, 0) != hipSuccess) {
+      ex = nullptr;
+      hipGraphDestroy(g);
+      return RST_E_HIP;
+    }
+    hipGraphDestroy(g);
+    RST_HIP(hipGraphLaunch(ex, st));
+  }
   ctx->pend.active = true;
   ctx->pend.p2plane = p2plane;
   ctx->pend.timing = timing;

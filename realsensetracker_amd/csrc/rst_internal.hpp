@@ -107,6 +107,10 @@ struct rst_ctx {
   std::vector<hipEvent_t> ev;
   float last_kernel_ms = 0.f;
   int32_t last_kernel_launches = 0;
+  // hipGraph replay of the ICP iteration loop (rst_ctx_enable_graphs):
+  // (iterations, mode) -> executable graph, updated in place per align
+  bool graphs = false;
+  std::map<std::pair<int, int>, hipGraphExec_t> gexec;
   // device memory of freed targets, kept for the next build (hipFree
   // synchronises the whole device, which would stall every stream of a
   // pipelined frame loop): size class -> blocks

@@ -810,3 +810,32 @@ def test_pyramid_contract(ctx):
     assert np.array_equal(r.pose, T0)
     with pytest.raises(ValueError):
         A.align_pyramid(sl, tl, [8])
+
+
+def test_hipgraph_mode_matches_stream_mode(ctx):
+    """rst_ctx_enable_graphs: the captured loop (executable reused and
+    updated across aligns of different sizes / modes) gives the same poses."""
+    gctx = A.Context(0)
+    gctx.enable_graphs(True)
+    try:
+        for name in PAIR_NAMES + PAIR_NAMES[:1]:  # repeat: the update path
+            g = load_golden(name)
+            for mode, it in ((L.RST_P2POINT_REF, 24), (L.RST_P2PLANE, 30)):
+                o = L.default_opts(mode=mode, max_iter=it)
+                res = []
+                for c in (ctx, gctx):
+                    t = A.Target.build(g["dst"], c)
+                    if mode == L.RST_P2PLANE:
+                        t.compute_normals(16)
+                    s = A.Target.build(g["src"], c)
+                    res.append(A.align_prepared(s, t, None, o))
+                assert np.array_equal(res[0].pose, res[1].pose), (name, mode)
+                assert res[0].iterations == res[1].iterations
+        g = load_golden("pair_160x120_s2")
+        sl, tl, _, _ = _pyramid(gctx, g, 3)
+        r = A.align_pyramid(sl, tl, [16, 24, 32])
+        sl0, tl0, _, _ = _pyramid(ctx, g, 3)
+        r0 = A.align_pyramid(sl0, tl0, [16, 24, 32])
+        assert np.array_equal(r.pose, r0.pose)
+    finally:
+        gctx.close()
