@@ -34,6 +34,10 @@ LIB_NAME = "librst_align.so"
 # weight arithmetic (DESIGN.md "Numerics").
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", f"--offload-arch={ARCH}",
           "-Wall", "-Wno-unused-function", "-Wno-unused-result", f"-I{INCLUDE}", f"-I{CSRC}"]
+# tuning experiments: RST_DEFINES="-DNAME=V ..." builds a variant library
+# (python -m realsensetracker_amd.build --lib --out lib/variants/x.so; load
+# it with RST_LIB=...)
+CFLAGS += os.environ.get("RST_DEFINES", "").split()
 
 
 def _hipcc() -> str:
@@ -65,13 +69,14 @@ def _compile(src: str) -> Path:
     return obj
 
 
-def build_library(jobs: int = 8) -> Path:
+def build_library(jobs: int = 8, out: Path | None = None) -> Path:
     OBJDIR.mkdir(parents=True, exist_ok=True)
     LIBDIR.mkdir(parents=True, exist_ok=True)
     with cf.ThreadPoolExecutor(max_workers=max(1, min(jobs, len(SOURCES)))) as ex:
         objs = list(ex.map(_compile, SOURCES))
-    out = LIBDIR / LIB_NAME
-    tmp = LIBDIR / (LIB_NAME + ".tmp")
+    out = Path(out) if out else LIBDIR / LIB_NAME
+    out.parent.mkdir(parents=True, exist_ok=True)
+    tmp = out.with_name(out.name + ".tmp")
     cmd = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", str(tmp),
            *map(str, objs), f"-L{ROCM / 'lib'}", "-lrccl", f"-Wl,-rpath,{ROCM / 'lib'}"]
     r = subprocess.run(cmd, capture_output=True, text=True)
@@ -100,10 +105,11 @@ def main(argv=None) -> int:
     ap.add_argument("--lib", action="store_true", help="library only")
     ap.add_argument("--clean", action="store_true")
     ap.add_argument("-j", type=int, default=8)
+    ap.add_argument("--out", default=None, help="library path (variant builds)")
     a = ap.parse_args(argv)
     if a.clean and OBJDIR.exists():
         shutil.rmtree(OBJDIR)
-    p = build_library(a.j)
+    p = build_library(a.j, PKG / a.out if a.out else None)
     print(p)
     if not a.lib:
         print(build_app())

@@ -224,6 +224,11 @@ __device__ inline void svd3_jacobi(const double* a_in, double* U, double* S,
 // at ~1e-16 relative; a few dozen fp64 flops per step instead of Jacobi
 // sweeps.  Returns false (the caller falls back to svd3_jacobi) when a is
 // numerically singular or the iteration does not settle.
+#ifndef RST_POLAR_MIN_IT
+#define RST_POLAR_MIN_IT 1  // r01h A/B: 6 -> 1 cut the solve 5.3 -> 4.6 us
+#endif
+constexpr int kPolarScaled = 6;                 // scaled Newton steps (then g = 1)
+constexpr int kPolarMinIt = RST_POLAR_MIN_IT;   // earliest converged exit
 __device__ inline bool polar3(const double* a, double* Q) {
   double X[9];
   double nx = 0.0;
@@ -261,7 +266,7 @@ __device__ inline bool polar3(const double* a, double* Q) {
       C[i] *= id;
       ni2 += C[i] * C[i];
     }
-    const double g = it < 6 ? sqrt(sqrt(ni2) / nX) : 1.0;
+    const double g = it < kPolarScaled ? sqrt(sqrt(ni2) / nX) : 1.0;
     const double ig = 1.0 / g;
     double diff = 0.0;
 #pragma unroll
@@ -270,7 +275,7 @@ __device__ inline bool polar3(const double* a, double* Q) {
       diff += (xn - X[i]) * (xn - X[i]);
       X[i] = xn;
     }
-    if (it >= 6 && diff <= 1e-30 * 3.0) {
+    if (it >= kPolarMinIt && diff <= 1e-30 * 3.0) {
 #pragma unroll
       for (int i = 0; i < 9; ++i) Q[i] = X[i];
       return true;
