@@ -13,7 +13,7 @@ step() {  # name, limit, command...
   echo "$name rc=$rc"; tail -3 gpurun_out/${TAG}_$name.log
   [ $rc -eq 0 ] || exit $rc
 }
-step pytest_gpu 600 python -u -m pytest tests/ -x -v -m gpu --timeout 120 --timeout-method thread
+[ -n "$SKIP_TESTS" ] || step pytest_gpu 600 python -u -m pytest tests/ -x -v -m gpu --timeout 120 --timeout-method thread
 step bench_pyramid 300 python bench.py --workload pyramid --no-p2plane
 step bench_sharded 300 python bench.py --workload sharded --steps 5 --warmup 1
 step bench_720p 300 python bench.py --width 1280 --height 720 --no-host-api --no-gicp
