@@ -30,7 +30,10 @@ int rst_debug_queue_trace(rst_ctx* ctx, int32_t* out, int32_t n);
  * adjacency first, 23 = both then the walk.  warm = original target indices
  * (may be NULL); path[i] & 15 = 2, 3 or 0 (which strategy answered),
  * path[i] >> 4 = the search's shader cycles / 16.  Results equal
- * rst_target_query_nn's. */
+ * rst_target_query_nn's.  mode 1000: the ICP loop's two-nearest search
+ * (level 2, level 3, walk; seeded with the warm point and its sorted
+ * neighbour): idx/d2 as above, path[i] = the float bits of the
+ * second-nearest d2 (FLT_MAX when m == 1). */
 int rst_debug_query_nn_fallback(rst_ctx* ctx, const rst_target* tgt, const float* q,
                                 int64_t nq, const int32_t* warm, int mode, int32_t* idx,
                                 float* d2, int32_t* path);

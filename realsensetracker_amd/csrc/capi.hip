@@ -416,7 +416,9 @@ int rst_debug_query_nn_fallback(rst_ctx* ctx, const rst_target* t, const float* 
                                 const int32_t* warm, int mode, int32_t* idx, float* d2,
                                 int32_t* path) {
   if (!ctx || !t || nq < 0 || (nq > 0 && (!q || !idx || !d2 || !path))) return RST_E_ARG;
-  if (mode != 0 && mode != 2 && mode != 3 && mode != 23 && (mode < 100 || mode > 102)) return RST_E_ARG;
+  if (mode != 0 && mode != 2 && mode != 3 && mode != 23 && (mode < 100 || mode > 102) &&
+      mode != 1000)
+    return RST_E_ARG;
   if (nq == 0) return RST_OK;
   if (t->m == 0) return RST_E_ARG;
   RST_HIP(hipSetDevice(ctx->device));

@@ -32,6 +32,19 @@ namespace {
 constexpr int kBS = 256;
 constexpr int kNP2Point = 16;  // sum w q u^T (9), sum w u (3), sum q (3), sum d2
 constexpr int kNP2Plane = 30;  // A (21), b (6), sum w r^2, count, sum d2
+// Far-point certificates.  The fallback search keeps the two nearest: its
+// answer p at q0 and a lower bound g (the second distance, less a margin)
+// on the distance from q0 to every other point.  In a later iteration the
+// same source point at q is certified to have p as its exact nearest
+// neighbour when |q - p| + |q - q0| < g (triangle inequality: every other
+// point lies at >= g - |q - q0| > |q - p| from q; relative margins 1e-5
+// cover the float arithmetic, and the strict gap excludes ties), with no
+// search.  nnpos carries kCertBit while the certificate of its point holds.
+#ifndef RST_FB_MIN_WAVES
+#define RST_FB_MIN_WAVES 4  // k_icp_fb<P2PointAcc>: 128 VGPRs (1 spill); r01h A/B 15.8k -> 16.2k it/s
+#endif
+constexpr int kCertBit = 1 << 30;
+constexpr int kPosMask = kCertBit - 1;
 constexpr int kFbBlocks = 2048;  // largest fallback grid (RST_FB_BLOCKS)
 constexpr int kFbDefault = 1024;  // fallback grid (4096 waves; r01g sweep: 2048 / 512 lose)
 // From a queue of lane_min entries (IcpParams; 3/4 of the source points: the
@@ -209,6 +222,7 @@ struct P2PointAcc {
   static constexpr int NV = kNP2Point;  // sum w q u^T (9), sum w u (3), sum q (3), sum d2
   static constexpr int RS = 16;         // slab row stride (doubles; divides kRedBS)
   static constexpr int kMinWaves = 5;   // k_icp_nn occupancy (waves/SIMD): one round of waves
+  static constexpr int kFbMinWaves = RST_FB_MIN_WAVES;  // k_icp_fb occupancy
   static constexpr bool kCanFinish = false;
   // q = the neighbour's coordinates (the caller has them), bp its sorted
   // position; no neighbour (bp < 0) -> dst[0], d2 = FLT_MAX
@@ -237,6 +251,7 @@ struct P2PlaneAcc {
   static constexpr int NV = kNP2Plane;  // A (21), b (6), sum w r^2, count, sum d2
   static constexpr int RS = 32;
   static constexpr int kMinWaves = 4;
+  static constexpr int kFbMinWaves = 1;
   static constexpr bool kCanFinish = true;
   __device__ static void add(double (&v)[NV], const BvhView& bv, const AccArgs& a, const Uni& u,
                              const float4& s, float px, float py, float pz, float bd, int bp,
@@ -323,6 +338,7 @@ __global__ __launch_bounds__(kBS, Acc::kMinWaves) void k_icp_nn(BvhView bv, AdjV
                                                 const float4* __restrict__ src, int64_t n,
                                                 const IcpState* __restrict__ st,
                                                 int32_t* __restrict__ nnpos,
+                                                const float4* __restrict__ cert,
                                                 int32_t* __restrict__ qbuf,
                                                 int32_t* __restrict__ qcnt,
                                                 double* __restrict__ slab) {
@@ -344,6 +360,8 @@ __global__ __launch_bounds__(kBS, Acc::kMinWaves) void k_icp_nn(BvhView bv, AdjV
   const bool fin = finite3(px, py, pz);
   // :112 exact 1-NN, starting from last iteration's neighbour
   int warm = act ? nnpos[i] : -1;
+  const bool has_cert = warm >= 0 && (warm & kCertBit);
+  if (warm >= 0) warm &= kPosMask;
   if (act && fin && warm < 0) warm = morton_seed(bv, px, py, pz);
   Best1 r;
   r.init();
@@ -351,7 +369,15 @@ __global__ __launch_bounds__(kBS, Acc::kMinWaves) void k_icp_nn(BvhView bv, AdjV
     const float4 w = bv.pts[warm];
     r.offer(d2_ref(px, py, pz, w.x, w.y, w.z), f2i(w.w), warm);
   }
-  const bool done = act && (!fin || adj_search_wide(bv, av, warm, px, py, pz, r));
+  bool certified = false;
+  if (act && fin && has_cert) {  // far point: its certificate (kCertBit)
+    const float4 c = cert[i];
+    const float dx = px - c.x, dy = py - c.y, dz = pz - c.z;
+    const float moved = sqrtf((dx * dx + dy * dy) + dz * dz) * 1.00001f;
+    certified = sqrtf(r.d) * 1.00001f + moved + 1e-30f < c.w;
+  }
+  const bool done =
+      act && (!fin || certified || adj_search_wide(bv, av, warm, px, py, pz, r));
   // lanes the adjacency could not certify go to the fallback queue, in
   // point order within the block's segment
   const bool need = act && !done;
@@ -368,7 +394,8 @@ __global__ __launch_bounds__(kBS, Acc::kMinWaves) void k_icp_nn(BvhView bv, AdjV
   if (need) qbuf[blockIdx.x * (int64_t)kBS + before + __popcll(bm & ((1ull << lane) - 1ull))] = (int)i;
   if (threadIdx.x == 0) qcnt[blockIdx.x] = total;
   if (done) {
-    nnpos[i] = r.pos;
+    // the certificate stays valid while its point is the answer
+    nnpos[i] = r.pos | (has_cert && r.pos == warm ? kCertBit : 0);
     Acc::add(v, bv, aa, u, s, px, py, pz, r.d, r.pos, bv.pts[r.pos >= 0 ? r.pos : 0]);
   }
   block_sum_to_slab<Acc::NV, kBS>(v, lds, slab + (int64_t)blockIdx.x * Acc::RS);
@@ -667,10 +694,11 @@ __global__ void k_solve_only(const double* __restrict__ totals, IcpParams prm,
 // then folds kernel 1's slab rows b, b + G, ... into its own row, so the
 // solve kernel reduces G rows, not nb1 + G.  Block 0 publishes E.
 template <class Acc>
-__global__ __launch_bounds__(kBS) void k_icp_fb(BvhView bv, AdjView av, AccArgs aa,
+__global__ __launch_bounds__(kBS, Acc::kFbMinWaves) void k_icp_fb(BvhView bv, AdjView av, AccArgs aa,
                                                 const float4* __restrict__ src,
                                                 IcpState* __restrict__ st,
                                                 int32_t* __restrict__ nnpos,
+                                                float4* __restrict__ cert,
                                                 const int32_t* __restrict__ qbuf,
                                                 const int32_t* __restrict__ qcnt, int nb1,
                                                 int lane_min, const double* __restrict__ slab1,
@@ -709,6 +737,7 @@ __global__ __launch_bounds__(kBS) void k_icp_fb(BvhView bv, AdjView av, AccArgs 
       xform(u.P, s.x, s.y, s.z, px, py, pz);
       const bool fin = finite3(px, py, pz);
       int warm = nnpos[i];
+      if (warm >= 0) warm &= kPosMask;
       if (fin && warm < 0) warm = morton_seed(bv, px, py, pz);
       Best1 r;
       r.init();
@@ -739,21 +768,32 @@ __global__ __launch_bounds__(kBS) void k_icp_fb(BvhView bv, AdjView av, AccArgs 
       xform(u.P, s.x, s.y, s.z, px, py, pz);
       const bool fin = finite3(px, py, pz);
       int warm = nnpos[i];
+      if (warm >= 0) warm &= kPosMask;
       if (fin && warm < 0) warm = morton_seed(bv, px, py, pz);
-      Best1 r;
-      r.init();
+      // the two nearest (their gap is the point's certificate), seeded with
+      // the warm point and its sorted neighbour so the bound starts finite
+      Best2 r2;
+      r2.init();
       if (fin) {
         const float4 w = bv.pts[warm];
-        r.offer(d2_ref(px, py, pz, w.x, w.y, w.z), f2i(w.w), warm);
+        r2.offer(d2_ref(px, py, pz, w.x, w.y, w.z), f2i(w.w), warm);
+        if (bv.m > 1) {
+          const int nb = warm + 1 < bv.m ? warm + 1 : warm - 1;
+          const float4 w2 = bv.pts[nb];
+          r2.offer(d2_ref(px, py, pz, w2.x, w2.y, w2.z), f2i(w2.w), nb);
+        }
       }
       // the level-2 and level-3 adjacency cover most far queries in a few
       // memory round trips; the full walk from the warm leaf is exact for
       // anything else
-      if (!nn_wave_adj(bv, av, kAdj2Shift, warm, px, py, pz, r, wsc[wid]) &&
-          !nn_wave_adj(bv, av, kAdj3Shift, warm, px, py, pz, r, wsc[wid]))
-        nn_wave_one(bv, warm, px, py, pz, r, wsc[wid]);
+      if (!nn_wave_adj(bv, av, kAdj2Shift, warm, px, py, pz, r2, wsc[wid]) &&
+          !nn_wave_adj(bv, av, kAdj3Shift, warm, px, py, pz, r2, wsc[wid]))
+        nn_wave_one(bv, warm, px, py, pz, r2, wsc[wid]);
+      const Best1 r = r2.first();
       if (lane == 0) {
-        nnpos[i] = r.pos;
+        const bool cok = fin && r.pos >= 0;
+        nnpos[i] = cok ? (r.pos | kCertBit) : r.pos;
+        if (cok) cert[i] = make_float4(px, py, pz, sqrtf(r2.d[1]) * 0.99999f);
         Acc::add(v, bv, aa, u, s, px, py, pz, r.d, r.pos, bv.pts[r.pos >= 0 ? r.pos : 0]);
       }
     }
@@ -841,6 +881,7 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
   if (opts.mode != RST_P2POINT_REF && opts.mode != RST_P2PLANE) return RST_E_ARG;
   if (opts.max_iter < 0) return RST_E_ARG;
   if (!tgt->has_bvh) return RST_E_ARG;
+  if (tgt->m >= kCertBit) return RST_E_ARG;  // positions carry kCertBit
   if (p2plane && !tgt->nrm) return RST_E_STATE;
   const int64_t n_local = src->m;
   int64_t n_total = n_local;
@@ -897,12 +938,15 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
   // start of the next iteration's exact search; -1 = cold); the fallback
   // queue (one kBS segment per kernel-1 block) and its per-block counts
   int32_t *nnpos = nullptr, *qbuf = nullptr, *qcnt = nullptr;
+  float4* cert = nullptr;  // far-point certificates (read only under kCertBit)
   {
     const size_t np = (size_t)std::max<int64_t>(n_local, 1);
     const size_t nq = (size_t)nblk * kBS;
     void* w = nullptr;
-    RST_CHECK(ctx_workspace(ctx, sizeof(int32_t) * (np + nq + 2 * nblk + 64), &w));
-    nnpos = (int32_t*)w;
+    RST_CHECK(ctx_workspace(ctx, sizeof(float4) * np + sizeof(int32_t) * (np + nq + 2 * nblk + 64),
+                            &w));
+    cert = (float4*)w;
+    nnpos = (int32_t*)(cert + np);
     qbuf = nnpos + np;
     qcnt = qbuf + nq;
     RST_HIP(hipMemsetAsync(nnpos, 0xff, sizeof(int32_t) * np, st));
@@ -956,19 +1000,19 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
     if (n_local > 0) {
       if (p2plane) {
         k_icp_nn<P2PlaneAcc><<<nblk, kBS, 0, st>>>(bv, av, aa, src->pts, n_local, ctx->d_state,
-                                                   nnpos, qbuf, qcnt, slab);
+                                                   nnpos, cert, qbuf, qcnt, slab);
         if (tm) RST_HIP(hipEventRecord(ctx->ev[2 * it + 1], st));
         k_icp_fb<P2PlaneAcc><<<fb_grid, kBS, fb_lds, st>>>(bv, av, aa, src->pts, ctx->d_state,
-                                                             nnpos, qbuf, qcnt, nblk,
+                                                             nnpos, cert, qbuf, qcnt, nblk,
                                                              prm.lane_min, slab, slab2);
         k_reduce_solve<P2PlaneAcc><<<1, kRedBS, 0, st>>>(slab, 0, slab2, fb_grid, prm,
                                                          ctx->d_state, red_out);
       } else {
         k_icp_nn<P2PointAcc><<<nblk, kBS, 0, st>>>(bv, av, aa, src->pts, n_local, ctx->d_state,
-                                                   nnpos, qbuf, qcnt, slab);
+                                                   nnpos, cert, qbuf, qcnt, slab);
         if (tm) RST_HIP(hipEventRecord(ctx->ev[2 * it + 1], st));
         k_icp_fb<P2PointAcc><<<fb_grid, kBS, fb_lds, st>>>(bv, av, aa, src->pts, ctx->d_state,
-                                                             nnpos, qbuf, qcnt, nblk,
+                                                             nnpos, cert, qbuf, qcnt, nblk,
                                                              prm.lane_min, slab, slab2);
         k_reduce_solve<P2PointAcc><<<1, kRedBS, 0, st>>>(slab, 0, slab2, fb_grid, prm,
                                                          ctx->d_state, red_out);

@@ -85,12 +85,36 @@ __global__ __launch_bounds__(kBS) void k_query_nn_fallback(BvhView bv, AdjView a
   if (i >= nq) return;  // wave-uniform
   const uint64_t t0 = __builtin_amdgcn_s_memtime();
   const float qx = q[3 * i], qy = q[3 * i + 1], qz = q[3 * i + 2];
-  Best1 r;
-  r.init();
   int start = -1;
   const int w = warm ? warm[i] : -1;
-  if (w >= 0 && w < bv.m && finite3(qx, qy, qz)) {
-    start = inv[w];
+  const bool seeded = w >= 0 && w < bv.m && finite3(qx, qy, qz);
+  if (seeded) start = inv[w];
+  if (mode >= 1000) {  // the two nearest, seeded like the ICP loop (warm + its sorted neighbour)
+    Best2 r2;
+    r2.init();
+    if (seeded) {
+      const float4 p = bv.pts[start];
+      r2.offer(d2_ref(qx, qy, qz, p.x, p.y, p.z), f2i(p.w), start);
+      if (bv.m > 1) {
+        const int nb = start + 1 < bv.m ? start + 1 : start - 1;
+        const float4 p2 = bv.pts[nb];
+        r2.offer(d2_ref(qx, qy, qz, p2.x, p2.y, p2.z), f2i(p2.w), nb);
+      }
+    }
+    if (!nn_wave_adj(bv, av, kAdj2Shift, start, qx, qy, qz, r2, wsc[wid]) &&
+        !nn_wave_adj(bv, av, kAdj3Shift, start, qx, qy, qz, r2, wsc[wid]))
+      nn_wave_one(bv, start, qx, qy, qz, r2, wsc[wid]);
+    if (lane == 0) {
+      const Best1 r = r2.first();
+      idx[i] = r.id;
+      d2[i] = r.d;
+      path[i] = __float_as_int(r2.d[1]);  // the second-nearest d2 (bits)
+    }
+    return;
+  }
+  Best1 r;
+  r.init();
+  if (seeded) {
     const float4 p = bv.pts[start];
     r.offer(d2_ref(qx, qy, qz, p.x, p.y, p.z), f2i(p.w), start);
   }

@@ -175,6 +175,41 @@ struct Best1 {
   }
 };
 
+// The two best (d2, id), sorted.  Offering a point already held (same id)
+// changes nothing, so every lane of a wave may start from the same entries
+// and a wave merge (wave_lex_min) may see a point twice.  bound() is the
+// second distance: a search pruned with it finds both exactly.
+struct Best2 {
+  float d[2];
+  int id[2];
+  int pos[2];
+  RST_HD void init() {
+    d[0] = d[1] = FLT_MAX;
+    id[0] = id[1] = 0x7fffffff;
+    pos[0] = pos[1] = -1;
+  }
+  RST_HD float bound() const { return d[1]; }
+  RST_HD float radius() const { return sqrtf(d[1]); }
+  RST_HD void offer(float nd, int nid, int np) {
+    // (nid == id[1] is never lex_less than itself)
+    const bool b1 = (nid != id[0]) && lex_less(nd, nid, d[1], id[1]);
+    const bool b0 = b1 && lex_less(nd, nid, d[0], id[0]);
+    d[1] = b0 ? d[0] : (b1 ? nd : d[1]);
+    id[1] = b0 ? id[0] : (b1 ? nid : id[1]);
+    pos[1] = b0 ? pos[0] : (b1 ? np : pos[1]);
+    d[0] = b0 ? nd : d[0];
+    id[0] = b0 ? nid : id[0];
+    pos[0] = b0 ? np : pos[0];
+  }
+  RST_HD Best1 first() const {
+    Best1 b;
+    b.d = d[0];
+    b.id = pos[0] >= 0 ? id[0] : 0;
+    b.pos = pos[0];
+    return b;
+  }
+};
+
 // K best, sorted; branch-free insertion with static indices (registers).
 template <int K>
 struct BestK {

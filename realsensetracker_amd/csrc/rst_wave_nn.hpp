@@ -411,6 +411,39 @@ __device__ __forceinline__ Best1 wave_lex_min(Best1 b) {
   return b;
 }
 
+// Wave merge of Best2 lists (sorted, distinct ids within each): the merge
+// is commutative, so every lane ends with the same two entries; a point
+// held by both lists (same id) counts once.
+__device__ __forceinline__ Best2 wave_lex_min(Best2 b) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float od0 = __shfl_xor(b.d[0], o, 64), od1 = __shfl_xor(b.d[1], o, 64);
+    const int oi0 = __shfl_xor(b.id[0], o, 64), oi1 = __shfl_xor(b.id[1], o, 64);
+    const int op0 = __shfl_xor(b.pos[0], o, 64), op1 = __shfl_xor(b.pos[1], o, 64);
+    const bool of = lex_less(od0, oi0, b.d[0], b.id[0]);  // the other list leads
+    const float fd = of ? od0 : b.d[0];
+    const int fi = of ? oi0 : b.id[0], fp = of ? op0 : b.pos[0];
+    // second: the leader's second, or the other head (its second when the
+    // two heads are the same point)
+    const float wd = of ? od1 : b.d[1];
+    const int wi = of ? oi1 : b.id[1], wp = of ? op1 : b.pos[1];
+    const float hd = of ? b.d[0] : od0, h2d = of ? b.d[1] : od1;
+    const int hi = of ? b.id[0] : oi0, h2i = of ? b.id[1] : oi1;
+    const int hp = of ? b.pos[0] : op0, h2p = of ? b.pos[1] : op1;
+    const bool dup = hi == fi;
+    const float cd = dup ? h2d : hd;
+    const int ci = dup ? h2i : hi, cp = dup ? h2p : hp;
+    const bool c2 = lex_less(cd, ci, wd, wi);
+    b.d[0] = fd;
+    b.id[0] = fi;
+    b.pos[0] = fp;
+    b.d[1] = c2 ? cd : wd;
+    b.id[1] = c2 ? ci : wi;
+    b.pos[1] = c2 ? cp : wp;
+  }
+  return b;
+}
+
 // Scan the staged leaves [0, ns) (ws.leaf_lo[s] = (box_d2, -, -, leaf bits))
 // for one query: leaf ranges first (one load per leaf, all lanes), then the
 // points 32 leaves at a time -- lanes 16g..16g+15 take leaf s+g's points,

@@ -394,7 +394,7 @@ def test_solve_kabsch_device_contract(ctx):
 
 
 # ---- the ICP fallback search (k_icp_fb's per-query strategies) ------------------------
-def _fallback(ctx, t, q, warm, mode):
+def _fallback(ctx, t, q, warm, mode, raw=False):
     n = len(q)
     idx = np.zeros(n, np.int32)
     d2 = np.zeros(n, np.float32)
@@ -407,7 +407,7 @@ def _fallback(ctx, t, q, warm, mode):
     w = None if warm is None else np.ascontiguousarray(warm, np.int32)
     L.check(f(ctx.handle, t.handle, L.fptr(q), n, None if w is None else L.iptr(w), mode,
               L.iptr(idx), L.fptr(d2), L.iptr(path)), "fallback")
-    return idx, d2, path & 15
+    return idx, d2, (path if raw else path & 15)
 
 
 @pytest.fixture(scope="module")
@@ -440,6 +440,43 @@ def test_icp_fallback_search_bitexact(ctx, frame_640, mode):
         paths.append(path)
     if mode in (2, 23):  # with a good warm point the level-2 index answers many
         assert np.mean(paths[0] == 2) > 0.2
+
+
+def test_icp_fallback_two_nearest_bitexact(ctx, frame_640):
+    """The ICP fallback's two-nearest search (far-point certificates): the
+    nearest (d2, index) and the second d2 exactly as the oracle's 2-NN."""
+    pa, pb, t, tree = frame_640
+    rng = np.random.default_rng(7)
+    sel = rng.choice(len(pb), 2000, replace=False)
+    off = rng.normal(size=(2000, 3)).astype(np.float32)
+    off *= (10 ** rng.uniform(-3, np.log10(0.5), 2000)).astype(np.float32)[:, None] / np.linalg.norm(off, axis=1, keepdims=True)
+    q = (pb[sel] + off).astype(np.float32)
+    q = np.concatenate([q, pa[:50]])  # exact hits (d2 = 0)
+    oi, od = tree.query(q, k=2)
+    gi0, _ = tree.query(pb[sel])
+    warms = (np.concatenate([gi0, np.arange(50)]).astype(np.int32),
+             rng.integers(0, len(pa), len(q)).astype(np.int32), None)
+    for warm in warms:
+        gi, gd, path = _fallback(ctx, t, q, warm, 1000, raw=True)
+        assert np.array_equal(gi, oi[:, 0]) and np.array_equal(gd, od[:, 0])
+        assert np.array_equal(path.view(np.float32), od[:, 1])
+
+
+def test_far_point_certificates_keep_the_loop_exact(ctx):
+    """A 640x480 pair at 128 iterations (far points certified from their
+    2nd-neighbour gap after their first fallback search) tracks the fp64-sum
+    oracle like the plain search did."""
+    K = driver.intrinsics(640, 480)
+    sc = driver.SyntheticScene(0)
+    da = sc.render(sc.trajectory(0), K, noise_seed=1)
+    db = sc.render(sc.trajectory(1), K, noise_seed=2)
+    K4 = [K.fx, K.fy, K.cx, K.cy]
+    pa, pb = O.unproject(da, K4), O.unproject(db, K4)
+    tgt = A.Target.build(pa, ctx)
+    T = np.eye(4, dtype=np.float32)
+    assert A.AlignIcp3d(pb, pa, tgt, 128, T)
+    _, To, _, _ = O.align_icp(pb, pa, 128, tree=O.KDTree(pa), sum_mode=1)
+    assert max(pose_err(T, To)) <= 2e-5, pose_err(T, To)
 
 
 # ---- several frame pairs in flight (one context / stream each) -----------------------
