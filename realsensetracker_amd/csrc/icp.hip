@@ -974,7 +974,14 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
   prm.p2plane_max_d2 = opts.p2plane_max_dist > 0 ? opts.p2plane_max_dist * opts.p2plane_max_dist
                                                  : FLT_MAX;
   prm.max_iter = opts.max_iter;
-  prm.lane_min = (int)std::max<int64_t>(16384, (3 * n_local) / 4);
+  // queue length from which the fallback runs one lane per query
+  // (RST_LANE_MIN_DIV = k: n / k; tuning knob -- r01h sweep: 3n/4 is best)
+  static const int lane_div = [] {
+    const char* e = getenv("RST_LANE_MIN_DIV");
+    return e ? atoi(e) : 0;
+  }();
+  prm.lane_min = (int)std::max<int64_t>(
+      16384, lane_div > 0 ? n_local / lane_div : (3 * n_local) / 4);
 
   const BvhView bv = view_of(tgt);
 

@@ -876,3 +876,27 @@ def test_hipgraph_mode_matches_stream_mode(ctx):
         assert np.array_equal(r.pose, r0.pose)
     finally:
         gctx.close()
+
+
+@pytest.mark.parametrize("mode", [L.RST_P2POINT_REF, L.RST_P2PLANE])
+def test_frame_targets_equal_host_targets(ctx, mode):
+    """Frames prepared from depth on the device and clouds built from the
+    same host points give identical poses (both modes)."""
+    torch = pytest.importorskip("torch")
+    for name in PAIR_NAMES:
+        g = load_golden(name)
+        K, _ = _pair_intrinsics(g)
+        da = torch.from_numpy(g["depth_a"].astype(np.int16)).cuda()
+        db = torch.from_numpy(g["depth_b"].astype(np.int16)).cuda()
+        torch.cuda.synchronize()
+        nk = 16 if mode == L.RST_P2PLANE else 0
+        tf = A.Target.from_depth_device(da.data_ptr(), K, nk, ctx)
+        sf = A.Target.from_depth_device(db.data_ptr(), K, nk, ctx)
+        th, sh = A.Target.build(g["dst"], ctx), A.Target.build(g["src"], ctx)
+        if nk:
+            th.compute_normals(16)
+        o = L.default_opts(mode=mode, max_iter=128 if mode == L.RST_P2POINT_REF else 30)
+        rf = A.align_prepared(sf, tf, None, o)
+        rh = A.align_prepared(sh, th, None, o)
+        assert np.array_equal(rf.pose, rh.pose), name
+        assert rf.ok == rh.ok and rf.iterations == rh.iterations
