@@ -44,6 +44,29 @@ constexpr int kNP2Plane = 30;  // A (21), b (6), sum w r^2, count, sum d2
 #define RST_FB_MIN_WAVES 4  // k_icp_fb<P2PointAcc>: 128 VGPRs (1 spill); r01h A/B 15.8k -> 16.2k it/s
 #endif
 constexpr int kCertBit = 1 << 30;
+#ifndef RST_XCD_REMAP
+#define RST_XCD_REMAP 0  // off: r01i A/B 16.2k -> 16.0k it/s, pyramid level-0 k_icp_nn 140 -> 174 us
+#endif
+// XCD-aware tile order of k_icp_nn (speed only, never correctness): blocks
+// are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md), so block b
+// takes tile xcd_tile(b) and each XCD walks one contiguous eighth of the
+// Morton-ordered source, whose neighbours are one region of the target: its
+// lines are fetched into one XCD's L2 instead of all eight.  Bijective for
+// any nb; the slab row and queue segment are the tile's, so the sums and
+// the queue order are the same as without the remap.  Measured slower: with
+// round-robin placement the blocks in flight at any moment cover one compact
+// stretch of the Morton order, whose target lines all eight L2s (and the
+// MALL) share; the remap spreads them over eight stretches at once.
+__device__ __forceinline__ int xcd_tile(int b, int nb) {
+#if RST_XCD_REMAP
+  const int x = b & 7, j = b >> 3, per = nb >> 3, rem = nb & 7;
+  return (x < rem ? x * (per + 1) : rem * (per + 1) + (x - rem) * per) + j;
+#else
+  (void)nb;
+  return b;
+#endif
+}
+
 constexpr int kPosMask = kCertBit - 1;
 constexpr int kFbBlocks = 2048;  // largest fallback grid (RST_FB_BLOCKS)
 constexpr int kFbDefault = 1024;  // fallback grid (4096 waves; r01g sweep: 2048 / 512 lose)
@@ -344,15 +367,16 @@ __global__ __launch_bounds__(kBS, Acc::kMinWaves) void k_icp_nn(BvhView bv, AdjV
                                                 double* __restrict__ slab) {
   __shared__ double lds[(kBS / kWave) * Acc::NV];
   __shared__ int wq[kBS / kWave];
+  const int tb = xcd_tile(blockIdx.x, gridDim.x);
   if (Acc::kCanFinish && st->done) {  // converged: uniform early exit
-    if (threadIdx.x == 0) qcnt[blockIdx.x] = 0;
+    if (threadIdx.x == 0) qcnt[tb] = 0;
     return;
   }
   const Uni u = load_uni(st);
   double v[Acc::NV];
 #pragma unroll
   for (int k = 0; k < Acc::NV; ++k) v[k] = 0.0;
-  const int64_t i = blockIdx.x * (int64_t)kBS + threadIdx.x;
+  const int64_t i = tb * (int64_t)kBS + threadIdx.x;
   const bool act = i < n;
   const float4 s = act ? src[i] : make_float4(0.f, 0.f, 0.f, 0.f);
   float px, py, pz;
@@ -391,14 +415,14 @@ __global__ __launch_bounds__(kBS, Acc::kMinWaves) void k_icp_nn(BvhView bv, AdjV
     before += w < wid ? wq[w] : 0;
     total += wq[w];
   }
-  if (need) qbuf[blockIdx.x * (int64_t)kBS + before + __popcll(bm & ((1ull << lane) - 1ull))] = (int)i;
-  if (threadIdx.x == 0) qcnt[blockIdx.x] = total;
+  if (need) qbuf[tb * (int64_t)kBS + before + __popcll(bm & ((1ull << lane) - 1ull))] = (int)i;
+  if (threadIdx.x == 0) qcnt[tb] = total;
   if (done) {
     // the certificate stays valid while its point is the answer
     nnpos[i] = r.pos | (has_cert && r.pos == warm ? kCertBit : 0);
     Acc::add(v, bv, aa, u, s, px, py, pz, r.d, r.pos, bv.pts[r.pos >= 0 ? r.pos : 0]);
   }
-  block_sum_to_slab<Acc::NV, kBS>(v, lds, slab + (int64_t)blockIdx.x * Acc::RS);
+  block_sum_to_slab<Acc::NV, kBS>(v, lds, slab + (int64_t)tb * Acc::RS);
 }
 
 // Kabsch solve (align_icp.cpp:139-151; SolveKabsch :58-69): fp64 SVD,
