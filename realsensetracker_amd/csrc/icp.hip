@@ -44,6 +44,9 @@ constexpr int kNP2Plane = 30;  // A (21), b (6), sum w r^2, count, sum d2
 #define RST_FB_MIN_WAVES 4  // k_icp_fb<P2PointAcc>: 128 VGPRs (1 spill); r01h A/B 15.8k -> 16.2k it/s
 #endif
 constexpr int kCertBit = 1 << 30;
+#ifndef RST_NN_MIN_WAVES
+#define RST_NN_MIN_WAVES 5  // k_icp_nn<P2PointAcc>: one round of waves at 640x480; r01i A/B: 6 -> 15.5k, 8 -> 14.2k it/s (vs 16.2k)
+#endif
 #ifndef RST_XCD_REMAP
 #define RST_XCD_REMAP 0  // off: r01i A/B 16.2k -> 16.0k it/s, pyramid level-0 k_icp_nn 140 -> 174 us
 #endif
@@ -244,7 +247,7 @@ struct AccArgs {
 struct P2PointAcc {
   static constexpr int NV = kNP2Point;  // sum w q u^T (9), sum w u (3), sum q (3), sum d2
   static constexpr int RS = 16;         // slab row stride (doubles; divides kRedBS)
-  static constexpr int kMinWaves = 5;   // k_icp_nn occupancy (waves/SIMD): one round of waves
+  static constexpr int kMinWaves = RST_NN_MIN_WAVES;  // k_icp_nn occupancy (waves/SIMD)
   static constexpr int kFbMinWaves = RST_FB_MIN_WAVES;  // k_icp_fb occupancy
   static constexpr bool kCanFinish = false;
   // q = the neighbour's coordinates (the caller has them), bp its sorted
