@@ -47,6 +47,9 @@ constexpr int kCertBit = 1 << 30;
 #ifndef RST_NN_MIN_WAVES
 #define RST_NN_MIN_WAVES 5  // k_icp_nn<P2PointAcc>: one round of waves at 640x480; r01i A/B: 6 -> 15.5k, 8 -> 14.2k it/s (vs 16.2k)
 #endif
+#ifndef RST_QUEUE_WARM
+#define RST_QUEUE_WARM 1
+#endif
 #ifndef RST_XCD_REMAP
 #define RST_XCD_REMAP 0  // off: r01i A/B 16.2k -> 16.0k it/s, pyramid level-0 k_icp_nn 140 -> 174 us
 #endif
@@ -419,6 +422,12 @@ __global__ __launch_bounds__(kBS, Acc::kMinWaves) void k_icp_nn(BvhView bv, AdjV
     total += wq[w];
   }
   if (need) qbuf[tb * (int64_t)kBS + before + __popcll(bm & ((1ull << lane) - 1ull))] = (int)i;
+#if RST_QUEUE_WARM
+  // a queued lane hands the fallback the nearest point its scan saw (at
+  // least as near as the warm point): a tighter starting bound and a warm
+  // leaf nearer the query (any start keeps the fallback's search exact)
+  if (need) nnpos[i] = r.pos;
+#endif
   if (threadIdx.x == 0) qcnt[tb] = total;
   if (done) {
     // the certificate stays valid while its point is the answer
