@@ -1011,13 +1011,16 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
                                                  : FLT_MAX;
   prm.max_iter = opts.max_iter;
   // queue length from which the fallback runs one lane per query
-  // (RST_LANE_MIN_DIV = k: n / k; tuning knob -- r01h sweep: 3n/4 is best)
+  // (RST_LANE_MIN_DIV = k: n / k; tuning knob -- r01h sweep: 3n/4 was best;
+  // r01j, with queued lanes seeding the fallback: n/3 17.0k, n/4 17.1k, n/2
+  // 16.8k, 3n/4 16.6k it/s on the 640x480 stream, the 720p pyramid 14.0k /
+  // 13.9k / 14.0k / 14.25k)
   static const int lane_div = [] {
     const char* e = getenv("RST_LANE_MIN_DIV");
     return e ? atoi(e) : 0;
   }();
   prm.lane_min = (int)std::max<int64_t>(
-      16384, lane_div > 0 ? n_local / lane_div : (3 * n_local) / 4);
+      16384, lane_div > 0 ? n_local / lane_div : n_local / 3);
 
   const BvhView bv = view_of(tgt);
 
