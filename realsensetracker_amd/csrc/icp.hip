@@ -41,7 +41,7 @@ constexpr int kNP2Plane = 30;  // A (21), b (6), sum w r^2, count, sum d2
 // cover the float arithmetic, and the strict gap excludes ties), with no
 // search.  nnpos carries kCertBit while the certificate of its point holds.
 #ifndef RST_FB_MIN_WAVES
-#define RST_FB_MIN_WAVES 4  // k_icp_fb<P2PointAcc>: 128 VGPRs (1 spill); r01h A/B 15.8k -> 16.2k it/s
+#define RST_FB_MIN_WAVES 4  // k_icp_fb<P2PointAcc>: 128 VGPRs (1 spill); r01h A/B 15.8k -> 16.2k it/s; r01k: 3 -> 16.7k, 5 -> 15.6k vs 17.1k
 #endif
 constexpr int kCertBit = 1 << 30;
 #ifndef RST_NN_MIN_WAVES
