@@ -50,6 +50,9 @@ constexpr int kCertBit = 1 << 30;
 #ifndef RST_QUEUE_WARM
 #define RST_QUEUE_WARM 1
 #endif
+#ifndef RST_LANE_SMALL_N
+#define RST_LANE_SMALL_N 150000  // clouds below this keep the 3n/4 lane-mode threshold (720p pyramid coarse levels; r01k A/B 14.0k -> 14.2k it/s)
+#endif
 #ifndef RST_XCD_REMAP
 #define RST_XCD_REMAP 0  // off: r01i A/B 16.2k -> 16.0k it/s, pyramid level-0 k_icp_nn 140 -> 174 us
 #endif
@@ -1020,7 +1023,8 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
     return e ? atoi(e) : 0;
   }();
   prm.lane_min = (int)std::max<int64_t>(
-      16384, lane_div > 0 ? n_local / lane_div : n_local / 3);
+      16384, lane_div > 0 ? n_local / lane_div
+                          : (n_local < RST_LANE_SMALL_N ? (3 * n_local) / 4 : n_local / 3));
 
   const BvhView bv = view_of(tgt);
 
