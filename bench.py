@@ -13,14 +13,22 @@ iteration chain is launch/latency-bound, so independent pairs overlap on the
 GPU.  A second timed loop runs the build's point-to-plane mode on the same
 frames (reported as extra fields).
 
+The value line runs the throughput mode (RST_SUM_FP64: fp64 partial sums);
+the reference-rounding mode (RST_SUM_REF, the library default: sequential
+fp32 sums exactly as align_icp.cpp rounds them) is timed on the same
+stream as the extra field "ref_sums".
+
 roofline: the dominant kernel k_icp_nn (transform + exact NN + weighted
 partial sums of one ICP iteration), algorithmic bytes per launch
 12 n + 12 m + S_idx, over its average duration from HIP
 events on the aligning stream (every 8th iteration), vs 8 TB/s.  traffic =
 HBM bytes per launch from the committed PMC pass (profiles/pmc_*.json:
-FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE).  Multi-GPU: one process per GPU, each rank tracks its own
-stream (frame pairs are independent; no data-path collective) -> weak
-scaling; barrier + max-over-ranks timing.
+FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE).  Multi-GPU: one process
+per GPU -- `--gpus N` without a launcher spawns the N ranks itself
+(realsensetracker_amd/rendezvous.py), or run under torch.distributed.run --
+each rank tracks its own stream (frame pairs are independent; no data-path
+collective) -> weak scaling; barrier + max-over-ranks timing over a TCP
+rendezvous (no torch in the process: the library is its only HIP runtime).
 
 Other BASELINE configs (extra bench lines, same JSON contract):
     --width 1280 --height 720     configs[2]: the stream at 720p
@@ -53,6 +61,7 @@ sys.path.insert(0, str(ROOT))
 from realsensetracker_amd import _lib as L  # noqa: E402
 from realsensetracker_amd import align as A  # noqa: E402
 from realsensetracker_amd import driver  # noqa: E402
+from realsensetracker_amd import rendezvous as RV  # noqa: E402
 
 METRIC = "ICP iterations/sec + frames/sec, 640×480 RGB-D, 1/2/4/8 MI355X"
 # workload -> default frame size (BASELINE.json configs[1] / [4] / [3])
@@ -134,7 +143,7 @@ def p2point_alg_bytes(n: float, m: float) -> float:
     return 12 * n + 12 * m + 64 * nleaves + 4 * (nleaves + 1)
 
 
-def run_sharded(a, K, frames, d_depth, hip, world, rank, local, dist, barrier, max_over_ranks):
+def run_sharded(a, K, frames, d_depth, hip, world, rank, local, rdv, barrier, max_over_ranks):
     """configs[3]: one large scan pair (default 1000x1000 depth, ~1M points),
     the source sharded across the ranks (contiguous point ranges), the target
     index replicated; per iteration one RCCL all-reduce of the 16 fp64
@@ -151,8 +160,8 @@ def run_sharded(a, K, frames, d_depth, hip, world, rank, local, dist, barrier, m
     L.check(L.lib().rst_unproject_device(ctx.handle, d_depth[1], C.byref(K), 0, d_src,
                                          C.byref(n)), "rst_unproject_device")
     lo, hi = shard_bounds(n.value, world, rank)
-    sh = ShardedAligner(ctx) if dist is not None else ShardedAligner(ctx, world=1, rank=0)
-    opts = L.default_opts(max_iter=a.iters)
+    sh = ShardedAligner(ctx, rendezvous=rdv)
+    opts = L.default_opts(max_iter=a.iters, sum_mode=L.RST_SUM_FP64)
     ptr = d_src.value + 12 * lo
 
     def step():
@@ -209,8 +218,7 @@ def run_sharded(a, K, frames, d_depth, hip, world, rank, local, dist, barrier, m
     sh.close()
     tgt.free()
     hip.hipFree(d_src)
-    if dist is not None:
-        dist.destroy_process_group()
+    rdv.close()
 
 
 def main():
@@ -239,7 +247,12 @@ def main():
                     help="replay each align's iteration loop as a hipGraph (no kernel timing)")
     ap.add_argument("--inflight", type=int, default=2,
                     help="frame pairs in flight per GPU (one HIP stream each)")
+    ap.add_argument("--ref-steps", type=int, default=4,
+                    help="frames timed in the reference-rounding mode (extra field; 0: skip)")
     a = ap.parse_args()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        # no launcher: one rank process per GPU, spawned before any GPU call
+        return RV.launch(a.gpus, sys.argv[1:], str(Path(__file__).resolve()))
     dw, dh = WORKLOADS[a.workload]
     a.width, a.height = a.width or dw, a.height or dh
     pyr = a.workload == "pyramid"
@@ -247,33 +260,19 @@ def main():
     if pyr and len(pyr_iters) != a.levels:
         ap.error("--pyr-iters needs one count per level")
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist  # gloo: timing/barrier only, no data path
-        dist.init_process_group("gloo")
+    world, rank, local = RV.world_from_env()
+    if world > 1 and a.gpus != world:
+        ap.error(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+    rdv = RV.Rendezvous(rank, world)  # barrier / timing only, no data path
 
     def barrier():
-        if dist is not None:
-            dist.barrier()
+        rdv.barrier()
 
     def max_over_ranks(x: float) -> float:
-        if dist is None:
-            return x
-        import torch
-        t = torch.tensor([x], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item())
+        return float(rdv.allreduce([x], "max")[0])
 
     def sum_over_ranks(x: float) -> float:
-        if dist is None:
-            return x
-        import torch
-        t = torch.tensor([x], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        return float(t.item())
+        return float(rdv.allreduce([x], "sum")[0])
 
     K = driver.intrinsics(a.width, a.height)
     nfr = max(2, a.frames if a.frames > 0 else min(512, max(a.steps, a.warmup) + 1))
@@ -292,10 +291,11 @@ def main():
         d_depth.append(p)
 
     if a.workload == "sharded":
-        return run_sharded(a, K, frames, d_depth, hip, world, rank, local, dist, barrier,
+        return run_sharded(a, K, frames, d_depth, hip, world, rank, local, rdv, barrier,
                            max_over_ranks)
 
-    opts_ref = L.default_opts(max_iter=a.iters)
+    opts_ref = L.default_opts(max_iter=a.iters, sum_mode=L.RST_SUM_FP64)
+    opts_exact = L.default_opts(max_iter=a.iters, sum_mode=L.RST_SUM_REF)
     opts_pl = L.default_opts(mode=L.RST_P2PLANE, max_iter=30)
     # frame preparation on its own context (stream); each frame pair in
     # flight on its own context, so the latency-bound per-iteration chains
@@ -396,6 +396,26 @@ def main():
               "ms_per_pair": 1000.0 * dtp / a.steps,
               "k_p2plane_avg_us": 1000.0 * sp["kernel_ms"] / max(1, sp["launches"])}
 
+    # ---- reference-rounding mode (RST_SUM_REF; extra field, not value) ----------
+    refs = None
+    if a.ref_steps > 0 and not pyr:
+        run(1, opts_exact, 0, None)
+        sr = {"iters": 0, "n": 0, "m": 0, "ok": 0, "kernel_ms": 0.0, "launches": 0}
+        barrier()
+        sync_all()
+        t4 = time.perf_counter()
+        run(a.ref_steps, opts_exact, 0, sr)
+        sync_all()
+        barrier()
+        dtr = max_over_ranks(time.perf_counter() - t4)
+        refs = {"iterations_per_s": sum_over_ranks(sr["iters"]) / dtr,
+                "frames_per_s": sum_over_ranks(a.ref_steps) / dtr,
+                "ms_per_pair": 1000.0 * dtr / a.ref_steps, "steps": a.ref_steps,
+                "pairs_ok": sr["ok"],
+                "note": "RST_SUM_REF (library default): source centroid, dst_mean and cost "
+                        "as sequential fp32 sums in source order, the reference's rounding "
+                        "(align_icp.cpp:113,120-122; point_cloud_utils.cpp:92-98)"}
+
     # ---- the reference-shaped host API (extra fields, not value) ------------------
     # AlignIcp3d(src, dst, 128, &T) on host clouds, one pair at a time: PCIe
     # upload of both clouds + index build + 128 iterations + pose readback
@@ -411,6 +431,7 @@ def main():
         dth = (time.perf_counter() - t2) / 3
         host = {"ms_per_pair": 1000.0 * dth, "pairs_per_s": 1.0 / dth,
                 "iterations_per_s": a.iters / dth,
+                "sum_mode": "RST_SUM_REF (the drop-in default)",
                 "note": "AlignIcp3d(src, dst, 128, T) with host clouds, one pair at a time: "
                         "PCIe-inclusive (upload, index build, ICP, readback)"}
 
@@ -445,9 +466,8 @@ def main():
     traffic = load_traffic() if (a.workload, a.width, a.height) == ("stream", 640, 480) else None
 
     if rank != 0:
-        if dist is not None:
-            dist.destroy_process_group()
-        return
+        rdv.close()
+        return 0
     cpu = None
     if not a.no_cpu and world == 1:
         cpu = cpu_baseline(a.width, a.height, a.cpu_iters)
@@ -481,6 +501,8 @@ def main():
     }
     if pl is not None:
         out["p2plane"] = pl
+    if refs is not None:
+        out["ref_sums"] = refs
     if host is not None:
         out["host_api"] = host
     if gicp is not None:
@@ -488,9 +510,9 @@ def main():
     if cpu is not None:
         out["speedup_vs_cpu_baseline"] = value / cpu["value"]
     print(json.dumps(out))
-    if dist is not None:
-        dist.destroy_process_group()
+    rdv.close()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

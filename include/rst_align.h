@@ -51,6 +51,19 @@ typedef enum {
   RST_P2PLANE = 1
 } rst_icp_mode;
 
+typedef enum {
+  /* the reference's own rounding (align_icp.cpp:101,113,120-122 and
+   * point_cloud_utils.cpp:92-98): the source centroid, dst_mean and cost are
+   * float32 sums taken sequentially in ascending source index, exactly as
+   * the CPU loop rounds them; the covariance is the fp64 sum of the same
+   * float products.  Bit-identical means and cost; the default. */
+  RST_SUM_REF = 0,
+  /* fp64 partial sums in any order (one pass, no sequential step): the
+   * throughput mode.  Differs from the reference by its own fp32-vs-fp64
+   * sensitivity (~1e-5 m typical, 1.5e-4 m seen on one golden pair). */
+  RST_SUM_FP64 = 1
+} rst_sum_mode;
+
 typedef struct {
   int32_t max_iter;       /* 128 at both reference call sites */
   int32_t mode;           /* rst_icp_mode */
@@ -60,7 +73,10 @@ typedef struct {
   float p2plane_eps;      /* P2PLANE: stop when |xi| < eps (1e-6) */
   float p2plane_mu;       /* P2PLANE: GM scale on plane residual (m^2) */
   float p2plane_max_dist; /* P2PLANE: reject NN beyond this (m); 0 = off */
-  int32_t reserved[8];
+  int32_t sum_mode;       /* rst_sum_mode (P2POINT_REF only; the sharded
+                           * align always runs RST_SUM_FP64: a sequential
+                           * sum has no shard decomposition) */
+  int32_t reserved[7];
 } rst_icp_opts;
 
 typedef struct {
@@ -102,6 +118,16 @@ int rst_ctx_enable_graphs(rst_ctx* ctx, int enable);
  * context's stream): 0 = off (default), 1 = every iteration, k > 1 = every
  * k-th iteration (fewer events in a timed loop). */
 int rst_ctx_enable_kernel_timing(rst_ctx* ctx, int enable);
+
+/* ---- device buffers ------------------------------------------------------ */
+/* Plain HBM allocations on the context's device, for callers that hand the
+ * *_device entry points their own buffers (bindings, tests, the bench)
+ * without a second runtime (e.g. torch's) in the process.  Copies are
+ * ordered on the context's stream and complete before returning. */
+int rst_dev_alloc(rst_ctx* ctx, int64_t bytes, void** d_out);
+int rst_dev_free(rst_ctx* ctx, void* d);
+int rst_dev_upload(rst_ctx* ctx, void* d_dst, const void* h_src, int64_t bytes);
+int rst_dev_download(rst_ctx* ctx, void* h_dst, const void* d_src, int64_t bytes);
 
 /* ---- target index (replaces KDTree3f{dst,16}; kdtree.hpp:27-57) --------- */
 /* Builds the exact-NN index (Morton-ordered bounding-volume hierarchy) over
@@ -207,7 +233,8 @@ int rst_kabsch_solve(rst_ctx* ctx, const double cov[9], const float smean[3],
  * index; weights may be NULL (unweighted branch, :38-45).  Means and the
  * fp64 covariance are computed on the device, then the same solve as
  * rst_kabsch_solve.  RST_FALSE when n < 3 or m < 3 (pose untouched, :22-24);
- * RST_E_ARG for k < 1 or an index out of range. */
+ * k == 0 gives what the reference computes from its 0/0 means: RST_OK,
+ * R = I, t = NaN.  RST_E_ARG for an index out of range. */
 int rst_solve_kabsch(rst_ctx* ctx, const float* src, int64_t n,
                      const float* dst, int64_t m, const int32_t* pairs,
                      const float* weights, int64_t k, float pose_out[16]);

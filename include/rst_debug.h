@@ -38,6 +38,11 @@ int rst_debug_query_nn_fallback(rst_ctx* ctx, const rst_target* tgt, const float
                                 int64_t nq, const int32_t* warm, int mode, int32_t* idx,
                                 float* d2, int32_t* path);
 
+/* The RST_SUM_REF loop's sequential-sum kernel on a host stream of n
+ * float4: out[c] = ((0 + x[0].c) + x[1].c) + ... in float32, i ascending --
+ * the rounding of `dst_mean += dst.GetPoint(j)` (align_icp.cpp:120). */
+int rst_debug_seq_sum4(rst_ctx* ctx, const float* xyzw, int64_t n, float out[4]);
+
 #ifdef __cplusplus
 }
 #endif

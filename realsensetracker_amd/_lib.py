@@ -18,6 +18,7 @@ LIB_PATH = Path(os.environ.get(
 RST_OK, RST_FALSE = 0, 1
 RST_E_ARG, RST_E_HIP, RST_E_NOMEM, RST_E_NODEVICE, RST_E_COMM, RST_E_STATE = -1, -2, -3, -4, -5, -6
 RST_P2POINT_REF, RST_P2PLANE = 0, 1
+RST_SUM_REF, RST_SUM_FP64 = 0, 1  # rst_sum_mode: reference fp32 sequential sums / fp64 sums
 COMM_ID_BYTES = 128
 
 c_float_p = C.POINTER(C.c_float)
@@ -30,7 +31,8 @@ class IcpOpts(C.Structure):
     _fields_ = [("max_iter", C.c_int32), ("mode", C.c_int32), ("mu0", C.c_float),
                 ("anneal_every", C.c_int32), ("anneal_div", C.c_float),
                 ("p2plane_eps", C.c_float), ("p2plane_mu", C.c_float),
-                ("p2plane_max_dist", C.c_float), ("reserved", C.c_int32 * 8)]
+                ("p2plane_max_dist", C.c_float), ("sum_mode", C.c_int32),
+                ("reserved", C.c_int32 * 7)]
 
 
 class Intrinsics(C.Structure):
@@ -47,6 +49,10 @@ PROTOTYPES = {
     "rst_icp_opts_default": (None, [C.POINTER(IcpOpts)]),
     "rst_device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "rst_ctx_create": (C.c_int, [C.c_int, C.POINTER(_P)]),
+    "rst_dev_alloc": (C.c_int, [_P, C.c_int64, C.POINTER(_P)]),
+    "rst_dev_free": (C.c_int, [_P, _P]),
+    "rst_dev_upload": (C.c_int, [_P, _P, _P, C.c_int64]),
+    "rst_dev_download": (C.c_int, [_P, _P, _P, C.c_int64]),
     "rst_ctx_destroy": (C.c_int, [_P]),
     "rst_ctx_set_stream": (C.c_int, [_P, _P]),
     "rst_ctx_synchronize": (C.c_int, [_P]),
@@ -127,33 +133,43 @@ PROTOTYPES = {
 _lib = None
 
 
-def _share_torch_runtime() -> None:
-    """One HIP runtime per process.  The torch wheel bundles its own
-    libamdhip64 / libhsa-runtime64 / librccl with the same sonames as
-    /opt/rocm's; whichever is mapped first satisfies our library's NEEDED
-    entries.  If ours were loaded first, a later `import torch` would map a
-    second runtime and the two tear each other down at exit ("free():
-    invalid pointer").  So when torch is importable it is imported first and
-    our library binds to its runtime; without torch, /opt/rocm's is used.
-    RST_NO_TORCH=1 skips this (pure C-ABI processes)."""
-    if os.environ.get("RST_NO_TORCH") == "1":
-        return
+def hip_runtimes_mapped() -> list[str]:
+    """Distinct libamdhip64 files mapped into this process (from
+    /proc/self/maps).  Two means two HIP runtimes -- e.g. torch's bundled
+    copy and /opt/rocm's -- which tear each other down at exit."""
+    seen = []
     try:
-        import torch  # noqa: F401
-    except Exception:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                parts = line.split()
+                if len(parts) >= 6 and "libamdhip64" in parts[-1]:
+                    path = os.path.realpath(parts[-1])
+                    if path not in seen:
+                        seen.append(path)
+    except OSError:
         pass
+    return seen
 
 
 def lib() -> C.CDLL:
-    """Load librst_align.so (raises if it is absent: no fallback path)."""
+    """Load librst_align.so (raises if it is absent: no fallback path).
+
+    The library binds whichever HIP runtime the process already has mapped
+    (the dynamic linker resolves its libamdhip64 soname to a loaded copy),
+    else /opt/rocm's.  Loading it into a process that ends up with two
+    runtimes mapped is refused."""
     global _lib
     if _lib is None:
-        _share_torch_runtime()
         if not LIB_PATH.exists():
             raise ImportError(
                 f"realsensetracker_amd: HIP library not built ({LIB_PATH}); run "
                 "`python -m realsensetracker_amd.build` (or __graft_entry__.build())")
         L = C.CDLL(str(LIB_PATH), mode=C.RTLD_GLOBAL)
+        rts = hip_runtimes_mapped()
+        if len(rts) > 1:
+            raise ImportError("realsensetracker_amd: two HIP runtimes mapped in this process "
+                              f"({', '.join(rts)}); load the library before or without a "
+                              "second runtime (e.g. torch's)")
         for name, (res, args) in PROTOTYPES.items():
             f = getattr(L, name)
             f.restype = res

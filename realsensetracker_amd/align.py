@@ -94,6 +94,58 @@ def get_context(device: int = 0) -> Context:
     return _contexts[device]
 
 
+class DeviceBuffer:
+    """An HBM allocation through the library (rst_dev_alloc), for the
+    *_device entry points: no second HIP runtime (torch's) in the process."""
+
+    def __init__(self, nbytes: int, ctx: Context | None = None):
+        self.ctx = ctx or get_context()
+        self.nbytes = int(nbytes)
+        self._p = C.c_void_p()
+        L.check(L.lib().rst_dev_alloc(self.ctx.handle, self.nbytes, C.byref(self._p)),
+                "rst_dev_alloc")
+
+    @classmethod
+    def from_array(cls, a: np.ndarray, ctx: Context | None = None) -> "DeviceBuffer":
+        a = np.ascontiguousarray(a)
+        b = cls(a.nbytes, ctx)
+        b.upload(a)
+        return b
+
+    @property
+    def ptr(self) -> int:
+        return self._p.value or 0
+
+    def upload(self, a: np.ndarray, offset: int = 0) -> None:
+        a = np.ascontiguousarray(a)
+        if offset < 0 or offset + a.nbytes > self.nbytes:
+            raise ValueError("upload past the buffer")
+        L.check(L.lib().rst_dev_upload(self.ctx.handle, C.c_void_p(self.ptr + offset),
+                                       a.ctypes.data_as(C.c_void_p), a.nbytes), "rst_dev_upload")
+
+    def download(self, shape, dtype, offset: int = 0) -> np.ndarray:
+        out = np.empty(shape, dtype)
+        if offset < 0 or offset + out.nbytes > self.nbytes:
+            raise ValueError("download past the buffer")
+        L.check(L.lib().rst_dev_download(self.ctx.handle, out.ctypes.data_as(C.c_void_p),
+                                         C.c_void_p(self.ptr + offset), out.nbytes),
+                "rst_dev_download")
+        return out
+
+    def free(self) -> None:
+        if self._p:
+            L.lib().rst_dev_free(self.ctx.handle, self._p)
+            self._p = C.c_void_p()
+
+    def __del__(self):
+        if sys.is_finalizing():
+            return
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
 class Target:
     """Prepared target cloud in HBM: Morton-sorted points + exact-NN BVH
     (+ normals).  Replaces KDTree3f{dst, 16} (kdtree.hpp:27-57)."""

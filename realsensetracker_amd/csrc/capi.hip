@@ -261,6 +261,42 @@ int rst_ctx_enable_kernel_timing(rst_ctx* ctx, int enable) {
   return RST_OK;
 }
 
+// ---- device buffers ------------------------------------------------------------
+int rst_dev_alloc(rst_ctx* ctx, int64_t bytes, void** d_out) {
+  if (!ctx || !d_out || bytes < 0) return RST_E_ARG;
+  *d_out = nullptr;
+  RST_HIP(hipSetDevice(ctx->device));
+  if (hipMalloc(d_out, (size_t)std::max<int64_t>(bytes, 1)) != hipSuccess) return RST_E_NOMEM;
+  return RST_OK;
+}
+
+int rst_dev_free(rst_ctx* ctx, void* d) {
+  if (!ctx) return RST_E_ARG;
+  if (!d) return RST_OK;
+  RST_HIP(hipSetDevice(ctx->device));
+  RST_HIP(hipStreamSynchronize(ctx->stream));  // no pending work may still use it
+  RST_HIP(hipFree(d));
+  return RST_OK;
+}
+
+int rst_dev_upload(rst_ctx* ctx, void* d_dst, const void* h_src, int64_t bytes) {
+  if (!ctx || bytes < 0 || (bytes > 0 && (!d_dst || !h_src))) return RST_E_ARG;
+  if (bytes == 0) return RST_OK;
+  RST_HIP(hipSetDevice(ctx->device));
+  RST_HIP(hipMemcpyAsync(d_dst, h_src, (size_t)bytes, hipMemcpyHostToDevice, ctx->stream));
+  RST_HIP(hipStreamSynchronize(ctx->stream));
+  return RST_OK;
+}
+
+int rst_dev_download(rst_ctx* ctx, void* h_dst, const void* d_src, int64_t bytes) {
+  if (!ctx || bytes < 0 || (bytes > 0 && (!d_src || !h_dst))) return RST_E_ARG;
+  if (bytes == 0) return RST_OK;
+  RST_HIP(hipSetDevice(ctx->device));
+  RST_HIP(hipMemcpyAsync(h_dst, d_src, (size_t)bytes, hipMemcpyDeviceToHost, ctx->stream));
+  RST_HIP(hipStreamSynchronize(ctx->stream));
+  return RST_OK;
+}
+
 // ---- target ------------------------------------------------------------------
 int rst_target_build(rst_ctx* ctx, const float* xyz, int64_t m, rst_target** out) {
   if (!ctx || !out || m < 0 || (m > 0 && !xyz)) return RST_E_ARG;
@@ -448,6 +484,27 @@ int rst_debug_query_nn_fallback(rst_ctx* ctx, const rst_target* t, const float* 
   return s < 0 ? s : RST_OK;
 }
 
+int rst_debug_seq_sum4(rst_ctx* ctx, const float* xyzw, int64_t n, float out[4]) {
+  if (!ctx || !out || n < 0 || (n > 0 && !xyzw)) return RST_E_ARG;
+  RST_HIP(hipSetDevice(ctx->device));
+  void* d = nullptr;
+  const size_t bytes = sizeof(float4) * (size_t)std::max<int64_t>(n, 1) + 64;
+  if (hipMalloc(&d, bytes) != hipSuccess) return RST_E_NOMEM;
+  float* dout = (float*)((char*)d + bytes - 64);
+  int s = RST_OK;
+  if (n > 0 && hipMemcpyAsync(d, xyzw, sizeof(float4) * n, hipMemcpyHostToDevice, ctx->stream) !=
+                   hipSuccess)
+    s = RST_E_HIP;
+  if (s >= 0) s = seq_sum4_device(ctx, (const float4*)d, n, dout);
+  if (s >= 0 && (hipMemcpyAsync(out, dout, sizeof(float) * 4, hipMemcpyDeviceToHost, ctx->stream) !=
+                     hipSuccess ||
+                 hipStreamSynchronize(ctx->stream) != hipSuccess))
+    s = RST_E_HIP;
+  hipStreamSynchronize(ctx->stream);
+  hipFree(d);
+  return s;
+}
+
 int rst_debug_queue_trace(rst_ctx* ctx, int32_t* out, int32_t n) {
   if (!ctx || !out || n < 0) return RST_E_ARG;
   for (int i = 0; i < n && i < kQTrace; ++i) {
@@ -528,7 +585,7 @@ int rst_icp_align_pyramid_async(rst_ctx* ctx, const rst_target* const* src,
   bool chained = false;  // a solve has been enqueued on the context's state
   for (int l = nlevels - 1; l >= 0; --l) {
     o.max_iter = iters[l];
-    const int s = icp_launch(ctx, src[l], tgt[l], &o, pose_in, nullptr, chained);
+    const int s = icp_launch(ctx, src[l], tgt[l], &o, pose_in, nullptr, chained, l);
     if (s == RST_FALSE) continue;  // early false: the pose passes through (level 0 excluded above)
     if (s != RST_OK) {
       ctx->pend = {};
@@ -598,7 +655,15 @@ int rst_solve_kabsch(rst_ctx* ctx, const float* src, int64_t n, const float* dst
       (k > 0 && !pairs))
     return RST_E_ARG;
   if (n < 3 || m < 3) return RST_FALSE;  // align_icp.cpp:22-24, pose untouched
-  if (k < 1) return RST_E_ARG;           // reference: 0/0 means (NaN pose)
+  if (k == 0) {
+    // the reference with no correspondences: means 0/0 = NaN (:33-34), an
+    // all-zero covariance whose Jacobi SVD is U = V = I, so R = I and
+    // t = dst_mean - R src_mean = NaN; it returns true (:69-70)
+    for (int c = 0; c < 4; ++c)
+      for (int r = 0; r < 4; ++r) pose_out[c * 4 + r] = (r == c) ? 1.0f : 0.0f;
+    for (int r = 0; r < 3; ++r) pose_out[12 + r] = NAN;
+    return RST_OK;
+  }
   for (int64_t c = 0; c < k; ++c)        // host-side bounds check before any launch
     if (pairs[2 * c] < 0 || pairs[2 * c] >= n || pairs[2 * c + 1] < 0 || pairs[2 * c + 1] >= m)
       return RST_E_ARG;

@@ -80,9 +80,17 @@ int rst_icp_align_sharded_device(rst_ctx* ctx, rst_comm* comm, const float* d_sr
   if (!ctx || !comm || !tgt || !pose_inout || n_shard < 0 || (n_shard > 0 && !d_src_shard))
     return RST_E_ARG;
   RST_HIP(hipSetDevice(ctx->device));
+  // a sequential sum over the whole source has no shard decomposition: the
+  // sharded loop always reduces fp64 partial sums (rst_align.h sum_mode)
+  rst_icp_opts o;
+  if (opts)
+    o = *opts;
+  else
+    rst_icp_opts_default(&o);
+  o.sum_mode = RST_SUM_FP64;
   rst_target* s = nullptr;
   RST_CHECK(target_build_device(ctx, d_src_shard, n_shard, false, &s));
-  int r = icp_align_prepared(ctx, s, tgt, opts, pose_inout, mean_cost, nullptr, comm);
+  int r = icp_align_prepared(ctx, s, tgt, &o, pose_inout, mean_cost, nullptr, comm);
   rst_target_free(s);
   return r;
 }

@@ -21,6 +21,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 #include "rst_device.hpp"
 #include "rst_wave_nn.hpp"
@@ -39,7 +40,8 @@ constexpr int kNP2Plane = 30;  // A (21), b (6), sum w r^2, count, sum d2
 // neighbour when |q - p| + |q - q0| < g (triangle inequality: every other
 // point lies at >= g - |q - q0| > |q - p| from q; relative margins 1e-5
 // cover the float arithmetic, and the strict gap excludes ties), with no
-// search.  nnpos carries kCertBit while the certificate of its point holds.
+// search.  nnq[i].w carries kCertBit while the certificate of its point
+// holds.  Kernel 1 makes certificates for near points too (adj_search2).
 #ifndef RST_FB_MIN_WAVES
 #define RST_FB_MIN_WAVES 4  // k_icp_fb<P2PointAcc>: 128 VGPRs (1 spill); r01h A/B 15.8k -> 16.2k it/s; r01k: 3 -> 16.7k, 5 -> 15.6k vs 17.1k
 #endif
@@ -167,20 +169,22 @@ __global__ __launch_bounds__(kRedBS) void k_slab_reduce(const double* __restrict
 struct InitArgs {
   float pose[16];
   float mu0;
-  int32_t need_centroid;
+  int32_t need_centroid;  // 0 none (P2PLANE), 1 fp64 slab, 2 sequential float sums
   int32_t chain;  // pyramid: start from the pose the previous solve on this state left
+  int64_t n;      // source points (all shards)
 };
 
 // State initialisation: pose from the caller (or, chained, the previous
 // solve's result: its pose, or its initial pose when it failed -- what
-// icp_finish would hand back), mu0, centroid = fp64 sum / n
-// rounded to float (reference: fp32 sequential sum * float(1.0/n),
-// point_cloud_utils.cpp:92-98; DESIGN.md "Numerics").
+// icp_finish would hand back), mu0, centroid: RST_SUM_REF the reference's
+// fp32 sequential sum (k_seq_sum4) * float(1.0 / n) (point_cloud_utils.cpp:
+// 92-98), RST_SUM_FP64 the fp64 sum / n rounded to float.
 __global__ __launch_bounds__(kBS) void k_init_state(const double* __restrict__ cslab, int rows,
-                                                    InitArgs a, IcpState* __restrict__ st) {
+                                                    const float* __restrict__ fsum, InitArgs a,
+                                                    IcpState* __restrict__ st) {
   __shared__ double red[(kBS / kWave) * 4];
   __shared__ double tot[4];
-  if (a.need_centroid) reduce_slab_rows<4>(cslab, rows, cslab, 0, nullptr, red, tot);
+  if (a.need_centroid == 1) reduce_slab_rows<4>(cslab, rows, cslab, 0, nullptr, red, tot);
   if (threadIdx.x == 0) {
     float P[12];  // R col-major, t
     for (int c = 0; c < 3; ++c)
@@ -200,7 +204,10 @@ __global__ __launch_bounds__(kBS) void k_init_state(const double* __restrict__ c
       st->t[r] = P[9 + r];
       st->td[r] = P[9 + r];
     }
-    if (a.need_centroid) {
+    if (a.need_centroid == 2) {
+      const float f = (float)(1.0 / (double)a.n);  // `*centroid *= (1.0 / n)`: double -> float
+      for (int r = 0; r < 3; ++r) st->smean[r] = fsum[r] * f;
+    } else if (a.need_centroid == 1) {
       const double n = tot[3] > 0 ? tot[3] : 1.0;
       for (int r = 0; r < 3; ++r) st->smean[r] = (float)(tot[r] / n);
     } else {
@@ -218,6 +225,7 @@ __global__ __launch_bounds__(kBS) void k_init_state(const double* __restrict__ c
     st->last_xi = 0;
     st->last_cnt = 0;
     st->last_d2 = 0;
+    for (int k = 0; k < 4; ++k) st->seq[k] = 0.f;
   }
 }
 
@@ -240,6 +248,7 @@ __device__ __forceinline__ Uni load_uni(const IcpState* __restrict__ st) {
 
 struct AccArgs {
   const float4* __restrict__ nrm;  // P2PLANE: target normals, sorted order
+  float4* __restrict__ corr;       // RST_SUM_REF: (q, d2) per original source index
   float pmu;                       // P2PLANE: Geman-McClure scale on r^2
   float max_d2;                    // P2PLANE: correspondence rejection
   int32_t pos0;                    // sorted position of dst[0]
@@ -256,6 +265,7 @@ struct P2PointAcc {
   static constexpr int kMinWaves = RST_NN_MIN_WAVES;  // k_icp_nn occupancy (waves/SIMD)
   static constexpr int kFbMinWaves = RST_FB_MIN_WAVES;  // k_icp_fb occupancy
   static constexpr bool kCanFinish = false;
+  static constexpr bool kSums = true;  // the search kernels write slab rows
   // q = the neighbour's coordinates (the caller has them), bp its sorted
   // position; no neighbour (bp < 0) -> dst[0], d2 = FLT_MAX
   __device__ static void add(double (&v)[NV], const BvhView& bv, const AccArgs& a, const Uni& u,
@@ -285,6 +295,7 @@ struct P2PlaneAcc {
   static constexpr int kMinWaves = 4;
   static constexpr int kFbMinWaves = 1;
   static constexpr bool kCanFinish = true;
+  static constexpr bool kSums = true;
   __device__ static void add(double (&v)[NV], const BvhView& bv, const AccArgs& a, const Uni& u,
                              const float4& s, float px, float py, float pz, float bd, int bp,
                              float4 q) {
@@ -312,6 +323,137 @@ struct P2PlaneAcc {
     v[29] += bd;
   }
 };
+
+// P2POINT_REF with RST_SUM_REF: the search kernels only record source
+// point i's correspondence -- q = dst[nbr_i] (dst[0] when there is none,
+// the query's untouched output) and d2 -- at its ORIGINAL index, so that
+// k_seq_sum4 can replay the reference's sequential float sums over i
+// ascending (align_icp.cpp:105-122) and k_cov_ref its covariance
+// (:125-136).  Nothing is summed in the search kernels.
+struct RefAcc {
+  static constexpr int NV = 9;   // k_cov_ref's rows: the 3x3 covariance
+  static constexpr int RS = 16;
+  static constexpr int kMinWaves = RST_NN_MIN_WAVES;
+  static constexpr int kFbMinWaves = RST_FB_MIN_WAVES;
+  static constexpr bool kCanFinish = false;
+  static constexpr bool kSums = false;
+  __device__ static void add(double (&v)[NV], const BvhView& bv, const AccArgs& a, const Uni& u,
+                             const float4& s, float px, float py, float pz, float bd, int bp,
+                             float4 q) {
+    (void)v; (void)u; (void)px; (void)py; (void)pz;
+    if (bp < 0) q = bv.pts[a.pos0];
+    a.corr[f2i(s.w)] = make_float4(q.x, q.y, q.z, bd);
+  }
+};
+
+// ---- RST_SUM_REF: the reference's sequential float32 sums ---------------------------
+// One wavefront; lane c < 4 carries chain c (x, y, z, w of a float4 stream)
+// through fl(s + x_i) for i ascending from s = +0 -- the order and rounding
+// of `dst_mean += dst.GetPoint(j)` / `cost += dist_sqr` (align_icp.cpp:113,
+// 120) and of ComputeCentroid's loop (point_cloud_utils.cpp:94-96).  The
+// chain is inherently serial (one dependent v_add_f32 per element); the
+// wave only keeps it fed: tiles of 64 x kSeqT float4 are loaded coalesced a
+// tile ahead and transposed through LDS so lane c reads four of its values
+// per ds_read_b128.  out[0..3] = the four sums.
+constexpr int kSeqT = 16;                   // float4 per lane per tile (1024 elements)
+constexpr int kSeqRow = kSeqT * kWave + 4;  // floats per chain row (+4: rows on distinct banks)
+__device__ __forceinline__ void seq_tile_load(const float4* __restrict__ x, int64_t n,
+                                              int64_t base, float4 (&v)[kSeqT]) {
+  const int lane = threadIdx.x;
+#pragma unroll
+  for (int t = 0; t < kSeqT; ++t) {
+    const int64_t i = base + (int64_t)t * kWave + lane;
+    v[t] = i < n ? x[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+// transpose one tile through LDS and run lane c's chain over its cnt values
+__device__ __forceinline__ void seq_tile_sum(const float4 (&v)[kSeqT], int cnt, float* tile,
+                                             float& acc) {
+  const int lane = threadIdx.x;
+#pragma unroll
+  for (int t = 0; t < kSeqT; ++t) {
+    tile[0 * kSeqRow + t * kWave + lane] = v[t].x;
+    tile[1 * kSeqRow + t * kWave + lane] = v[t].y;
+    tile[2 * kSeqRow + t * kWave + lane] = v[t].z;
+    tile[3 * kSeqRow + t * kWave + lane] = v[t].w;
+  }
+  wave_sync();
+  if (lane < 4) {
+    const float* row = tile + lane * kSeqRow;
+    int j = 0;
+    for (; j + 4 <= cnt; j += 4) {
+      const float4 q = *reinterpret_cast<const float4*>(row + j);
+      acc = acc + q.x;
+      acc = acc + q.y;
+      acc = acc + q.z;
+      acc = acc + q.w;
+    }
+    for (; j < cnt; ++j) acc = acc + row[j];
+  }
+  wave_sync();
+}
+
+__global__ __launch_bounds__(kWave) void k_seq_sum4(const float4* __restrict__ x, int64_t n,
+                                                    float* __restrict__ out) {
+  __shared__ float4 tile4[4 * kSeqRow / 4];
+  float* tile = reinterpret_cast<float*>(tile4);
+  constexpr int64_t kT = kSeqT * kWave;
+  float acc = 0.0f;
+  float4 a[kSeqT], b[kSeqT];
+  seq_tile_load(x, n, 0, a);
+  for (int64_t base = 0; base < n; base += 2 * kT) {
+    seq_tile_load(x, n, base + kT, b);  // in flight during a's chain
+    seq_tile_sum(a, (int)min<int64_t>(n - base, kT), tile, acc);
+    if (base + kT >= n) break;
+    seq_tile_load(x, n, base + 2 * kT, a);
+    seq_tile_sum(b, (int)min<int64_t>(n - base - kT, kT), tile, acc);
+  }
+  if (threadIdx.x < 4) out[threadIdx.x] = acc;
+}
+
+// src in original order (the reference iterates i ascending; the prepared
+// source is Morton-sorted): out[i] = pts[inv[i]].
+__global__ __launch_bounds__(kBS) void k_gather_orig(const float4* __restrict__ pts,
+                                                     const int32_t* __restrict__ inv, int64_t n,
+                                                     float4* __restrict__ out) {
+  const int64_t i = blockIdx.x * (int64_t)kBS + threadIdx.x;
+  if (i < n) out[i] = pts[inv[i]];
+}
+
+// The covariance of align_icp.cpp:125-136 with the sequential dst_mean:
+// cov += double(float(w_i (q_i - dbar)) * float(s_i - sbar)) per
+// coefficient -- the reference's float products, summed in fp64 (the sum
+// order only moves the last bits of a double).  dbar = seq / float(n)
+// (:122); w_i = (mu / (d2_i + mu))^2 (:116-117).  Grid-stride over the
+// original order; one 9-double row (stride RefAcc::RS) per block.
+constexpr int kCovBlocks = 1024;
+__global__ __launch_bounds__(kBS) void k_cov_ref(const float4* __restrict__ srco,
+                                                 const float4* __restrict__ corr, int64_t n,
+                                                 const IcpState* __restrict__ st,
+                                                 double* __restrict__ slab) {
+  __shared__ double lds[(kBS / kWave) * 9];
+  const float nf = (float)n;
+  const float dm0 = st->seq[0] / nf, dm1 = st->seq[1] / nf, dm2 = st->seq[2] / nf;
+  const float sm0 = st->smean[0], sm1 = st->smean[1], sm2 = st->smean[2];
+  const float mu = st->mu;
+  double v[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) v[k] = 0.0;
+  for (int64_t i = blockIdx.x * (int64_t)kBS + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kBS) {
+    const float4 s = srco[i];
+    const float4 c = corr[i];
+    const float l = mu / (c.w + mu);
+    const float w = l * l;
+    const float a0 = w * (c.x - dm0), a1 = w * (c.y - dm1), a2 = w * (c.z - dm2);
+    const float b0 = s.x - sm0, b1 = s.y - sm1, b2 = s.z - sm2;
+    v[0] += (double)(a0 * b0); v[1] += (double)(a0 * b1); v[2] += (double)(a0 * b2);
+    v[3] += (double)(a1 * b0); v[4] += (double)(a1 * b1); v[5] += (double)(a1 * b2);
+    v[6] += (double)(a2 * b0); v[7] += (double)(a2 * b1); v[8] += (double)(a2 * b2);
+  }
+  block_sum_to_slab<9, kBS>(v, lds, slab + (int64_t)blockIdx.x * RefAcc::RS);
+}
 
 // ---- kernel 1: adjacency search, one point per thread ----------------------------------
 // Exclusive prefix of the per-block queue counts (one block, kBS threads):
@@ -365,12 +507,20 @@ __device__ void queue_prefix(const int32_t* __restrict__ qcnt, int nb, int32_t* 
   }
 }
 
+// Per source point the loop keeps its neighbour and certificate:
+//   nnq[i]  = (p.x, p.y, p.z, pos | kCertBit?): the last exact neighbour's
+//             coordinates and sorted position (-1 = cold);
+//   cert[i] = (q0.x, q0.y, q0.z, g), valid under kCertBit: when the query
+//             was at q0 every target point but p lay at >= g.
+// A query now at q keeps p as its exact neighbour while |q - p| + |q - q0|
+// < g (triangle inequality, strict: no tie can arise), which kernel 1 tests
+// from coalesced loads alone -- no search, no dependent gather.
 template <class Acc>
 __global__ __launch_bounds__(kBS, Acc::kMinWaves) void k_icp_nn(BvhView bv, AdjView av, AccArgs aa,
                                                 const float4* __restrict__ src, int64_t n,
                                                 const IcpState* __restrict__ st,
-                                                int32_t* __restrict__ nnpos,
-                                                const float4* __restrict__ cert,
+                                                float4* __restrict__ nnq,
+                                                float4* __restrict__ cert,
                                                 int32_t* __restrict__ qbuf,
                                                 int32_t* __restrict__ qcnt,
                                                 double* __restrict__ slab) {
@@ -388,29 +538,45 @@ __global__ __launch_bounds__(kBS, Acc::kMinWaves) void k_icp_nn(BvhView bv, AdjV
   const int64_t i = tb * (int64_t)kBS + threadIdx.x;
   const bool act = i < n;
   const float4 s = act ? src[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4 tq = act ? nnq[i] : make_float4(0.f, 0.f, 0.f, i2f(-1));
+  float4 c = make_float4(0.f, 0.f, 0.f, 0.f);
+  const int wb = f2i(tq.w);
+  const bool has_cert = wb >= 0 && (wb & kCertBit);
+  if (act && has_cert) c = cert[i];
   float px, py, pz;
   xform(u.P, s.x, s.y, s.z, px, py, pz);  // align_icp.cpp:107
   const bool fin = finite3(px, py, pz);
-  // :112 exact 1-NN, starting from last iteration's neighbour
-  int warm = act ? nnpos[i] : -1;
-  const bool has_cert = warm >= 0 && (warm & kCertBit);
-  if (warm >= 0) warm &= kPosMask;
-  if (act && fin && warm < 0) warm = morton_seed(bv, px, py, pz);
-  Best1 r;
-  r.init();
-  if (act && fin) {
-    const float4 w = bv.pts[warm];
-    r.offer(d2_ref(px, py, pz, w.x, w.y, w.z), f2i(w.w), warm);
-  }
+  int warm = wb >= 0 ? (wb & kPosMask) : -1;
+  // :112 exact 1-NN: the certificate first
   bool certified = false;
-  if (act && fin && has_cert) {  // far point: its certificate (kCertBit)
-    const float4 c = cert[i];
+  float dq = FLT_MAX;
+  if (act && fin && has_cert) {
+    dq = d2_ref(px, py, pz, tq.x, tq.y, tq.z);
     const float dx = px - c.x, dy = py - c.y, dz = pz - c.z;
-    const float moved = sqrtf((dx * dx + dy * dy) + dz * dz) * 1.00001f;
-    certified = sqrtf(r.d) * 1.00001f + moved + 1e-30f < c.w;
+    const float moved = margin_sqrt((dx * dx + dy * dy) + dz * dz) * 1.00001f;
+    certified = margin_sqrt(dq) * 1.00001f + moved + 1e-30f < c.w;
   }
-  const bool done =
-      act && (!fin || certified || adj_search_wide(bv, av, warm, px, py, pz, r));
+  // otherwise the two nearest through the leaf adjacency of the last
+  // neighbour (cold lanes: a Morton-code seed), seeded with it and its
+  // sorted successor so the second bound starts finite
+  Best2 r2;
+  r2.init();
+  bool exact = false;
+  float g = 0.f;
+  if (act && fin && !certified) {
+    if (warm < 0) warm = morton_seed(bv, px, py, pz);
+    const float4 w = bv.pts[warm];
+    r2.offer(d2_ref(px, py, pz, w.x, w.y, w.z), f2i(w.w), warm);
+    if (bv.m > 1) {
+      const int nb = warm + 1 < bv.m ? warm + 1 : warm - 1;
+      const float4 w2 = bv.pts[nb];
+      r2.offer(d2_ref(px, py, pz, w2.x, w2.y, w2.z), f2i(w2.w), nb);
+    }
+    const float rc = adj_search2(bv, av, warm, px, py, pz, r2);
+    exact = margin_sqrt(r2.d[0]) * 1.00001f + 1e-30f < rc;
+    if (exact) g = cert_bound(r2, rc);
+  }
+  const bool done = act && (!fin || certified || exact);
   // lanes the adjacency could not certify go to the fallback queue, in
   // point order within the block's segment
   const bool need = act && !done;
@@ -429,15 +595,21 @@ __global__ __launch_bounds__(kBS, Acc::kMinWaves) void k_icp_nn(BvhView bv, AdjV
   // a queued lane hands the fallback the nearest point its scan saw (at
   // least as near as the warm point): a tighter starting bound and a warm
   // leaf nearer the query (any start keeps the fallback's search exact)
-  if (need) nnpos[i] = r.pos;
+  if (need) nnq[i] = make_float4(0.f, 0.f, 0.f, i2f(r2.pos[0]));
 #endif
   if (threadIdx.x == 0) qcnt[tb] = total;
-  if (done) {
-    // the certificate stays valid while its point is the answer
-    nnpos[i] = r.pos | (has_cert && r.pos == warm ? kCertBit : 0);
-    Acc::add(v, bv, aa, u, s, px, py, pz, r.d, r.pos, bv.pts[r.pos >= 0 ? r.pos : 0]);
+  if (certified) {
+    Acc::add(v, bv, aa, u, s, px, py, pz, dq, warm, tq);
+  } else if (done) {
+    const int pos = r2.pos[0];
+    const float4 q = bv.pts[pos >= 0 ? pos : 0];
+    if (exact) {
+      nnq[i] = make_float4(q.x, q.y, q.z, i2f(pos | (g > 0.f ? kCertBit : 0)));
+      if (g > 0.f) cert[i] = make_float4(px, py, pz, g);
+    }
+    Acc::add(v, bv, aa, u, s, px, py, pz, r2.d[0], pos, q);
   }
-  block_sum_to_slab<Acc::NV, kBS>(v, lds, slab + (int64_t)tb * Acc::RS);
+  if constexpr (Acc::kSums) block_sum_to_slab<Acc::NV, kBS>(v, lds, slab + (int64_t)tb * Acc::RS);
 }
 
 // Kabsch solve (align_icp.cpp:139-151; SolveKabsch :58-69): fp64 SVD,
@@ -647,9 +819,31 @@ __device__ void p2plane_update(const double* tot, const IcpParams& prm, IcpCore*
   if (nx < (double)prm.p2plane_eps) st->done = 1;
 }
 
+// RST_SUM_REF: tot = the covariance (row-major sums of k_cov_ref), the means
+// and cost from this iteration's sequential sums (align_icp.cpp:122,
+// 139-151; `dst_mean /= n` divides by float(n)).
+__device__ void p2point_ref_update(const double* tot, const IcpParams& prm, IcpCore* st) {
+  const float nf = (float)prm.n;
+  float dmean[3];
+  for (int r = 0; r < 3; ++r) dmean[r] = st->seq[r] / nf;
+  double cov[9];
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < 3; ++c) RST_M3(cov, r, c) = tot[r * 3 + c];
+  float Rq[9], t[3];
+  kabsch_solve(cov, st->smean, dmean, Rq, t);
+  for (int k = 0; k < 9; ++k) st->R[k] = Rq[k];
+  for (int k = 0; k < 3; ++k) st->t[k] = t[k];
+  st->last_cost = st->seq[3];
+  const int next = st->iter + 1;
+  st->iter = next;
+  if (next > 0 && prm.anneal_every > 0 && next % prm.anneal_every == 0) st->mu = st->mu / prm.anneal_div;
+}
+
 template <class Acc>
 __device__ __forceinline__ void acc_update(const double* tot, const IcpParams& prm, IcpCore* st) {
-  if constexpr (Acc::NV == kNP2Point)
+  if constexpr (std::is_same<Acc, RefAcc>::value)
+    p2point_ref_update(tot, prm, st);
+  else if constexpr (std::is_same<Acc, P2PointAcc>::value)
     p2point_update(tot, prm, st);
   else
     p2plane_update(tot, prm, st);
@@ -736,7 +930,7 @@ template <class Acc>
 __global__ __launch_bounds__(kBS, Acc::kFbMinWaves) void k_icp_fb(BvhView bv, AdjView av, AccArgs aa,
                                                 const float4* __restrict__ src,
                                                 IcpState* __restrict__ st,
-                                                int32_t* __restrict__ nnpos,
+                                                float4* __restrict__ nnq,
                                                 float4* __restrict__ cert,
                                                 const int32_t* __restrict__ qbuf,
                                                 const int32_t* __restrict__ qcnt, int nb1,
@@ -775,7 +969,7 @@ __global__ __launch_bounds__(kBS, Acc::kFbMinWaves) void k_icp_fb(BvhView bv, Ad
       float px, py, pz;
       xform(u.P, s.x, s.y, s.z, px, py, pz);
       const bool fin = finite3(px, py, pz);
-      int warm = nnpos[i];
+      int warm = f2i(nnq[i].w);
       if (warm >= 0) warm &= kPosMask;
       if (fin && warm < 0) warm = morton_seed(bv, px, py, pz);
       Best1 r;
@@ -785,8 +979,9 @@ __global__ __launch_bounds__(kBS, Acc::kFbMinWaves) void k_icp_fb(BvhView bv, Ad
         r.offer(d2_ref(px, py, pz, w.x, w.y, w.z), f2i(w.w), warm);
         search(bv, warm, px, py, pz, r);  // exact: warm leaf, then each ancestor's sibling
       }
-      nnpos[i] = r.pos;
-      Acc::add(v, bv, aa, u, s, px, py, pz, r.d, r.pos, bv.pts[r.pos >= 0 ? r.pos : 0]);
+      const float4 q = bv.pts[r.pos >= 0 ? r.pos : 0];
+      nnq[i] = make_float4(q.x, q.y, q.z, i2f(r.pos));
+      Acc::add(v, bv, aa, u, s, px, py, pz, r.d, r.pos, q);
     }
   } else if (E > 0) {
     const Uni u = load_uni(st);
@@ -806,7 +1001,7 @@ __global__ __launch_bounds__(kBS, Acc::kFbMinWaves) void k_icp_fb(BvhView bv, Ad
       float px, py, pz;
       xform(u.P, s.x, s.y, s.z, px, py, pz);
       const bool fin = finite3(px, py, pz);
-      int warm = nnpos[i];
+      int warm = f2i(nnq[i].w);
       if (warm >= 0) warm &= kPosMask;
       if (fin && warm < 0) warm = morton_seed(bv, px, py, pz);
       // the two nearest (their gap is the point's certificate), seeded with
@@ -831,14 +1026,16 @@ __global__ __launch_bounds__(kBS, Acc::kFbMinWaves) void k_icp_fb(BvhView bv, Ad
       const Best1 r = r2.first();
       if (lane == 0) {
         const bool cok = fin && r.pos >= 0;
-        nnpos[i] = cok ? (r.pos | kCertBit) : r.pos;
+        const float4 q = bv.pts[r.pos >= 0 ? r.pos : 0];
+        nnq[i] = make_float4(q.x, q.y, q.z, i2f(cok ? (r.pos | kCertBit) : r.pos));
         if (cok) cert[i] = make_float4(px, py, pz, sqrtf(r2.d[1]) * 0.99999f);
-        Acc::add(v, bv, aa, u, s, px, py, pz, r.d, r.pos, bv.pts[r.pos >= 0 ? r.pos : 0]);
+        Acc::add(v, bv, aa, u, s, px, py, pz, r.d, r.pos, q);
       }
     }
   }
-  block_sum_to_slab_fold<Acc::NV, kBS>(v, lds, slab2 + (int64_t)blockIdx.x * Acc::RS, slab1, nb1,
-                                       Acc::RS, blockIdx.x, gridDim.x);
+  if constexpr (Acc::kSums)
+    block_sum_to_slab_fold<Acc::NV, kBS>(v, lds, slab2 + (int64_t)blockIdx.x * Acc::RS, slab1, nb1,
+                                         Acc::RS, blockIdx.x, gridDim.x);
 }
 
 inline int blocks_for(int64_t n) { return (int)std::max<int64_t>(1, (n + kBS - 1) / kBS); }
@@ -895,6 +1092,13 @@ int solve_kabsch_device(rst_ctx* ctx, const float* d_src, const float* d_dst,
   return RST_OK;
 }
 
+// k_seq_sum4 on a device float4 stream (rst_debug_seq_sum4): d_out[4]
+int seq_sum4_device(rst_ctx* ctx, const float4* d_x, int64_t n, float* d_out) {
+  k_seq_sum4<<<1, kWave, 0, ctx->stream>>>(d_x, n, d_out);
+  RST_HIP(hipGetLastError());
+  return RST_OK;
+}
+
 int centroid_device(rst_ctx* ctx, const float4* d_pts, int64_t n, double* d_out) {
   const int nb = std::min(1024, blocks_for(n));
   k_centroid_partial<<<nb, kBS, 0, ctx->stream>>>(d_pts, n, d_out);
@@ -908,7 +1112,7 @@ int centroid_device(rst_ctx* ctx, const float4* d_pts, int64_t n, double* d_out)
 // enqueued), or an error.
 int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
                const rst_icp_opts* opts_in, const float pose_in[16], rst_comm* comm,
-               bool chain) {
+               bool chain, int level) {
   if (!ctx || !src || !tgt || !pose_in) return RST_E_ARG;
   ctx->pend = {};
   rst_icp_opts opts;
@@ -919,6 +1123,11 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
   const bool p2plane = opts.mode == RST_P2PLANE;
   if (opts.mode != RST_P2POINT_REF && opts.mode != RST_P2PLANE) return RST_E_ARG;
   if (opts.max_iter < 0) return RST_E_ARG;
+  if (opts.sum_mode != RST_SUM_REF && opts.sum_mode != RST_SUM_FP64) return RST_E_ARG;
+  // the reference's sequential sums (P2POINT_REF only; one ordered pass over
+  // the whole source has no shard decomposition)
+  const bool refsum = !p2plane && opts.sum_mode == RST_SUM_REF;
+  if (refsum && comm) return RST_E_ARG;
   if (!tgt->has_bvh) return RST_E_ARG;
   if (tgt->m >= kCertBit) return RST_E_ARG;  // positions carry kCertBit
   if (p2plane && !tgt->nrm) return RST_E_STATE;
@@ -927,6 +1136,10 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
   hipStream_t st = ctx->stream;
   // one scratch buffer: [centroid / kernel-1 slab | kernel-2 slab | totals]
   const int nblk = blocks_for(n_local);
+  // k_icp_fb scans the per-block queue counts into dynamic LDS, on top of
+  // ~28 KB of static LDS (4 WnnScratch + the reductions): 96 KB caps the
+  // source at ~6.3M points per align (per shard when sharded)
+  if (sizeof(int) * ((size_t)nblk + 1) > (size_t)96 * 1024) return RST_E_ARG;
   const int NV = p2plane ? kNP2Plane : kNP2Point;
   const int RS = p2plane ? P2PlaneAcc::RS : P2PointAcc::RS;
   const int ncb = std::min(1024, blocks_for(n_local));
@@ -952,13 +1165,43 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
   if (n_total < 3 || tgt->m < 3) return RST_FALSE;
   if (p2plane && n_total < 6) return RST_FALSE;
 
+  // per source point: sorted target position of its last neighbour (warm
+  // start of the next iteration's exact search; -1 = cold); the fallback
+  // queue (one kBS segment per kernel-1 block) and its per-block counts;
+  // RST_SUM_REF: the correspondences and the source in original order
+  float4* nnq = nullptr;  // last neighbour (p, pos | kCertBit), -1 = cold
+  int32_t *qbuf = nullptr, *qcnt = nullptr;
+  float4* cert = nullptr;  // far-point certificates (read only under kCertBit)
+  float4 *corr = nullptr, *srco = nullptr;
+  {
+    const size_t np = (size_t)std::max<int64_t>(n_local, 1);
+    const size_t nq = (size_t)nblk * kBS;
+    void* w = nullptr;
+    RST_CHECK(ctx_workspace(ctx, sizeof(float4) * np * (refsum ? 4 : 2) +
+                                     sizeof(int32_t) * (nq + 2 * nblk + 64),
+                            &w));
+    cert = (float4*)w;
+    nnq = cert + np;
+    corr = refsum ? cert + 2 * np : nullptr;
+    srco = refsum ? cert + 3 * np : nullptr;
+    qbuf = (int32_t*)(cert + np * (refsum ? 4 : 2));
+    qcnt = qbuf + nq;
+    RST_HIP(hipMemsetAsync(nnq, 0xff, sizeof(float4) * np, st));
+  }
+
   InitArgs ia;
   memcpy(ia.pose, pose_in, sizeof(ia.pose));
   ia.mu0 = opts.mu0;
-  ia.need_centroid = p2plane ? 0 : 1;
+  ia.need_centroid = p2plane ? 0 : (refsum ? 2 : 1);
   ia.chain = chain ? 1 : 0;
+  ia.n = n_total;
   int crows = 0;
-  if (!p2plane) {
+  float* fsum = (float*)totals;  // RST_SUM_REF: the centroid's sequential sums
+  if (refsum) {
+    k_gather_orig<<<blocks_for(n_local), kBS, 0, st>>>(src->pts, src->inv, n_local, srco);
+    k_seq_sum4<<<1, kWave, 0, st>>>(srco, n_local, fsum);  // point_cloud_utils.cpp:94-96
+    k_init_state<<<1, kBS, 0, st>>>(slab, 0, fsum, ia, ctx->d_state);
+  } else if (!p2plane) {
     if (n_local > 0) {
       crows = centroid_device(ctx, src->pts, n_local, slab);
       if (crows < 0) return crows;
@@ -966,31 +1209,15 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
     if (comm) {
       k_slab_reduce<4><<<1, kRedBS, 0, st>>>(slab, crows, slab, 0, nullptr, totals);
       RST_CHECK(comm_allreduce_sum_f64(comm, totals, 4, st));
-      k_init_state<<<1, kBS, 0, st>>>(totals, 1, ia, ctx->d_state);
+      k_init_state<<<1, kBS, 0, st>>>(totals, 1, nullptr, ia, ctx->d_state);
     } else {
-      k_init_state<<<1, kBS, 0, st>>>(slab, crows, ia, ctx->d_state);
+      k_init_state<<<1, kBS, 0, st>>>(slab, crows, nullptr, ia, ctx->d_state);
     }
   } else {
-    k_init_state<<<1, kBS, 0, st>>>(slab, 0, ia, ctx->d_state);
-  }
-  // per source point: sorted target position of its last neighbour (warm
-  // start of the next iteration's exact search; -1 = cold); the fallback
-  // queue (one kBS segment per kernel-1 block) and its per-block counts
-  int32_t *nnpos = nullptr, *qbuf = nullptr, *qcnt = nullptr;
-  float4* cert = nullptr;  // far-point certificates (read only under kCertBit)
-  {
-    const size_t np = (size_t)std::max<int64_t>(n_local, 1);
-    const size_t nq = (size_t)nblk * kBS;
-    void* w = nullptr;
-    RST_CHECK(ctx_workspace(ctx, sizeof(float4) * np + sizeof(int32_t) * (np + nq + 2 * nblk + 64),
-                            &w));
-    cert = (float4*)w;
-    nnpos = (int32_t*)(cert + np);
-    qbuf = nnpos + np;
-    qcnt = qbuf + nq;
-    RST_HIP(hipMemsetAsync(nnpos, 0xff, sizeof(int32_t) * np, st));
+    k_init_state<<<1, kBS, 0, st>>>(slab, 0, nullptr, ia, ctx->d_state);
   }
   AccArgs aa;
+  aa.corr = corr;
   aa.nrm = tgt->nrm;
   aa.pmu = opts.p2plane_mu;
   aa.max_d2 = opts.p2plane_max_dist > 0 ? opts.p2plane_max_dist * opts.p2plane_max_dist : FLT_MAX;
@@ -1013,6 +1240,7 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
   prm.p2plane_max_d2 = opts.p2plane_max_dist > 0 ? opts.p2plane_max_dist * opts.p2plane_max_dist
                                                  : FLT_MAX;
   prm.max_iter = opts.max_iter;
+  prm.sum_mode = opts.sum_mode;
   // queue length from which the fallback runs one lane per query
   // (RST_LANE_MIN_DIV = k: n / k; tuning knob -- r01h sweep: 3n/4 was best;
   // r01j, with queued lanes seeding the fallback: n/3 17.0k, n/4 17.1k, n/2
@@ -1050,19 +1278,31 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
     if (n_local > 0) {
       if (p2plane) {
         k_icp_nn<P2PlaneAcc><<<nblk, kBS, 0, st>>>(bv, av, aa, src->pts, n_local, ctx->d_state,
-                                                   nnpos, cert, qbuf, qcnt, slab);
+                                                   nnq, cert, qbuf, qcnt, slab);
         if (tm) RST_HIP(hipEventRecord(ctx->ev[2 * it + 1], st));
         k_icp_fb<P2PlaneAcc><<<fb_grid, kBS, fb_lds, st>>>(bv, av, aa, src->pts, ctx->d_state,
-                                                             nnpos, cert, qbuf, qcnt, nblk,
+                                                             nnq, cert, qbuf, qcnt, nblk,
                                                              prm.lane_min, slab, slab2);
         k_reduce_solve<P2PlaneAcc><<<1, kRedBS, 0, st>>>(slab, 0, slab2, fb_grid, prm,
                                                          ctx->d_state, red_out);
+      } else if (refsum) {
+        k_icp_nn<RefAcc><<<nblk, kBS, 0, st>>>(bv, av, aa, src->pts, n_local, ctx->d_state,
+                                               nnq, cert, qbuf, qcnt, slab);
+        if (tm) RST_HIP(hipEventRecord(ctx->ev[2 * it + 1], st));
+        k_icp_fb<RefAcc><<<fb_grid, kBS, fb_lds, st>>>(bv, av, aa, src->pts, ctx->d_state, nnq,
+                                                         cert, qbuf, qcnt, nblk, prm.lane_min,
+                                                         slab, slab2);
+        // align_icp.cpp:113,120: sum dst[nbr_i] and cost, i ascending, fp32
+        k_seq_sum4<<<1, kWave, 0, st>>>(corr, n_local, ctx->d_state->seq);
+        k_cov_ref<<<kCovBlocks, kBS, 0, st>>>(srco, corr, n_local, ctx->d_state, slab2);
+        k_reduce_solve<RefAcc><<<1, kRedBS, 0, st>>>(slab, 0, slab2, kCovBlocks, prm,
+                                                     ctx->d_state, nullptr);
       } else {
         k_icp_nn<P2PointAcc><<<nblk, kBS, 0, st>>>(bv, av, aa, src->pts, n_local, ctx->d_state,
-                                                   nnpos, cert, qbuf, qcnt, slab);
+                                                   nnq, cert, qbuf, qcnt, slab);
         if (tm) RST_HIP(hipEventRecord(ctx->ev[2 * it + 1], st));
         k_icp_fb<P2PointAcc><<<fb_grid, kBS, fb_lds, st>>>(bv, av, aa, src->pts, ctx->d_state,
-                                                             nnpos, cert, qbuf, qcnt, nblk,
+                                                             nnq, cert, qbuf, qcnt, nblk,
                                                              prm.lane_min, slab, slab2);
         k_reduce_solve<P2PointAcc><<<1, kRedBS, 0, st>>>(slab, 0, slab2, fb_grid, prm,
                                                          ctx->d_state, red_out);
@@ -1085,7 +1325,10 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
   if (graph) {
     hipGraph_t g = nullptr;
     RST_HIP(hipStreamEndCapture(st, &g));
-    hipGraphExec_t& ex = ctx->gexec[{opts.max_iter, (int)p2plane}];
+    // one executable per (pyramid level, iterations, kernel sequence): the
+    // levels of one pyramid are queued back to back, so a level must never
+    // update an executable whose launch for another level is still pending
+    hipGraphExec_t& ex = ctx->gexec[std::make_tuple(level, opts.max_iter, (int)p2plane, (int)refsum)];
     if (ex) {
       hipGraphNode_t err_node = nullptr;
       hipGraphExecUpdateResult ur;

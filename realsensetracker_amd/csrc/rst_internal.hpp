@@ -12,6 +12,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <map>
+#include <tuple>
 #include <utility>
 #include <vector>
 
@@ -65,6 +66,8 @@ struct IcpCore {
   double last_d2;    // sum d2 of the last step
   int32_t fail;      // P2PLANE: singular system / too few points
   int32_t fb_e;      // fallback-queue entries of the current iteration
+  float seq[4];      // RST_SUM_REF: this iteration's sequential fp32 sums
+                     // (sum dst[nbr_i] xyz, cost), align_icp.cpp:113,120
 };
 
 struct IcpState : IcpCore {
@@ -83,6 +86,7 @@ struct IcpParams {
   float p2plane_max_d2;
   int32_t max_iter;
   int32_t lane_min;    // fallback queue length from which it runs one lane per query
+  int32_t sum_mode;    // rst_sum_mode
 };
 
 }  // namespace rst
@@ -108,9 +112,10 @@ struct rst_ctx {
   float last_kernel_ms = 0.f;
   int32_t last_kernel_launches = 0;
   // hipGraph replay of the ICP iteration loop (rst_ctx_enable_graphs):
-  // (iterations, mode) -> executable graph, updated in place per align
+  // (pyramid level, iterations, P2PLANE, RST_SUM_REF) -> executable graph,
+  // updated in place per align
   bool graphs = false;
-  std::map<std::pair<int, int>, hipGraphExec_t> gexec;
+  std::map<std::tuple<int, int, int, int>, hipGraphExec_t> gexec;
   // device memory of freed targets, kept for the next build (hipFree
   // synchronises the whole device, which would stall every stream of a
   // pipelined frame loop): size class -> blocks
@@ -190,7 +195,7 @@ int compute_normals(rst_ctx* ctx, rst_target* tgt, int k, const float vp[3]);
 // ICP (icp.hip)
 int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
                const rst_icp_opts* opts, const float pose_in[16], rst_comm* comm,
-               bool chain = false);
+               bool chain = false, int level = 0);
 int icp_finish(rst_ctx* ctx, float pose_inout[16], float* mean_cost, int32_t* iters_run);
 int icp_align_prepared(rst_ctx* ctx, const rst_target* src,
                        const rst_target* tgt, const rst_icp_opts* opts,
@@ -200,6 +205,7 @@ int solve_kabsch_device(rst_ctx* ctx, const float* d_src, const float* d_dst,
                         const int32_t* d_pairs, const float* d_w, int64_t k, float pose_out[16]);
 int centroid_device(rst_ctx* ctx, const float4* d_pts, int64_t n,
                     double* d_out3);
+int seq_sum4_device(rst_ctx* ctx, const float4* d_x, int64_t n, float* d_out);
 int kabsch_device(rst_ctx* ctx, const double cov[9], const float smean[3],
                   const float dmean[3], float pose_out[16]);
 

@@ -708,6 +708,47 @@ RST_HD void scan_range_wide<Best1>(const BvhView& bv, int b, int n, float qx, fl
   r.pos = bj >= 0 ? b + bj : r.pos;
 }
 
+// Best2 form: the two lexicographically smallest (d2, id) keys as 64-bit
+// integers (d2 >= 0 orders like its bits); a point already held (same id)
+// is never re-inserted.
+template <>
+RST_HD void scan_range_wide<Best2>(const BvhView& bv, int b, int n, float qx, float qy, float qz,
+                                   Best2& r) {
+  const rst_f2 qxy = {qx, qy};
+  uint64_t k0 = ((uint64_t)(uint32_t)f2i(r.d[0]) << 32) | (uint32_t)r.id[0];
+  uint64_t k1 = ((uint64_t)(uint32_t)f2i(r.d[1]) << 32) | (uint32_t)r.id[1];
+  int p0 = r.pos[0], p1 = r.pos[1];
+  for (int j0 = 0; j0 < n; j0 += 8) {
+    const float4* base = bv.pts + b + j0;
+    float4 p[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) p[j] = base[j];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const rst_f2 pxy = {p[j].x, p[j].y};
+      const rst_f2 dxy = qxy - pxy;
+      const rst_f2 sq = dxy * dxy;
+      const float dz = qz - p[j].z;
+      float d2 = sq.x + sq.y;
+      d2 = d2 + dz * dz;
+      const uint64_t key = ((uint64_t)(uint32_t)f2i(d2) << 32) | (uint32_t)f2i(p[j].w);
+      const bool in = (j0 + j < n) & (key != k0) & (key < k1);
+      const bool first = in & (key < k0);
+      const int pos = b + j0 + j;
+      k1 = first ? k0 : (in ? key : k1);
+      p1 = first ? p0 : (in ? pos : p1);
+      k0 = first ? key : k0;
+      p0 = first ? pos : p0;
+    }
+  }
+  r.d[0] = i2f((int)(uint32_t)(k0 >> 32));
+  r.id[0] = (int)(uint32_t)k0;
+  r.pos[0] = p0;
+  r.d[1] = i2f((int)(uint32_t)(k1 >> 32));
+  r.id[1] = (int)(uint32_t)k1;
+  r.pos[1] = p1;
+}
+
 // When the ball is not covered (the query moved away from its last
 // neighbour, early ICP iterations), the warm candidate is first walked
 // through the adjacency: the listed leaf whose box is nearest to the query
@@ -784,6 +825,82 @@ RST_HD bool adj_search_wide(const BvhView& bv, const AdjView& av, int start,
     if (stop) break;
   }
   return true;
+}
+
+// The certificate search of the ICP fast path (icp.hip k_icp_nn): the two
+// nearest through the leaf adjacency of the leaf holding sorted position
+// `start`, every listed leaf whose box meets the ball of the running SECOND
+// distance scanned.  Returns the covered radius Rc (reach - dist(q, box(L)),
+// float margins applied): every point within Rc of q lies in a listed leaf.
+// Hence, with the scan's stop rule at the second radius r2:
+//   * r.first() is the exact nearest neighbour when sqrt(d[0]) < Rc;
+//   * every point other than it lies at >= min(r2, Rc) from q -- the
+//     point's certificate for later iterations (a query that moved by
+//     delta keeps the neighbour while |q' - p| + delta < that bound).
+// r arrives holding the warm offers.  Like adj_search_wide, one walk step
+// moves L to the listed leaf nearest to q when q lies outside the coverage
+// of the start leaf.
+RST_HD float adj_search2(const BvhView& bv, const AdjView& av, int start, float qx, float qy,
+                         float qz, Best2& r) {
+  const int nl = bv.nleaves;
+  int L = leaf_of(bv, start);
+  float dl = 0.f, reach = 0.f;
+  for (int step = 0;; ++step) {
+    const float4 lo = bv.nodes[2 * (nl + L)], hi = bv.nodes[2 * (nl + L) + 1];
+    reach = av.reach[L];
+    dl = margin_sqrt(box_d2(qx, qy, qz, lo, hi)) * 1.00001f;
+    if (dl + margin_sqrt(r.d[0]) * 1.00001f + 1e-30f < reach * 0.99999f || step == kWalkSteps)
+      break;
+    const float4* e = av.ent + (int64_t)L * kAdjK * 2;
+    float bb = FLT_MAX;
+    int bx = -1;
+    for (int k = 1; k < kAdjK; ++k) {
+      const float4 l = e[2 * k], h = e[2 * k + 1];
+      const int tag = f2i(h.w);
+      const float b = box_d2(qx, qy, qz, l, h);
+      const bool t = tag >= 0 && b < bb;
+      bb = t ? b : bb;
+      bx = t ? tag : bx;
+    }
+    if (bx < 0 || !(bb < r.d[0])) break;
+    scan_range_wide(bv, bx >> 5, bx & 31, qx, qy, qz, r);
+    L = leaf_of(bv, r.pos[0]);
+  }
+  const float rc = reach * 0.99999f - dl;
+  if (!(dl + margin_sqrt(r.d[0]) * 1.00001f + 1e-30f < reach * 0.99999f)) return rc;
+  const float4* e = av.ent + (int64_t)L * kAdjK * 2;
+  for (int k0 = 0; k0 < kAdjK; k0 += 4) {
+    float4 l[4], h[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      l[j] = e[2 * (k0 + j)];
+      h[j] = e[2 * (k0 + j) + 1];
+    }
+    bool stop = false;
+    // stop radius from the second bound at the batch's start (it only
+    // shrinks: a later entry tested against it stops no earlier)
+    const float rad = margin_sqrt(r.d[1]) * 1.00001f + 1e-30f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (stop) break;
+      const int tag = f2i(h[j].w);
+      if (tag < 0 || l[j].w * 0.99999f - dl > rad) {
+        stop = true;
+      } else if (box_d2(qx, qy, qz, l[j], h[j]) <= r.d[1]) {
+        scan_range_wide(bv, tag >> 5, tag & 31, qx, qy, qz, r);
+      }
+    }
+    if (stop) break;
+  }
+  return rc;
+}
+
+// The certificate bound of adj_search2's result (0: none): min(r2, Rc)
+// with the 1e-5 relative margins of every distance test here.
+RST_HD float cert_bound(const Best2& r, float rc) {
+  const float r2 = r.d[1] < FLT_MAX ? margin_sqrt(r.d[1]) * 0.99999f : FLT_MAX;
+  const float g = fminf(r2, rc);
+  return g > 0.f ? g : 0.f;
 }
 
 // ---- the ICP loop's candidate lists ----------------------------------------------------

@@ -10,9 +10,12 @@ scaling of AlignIcp3d (align_icp.cpp:92-153) to one node:
   global; every rank then solves the same pose (no broadcast).
 
 Host logic only: the RCCL communicator is created from a unique id that
-rank 0 draws and ``torch.distributed`` broadcasts (any backend; gloo in the
-CPU tests).  The per-iteration exchange is inside librst_align.so
-(``rst_icp_align_sharded_device``).
+rank 0 draws and broadcasts -- through ``rendezvous.Rendezvous`` (TCP; what
+``bench.py`` uses, no second HIP runtime in the process) or through a
+``torch.distributed`` group (the gloo CPU tests).  The per-iteration
+exchange is inside librst_align.so (``rst_icp_align_sharded_device``).
+The sequential-sum mode (RST_SUM_REF) has no shard decomposition: the
+sharded align runs RST_SUM_FP64.
 """
 from __future__ import annotations
 
@@ -33,8 +36,19 @@ def shard_bounds(n: int, world: int, rank: int) -> tuple[int, int]:
     return lo, lo + base + (1 if rank < extra else 0)
 
 
-def exchange_unique_id(group=None) -> bytes:
-    """Rank 0 draws the RCCL unique id; every rank returns the same bytes."""
+def _draw_unique_id() -> bytes:
+    raw = C.create_string_buffer(L.COMM_ID_BYTES)
+    L.check(L.lib().rst_comm_get_unique_id(raw), "rst_comm_get_unique_id")
+    return raw.raw
+
+
+def exchange_unique_id(group=None, rendezvous=None) -> bytes:
+    """Rank 0 draws the RCCL unique id; every rank returns the same bytes
+    (over a Rendezvous when given, else a torch.distributed group)."""
+    if rendezvous is not None:
+        uid = rendezvous.broadcast(_draw_unique_id() if rendezvous.rank == 0 else None)
+        assert len(uid) == L.COMM_ID_BYTES
+        return uid
     import torch.distributed as dist
     buf = [None]
     if dist.get_rank(group) == 0:
@@ -52,12 +66,15 @@ class ShardedAligner:
     target; all ranks return the same pose."""
 
     def __init__(self, ctx, group=None, world: int | None = None, rank: int | None = None,
-                 uid: bytes | None = None):
-        """Ranks from ``torch.distributed`` (the default), or given
-        explicitly with the RCCL unique id (e.g. world 1 without a process
-        group: the id is drawn locally)."""
+                 uid: bytes | None = None, rendezvous=None):
+        """Ranks from a ``rendezvous.Rendezvous``, from ``torch.distributed``
+        (the default), or given explicitly with the RCCL unique id (e.g.
+        world 1 without a process group: the id is drawn locally)."""
         self.ctx = ctx
-        if world is None:
+        if rendezvous is not None:
+            self.rank, self.world = rendezvous.rank, rendezvous.world
+            uid = exchange_unique_id(rendezvous=rendezvous)
+        elif world is None:
             import torch.distributed as dist
             self.rank = dist.get_rank(group)
             self.world = dist.get_world_size(group)
@@ -78,7 +95,7 @@ class ShardedAligner:
         pose = np.eye(4, dtype=np.float32) if pose is None else np.asarray(pose, np.float32)
         buf = L.pose_to_cm(pose)
         mc = C.c_float(0)
-        o = opts if opts is not None else L.default_opts()
+        o = opts if opts is not None else L.default_opts(sum_mode=L.RST_SUM_FP64)
         st = L.check(L.lib().rst_icp_align_sharded_device(
             self.ctx.handle, self._comm, C.c_void_p(d_src_shard), int(n_shard), target.handle,
             C.byref(o), L.fptr(buf), C.byref(mc)), "rst_icp_align_sharded_device")

@@ -47,6 +47,16 @@ def test_default_opts_are_reference_constants():
     assert o.mu0 == np.float32(1.0)     # align_icp.cpp:91
     assert o.anneal_every == 8          # align_icp.cpp:96
     assert o.anneal_div == np.float32(1.4)
+    assert o.sum_mode == L.RST_SUM_REF  # the reference's sequential fp32 sums
+    assert C.sizeof(L.IcpOpts) == 64    # layout unchanged: sum_mode took a reserved word
+
+
+def test_library_is_the_only_hip_runtime():
+    """_lib.lib() maps exactly one libamdhip64 (no torch import behind it)."""
+    import sys
+    L.lib()
+    assert "torch" not in sys.modules or L.hip_runtimes_mapped()
+    assert len(L.hip_runtimes_mapped()) <= 1
 
 
 def test_no_device_fails_loudly():

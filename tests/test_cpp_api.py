@@ -100,13 +100,10 @@ def test_replay_app_matches_oracle_replay(tmp_path, voxel_mm):
     if voxel_mm:
         frames = [O.downsample_voxel(O.remove_nans(c), voxel_mm * 1e-3) for c in frames]
     for f in range(1, 5):
-        ok, T, _, _ = O.align_icp(frames[f], frames[f - 1], 128)
-        ok64, T64, _, _ = O.align_icp(frames[f], frames[f - 1], 128, sum_mode=1)
-        assert ok and ok64
-        # the gates of test_gpu_parity.py: the oracle with the GPU's fp64 sums
-        # tightly; the reference's fp32 sequential sums within 1e-4 or twice
-        # the reference's own fp32-vs-fp64 sensitivity (small downsampled
-        # clouds are the sensitive case)
-        assert max(pose_err(got[f - 1], T64)) <= 2e-5, f
-        sens = max(pose_err(T, T64))
-        assert max(pose_err(got[f - 1], T)) <= max(1e-4, 2 * sens), (f, sens)
+        ok, T, _, _ = O.align_icp(frames[f], frames[f - 1], 128)  # reference arithmetic
+        assert ok
+        # the header's AlignIcp3d runs the library default RST_SUM_REF (the
+        # reference's fp32 sequential sums): the north_star gate, hard
+        e = pose_err(got[f - 1], T)
+        assert max(e) <= 1e-4, (f, e)
+        assert max(e) <= 2e-6, (f, e)

@@ -1,0 +1,84 @@
+"""CPU: the torch-free process plumbing of the multi-GPU bench and the
+sharded align (realsensetracker_amd/rendezvous.py) -- the launcher's rank
+environments and the TCP collectives at world size 2 and 3."""
+from __future__ import annotations
+
+import multiprocessing as mp
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from realsensetracker_amd import rendezvous as RV
+
+
+def test_rank_envs():
+    envs = RV.rank_envs(4, 29500, base={"PATH": "/bin", "RANK": "9"})
+    assert [e["RANK"] for e in envs] == ["0", "1", "2", "3"]
+    assert [e["LOCAL_RANK"] for e in envs] == ["0", "1", "2", "3"]
+    assert all(e["WORLD_SIZE"] == "4" and e["MASTER_PORT"] == "29500" for e in envs)
+    assert all(e["MASTER_ADDR"] == "127.0.0.1" and e["PATH"] == "/bin" for e in envs)
+    with pytest.raises(ValueError):
+        RV.rank_envs(0, 1)
+
+
+def _worker(rank, world, port, q):
+    r = RV.Rendezvous(rank, world, "127.0.0.1", port, timeout=60)
+    r.barrier()
+    s = r.allreduce([rank + 1.0, 10.0 * rank], "sum")
+    m = r.allreduce([float(rank)], "max")
+    b = r.broadcast(b"unique-id-bytes" if rank == 0 else None)
+    r.barrier()
+    r.close()
+    q.put((rank, s.tolist(), float(m[0]), b))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_collectives(world):
+    port = RV.free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    out = sorted(q.get(timeout=120) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want_sum = [sum(r + 1.0 for r in range(world)), sum(10.0 * r for r in range(world))]
+    for rank, s, m, b in out:
+        assert s == want_sum and m == world - 1 and b == b"unique-id-bytes"
+
+
+def test_world_one_needs_no_socket():
+    r = RV.Rendezvous(0, 1)
+    assert np.array_equal(r.allreduce([2.0, 3.0], "max"), [2.0, 3.0])
+    assert r.broadcast(b"x") == b"x"
+    r.barrier()
+
+
+def test_launch_runs_every_rank(tmp_path):
+    """bench.py --gpus N without a launcher: N processes with the rank
+    environment, the job's status the worst rank's."""
+    script = tmp_path / "probe.py"
+    root = str(RV.__file__).rsplit("/realsensetracker_amd", 1)[0]
+    script.write_text(
+        "import os, sys\n"
+        f"sys.path.insert(0, {root!r})\n"
+        "from realsensetracker_amd import rendezvous as RV\n"
+        "w, r, lr = RV.world_from_env()\n"
+        "rv = RV.Rendezvous(r, w)\n"
+        "tot = rv.allreduce([1.0])[0]\n"
+        "open(os.path.join(sys.argv[1], f'rank{r}'), 'w').write(f'{w} {lr} {tot}')\n"
+        "rv.close()\n"
+        "sys.exit(3 if (r == 1 and len(sys.argv) > 2) else 0)\n")
+    code = ("import sys; sys.path.insert(0, %r); from realsensetracker_amd import rendezvous as RV; "
+            "sys.exit(RV.launch(int(sys.argv[1]), sys.argv[2:], %r))"
+            % (root, str(script)))
+    r = subprocess.run([sys.executable, "-c", code, "3", str(tmp_path)], timeout=120)
+    assert r.returncode == 0
+    for k in range(3):
+        assert (tmp_path / f"rank{k}").read_text() == f"3 {k} 3.0"
+    r = subprocess.run([sys.executable, "-c", code, "2", str(tmp_path), "fail"], timeout=120)
+    assert r.returncode == 3
