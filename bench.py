@@ -98,40 +98,74 @@ def pingpong(k: int, n: int) -> int:
     return p if p < n else 2 * n - 2 - p
 
 
-def cpu_baseline(width: int, height: int, iters: int):
+def cpu_baseline(width: int, height: int, iters: int, levels: list | None = None):
     """The oracle's AlignIcp3d restatement (reference arithmetic, own
-    nanoflann-style kd-tree, 1 core) on one frame pair, first `iters` of the
-    128 iterations; tree build timed separately."""
+    nanoflann-style kd-tree) on one frame pair: 1 core (the reference is
+    single-threaded), then all cores (OpenMP over the per-point NN loop, the
+    sums sequential: same result) as a secondary field.  Sample: the first
+    `iters` of the 128 iterations; with `levels` (the pyramid), the same
+    coarse-to-fine chain as the GPU on the strided levels, `levels[l]`
+    iterations each, counted in level-0 equivalents.  Tree builds are timed
+    separately."""
     from oracle import oracle as O
     K = driver.intrinsics(width, height)
     sc = driver.SyntheticScene(0)
     da = sc.render(sc.trajectory(0), K, noise_seed=1)
     db = sc.render(sc.trajectory(1), K, noise_seed=2)
     K4 = [K.fx, K.fy, K.cx, K.cy]
-    pa, pb = O.unproject(da, K4), O.unproject(db, K4)
+    nlev = len(levels) if levels else 1
+    pa = [O.unproject(da, K4, stride=1 << lv) for lv in range(nlev)]
+    pb = [O.unproject(db, K4, stride=1 << lv) for lv in range(nlev)]
     t0 = time.perf_counter()
-    tree = O.KDTree(pa, 16)
+    trees = [O.KDTree(x, 16) for x in pa]
     t1 = time.perf_counter()
-    O.align_icp(pb, pa, iters, tree=tree)
-    t2 = time.perf_counter()
-    return {"value": iters / (t2 - t1), "unit": "ICP iterations/s", "cores": 1, "kind": "port",
-            "sample": f"1 frame pair {width}x{height} (n={len(pb)}, m={len(pa)}), first {iters} "
-                      f"of 128 P2POINT_REF iterations, oracle/rst_oracle.c -O3, kd-tree leaf 16 "
-                      f"prebuilt ({t1 - t0:.3f} s)",
-            "seconds": t2 - t1, "cpu": cpu_model()}
+    its = levels if levels else [iters]
+    eq = sum(its[lv] * len(pb[lv]) / len(pb[0]) for lv in range(nlev))  # level-0 equivalents
+
+    def one():
+        T = np.eye(4, dtype=np.float32)
+        ts = time.perf_counter()
+        for lv in reversed(range(nlev)):
+            _, T, _, _ = O.align_icp(pb[lv], pa[lv], its[lv], T=T, tree=trees[lv])
+        return time.perf_counter() - ts
+
+    dt1 = one()
+    cores = max(1, min(16, os.cpu_count() or 1))
+    O.set_threads(cores)
+    try:
+        dtn = one()
+    finally:
+        O.set_threads(1)
+    what = (f"{nlev}-level pyramid {width}x{height}, iterations {its} (finest first), "
+            f"{eq:.1f} level-0-equivalent iterations" if levels else
+            f"first {iters} of 128 P2POINT_REF iterations")
+    return {"value": eq / dt1, "unit": "ICP iterations/s", "cores": 1, "kind": "port",
+            "sample": f"1 frame pair {width}x{height} (n={len(pb[0])}, m={len(pa[0])}), {what}, "
+                      f"oracle/rst_oracle.c -O3, kd-tree leaf 16 prebuilt ({t1 - t0:.3f} s)",
+            "seconds": dt1, "cpu": cpu_model(),
+            "all_cores": {"value": eq / dtn, "cores": cores, "seconds": dtn,
+                          "note": "OpenMP over the per-point NN loop; sums sequential (identical "
+                                  "result); secondary baseline, for context"}}
 
 
 def load_traffic():
-    """Per-launch HBM bytes of the dominant kernel from the committed PMC
-    summary (profiles/pmc_*.json, written by scripts/pmc_summary.py)."""
-    files = sorted(ROOT.glob("profiles/pmc_*.json"))
-    if not files:
-        return None
+    """HBM bytes per iteration of the NN pass (k_icp_nn + k_icp_fb) from a
+    committed PMC summary (profiles/pmc_*.json, scripts/pmc_traffic.py) --
+    only one stamped with this library's source hash (lib/BUILD_INFO.json):
+    a pass of other code is not reported.  Returns (bytes | None, origin)."""
     try:
-        d = json.loads(files[-1].read_text())
-        return d.get("k_icp_nn_bytes_per_launch")
-    except Exception:
-        return None
+        cur = json.loads((ROOT / "realsensetracker_amd" / "lib" / "BUILD_INFO.json").read_text())
+        cur = cur.get("source_hash")
+    except (OSError, ValueError):
+        cur = None
+    for f in sorted(ROOT.glob("profiles/pmc_*.json"), reverse=True):
+        try:
+            d = json.loads(f.read_text())
+        except ValueError:
+            continue
+        if cur and d.get("source_hash") == cur and "nn_pass_bytes_per_iteration" in d:
+            return d["nn_pass_bytes_per_iteration"], f.name
+    return None, f"no PMC pass of this build (source hash {cur}) under profiles/"
 
 
 def p2point_alg_bytes(n: float, m: float) -> float:
@@ -249,6 +283,8 @@ def main():
                     help="frame pairs in flight per GPU (one HIP stream each)")
     ap.add_argument("--ref-steps", type=int, default=4,
                     help="frames timed in the reference-rounding mode (extra field; 0: skip)")
+    ap.add_argument("--roof-steps", type=int, default=4,
+                    help="frames of the one-pair-in-flight kernel timing pass (roofline)")
     a = ap.parse_args()
     if "WORLD_SIZE" not in os.environ and a.gpus > 1:
         # no launcher: one rank process per GPU, spawned before any GPU call
@@ -303,7 +339,8 @@ def main():
     pctx = A.Context(local)
     actx = [A.Context(local) for _ in range(max(1, a.inflight))]
 
-    def run(nsteps: int, opts, normals_k: int, stats: dict | None):
+    def run(nsteps: int, opts, normals_k: int, stats: dict | None, ctxs=None):
+        ctxs = ctxs or actx
         pending = deque()
 
         def prep(f):  # frame -> its level targets (one level unless pyramid)
@@ -316,15 +353,22 @@ def main():
             pa, c, cur, tgt = pending.popleft()
             r = pa.wait()
             if stats is not None:
-                # pyramid P2POINT_REF: every level runs its fixed count
-                stats["iters"] += r.iterations + (sum(lv_iters[1:]) if pyr and
-                                                  opts.mode == L.RST_P2POINT_REF else 0)
+                # pyramid P2POINT_REF: every level runs its fixed count; a coarse
+                # level's iteration is worth n_l / n_0 of a level-0 one
+                coarse = lv_iters[1:] if pyr and opts.mode == L.RST_P2POINT_REF else []
+                stats["iters"] += r.iterations + sum(
+                    it * len(cur[lv + 1]) / max(1, len(cur[0])) for lv, it in enumerate(coarse))
+                stats["iters_all"] += r.iterations + sum(coarse)
                 stats["n"] += len(cur[0])
                 stats["m"] += len(tgt[0])
                 stats["ok"] += int(r.ok)
                 ms, nl = c.last_kernel_time()
                 stats["kernel_ms"] += ms * nl
                 stats["launches"] += nl
+                if nl:
+                    it3, _ = c.last_iteration_times()
+                    for k in range(3):
+                        stats["iter_ms"][k] += it3[k] * nl
             for t in tgt:  # frame f: target of pair f, source of pair f-1 (done)
                 t.free()
 
@@ -333,9 +377,9 @@ def main():
         k = 1
         for s in range(nsteps):
             cur = prep(pingpong(k, nfr))
-            if len(pending) == len(actx):
+            if len(pending) == len(ctxs):
                 finish_one()
-            c = actx[s % len(actx)]
+            c = ctxs[s % len(ctxs)]
             # AlignIcp3d(curr, prev, 128, &xfm), xfm = Identity (rs_replay_app.cpp:235,251)
             if pyr:
                 pa = A.align_pyramid_async(cur, prev, c, lv_iters, None, opts)
@@ -349,22 +393,25 @@ def main():
         for t in prev:
             t.free()
 
+    def new_stats():
+        return {"iters": 0.0, "iters_all": 0, "n": 0, "m": 0, "ok": 0, "kernel_ms": 0.0,
+                "launches": 0, "iter_ms": [0.0, 0.0, 0.0]}
+
     if a.graphs:
         for c in actx:
             c.enable_graphs(True)
 
-    def timing(on: bool):
-        for c in actx:  # HIP events around k_icp_nn on every 8th iteration
-            c.enable_kernel_timing(8 if on and not a.graphs else 0)
+    def timing(on, ctxs=None):
+        for c in ctxs or actx:  # HIP events in each (every `on`-th) iteration
+            c.enable_kernel_timing(0 if a.graphs else int(on))
 
     def sync_all():
         for c in [pctx] + actx:
             c.synchronize()
 
-    # ---- reference mode (value) ------------------------------------------------
+    # ---- throughput mode (value): no events in the timed region -----------------
     run(a.warmup, opts_ref, 0, None)
-    timing(True)
-    st = {"iters": 0, "n": 0, "m": 0, "ok": 0, "kernel_ms": 0.0, "launches": 0}
+    st = new_stats()
     barrier()
     sync_all()
     t0 = time.perf_counter()
@@ -372,23 +419,32 @@ def main():
     sync_all()
     barrier()
     dt = max_over_ranks(time.perf_counter() - t0)
-    timing(False)
     iters_all = sum_over_ranks(st["iters"])
+    iters_raw = sum_over_ranks(st["iters_all"])  # pyramid: every level's iteration counted once
     frames_all = sum_over_ranks(a.steps)
+
+    # ---- roofline: one pair in flight, events around every iteration's kernels --
+    # (with two pairs in flight an event span also counts the CUs the other
+    # pair holds; alone, the spans agree with rocprof's kernel durations)
+    sr1 = new_stats()
+    if not a.graphs:
+        timing(1, actx[:1])
+        run(a.roof_steps, opts_ref, 0, sr1, ctxs=actx[:1])
+        timing(0, actx[:1])
 
     # ---- point-to-plane mode (extra fields) ---------------------------------------
     pl = None
     if not a.no_p2plane:
         run(a.warmup, opts_pl, 16, None)
-        timing(True)
-        sp = {"iters": 0, "n": 0, "m": 0, "ok": 0, "kernel_ms": 0.0, "launches": 0}
+        timing(8)
+        sp = new_stats()
         barrier()
         sync_all()
         t1 = time.perf_counter()
         run(a.steps, opts_pl, 16, sp)
         sync_all()
         barrier()
-        timing(False)
+        timing(0)
         dtp = max_over_ranks(time.perf_counter() - t1)
         pl = {"iterations_per_s": sum_over_ranks(sp["iters"]) / dtp,
               "frames_per_s": sum_over_ranks(a.steps) / dtp,
@@ -400,7 +456,7 @@ def main():
     refs = None
     if a.ref_steps > 0 and not pyr:
         run(1, opts_exact, 0, None)
-        sr = {"iters": 0, "n": 0, "m": 0, "ok": 0, "kernel_ms": 0.0, "launches": 0}
+        sr = new_stats()
         barrier()
         sync_all()
         t4 = time.perf_counter()
@@ -456,21 +512,24 @@ def main():
                 "note": "rs_tracker.cpp loop: DownsampleVoxel(0.1) + GICP ComputeAlignment "
                         "(covariances k=32, 16 x {exact NN, fp64 LM <= 64 evaluations})"}
 
-    # ---- roofline of the dominant kernel (k_p2point, HIP events) --------------------
-    avg_ms = st["kernel_ms"] / max(1, st["launches"])
+    # ---- roofline of the NN pass (k_icp_nn + k_icp_fb, one pair in flight) ----------
+    nl1 = max(1, sr1["launches"])
+    kern_us = [1000.0 * x / nl1 for x in sr1["iter_ms"]]  # nn | fb | rest, per iteration
+    nn_us = kern_us[0] + kern_us[1]
     n_avg = st["n"] / max(1, a.steps)
     m_avg = st["m"] / max(1, a.steps)
     alg_bytes = p2point_alg_bytes(n_avg, m_avg)
-    achieved = alg_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    achieved = alg_bytes / (nn_us * 1e-6) / 1e9 if nn_us > 0 else 0.0
     # the committed PMC pass is of the default workload only
-    traffic = load_traffic() if (a.workload, a.width, a.height) == ("stream", 640, 480) else None
+    traffic, traffic_src = (load_traffic() if (a.workload, a.width, a.height) ==
+                            ("stream", 640, 480) else (None, "PMC pass is of the 640x480 stream"))
 
     if rank != 0:
         rdv.close()
         return 0
     cpu = None
     if not a.no_cpu and world == 1:
-        cpu = cpu_baseline(a.width, a.height, a.cpu_iters)
+        cpu = cpu_baseline(a.width, a.height, a.cpu_iters, pyr_iters if pyr else None)
     value = iters_all / dt
     out = {
         "metric": METRIC, "value": value, "unit": "ICP iterations/s", "n_gpus": world,
@@ -488,15 +547,24 @@ def main():
                                 f"{a.iters} iters (reference loop)"),
                    "width": a.width, "height": a.height,
                    "iters_per_pair": sum(pyr_iters) if pyr else a.iters,
+                   "iteration_unit": ("level-0 equivalents: a level-l iteration counts n_l / n_0"
+                                      if pyr else "full-resolution ICP iteration"),
                    "points_per_frame": round(n_avg), "frames_cycled": nfr,
                    "accumulation": "fp64 partial sums", "parallelism": f"replica{world}",
                    "pairs_in_flight_per_gpu": len(actx), "hipgraph": bool(a.graphs)},
         "frames_per_s": frames_all / dt,
         "pairs_ok": st["ok"],
+        **({"iterations_all_levels_per_s": iters_raw / dt} if pyr else {}),
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "k_icp_nn", "avg_us": 1000.0 * avg_ms,
-                     "alg_bytes_per_launch": alg_bytes},
+                     "kernel": "k_icp_nn+k_icp_fb (one ICP iteration's NN pass: certificate "
+                               "stream + compacted searches)",
+                     "avg_us": nn_us, "alg_bytes_per_launch": alg_bytes,
+                     "kernels_avg_us": {"k_icp_nn": kern_us[0], "k_icp_fb": kern_us[1],
+                                        "rest_of_iteration": kern_us[2]},
+                     "timing": f"HIP events around every iteration's kernels, one pair in "
+                               f"flight, {a.roof_steps} frames ({sr1['launches']} iterations)",
+                     "traffic_source": traffic_src},
         "cpu_baseline": cpu,
     }
     if pl is not None:

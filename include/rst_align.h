@@ -108,6 +108,11 @@ int rst_ctx_synchronize(rst_ctx* ctx);
  * align call, measured with HIP events on the context's stream; and the
  * number of launches it covers.  Used by bench.py's roofline. */
 int rst_ctx_last_kernel_time(rst_ctx* ctx, float* avg_ms, int32_t* launches);
+/* The same events split over the whole iteration: avg_ms[0] = kernel 1
+ * (k_icp_nn, the certificate stream), [1] = kernel 2 (k_icp_fb, the
+ * searches), [2] = the rest (reductions and the solve; RST_SUM_REF: also the
+ * sequential sums). */
+int rst_ctx_last_iteration_times(rst_ctx* ctx, float avg_ms[3], int32_t* iterations);
 /* hipGraph mode (BASELINE configs[4]): each align's iteration loop is
  * captured and replayed as one graph (the executable for a given iteration
  * count and mode is kept on the context and updated in place with the next

@@ -57,6 +57,7 @@ def lib():
         L.orc_align_icp_ex.argtypes = [_f, C.c_int64, _f, C.c_int64, P, C.c_int, _f, _f,
                                        C.POINTER(_Trace), C.c_int]
         L.orc_p2point_partials.argtypes = [_f, C.c_int64, P, _f, _f, _f, C.c_float, _d]
+        L.orc_set_threads.argtypes = [C.c_int]
         L.orc_compute_normals.argtypes = [_f, C.c_int64, P, C.c_int, _f, _f]
         L.orc_unproject.restype = C.c_int64
         L.orc_unproject_strided.restype = C.c_int64
@@ -186,6 +187,11 @@ def solve_kabsch(src, dst, pairs, weights=None, T=None):
     ok = lib().orc_solve_kabsch(_fp(src), len(src), _fp(dst), len(dst), p.ctypes.data_as(_i),
                                 None if w is None else _fp(w), len(p), _fp(out))
     return bool(ok), _uncm(out)
+
+
+def set_threads(k: int) -> None:
+    """OpenMP threads of the NN loop (1 = the reference's single thread)."""
+    lib().orc_set_threads(int(k))
 
 
 def align_icp(src, dst, max_iter=128, T=None, tree: KDTree | None = None, trace=False,

@@ -689,6 +689,11 @@ int orc_solve_kabsch(const float* src, int64_t n, const float* dst, int64_t m,
 }
 
 /* ------------------------------------------------------------------------ */
+/* OpenMP threads of the per-point NN loop (1 = the reference's single
+ * thread; the all-cores CPU baseline sets more).  Results do not depend on it. */
+static int g_threads = 1;
+void orc_set_threads(int k) { g_threads = k < 1 ? 1 : k; }
+
 /* AlignIcp3d (align_icp.cpp:73-161; 4-arg overload :163-167) */
 int orc_align_icp(const float* src, int64_t n, const float* dst, int64_t m,
                   const orc_kdtree* tree, int max_iter, float pose_inout[16],
@@ -719,6 +724,7 @@ int orc_align_icp_ex(const float* src, int64_t n, const float* dst, int64_t m,
   }
   int32_t* nbrs = (int32_t*)malloc(sizeof(int32_t) * (size_t)n);
   float* weights = (float*)malloc(sizeof(float) * (size_t)n);
+  float* d2s = (float*)malloc(sizeof(float) * (size_t)n);
   float cost = 0.0f;
   float mu = 1.0f;
   for (int iter = 0; iter < max_iter; ++iter) {
@@ -726,12 +732,23 @@ int orc_align_icp_ex(const float* src, int64_t n, const float* dst, int64_t m,
     float dmean[3] = {0.0f, 0.0f, 0.0f};
     double dsum[3] = {0, 0, 0}, csum = 0;
     cost = 0.0f;
-    for (int64_t i = 0; i < n; ++i) { /* :105-121 */
+    /* :107,112 -- the per-point transform and exact 1-NN are independent of
+     * each other: with orc_set_threads(k > 1) they run on k OpenMP threads
+     * (the all-cores CPU baseline); every sum below stays sequential in i,
+     * so the result is identical for any thread count */
+#pragma omp parallel for schedule(static) num_threads(g_threads) if (g_threads > 1)
+    for (int64_t i = 0; i < n; ++i) {
       float p[3];
       xform(R, t, src + 3 * i, p);
       int32_t j = 0;
       float d2 = 0;
       orc_kdtree_knn(tree, p, 1, &j, &d2);
+      nbrs[i] = j;
+      d2s[i] = d2;
+    }
+    for (int64_t i = 0; i < n; ++i) { /* :105-121 */
+      const int32_t j = nbrs[i];
+      const float d2 = d2s[i];
       cost += d2;
       csum += (double)d2;
       nbrs[i] = j;
@@ -796,6 +813,7 @@ int orc_align_icp_ex(const float* src, int64_t n, const float* dst, int64_t m,
   if (mean_cost) *mean_cost = mc;
   free(nbrs);
   free(weights);
+  free(d2s);
   if (own) orc_kdtree_free(own);
   return mc < 10000.0f; /* :160 */
 }

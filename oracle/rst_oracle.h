@@ -110,6 +110,10 @@ int orc_align_icp_ex(const float* src, int64_t n, const float* dst, int64_t m,
                      const orc_kdtree* tree, int max_iter, float pose_inout[16],
                      float* mean_cost, orc_icp_trace* trace, int sum_mode);
 
+/* Threads of orc_align_icp*'s per-point NN loop (OpenMP; default 1).  The
+ * sums stay sequential: results are identical for any count. */
+void orc_set_threads(int k);
+
 /* One P2POINT_REF iteration's 16 fp64 partial sums over a source range, given
  * the current pose (the quantities the GPU kernels reduce; used by the
  * sharded-host-logic tests):

@@ -69,6 +69,13 @@ class Context:
         L.check(L.lib().rst_ctx_last_kernel_time(self._h, C.byref(ms), C.byref(n)), "timing")
         return ms.value, n.value
 
+    def last_iteration_times(self):
+        """Average ms per timed iteration: (kernel 1, kernel 2, the rest), n."""
+        ms = np.zeros(3, np.float32)
+        n = C.c_int32(0)
+        L.check(L.lib().rst_ctx_last_iteration_times(self._h, L.fptr(ms), C.byref(n)), "timing")
+        return [float(x) for x in ms], n.value
+
     def close(self):
         if self._h:
             L.lib().rst_ctx_destroy(self._h)

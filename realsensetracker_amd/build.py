@@ -12,6 +12,7 @@ from __future__ import annotations
 import argparse
 import concurrent.futures as cf
 import hashlib
+import json
 import os
 import shutil
 import subprocess
@@ -83,7 +84,22 @@ def build_library(jobs: int = 8, out: Path | None = None) -> Path:
     if r.returncode != 0:
         raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
     os.replace(tmp, out)
+    if out == LIBDIR / LIB_NAME:
+        (LIBDIR / "BUILD_INFO.json").write_text(json.dumps({"source_hash": source_hash()}) + "\n")
     return out
+
+
+def source_hash() -> str:
+    """Hash of every kernel / C-ABI source and the flags: identifies the
+    code a measurement (PMC traffic, profiles) was taken on, on the GPU box
+    too (no .git there)."""
+    h = hashlib.sha1()
+    for p in sorted(CSRC.glob("*.hip")) + sorted(CSRC.glob("*.hpp")) + sorted(CSRC.glob("*.cpp")) + \
+            sorted(INCLUDE.glob("*.h")):
+        h.update(p.name.encode())
+        h.update(p.read_bytes())
+    h.update(" ".join(CFLAGS).encode())
+    return h.hexdigest()[:16]
 
 
 def build_app() -> Path:

@@ -248,6 +248,13 @@ int rst_ctx_last_kernel_time(rst_ctx* ctx, float* avg_ms, int32_t* launches) {
   return RST_OK;
 }
 
+int rst_ctx_last_iteration_times(rst_ctx* ctx, float avg_ms[3], int32_t* iterations) {
+  if (!ctx || !avg_ms) return RST_E_ARG;
+  for (int k = 0; k < 3; ++k) avg_ms[k] = ctx->last_iter_ms[k];
+  if (iterations) *iterations = ctx->last_kernel_launches;
+  return RST_OK;
+}
+
 int rst_ctx_enable_graphs(rst_ctx* ctx, int enable) {
   if (!ctx) return RST_E_ARG;
   ctx->graphs = enable != 0;

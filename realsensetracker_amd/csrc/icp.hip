@@ -47,10 +47,27 @@ constexpr int kNP2Plane = 30;  // A (21), b (6), sum w r^2, count, sum d2
 #endif
 constexpr int kCertBit = 1 << 30;
 #ifndef RST_NN_MIN_WAVES
-#define RST_NN_MIN_WAVES 5  // k_icp_nn<P2PointAcc>: one round of waves at 640x480; r01i A/B: 6 -> 15.5k, 8 -> 14.2k it/s (vs 16.2k)
+#define RST_NN_MIN_WAVES 4  // k_icp_nn<P2PointAcc> (r02: Best2 certificate search, 96 VGPRs spilled at 5)
 #endif
-#ifndef RST_QUEUE_WARM
-#define RST_QUEUE_WARM 1
+#ifndef RST_COLD_ITERS
+#define RST_COLD_ITERS 0  // iterations of a pair that run the LDS-tile kernel 1 (r02g: the cold
+                          // NN distances of the stream, 4 cm median, 15 cm p99.9, need tiles
+                          // far larger than LDS holds; off)
+#endif
+#ifndef RST_TILE_MARGIN
+#define RST_TILE_MARGIN 0.025f  // metres the tile's box is grown by
+#endif
+#ifndef RST_COLD_FAST
+#define RST_COLD_FAST 1
+#endif
+#ifndef RST_COLD_ADJ2
+#define RST_COLD_ADJ2 0
+#endif
+#ifndef RST_PROJ_SEED
+#define RST_PROJ_SEED 1  // cold queries start at their projection into a frame target's pixel grid
+#endif
+#ifndef RST_DIAG
+#define RST_DIAG 0  // 1: per-iteration certificate counters (rst_debug_queue_trace)
 #endif
 #ifndef RST_LANE_SMALL_N
 #define RST_LANE_SMALL_N 150000  // clouds below this keep the 3n/4 lane-mode threshold (720p pyramid coarse levels; r01k A/B 14.0k -> 14.2k it/s)
@@ -81,19 +98,13 @@ __device__ __forceinline__ int xcd_tile(int b, int nb) {
 constexpr int kPosMask = kCertBit - 1;
 constexpr int kFbBlocks = 2048;  // largest fallback grid (RST_FB_BLOCKS)
 constexpr int kFbDefault = 1024;  // fallback grid (4096 waves; r01g sweep: 2048 / 512 lose)
-// From a queue of lane_min entries (IcpParams; 3/4 of the source points: the
-// cold first iteration, where most lanes' warm balls are not covered) the
-// fallback kernel gives every queued query one lane instead of one
-// wavefront: the per-lane exact search (rst_bvh.hpp search_from) issues 64x
-// fewer instructions per query.  Shorter queues hold the far points, whose
-// per-lane searches are long chains: the wave search wins there (measured).
-// Blocks of the fallback grid that hold queue entries (k_icp_fb writes their
-// slab rows, k_reduce_solve reads them):
-__device__ __forceinline__ int fb_blocks(int E, int grid, int lane_min) {
-  const int per = E >= lane_min ? kBS : kBS / kWave;
-  return max(1, min(grid, (E + per - 1) / per));
-}
-
+// From a queue of lane_min entries (IcpParams: the cold first iterations,
+// where most lanes' last neighbour is far or missing) kernel 2 finishes the
+// queries its adjacency search leaves open one lane per query instead of
+// one wavefront per query: the per-lane exact search (rst_bvh.hpp
+// search_from) issues 64x fewer instructions per query.  Shorter queues
+// hold the far points, whose per-lane searches are long chains: the wave
+// search wins there (measured r01).
 __device__ __forceinline__ Pose3 load_pose(const IcpState* __restrict__ st) {
   Pose3 P;
 #pragma unroll
@@ -226,6 +237,7 @@ __global__ __launch_bounds__(kBS) void k_init_state(const double* __restrict__ c
     st->last_cnt = 0;
     st->last_d2 = 0;
     for (int k = 0; k < 4; ++k) st->seq[k] = 0.f;
+    st->guard = 0;
   }
 }
 
@@ -513,10 +525,16 @@ __device__ void queue_prefix(const int32_t* __restrict__ qcnt, int nb, int32_t* 
 //   cert[i] = (q0.x, q0.y, q0.z, g), valid under kCertBit: when the query
 //             was at q0 every target point but p lay at >= g.
 // A query now at q keeps p as its exact neighbour while |q - p| + |q - q0|
-// < g (triangle inequality, strict: no tie can arise), which kernel 1 tests
-// from coalesced loads alone -- no search, no dependent gather.
+// < g (triangle inequality, strict: no tie can arise).
+//
+// Kernel 1 is a pure stream: every lane tests its certificate from three
+// coalesced loads (source point, nnq, cert) -- no search, no dependent
+// gather -- and accumulates the certified correspondences; every other
+// lane goes to the search queue (in point order, one segment per block).
+// The searches run compacted in kernel 2, so no wavefront here waits on
+// one lane's search.
 template <class Acc>
-__global__ __launch_bounds__(kBS, Acc::kMinWaves) void k_icp_nn(BvhView bv, AdjView av, AccArgs aa,
+__global__ __launch_bounds__(kBS) void k_icp_nn(BvhView bv, AdjView av, AccArgs aa,
                                                 const float4* __restrict__ src, int64_t n,
                                                 const IcpState* __restrict__ st,
                                                 float4* __restrict__ nnq,
@@ -524,6 +542,7 @@ __global__ __launch_bounds__(kBS, Acc::kMinWaves) void k_icp_nn(BvhView bv, AdjV
                                                 int32_t* __restrict__ qbuf,
                                                 int32_t* __restrict__ qcnt,
                                                 double* __restrict__ slab) {
+  (void)av;
   __shared__ double lds[(kBS / kWave) * Acc::NV];
   __shared__ int wq[kBS / kWave];
   const int tb = xcd_tile(blockIdx.x, gridDim.x);
@@ -539,15 +558,13 @@ __global__ __launch_bounds__(kBS, Acc::kMinWaves) void k_icp_nn(BvhView bv, AdjV
   const bool act = i < n;
   const float4 s = act ? src[i] : make_float4(0.f, 0.f, 0.f, 0.f);
   const float4 tq = act ? nnq[i] : make_float4(0.f, 0.f, 0.f, i2f(-1));
-  float4 c = make_float4(0.f, 0.f, 0.f, 0.f);
   const int wb = f2i(tq.w);
   const bool has_cert = wb >= 0 && (wb & kCertBit);
-  if (act && has_cert) c = cert[i];
+  const float4 c = (act && has_cert) ? cert[i] : make_float4(0.f, 0.f, 0.f, 0.f);
   float px, py, pz;
   xform(u.P, s.x, s.y, s.z, px, py, pz);  // align_icp.cpp:107
   const bool fin = finite3(px, py, pz);
-  int warm = wb >= 0 ? (wb & kPosMask) : -1;
-  // :112 exact 1-NN: the certificate first
+  // :112 exact 1-NN by the certificate
   bool certified = false;
   float dq = FLT_MAX;
   if (act && fin && has_cert) {
@@ -556,32 +573,16 @@ __global__ __launch_bounds__(kBS, Acc::kMinWaves) void k_icp_nn(BvhView bv, AdjV
     const float moved = margin_sqrt((dx * dx + dy * dy) + dz * dz) * 1.00001f;
     certified = margin_sqrt(dq) * 1.00001f + moved + 1e-30f < c.w;
   }
-  // otherwise the two nearest through the leaf adjacency of the last
-  // neighbour (cold lanes: a Morton-code seed), seeded with it and its
-  // sorted successor so the second bound starts finite
-  Best2 r2;
-  r2.init();
-  bool exact = false;
-  float g = 0.f;
-  if (act && fin && !certified) {
-    if (warm < 0) warm = morton_seed(bv, px, py, pz);
-    const float4 w = bv.pts[warm];
-    r2.offer(d2_ref(px, py, pz, w.x, w.y, w.z), f2i(w.w), warm);
-    if (bv.m > 1) {
-      const int nb = warm + 1 < bv.m ? warm + 1 : warm - 1;
-      const float4 w2 = bv.pts[nb];
-      r2.offer(d2_ref(px, py, pz, w2.x, w2.y, w2.z), f2i(w2.w), nb);
-    }
-    const float rc = adj_search2(bv, av, warm, px, py, pz, r2);
-    exact = margin_sqrt(r2.d[0]) * 1.00001f + 1e-30f < rc;
-    if (exact) g = cert_bound(r2, rc);
-  }
-  const bool done = act && (!fin || certified || exact);
-  // lanes the adjacency could not certify go to the fallback queue, in
-  // point order within the block's segment
-  const bool need = act && !done;
+  const bool need = act && fin && !certified;
   const uint64_t bm = __ballot(need);
   const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+#if RST_DIAG
+  {  // diagnostics build: per iteration, lanes certified
+    const uint64_t cm = __ballot(act && certified);
+    const int it = st->iter;
+    if (lane == 0 && it < kQTrace) atomicAdd(&const_cast<IcpState*>(st)->path[it][0], __popcll(cm));
+  }
+#endif
   if (lane == 0) wq[wid] = __popcll(bm);
   __syncthreads();
   int before = 0, total = 0;
@@ -591,23 +592,97 @@ __global__ __launch_bounds__(kBS, Acc::kMinWaves) void k_icp_nn(BvhView bv, AdjV
     total += wq[w];
   }
   if (need) qbuf[tb * (int64_t)kBS + before + __popcll(bm & ((1ull << lane) - 1ull))] = (int)i;
-#if RST_QUEUE_WARM
-  // a queued lane hands the fallback the nearest point its scan saw (at
-  // least as near as the warm point): a tighter starting bound and a warm
-  // leaf nearer the query (any start keeps the fallback's search exact)
-  if (need) nnq[i] = make_float4(0.f, 0.f, 0.f, i2f(r2.pos[0]));
-#endif
   if (threadIdx.x == 0) qcnt[tb] = total;
-  if (certified) {
-    Acc::add(v, bv, aa, u, s, px, py, pz, dq, warm, tq);
-  } else if (done) {
+  if (certified)
+    Acc::add(v, bv, aa, u, s, px, py, pz, dq, f2i(tq.w) & kPosMask, tq);
+  else if (act && !fin)  // no neighbour: the query's untouched outputs
+    Acc::add(v, bv, aa, u, s, px, py, pz, FLT_MAX, -1, tq);
+  if constexpr (Acc::kSums) block_sum_to_slab<Acc::NV, kBS>(v, lds, slab + (int64_t)tb * Acc::RS);
+}
+
+// Kernel 1 of the cold iterations (the first of a pair: no neighbour is
+// known yet, or the pose still moves by centimetres, so the certificates
+// fail): each wavefront stages the target points around its 64 queries in
+// LDS (rst_wave_nn.hpp tile_stage, the box of the queries grown by
+// `margin`) and every lane scans the tile: its exact nearest neighbour when
+// that lies inside the grown box, with a fresh certificate.  The rest -- and
+// a wave whose tile does not fit (e.g. straddling a depth edge) -- goes to
+// the search queue exactly as in k_icp_nn.
+template <class Acc>
+__global__ __launch_bounds__(kBS) void k_icp_tile(BvhView bv, AccArgs aa,
+                                                  const float4* __restrict__ src, int64_t n,
+                                                  const IcpState* __restrict__ st,
+                                                  float4* __restrict__ nnq,
+                                                  float4* __restrict__ cert,
+                                                  int32_t* __restrict__ qbuf,
+                                                  int32_t* __restrict__ qcnt,
+                                                  double* __restrict__ slab, float margin) {
+  __shared__ double lds[(kBS / kWave) * Acc::NV];
+  __shared__ int wq[kBS / kWave];
+  __shared__ TileScratch tsc[kBS / kWave];
+  const int tb = blockIdx.x;
+  if (Acc::kCanFinish && st->done) {
+    if (threadIdx.x == 0) qcnt[tb] = 0;
+    return;
+  }
+  const Uni u = load_uni(st);
+  double v[Acc::NV];
+#pragma unroll
+  for (int k = 0; k < Acc::NV; ++k) v[k] = 0.0;
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+  const int64_t i = tb * (int64_t)kBS + threadIdx.x;
+  const bool act = i < n;
+  const float4 s = act ? src[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+  float px, py, pz;
+  xform(u.P, s.x, s.y, s.z, px, py, pz);  // align_icp.cpp:107
+  const bool fin = act && finite3(px, py, pz);
+  // the wave's queries' box, grown by the margin
+  const float lx = wnn_min_f(fin ? px : FLT_MAX) - margin;
+  const float ly = wnn_min_f(fin ? py : FLT_MAX) - margin;
+  const float lz = wnn_min_f(fin ? pz : FLT_MAX) - margin;
+  const float hx = wnn_max_f(fin ? px : -FLT_MAX) + margin;
+  const float hy = wnn_max_f(fin ? py : -FLT_MAX) + margin;
+  const float hz = wnn_max_f(fin ? pz : -FLT_MAX) + margin;
+  int ns = -1;
+  if (__ballot(fin) != 0) ns = tile_stage(bv, lx, ly, lz, hx, hy, hz, tsc[wid]);
+  if (ns == -2 && lane == 0) atomicOr(&const_cast<IcpState*>(st)->guard, 4);
+  Best2 r2;
+  r2.init();
+  bool exact = false;
+  float g = 0.f;
+  if (ns > 0 && fin) {
+    tile_scan(tsc[wid], ns, px, py, pz, r2);
+    // every target point off the tile lies beyond one face of the box
+    const float mq = fminf(fminf(fminf(px - lx, hx - px), fminf(py - ly, hy - py)),
+                           fminf(pz - lz, hz - pz)) * 0.99999f;
+    exact = r2.pos[0] >= 0 && margin_sqrt(r2.d[0]) * 1.00001f + 1e-30f < mq;
+    if (exact)
+      g = fminf(r2.d[1] < FLT_MAX ? margin_sqrt(r2.d[1]) * 0.99999f : FLT_MAX, mq);
+  }
+  const bool need = fin && !exact;
+  const uint64_t bm = __ballot(need);
+  if (lane == 0) wq[wid] = __popcll(bm);
+  __syncthreads();
+  int before = 0, total = 0;
+#pragma unroll
+  for (int w = 0; w < kBS / kWave; ++w) {
+    before += w < wid ? wq[w] : 0;
+    total += wq[w];
+  }
+  if (need) {
+    qbuf[tb * (int64_t)kBS + before + __popcll(bm & ((1ull << lane) - 1ull))] = (int)i;
+    // the tile's best point (if any) is the search's warm start
+    nnq[i] = make_float4(0.f, 0.f, 0.f, i2f(r2.pos[0]));
+  }
+  if (threadIdx.x == 0) qcnt[tb] = total;
+  if (exact) {
     const int pos = r2.pos[0];
-    const float4 q = bv.pts[pos >= 0 ? pos : 0];
-    if (exact) {
-      nnq[i] = make_float4(q.x, q.y, q.z, i2f(pos | (g > 0.f ? kCertBit : 0)));
-      if (g > 0.f) cert[i] = make_float4(px, py, pz, g);
-    }
+    const float4 q = bv.pts[pos];
+    nnq[i] = make_float4(q.x, q.y, q.z, i2f(pos | (g > 0.f ? kCertBit : 0)));
+    if (g > 0.f) cert[i] = make_float4(px, py, pz, g);
     Acc::add(v, bv, aa, u, s, px, py, pz, r2.d[0], pos, q);
+  } else if (act && !fin) {  // no neighbour: the query's untouched outputs
+    Acc::add(v, bv, aa, u, s, px, py, pz, FLT_MAX, -1, make_float4(0.f, 0.f, 0.f, 0.f));
   }
   if constexpr (Acc::kSums) block_sum_to_slab<Acc::NV, kBS>(v, lds, slab + (int64_t)tb * Acc::RS);
 }
@@ -918,16 +993,56 @@ __global__ void k_solve_only(const double* __restrict__ totals, IcpParams prm,
   *static_cast<IcpCore*>(st) = core;
 }
 
-// ---- kernel 2: the queued queries, one wavefront each --------------------------------
+// ---- kernel 2: the searches of the queued queries -----------------------------------
 // Queue entry e (global order: kernel 1's block segments in block order;
-// every block rebuilds their prefix in LDS from the per-block counts) is
-// handled by wave e mod W of this fixed grid; each wave adds its entries in
-// increasing e, so the slab is reproducible.  Only the first
-// nw = max(1, ceil(E / waves-per-block)) blocks have queries.  Every block
-// then folds kernel 1's slab rows b, b + G, ... into its own row, so the
-// solve kernel reduces G rows, not nb1 + G.  Block 0 publishes E.
+// every block rebuilds their prefix in LDS from the per-block counts) goes
+// to wavefront e / C of the grid (C = ceil(E / W)): each lane runs the
+// two-nearest search through the leaf adjacency of its last neighbour
+// (rst_wave_nn.hpp adj_search2; cold lanes: a Morton-code seed), which
+// answers most and refreshes their certificate.  What the adjacency does
+// not cover is finished by
+//   * (queue < lane_min) the whole wavefront, one query at a time: level-2,
+//     then level-3 adjacency with the leaves staged in LDS, else the staged
+//     BVH walk from the best point so far -- two nearest, so it leaves a
+//     certificate (far points: frame borders, occlusions);
+//   * (queue >= lane_min: the cold first iterations) the lane alone, a
+//     bottom-up BVH walk from its best point (rst_bvh.hpp search).
+// Each entry is added to its own lane's sums, so the slab is reproducible.
+// Every block then folds kernel 1's slab rows b, b + G, ... into its own
+// row, so the solve kernel reduces G rows.  Block 0 publishes E.
+// Projective warm start (frame targets): the query projected through the
+// target's pixel grid, the valid points of the 3 x 3 level pixels around it
+// offered to r.  Returns r's best position, -1 when no pixel held a point.
+// A start for the exact searches only -- never taken as the answer.
+__device__ __forceinline__ int proj_seed(const BvhView& bv, const PixView& pv, float x, float y,
+                                         float z, Best2& r) {
+  if (!pv.map || !(z > 0.f)) return -1;
+  const float iz = 1.0f / z;
+  const float u = (pv.fx * x * iz + pv.cx) / (float)pv.s;
+  const float v = (pv.fy * y * iz + pv.cy) / (float)pv.s;
+  if (!(u > -2.f && v > -2.f && u < (float)pv.w + 1.f && v < (float)pv.h + 1.f)) return -1;
+  const int uc = (int)floorf(u + 0.5f), vc = (int)floorf(v + 0.5f);
+  int cand[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {  // all map loads first: one latency
+    const int uu = uc + k % 3 - 1, vv = vc + k / 3 - 1;
+    const bool in = uu >= 0 && vv >= 0 && uu < pv.w && vv < pv.h;
+    cand[k] = in ? pv.map[(int64_t)vv * pv.w + uu] : -1;
+  }
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    const int c = cand[k];
+    if ((uint32_t)c < (uint32_t)bv.m) {
+      const float4 w = bv.pts[c];
+      r.offer(d2_ref(x, y, z, w.x, w.y, w.z), f2i(w.w), c);
+    }
+  }
+  return r.pos[0];
+}
+
 template <class Acc>
-__global__ __launch_bounds__(kBS, Acc::kFbMinWaves) void k_icp_fb(BvhView bv, AdjView av, AccArgs aa,
+__global__ __launch_bounds__(kBS, Acc::kFbMinWaves) void k_icp_fb(BvhView bv, AdjView av, PixView pv,
+                                                AccArgs aa,
                                                 const float4* __restrict__ src,
                                                 IcpState* __restrict__ st,
                                                 float4* __restrict__ nnq,
@@ -935,80 +1050,68 @@ __global__ __launch_bounds__(kBS, Acc::kFbMinWaves) void k_icp_fb(BvhView bv, Ad
                                                 const int32_t* __restrict__ qbuf,
                                                 const int32_t* __restrict__ qcnt, int nb1,
                                                 int lane_min, const double* __restrict__ slab1,
-                                                double* __restrict__ slab2) {
+                                                double* __restrict__ slab2, int64_t n) {
   extern __shared__ int pref[];  // [nb1 + 1]
   __shared__ double lds[(kBS / kWave) * Acc::NV];
   __shared__ WnnScratch wsc[kBS / kWave];
   if (Acc::kCanFinish && st->done) return;  // converged: nothing reads the slabs
-  // every block scans kernel 1's per-block queue counts into LDS (a few KB
-  // of L2 reads; cheaper than a separate prefix launch); block 0 publishes
-  // the queue length for the reduction
   queue_prefix(qcnt, nb1, pref, blockIdx.x == 0 ? st : nullptr);
   __syncthreads();
   const int E = pref[nb1];
-  const bool work = (int)blockIdx.x < fb_blocks(E, gridDim.x, lane_min);
   double v[Acc::NV];
 #pragma unroll
   for (int k = 0; k < Acc::NV; ++k) v[k] = 0.0;
-  if (!work) {
-    // no queries: the fold of kernel 1's rows only
-  } else if (E >= lane_min) {  // uniform: one lane per query, entries in order
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+  const bool many = E >= lane_min;  // uniform
+  // wavefront w of the grid takes the contiguous entries [w C, (w + 1) C),
+  // C = ceil(E / W): a short steady-state queue spreads a couple of entries
+  // over every wave (not all of it onto the first blocks' lanes), a long
+  // cold-start queue gives each wave runs of consecutive -- spatially
+  // coherent -- entries
+  const int W = gridDim.x * (kBS / kWave);
+  const int gw = blockIdx.x * (kBS / kWave) + wid;
+  const int C = (E + W - 1) / W;
+  const int e0 = gw * C, e1 = min(E, e0 + C);
+  if (e0 < e1) {
     const Uni u = load_uni(st);
-    const int T = gridDim.x * kBS;
-    for (int e = blockIdx.x * kBS + threadIdx.x; e < E; e += T) {
-      int lo = 0, hi = nb1 - 1;
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (pref[mid] <= e)
-          lo = mid;
-        else
-          hi = mid - 1;
-      }
-      const int i = qbuf[lo * (int64_t)kBS + (e - pref[lo])];
-      const float4 s = src[i];
-      float px, py, pz;
-      xform(u.P, s.x, s.y, s.z, px, py, pz);
-      const bool fin = finite3(px, py, pz);
-      int warm = f2i(nnq[i].w);
-      if (warm >= 0) warm &= kPosMask;
-      if (fin && warm < 0) warm = morton_seed(bv, px, py, pz);
-      Best1 r;
-      r.init();
-      if (fin) {
-        const float4 w = bv.pts[warm];
-        r.offer(d2_ref(px, py, pz, w.x, w.y, w.z), f2i(w.w), warm);
-        search(bv, warm, px, py, pz, r);  // exact: warm leaf, then each ancestor's sibling
-      }
-      const float4 q = bv.pts[r.pos >= 0 ? r.pos : 0];
-      nnq[i] = make_float4(q.x, q.y, q.z, i2f(r.pos));
-      Acc::add(v, bv, aa, u, s, px, py, pz, r.d, r.pos, q);
-    }
-  } else if (E > 0) {
-    const Uni u = load_uni(st);
-    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
-    const int W = gridDim.x * (kBS / kWave);
-    for (int e = blockIdx.x * (kBS / kWave) + wid; e < E; e += W) {
-      int lo = 0, hi = nb1 - 1;  // block segment holding entry e
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (pref[mid] <= e)
-          lo = mid;
-        else
-          hi = mid - 1;
-      }
-      const int i = qbuf[lo * (int64_t)kBS + (e - pref[lo])];
-      const float4 s = src[i];
-      float px, py, pz;
-      xform(u.P, s.x, s.y, s.z, px, py, pz);
-      const bool fin = finite3(px, py, pz);
-      int warm = f2i(nnq[i].w);
-      if (warm >= 0) warm &= kPosMask;
-      if (fin && warm < 0) warm = morton_seed(bv, px, py, pz);
-      // the two nearest (their gap is the point's certificate), seeded with
-      // the warm point and its sorted neighbour so the bound starts finite
+    for (int r0 = e0; r0 < e1; r0 += kWave) {  // uniform per wave
+      const int e = r0 + lane;
+      const bool has = e < e1;
+      int i = 0;
+      float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+      float px = 0.f, py = 0.f, pz = 0.f;
+      bool fin = false;
       Best2 r2;
       r2.init();
-      if (fin) {
+      bool exact = false;
+      float g = 0.f;
+      if (has) {
+        int lo = 0, hi = nb1 - 1;  // block segment holding entry e
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (pref[mid] <= e)
+            lo = mid;
+          else
+            hi = mid - 1;
+        }
+        i = qbuf[lo * (int64_t)kBS + (e - pref[lo])];
+        if ((uint32_t)i >= (uint32_t)n) {  // index guard (never expected)
+          atomicOr(&st->guard, 1);
+          i = 0;
+        }
+        s = src[i];
+        xform(u.P, s.x, s.y, s.z, px, py, pz);
+        fin = finite3(px, py, pz);  // (kernel 1 queues finite queries only)
+        int warm = f2i(nnq[i].w);
+        if (warm >= 0) warm &= kPosMask;
+        if (warm >= bv.m) {
+          atomicOr(&st->guard, 2);
+          warm = -1;
+        }
+        if (warm < 0) warm = proj_seed(bv, pv, px, py, pz, r2);
+        if (warm < 0) warm = morton_seed(bv, px, py, pz);
+        // seeded with the warm point and its sorted neighbour, so the
+        // second bound starts finite
         const float4 w = bv.pts[warm];
         r2.offer(d2_ref(px, py, pz, w.x, w.y, w.z), f2i(w.w), warm);
         if (bv.m > 1) {
@@ -1016,20 +1119,72 @@ __global__ __launch_bounds__(kBS, Acc::kFbMinWaves) void k_icp_fb(BvhView bv, Ad
           const float4 w2 = bv.pts[nb];
           r2.offer(d2_ref(px, py, pz, w2.x, w2.y, w2.z), f2i(w2.w), nb);
         }
+        const float rc = adj_search2(bv, av, warm, px, py, pz, r2);
+        exact = margin_sqrt(r2.d[0]) * 1.00001f + 1e-30f < rc;
+        if (exact) {
+          g = cert_bound(r2, rc);
+          const int pos = r2.pos[0];
+          const float4 q = bv.pts[pos];
+          nnq[i] = make_float4(q.x, q.y, q.z, i2f(pos | (g > 0.f ? kCertBit : 0)));
+          if (g > 0.f) cert[i] = make_float4(px, py, pz, g);
+          Acc::add(v, bv, aa, u, s, px, py, pz, r2.d[0], pos, q);
+        }
       }
-      // the level-2 and level-3 adjacency cover most far queries in a few
-      // memory round trips; the full walk from the warm leaf is exact for
-      // anything else
-      if (!nn_wave_adj(bv, av, kAdj2Shift, warm, px, py, pz, r2, wsc[wid]) &&
-          !nn_wave_adj(bv, av, kAdj3Shift, warm, px, py, pz, r2, wsc[wid]))
-        nn_wave_one(bv, warm, px, py, pz, r2, wsc[wid]);
-      const Best1 r = r2.first();
-      if (lane == 0) {
-        const bool cok = fin && r.pos >= 0;
-        const float4 q = bv.pts[r.pos >= 0 ? r.pos : 0];
-        nnq[i] = make_float4(q.x, q.y, q.z, i2f(cok ? (r.pos | kCertBit) : r.pos));
-        if (cok) cert[i] = make_float4(px, py, pz, sqrtf(r2.d[1]) * 0.99999f);
-        Acc::add(v, bv, aa, u, s, px, py, pz, r.d, r.pos, q);
+      const bool unres = has && fin && !exact;
+#if RST_DIAG
+      {  // diagnostics build: lanes answered by the adjacency search
+        const uint64_t em = __ballot(has && exact);
+        const int it = st->iter;
+        if (lane == 0 && it < kQTrace) atomicAdd(&st->path[it][1], __popcll(em));
+      }
+#endif
+      if (many) {
+        if (unres) {  // cold start: this lane's own exact walk
+          Best1 r = r2.first();
+#if RST_COLD_ADJ2
+          // the level-2 adjacency (nodes of 8 leaves: a reach several times
+          // larger) answers many cold queries before the full walk
+          if (!adj2_search(bv, av, r.pos, px, py, pz, r))
+#endif
+          {
+            // bottom-up from the best point so far, every ancestor's
+            // sibling box loaded up front (one latency, not one per level)
+#if RST_COLD_FAST
+            search_from_fast(bv, r.pos, px, py, pz, r);
+#else
+            search(bv, r.pos, px, py, pz, r);
+#endif
+          }
+          const float4 q = bv.pts[r.pos >= 0 ? r.pos : 0];
+          nnq[i] = make_float4(q.x, q.y, q.z, i2f(r.pos));
+          Acc::add(v, bv, aa, u, s, px, py, pz, r.d, r.pos, q);
+        }
+      } else {
+        uint64_t m = __ballot(unres);
+        while (m) {  // the wave on one query at a time
+          const int j = __ffsll((long long)m) - 1;
+          m &= m - 1;
+          const float qx = wnn_rl(px, j), qy = wnn_rl(py, j), qz = wnn_rl(pz, j);
+          Best2 rr;
+          rr.d[0] = wnn_rl(r2.d[0], j);
+          rr.d[1] = wnn_rl(r2.d[1], j);
+          rr.id[0] = __builtin_amdgcn_readlane(r2.id[0], j);
+          rr.id[1] = __builtin_amdgcn_readlane(r2.id[1], j);
+          rr.pos[0] = __builtin_amdgcn_readlane(r2.pos[0], j);
+          rr.pos[1] = __builtin_amdgcn_readlane(r2.pos[1], j);
+          const int start = rr.pos[0];
+          if (!nn_wave_adj(bv, av, kAdj2Shift, start, qx, qy, qz, rr, wsc[wid]) &&
+              !nn_wave_adj(bv, av, kAdj3Shift, start, qx, qy, qz, rr, wsc[wid]))
+            nn_wave_one(bv, start, qx, qy, qz, rr, wsc[wid]);
+          if (lane == j) {
+            const Best1 r = rr.first();
+            const bool cok = r.pos >= 0;
+            const float4 q = bv.pts[cok ? r.pos : 0];
+            nnq[i] = make_float4(q.x, q.y, q.z, i2f(cok ? (r.pos | kCertBit) : r.pos));
+            if (cok) cert[i] = make_float4(px, py, pz, margin_sqrt(rr.d[1]) * 0.99999f);
+            Acc::add(v, bv, aa, u, s, px, py, pz, r.d, r.pos, q);
+          }
+        }
       }
     }
   }
@@ -1223,6 +1378,7 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
   aa.max_d2 = opts.p2plane_max_dist > 0 ? opts.p2plane_max_dist * opts.p2plane_max_dist : FLT_MAX;
   aa.pos0 = tgt->pos0;
   const AdjView av = adj_of(tgt);
+  const PixView pv = RST_PROJ_SEED ? tgt->pix : PixView{};
   const size_t fb_lds = sizeof(int) * ((size_t)nblk + 1);
   // fallback grid (RST_FB_BLOCKS: tuning knob, <= kFbBlocks)
   static const int fb_grid = [] {
@@ -1255,10 +1411,20 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
                           : (n_local < RST_LANE_SMALL_N ? (3 * n_local) / 4 : n_local / 3));
 
   const BvhView bv = view_of(tgt);
+  // the first cold_iters iterations of a pair run the LDS-tile kernel 1
+  // (RST_COLD_ITERS, RST_TILE_MARGIN: tuning knobs, never correctness)
+  static const int cold_iters = [] {
+    const char* e = getenv("RST_COLD_ITERS");
+    return e ? atoi(e) : RST_COLD_ITERS;
+  }();
+  static const float tile_margin = [] {
+    const char* e = getenv("RST_TILE_MARGIN");
+    return e ? (float)atof(e) : RST_TILE_MARGIN;
+  }();
 
   const bool timing = ctx->timing && opts.max_iter > 0;
-  if (timing) {
-    const size_t need = 2 * (size_t)opts.max_iter;
+  if (timing) {  // four events per timed iteration: k1 | k2 | the rest
+    const size_t need = 4 * (size_t)opts.max_iter;
     while (ctx->ev.size() < need) {
       hipEvent_t e;
       RST_HIP(hipEventCreate(&e));
@@ -1274,41 +1440,61 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
   if (graph) RST_HIP(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
   for (int it = 0; it < opts.max_iter; ++it) {
     const bool tm = timing && it % ctx->timing_stride == 0;  // sampled iterations
-    if (tm) RST_HIP(hipEventRecord(ctx->ev[2 * it], st));
+    auto mark = [&](int k) -> int {
+      if (tm) RST_HIP(hipEventRecord(ctx->ev[4 * it + k], st));
+      return RST_OK;
+    };
+    RST_CHECK(mark(0));
     if (n_local > 0) {
       if (p2plane) {
-        k_icp_nn<P2PlaneAcc><<<nblk, kBS, 0, st>>>(bv, av, aa, src->pts, n_local, ctx->d_state,
-                                                   nnq, cert, qbuf, qcnt, slab);
-        if (tm) RST_HIP(hipEventRecord(ctx->ev[2 * it + 1], st));
-        k_icp_fb<P2PlaneAcc><<<fb_grid, kBS, fb_lds, st>>>(bv, av, aa, src->pts, ctx->d_state,
+        if (it < cold_iters)
+          k_icp_tile<P2PlaneAcc><<<nblk, kBS, 0, st>>>(bv, aa, src->pts, n_local, ctx->d_state, nnq,
+                                              cert, qbuf, qcnt, slab, tile_margin);
+        else
+          k_icp_nn<P2PlaneAcc><<<nblk, kBS, 0, st>>>(bv, av, aa, src->pts, n_local, ctx->d_state,
+                                             nnq, cert, qbuf, qcnt, slab);
+        RST_CHECK(mark(1));
+        k_icp_fb<P2PlaneAcc><<<fb_grid, kBS, fb_lds, st>>>(bv, av, pv, aa, src->pts, ctx->d_state,
                                                              nnq, cert, qbuf, qcnt, nblk,
-                                                             prm.lane_min, slab, slab2);
+                                                             prm.lane_min, slab, slab2, n_local);
+        RST_CHECK(mark(2));
         k_reduce_solve<P2PlaneAcc><<<1, kRedBS, 0, st>>>(slab, 0, slab2, fb_grid, prm,
                                                          ctx->d_state, red_out);
       } else if (refsum) {
-        k_icp_nn<RefAcc><<<nblk, kBS, 0, st>>>(bv, av, aa, src->pts, n_local, ctx->d_state,
-                                               nnq, cert, qbuf, qcnt, slab);
-        if (tm) RST_HIP(hipEventRecord(ctx->ev[2 * it + 1], st));
-        k_icp_fb<RefAcc><<<fb_grid, kBS, fb_lds, st>>>(bv, av, aa, src->pts, ctx->d_state, nnq,
+        if (it < cold_iters)
+          k_icp_tile<RefAcc><<<nblk, kBS, 0, st>>>(bv, aa, src->pts, n_local, ctx->d_state, nnq,
+                                              cert, qbuf, qcnt, slab, tile_margin);
+        else
+          k_icp_nn<RefAcc><<<nblk, kBS, 0, st>>>(bv, av, aa, src->pts, n_local, ctx->d_state,
+                                             nnq, cert, qbuf, qcnt, slab);
+        RST_CHECK(mark(1));
+        k_icp_fb<RefAcc><<<fb_grid, kBS, fb_lds, st>>>(bv, av, pv, aa, src->pts, ctx->d_state, nnq,
                                                          cert, qbuf, qcnt, nblk, prm.lane_min,
-                                                         slab, slab2);
+                                                         slab, slab2, n_local);
+        RST_CHECK(mark(2));
         // align_icp.cpp:113,120: sum dst[nbr_i] and cost, i ascending, fp32
         k_seq_sum4<<<1, kWave, 0, st>>>(corr, n_local, ctx->d_state->seq);
         k_cov_ref<<<kCovBlocks, kBS, 0, st>>>(srco, corr, n_local, ctx->d_state, slab2);
         k_reduce_solve<RefAcc><<<1, kRedBS, 0, st>>>(slab, 0, slab2, kCovBlocks, prm,
                                                      ctx->d_state, nullptr);
       } else {
-        k_icp_nn<P2PointAcc><<<nblk, kBS, 0, st>>>(bv, av, aa, src->pts, n_local, ctx->d_state,
-                                                   nnq, cert, qbuf, qcnt, slab);
-        if (tm) RST_HIP(hipEventRecord(ctx->ev[2 * it + 1], st));
-        k_icp_fb<P2PointAcc><<<fb_grid, kBS, fb_lds, st>>>(bv, av, aa, src->pts, ctx->d_state,
+        if (it < cold_iters)
+          k_icp_tile<P2PointAcc><<<nblk, kBS, 0, st>>>(bv, aa, src->pts, n_local, ctx->d_state, nnq,
+                                              cert, qbuf, qcnt, slab, tile_margin);
+        else
+          k_icp_nn<P2PointAcc><<<nblk, kBS, 0, st>>>(bv, av, aa, src->pts, n_local, ctx->d_state,
+                                             nnq, cert, qbuf, qcnt, slab);
+        RST_CHECK(mark(1));
+        k_icp_fb<P2PointAcc><<<fb_grid, kBS, fb_lds, st>>>(bv, av, pv, aa, src->pts, ctx->d_state,
                                                              nnq, cert, qbuf, qcnt, nblk,
-                                                             prm.lane_min, slab, slab2);
+                                                             prm.lane_min, slab, slab2, n_local);
+        RST_CHECK(mark(2));
         k_reduce_solve<P2PointAcc><<<1, kRedBS, 0, st>>>(slab, 0, slab2, fb_grid, prm,
                                                          ctx->d_state, red_out);
       }
     } else {
-      if (tm) RST_HIP(hipEventRecord(ctx->ev[2 * it + 1], st));
+      RST_CHECK(mark(1));
+      RST_CHECK(mark(2));
       // an empty shard still joins the all-reduce with zero partial sums
       RST_HIP(hipMemsetAsync(totals, 0, sizeof(double) * NV, st));
     }
@@ -1319,6 +1505,7 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
       else
         k_solve_only<P2PointAcc><<<1, 64, 0, st>>>(totals, prm, ctx->d_state);
     }
+    RST_CHECK(mark(3));
   }
   RST_HIP(hipGetLastError());
   RST_HIP(hipMemcpyAsync(ctx->h_state, ctx->d_state, sizeof(IcpState), hipMemcpyDeviceToHost, st));
@@ -1363,18 +1550,25 @@ int icp_finish(rst_ctx* ctx, float pose_inout[16], float* mean_cost, int32_t* it
   if (pd.early_false) return RST_FALSE;  // pose untouched (align_icp.cpp:77-79)
   RST_HIP(hipStreamSynchronize(ctx->stream));
   if (pd.timing) {
-    float total = 0.f;
+    float tot[3] = {0.f, 0.f, 0.f};
     int cnt = 0;
     for (int it = 0; it < pd.max_iter; it += ctx->timing_stride) {
-      float ms = 0.f;
-      RST_HIP(hipEventElapsedTime(&ms, ctx->ev[2 * it], ctx->ev[2 * it + 1]));
-      total += ms;
+      for (int k = 0; k < 3; ++k) {
+        float ms = 0.f;
+        RST_HIP(hipEventElapsedTime(&ms, ctx->ev[4 * it + k], ctx->ev[4 * it + k + 1]));
+        tot[k] += ms;
+      }
       ++cnt;
     }
-    ctx->last_kernel_ms = cnt ? total / cnt : 0.f;
+    ctx->last_kernel_ms = cnt ? tot[0] / cnt : 0.f;
+    for (int k = 0; k < 3; ++k) ctx->last_iter_ms[k] = cnt ? tot[k] / cnt : 0.f;
     ctx->last_kernel_launches = cnt;
   }
   const IcpState& h = *ctx->h_state;
+  if (h.guard) {  // an index guard tripped: corrupted queue / neighbour state
+    set_last_error(hipErrorIllegalAddress, "ICP index guard", __FILE__, h.guard);
+    return RST_E_HIP;
+  }
   if (pd.p2plane && h.fail) {
     if (iters_run) *iters_run = h.iter;
     if (pd.pyramid) {  // the pose level 0 started from (the coarser levels' result)

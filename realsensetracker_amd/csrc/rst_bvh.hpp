@@ -88,6 +88,18 @@ struct BvhView {
   int32_t pad;
 };
 
+// A target prepared from a depth frame keeps its pixel grid: map[p] = the
+// sorted position of grid pixel p's point (-1: no valid depth), p = vl * w +
+// ul on the level grid (pixel (s ul, s vl) of the full image, intrinsics of
+// the full image).  Projecting a query through it gives a candidate near its
+// nearest neighbour -- a warm start for the exact searches, never a result.
+struct PixView {
+  const int32_t* __restrict__ map;  // null: the target has no pixel grid
+  float fx, fy, cx, cy;
+  int32_t w, h, s;
+  int32_t pad;
+};
+
 // ---- Morton order ------------------------------------------------------------------
 RST_HD uint32_t spread10(uint32_t v) {
   v &= 0x3ffu;

@@ -61,6 +61,124 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// ---- transpose-reduce: NV sums over a wavefront in ~NV cross-lane moves ----
+// A plain per-value butterfly costs 6 lane exchanges per value (6 NV
+// ds_bpermute pairs for doubles).  Here every exchange step also halves the
+// number of values a lane carries: at the step pairing lanes l and l ^ m,
+// the lane without bit m keeps the lower half of its values and adds its
+// partner's copy of that half, the other lane the upper half.  After
+// log2(NV) such steps a lane carries one value -- the partial sum of value
+// (lane >> (6 - log2 NV)) -- and the remaining steps reduce it plainly.
+// Exchanges: v_permlane32_swap (lanes 32-63 of one register <-> lanes 0-31
+// of another) and v_permlane16_swap (the same between adjacent 16-lane
+// rows) pair whole registers, so each half-step is one swap per dword;
+// inside a row DPP row_mirror (l <-> 15 - l), row_half_mirror (l <-> 7 - l)
+// and quad_perm do the rest -- no LDS traffic.  Bitwise deterministic.
+__device__ __forceinline__ void swap_halves32(double& a, double& b) {
+  uint2 ua = __builtin_bit_cast(uint2, a), ub = __builtin_bit_cast(uint2, b);
+  const auto rx = __builtin_amdgcn_permlane32_swap(ua.x, ub.x, false, false);
+  const auto ry = __builtin_amdgcn_permlane32_swap(ua.y, ub.y, false, false);
+  a = __builtin_bit_cast(double, make_uint2(rx[0], ry[0]));
+  b = __builtin_bit_cast(double, make_uint2(rx[1], ry[1]));
+}
+__device__ __forceinline__ void swap_rows16(double& a, double& b) {
+  uint2 ua = __builtin_bit_cast(uint2, a), ub = __builtin_bit_cast(uint2, b);
+  const auto rx = __builtin_amdgcn_permlane16_swap(ua.x, ub.x, false, false);
+  const auto ry = __builtin_amdgcn_permlane16_swap(ua.y, ub.y, false, false);
+  a = __builtin_bit_cast(double, make_uint2(rx[0], ry[0]));
+  b = __builtin_bit_cast(double, make_uint2(rx[1], ry[1]));
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double x) {
+  const uint2 u = __builtin_bit_cast(uint2, x);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)u.x, CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)u.y, CTRL, 0xf, 0xf, false);
+  return __builtin_bit_cast(double, make_uint2((unsigned)lo, (unsigned)hi));
+}
+constexpr int kDppRowMirror = 0x140, kDppRowHalfMirror = 0x141;
+constexpr int kDppXor2 = 0x4E, kDppXor1 = 0xB1;  // quad_perm [2,3,0,1] / [1,0,3,2]
+
+// One step of the transpose-reduce: `cnt` values in v[0..cnt) -> cnt / 2
+// (or, at cnt == 1, a plain pairwise sum).  STEP 0..5 pairs lanes across
+// bit 5 .. bit 0 of the lane id.
+template <int STEP, int N>
+__device__ __forceinline__ void transpose_step(double (&v)[N], int cnt, int lane) {
+  const int h = cnt > 1 ? cnt / 2 : 1;
+  if (cnt == 1) {
+    double a = v[0];
+    if constexpr (STEP == 0) {
+      double b = a;
+      swap_halves32(a, b);
+      v[0] = a + b;
+    } else if constexpr (STEP == 1) {
+      double b = a;
+      swap_rows16(a, b);
+      v[0] = a + b;
+    } else if constexpr (STEP == 2) {
+      v[0] = a + dpp_f64<kDppRowMirror>(a);
+    } else if constexpr (STEP == 3) {
+      v[0] = a + dpp_f64<kDppRowHalfMirror>(a);
+    } else if constexpr (STEP == 4) {
+      v[0] = a + dpp_f64<kDppXor2>(a);
+    } else {
+      v[0] = a + dpp_f64<kDppXor1>(a);
+    }
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < N / 2; ++j) {
+    if (j >= h) break;
+    if constexpr (STEP == 0) {
+      swap_halves32(v[j], v[j + h]);
+      v[j] = v[j] + v[j + h];
+    } else if constexpr (STEP == 1) {
+      swap_rows16(v[j], v[j + h]);
+      v[j] = v[j] + v[j + h];
+    } else {
+      const bool up = (lane >> (5 - STEP)) & 1;  // keeps the upper half
+      const double send = up ? v[j] : v[j + h];
+      double recv;
+      if constexpr (STEP == 2)
+        recv = dpp_f64<kDppRowMirror>(send);
+      else if constexpr (STEP == 3)
+        recv = dpp_f64<kDppRowHalfMirror>(send);
+      else if constexpr (STEP == 4)
+        recv = dpp_f64<kDppXor2>(send);
+      else
+        recv = dpp_f64<kDppXor1>(send);
+      v[j] = (up ? v[j + h] : v[j]) + recv;
+    }
+  }
+}
+
+constexpr int pow2_ceil(int x) { return x <= 1 ? 1 : 2 * pow2_ceil((x + 1) / 2); }
+constexpr int log2_exact(int x) { return x <= 1 ? 0 : 1 + log2_exact(x / 2); }
+
+// Wave sums of NV doubles: returns the total of value (lane >> (6 - k)),
+// k = log2(pow2_ceil(NV)), held by every lane of that group (the caller
+// writes it from lanes with (lane & ((1 << (6 - k)) - 1)) == 0).
+template <int NV>
+__device__ __forceinline__ double wave_sum_transpose(const double (&v)[NV], int lane) {
+  constexpr int P = pow2_ceil(NV);
+  static_assert(P <= kWave, "at most 64 values");
+  double w[P];
+#pragma unroll
+  for (int k = 0; k < P; ++k) w[k] = k < NV ? v[k] : 0.0;
+  int cnt = P;
+  transpose_step<0>(w, cnt, lane);
+  cnt = cnt > 1 ? cnt / 2 : 1;
+  transpose_step<1>(w, cnt, lane);
+  cnt = cnt > 1 ? cnt / 2 : 1;
+  transpose_step<2>(w, cnt, lane);
+  cnt = cnt > 1 ? cnt / 2 : 1;
+  transpose_step<3>(w, cnt, lane);
+  cnt = cnt > 1 ? cnt / 2 : 1;
+  transpose_step<4>(w, cnt, lane);
+  cnt = cnt > 1 ? cnt / 2 : 1;
+  transpose_step<5>(w, cnt, lane);
+  return w[0];
+}
+
 // Reduce NV doubles per thread over a block of BS threads; lane results land
 // in out[] on thread 0..NV-1 (out must be __shared__ double[BS/64][NV]).
 template <int NV, int BS>
@@ -69,12 +187,10 @@ __device__ __forceinline__ void block_sum_to_slab(double (&v)[NV],
                                                   double* slab_row) {
   const int lane = threadIdx.x & (kWave - 1);
   const int wid = threadIdx.x / kWave;
-#pragma unroll
-  for (int k = 0; k < NV; ++k) v[k] = wave_sum(v[k]);
-  if (lane == 0) {
-#pragma unroll
-    for (int k = 0; k < NV; ++k) lds[wid * NV + k] = v[k];
-  }
+  constexpr int K = log2_exact(pow2_ceil(NV));
+  const double t = wave_sum_transpose<NV>(v, lane);
+  const int idx = lane >> (6 - K);
+  if ((lane & ((1 << (6 - K)) - 1)) == 0 && idx < NV) lds[wid * NV + idx] = t;
   __syncthreads();
   if (threadIdx.x < NV) {
     double s = 0.0;
@@ -97,12 +213,10 @@ __device__ __forceinline__ void block_sum_to_slab_fold(double (&v)[NV], double* 
   double ex = 0.0;  // loads issued before the wave sums (latency overlap)
   if (threadIdx.x < NV)
     for (int r = blk; r < rows; r += step) ex += other[(int64_t)r * stride + threadIdx.x];
-#pragma unroll
-  for (int k = 0; k < NV; ++k) v[k] = wave_sum(v[k]);
-  if (lane == 0) {
-#pragma unroll
-    for (int k = 0; k < NV; ++k) lds[wid * NV + k] = v[k];
-  }
+  constexpr int K = log2_exact(pow2_ceil(NV));
+  const double t = wave_sum_transpose<NV>(v, lane);
+  const int idx = lane >> (6 - K);
+  if ((lane & ((1 << (6 - K)) - 1)) == 0 && idx < NV) lds[wid * NV + idx] = t;
   __syncthreads();
   if (threadIdx.x < NV) {
     double s = 0.0;

@@ -68,6 +68,8 @@ struct IcpCore {
   int32_t fb_e;      // fallback-queue entries of the current iteration
   float seq[4];      // RST_SUM_REF: this iteration's sequential fp32 sums
                      // (sum dst[nbr_i] xyz, cost), align_icp.cpp:113,120
+  int32_t guard;     // bit mask of index guards that tripped (0: none; diagnostics)
+  int32_t pad1;
 };
 
 struct IcpState : IcpCore {
@@ -110,6 +112,7 @@ struct rst_ctx {
   int timing_stride = 1;              // time every timing_stride-th iteration
   std::vector<hipEvent_t> ev;
   float last_kernel_ms = 0.f;
+  float last_iter_ms[3] = {0.f, 0.f, 0.f};  // k_icp_nn | k_icp_fb | the rest of the iteration
   int32_t last_kernel_launches = 0;
   // hipGraph replay of the ICP iteration loop (rst_ctx_enable_graphs):
   // (pyramid level, iterations, P2PLANE, RST_SUM_REF) -> executable graph,
@@ -152,6 +155,7 @@ struct rst_target {
   float4* adj3 = nullptr;       // ... and over the nodes of 64 leaves
   float* reach3 = nullptr;
   float4* nrm = nullptr;        // [m] normals in sorted order (optional)
+  rst::PixView pix = {};        // pixel grid -> sorted position (frames from depth only)
   float bbox[6] = {0, 0, 0, 0, 0, 0};
   int32_t pos0 = 0;             // sorted position of original point 0
   bool has_bvh = false;
@@ -212,7 +216,8 @@ int kabsch_device(rst_ctx* ctx, const double cov[9], const float smean[3],
 // unprojection (unproject.hip)
 int unproject_device(rst_ctx* ctx, const uint16_t* d_depth,
                      const rst_intrinsics* K, int keep_invalid,
-                     float* d_xyz, int64_t* n_out, int stride = 1);
+                     float* d_xyz, int64_t* n_out, int stride = 1,
+                     int32_t* d_pixmap = nullptr);
 
 // RemoveNans / DownsampleVoxel (voxel.hip); synchronous (n_out is host)
 int remove_nans_device(rst_ctx* ctx, const float* d_xyz, int64_t n, float* d_out,

@@ -755,7 +755,10 @@ RST_HD void scan_range_wide<Best2>(const BvhView& bv, int b, int n, float qx, fl
 // is scanned and the best point found becomes the new start, up to
 // kWalkSteps times.  Walking only lowers the bound; exactness still comes
 // from the coverage test of the final leaf.
-constexpr int kWalkSteps = 1;
+#ifndef RST_WALK_STEPS
+#define RST_WALK_STEPS 1
+#endif
+constexpr int kWalkSteps = RST_WALK_STEPS;
 
 // sqrt for the coverage / stop tests: the hardware v_sqrt_f32 (about 1 ulp)
 // on the device; every use carries the 1.00001 / 0.99999 margins of
@@ -901,6 +904,134 @@ RST_HD float cert_bound(const Best2& r, float rc) {
   const float r2 = r.d[1] < FLT_MAX ? margin_sqrt(r.d[1]) * 0.99999f : FLT_MAX;
   const float g = fminf(r2, rc);
   return g > 0.f ? g : 0.f;
+}
+
+// ---- LDS-staged target tiles (the cold iterations of an ICP pair) -------------------
+// A wavefront's 64 Morton-consecutive queries cover one compact patch.  The
+// target points inside the patch's bounding box grown by a margin are
+// staged in LDS once (a top-down BVH range query, 64 nodes per round, then
+// the listed leaves' points, 16 lanes per leaf), and every lane scans the
+// whole tile from LDS (broadcast reads: all lanes read the same point).
+// For a query q inside the box the tile holds every target point within
+// Mq = dist(q, outside of the grown box); so its tile minimum is its exact
+// nearest neighbour when that lies closer than Mq, and min(second, Mq)
+// bounds every other point -- the certificate.
+constexpr int kTileStack = 384;  // node ids
+constexpr int kTileLeaves = 64;  // staged leaves
+constexpr int kTilePts = 768;    // staged points
+struct TileScratch {             // per-wave LDS (~16 KB)
+  float4 pts[kTilePts];          // x, y, z, original index bits
+  int pos[kTilePts];             // sorted position
+  int stack[kTileStack];
+  int leaves[kTileLeaves];
+};
+
+__device__ __forceinline__ bool box_meets(const float4& lo, const float4& hi, float lx, float ly,
+                                          float lz, float hx, float hy, float hz) {
+  return lo.x <= hx && hi.x >= lx && lo.y <= hy && hi.y >= ly && lo.z <= hz && hi.z >= lz;
+}
+
+// Stage the target points inside [l, h] (per-axis bounds) in ts; returns
+// their count, or -1 when they do not fit (the caller falls back; -2: an
+// index guard tripped, never expected).  The whole wave must call it
+// (converged).
+__device__ __forceinline__ int tile_stage(const BvhView& bv, float lx, float ly, float lz, float hx,
+                                          float hy, float hz, TileScratch& ts) {
+  const int lane = __lane_id();
+  const int nl = bv.nleaves;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  if (lane == 0) ts.stack[0] = 1;
+  int sp = 1, ns = 0;
+  bool over = false;
+  wave_sync();
+  while (sp > 0) {
+    const int k = min(kWave, sp);
+    int node = 0;
+    if (lane < k) node = ts.stack[sp - 1 - lane];
+    sp -= k;
+    wave_sync();
+    bool pass = false;
+    if (__ballot(lane < k && (node < 1 || node >= 2 * nl)) != 0) return -2;  // index guard
+    if (lane < k) {
+      const float4 lo = bv.nodes[2 * node], hi = bv.nodes[2 * node + 1];
+      pass = box_meets(lo, hi, lx, ly, lz, hx, hy, hz);
+    }
+    const bool isleaf = node >= nl;
+    const uint64_t im = __ballot(pass && !isleaf), lm = __ballot(pass && isleaf);
+    const int ni = __popcll(im), nlv = __popcll(lm);
+    if (sp + 2 * ni > kTileStack || ns + nlv > kTileLeaves) {
+      over = true;
+      break;
+    }
+    if (pass && !isleaf) {
+      const int rk = __popcll(im & lt);
+      ts.stack[sp + 2 * rk] = 2 * node;
+      ts.stack[sp + 2 * rk + 1] = 2 * node + 1;
+    }
+    if (pass && isleaf) ts.leaves[ns + __popcll(lm & lt)] = node - nl;
+    sp += 2 * ni;
+    ns += nlv;
+    wave_sync();
+  }
+  if (over) return -1;
+  // leaf point ranges -> LDS offsets (exclusive scan over <= 64 leaves)
+  int b = 0, c = 0;
+  if (lane < ns) {
+    const int L = ts.leaves[lane];
+    b = leaf_begin(bv, L);
+    c = leaf_begin(bv, L + 1) - b;
+  }
+  int inc = c;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const int y = __shfl_up(inc, o, kWave);
+    if (lane >= o) inc += y;
+  }
+  const int total = __shfl(inc, kWave - 1, kWave);
+  if (total > kTilePts) return -1;
+  const int off = inc - c;
+  const int g = lane >> 4, o = lane & 15;
+  for (int k0 = 0; k0 < ns; k0 += 4) {  // one leaf per 16 lanes
+    const int kk = k0 + g;
+    const int lb = __shfl(b, kk & 63, kWave), lc = __shfl(c, kk & 63, kWave);
+    const int lo = __shfl(off, kk & 63, kWave);
+    if (kk < ns && o < lc) {
+      ts.pts[lo + o] = bv.pts[lb + o];
+      ts.pos[lo + o] = lb + o;
+    }
+  }
+  wave_sync();
+  return total;
+}
+
+// The two nearest of (qx, qy, qz) among the ns staged points
+// (lexicographic (d2, original index), as every search here).
+__device__ __forceinline__ void tile_scan(const TileScratch& ts, int ns, float qx, float qy,
+                                          float qz, Best2& r) {
+  uint64_t k0 = ((uint64_t)(uint32_t)f2i(r.d[0]) << 32) | (uint32_t)r.id[0];
+  uint64_t k1 = ((uint64_t)(uint32_t)f2i(r.d[1]) << 32) | (uint32_t)r.id[1];
+  int j0 = -1, j1 = -1;
+  for (int j = 0; j < ns; ++j) {
+    const float4 p = ts.pts[j];
+    const float d2 = d2_ref(qx, qy, qz, p.x, p.y, p.z);
+    const uint64_t key = ((uint64_t)(uint32_t)f2i(d2) << 32) | (uint32_t)f2i(p.w);
+    const bool in = (key != k0) & (key < k1);
+    const bool first = in & (key < k0);
+    k1 = first ? k0 : (in ? key : k1);
+    j1 = first ? j0 : (in ? j : j1);
+    k0 = first ? key : k0;
+    j0 = first ? j : j0;
+  }
+  if (j0 >= 0) {
+    r.d[0] = i2f((int)(uint32_t)(k0 >> 32));
+    r.id[0] = (int)(uint32_t)k0;
+    r.pos[0] = ts.pos[j0];
+  }
+  if (j1 >= 0) {
+    r.d[1] = i2f((int)(uint32_t)(k1 >> 32));
+    r.id[1] = (int)(uint32_t)k1;
+    r.pos[1] = ts.pos[j1];
+  }
 }
 
 // ---- the ICP loop's candidate lists ----------------------------------------------------

@@ -69,7 +69,8 @@ __global__ __launch_bounds__(kBS) void k_count(const uint16_t* __restrict__ dept
 __global__ __launch_bounds__(kBS) void k_write(const uint16_t* __restrict__ depth, int64_t npx,
                                                Cam c, int keep_invalid,
                                                const uint32_t* __restrict__ offsets,
-                                               float* __restrict__ xyz) {
+                                               float* __restrict__ xyz,
+                                               int32_t* __restrict__ pixmap) {
   __shared__ uint32_t wtot[kBS / kWave];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -103,10 +104,21 @@ __global__ __launch_bounds__(kBS) void k_write(const uint16_t* __restrict__ dept
       xyz[3 * o + 1] = z * y;
       xyz[3 * o + 2] = z;
     }
+    if (pixmap && inb) pixmap[p] = ok ? (int32_t)(off + __popcll(bal & lt)) : -1;
     uint32_t tot = 0;
     for (int k = 0; k < kBS / kWave; ++k) tot += wtot[k];
     run += tot;
     __syncthreads();
+  }
+}
+
+// pixel map: original point index -> sorted position of the built target
+__global__ __launch_bounds__(kBS) void k_pixmap_sorted(int32_t* __restrict__ map, int64_t npx,
+                                                       const int32_t* __restrict__ inv) {
+  const int64_t p = (int64_t)blockIdx.x * kBS + threadIdx.x;
+  if (p < npx) {
+    const int32_t o = map[p];
+    map[p] = o >= 0 ? inv[o] : -1;
   }
 }
 
@@ -140,7 +152,8 @@ __global__ __launch_bounds__(1024) void k_scan_small(uint32_t* __restrict__ a, i
 }  // namespace
 
 int unproject_device(rst_ctx* ctx, const uint16_t* d_depth, const rst_intrinsics* K,
-                     int keep_invalid, float* d_xyz, int64_t* n_out, int stride) {
+                     int keep_invalid, float* d_xyz, int64_t* n_out, int stride,
+                     int32_t* d_pixmap) {
   if (!ctx || !d_depth || !K || !d_xyz || !n_out) return RST_E_ARG;
   if (K->width <= 0 || K->height <= 0 || !(K->fx != 0.f) || !(K->fy != 0.f)) return RST_E_ARG;
   if (stride < 1 || stride > 1024) return RST_E_ARG;
@@ -151,7 +164,7 @@ int unproject_device(rst_ctx* ctx, const uint16_t* d_depth, const rst_intrinsics
   const int nb = (int)((npx + kTile - 1) / kTile);
   hipStream_t st = ctx->stream;
   if (keep_invalid) {
-    k_write<<<nb, kBS, 0, st>>>(d_depth, npx, c, 1, nullptr, d_xyz);
+    k_write<<<nb, kBS, 0, st>>>(d_depth, npx, c, 1, nullptr, d_xyz, nullptr);
     RST_HIP(hipGetLastError());
     *n_out = npx;
     return RST_OK;
@@ -162,7 +175,7 @@ int unproject_device(rst_ctx* ctx, const uint16_t* d_depth, const rst_intrinsics
   uint32_t* total = counts + nb + 16;
   k_count<<<nb, kBS, 0, st>>>(d_depth, npx, c, counts);
   k_scan_small<<<1, 1024, 0, st>>>(counts, nb, total);
-  k_write<<<nb, kBS, 0, st>>>(d_depth, npx, c, 0, counts, d_xyz);
+  k_write<<<nb, kBS, 0, st>>>(d_depth, npx, c, 0, counts, d_xyz, d_pixmap);
   RST_HIP(hipGetLastError());
   uint32_t h = 0;
   RST_HIP(hipMemcpyAsync(&h, total, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
@@ -231,19 +244,41 @@ namespace rst {
 static int frame_prepare(rst_ctx* ctx, const uint16_t* d_depth, const rst_intrinsics* K,
                          int stride, int normals_k, rst_target** out) {
   const int64_t npx = (int64_t)K->width * K->height;
+  if (stride < 1) return RST_E_ARG;
+  const int wl = (K->width + stride - 1) / stride, hl = (K->height + stride - 1) / stride;
+  const int64_t npl = (int64_t)wl * hl;
   float* dx = nullptr;
-  size_t dxc = 0;
+  size_t dxc = 0, pmc = 0;
+  int32_t* pm = nullptr;  // the level's pixel map (the target keeps it)
   RST_CHECK(ctx_alloc(ctx, sizeof(float) * 3 * std::max<int64_t>(npx, 1), (void**)&dx, &dxc));
+  if (ctx_alloc(ctx, sizeof(int32_t) * std::max<int64_t>(npl, 1), (void**)&pm, &pmc) < 0) {
+    ctx_release(ctx, dx, dxc);
+    return RST_E_NOMEM;
+  }
   int64_t n = 0;
-  int s = unproject_device(ctx, d_depth, K, 0, dx, &n, stride);
+  int s = unproject_device(ctx, d_depth, K, 0, dx, &n, stride, pm);
   rst_target* t = nullptr;
   if (s >= 0) s = target_build_device(ctx, dx, n, true, &t);
+  if (s >= 0) {
+    k_pixmap_sorted<<<(int)((npl + kBS - 1) / kBS), kBS, 0, ctx->stream>>>(pm, npl, t->inv);
+    t->allocs.emplace_back(pm, pmc);  // freed with the target
+    pm = nullptr;
+    t->pix.map = t->allocs.back().first ? (const int32_t*)t->allocs.back().first : nullptr;
+    t->pix.fx = K->fx;
+    t->pix.fy = K->fy;
+    t->pix.cx = K->cx;
+    t->pix.cy = K->cy;
+    t->pix.w = wl;
+    t->pix.h = hl;
+    t->pix.s = stride;
+  }
   if (s >= 0 && normals_k > 0) {
     const float vp[3] = {0.f, 0.f, 0.f};
     s = compute_normals(ctx, t, normals_k, vp);
   }
   hipStreamSynchronize(ctx->stream);
   ctx_release(ctx, dx, dxc);
+  if (pm) ctx_release(ctx, pm, pmc);
   if (s < 0) {
     if (t) rst_target_free(t);
     return s;

@@ -1,21 +1,24 @@
-"""HBM traffic per launch of k_icp_nn<P2PointAcc> from two rocprofv3 --pmc
+"""HBM traffic per ICP iteration of the NN pass -- k_icp_nn<P2PointAcc> and
+k_icp_fb<P2PointAcc>, per launch each and summed -- from two rocprofv3 --pmc
 passes (FETCH_SIZE, WRITE_SIZE; counter_collection.csv each), corrected as
 /opt/skills/guides/MI355X_MICROARCH.md "HBM" prescribes: FETCH_SIZE (KiB) x 2
-on gfx950, WRITE_SIZE (KiB) as is.  Writes the JSON bench.py reads.
+on gfx950, WRITE_SIZE (KiB) as is.  Writes the JSON bench.py reads, stamped
+with the library's source hash (lib/BUILD_INFO.json): bench.py reports the
+traffic only while it matches the library it runs.
 
   python scripts/pmc_traffic.py OUT.json FETCH.csv WRITE.csv"""
 import csv
 import json
 import sys
 
-KERNEL = "k_icp_nn<rst::(anonymous namespace)::P2PointAcc>"
+KERNELS = ("k_icp_nn<", "k_icp_fb<")
 
 
-def per_dispatch(path, counter):
+def per_dispatch(path, counter, kernel):
     vals = {}
     for r in csv.DictReader(open(path)):
         name = r["Kernel_Name"]
-        if r["Counter_Name"] != counter or "k_icp_nn<" not in name or "P2PointAcc" not in name:
+        if r["Counter_Name"] != counter or kernel not in name or "P2PointAcc" not in name:
             continue
         # one row per (dispatch, counter); sum any per-dimension rows
         key = r.get("Dispatch_Id") or r.get("Correlation_Id") or len(vals)
@@ -26,17 +29,26 @@ def per_dispatch(path, counter):
 
 def main():
     out, fpath, wpath = sys.argv[1:4]
-    f = per_dispatch(fpath, "FETCH_SIZE")
-    w = per_dispatch(wpath, "WRITE_SIZE")
-    if not f or not w:
-        raise SystemExit("no k_icp_nn<P2PointAcc> rows")
-    fm = sum(f) / len(f) * 1024.0 * 2.0  # KiB -> B, gfx950 half-count correction
-    wm = sum(w) / len(w) * 1024.0
-    d = {"kernel": KERNEL, "dispatches": [len(f), len(w)],
-         "fetch_bytes_per_launch_corrected": fm, "write_bytes_per_launch": wm,
-         "k_icp_nn_bytes_per_launch": fm + wm,
-         "fetch_size_kib_median_raw": f[len(f) // 2],
-         "note": "FETCH_SIZE x2 (gfx950), WRITE_SIZE as is; rocprofv3 --pmc, separate passes"}
+    d = {"kernels": {}, "note": "FETCH_SIZE x2 (gfx950), WRITE_SIZE as is; rocprofv3 --pmc, "
+                                "separate passes; per launch, P2PointAcc instances"}
+    tot = 0.0
+    for k in KERNELS:
+        f = per_dispatch(fpath, "FETCH_SIZE", k)
+        w = per_dispatch(wpath, "WRITE_SIZE", k)
+        if not f or not w:
+            raise SystemExit(f"no {k}P2PointAcc> rows")
+        fm = sum(f) / len(f) * 1024.0 * 2.0  # KiB -> B, gfx950 half-count correction
+        wm = sum(w) / len(w) * 1024.0
+        d["kernels"][k.rstrip("<")] = {"dispatches": [len(f), len(w)],
+                                       "fetch_bytes_corrected": fm, "write_bytes": wm,
+                                       "bytes_per_launch": fm + wm,
+                                       "fetch_size_kib_median_raw": f[len(f) // 2]}
+        tot += fm + wm
+    d["nn_pass_bytes_per_iteration"] = tot
+    try:
+        d["source_hash"] = json.load(open("realsensetracker_amd/lib/BUILD_INFO.json"))["source_hash"]
+    except (OSError, KeyError, ValueError):
+        d["source_hash"] = None
     json.dump(d, open(out, "w"), indent=1)
     print(json.dumps(d))
 
