@@ -433,24 +433,32 @@ def main():
         timing(0, actx[:1])
 
     # ---- point-to-plane mode (extra fields) ---------------------------------------
-    pl = None
-    if not a.no_p2plane:
-        run(a.warmup, opts_pl, 16, None)
+    def p2plane_leg(normals_k: int) -> dict:
+        run(a.warmup, opts_pl, normals_k, None)
         timing(8)
         sp = new_stats()
         barrier()
         sync_all()
         t1 = time.perf_counter()
-        run(a.steps, opts_pl, 16, sp)
+        run(a.steps, opts_pl, normals_k, sp)
         sync_all()
         barrier()
         timing(0)
         dtp = max_over_ranks(time.perf_counter() - t1)
-        pl = {"iterations_per_s": sum_over_ranks(sp["iters"]) / dtp,
-              "frames_per_s": sum_over_ranks(a.steps) / dtp,
-              "mean_iterations_per_pair": sp["iters"] / max(1, a.steps),
-              "ms_per_pair": 1000.0 * dtp / a.steps,
-              "k_p2plane_avg_us": 1000.0 * sp["kernel_ms"] / max(1, sp["launches"])}
+        return {"iterations_per_s": sum_over_ranks(sp["iters"]) / dtp,
+                "frames_per_s": sum_over_ranks(a.steps) / dtp,
+                "mean_iterations_per_pair": sp["iters"] / max(1, a.steps),
+                "ms_per_pair": 1000.0 * dtp / a.steps,
+                "k_p2plane_avg_us": 1000.0 * sp["kernel_ms"] / max(1, sp["launches"]),
+                "normals": ("image-grid PCA, %dx%d window (rst_target_compute_grid_normals)"
+                            % (1 - 2 * normals_k, 1 - 2 * normals_k)) if normals_k < 0 else
+                           "kNN-%d PCA (ComputeNormals, point_cloud_utils.cpp:176-216)" % normals_k}
+
+    pl = None
+    if not a.no_p2plane:
+        # perf mode: image-grid normals; the reference's kNN-16 normals beside it
+        pl = p2plane_leg(-2)
+        pl["knn16_normals"] = p2plane_leg(16)
 
     # ---- reference-rounding mode (RST_SUM_REF; extra field, not value) ----------
     refs = None

@@ -149,6 +149,14 @@ int64_t rst_target_size(const rst_target* tgt);
  * point_cloud_utils.cpp:176-216), stored in the handle for P2PLANE. */
 int rst_target_compute_normals(rst_ctx* ctx, rst_target* tgt, int k,
                                const float viewpoint[3]);
+/* Image-grid normals (point-to-plane perf mode; no reference counterpart):
+ * for a target prepared from a depth frame (rst_frame_prepare_device / the
+ * pyramid), the PCA normal of each point's (2 radius + 1)^2 pixel window
+ * (radius 1 or 2; window points farther than 5 pixel pitches excluded),
+ * oriented as OrientNormals.  The kNN-PCA normals above stay the reference
+ * semantics.  RST_E_STATE for a target without a pixel grid. */
+int rst_target_compute_grid_normals(rst_ctx* ctx, rst_target* tgt, int radius,
+                                    const float viewpoint[3]);
 /* Copy normals out in the target's original point order (host m*3). */
 int rst_target_get_normals(rst_ctx* ctx, const rst_target* tgt,
                            float* normals);
@@ -260,7 +268,9 @@ int rst_unproject_device(rst_ctx* ctx, const uint16_t* d_depth,
                          const rst_intrinsics* K, int keep_invalid,
                          float* d_xyz_out, int64_t* n_out);
 /* Fused frame preparation: depth (device) -> points -> target handle
- * (+ normals when normals_k > 0).  One call per incoming frame. */
+ * (+ normals: normals_k > 0 kNN-PCA with k = normals_k, normals_k = -1 / -2
+ * image-grid normals of radius 1 / 2, 0 none; viewpoint = the camera).
+ * One call per incoming frame. */
 int rst_frame_prepare_device(rst_ctx* ctx, const uint16_t* d_depth,
                              const rst_intrinsics* K, int normals_k,
                              rst_target** out);

@@ -43,6 +43,13 @@ int rst_debug_query_nn_fallback(rst_ctx* ctx, const rst_target* tgt, const float
  * the rounding of `dst_mean += dst.GetPoint(j)` (align_icp.cpp:120). */
 int rst_debug_seq_sum4(rst_ctx* ctx, const float* xyzw, int64_t n, float out[4]);
 
+/* The target's leaf table: lstart[0 .. nleaves] (leaf L holds sorted
+ * positions [lstart[L], lstart[L+1])) copied to the host when cap >=
+ * nleaves + 1, and pleaf[0 .. m) (the leaf of each sorted position) when
+ * pleaf is not NULL; *nleaves receives the leaf count either way. */
+int rst_debug_target_leaves(rst_ctx* ctx, const rst_target* tgt, int32_t* lstart, int32_t cap,
+                            int32_t* pleaf, int32_t* nleaves);
+
 #ifdef __cplusplus
 }
 #endif

@@ -61,6 +61,9 @@ def lib():
         L.orc_compute_normals.argtypes = [_f, C.c_int64, P, C.c_int, _f, _f]
         L.orc_unproject.restype = C.c_int64
         L.orc_unproject_strided.restype = C.c_int64
+        L.orc_grid_normals.restype = C.c_int64
+        L.orc_grid_normals.argtypes = [_u16, C.c_int, C.c_int, C.c_int, _f, C.c_float, C.c_int,
+                                       _f, _f]
         L.orc_remove_nans.argtypes = [_f, C.c_int64, _f]
         L.orc_remove_nans.restype = C.c_int64
         L.orc_downsample_voxel.argtypes = [_f, C.c_int64, C.c_float, _f]
@@ -249,6 +252,19 @@ def unproject(depth, K4, depth_scale=0.001, keep_invalid=False, stride=1):
     n = lib().orc_unproject_strided(d.ctypes.data_as(_u16), w, h, int(stride),
                                     _fp(np.asarray(K4, np.float32)), C.c_float(depth_scale),
                                     int(keep_invalid), _fp(out))
+    return out[:n].copy()
+
+
+def grid_normals(depth, K4, radius=2, stride=1, viewpoint=(0, 0, 0), depth_scale=0.001):
+    """Image-grid normals of the frame's level `stride` (k_grid_normals'
+    restatement), in unproject order."""
+    d = np.ascontiguousarray(depth, np.uint16)
+    h, w = d.shape
+    out = np.zeros((((h + stride - 1) // stride) * ((w + stride - 1) // stride), 3), np.float32)
+    n = lib().orc_grid_normals(d.ctypes.data_as(_u16), w, h, int(stride),
+                               _fp(np.asarray(K4, np.float32)), C.c_float(depth_scale),
+                               int(radius), _fp(np.asarray(viewpoint, np.float32)), _fp(out))
+    assert n >= 0
     return out[:n].copy()
 
 

@@ -929,6 +929,88 @@ void orc_compute_normals(const float* xyz, int64_t m, const orc_kdtree* tree,
   }
 }
 
+/* Image-grid normals (the build's point-to-plane perf mode; no reference
+ * counterpart -- restates k_grid_normals, query.hip): per valid pixel of
+ * pyramid level s, the valid points of its (2r+1)^2 level-pixel window
+ * within 5 r s z / fx of it (window order: rows, then columns), fp32
+ * centroid and covariance as ComputeNormals (point_cloud_utils.cpp:186-198),
+ * smallest eigenvector, OrientNormals (:206-216); < 3 points: the unit ray
+ * towards the viewpoint.  Output in unproject order (valid pixels,
+ * row-major). */
+int64_t orc_grid_normals(const uint16_t* depth, int w, int h, int s, const float K[4],
+                         float depth_scale, int r, const float viewpoint[3], float* normals) {
+  const int wl = (w + s - 1) / s, hl = (h + s - 1) / s;
+  float* g = (float*)malloc(sizeof(float) * 3 * (size_t)wl * hl);
+  if (!g) return -1;
+  orc_unproject_strided(depth, w, h, s, K, depth_scale, 1, g);
+  int64_t k = 0;
+  for (int v = 0; v < hl; ++v)
+    for (int u = 0; u < wl; ++u) {
+      const float* p = g + 3 * ((int64_t)v * wl + u);
+      if (depth[(int64_t)v * s * w + (int64_t)u * s] == 0) continue;
+      const float reach = 5.0f * (float)r * (float)s * p[2] / fabsf(K[0]);
+      const float reach2 = reach * reach;
+      float c[3] = {0, 0, 0}, cov[6] = {0, 0, 0, 0, 0, 0};
+      int cnt = 0;
+      for (int pass = 0; pass < 2; ++pass) {
+        for (int dv = -r; dv <= r; ++dv)
+          for (int du = -r; du <= r; ++du) {
+            const int uu = u + du, vv = v + dv;
+            if (uu < 0 || vv < 0 || uu >= wl || vv >= hl) continue;
+            if (depth[(int64_t)vv * s * w + (int64_t)uu * s] == 0) continue;
+            const float* q = g + 3 * ((int64_t)vv * wl + uu);
+            const float ex = q[0] - p[0], ey = q[1] - p[1], ez = q[2] - p[2];
+            if ((ex * ex + ey * ey) + ez * ez > reach2) continue;
+            if (pass == 0) {
+              c[0] += q[0];
+              c[1] += q[1];
+              c[2] += q[2];
+              ++cnt;
+            } else {
+              const float dx = q[0] - c[0], dy = q[1] - c[1], dz = q[2] - c[2];
+              cov[0] += dx * dx; cov[1] += dx * dy; cov[2] += dx * dz;
+              cov[3] += dy * dy; cov[4] += dy * dz; cov[5] += dz * dz;
+            }
+          }
+        if (pass == 0) {
+          if (cnt < 3) break;
+          const float kf = (float)cnt;
+          for (int d = 0; d < 3; ++d) c[d] = c[d] / kf;
+        }
+      }
+      float n[3];
+      if (cnt >= 3) {
+        const double cd[9] = {cov[0], cov[1], cov[2], cov[1], cov[3], cov[4], cov[2], cov[4], cov[5]};
+        double nv[3];
+        sym3_min_eigvec(cd, nv);
+        n[0] = (float)nv[0];
+        n[1] = (float)nv[1];
+        n[2] = (float)nv[2];
+      } else {
+        n[0] = p[0] - viewpoint[0];
+        n[1] = p[1] - viewpoint[1];
+        n[2] = p[2] - viewpoint[2];
+        const float l = sqrtf((n[0] * n[0] + n[1] * n[1]) + n[2] * n[2]);
+        const float il = l > 0.f ? 1.0f / l : 0.f;
+        n[0] *= il;
+        n[1] *= il;
+        n[2] = l > 0.f ? n[2] * il : 1.f;
+      }
+      const float ray[3] = {p[0] - viewpoint[0], p[1] - viewpoint[1], p[2] - viewpoint[2]};
+      if (ray[0] * n[0] + (ray[1] * n[1] + ray[2] * n[2]) > 0) {
+        n[0] = -n[0];
+        n[1] = -n[1];
+        n[2] = -n[2];
+      }
+      normals[3 * k + 0] = n[0];
+      normals[3 * k + 1] = n[1];
+      normals[3 * k + 2] = n[2];
+      ++k;
+    }
+  free(g);
+  return k;
+}
+
 /* ------------------------------------------------------------------------ */
 /* librealsense rs2_deproject_pixel_to_point, no distortion:
  *   x = (u - ppx)/fx; y = (v - ppy)/fy; P = (z*x, z*y, z), z = scale*d. */

@@ -135,6 +135,9 @@ void orc_compute_normals(const float* xyz, int64_t m, const orc_kdtree* tree,
  * NaN->0 mapping) when keep_invalid, else dropped.  Returns point count. */
 int64_t orc_unproject(const uint16_t* depth, int w, int h, const float K[4],
                       float depth_scale, int keep_invalid, float* xyz);
+/* image-grid normals of pyramid level s (restates k_grid_normals) */
+int64_t orc_grid_normals(const uint16_t* depth, int w, int h, int s, const float K[4],
+                         float depth_scale, int r, const float viewpoint[3], float* normals);
 int64_t orc_unproject_strided(const uint16_t* depth, int w, int h, int s, const float K[4],
                               float depth_scale, int keep_invalid, float* xyz);
 

@@ -64,6 +64,7 @@ PROTOTYPES = {
     "rst_target_free": (C.c_int, [_P]),
     "rst_target_size": (C.c_int64, [_P]),
     "rst_target_compute_normals": (C.c_int, [_P, _P, C.c_int, c_float_p]),
+    "rst_target_compute_grid_normals": (C.c_int, [_P, _P, C.c_int, c_float_p]),
     "rst_target_get_normals": (C.c_int, [_P, _P, c_float_p]),
     "rst_target_query_nn": (C.c_int, [_P, _P, c_float_p, C.c_int64, c_int32_p, c_float_p]),
     "rst_target_query_nn_device": (C.c_int, [_P, _P, _P, C.c_int64, _P, _P]),

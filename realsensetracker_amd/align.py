@@ -246,6 +246,13 @@ class Target:
         L.check(L.lib().rst_target_compute_normals(self.ctx.handle, self._h, k, L.fptr(vp)),
                 "compute_normals")
 
+    def compute_grid_normals(self, radius: int = 2, viewpoint=(0.0, 0.0, 0.0)):
+        """Image-grid PCA normals over a (2 radius + 1)^2 pixel window (frame
+        targets only: from_depth_device / pyramid_from_depth_device)."""
+        vp = np.asarray(viewpoint, np.float32)
+        L.check(L.lib().rst_target_compute_grid_normals(self.ctx.handle, self._h, radius,
+                                                        L.fptr(vp)), "compute_grid_normals")
+
     def normals(self) -> np.ndarray:
         out = np.zeros((len(self), 3), np.float32)
         L.check(L.lib().rst_target_get_normals(self.ctx.handle, self._h, L.fptr(out)),

@@ -125,8 +125,8 @@ __device__ __forceinline__ int32_t sop(int32_t a, int32_t b) {
 }
 
 template <bool Max, bool Excl>
-__global__ __launch_bounds__(kBS) void k_scan_tile(const int32_t* __restrict__ in,
-                                                   int32_t* __restrict__ out, int64_t n,
+// (in may equal out: in-place scans, so no __restrict__ on either)
+__global__ __launch_bounds__(kBS) void k_scan_tile(const int32_t* in, int32_t* out, int64_t n,
                                                    int32_t* __restrict__ tot) {
   __shared__ int32_t sh[kBS];
   const int32_t ident = Max ? INT32_MIN : 0;
@@ -296,14 +296,23 @@ __global__ __launch_bounds__(kBS) void k_leaf_cutflag(const uint32_t* __restrict
   cut[i] = leaf_cut(codes, (int)i, seg[i]) ? 1 : 0;
 }
 
-// pleaf = inclusive count of cuts - 1; the cut positions are the leaf starts
-__global__ __launch_bounds__(kBS) void k_leaf_start(int32_t* __restrict__ pleaf, int64_t m,
+// the cut positions (where the inclusive count of cuts steps) are the leaf
+// starts.  Read-only over the counts: thread i reads entry i - 1, so the
+// counts -> leaf ids rewrite (k_leaf_ids) must be a separate launch (a
+// wavefront writing entry i - 1 first made leaf starts vanish at random --
+// leaves of up to 31 points)
+__global__ __launch_bounds__(kBS) void k_leaf_start(const int32_t* __restrict__ pleaf, int64_t m,
                                                     int32_t* __restrict__ lstart) {
   const int64_t i = blockIdx.x * (int64_t)kBS + threadIdx.x;
   if (i >= m) return;
   const int32_t c = pleaf[i];
   if (i == 0 || pleaf[i - 1] != c) lstart[c - 1] = (int32_t)i;
-  pleaf[i] = c - 1;
+}
+
+// pleaf = inclusive count of cuts - 1
+__global__ __launch_bounds__(kBS) void k_leaf_ids(int32_t* __restrict__ pleaf, int64_t m) {
+  const int64_t i = blockIdx.x * (int64_t)kBS + threadIdx.x;
+  if (i < m) pleaf[i] -= 1;
 }
 
 __global__ __launch_bounds__(kBS) void k_leaf_tail(int32_t* __restrict__ lstart, int nl0, int nl,
@@ -530,6 +539,7 @@ int target_build_device(rst_ctx* ctx, const float* d_xyz, int64_t m, bool with_b
     }
     const int nl = t->nleaves;
     k_leaf_start<<<blocks_for(m), kBS, 0, st>>>(t->pleaf, m, t->lstart);
+    k_leaf_ids<<<blocks_for(m), kBS, 0, st>>>(t->pleaf, m);
     k_leaf_tail<<<blocks_for(nl + 1 - NL), kBS, 0, st>>>(t->lstart, NL, nl, (int32_t)m);
     k_leaf_boxes<<<blocks_for(nl), kBS, 0, st>>>(view_of(t), t->nodes);
     int64_t cnt = nl / 2;

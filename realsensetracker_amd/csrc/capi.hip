@@ -352,6 +352,14 @@ int rst_target_compute_normals(rst_ctx* ctx, rst_target* t, int k, const float v
   return RST_OK;
 }
 
+int rst_target_compute_grid_normals(rst_ctx* ctx, rst_target* t, int radius, const float vp[3]) {
+  if (!ctx || !t) return RST_E_ARG;
+  RST_HIP(hipSetDevice(ctx->device));
+  RST_CHECK(compute_grid_normals(ctx, t, radius, vp));
+  RST_HIP(hipStreamSynchronize(ctx->stream));
+  return RST_OK;
+}
+
 int rst_target_get_normals(rst_ctx* ctx, const rst_target* t, float* normals) {
   if (!ctx || !t || (t->m > 0 && !normals)) return RST_E_ARG;
   if (!t->nrm) return RST_E_STATE;
@@ -489,6 +497,22 @@ int rst_debug_query_nn_fallback(rst_ctx* ctx, const rst_target* t, const float* 
   hipStreamSynchronize(ctx->stream);
   hipFree(dq);
   return s < 0 ? s : RST_OK;
+}
+
+int rst_debug_target_leaves(rst_ctx* ctx, const rst_target* t, int32_t* lstart, int32_t cap,
+                            int32_t* pleaf, int32_t* nleaves) {
+  if (!ctx || !t || !nleaves || !t->has_bvh) return RST_E_ARG;
+  RST_HIP(hipSetDevice(ctx->device));
+  *nleaves = t->nleaves;
+  if (lstart && cap >= t->nleaves + 1) {
+    RST_HIP(hipMemcpyAsync(lstart, t->lstart, sizeof(int32_t) * (t->nleaves + 1),
+                           hipMemcpyDeviceToHost, ctx->stream));
+  }
+  if (pleaf && t->m > 0)
+    RST_HIP(hipMemcpyAsync(pleaf, t->pleaf, sizeof(int32_t) * t->m, hipMemcpyDeviceToHost,
+                           ctx->stream));
+  RST_HIP(hipStreamSynchronize(ctx->stream));
+  return RST_OK;
 }
 
 int rst_debug_seq_sum4(rst_ctx* ctx, const float* xyzw, int64_t n, float out[4]) {

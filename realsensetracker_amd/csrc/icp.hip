@@ -63,8 +63,12 @@ constexpr int kCertBit = 1 << 30;
 #ifndef RST_COLD_ADJ2
 #define RST_COLD_ADJ2 0
 #endif
-#ifndef RST_PROJ_SEED
-#define RST_PROJ_SEED 1  // cold queries start at their projection into a frame target's pixel grid
+#ifndef RST_BALL_TILES
+#define RST_BALL_TILES 1  // cold iterations: wave-shared branch-and-bound tiles (k_icp_fb)
+#endif
+#ifndef RST_BALL_ITERS
+#define RST_BALL_ITERS 4  // ... in the first iterations of a pair (r02r: iterations 0-3
+                          // 1237/531/426/432 us vs 1668/674/568/492 per-lane; later ones lose)
 #endif
 #ifndef RST_DIAG
 #define RST_DIAG 0  // 1: per-iteration certificate counters (rst_debug_queue_trace)
@@ -1010,39 +1014,8 @@ __global__ void k_solve_only(const double* __restrict__ totals, IcpParams prm,
 // Each entry is added to its own lane's sums, so the slab is reproducible.
 // Every block then folds kernel 1's slab rows b, b + G, ... into its own
 // row, so the solve kernel reduces G rows.  Block 0 publishes E.
-// Projective warm start (frame targets): the query projected through the
-// target's pixel grid, the valid points of the 3 x 3 level pixels around it
-// offered to r.  Returns r's best position, -1 when no pixel held a point.
-// A start for the exact searches only -- never taken as the answer.
-__device__ __forceinline__ int proj_seed(const BvhView& bv, const PixView& pv, float x, float y,
-                                         float z, Best2& r) {
-  if (!pv.map || !(z > 0.f)) return -1;
-  const float iz = 1.0f / z;
-  const float u = (pv.fx * x * iz + pv.cx) / (float)pv.s;
-  const float v = (pv.fy * y * iz + pv.cy) / (float)pv.s;
-  if (!(u > -2.f && v > -2.f && u < (float)pv.w + 1.f && v < (float)pv.h + 1.f)) return -1;
-  const int uc = (int)floorf(u + 0.5f), vc = (int)floorf(v + 0.5f);
-  int cand[9];
-#pragma unroll
-  for (int k = 0; k < 9; ++k) {  // all map loads first: one latency
-    const int uu = uc + k % 3 - 1, vv = vc + k / 3 - 1;
-    const bool in = uu >= 0 && vv >= 0 && uu < pv.w && vv < pv.h;
-    cand[k] = in ? pv.map[(int64_t)vv * pv.w + uu] : -1;
-  }
-#pragma unroll
-  for (int k = 0; k < 9; ++k) {
-    const int c = cand[k];
-    if ((uint32_t)c < (uint32_t)bv.m) {
-      const float4 w = bv.pts[c];
-      r.offer(d2_ref(x, y, z, w.x, w.y, w.z), f2i(w.w), c);
-    }
-  }
-  return r.pos[0];
-}
-
 template <class Acc>
-__global__ __launch_bounds__(kBS, Acc::kFbMinWaves) void k_icp_fb(BvhView bv, AdjView av, PixView pv,
-                                                AccArgs aa,
+__global__ __launch_bounds__(kBS, Acc::kFbMinWaves) void k_icp_fb(BvhView bv, AdjView av, AccArgs aa,
                                                 const float4* __restrict__ src,
                                                 IcpState* __restrict__ st,
                                                 float4* __restrict__ nnq,
@@ -1050,19 +1023,30 @@ __global__ __launch_bounds__(kBS, Acc::kFbMinWaves) void k_icp_fb(BvhView bv, Ad
                                                 const int32_t* __restrict__ qbuf,
                                                 const int32_t* __restrict__ qcnt, int nb1,
                                                 int lane_min, const double* __restrict__ slab1,
-                                                double* __restrict__ slab2, int64_t n) {
+                                                double* __restrict__ slab2, int64_t n,
+                                                int4* __restrict__ qbuf2,
+                                                int32_t* __restrict__ qcnt2, int wave_max) {
   extern __shared__ int pref[];  // [nb1 + 1]
   __shared__ double lds[(kBS / kWave) * Acc::NV];
-  __shared__ WnnScratch wsc[kBS / kWave];
+  __shared__ int wcnt[kBS / kWave];
+#if RST_BALL_TILES
+  __shared__ BallScratch bsc[kBS / kWave];
+#endif
   if (Acc::kCanFinish && st->done) return;  // converged: nothing reads the slabs
   queue_prefix(qcnt, nb1, pref, blockIdx.x == 0 ? st : nullptr);
   __syncthreads();
-  const int E = pref[nb1];
+  // a short queue goes to k_icp_wave whole (one wavefront per query)
+  const int E = pref[nb1] <= wave_max ? 0 : pref[nb1];
   double v[Acc::NV];
 #pragma unroll
   for (int k = 0; k < Acc::NV; ++k) v[k] = 0.0;
   const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
   const bool many = E >= lane_min;  // uniform
+#if RST_BALL_TILES
+  // the first iterations of a pair (no neighbour yet, or the pose still
+  // moving by centimetres): the wave-shared ball tiles
+  const bool ball = many && st->iter < RST_BALL_ITERS;
+#endif
   // wavefront w of the grid takes the contiguous entries [w C, (w + 1) C),
   // C = ceil(E / W): a short steady-state queue spreads a couple of entries
   // over every wave (not all of it onto the first blocks' lanes), a long
@@ -1070,8 +1054,11 @@ __global__ __launch_bounds__(kBS, Acc::kFbMinWaves) void k_icp_fb(BvhView bv, Ad
   // coherent -- entries
   const int W = gridDim.x * (kBS / kWave);
   const int gw = blockIdx.x * (kBS / kWave) + wid;
-  const int C = (E + W - 1) / W;
+  // whole wavefronts of entries (a partial chunk idles lanes through the
+  // whole search): C = ceil(E / W) rounded up to a multiple of 64
+  const int C = ((E + W - 1) / W + kWave - 1) & ~(kWave - 1);
   const int e0 = gw * C, e1 = min(E, e0 + C);
+  int nq2 = 0;  // this wave's entries left to the wave search (k_icp_wave)
   if (e0 < e1) {
     const Uni u = load_uni(st);
     for (int r0 = e0; r0 < e1; r0 += kWave) {  // uniform per wave
@@ -1108,7 +1095,6 @@ __global__ __launch_bounds__(kBS, Acc::kFbMinWaves) void k_icp_fb(BvhView bv, Ad
           atomicOr(&st->guard, 2);
           warm = -1;
         }
-        if (warm < 0) warm = proj_seed(bv, pv, px, py, pz, r2);
         if (warm < 0) warm = morton_seed(bv, px, py, pz);
         // seeded with the warm point and its sorted neighbour, so the
         // second bound starts finite
@@ -1119,10 +1105,37 @@ __global__ __launch_bounds__(kBS, Acc::kFbMinWaves) void k_icp_fb(BvhView bv, Ad
           const float4 w2 = bv.pts[nb];
           r2.offer(d2_ref(px, py, pz, w2.x, w2.y, w2.z), f2i(w2.w), nb);
         }
-        const float rc = adj_search2(bv, av, warm, px, py, pz, r2);
+      }
+#if RST_BALL_TILES
+      if (ball) {
+        // cold: the wave's queries share one branch-and-bound walk
+        float mq = 0.f;
+        const bool act = has && fin;
+        int gfail = 0;
+        int4 gdet = make_int4(0, 0, 0, 0);
+        if (ball_tile_search(bv, act, px, py, pz, r2, mq, bsc[wid], gfail, gdet)) {
+          if (act) {
+            g = fminf(r2.d[1] < FLT_MAX ? margin_sqrt(r2.d[1]) * 0.99999f : FLT_MAX, mq);
+            exact = true;
+          }
+        }
+        if (gfail && lane == 0) {
+          if (atomicOr(&st->guard, 8 * gfail) == 0) {
+            st->path[kQTrace - 1][0] = gdet.x;
+            st->path[kQTrace - 1][1] = gdet.y;
+            st->path[kQTrace - 1][2] = gdet.z;
+            st->path[kQTrace - 1][3] = gdet.w;
+          }
+        }
+      } else
+#endif
+      if (has) {
+        const float rc = adj_search2(bv, av, r2.pos[0], px, py, pz, r2);
         exact = margin_sqrt(r2.d[0]) * 1.00001f + 1e-30f < rc;
+        if (exact) g = cert_bound(r2, rc);
+      }
+      if (has) {
         if (exact) {
-          g = cert_bound(r2, rc);
           const int pos = r2.pos[0];
           const float4 q = bv.pts[pos];
           nnq[i] = make_float4(q.x, q.y, q.z, i2f(pos | (g > 0.f ? kCertBit : 0)));
@@ -1160,38 +1173,180 @@ __global__ __launch_bounds__(kBS, Acc::kFbMinWaves) void k_icp_fb(BvhView bv, Ad
           Acc::add(v, bv, aa, u, s, px, py, pz, r.d, r.pos, q);
         }
       } else {
-        uint64_t m = __ballot(unres);
-        while (m) {  // the wave on one query at a time
-          const int j = __ffsll((long long)m) - 1;
-          m &= m - 1;
-          const float qx = wnn_rl(px, j), qy = wnn_rl(py, j), qz = wnn_rl(pz, j);
-          Best2 rr;
-          rr.d[0] = wnn_rl(r2.d[0], j);
-          rr.d[1] = wnn_rl(r2.d[1], j);
-          rr.id[0] = __builtin_amdgcn_readlane(r2.id[0], j);
-          rr.id[1] = __builtin_amdgcn_readlane(r2.id[1], j);
-          rr.pos[0] = __builtin_amdgcn_readlane(r2.pos[0], j);
-          rr.pos[1] = __builtin_amdgcn_readlane(r2.pos[1], j);
-          const int start = rr.pos[0];
-          if (!nn_wave_adj(bv, av, kAdj2Shift, start, qx, qy, qz, rr, wsc[wid]) &&
-              !nn_wave_adj(bv, av, kAdj3Shift, start, qx, qy, qz, rr, wsc[wid]))
-            nn_wave_one(bv, start, qx, qy, qz, rr, wsc[wid]);
-          if (lane == j) {
-            const Best1 r = rr.first();
-            const bool cok = r.pos >= 0;
-            const float4 q = bv.pts[cok ? r.pos : 0];
-            nnq[i] = make_float4(q.x, q.y, q.z, i2f(cok ? (r.pos | kCertBit) : r.pos));
-            if (cok) cert[i] = make_float4(px, py, pz, margin_sqrt(rr.d[1]) * 0.99999f);
-            Acc::add(v, bv, aa, u, s, px, py, pz, r.d, r.pos, q);
-          }
-        }
+        // to the wave search, compacted in entry order behind this wave's
+        // chunk start (fewer than the chunk's entries: always fits)
+        const uint64_t m = __ballot(unres);
+        if (unres)
+          qbuf2[e0 + nq2 + __popcll(m & ((1ull << lane) - 1ull))] =
+              make_int4(i, r2.pos[0], r2.pos[1], 0);
+        nq2 += __popcll(m);
       }
     }
+  }
+  // per-wave and per-block counts of the wave-search queue
+  if (lane == 0) {
+    qcnt2[gw] = nq2;
+    wcnt[wid] = nq2;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int t = 0;
+#pragma unroll
+    for (int k = 0; k < kBS / kWave; ++k) t += wcnt[k];
+    qcnt2[W + blockIdx.x] = t;
   }
   if constexpr (Acc::kSums)
     block_sum_to_slab_fold<Acc::NV, kBS>(v, lds, slab2 + (int64_t)blockIdx.x * Acc::RS, slab1, nb1,
                                          Acc::RS, blockIdx.x, gridDim.x);
 }
+
+// ---- kernel 2b: the wave searches -------------------------------------------------
+// One query per wavefront at a time, spread round-robin over the grid so no
+// wavefront carries several:
+//   * a short kernel-1 queue (E <= wave_max: the steady state) is taken
+//     here whole: the leaf adjacency of the last neighbour searched by the
+//     whole wave (nn_wave_adj1 -- a few memory latencies, where a lane alone
+//     pays one per listed leaf), then as below when it does not cover;
+//   * otherwise the queries k_icp_fb's lanes left open: level-2, then
+//     level-3 adjacency with the leaves staged in LDS, else the staged BVH
+//     walk from the best point so far.
+// Two nearest throughout, so each leaves a certificate.  Entry g (kernel-1
+// block segments, or fallback-wave segments in wave order, rebuilt from the
+// per-block counts) always goes to the same wave, so the slab is
+// reproducible.  Every block then folds the fallback slab's rows b, b + G,
+// ... into its own row.
+template <class Acc>
+__global__ __launch_bounds__(kBS) void k_icp_wave(BvhView bv, AdjView av, AccArgs aa,
+                                                  const float4* __restrict__ src,
+                                                  IcpState* __restrict__ st,
+                                                  float4* __restrict__ nnq,
+                                                  float4* __restrict__ cert,
+                                                  const int32_t* __restrict__ qbuf,
+                                                  const int32_t* __restrict__ qcnt, int nb1,
+                                                  const int4* __restrict__ qbuf2,
+                                                  const int32_t* __restrict__ qcnt2, int w1,
+                                                  int wave_max, const double* __restrict__ slab2,
+                                                  int rows2, double* __restrict__ slab3,
+                                                  int64_t n) {
+  extern __shared__ int pref[];  // [max(nb1, w1 / 4) + 1]
+  __shared__ double lds[(kBS / kWave) * Acc::NV];
+  __shared__ WnnScratch wsc[kBS / kWave];
+  if (Acc::kCanFinish && st->done) return;
+  const int E = st->fb_e;  // kernel 1's queue length (k_icp_fb block 0)
+  const bool whole = E <= wave_max;  // uniform
+  const int g1 = w1 / (kBS / kWave);  // fallback blocks
+  const int NB = whole ? nb1 : g1;
+  queue_prefix(whole ? qcnt : qcnt2 + w1, NB, pref, nullptr);
+  __syncthreads();
+  const int E2 = pref[NB];
+  double v[Acc::NV];
+#pragma unroll
+  for (int k = 0; k < Acc::NV; ++k) v[k] = 0.0;
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+  const int W = gridDim.x * (kBS / kWave);
+  const int gw = blockIdx.x * (kBS / kWave) + wid;
+  if (gw < E2) {
+    // the fallback's chunk size (k_icp_fb): its wave w's entries start at w C
+    const int C = ((E + w1 - 1) / w1 + kWave - 1) & ~(kWave - 1);
+    const Uni u = load_uni(st);
+    for (int g = gw; g < E2; g += W) {  // uniform per wave
+      int lo = 0, hi = NB - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (pref[mid] <= g)
+          lo = mid;
+        else
+          hi = mid - 1;
+      }
+      int off = g - pref[lo];
+      int i, p0 = -1, p1 = -1;
+      if (whole) {
+        i = qbuf[lo * (int64_t)kBS + off];
+      } else {
+        // block lo's four wave segments
+        const int4 c4 = *reinterpret_cast<const int4*>(qcnt2 + (kBS / kWave) * lo);
+        int k = 0;
+        if (off >= c4.x) {
+          off -= c4.x;
+          k = 1;
+          if (off >= c4.y) {
+            off -= c4.y;
+            k = 2;
+            if (off >= c4.z) {
+              off -= c4.z;
+              k = 3;
+            }
+          }
+        }
+        const int4 ent = qbuf2[(int64_t)((kBS / kWave) * lo + k) * C + off];
+        i = ent.x;
+        p0 = ent.y;
+        p1 = ent.z;
+      }
+      if ((uint32_t)i >= (uint32_t)n) {  // index guard (never expected)
+        if (lane == 0) atomicOr(&st->guard, 4);
+        continue;
+      }
+      const float4 s = src[i];
+      float px, py, pz;
+      xform(u.P, s.x, s.y, s.z, px, py, pz);
+      if (whole) {  // seeds as k_icp_fb's: the last neighbour and its sorted neighbour
+        p0 = f2i(nnq[i].w);
+        if (p0 >= 0) p0 &= kPosMask;
+        if (p0 >= bv.m) {
+          if (lane == 0) atomicOr(&st->guard, 2);
+          p0 = -1;
+        }
+        if (p0 < 0) p0 = morton_seed(bv, px, py, pz);
+        p1 = bv.m > 1 ? (p0 + 1 < bv.m ? p0 + 1 : p0 - 1) : -1;
+      }
+      Best2 rr;
+      rr.init();
+      if ((uint32_t)p0 < (uint32_t)bv.m) {
+        const float4 w = bv.pts[p0];
+        rr.offer(d2_ref(px, py, pz, w.x, w.y, w.z), f2i(w.w), p0);
+      } else {
+        if (lane == 0) atomicOr(&st->guard, 2);
+        continue;
+      }
+      if ((uint32_t)p1 < (uint32_t)bv.m) {
+        const float4 w = bv.pts[p1];
+        rr.offer(d2_ref(px, py, pz, w.x, w.y, w.z), f2i(w.w), p1);
+      }
+      float gcert = -1.f;
+      if (whole) {
+        const float rc = nn_wave_adj1(bv, av, p0, px, py, pz, rr, wsc[wid]);
+        if (margin_sqrt(rr.d[0]) * 1.00001f + 1e-30f < rc) gcert = cert_bound(rr, rc);
+#if RST_DIAG
+        if (lane == 0 && gcert >= 0.f && st->iter < kQTrace) atomicAdd(&st->path[st->iter][1], 1);
+#endif
+      }
+      if (gcert < 0.f) {
+        const int start = rr.pos[0];
+        if (!nn_wave_adj(bv, av, kAdj2Shift, start, px, py, pz, rr, wsc[wid]) &&
+            !nn_wave_adj(bv, av, kAdj3Shift, start, px, py, pz, rr, wsc[wid]))
+          nn_wave_one(bv, start, px, py, pz, rr, wsc[wid]);
+        gcert = rr.d[1] < FLT_MAX ? margin_sqrt(rr.d[1]) * 0.99999f : FLT_MAX;
+      }
+      if (lane == 0) {
+        const Best1 r = rr.first();
+        const bool cok = r.pos >= 0 && gcert > 0.f;
+        const float4 q = bv.pts[r.pos >= 0 ? r.pos : 0];
+        nnq[i] = make_float4(q.x, q.y, q.z, i2f(cok ? (r.pos | kCertBit) : r.pos));
+        if (cok) cert[i] = make_float4(px, py, pz, gcert);
+        Acc::add(v, bv, aa, u, s, px, py, pz, r.d, r.pos, q);
+      }
+    }
+  }
+  if constexpr (Acc::kSums)
+    block_sum_to_slab_fold<Acc::NV, kBS>(v, lds, slab3 + (int64_t)blockIdx.x * Acc::RS, slab2, rows2,
+                                         Acc::RS, blockIdx.x, gridDim.x);
+}
+
+template <class A>
+struct AccTag {
+  using type = A;
+};
 
 inline int blocks_for(int64_t n) { return (int)std::max<int64_t>(1, (n + kBS - 1) / kBS); }
 
@@ -1300,11 +1455,12 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
   const int ncb = std::min(1024, blocks_for(n_local));
   // [kernel 1 (+ centroid) | kernel 3 | totals]
   const size_t rows1 = (size_t)std::max(nblk * RS, ncb * 4);
-  const size_t slab_doubles = rows1 + (size_t)kFbBlocks * RS + 64;
+  const size_t slab_doubles = rows1 + 2 * (size_t)kFbBlocks * RS + 64;
   double* slab = nullptr;
   RST_CHECK(ctx_slab(ctx, sizeof(double) * slab_doubles, &slab));
   double* slab2 = slab + rows1;
-  double* totals = slab2 + (size_t)kFbBlocks * RS;  // 64 doubles
+  double* slab3 = slab2 + (size_t)kFbBlocks * RS;
+  double* totals = slab3 + (size_t)kFbBlocks * RS;  // 64 doubles
 
   // n_total and the centroid are global quantities under sharding
   if (comm) {
@@ -1325,22 +1481,25 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
   // queue (one kBS segment per kernel-1 block) and its per-block counts;
   // RST_SUM_REF: the correspondences and the source in original order
   float4* nnq = nullptr;  // last neighbour (p, pos | kCertBit), -1 = cold
-  int32_t *qbuf = nullptr, *qcnt = nullptr;
+  int32_t *qbuf = nullptr, *qcnt = nullptr, *qcnt2 = nullptr;
+  int4* qbuf2 = nullptr;  // the wave-search queue (k_icp_fb -> k_icp_wave)
   float4* cert = nullptr;  // far-point certificates (read only under kCertBit)
   float4 *corr = nullptr, *srco = nullptr;
   {
     const size_t np = (size_t)std::max<int64_t>(n_local, 1);
     const size_t nq = (size_t)nblk * kBS;
     void* w = nullptr;
-    RST_CHECK(ctx_workspace(ctx, sizeof(float4) * np * (refsum ? 4 : 2) +
-                                     sizeof(int32_t) * (nq + 2 * nblk + 64),
+    RST_CHECK(ctx_workspace(ctx, sizeof(float4) * np * (refsum ? 4 : 2) + sizeof(int4) * nq +
+                                     sizeof(int32_t) * (nq + 2 * nblk + 5 * kFbBlocks + 64),
                             &w));
     cert = (float4*)w;
     nnq = cert + np;
     corr = refsum ? cert + 2 * np : nullptr;
     srco = refsum ? cert + 3 * np : nullptr;
-    qbuf = (int32_t*)(cert + np * (refsum ? 4 : 2));
+    qbuf2 = (int4*)(cert + np * (refsum ? 4 : 2));
+    qbuf = (int32_t*)(qbuf2 + nq);
     qcnt = qbuf + nq;
+    qcnt2 = qcnt + ((2 * nblk + 3) & ~3);  // 16 B aligned (int4 reads)
     RST_HIP(hipMemsetAsync(nnq, 0xff, sizeof(float4) * np, st));
   }
 
@@ -1378,14 +1537,23 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
   aa.max_d2 = opts.p2plane_max_dist > 0 ? opts.p2plane_max_dist * opts.p2plane_max_dist : FLT_MAX;
   aa.pos0 = tgt->pos0;
   const AdjView av = adj_of(tgt);
-  const PixView pv = RST_PROJ_SEED ? tgt->pix : PixView{};
   const size_t fb_lds = sizeof(int) * ((size_t)nblk + 1);
+
   // fallback grid (RST_FB_BLOCKS: tuning knob, <= kFbBlocks)
   static const int fb_grid = [] {
     const char* e = getenv("RST_FB_BLOCKS");
     const int v = e ? atoi(e) : kFbDefault;
     return (v >= 1 && v <= kFbBlocks) ? v : kFbBlocks;
   }();
+  const size_t wave_lds = sizeof(int) * ((size_t)std::max(nblk, fb_grid) + 1);
+  const int fb_waves = (kBS / kWave) * fb_grid;  // fallback wavefronts
+  // kernel-1 queues up to wave_max go to k_icp_wave whole, one wavefront per
+  // query (RST_WAVE_PER: queries per wavefront; tuning knob)
+  static const int wave_per = [] {
+    const char* e = getenv("RST_WAVE_PER");
+    return e ? atoi(e) : 2;
+  }();
+  const int wave_max = wave_per * fb_waves;
 
   IcpParams prm;
   prm.n = n_total;
@@ -1446,50 +1614,39 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
     };
     RST_CHECK(mark(0));
     if (n_local > 0) {
-      if (p2plane) {
+      // kernel 1 (certificates), the fallback's lane searches, the wave searches
+      auto nn_pass = [&](auto tag) -> int {
+        using Acc = typename decltype(tag)::type;
         if (it < cold_iters)
-          k_icp_tile<P2PlaneAcc><<<nblk, kBS, 0, st>>>(bv, aa, src->pts, n_local, ctx->d_state, nnq,
-                                              cert, qbuf, qcnt, slab, tile_margin);
+          k_icp_tile<Acc><<<nblk, kBS, 0, st>>>(bv, aa, src->pts, n_local, ctx->d_state, nnq, cert,
+                                                qbuf, qcnt, slab, tile_margin);
         else
-          k_icp_nn<P2PlaneAcc><<<nblk, kBS, 0, st>>>(bv, av, aa, src->pts, n_local, ctx->d_state,
-                                             nnq, cert, qbuf, qcnt, slab);
+          k_icp_nn<Acc><<<nblk, kBS, 0, st>>>(bv, av, aa, src->pts, n_local, ctx->d_state, nnq,
+                                              cert, qbuf, qcnt, slab);
         RST_CHECK(mark(1));
-        k_icp_fb<P2PlaneAcc><<<fb_grid, kBS, fb_lds, st>>>(bv, av, pv, aa, src->pts, ctx->d_state,
-                                                             nnq, cert, qbuf, qcnt, nblk,
-                                                             prm.lane_min, slab, slab2, n_local);
-        RST_CHECK(mark(2));
-        k_reduce_solve<P2PlaneAcc><<<1, kRedBS, 0, st>>>(slab, 0, slab2, fb_grid, prm,
+        k_icp_fb<Acc><<<fb_grid, kBS, fb_lds, st>>>(bv, av, aa, src->pts, ctx->d_state, nnq, cert,
+                                                     qbuf, qcnt, nblk, prm.lane_min, slab, slab2,
+                                                     n_local, qbuf2, qcnt2, wave_max);
+        k_icp_wave<Acc><<<fb_grid, kBS, wave_lds, st>>>(bv, av, aa, src->pts, ctx->d_state, nnq,
+                                                         cert, qbuf, qcnt, nblk, qbuf2, qcnt2,
+                                                         fb_waves, wave_max, slab2, fb_grid, slab3,
+                                                         n_local);
+        return mark(2);
+      };
+      if (p2plane) {
+        RST_CHECK(nn_pass(AccTag<P2PlaneAcc>{}));
+        k_reduce_solve<P2PlaneAcc><<<1, kRedBS, 0, st>>>(slab, 0, slab3, fb_grid, prm,
                                                          ctx->d_state, red_out);
       } else if (refsum) {
-        if (it < cold_iters)
-          k_icp_tile<RefAcc><<<nblk, kBS, 0, st>>>(bv, aa, src->pts, n_local, ctx->d_state, nnq,
-                                              cert, qbuf, qcnt, slab, tile_margin);
-        else
-          k_icp_nn<RefAcc><<<nblk, kBS, 0, st>>>(bv, av, aa, src->pts, n_local, ctx->d_state,
-                                             nnq, cert, qbuf, qcnt, slab);
-        RST_CHECK(mark(1));
-        k_icp_fb<RefAcc><<<fb_grid, kBS, fb_lds, st>>>(bv, av, pv, aa, src->pts, ctx->d_state, nnq,
-                                                         cert, qbuf, qcnt, nblk, prm.lane_min,
-                                                         slab, slab2, n_local);
-        RST_CHECK(mark(2));
+        RST_CHECK(nn_pass(AccTag<RefAcc>{}));
         // align_icp.cpp:113,120: sum dst[nbr_i] and cost, i ascending, fp32
         k_seq_sum4<<<1, kWave, 0, st>>>(corr, n_local, ctx->d_state->seq);
         k_cov_ref<<<kCovBlocks, kBS, 0, st>>>(srco, corr, n_local, ctx->d_state, slab2);
         k_reduce_solve<RefAcc><<<1, kRedBS, 0, st>>>(slab, 0, slab2, kCovBlocks, prm,
                                                      ctx->d_state, nullptr);
       } else {
-        if (it < cold_iters)
-          k_icp_tile<P2PointAcc><<<nblk, kBS, 0, st>>>(bv, aa, src->pts, n_local, ctx->d_state, nnq,
-                                              cert, qbuf, qcnt, slab, tile_margin);
-        else
-          k_icp_nn<P2PointAcc><<<nblk, kBS, 0, st>>>(bv, av, aa, src->pts, n_local, ctx->d_state,
-                                             nnq, cert, qbuf, qcnt, slab);
-        RST_CHECK(mark(1));
-        k_icp_fb<P2PointAcc><<<fb_grid, kBS, fb_lds, st>>>(bv, av, pv, aa, src->pts, ctx->d_state,
-                                                             nnq, cert, qbuf, qcnt, nblk,
-                                                             prm.lane_min, slab, slab2, n_local);
-        RST_CHECK(mark(2));
-        k_reduce_solve<P2PointAcc><<<1, kRedBS, 0, st>>>(slab, 0, slab2, fb_grid, prm,
+        RST_CHECK(nn_pass(AccTag<P2PointAcc>{}));
+        k_reduce_solve<P2PointAcc><<<1, kRedBS, 0, st>>>(slab, 0, slab3, fb_grid, prm,
                                                          ctx->d_state, red_out);
       }
     } else {
@@ -1566,7 +1723,11 @@ int icp_finish(rst_ctx* ctx, float pose_inout[16], float* mean_cost, int32_t* it
   }
   const IcpState& h = *ctx->h_state;
   if (h.guard) {  // an index guard tripped: corrupted queue / neighbour state
-    set_last_error(hipErrorIllegalAddress, "ICP index guard", __FILE__, h.guard);
+    static thread_local char msg[160];
+    const int32_t* d = h.path[kQTrace - 1];  // the first trip's details (kernel-specific)
+    snprintf(msg, sizeof(msg), "ICP index guard bits %d (detail %d %d %d %d)", h.guard, d[0], d[1],
+             d[2], d[3]);
+    set_last_error(hipErrorIllegalAddress, msg, __FILE__, __LINE__);
     return RST_E_HIP;
   }
   if (pd.p2plane && h.fail) {

@@ -255,6 +255,97 @@ __global__ __launch_bounds__(kBS) void k_normals(BvhView bv, int64_t m, float vx
   nrm[i] = make_float4(nx, ny, nz, 0.0f);
 }
 
+// Image-grid normals (the point-to-plane perf mode; the reference's
+// ComputeNormals, point_cloud_utils.cpp:176-204, finds its 16 neighbours by
+// kNN -- a frame target already has them on its pixel grid).  A 16 x 16
+// block of level pixels stages its (16 + 2r)^2 window of points in LDS (map
+// -> sorted position -> point); each valid pixel takes the window points
+// within kGridReach window-pitches of itself (depth edges excluded), and
+// their fp32 centroid / covariance PCA (as the reference's, in window order)
+// gives the normal, oriented as OrientNormals (:206-216).  Fewer than 3
+// points: the normal faces the viewpoint.  12 B map/pt in, 16 B/pt out.
+constexpr int kGridT = 16;
+constexpr int kGridMaxR = 2;
+constexpr float kGridReach = 5.0f;  // allows surfaces ~78 deg from the image plane
+
+__global__ __launch_bounds__(kGridT* kGridT) void k_grid_normals(PixView pv, const float4* __restrict__ pts,
+                                                                int r, float vx, float vy, float vz,
+                                                                float4* __restrict__ nrm) {
+  constexpr int TW = kGridT + 2 * kGridMaxR;
+  __shared__ float4 tile[TW * TW];
+  const int tw = kGridT + 2 * r;
+  const int u0 = blockIdx.x * kGridT - r, v0 = blockIdx.y * kGridT - r;
+  for (int k = threadIdx.x; k < tw * tw; k += kGridT * kGridT) {
+    const int uu = u0 + k % tw, vv = v0 + k / tw;
+    int pos = -1;
+    if (uu >= 0 && vv >= 0 && uu < pv.w && vv < pv.h) pos = pv.map[(int64_t)vv * pv.w + uu];
+    tile[k] = pos >= 0 ? pts[pos] : make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
+  }
+  __syncthreads();
+  const int lu = threadIdx.x % kGridT, lv = threadIdx.x / kGridT;
+  const int u = blockIdx.x * kGridT + lu, v = blockIdx.y * kGridT + lv;
+  if (u >= pv.w || v >= pv.h) return;
+  const int pos = pv.map[(int64_t)v * pv.w + u];
+  if (pos < 0) return;
+  const float4 p = tile[(lv + r) * tw + (lu + r)];
+  // window pitch at this depth: pixel spacing s z / fx, r of them
+  const float reach = kGridReach * (float)(r > 0 ? r : 1) * (float)pv.s * p.z / fabsf(pv.fx);
+  const float reach2 = reach * reach;
+  int cnt = 0;
+  float cx = 0.f, cy = 0.f, cz = 0.f;
+  for (int dv = 0; dv <= 2 * r; ++dv)
+    for (int du = 0; du <= 2 * r; ++du) {
+      const float4 q = tile[(lv + dv) * tw + (lu + du)];
+      if (__float_as_int(q.w) < 0) continue;
+      const float dx = q.x - p.x, dy = q.y - p.y, dz = q.z - p.z;
+      if ((dx * dx + dy * dy) + dz * dz > reach2) continue;
+      cx += q.x;
+      cy += q.y;
+      cz += q.z;
+      ++cnt;
+    }
+  float nx, ny, nz;
+  if (cnt >= 3) {
+    const float kf = (float)cnt;
+    cx = cx / kf;
+    cy = cy / kf;
+    cz = cz / kf;
+    float c00 = 0, c01 = 0, c02 = 0, c11 = 0, c12 = 0, c22 = 0;
+    for (int dv = 0; dv <= 2 * r; ++dv)
+      for (int du = 0; du <= 2 * r; ++du) {
+        const float4 q = tile[(lv + dv) * tw + (lu + du)];
+        if (__float_as_int(q.w) < 0) continue;
+        const float ex = q.x - p.x, ey = q.y - p.y, ez = q.z - p.z;
+        if ((ex * ex + ey * ey) + ez * ez > reach2) continue;
+        const float dx = q.x - cx, dy = q.y - cy, dz = q.z - cz;
+        c00 += dx * dx; c01 += dx * dy; c02 += dx * dz;
+        c11 += dy * dy; c12 += dy * dz; c22 += dz * dz;
+      }
+    const double a[6] = {c00, c01, c02, c11, c12, c22};
+    double e[3];
+    sym3_min_vec(a, e);
+    nx = (float)e[0];
+    ny = (float)e[1];
+    nz = (float)e[2];
+  } else {
+    nx = p.x - vx;
+    ny = p.y - vy;
+    nz = p.z - vz;
+    const float l = sqrtf((nx * nx + ny * ny) + nz * nz);
+    const float il = l > 0.f ? 1.0f / l : 0.f;
+    nx *= il;
+    ny *= il;
+    nz = l > 0.f ? nz * il : 1.f;
+  }
+  const float rx = p.x - vx, ry = p.y - vy, rz = p.z - vz;
+  if (rx * nx + (ry * ny + rz * nz) > 0) {  // OrientNormals
+    nx = -nx;
+    ny = -ny;
+    nz = -nz;
+  }
+  nrm[pos] = make_float4(nx, ny, nz, 0.0f);
+}
+
 inline int blocks_for(int64_t n) { return (int)std::max<int64_t>(1, (n + kBS - 1) / kBS); }
 
 }  // namespace
@@ -342,6 +433,23 @@ int compute_normals(rst_ctx* ctx, rst_target* tgt, int k, const float vp[3]) {
     k_normals<16><<<blocks_for(tgt->m), kBS, 0, st>>>(v, tgt->m, x, y, z, tgt->nrm);
   else
     k_normals<32><<<blocks_for(tgt->m), kBS, 0, st>>>(v, tgt->m, x, y, z, tgt->nrm);
+  RST_HIP(hipGetLastError());
+  return RST_OK;
+}
+
+int compute_grid_normals(rst_ctx* ctx, rst_target* tgt, int r, const float vp[3]) {
+  if (!ctx || !tgt) return RST_E_ARG;
+  if (r < 1 || r > kGridMaxR) return RST_E_ARG;
+  if (!tgt->pix.map) return RST_E_STATE;  // not prepared from a depth frame
+  if (!tgt->nrm) {
+    if (target_alloc(tgt, sizeof(float4) * std::max<int64_t>(tgt->m, 1), (void**)&tgt->nrm) < 0)
+      return RST_E_NOMEM;
+  }
+  if (tgt->m == 0) return RST_OK;
+  const float x = vp ? vp[0] : 0.f, y = vp ? vp[1] : 0.f, z = vp ? vp[2] : 0.f;
+  const dim3 grid((tgt->pix.w + kGridT - 1) / kGridT, (tgt->pix.h + kGridT - 1) / kGridT);
+  k_grid_normals<<<grid, kGridT * kGridT, 0, ctx->stream>>>(tgt->pix, tgt->pts, r, x, y, z,
+                                                            tgt->nrm);
   RST_HIP(hipGetLastError());
   return RST_OK;
 }

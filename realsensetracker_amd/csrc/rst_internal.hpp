@@ -195,6 +195,8 @@ int query_nn_fallback_device(rst_ctx* ctx, const rst_target* tgt, const float* d
 int query_knn_device(rst_ctx* ctx, const rst_target* tgt, const float* d_q,
                      int64_t nq, int k, int32_t* d_idx, float* d_d2);
 int compute_normals(rst_ctx* ctx, rst_target* tgt, int k, const float vp[3]);
+// image-grid normals over a (2r+1)^2 pixel window (frame targets only)
+int compute_grid_normals(rst_ctx* ctx, rst_target* tgt, int r, const float vp[3]);
 
 // ICP (icp.hip)
 int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,

@@ -452,6 +452,10 @@ __device__ __forceinline__ Best2 wave_lex_min(Best2 b) {
 // box_d2 exceeds the current (uniform) bound are skipped.  r <- the wave
 // minimum of every lane's offers.
 template <class R>
+__device__ __forceinline__ void wnn_scan_ranges(const BvhView& bv, WnnScratch& ws, int ns, float qx,
+                                                float qy, float qz, R& mine, R& r, int variant);
+
+template <class R>
 __device__ __forceinline__ void wnn_flush_one(const BvhView& bv, WnnScratch& ws, int ns, float qx,
                                               float qy, float qz, R& mine, R& r, int variant = 0) {
   const int lane = __lane_id();
@@ -481,6 +485,15 @@ __device__ __forceinline__ void wnn_flush_one(const BvhView& bv, WnnScratch& ws,
     ws.leaf_hi[s] = make_float4(0.f, 0.f, i2f(b), i2f(e - b));
   }
   wave_sync();
+  wnn_scan_ranges(bv, ws, ns, qx, qy, qz, mine, r, variant);
+}
+
+// The point scan of wnn_flush_one over staged ranges (ws.leaf_lo[s].x =
+// box_d2, ws.leaf_hi[s] = (-, -, begin, count) for s < ns).
+template <class R>
+__device__ __forceinline__ void wnn_scan_ranges(const BvhView& bv, WnnScratch& ws, int ns, float qx,
+                                                float qy, float qz, R& mine, R& r, int variant) {
+  const int lane = __lane_id();
   const int g = lane >> 4, o = lane & 15;
   const float bnd = r.bound();
   const int last = bv.m - 1;
@@ -898,6 +911,52 @@ RST_HD float adj_search2(const BvhView& bv, const AdjView& av, int start, float 
   return rc;
 }
 
+// The two nearest of one query through the leaf adjacency of the leaf
+// holding sorted position `warm`, whole wave (adj_search2 with the 24
+// entries tested by 24 lanes at once and the listed leaves' points scanned
+// 16 lanes per leaf, all loads of a round in flight): a few memory
+// latencies instead of a lane's chain of one per leaf.  r (uniform) holds
+// the seeds.  Returns the covered radius Rc as adj_search2 does -- r.first()
+// is exact when sqrt(d[0]) < Rc, and min(r2, Rc) bounds every other point;
+// when the warm leaf's coverage does not reach the first radius nothing is
+// scanned (the return value then fails that test).
+template <class R>
+__device__ __forceinline__ float nn_wave_adj1(const BvhView& bv, const AdjView& av, int warm,
+                                              float qx, float qy, float qz, R& r, WnnScratch& ws) {
+  const int lane = __lane_id();
+  const int nl = bv.nleaves;
+  const int L = leaf_of(bv, warm);
+  float4 l = make_float4(0.f, 0.f, 0.f, 0.f), h = l;
+  int tag = -1;
+  if (lane < kAdjK) {
+    l = av.ent[((int64_t)L * kAdjK + lane) * 2];
+    h = av.ent[((int64_t)L * kAdjK + lane) * 2 + 1];
+    tag = f2i(h.w);
+  }
+  const float4 nlo = bv.nodes[2 * (nl + L)], nhi = bv.nodes[2 * (nl + L) + 1];
+  const float reach = av.reach[L];
+  // the margins of adj_search2
+  const float dl = margin_sqrt(box_d2(qx, qy, qz, nlo, nhi)) * 1.00001f;
+  const float rc = reach * 0.99999f - dl;
+  if (!(dl + margin_sqrt(r.d[0]) * 1.00001f + 1e-30f < reach * 0.99999f)) return rc;
+  // entries are sorted by bbd: testing each against the stop rule is the
+  // sequential scan's early exit
+  const float rad = margin_sqrt(r.bound()) * 1.00001f + 1e-30f;
+  const float bd = box_d2(qx, qy, qz, l, h);
+  const bool cand = tag >= 0 && !(l.w * 0.99999f - dl > rad) && bd <= r.bound();
+  const uint64_t cm = __ballot(cand);
+  const int ns = __popcll(cm);
+  if (cand) {
+    const int k = __popcll(cm & ((1ull << lane) - 1ull));
+    ws.leaf_lo[k] = make_float4(bd, 0.f, 0.f, 0.f);
+    ws.leaf_hi[k] = make_float4(0.f, 0.f, i2f(tag >> 5), i2f(tag & 31));
+  }
+  wave_sync();
+  R mine = r;
+  if (ns > 0) wnn_scan_ranges(bv, ws, ns, qx, qy, qz, mine, r, 0);
+  return rc;
+}
+
 // The certificate bound of adj_search2's result (0: none): min(r2, Rc)
 // with the 1e-5 relative margins of every distance test here.
 RST_HD float cert_bound(const Best2& r, float rc) {
@@ -1032,6 +1091,205 @@ __device__ __forceinline__ void tile_scan(const TileScratch& ts, int ns, float q
     r.id[1] = (int)(uint32_t)k1;
     r.pos[1] = ts.pos[j1];
   }
+}
+
+// ---- ball tiles: the cold iterations' wave-shared search --------------------------------
+// The 64 queries of a wavefront (Morton-consecutive: one compact patch) each
+// hold an upper bound u_i of their nearest distance (the distance to a seed
+// point: the last neighbour, or the Morton seed).  The wave walks the BVH
+// top-down once for the box B = union of the balls (q_i, u_i) (64 nodes per
+// round, the stack in LDS), streaming the leaves that meet B through LDS
+// kBallChunk points at a time; every lane scans every chunk (broadcast
+// reads) for its two nearest, and after each chunk the balls -- and B --
+// shrink to the lanes' new first distances (branch and bound for the whole
+// wave).  A node is dropped only when it misses the current B, which holds
+// every later B, so every target point inside the final B is scanned: each
+// lane's first is exact (its ball lies in B), and the distance Mq from q_i
+// to the outside of the final B bounds every unscanned point -- with the
+// second distance, the certificate min(r2, Mq).  Returns false (lanes keep a
+// valid but unfinished r) when the walk exceeds kBallMaxChunks chunks: the
+// caller finishes those lanes alone.
+constexpr int kBallChunk = 512;    // staged points per scan
+constexpr int kBallLeaves = 128;   // collected leaves (a round adds <= 64)
+constexpr int kBallStack = 320;    // node ids
+constexpr int kBallMaxChunks = 24;
+struct BallScratch {               // per-wave LDS (~12.5 KB)
+  float4 pts[kBallChunk];          // x, y, z, original index bits
+  int pos[kBallChunk];             // sorted position
+  int stack[kBallStack];
+  int leaves[kBallLeaves];
+};
+
+__device__ __forceinline__ float wave_min_f(float x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x = fminf(x, __shfl_xor(x, o, 64));
+  return x;
+}
+
+__device__ __forceinline__ float wave_max_f(float x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x = fmaxf(x, __shfl_xor(x, o, 64));
+  return x;
+}
+
+// The box of the active lanes' balls (radius: the first distance, rounded
+// up by the 1e-5 margins of every coverage test here).
+__device__ __forceinline__ void ball_box(bool act, float qx, float qy, float qz, const Best2& r,
+                                         float4& lo, float4& hi) {
+  const float u = act ? margin_sqrt(r.d[0]) * 1.00001f + 1e-30f : 0.f;
+  lo.x = wave_min_f(act ? qx - u : FLT_MAX);
+  lo.y = wave_min_f(act ? qy - u : FLT_MAX);
+  lo.z = wave_min_f(act ? qz - u : FLT_MAX);
+  hi.x = wave_max_f(act ? qx + u : -FLT_MAX);
+  hi.y = wave_max_f(act ? qy + u : -FLT_MAX);
+  hi.z = wave_max_f(act ? qz + u : -FLT_MAX);
+}
+
+// Scan the leaves ts.leaves[0, nlv) for every lane: their points staged
+// kBallChunk at a time, 16 lanes per leaf.  Returns the chunk count, or -1
+// when an index guard trips (never expected).
+__device__ __forceinline__ int ball_flush(const BvhView& bv, BallScratch& ts, int nlv, float qx,
+                                          float qy, float qz, Best2& r, int4& det) {
+  const int lane = __lane_id();
+  int chunks = 0;
+  for (int l0 = 0; l0 < nlv;) {
+    // leaves [l0, l1) fill one chunk (<= 16 points each)
+    const int l1 = min(nlv, l0 + kBallChunk / 16);
+    int b = 0, c = 0;
+    bool bad = false;
+    if (lane < l1 - l0) {
+      const int L = ts.leaves[l0 + lane];
+      bad = (uint32_t)L >= (uint32_t)bv.nleaves;
+      if (!bad) {
+        b = leaf_begin(bv, L);
+        c = leaf_begin(bv, L + 1) - b;
+        bad = c < 0 || c > 16 || b < 0 || b + c > bv.m;
+      }
+    }
+    const uint64_t bm = __ballot(bad);
+    if (bm != 0) {
+      const int j = __ffsll((long long)bm) - 1;
+      det = make_int4(__shfl(l0 + lane < nlv ? ts.leaves[l0 + lane] : -7, j, kWave),
+                      __shfl(b, j, kWave), __shfl(c, j, kWave), nlv * 1000 + l0);
+      return -1;
+    }
+    int inc = c;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+      const int y = __shfl_up(inc, o, kWave);
+      if (lane >= o) inc += y;
+    }
+    const int total = __shfl(inc, kWave - 1, kWave);
+    const int off = inc - c;
+    const int g = lane >> 4, o = lane & 15;
+    for (int k0 = 0; k0 < l1 - l0; k0 += 4) {  // one leaf per 16 lanes
+      const int kk = k0 + g;
+      const int lb = __shfl(b, kk & 63, kWave), lc = __shfl(c, kk & 63, kWave);
+      const int lo = __shfl(off, kk & 63, kWave);
+      if (kk < l1 - l0 && o < lc) {
+        ts.pts[lo + o] = bv.pts[lb + o];
+        ts.pos[lo + o] = lb + o;
+      }
+    }
+    wave_sync();
+    {
+      uint64_t k0 = ((uint64_t)(uint32_t)f2i(r.d[0]) << 32) | (uint32_t)r.id[0];
+      uint64_t k1 = ((uint64_t)(uint32_t)f2i(r.d[1]) << 32) | (uint32_t)r.id[1];
+      int j0 = -1, j1 = -1;
+      for (int j = 0; j < total; ++j) {
+        const float4 p = ts.pts[j];
+        const float d2 = d2_ref(qx, qy, qz, p.x, p.y, p.z);
+        const uint64_t key = ((uint64_t)(uint32_t)f2i(d2) << 32) | (uint32_t)f2i(p.w);
+        const bool in = (key != k0) & (key < k1);
+        const bool first = in & (key < k0);
+        k1 = first ? k0 : (in ? key : k1);
+        j1 = first ? j0 : (in ? j : j1);
+        k0 = first ? key : k0;
+        j0 = first ? j : j0;
+      }
+      // positions of the chunk's winners before the next chunk overwrites it
+      const int p0 = j0 >= 0 ? ts.pos[j0] : r.pos[0];
+      const int p1 = j1 >= 0 ? ts.pos[j1] : (j0 >= 0 ? r.pos[0] : r.pos[1]);
+      if (j0 >= 0 || j1 >= 0) {
+        r.d[0] = i2f((int)(uint32_t)(k0 >> 32));
+        r.id[0] = (int)(uint32_t)k0;
+        r.d[1] = i2f((int)(uint32_t)(k1 >> 32));
+        r.id[1] = (int)(uint32_t)k1;
+        r.pos[1] = p1;
+        r.pos[0] = p0;
+      }
+    }
+    wave_sync();
+    l0 = l1;
+    ++chunks;
+  }
+  return chunks;
+}
+
+// act: the lane holds a query (r: its seeds, r.d[0] finite); inactive lanes
+// only help.  On true, Mq (per active lane) = the distance from q to the
+// outside of the final box, margins applied.  The whole wave calls it.
+__device__ __forceinline__ bool ball_tile_search(const BvhView& bv, bool act, float qx, float qy,
+                                                 float qz, Best2& r, float& mq, BallScratch& ts,
+                                                 int& gfail, int4& det) {
+  const int lane = __lane_id();
+  const int nl = bv.nleaves;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  float4 lo, hi;
+  ball_box(act, qx, qy, qz, r, lo, hi);
+  if (lane == 0) ts.stack[0] = 1;
+  int sp = 1, nlv = 0, chunks = 0;
+  wave_sync();
+  while (sp > 0 || nlv > 0) {
+    if (sp > 0 && nlv <= kBallLeaves - kWave && sp <= kBallStack - 2 * kWave) {
+      const int k = min(kWave, sp);
+      int node = 0;
+      if (lane < k) node = ts.stack[sp - 1 - lane];
+      sp -= k;
+      wave_sync();
+      bool pass = false;
+      const uint64_t gm = __ballot(lane < k && (node < 1 || node >= 2 * nl));
+      if (gm != 0) {  // index guard
+        const int j = __ffsll((long long)gm) - 1;
+        det = make_int4(__shfl(node, j, kWave), sp, nlv, nl);
+        gfail = 1;
+        return false;
+      }
+      if (lane < k) {
+        const float4 nlo = bv.nodes[2 * node], nhi = bv.nodes[2 * node + 1];
+        pass = box_meets(nlo, nhi, lo.x, lo.y, lo.z, hi.x, hi.y, hi.z);
+      }
+      const bool isleaf = node >= nl;
+      const uint64_t im = __ballot(pass && !isleaf), lm = __ballot(pass && isleaf);
+      if (pass && !isleaf) {
+        const int rk = __popcll(im & lt);
+        ts.stack[sp + 2 * rk] = 2 * node;
+        ts.stack[sp + 2 * rk + 1] = 2 * node + 1;
+      }
+      if (pass && isleaf) ts.leaves[nlv + __popcll(lm & lt)] = node - nl;
+      sp += 2 * __popcll(im);
+      nlv += __popcll(lm);
+      wave_sync();
+      if (sp > 0 && nlv <= kBallLeaves - kWave && sp <= kBallStack - 2 * kWave) continue;
+    }
+    if (nlv == 0) {
+      if (sp == 0) break;
+      return false;  // stack full with no leaf to drain (never expected)
+    }
+    const int c = ball_flush(bv, ts, nlv, qx, qy, qz, r, det);
+    if (c < 0) {
+      gfail = 2;
+      return false;
+    }
+    chunks += c;
+    nlv = 0;
+    if (chunks > kBallMaxChunks) return false;
+    ball_box(act, qx, qy, qz, r, lo, hi);  // the balls shrink
+  }
+  const float m = fminf(fminf(fminf(qx - lo.x, hi.x - qx), fminf(qy - lo.y, hi.y - qy)),
+                        fminf(qz - lo.z, hi.z - qz));
+  mq = m * 0.99999f;
+  return true;
 }
 
 // ---- the ICP loop's candidate lists ----------------------------------------------------

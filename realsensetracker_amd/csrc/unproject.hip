@@ -240,7 +240,7 @@ int rst_unproject(rst_ctx* ctx, const uint16_t* depth, const rst_intrinsics* K, 
 
 namespace rst {
 // depth (device) -> points of pyramid level `stride` -> target handle
-// (+ normals when normals_k > 0)
+// (+ normals: normals_k > 0 kNN-PCA, < 0 image-grid window of radius -normals_k)
 static int frame_prepare(rst_ctx* ctx, const uint16_t* d_depth, const rst_intrinsics* K,
                          int stride, int normals_k, rst_target** out) {
   const int64_t npx = (int64_t)K->width * K->height;
@@ -272,9 +272,10 @@ static int frame_prepare(rst_ctx* ctx, const uint16_t* d_depth, const rst_intrin
     t->pix.h = hl;
     t->pix.s = stride;
   }
-  if (s >= 0 && normals_k > 0) {
-    const float vp[3] = {0.f, 0.f, 0.f};
-    s = compute_normals(ctx, t, normals_k, vp);
+  if (s >= 0 && normals_k != 0) {
+    const float vp[3] = {0.f, 0.f, 0.f};  // the camera
+    s = normals_k > 0 ? compute_normals(ctx, t, normals_k, vp)
+                      : compute_grid_normals(ctx, t, -normals_k, vp);
   }
   hipStreamSynchronize(ctx->stream);
   ctx_release(ctx, dx, dxc);

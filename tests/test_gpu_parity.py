@@ -441,6 +441,123 @@ def test_frame_prepare_device(ctx):
     assert np.array_equal(idx, g["nn_idx0"]) and np.array_equal(d2, g["nn_d20"])
 
 
+def _leaf_table(ctx, t):
+    f = L.lib().rst_debug_target_leaves
+    f.restype = C.c_int
+    f.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_int32), C.c_int32,
+                  C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
+    nl = C.c_int32()
+    L.check(f(ctx.handle, t.handle, None, 0, None, C.byref(nl)), "leaves")
+    ls = np.zeros(nl.value + 1, np.int32)
+    pl = np.zeros(max(1, len(t)), np.int32)
+    ip = C.POINTER(C.c_int32)
+    L.check(f(ctx.handle, t.handle, ls.ctypes.data_as(ip), len(ls), pl.ctypes.data_as(ip),
+              C.byref(nl)), "leaves")
+    return ls, pl[:len(t)]
+
+
+def test_index_leaves_consistent_under_reuse(ctx):
+    """The BVH build's leaf table, over repeated builds of 640x480 frames
+    (pool blocks reused): every leaf <= 16 points (rst_bvh.hpp leaf_cut;
+    the LDS-staged searches rely on it), lstart a partition of [0, m), and
+    pleaf the inverse of it."""
+    K = driver.intrinsics(640, 480)
+    sc = driver.SyntheticScene(0)
+    bufs = [A.DeviceBuffer.from_array(sc.render(sc.trajectory(i), K, noise_seed=i), ctx)
+            for i in range(3)]
+    for rep in range(4):
+        for b in bufs:
+            t = A.Target.from_depth_device(b.ptr, K, 0, ctx)
+            ls, pl = _leaf_table(ctx, t)
+            sz = np.diff(ls)
+            assert ls[0] == 0 and ls[-1] == len(t)
+            assert sz.min() >= 0 and sz.max() <= 16, (rep, sz.max())
+            assert np.array_equal(pl, np.repeat(np.arange(len(sz)), sz))
+            t.free()
+
+
+def _frame(ctx, K, seed, normals_k):
+    sc = driver.SyntheticScene(seed)
+    d = sc.render(sc.trajectory(0), K, noise_seed=seed + 1)
+    dd = A.DeviceBuffer.from_array(d, ctx)
+    return d, A.Target.from_depth_device(dd.ptr, K, normals_k, ctx)
+
+
+@pytest.mark.parametrize("radius", [1, 2])
+def test_grid_normals_match_restatement(ctx, radius):
+    """Image-grid normals (k_grid_normals) vs their C restatement at 640x480:
+    the same window points and fp32 sums, eigenvectors from two different
+    solvers (closed form vs Jacobi) -- compared by angle."""
+    K = driver.intrinsics(640, 480)
+    d, t = _frame(ctx, K, 3, -radius)
+    g = t.normals()
+    o = O.grid_normals(d, [K.fx, K.fy, K.cx, K.cy], radius)
+    assert g.shape == o.shape
+    cos = np.sum(g * o, axis=1)
+    assert np.mean(cos > 1 - 1e-5) > 0.999, np.mean(cos > 1 - 1e-5)
+    assert np.mean(cos > 0.99) > 0.999  # near-degenerate windows: two solvers
+
+
+def test_grid_normals_pyramid_level(ctx):
+    K = driver.intrinsics(640, 480)
+    sc = driver.SyntheticScene(8)
+    d = sc.render(sc.trajectory(0), K, noise_seed=2)
+    dd = A.DeviceBuffer.from_array(d, ctx)
+    lv = A.Target.pyramid_from_depth_device(dd.ptr, K, 3, -1, ctx)
+    for l, t in enumerate(lv):
+        o = O.grid_normals(d, [K.fx, K.fy, K.cx, K.cy], 1, stride=1 << l)
+        cos = np.sum(t.normals() * o, axis=1)
+        assert np.mean(cos > 1 - 1e-5) > 0.999, (l, np.mean(cos > 1 - 1e-5))
+
+
+def test_grid_normals_agree_with_knn_normals(ctx):
+    """The perf-mode normals against the reference's kNN-16 PCA normals on
+    the same 640x480 frame (both oriented to the camera)."""
+    K = driver.intrinsics(640, 480)
+    _, t = _frame(ctx, K, 5, -2)
+    g = t.normals()
+    t.compute_normals(16)
+    k = t.normals()
+    cos = np.sum(g * k, axis=1)
+    print(f"grid vs kNN-16 normals: cos>0.99 {np.mean(cos > 0.99):.4f} cos>0.9 "
+          f"{np.mean(cos > 0.9):.4f} cos>0 {np.mean(cos > 0):.5f}")
+    assert np.mean(cos > 0.9) > 0.98
+    assert np.mean(cos > 0) > 0.999
+
+
+def test_grid_normals_contract(ctx):
+    g = load_golden("pair_120x90_s1")
+    t = A.Target.build(g["dst"], ctx)  # no pixel grid
+    with pytest.raises(L.RstError):
+        t.compute_grid_normals(2)
+    K = driver.intrinsics(160, 120)
+    _, tf = _frame(ctx, K, 2, 0)
+    for bad in (0, 3):
+        with pytest.raises(L.RstError):
+            tf.compute_grid_normals(bad)
+    tf.compute_grid_normals(1)
+    n = tf.normals()
+    assert np.all(np.isfinite(n)) and np.allclose(np.linalg.norm(n, axis=1), 1.0, atol=1e-5)
+
+
+@pytest.mark.parametrize("normals_k", [-2, 16])
+def test_p2plane_640_recovers_motion(ctx, normals_k):
+    """640x480 frame pair at a known offset (1-3 deg, 1-3 cm): P2PLANE from
+    frame targets, image-grid or kNN-16 target normals, recovers it."""
+    K = driver.intrinsics(640, 480)
+    sc = driver.SyntheticScene(7)
+    da, db, D = driver.make_pair(sc, K, seed=33)
+    ba = A.DeviceBuffer.from_array(da, ctx)
+    bb = A.DeviceBuffer.from_array(db, ctx)
+    t = A.Target.from_depth_device(ba.ptr, K, normals_k, ctx)
+    s = A.Target.from_depth_device(bb.ptr, K, 0, ctx)
+    r = A.align_prepared(s, t, None, L.default_opts(mode=L.RST_P2PLANE, max_iter=30))
+    e = pose_err(r.pose, D)
+    print(f"P2PLANE 640x480 normals_k={normals_k}: {r.iterations} iterations, error {e}")
+    assert r.ok
+    assert e[0] < 5e-4 and e[1] < 5e-4, e  # measured ~3e-5 rad, ~1.1e-4 m
+
+
 # ---- SolveKabsch (align_icp.cpp:18-71) -------------------------------------------------
 @pytest.mark.parametrize("weighted", [False, True])
 def test_solve_kabsch_device_vs_oracle(ctx, weighted):

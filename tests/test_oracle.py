@@ -203,6 +203,31 @@ def test_normals_oracle_unit_and_oriented():
     assert np.all(np.sum(g["dst"] * n, axis=1) <= 0)  # face the viewpoint (origin)
 
 
+def test_grid_normals_oracle_plane_and_golden_frames():
+    """The image-grid normal restatement: a tilted plane's exact normal, and
+    on the golden depth frames agreement with the kNN-16 normals."""
+    h, w = 60, 80
+    K4 = np.array([70.0, 70.0, 40.0, 30.0], np.float32)
+    v, u = np.mgrid[0:h, 0:w].astype(np.float64)
+    # plane z = 1.5 + 0.2 x  (x = (u - cx) / fx * z) -> solve z per pixel
+    xr = (u - K4[2]) / K4[0]
+    z = 1.5 / (1.0 - 0.2 * xr)
+    depth = np.round(z * 1000).astype(np.uint16)
+    n = O.grid_normals(depth, K4, 2)
+    pts = O.unproject(depth, K4)
+    assert n.shape == pts.shape
+    true = np.array([0.2, 0.0, -1.0]) / np.linalg.norm([0.2, 0.0, -1.0])
+    cos = n @ true
+    assert np.median(cos) > 0.999, np.median(cos)
+    np.testing.assert_allclose(np.linalg.norm(n, axis=1), 1.0, atol=1e-5)
+    assert np.all(np.sum(pts * n, axis=1) <= 0)  # OrientNormals: face the camera
+    for name in PAIR_NAMES:
+        g = load_golden(name)
+        gn = O.grid_normals(g["depth_a"], g["K4"], 2)
+        assert gn.shape == g["normals_dst"].shape
+        assert np.mean(np.sum(gn * g["normals_dst"], axis=1) > 0.9) > 0.9, name
+
+
 def test_solve_kabsch_oracle_recovers_motion_and_matches_numpy():
     """SolveKabsch (align_icp.cpp:18-71): exact correspondences under a known
     rigid motion give that motion; weights enter the covariance linearly."""

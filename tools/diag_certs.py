@@ -27,6 +27,8 @@ for sm in (L.RST_SUM_FP64,):
     r = A.align_prepared(fb, fa, None, L.default_opts(sum_mode=sm))
     q = np.zeros((256, 5), np.int32)
     qt(ctx.handle, L.iptr(q), 256)
-    print(f"n={n} ok={r.ok}; iter: queue certified adj-exact  (fractions of n)")
+    print(f"n={n} ok={r.ok}; iter: queue certified adj-exact (fractions of n), "
+          "solve kernel: reduce us, solve us")
     for it in list(range(12)) + [16, 24, 32, 48, 64, 96, 127]:
-        print(f"{it:4d} {q[it, 0] / n:8.4f} {q[it, 1] / n:8.4f} {q[it, 2] / n:8.4f}")
+        print(f"{it:4d} {q[it, 0] / n:8.4f} {q[it, 1] / n:8.4f} {q[it, 2] / n:8.4f}"
+              f" {q[it, 3] * 0.01:7.2f} {q[it, 4] * 0.01:7.2f}")
