@@ -7,8 +7,8 @@ One step = one incoming frame of the stream, fully on the GPU:
     -> AlignIcp3d(curr, prev) with the reference's P2POINT_REF loop,
        128 fixed iterations (rs_replay_app.cpp:246-251).
 value = ICP iterations/s over all ranks (steps * 128 / time).  Frame
-preparation runs on its own HIP stream and --inflight frame pairs (default 2)
-are aligned concurrently, each on its own context/stream: one pair's
+preparation runs on its own HIP stream and --inflight frame pairs (default 4,
+on 8 hardware queues: --hw-queues) are aligned concurrently, each on its own context/stream: one pair's
 iteration chain is launch/latency-bound, so independent pairs overlap on the
 GPU.  A second timed loop runs the build's point-to-plane mode on the same
 frames (reported as extra fields).
@@ -279,13 +279,20 @@ def main():
     ap.add_argument("--no-gicp", action="store_true")
     ap.add_argument("--graphs", action="store_true",
                     help="replay each align's iteration loop as a hipGraph (no kernel timing)")
-    ap.add_argument("--inflight", type=int, default=2,
+    ap.add_argument("--inflight", type=int, default=4,
                     help="frame pairs in flight per GPU (one HIP stream each)")
+    ap.add_argument("--hw-queues", type=int, default=8,
+                    help="GPU_MAX_HW_QUEUES for this process (HIP's default, 4, puts the "
+                         "frame-preparation stream and 4 pairs' streams on 4 hardware queues; "
+                         "r02u/v: 2 pairs 16.2k, 4 pairs 15.8k it/s at 4 queues, 19.4k at 8; "
+                         "0: leave the environment's value)")
     ap.add_argument("--ref-steps", type=int, default=4,
                     help="frames timed in the reference-rounding mode (extra field; 0: skip)")
     ap.add_argument("--roof-steps", type=int, default=4,
                     help="frames of the one-pair-in-flight kernel timing pass (roofline)")
     a = ap.parse_args()
+    if a.hw_queues > 0:  # read by the HIP runtime at its first call (none yet)
+        os.environ["GPU_MAX_HW_QUEUES"] = str(a.hw_queues)
     if "WORLD_SIZE" not in os.environ and a.gpus > 1:
         # no launcher: one rank process per GPU, spawned before any GPU call
         return RV.launch(a.gpus, sys.argv[1:], str(Path(__file__).resolve()))
@@ -559,7 +566,8 @@ def main():
                                       if pyr else "full-resolution ICP iteration"),
                    "points_per_frame": round(n_avg), "frames_cycled": nfr,
                    "accumulation": "fp64 partial sums", "parallelism": f"replica{world}",
-                   "pairs_in_flight_per_gpu": len(actx), "hipgraph": bool(a.graphs)},
+                   "pairs_in_flight_per_gpu": len(actx), "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
+                   "hipgraph": bool(a.graphs)},
         "frames_per_s": frames_all / dt,
         "pairs_ok": st["ok"],
         **({"iterations_all_levels_per_s": iters_raw / dt} if pyr else {}),

@@ -49,14 +49,6 @@ constexpr int kCertBit = 1 << 30;
 #ifndef RST_NN_MIN_WAVES
 #define RST_NN_MIN_WAVES 4  // k_icp_nn<P2PointAcc> (r02: Best2 certificate search, 96 VGPRs spilled at 5)
 #endif
-#ifndef RST_COLD_ITERS
-#define RST_COLD_ITERS 0  // iterations of a pair that run the LDS-tile kernel 1 (r02g: the cold
-                          // NN distances of the stream, 4 cm median, 15 cm p99.9, need tiles
-                          // far larger than LDS holds; off)
-#endif
-#ifndef RST_TILE_MARGIN
-#define RST_TILE_MARGIN 0.025f  // metres the tile's box is grown by
-#endif
 #ifndef RST_COLD_FAST
 #define RST_COLD_FAST 1
 #endif
@@ -99,7 +91,11 @@ __device__ __forceinline__ int xcd_tile(int b, int nb) {
 #endif
 }
 
-constexpr int kPosMask = kCertBit - 1;
+// nnq position flags: kCertBit (the certificate in cert[] is valid),
+// kFarBit (the last search needed more than the leaf adjacency: the next
+// search goes straight to the wave-wide deep search)
+constexpr int kFarBit = 1 << 29;
+constexpr int kPosMask = kFarBit - 1;
 constexpr int kFbBlocks = 2048;  // largest fallback grid (RST_FB_BLOCKS)
 constexpr int kFbDefault = 1024;  // fallback grid (4096 waves; r01g sweep: 2048 / 512 lose)
 // From a queue of lane_min entries (IcpParams: the cold first iterations,
@@ -548,10 +544,13 @@ __global__ __launch_bounds__(kBS) void k_icp_nn(BvhView bv, AdjView av, AccArgs 
                                                 double* __restrict__ slab) {
   (void)av;
   __shared__ double lds[(kBS / kWave) * Acc::NV];
-  __shared__ int wq[kBS / kWave];
+  __shared__ int wq[2][kBS / kWave];
   const int tb = xcd_tile(blockIdx.x, gridDim.x);
+  // the far queue: the second half of qbuf / qcnt
+  int32_t* __restrict__ qbuff = qbuf + (int64_t)gridDim.x * kBS;
+  int32_t* __restrict__ qcntf = qcnt + gridDim.x;
   if (Acc::kCanFinish && st->done) {  // converged: uniform early exit
-    if (threadIdx.x == 0) qcnt[tb] = 0;
+    if (threadIdx.x == 0) qcnt[tb] = qcntf[tb] = 0;
     return;
   }
   const Uni u = load_uni(st);
@@ -578,7 +577,8 @@ __global__ __launch_bounds__(kBS) void k_icp_nn(BvhView bv, AdjView av, AccArgs 
     certified = margin_sqrt(dq) * 1.00001f + moved + 1e-30f < c.w;
   }
   const bool need = act && fin && !certified;
-  const uint64_t bm = __ballot(need);
+  const bool far = wb >= 0 && (wb & kFarBit);
+  const uint64_t bm = __ballot(need && !far), fm = __ballot(need && far);
   const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
 #if RST_DIAG
   {  // diagnostics build: per iteration, lanes certified
@@ -587,107 +587,30 @@ __global__ __launch_bounds__(kBS) void k_icp_nn(BvhView bv, AdjView av, AccArgs 
     if (lane == 0 && it < kQTrace) atomicAdd(&const_cast<IcpState*>(st)->path[it][0], __popcll(cm));
   }
 #endif
-  if (lane == 0) wq[wid] = __popcll(bm);
+  if (lane == 0) {
+    wq[0][wid] = __popcll(bm);
+    wq[1][wid] = __popcll(fm);
+  }
   __syncthreads();
-  int before = 0, total = 0;
+  int before = 0, total = 0, beforef = 0, totalf = 0;
 #pragma unroll
   for (int w = 0; w < kBS / kWave; ++w) {
-    before += w < wid ? wq[w] : 0;
-    total += wq[w];
+    before += w < wid ? wq[0][w] : 0;
+    total += wq[0][w];
+    beforef += w < wid ? wq[1][w] : 0;
+    totalf += wq[1][w];
   }
-  if (need) qbuf[tb * (int64_t)kBS + before + __popcll(bm & ((1ull << lane) - 1ull))] = (int)i;
-  if (threadIdx.x == 0) qcnt[tb] = total;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  if (need && !far) qbuf[tb * (int64_t)kBS + before + __popcll(bm & lt)] = (int)i;
+  if (need && far) qbuff[tb * (int64_t)kBS + beforef + __popcll(fm & lt)] = (int)i;
+  if (threadIdx.x == 0) {
+    qcnt[tb] = total;
+    qcntf[tb] = totalf;
+  }
   if (certified)
     Acc::add(v, bv, aa, u, s, px, py, pz, dq, f2i(tq.w) & kPosMask, tq);
   else if (act && !fin)  // no neighbour: the query's untouched outputs
     Acc::add(v, bv, aa, u, s, px, py, pz, FLT_MAX, -1, tq);
-  if constexpr (Acc::kSums) block_sum_to_slab<Acc::NV, kBS>(v, lds, slab + (int64_t)tb * Acc::RS);
-}
-
-// Kernel 1 of the cold iterations (the first of a pair: no neighbour is
-// known yet, or the pose still moves by centimetres, so the certificates
-// fail): each wavefront stages the target points around its 64 queries in
-// LDS (rst_wave_nn.hpp tile_stage, the box of the queries grown by
-// `margin`) and every lane scans the tile: its exact nearest neighbour when
-// that lies inside the grown box, with a fresh certificate.  The rest -- and
-// a wave whose tile does not fit (e.g. straddling a depth edge) -- goes to
-// the search queue exactly as in k_icp_nn.
-template <class Acc>
-__global__ __launch_bounds__(kBS) void k_icp_tile(BvhView bv, AccArgs aa,
-                                                  const float4* __restrict__ src, int64_t n,
-                                                  const IcpState* __restrict__ st,
-                                                  float4* __restrict__ nnq,
-                                                  float4* __restrict__ cert,
-                                                  int32_t* __restrict__ qbuf,
-                                                  int32_t* __restrict__ qcnt,
-                                                  double* __restrict__ slab, float margin) {
-  __shared__ double lds[(kBS / kWave) * Acc::NV];
-  __shared__ int wq[kBS / kWave];
-  __shared__ TileScratch tsc[kBS / kWave];
-  const int tb = blockIdx.x;
-  if (Acc::kCanFinish && st->done) {
-    if (threadIdx.x == 0) qcnt[tb] = 0;
-    return;
-  }
-  const Uni u = load_uni(st);
-  double v[Acc::NV];
-#pragma unroll
-  for (int k = 0; k < Acc::NV; ++k) v[k] = 0.0;
-  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
-  const int64_t i = tb * (int64_t)kBS + threadIdx.x;
-  const bool act = i < n;
-  const float4 s = act ? src[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-  float px, py, pz;
-  xform(u.P, s.x, s.y, s.z, px, py, pz);  // align_icp.cpp:107
-  const bool fin = act && finite3(px, py, pz);
-  // the wave's queries' box, grown by the margin
-  const float lx = wnn_min_f(fin ? px : FLT_MAX) - margin;
-  const float ly = wnn_min_f(fin ? py : FLT_MAX) - margin;
-  const float lz = wnn_min_f(fin ? pz : FLT_MAX) - margin;
-  const float hx = wnn_max_f(fin ? px : -FLT_MAX) + margin;
-  const float hy = wnn_max_f(fin ? py : -FLT_MAX) + margin;
-  const float hz = wnn_max_f(fin ? pz : -FLT_MAX) + margin;
-  int ns = -1;
-  if (__ballot(fin) != 0) ns = tile_stage(bv, lx, ly, lz, hx, hy, hz, tsc[wid]);
-  if (ns == -2 && lane == 0) atomicOr(&const_cast<IcpState*>(st)->guard, 4);
-  Best2 r2;
-  r2.init();
-  bool exact = false;
-  float g = 0.f;
-  if (ns > 0 && fin) {
-    tile_scan(tsc[wid], ns, px, py, pz, r2);
-    // every target point off the tile lies beyond one face of the box
-    const float mq = fminf(fminf(fminf(px - lx, hx - px), fminf(py - ly, hy - py)),
-                           fminf(pz - lz, hz - pz)) * 0.99999f;
-    exact = r2.pos[0] >= 0 && margin_sqrt(r2.d[0]) * 1.00001f + 1e-30f < mq;
-    if (exact)
-      g = fminf(r2.d[1] < FLT_MAX ? margin_sqrt(r2.d[1]) * 0.99999f : FLT_MAX, mq);
-  }
-  const bool need = fin && !exact;
-  const uint64_t bm = __ballot(need);
-  if (lane == 0) wq[wid] = __popcll(bm);
-  __syncthreads();
-  int before = 0, total = 0;
-#pragma unroll
-  for (int w = 0; w < kBS / kWave; ++w) {
-    before += w < wid ? wq[w] : 0;
-    total += wq[w];
-  }
-  if (need) {
-    qbuf[tb * (int64_t)kBS + before + __popcll(bm & ((1ull << lane) - 1ull))] = (int)i;
-    // the tile's best point (if any) is the search's warm start
-    nnq[i] = make_float4(0.f, 0.f, 0.f, i2f(r2.pos[0]));
-  }
-  if (threadIdx.x == 0) qcnt[tb] = total;
-  if (exact) {
-    const int pos = r2.pos[0];
-    const float4 q = bv.pts[pos];
-    nnq[i] = make_float4(q.x, q.y, q.z, i2f(pos | (g > 0.f ? kCertBit : 0)));
-    if (g > 0.f) cert[i] = make_float4(px, py, pz, g);
-    Acc::add(v, bv, aa, u, s, px, py, pz, r2.d[0], pos, q);
-  } else if (act && !fin) {  // no neighbour: the query's untouched outputs
-    Acc::add(v, bv, aa, u, s, px, py, pz, FLT_MAX, -1, make_float4(0.f, 0.f, 0.f, 0.f));
-  }
   if constexpr (Acc::kSums) block_sum_to_slab<Acc::NV, kBS>(v, lds, slab + (int64_t)tb * Acc::RS);
 }
 
@@ -998,22 +921,92 @@ __global__ void k_solve_only(const double* __restrict__ totals, IcpParams prm,
 }
 
 // ---- kernel 2: the searches of the queued queries -----------------------------------
-// Queue entry e (global order: kernel 1's block segments in block order;
-// every block rebuilds their prefix in LDS from the per-block counts) goes
-// to wavefront e / C of the grid (C = ceil(E / W)): each lane runs the
-// two-nearest search through the leaf adjacency of its last neighbour
-// (rst_wave_nn.hpp adj_search2; cold lanes: a Morton-code seed), which
-// answers most and refreshes their certificate.  What the adjacency does
-// not cover is finished by
-//   * (queue < lane_min) the whole wavefront, one query at a time: level-2,
-//     then level-3 adjacency with the leaves staged in LDS, else the staged
-//     BVH walk from the best point so far -- two nearest, so it leaves a
-//     certificate (far points: frame borders, occlusions);
-//   * (queue >= lane_min: the cold first iterations) the lane alone, a
-//     bottom-up BVH walk from its best point (rst_bvh.hpp search).
-// Each entry is added to its own lane's sums, so the slab is reproducible.
-// Every block then folds kernel 1's slab rows b, b + G, ... into its own
-// row, so the solve kernel reduces G rows.  Block 0 publishes E.
+// Kernel 1 leaves two queues (block segments in block order; every block
+// here rebuilds both prefixes in LDS from the per-block counts): the near
+// queue (certificate failed) and the far queue (certificate failed and the
+// last search needed more than the leaf adjacency: frame borders,
+// occlusions -- points whose neighbour is far and changes every iteration).
+//   * cold (queues >= lane_min: the first iterations of a pair): one entry
+//     per lane over both queues -- the wave-shared ball tiles in the first
+//     RST_BALL_ITERS iterations, else the two-nearest leaf-adjacency search
+//     of the lane's last neighbour (rst_wave_nn.hpp adj_search2), then what
+//     that does not cover by the lane's own bottom-up walk;
+//   * otherwise the near queue one entry per row of 16 lanes (row_adj2: the
+//     leaf adjacency at a few memory latencies), what it does not cover
+//     finished at once by the whole wave (deep_search), and the far queue
+//     one entry per wavefront, from the last wavefront of the grid down (the
+//     ones the near queue leaves idle): the two searches run side by side
+//     instead of one after the other.
+// Wavefront w takes the contiguous near entries [w C, (w + 1) C), C =
+// ceil(E / W) rounded up to whole rounds (spatially coherent runs; a short
+// steady-state queue spreads over many waves).  Each entry is added by one
+// fixed lane, so the slab is reproducible.  Every block then folds kernel
+// 1's slab rows b, b + G, ... into its own row, so the solve kernel reduces
+// G rows.  Block 0 publishes the near queue length.
+
+// One query, the whole wavefront (r: uniform seeds in, the two nearest out):
+// the leaf adjacency (when try1), level-2 then level-3 adjacency with the
+// leaves staged in LDS, else the staged BVH walk.  Returns the certificate
+// bound; far = the leaf adjacency did not answer.
+__device__ __forceinline__ float deep_search(const BvhView& bv, const AdjView& av, bool try1,
+                                             float qx, float qy, float qz, Best2& r,
+                                             WnnScratch& ws, bool& far) {
+  far = true;
+  if (try1) {
+    const float rc = nn_wave_adj1(bv, av, r.pos[0], qx, qy, qz, r, ws);
+    if (margin_sqrt(r.d[0]) * 1.00001f + 1e-30f < rc) {
+      far = false;
+      return cert_bound(r, rc);
+    }
+  }
+  const int start = r.pos[0];
+  if (!nn_wave_adj(bv, av, kAdj2Shift, start, qx, qy, qz, r, ws) &&
+      !nn_wave_adj(bv, av, kAdj3Shift, start, qx, qy, qz, r, ws))
+    nn_wave_one(bv, start, qx, qy, qz, r, ws);
+  return r.d[1] < FLT_MAX ? margin_sqrt(r.d[1]) * 0.99999f : FLT_MAX;
+}
+
+// Source index of queue entry e: near entries [0, E), then far ones.
+__device__ __forceinline__ int queue_entry(int e, int E, const int* pref, const int* preff,
+                                           int nb1, const int32_t* __restrict__ qbuf,
+                                           const int32_t* __restrict__ qbuff) {
+  const bool f = e >= E;
+  const int* p = f ? preff : pref;
+  const int x = f ? e - E : e;
+  int lo = 0, hi = nb1 - 1;  // block segment holding entry x
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (p[mid] <= x)
+      lo = mid;
+    else
+      hi = mid - 1;
+  }
+  return (f ? qbuff : qbuf)[lo * (int64_t)kBS + (x - p[lo])];
+}
+
+// The outputs of one answered query: its neighbour (+ certificate, far
+// flag) and its term of the sums.
+template <class Acc>
+__device__ __forceinline__ void fb_record(double (&v)[Acc::NV], const BvhView& bv,
+                                          const AccArgs& aa, const Uni& u, float4* __restrict__ nnq,
+                                          float4* __restrict__ cert, int i, const float4& s,
+                                          float px, float py, float pz, const Best2& r, float g,
+                                          bool far) {
+  const int pos = r.pos[0];
+  const bool cok = pos >= 0 && g > 0.f;
+  const float4 q = bv.pts[pos >= 0 ? pos : 0];
+  nnq[i] = make_float4(q.x, q.y, q.z,
+                       i2f(pos < 0 ? pos : (pos | (cok ? kCertBit : 0) | (far ? kFarBit : 0))));
+  if (cok) cert[i] = make_float4(px, py, pz, g);
+  Acc::add(v, bv, aa, u, s, px, py, pz, r.d[0], pos, q);
+}
+
+// per-wave LDS: the deep search's staging or the ball tiles (never both)
+union FbScratch {
+  WnnScratch w;
+  BallScratch b;
+};
+
 template <class Acc>
 __global__ __launch_bounds__(kBS, Acc::kFbMinWaves) void k_icp_fb(BvhView bv, AdjView av, AccArgs aa,
                                                 const float4* __restrict__ src,
@@ -1023,47 +1016,60 @@ __global__ __launch_bounds__(kBS, Acc::kFbMinWaves) void k_icp_fb(BvhView bv, Ad
                                                 const int32_t* __restrict__ qbuf,
                                                 const int32_t* __restrict__ qcnt, int nb1,
                                                 int lane_min, const double* __restrict__ slab1,
-                                                double* __restrict__ slab2, int64_t n,
-                                                int4* __restrict__ qbuf2,
-                                                int32_t* __restrict__ qcnt2, int wave_max) {
-  extern __shared__ int pref[];  // [nb1 + 1]
+                                                double* __restrict__ slab2, int64_t n) {
+  extern __shared__ int pref[];  // [2 (nb1 + 1)]: near prefix, far prefix
+  int* preff = pref + nb1 + 1;
+  const int32_t* __restrict__ qbuff = qbuf + (int64_t)nb1 * kBS;
+  const int32_t* __restrict__ qcntf = qcnt + nb1;
   __shared__ double lds[(kBS / kWave) * Acc::NV];
-  __shared__ int wcnt[kBS / kWave];
-#if RST_BALL_TILES
-  __shared__ BallScratch bsc[kBS / kWave];
-#endif
+  __shared__ int rtags[kBS / kWave][kWave / 16][kAdjK];  // row_adj2 candidates
+  __shared__ FbScratch scr[kBS / kWave];
+  __shared__ int4 left[kBS / kWave][kWave / 16];  // a round's leftovers (i, seeds)
   if (Acc::kCanFinish && st->done) return;  // converged: nothing reads the slabs
   queue_prefix(qcnt, nb1, pref, blockIdx.x == 0 ? st : nullptr);
   __syncthreads();
-  // a short queue goes to k_icp_wave whole (one wavefront per query)
-  const int E = pref[nb1] <= wave_max ? 0 : pref[nb1];
+  queue_prefix(qcntf, nb1, preff, nullptr);
+  __syncthreads();
+  const int E = pref[nb1], EF = preff[nb1];
   double v[Acc::NV];
 #pragma unroll
   for (int k = 0; k < Acc::NV; ++k) v[k] = 0.0;
   const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
-  const bool many = E >= lane_min;  // uniform
+  const bool many = E + EF >= lane_min;  // uniform
 #if RST_BALL_TILES
   // the first iterations of a pair (no neighbour yet, or the pose still
   // moving by centimetres): the wave-shared ball tiles
   const bool ball = many && st->iter < RST_BALL_ITERS;
 #endif
-  // wavefront w of the grid takes the contiguous entries [w C, (w + 1) C),
-  // C = ceil(E / W): a short steady-state queue spreads a couple of entries
-  // over every wave (not all of it onto the first blocks' lanes), a long
-  // cold-start queue gives each wave runs of consecutive -- spatially
-  // coherent -- entries
   const int W = gridDim.x * (kBS / kWave);
   const int gw = blockIdx.x * (kBS / kWave) + wid;
-  // whole wavefronts of entries (a partial chunk idles lanes through the
-  // whole search): C = ceil(E / W) rounded up to a multiple of 64
-  const int C = ((E + W - 1) / W + kWave - 1) & ~(kWave - 1);
-  const int e0 = gw * C, e1 = min(E, e0 + C);
-  int nq2 = 0;  // this wave's entries left to the wave search (k_icp_wave)
-  if (e0 < e1) {
-    const Uni u = load_uni(st);
-    for (int r0 = e0; r0 < e1; r0 += kWave) {  // uniform per wave
-      const int e = r0 + lane;
+  // cold: one entry per lane over both queues; else the near queue, one
+  // entry per row of 16 lanes
+  const int EN = many ? E + EF : E;
+  const int per = many ? kWave : kWave / 16;
+  const int C = ((EN + W - 1) / W + per - 1) / per * per;
+  const int e0 = gw * C, e1 = min(EN, e0 + C);
+  const Uni u = load_uni(st);
+  // One work loop, so the deep search has a single call site (two inlined
+  // copies spill): a pending leftover of the last round, else the next
+  // round of entries, else this wave's next far entry.  All uniform.
+  const int fg0 = W - 1 - gw;  // this wave's far entries: fg0, fg0 + W, ...
+  const int nfar = (!many && fg0 < EF) ? (EF - fg0 + W - 1) / W : 0;
+  int r0 = e0, nleft = 0, fdone = 0;
+  while (true) {
+    bool deep = false, try1 = false;
+    int di = 0, dp0 = -1, dp1 = -1;
+    if (nleft > 0) {  // a leftover of the last round (the leaf adjacency did not cover it)
+      --nleft;
+      const int4 en = left[wid][nleft];
+      di = en.x;
+      dp0 = en.y;
+      dp1 = en.z;
+      deep = true;
+    } else if (r0 < e1) {
+      const int e = r0 + (many ? lane : lane >> 4);
       const bool has = e < e1;
+      const bool lead = many || (lane & 15) == 0;  // the lane that records the entry
       int i = 0;
       float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
       float px = 0.f, py = 0.f, pz = 0.f;
@@ -1073,15 +1079,7 @@ __global__ __launch_bounds__(kBS, Acc::kFbMinWaves) void k_icp_fb(BvhView bv, Ad
       bool exact = false;
       float g = 0.f;
       if (has) {
-        int lo = 0, hi = nb1 - 1;  // block segment holding entry e
-        while (lo < hi) {
-          const int mid = (lo + hi + 1) >> 1;
-          if (pref[mid] <= e)
-            lo = mid;
-          else
-            hi = mid - 1;
-        }
-        i = qbuf[lo * (int64_t)kBS + (e - pref[lo])];
+        i = queue_entry(e, E, pref, preff, nb1, qbuf, qbuff);
         if ((uint32_t)i >= (uint32_t)n) {  // index guard (never expected)
           atomicOr(&st->guard, 1);
           i = 0;
@@ -1113,7 +1111,7 @@ __global__ __launch_bounds__(kBS, Acc::kFbMinWaves) void k_icp_fb(BvhView bv, Ad
         const bool act = has && fin;
         int gfail = 0;
         int4 gdet = make_int4(0, 0, 0, 0);
-        if (ball_tile_search(bv, act, px, py, pz, r2, mq, bsc[wid], gfail, gdet)) {
+        if (ball_tile_search(bv, act, px, py, pz, r2, mq, scr[wid].b, gfail, gdet)) {
           if (act) {
             g = fminf(r2.d[1] < FLT_MAX ? margin_sqrt(r2.d[1]) * 0.99999f : FLT_MAX, mq);
             exact = true;
@@ -1129,24 +1127,23 @@ __global__ __launch_bounds__(kBS, Acc::kFbMinWaves) void k_icp_fb(BvhView bv, Ad
         }
       } else
 #endif
-      if (has) {
-        const float rc = adj_search2(bv, av, r2.pos[0], px, py, pz, r2);
-        exact = margin_sqrt(r2.d[0]) * 1.00001f + 1e-30f < rc;
+      if (many) {
+        if (has) {
+          const float rc = adj_search2(bv, av, r2.pos[0], px, py, pz, r2);
+          exact = margin_sqrt(r2.d[0]) * 1.00001f + 1e-30f < rc;
+          if (exact) g = cert_bound(r2, rc);
+        }
+      } else {
+        const bool act = has && fin;
+        const float rc = row_adj2(bv, av, act, r2.pos[0], px, py, pz, r2, rtags[wid][lane >> 4]);
+        exact = act && margin_sqrt(r2.d[0]) * 1.00001f + 1e-30f < rc;
         if (exact) g = cert_bound(r2, rc);
       }
-      if (has) {
-        if (exact) {
-          const int pos = r2.pos[0];
-          const float4 q = bv.pts[pos];
-          nnq[i] = make_float4(q.x, q.y, q.z, i2f(pos | (g > 0.f ? kCertBit : 0)));
-          if (g > 0.f) cert[i] = make_float4(px, py, pz, g);
-          Acc::add(v, bv, aa, u, s, px, py, pz, r2.d[0], pos, q);
-        }
-      }
-      const bool unres = has && fin && !exact;
+      if (has && lead && exact) fb_record<Acc>(v, bv, aa, u, nnq, cert, i, s, px, py, pz, r2, g, false);
+      const bool unres = lead && has && fin && !exact;
 #if RST_DIAG
-      {  // diagnostics build: lanes answered by the adjacency search
-        const uint64_t em = __ballot(has && exact);
+      {  // diagnostics build: entries answered by the adjacency search
+        const uint64_t em = __ballot(lead && has && exact);
         const int it = st->iter;
         if (lane == 0 && it < kQTrace) atomicAdd(&st->path[it][1], __popcll(em));
       }
@@ -1173,173 +1170,63 @@ __global__ __launch_bounds__(kBS, Acc::kFbMinWaves) void k_icp_fb(BvhView bv, Ad
           Acc::add(v, bv, aa, u, s, px, py, pz, r.d, r.pos, q);
         }
       } else {
-        // to the wave search, compacted in entry order behind this wave's
-        // chunk start (fewer than the chunk's entries: always fits)
+        // the row leaders the leaf adjacency did not answer: to the deep
+        // search, one at a time (rare once far points have their own queue)
         const uint64_t m = __ballot(unres);
         if (unres)
-          qbuf2[e0 + nq2 + __popcll(m & ((1ull << lane) - 1ull))] =
-              make_int4(i, r2.pos[0], r2.pos[1], 0);
-        nq2 += __popcll(m);
+          left[wid][__popcll(m & ((1ull << lane) - 1ull))] = make_int4(i, r2.pos[0], r2.pos[1], 0);
+        nleft = __popcll(m);
+        wave_sync();
       }
+      r0 += per;
+    } else if (fdone < nfar) {  // the far queue: one entry per wavefront
+      di = queue_entry(E + fg0 + fdone * W, E, pref, preff, nb1, qbuf, qbuff);
+      ++fdone;
+      try1 = true;
+      deep = true;
+    } else {
+      break;
     }
-  }
-  // per-wave and per-block counts of the wave-search queue
-  if (lane == 0) {
-    qcnt2[gw] = nq2;
-    wcnt[wid] = nq2;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int t = 0;
-#pragma unroll
-    for (int k = 0; k < kBS / kWave; ++k) t += wcnt[k];
-    qcnt2[W + blockIdx.x] = t;
-  }
-  if constexpr (Acc::kSums)
-    block_sum_to_slab_fold<Acc::NV, kBS>(v, lds, slab2 + (int64_t)blockIdx.x * Acc::RS, slab1, nb1,
-                                         Acc::RS, blockIdx.x, gridDim.x);
-}
-
-// ---- kernel 2b: the wave searches -------------------------------------------------
-// One query per wavefront at a time, spread round-robin over the grid so no
-// wavefront carries several:
-//   * a short kernel-1 queue (E <= wave_max: the steady state) is taken
-//     here whole: the leaf adjacency of the last neighbour searched by the
-//     whole wave (nn_wave_adj1 -- a few memory latencies, where a lane alone
-//     pays one per listed leaf), then as below when it does not cover;
-//   * otherwise the queries k_icp_fb's lanes left open: level-2, then
-//     level-3 adjacency with the leaves staged in LDS, else the staged BVH
-//     walk from the best point so far.
-// Two nearest throughout, so each leaves a certificate.  Entry g (kernel-1
-// block segments, or fallback-wave segments in wave order, rebuilt from the
-// per-block counts) always goes to the same wave, so the slab is
-// reproducible.  Every block then folds the fallback slab's rows b, b + G,
-// ... into its own row.
-template <class Acc>
-__global__ __launch_bounds__(kBS) void k_icp_wave(BvhView bv, AdjView av, AccArgs aa,
-                                                  const float4* __restrict__ src,
-                                                  IcpState* __restrict__ st,
-                                                  float4* __restrict__ nnq,
-                                                  float4* __restrict__ cert,
-                                                  const int32_t* __restrict__ qbuf,
-                                                  const int32_t* __restrict__ qcnt, int nb1,
-                                                  const int4* __restrict__ qbuf2,
-                                                  const int32_t* __restrict__ qcnt2, int w1,
-                                                  int wave_max, const double* __restrict__ slab2,
-                                                  int rows2, double* __restrict__ slab3,
-                                                  int64_t n) {
-  extern __shared__ int pref[];  // [max(nb1, w1 / 4) + 1]
-  __shared__ double lds[(kBS / kWave) * Acc::NV];
-  __shared__ WnnScratch wsc[kBS / kWave];
-  if (Acc::kCanFinish && st->done) return;
-  const int E = st->fb_e;  // kernel 1's queue length (k_icp_fb block 0)
-  const bool whole = E <= wave_max;  // uniform
-  const int g1 = w1 / (kBS / kWave);  // fallback blocks
-  const int NB = whole ? nb1 : g1;
-  queue_prefix(whole ? qcnt : qcnt2 + w1, NB, pref, nullptr);
-  __syncthreads();
-  const int E2 = pref[NB];
-  double v[Acc::NV];
-#pragma unroll
-  for (int k = 0; k < Acc::NV; ++k) v[k] = 0.0;
-  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
-  const int W = gridDim.x * (kBS / kWave);
-  const int gw = blockIdx.x * (kBS / kWave) + wid;
-  if (gw < E2) {
-    // the fallback's chunk size (k_icp_fb): its wave w's entries start at w C
-    const int C = ((E + w1 - 1) / w1 + kWave - 1) & ~(kWave - 1);
-    const Uni u = load_uni(st);
-    for (int g = gw; g < E2; g += W) {  // uniform per wave
-      int lo = 0, hi = NB - 1;
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (pref[mid] <= g)
-          lo = mid;
-        else
-          hi = mid - 1;
-      }
-      int off = g - pref[lo];
-      int i, p0 = -1, p1 = -1;
-      if (whole) {
-        i = qbuf[lo * (int64_t)kBS + off];
-      } else {
-        // block lo's four wave segments
-        const int4 c4 = *reinterpret_cast<const int4*>(qcnt2 + (kBS / kWave) * lo);
-        int k = 0;
-        if (off >= c4.x) {
-          off -= c4.x;
-          k = 1;
-          if (off >= c4.y) {
-            off -= c4.y;
-            k = 2;
-            if (off >= c4.z) {
-              off -= c4.z;
-              k = 3;
-            }
-          }
-        }
-        const int4 ent = qbuf2[(int64_t)((kBS / kWave) * lo + k) * C + off];
-        i = ent.x;
-        p0 = ent.y;
-        p1 = ent.z;
-      }
-      if ((uint32_t)i >= (uint32_t)n) {  // index guard (never expected)
+    if (deep) {
+      if ((uint32_t)di >= (uint32_t)n) {  // index guard (never expected)
         if (lane == 0) atomicOr(&st->guard, 4);
         continue;
       }
-      const float4 s = src[i];
+      const float4 s = src[di];
       float px, py, pz;
       xform(u.P, s.x, s.y, s.z, px, py, pz);
-      if (whole) {  // seeds as k_icp_fb's: the last neighbour and its sorted neighbour
-        p0 = f2i(nnq[i].w);
-        if (p0 >= 0) p0 &= kPosMask;
-        if (p0 >= bv.m) {
+      if (try1) {  // seeds as the lanes': the last neighbour and its sorted neighbour
+        int warm = f2i(nnq[di].w);
+        if (warm >= 0) warm &= kPosMask;
+        if (warm >= bv.m) {
           if (lane == 0) atomicOr(&st->guard, 2);
-          p0 = -1;
+          warm = -1;
         }
-        if (p0 < 0) p0 = morton_seed(bv, px, py, pz);
-        p1 = bv.m > 1 ? (p0 + 1 < bv.m ? p0 + 1 : p0 - 1) : -1;
+        if (warm < 0) warm = morton_seed(bv, px, py, pz);
+        dp0 = warm;
+        dp1 = bv.m > 1 ? (warm + 1 < bv.m ? warm + 1 : warm - 1) : -1;
       }
       Best2 rr;
       rr.init();
-      if ((uint32_t)p0 < (uint32_t)bv.m) {
-        const float4 w = bv.pts[p0];
-        rr.offer(d2_ref(px, py, pz, w.x, w.y, w.z), f2i(w.w), p0);
-      } else {
+      if ((uint32_t)dp0 < (uint32_t)bv.m) {
+        const float4 w = bv.pts[dp0];
+        rr.offer(d2_ref(px, py, pz, w.x, w.y, w.z), f2i(w.w), dp0);
+      }
+      if ((uint32_t)dp1 < (uint32_t)bv.m) {
+        const float4 w = bv.pts[dp1];
+        rr.offer(d2_ref(px, py, pz, w.x, w.y, w.z), f2i(w.w), dp1);
+      }
+      if (rr.pos[0] < 0) {  // (never expected: a queued query always has a seed)
         if (lane == 0) atomicOr(&st->guard, 2);
         continue;
       }
-      if ((uint32_t)p1 < (uint32_t)bv.m) {
-        const float4 w = bv.pts[p1];
-        rr.offer(d2_ref(px, py, pz, w.x, w.y, w.z), f2i(w.w), p1);
-      }
-      float gcert = -1.f;
-      if (whole) {
-        const float rc = nn_wave_adj1(bv, av, p0, px, py, pz, rr, wsc[wid]);
-        if (margin_sqrt(rr.d[0]) * 1.00001f + 1e-30f < rc) gcert = cert_bound(rr, rc);
-#if RST_DIAG
-        if (lane == 0 && gcert >= 0.f && st->iter < kQTrace) atomicAdd(&st->path[st->iter][1], 1);
-#endif
-      }
-      if (gcert < 0.f) {
-        const int start = rr.pos[0];
-        if (!nn_wave_adj(bv, av, kAdj2Shift, start, px, py, pz, rr, wsc[wid]) &&
-            !nn_wave_adj(bv, av, kAdj3Shift, start, px, py, pz, rr, wsc[wid]))
-          nn_wave_one(bv, start, px, py, pz, rr, wsc[wid]);
-        gcert = rr.d[1] < FLT_MAX ? margin_sqrt(rr.d[1]) * 0.99999f : FLT_MAX;
-      }
-      if (lane == 0) {
-        const Best1 r = rr.first();
-        const bool cok = r.pos >= 0 && gcert > 0.f;
-        const float4 q = bv.pts[r.pos >= 0 ? r.pos : 0];
-        nnq[i] = make_float4(q.x, q.y, q.z, i2f(cok ? (r.pos | kCertBit) : r.pos));
-        if (cok) cert[i] = make_float4(px, py, pz, gcert);
-        Acc::add(v, bv, aa, u, s, px, py, pz, r.d, r.pos, q);
-      }
+      bool far = true;
+      const float gj = deep_search(bv, av, try1, px, py, pz, rr, scr[wid].w, far);
+      if (lane == 0) fb_record<Acc>(v, bv, aa, u, nnq, cert, di, s, px, py, pz, rr, gj, far);
     }
   }
   if constexpr (Acc::kSums)
-    block_sum_to_slab_fold<Acc::NV, kBS>(v, lds, slab3 + (int64_t)blockIdx.x * Acc::RS, slab2, rows2,
+    block_sum_to_slab_fold<Acc::NV, kBS>(v, lds, slab2 + (int64_t)blockIdx.x * Acc::RS, slab1, nb1,
                                          Acc::RS, blockIdx.x, gridDim.x);
 }
 
@@ -1446,21 +1333,20 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
   hipStream_t st = ctx->stream;
   // one scratch buffer: [centroid / kernel-1 slab | kernel-2 slab | totals]
   const int nblk = blocks_for(n_local);
-  // k_icp_fb scans the per-block queue counts into dynamic LDS, on top of
-  // ~28 KB of static LDS (4 WnnScratch + the reductions): 96 KB caps the
-  // source at ~6.3M points per align (per shard when sharded)
-  if (sizeof(int) * ((size_t)nblk + 1) > (size_t)96 * 1024) return RST_E_ARG;
+  // k_icp_fb scans both queues' per-block counts into dynamic LDS, on top of
+  // ~52 KB of static LDS (4 FbScratch + the reductions): 96 KB caps the
+  // source at ~3.1M points per align (per shard when sharded)
+  if (2 * sizeof(int) * ((size_t)nblk + 1) > (size_t)96 * 1024) return RST_E_ARG;
   const int NV = p2plane ? kNP2Plane : kNP2Point;
   const int RS = p2plane ? P2PlaneAcc::RS : P2PointAcc::RS;
   const int ncb = std::min(1024, blocks_for(n_local));
   // [kernel 1 (+ centroid) | kernel 3 | totals]
   const size_t rows1 = (size_t)std::max(nblk * RS, ncb * 4);
-  const size_t slab_doubles = rows1 + 2 * (size_t)kFbBlocks * RS + 64;
+  const size_t slab_doubles = rows1 + (size_t)kFbBlocks * RS + 64;
   double* slab = nullptr;
   RST_CHECK(ctx_slab(ctx, sizeof(double) * slab_doubles, &slab));
   double* slab2 = slab + rows1;
-  double* slab3 = slab2 + (size_t)kFbBlocks * RS;
-  double* totals = slab3 + (size_t)kFbBlocks * RS;  // 64 doubles
+  double* totals = slab2 + (size_t)kFbBlocks * RS;  // 64 doubles
 
   // n_total and the centroid are global quantities under sharding
   if (comm) {
@@ -1481,8 +1367,7 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
   // queue (one kBS segment per kernel-1 block) and its per-block counts;
   // RST_SUM_REF: the correspondences and the source in original order
   float4* nnq = nullptr;  // last neighbour (p, pos | kCertBit), -1 = cold
-  int32_t *qbuf = nullptr, *qcnt = nullptr, *qcnt2 = nullptr;
-  int4* qbuf2 = nullptr;  // the wave-search queue (k_icp_fb -> k_icp_wave)
+  int32_t *qbuf = nullptr, *qcnt = nullptr;  // near queue, then far queue (k_icp_nn)
   float4* cert = nullptr;  // far-point certificates (read only under kCertBit)
   float4 *corr = nullptr, *srco = nullptr;
   {
@@ -1490,16 +1375,14 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
     const size_t nq = (size_t)nblk * kBS;
     void* w = nullptr;
     RST_CHECK(ctx_workspace(ctx, sizeof(float4) * np * (refsum ? 4 : 2) + sizeof(int4) * nq +
-                                     sizeof(int32_t) * (nq + 2 * nblk + 5 * kFbBlocks + 64),
+                                     sizeof(int32_t) * (2 * nq + 2 * nblk + 64),
                             &w));
     cert = (float4*)w;
     nnq = cert + np;
     corr = refsum ? cert + 2 * np : nullptr;
     srco = refsum ? cert + 3 * np : nullptr;
-    qbuf2 = (int4*)(cert + np * (refsum ? 4 : 2));
-    qbuf = (int32_t*)(qbuf2 + nq);
-    qcnt = qbuf + nq;
-    qcnt2 = qcnt + ((2 * nblk + 3) & ~3);  // 16 B aligned (int4 reads)
+    qbuf = (int32_t*)(cert + np * (refsum ? 4 : 2));
+    qcnt = qbuf + 2 * nq;
     RST_HIP(hipMemsetAsync(nnq, 0xff, sizeof(float4) * np, st));
   }
 
@@ -1537,7 +1420,7 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
   aa.max_d2 = opts.p2plane_max_dist > 0 ? opts.p2plane_max_dist * opts.p2plane_max_dist : FLT_MAX;
   aa.pos0 = tgt->pos0;
   const AdjView av = adj_of(tgt);
-  const size_t fb_lds = sizeof(int) * ((size_t)nblk + 1);
+  const size_t fb_lds = 2 * sizeof(int) * ((size_t)nblk + 1);
 
   // fallback grid (RST_FB_BLOCKS: tuning knob, <= kFbBlocks)
   static const int fb_grid = [] {
@@ -1545,15 +1428,6 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
     const int v = e ? atoi(e) : kFbDefault;
     return (v >= 1 && v <= kFbBlocks) ? v : kFbBlocks;
   }();
-  const size_t wave_lds = sizeof(int) * ((size_t)std::max(nblk, fb_grid) + 1);
-  const int fb_waves = (kBS / kWave) * fb_grid;  // fallback wavefronts
-  // kernel-1 queues up to wave_max go to k_icp_wave whole, one wavefront per
-  // query (RST_WAVE_PER: queries per wavefront; tuning knob)
-  static const int wave_per = [] {
-    const char* e = getenv("RST_WAVE_PER");
-    return e ? atoi(e) : 2;
-  }();
-  const int wave_max = wave_per * fb_waves;
 
   IcpParams prm;
   prm.n = n_total;
@@ -1579,17 +1453,6 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
                           : (n_local < RST_LANE_SMALL_N ? (3 * n_local) / 4 : n_local / 3));
 
   const BvhView bv = view_of(tgt);
-  // the first cold_iters iterations of a pair run the LDS-tile kernel 1
-  // (RST_COLD_ITERS, RST_TILE_MARGIN: tuning knobs, never correctness)
-  static const int cold_iters = [] {
-    const char* e = getenv("RST_COLD_ITERS");
-    return e ? atoi(e) : RST_COLD_ITERS;
-  }();
-  static const float tile_margin = [] {
-    const char* e = getenv("RST_TILE_MARGIN");
-    return e ? (float)atof(e) : RST_TILE_MARGIN;
-  }();
-
   const bool timing = ctx->timing && opts.max_iter > 0;
   if (timing) {  // four events per timed iteration: k1 | k2 | the rest
     const size_t need = 4 * (size_t)opts.max_iter;
@@ -1614,28 +1477,20 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
     };
     RST_CHECK(mark(0));
     if (n_local > 0) {
-      // kernel 1 (certificates), the fallback's lane searches, the wave searches
+      // kernel 1 (certificates), kernel 2 (the queued searches)
       auto nn_pass = [&](auto tag) -> int {
         using Acc = typename decltype(tag)::type;
-        if (it < cold_iters)
-          k_icp_tile<Acc><<<nblk, kBS, 0, st>>>(bv, aa, src->pts, n_local, ctx->d_state, nnq, cert,
-                                                qbuf, qcnt, slab, tile_margin);
-        else
-          k_icp_nn<Acc><<<nblk, kBS, 0, st>>>(bv, av, aa, src->pts, n_local, ctx->d_state, nnq,
-                                              cert, qbuf, qcnt, slab);
+        k_icp_nn<Acc><<<nblk, kBS, 0, st>>>(bv, av, aa, src->pts, n_local, ctx->d_state, nnq,
+                                            cert, qbuf, qcnt, slab);
         RST_CHECK(mark(1));
         k_icp_fb<Acc><<<fb_grid, kBS, fb_lds, st>>>(bv, av, aa, src->pts, ctx->d_state, nnq, cert,
                                                      qbuf, qcnt, nblk, prm.lane_min, slab, slab2,
-                                                     n_local, qbuf2, qcnt2, wave_max);
-        k_icp_wave<Acc><<<fb_grid, kBS, wave_lds, st>>>(bv, av, aa, src->pts, ctx->d_state, nnq,
-                                                         cert, qbuf, qcnt, nblk, qbuf2, qcnt2,
-                                                         fb_waves, wave_max, slab2, fb_grid, slab3,
-                                                         n_local);
+                                                     n_local);
         return mark(2);
       };
       if (p2plane) {
         RST_CHECK(nn_pass(AccTag<P2PlaneAcc>{}));
-        k_reduce_solve<P2PlaneAcc><<<1, kRedBS, 0, st>>>(slab, 0, slab3, fb_grid, prm,
+        k_reduce_solve<P2PlaneAcc><<<1, kRedBS, 0, st>>>(slab, 0, slab2, fb_grid, prm,
                                                          ctx->d_state, red_out);
       } else if (refsum) {
         RST_CHECK(nn_pass(AccTag<RefAcc>{}));
@@ -1646,7 +1501,7 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
                                                      ctx->d_state, nullptr);
       } else {
         RST_CHECK(nn_pass(AccTag<P2PointAcc>{}));
-        k_reduce_solve<P2PointAcc><<<1, kRedBS, 0, st>>>(slab, 0, slab3, fb_grid, prm,
+        k_reduce_solve<P2PointAcc><<<1, kRedBS, 0, st>>>(slab, 0, slab2, fb_grid, prm,
                                                          ctx->d_state, red_out);
       }
     } else {

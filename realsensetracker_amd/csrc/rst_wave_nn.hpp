@@ -414,9 +414,11 @@ __device__ __forceinline__ Best1 wave_lex_min(Best1 b) {
 // Wave merge of Best2 lists (sorted, distinct ids within each): the merge
 // is commutative, so every lane ends with the same two entries; a point
 // held by both lists (same id) counts once.
+// (kTop = 8: the merge within each row of 16 lanes only)
+template <int kTop = 32>
 __device__ __forceinline__ Best2 wave_lex_min(Best2 b) {
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
+  for (int o = kTop; o > 0; o >>= 1) {
     const float od0 = __shfl_xor(b.d[0], o, 64), od1 = __shfl_xor(b.d[1], o, 64);
     const int oi0 = __shfl_xor(b.id[0], o, 64), oi1 = __shfl_xor(b.id[1], o, 64);
     const int op0 = __shfl_xor(b.pos[0], o, 64), op1 = __shfl_xor(b.pos[1], o, 64);
@@ -957,6 +959,82 @@ __device__ __forceinline__ float nn_wave_adj1(const BvhView& bv, const AdjView& 
   return rc;
 }
 
+// adj_search2 with one query per row of 16 lanes (lanes 16g .. 16g+15 hold the same query q and the same seeds r), four
+// queries per wavefront.  The warm leaf's 24 adjacency entries are tested
+// by the row at once (lane k: entries k and k + 16), the candidates' point
+// ranges compacted in LDS (`tags`, 24 ints per row), and each lane takes
+// one point of every candidate leaf (a leaf holds <= 16), all loads in
+// flight before the offers; a row merge then leaves every lane of the row
+// with the row's two nearest.  Candidates are tested against the seeds'
+// second bound (the sequential scan tightens it as it goes: this tests a
+// superset).  Returns the covered radius Rc exactly as adj_search2: r.first()
+// is exact when sqrt(d[0]) < Rc, min(r2, Rc) bounds every other point.
+// Rows with act == false take no part in the loads (their result is
+// meaningless); the whole wavefront must call it.
+__device__ __forceinline__ float row_adj2(const BvhView& bv, const AdjView& av, bool act, int warm,
+                                          float qx, float qy, float qz, Best2& r, int* tags) {
+  const int lane = __lane_id();
+  const int sub = lane & 15;
+  const int nl = bv.nleaves;
+  const int L = act ? leaf_of(bv, warm) : 0;
+  float4 l0 = make_float4(0.f, 0.f, 0.f, 0.f), h0 = l0, l1 = l0, h1 = l0;
+  int t0 = -1, t1 = -1;
+  if (act) {
+    const float4* e = av.ent + (int64_t)L * kAdjK * 2;
+    l0 = e[2 * sub];
+    h0 = e[2 * sub + 1];
+    t0 = f2i(h0.w);
+    if (sub < kAdjK - 16) {
+      l1 = e[2 * (sub + 16)];
+      h1 = e[2 * (sub + 16) + 1];
+      t1 = f2i(h1.w);
+    }
+  }
+  float4 nlo = l0, nhi = l0;
+  float reach = 0.f;
+  if (act) {
+    nlo = bv.nodes[2 * (nl + L)];
+    nhi = bv.nodes[2 * (nl + L) + 1];
+    reach = av.reach[L];
+  }
+  // the margins of adj_search2
+  const float dl = margin_sqrt(box_d2(qx, qy, qz, nlo, nhi)) * 1.00001f;
+  const float rc = reach * 0.99999f - dl;
+  const bool cov = act && dl + margin_sqrt(r.d[0]) * 1.00001f + 1e-30f < reach * 0.99999f;
+  const float rad = margin_sqrt(r.d[1]) * 1.00001f + 1e-30f;
+  const bool c0 = cov && t0 >= 0 && !(l0.w * 0.99999f - dl > rad) && box_d2(qx, qy, qz, l0, h0) <= r.d[1];
+  const bool c1 = cov && t1 >= 0 && !(l1.w * 0.99999f - dl > rad) && box_d2(qx, qy, qz, l1, h1) <= r.d[1];
+  const int sh = lane & ~15;
+  const uint32_t m0 = (uint32_t)(__ballot(c0) >> sh) & 0xffffu;
+  const uint32_t m1 = (uint32_t)(__ballot(c1) >> sh) & 0xffffu;
+  const uint32_t below = (1u << sub) - 1u;
+  if (c0) tags[__popc(m0 & below)] = t0;
+  if (c1) tags[__popc(m0) + __popc(m1 & below)] = t1;
+  wave_sync();
+  const int nc = __popc(m0) + __popc(m1);
+  Best2 mine = r;
+  const int last = bv.m - 1;
+  for (int c0i = 0; c0i < nc; c0i += 8) {
+    float4 p[8];
+    int pos[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      pos[k] = -1;
+      if (c0i + k < nc) {
+        const int tg = tags[c0i + k];
+        if (sub < (tg & 31)) pos[k] = (tg >> 5) + sub;
+      }
+      p[k] = bv.pts[pos[k] >= 0 ? pos[k] : last];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (pos[k] >= 0) mine.offer(d2_ref(qx, qy, qz, p[k].x, p[k].y, p[k].z), f2i(p[k].w), pos[k]);
+  }
+  r = wave_lex_min<8>(mine);
+  wave_sync();
+  return rc;
+}
+
 // The certificate bound of adj_search2's result (0: none): min(r2, Rc)
 // with the 1e-5 relative margins of every distance test here.
 RST_HD float cert_bound(const Best2& r, float rc) {
@@ -965,132 +1043,9 @@ RST_HD float cert_bound(const Best2& r, float rc) {
   return g > 0.f ? g : 0.f;
 }
 
-// ---- LDS-staged target tiles (the cold iterations of an ICP pair) -------------------
-// A wavefront's 64 Morton-consecutive queries cover one compact patch.  The
-// target points inside the patch's bounding box grown by a margin are
-// staged in LDS once (a top-down BVH range query, 64 nodes per round, then
-// the listed leaves' points, 16 lanes per leaf), and every lane scans the
-// whole tile from LDS (broadcast reads: all lanes read the same point).
-// For a query q inside the box the tile holds every target point within
-// Mq = dist(q, outside of the grown box); so its tile minimum is its exact
-// nearest neighbour when that lies closer than Mq, and min(second, Mq)
-// bounds every other point -- the certificate.
-constexpr int kTileStack = 384;  // node ids
-constexpr int kTileLeaves = 64;  // staged leaves
-constexpr int kTilePts = 768;    // staged points
-struct TileScratch {             // per-wave LDS (~16 KB)
-  float4 pts[kTilePts];          // x, y, z, original index bits
-  int pos[kTilePts];             // sorted position
-  int stack[kTileStack];
-  int leaves[kTileLeaves];
-};
-
 __device__ __forceinline__ bool box_meets(const float4& lo, const float4& hi, float lx, float ly,
                                           float lz, float hx, float hy, float hz) {
   return lo.x <= hx && hi.x >= lx && lo.y <= hy && hi.y >= ly && lo.z <= hz && hi.z >= lz;
-}
-
-// Stage the target points inside [l, h] (per-axis bounds) in ts; returns
-// their count, or -1 when they do not fit (the caller falls back; -2: an
-// index guard tripped, never expected).  The whole wave must call it
-// (converged).
-__device__ __forceinline__ int tile_stage(const BvhView& bv, float lx, float ly, float lz, float hx,
-                                          float hy, float hz, TileScratch& ts) {
-  const int lane = __lane_id();
-  const int nl = bv.nleaves;
-  const uint64_t lt = (1ull << lane) - 1ull;
-  if (lane == 0) ts.stack[0] = 1;
-  int sp = 1, ns = 0;
-  bool over = false;
-  wave_sync();
-  while (sp > 0) {
-    const int k = min(kWave, sp);
-    int node = 0;
-    if (lane < k) node = ts.stack[sp - 1 - lane];
-    sp -= k;
-    wave_sync();
-    bool pass = false;
-    if (__ballot(lane < k && (node < 1 || node >= 2 * nl)) != 0) return -2;  // index guard
-    if (lane < k) {
-      const float4 lo = bv.nodes[2 * node], hi = bv.nodes[2 * node + 1];
-      pass = box_meets(lo, hi, lx, ly, lz, hx, hy, hz);
-    }
-    const bool isleaf = node >= nl;
-    const uint64_t im = __ballot(pass && !isleaf), lm = __ballot(pass && isleaf);
-    const int ni = __popcll(im), nlv = __popcll(lm);
-    if (sp + 2 * ni > kTileStack || ns + nlv > kTileLeaves) {
-      over = true;
-      break;
-    }
-    if (pass && !isleaf) {
-      const int rk = __popcll(im & lt);
-      ts.stack[sp + 2 * rk] = 2 * node;
-      ts.stack[sp + 2 * rk + 1] = 2 * node + 1;
-    }
-    if (pass && isleaf) ts.leaves[ns + __popcll(lm & lt)] = node - nl;
-    sp += 2 * ni;
-    ns += nlv;
-    wave_sync();
-  }
-  if (over) return -1;
-  // leaf point ranges -> LDS offsets (exclusive scan over <= 64 leaves)
-  int b = 0, c = 0;
-  if (lane < ns) {
-    const int L = ts.leaves[lane];
-    b = leaf_begin(bv, L);
-    c = leaf_begin(bv, L + 1) - b;
-  }
-  int inc = c;
-#pragma unroll
-  for (int o = 1; o < kWave; o <<= 1) {
-    const int y = __shfl_up(inc, o, kWave);
-    if (lane >= o) inc += y;
-  }
-  const int total = __shfl(inc, kWave - 1, kWave);
-  if (total > kTilePts) return -1;
-  const int off = inc - c;
-  const int g = lane >> 4, o = lane & 15;
-  for (int k0 = 0; k0 < ns; k0 += 4) {  // one leaf per 16 lanes
-    const int kk = k0 + g;
-    const int lb = __shfl(b, kk & 63, kWave), lc = __shfl(c, kk & 63, kWave);
-    const int lo = __shfl(off, kk & 63, kWave);
-    if (kk < ns && o < lc) {
-      ts.pts[lo + o] = bv.pts[lb + o];
-      ts.pos[lo + o] = lb + o;
-    }
-  }
-  wave_sync();
-  return total;
-}
-
-// The two nearest of (qx, qy, qz) among the ns staged points
-// (lexicographic (d2, original index), as every search here).
-__device__ __forceinline__ void tile_scan(const TileScratch& ts, int ns, float qx, float qy,
-                                          float qz, Best2& r) {
-  uint64_t k0 = ((uint64_t)(uint32_t)f2i(r.d[0]) << 32) | (uint32_t)r.id[0];
-  uint64_t k1 = ((uint64_t)(uint32_t)f2i(r.d[1]) << 32) | (uint32_t)r.id[1];
-  int j0 = -1, j1 = -1;
-  for (int j = 0; j < ns; ++j) {
-    const float4 p = ts.pts[j];
-    const float d2 = d2_ref(qx, qy, qz, p.x, p.y, p.z);
-    const uint64_t key = ((uint64_t)(uint32_t)f2i(d2) << 32) | (uint32_t)f2i(p.w);
-    const bool in = (key != k0) & (key < k1);
-    const bool first = in & (key < k0);
-    k1 = first ? k0 : (in ? key : k1);
-    j1 = first ? j0 : (in ? j : j1);
-    k0 = first ? key : k0;
-    j0 = first ? j : j0;
-  }
-  if (j0 >= 0) {
-    r.d[0] = i2f((int)(uint32_t)(k0 >> 32));
-    r.id[0] = (int)(uint32_t)k0;
-    r.pos[0] = ts.pos[j0];
-  }
-  if (j1 >= 0) {
-    r.d[1] = i2f((int)(uint32_t)(k1 >> 32));
-    r.id[1] = (int)(uint32_t)k1;
-    r.pos[1] = ts.pos[j1];
-  }
 }
 
 // ---- ball tiles: the cold iterations' wave-shared search --------------------------------

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Per-iteration kernel profile (one pair in flight) of the default library
 # under each environment setting given ("NAME=V,NAME2=V2" per setting):
-#   TAG=x bash tools/gpu_sweep_env.sh RST_COLD_ITERS=0 "RST_COLD_ITERS=4,RST_TILE_MARGIN=0.04"
+#   TAG=x bash tools/gpu_sweep_env.sh RST_LANE_MIN_DIV=3 "RST_LANE_MIN_DIV=4,RST_FB_BLOCKS=2048"
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
