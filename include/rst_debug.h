@@ -25,6 +25,11 @@ int rst_debug_query_nn_warm_stats(rst_ctx* ctx, const rst_target* tgt, const flo
  * solve kernel's reduction and solve times (10 ns ticks). */
 int rst_debug_queue_trace(rst_ctx* ctx, int32_t* out, int32_t n);
 
+/* RST_DIAG builds, per iteration of the last align call on ctx (first n <=
+ * 256), 4 int32: far-queue length, ball-tile chunks scanned (all waves),
+ * ball-tile walks abandoned, deep (whole-wave) searches.  Zeros otherwise. */
+int rst_debug_iter_diag(rst_ctx* ctx, int32_t* out, int32_t n);
+
 /* The ICP loop's fallback search (one wavefront per query) on a host batch:
  * mode 0 = full walk from the warm leaf, 2 / 3 = level-2 / level-3
  * adjacency first, 23 = both then the walk.  warm = original target indices
@@ -49,6 +54,28 @@ int rst_debug_seq_sum4(rst_ctx* ctx, const float* xyzw, int64_t n, float out[4])
  * pleaf is not NULL; *nleaves receives the leaf count either way. */
 int rst_debug_target_leaves(rst_ctx* ctx, const rst_target* tgt, int32_t* lstart, int32_t cap,
                             int32_t* pleaf, int32_t* nleaves);
+
+/* The two halves of one sharded ICP iteration (rst_icp_align_sharded_device
+ * runs them with an RCCL all-reduce between), for testing the shard
+ * decomposition without a second GPU.
+ *
+ * rst_debug_icp_partials: the partial sums of source shard `src` against
+ * tgt at the given state (pose column-major 4x4, mu, the WHOLE source's
+ * centroid smean, iteration index `iter`): exact NN of every shard point,
+ * then the fixed-order reduction -- the vector a rank contributes to the
+ * all-reduce.  *nv receives its length (16 for RST_P2POINT_REF, 30 for
+ * RST_P2PLANE); out holds >= 32 doubles.  RST_P2POINT_REF needs sum_mode
+ * RST_SUM_FP64 (sequential sums have no shard decomposition: RST_E_ARG).
+ *
+ * rst_debug_icp_solve: the solve step every rank runs on the all-reduced
+ * vector (n_total = points of all shards): state in -> the next pose, mu and
+ * iteration count out, exactly as the loop's k_solve_only. */
+int rst_debug_icp_partials(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
+                           const rst_icp_opts* opts, const float pose[16], float mu,
+                           const float smean[3], int32_t iter, double* out, int32_t* nv);
+int rst_debug_icp_solve(rst_ctx* ctx, const rst_icp_opts* opts, int64_t n_total,
+                        const double* totals, const float smean[3], float pose_inout[16],
+                        float* mu_inout, int32_t* iter_inout);
 
 #ifdef __cplusplus
 }

@@ -536,6 +536,29 @@ int rst_debug_seq_sum4(rst_ctx* ctx, const float* xyzw, int64_t n, float out[4])
   return s;
 }
 
+int rst_debug_icp_partials(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
+                           const rst_icp_opts* opts, const float pose[16], float mu,
+                           const float smean[3], int32_t iter, double* out, int32_t* nv) {
+  if (!ctx) return RST_E_ARG;
+  RST_HIP(hipSetDevice(ctx->device));
+  return icp_debug_partials(ctx, src, tgt, opts, pose, mu, smean, iter, out, nv);
+}
+
+int rst_debug_icp_solve(rst_ctx* ctx, const rst_icp_opts* opts, int64_t n_total,
+                        const double* totals, const float smean[3], float pose_inout[16],
+                        float* mu_inout, int32_t* iter_inout) {
+  if (!ctx) return RST_E_ARG;
+  RST_HIP(hipSetDevice(ctx->device));
+  return icp_debug_solve(ctx, opts, n_total, totals, smean, pose_inout, mu_inout, iter_inout);
+}
+
+int rst_debug_iter_diag(rst_ctx* ctx, int32_t* out, int32_t n) {
+  if (!ctx || !out || n < 0) return RST_E_ARG;
+  for (int i = 0; i < n && i < kQTrace; ++i)
+    for (int j = 0; j < 4; ++j) out[4 * i + j] = ctx->h_state->diag[i][j];
+  return RST_OK;
+}
+
 int rst_debug_queue_trace(rst_ctx* ctx, int32_t* out, int32_t n) {
   if (!ctx || !out || n < 0) return RST_E_ARG;
   for (int i = 0; i < n && i < kQTrace; ++i) {

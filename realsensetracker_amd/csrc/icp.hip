@@ -228,7 +228,7 @@ __global__ __launch_bounds__(kBS) void k_init_state(const double* __restrict__ c
     st->iter = 0;
     for (int k = 0; k < kQTrace; ++k) {
       st->qlen[k] = 0;
-      for (int j = 0; j < 4; ++j) st->path[k][j] = 0;
+      for (int j = 0; j < 4; ++j) st->path[k][j] = st->diag[k][j] = 0;
     }
     st->done = 0;
     st->fail = 0;
@@ -1031,6 +1031,9 @@ __global__ __launch_bounds__(kBS, Acc::kFbMinWaves) void k_icp_fb(BvhView bv, Ad
   queue_prefix(qcntf, nb1, preff, nullptr);
   __syncthreads();
   const int E = pref[nb1], EF = preff[nb1];
+#if RST_DIAG
+  if (blockIdx.x == 0 && threadIdx.x == 0 && st->iter < kQTrace) st->diag[st->iter][0] = EF;
+#endif
   double v[Acc::NV];
 #pragma unroll
   for (int k = 0; k < Acc::NV; ++k) v[k] = 0.0;
@@ -1109,14 +1112,23 @@ __global__ __launch_bounds__(kBS, Acc::kFbMinWaves) void k_icp_fb(BvhView bv, Ad
         // cold: the wave's queries share one branch-and-bound walk
         float mq = 0.f;
         const bool act = has && fin;
-        int gfail = 0;
+        int gfail = 0, chunks = 0;
         int4 gdet = make_int4(0, 0, 0, 0);
-        if (ball_tile_search(bv, act, px, py, pz, r2, mq, scr[wid].b, gfail, gdet)) {
-          if (act) {
-            g = fminf(r2.d[1] < FLT_MAX ? margin_sqrt(r2.d[1]) * 0.99999f : FLT_MAX, mq);
-            exact = true;
-          }
+        const bool done =
+            ball_tile_search(bv, act, px, py, pz, r2, mq, scr[wid].b, gfail, gdet, chunks);
+        // exact: the lane's own ball built the final box (uncapped), or its
+        // first lies inside the box anyway
+        const float u0 = margin_sqrt(r2.d[0]) * 1.00001f + 4e-6f;  // ball_box's radius
+        if (done && act && (u0 <= RST_BALL_CAP || u0 < mq)) {
+          g = fminf(r2.d[1] < FLT_MAX ? margin_sqrt(r2.d[1]) * 0.99999f : FLT_MAX, mq);
+          exact = true;
         }
+#if RST_DIAG
+        if (lane == 0 && st->iter < kQTrace) {
+          atomicAdd(&st->diag[st->iter][1], chunks);
+          if (!done) atomicAdd(&st->diag[st->iter][2], 1);
+        }
+#endif
         if (gfail && lane == 0) {
           if (atomicOr(&st->guard, 8 * gfail) == 0) {
             st->path[kQTrace - 1][0] = gdet.x;
@@ -1222,6 +1234,9 @@ __global__ __launch_bounds__(kBS, Acc::kFbMinWaves) void k_icp_fb(BvhView bv, Ad
       }
       bool far = true;
       const float gj = deep_search(bv, av, try1, px, py, pz, rr, scr[wid].w, far);
+#if RST_DIAG
+      if (lane == 0 && st->iter < kQTrace) atomicAdd(&st->diag[st->iter][3], 1);
+#endif
       if (lane == 0) fb_record<Acc>(v, bv, aa, u, nnq, cert, di, s, px, py, pz, rr, gj, far);
     }
   }
@@ -1307,6 +1322,42 @@ int centroid_device(rst_ctx* ctx, const float4* d_pts, int64_t n, double* d_out)
 // on a single GPU); icp_finish waits and reads the result.  Returns RST_OK
 // when enqueued, RST_FALSE for the reference's early false (nothing
 // enqueued), or an error.
+// fallback grid (RST_FB_BLOCKS: tuning knob, <= kFbBlocks)
+static int fb_grid_size() {
+  static const int g = [] {
+    const char* e = getenv("RST_FB_BLOCKS");
+    const int v = e ? atoi(e) : kFbDefault;
+    return (v >= 1 && v <= kFbBlocks) ? v : kFbBlocks;
+  }();
+  return g;
+}
+
+static IcpParams make_params(const rst_icp_opts& opts, int64_t n_total, int64_t n_local) {
+  IcpParams prm;
+  prm.n = n_total;
+  prm.anneal_every = opts.anneal_every;
+  prm.anneal_div = opts.anneal_div;
+  prm.p2plane_eps = opts.p2plane_eps;
+  prm.p2plane_mu = opts.p2plane_mu;
+  prm.p2plane_max_d2 = opts.p2plane_max_dist > 0 ? opts.p2plane_max_dist * opts.p2plane_max_dist
+                                                 : FLT_MAX;
+  prm.max_iter = opts.max_iter;
+  prm.sum_mode = opts.sum_mode;
+  // queue length from which the fallback runs one lane per query
+  // (RST_LANE_MIN_DIV = k: n / k; tuning knob -- r01h sweep: 3n/4 was best;
+  // r01j, with queued lanes seeding the fallback: n/3 17.0k, n/4 17.1k, n/2
+  // 16.8k, 3n/4 16.6k it/s on the 640x480 stream, the 720p pyramid 14.0k /
+  // 13.9k / 14.0k / 14.25k)
+  static const int lane_div = [] {
+    const char* e = getenv("RST_LANE_MIN_DIV");
+    return e ? atoi(e) : 0;
+  }();
+  prm.lane_min = (int)std::max<int64_t>(
+      16384, lane_div > 0 ? n_local / lane_div
+                          : (n_local < RST_LANE_SMALL_N ? (3 * n_local) / 4 : n_local / 3));
+  return prm;
+}
+
 int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
                const rst_icp_opts* opts_in, const float pose_in[16], rst_comm* comm,
                bool chain, int level) {
@@ -1422,35 +1473,8 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
   const AdjView av = adj_of(tgt);
   const size_t fb_lds = 2 * sizeof(int) * ((size_t)nblk + 1);
 
-  // fallback grid (RST_FB_BLOCKS: tuning knob, <= kFbBlocks)
-  static const int fb_grid = [] {
-    const char* e = getenv("RST_FB_BLOCKS");
-    const int v = e ? atoi(e) : kFbDefault;
-    return (v >= 1 && v <= kFbBlocks) ? v : kFbBlocks;
-  }();
-
-  IcpParams prm;
-  prm.n = n_total;
-  prm.anneal_every = opts.anneal_every;
-  prm.anneal_div = opts.anneal_div;
-  prm.p2plane_eps = opts.p2plane_eps;
-  prm.p2plane_mu = opts.p2plane_mu;
-  prm.p2plane_max_d2 = opts.p2plane_max_dist > 0 ? opts.p2plane_max_dist * opts.p2plane_max_dist
-                                                 : FLT_MAX;
-  prm.max_iter = opts.max_iter;
-  prm.sum_mode = opts.sum_mode;
-  // queue length from which the fallback runs one lane per query
-  // (RST_LANE_MIN_DIV = k: n / k; tuning knob -- r01h sweep: 3n/4 was best;
-  // r01j, with queued lanes seeding the fallback: n/3 17.0k, n/4 17.1k, n/2
-  // 16.8k, 3n/4 16.6k it/s on the 640x480 stream, the 720p pyramid 14.0k /
-  // 13.9k / 14.0k / 14.25k)
-  static const int lane_div = [] {
-    const char* e = getenv("RST_LANE_MIN_DIV");
-    return e ? atoi(e) : 0;
-  }();
-  prm.lane_min = (int)std::max<int64_t>(
-      16384, lane_div > 0 ? n_local / lane_div
-                          : (n_local < RST_LANE_SMALL_N ? (3 * n_local) / 4 : n_local / 3));
+  const int fb_grid = fb_grid_size();
+  const IcpParams prm = make_params(opts, n_total, n_local);
 
   const BvhView bv = view_of(tgt);
   const bool timing = ctx->timing && opts.max_iter > 0;
@@ -1616,6 +1640,143 @@ int icp_finish(rst_ctx* ctx, float pose_inout[16], float* mean_cost, int32_t* it
   if (mean_cost) *mean_cost = mc;
   if (pd.p2plane) return RST_OK;
   return (mc < 10000.0f) ? RST_OK : RST_FALSE;  // :160 (NaN -> false)
+}
+
+// ---- diagnostics: the sharded loop's two halves (rst_debug.h) ------------------------
+// The state a sharded iteration starts from: pose, mu, source centroid and
+// iteration count set directly (k_init_state, then these).
+__global__ void k_debug_state(IcpState* __restrict__ st, const float* __restrict__ smean, float mu,
+                              int iter) {
+  if (threadIdx.x != 0) return;
+  for (int r = 0; r < 3; ++r) st->smean[r] = smean[r];
+  st->mu = mu;
+  st->iter = iter;
+}
+
+int icp_debug_partials(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
+                       const rst_icp_opts* opts_in, const float pose[16], float mu,
+                       const float smean[3], int32_t iter, double* out, int32_t* nv) {
+  if (!ctx || !src || !tgt || !pose || !smean || !out || !nv) return RST_E_ARG;
+  rst_icp_opts opts;
+  if (opts_in)
+    opts = *opts_in;
+  else
+    rst_icp_opts_default(&opts);
+  const bool p2plane = opts.mode == RST_P2PLANE;
+  if (opts.mode != RST_P2POINT_REF && opts.mode != RST_P2PLANE) return RST_E_ARG;
+  if (!p2plane && opts.sum_mode != RST_SUM_FP64) return RST_E_ARG;  // no shard decomposition
+  if (!tgt->has_bvh || tgt->m < 1 || tgt->m >= kCertBit) return RST_E_ARG;
+  if (p2plane && !tgt->nrm) return RST_E_STATE;
+  const int64_t n = src->m;
+  *nv = p2plane ? kNP2Plane : kNP2Point;
+  hipStream_t st = ctx->stream;
+  const int nblk = blocks_for(n);
+  if (2 * sizeof(int) * ((size_t)nblk + 1) > (size_t)96 * 1024) return RST_E_ARG;
+  const int RS = p2plane ? P2PlaneAcc::RS : P2PointAcc::RS;
+  const int fb_grid = fb_grid_size();
+  double* slab = nullptr;
+  RST_CHECK(ctx_slab(ctx, sizeof(double) * ((size_t)nblk * RS + (size_t)kFbBlocks * RS + 64), &slab));
+  double* slab2 = slab + (size_t)nblk * RS;
+  double* totals = slab2 + (size_t)kFbBlocks * RS;
+  void* w = nullptr;
+  const size_t np = (size_t)std::max<int64_t>(n, 1), nq = (size_t)nblk * kBS;
+  RST_CHECK(ctx_workspace(ctx, sizeof(float4) * np * 2 + sizeof(int32_t) * (2 * nq + 2 * nblk + 64), &w));
+  float4* cert = (float4*)w;
+  float4* nnq = cert + np;
+  int32_t* qbuf = (int32_t*)(cert + 2 * np);
+  int32_t* qcnt = qbuf + 2 * nq;
+  RST_HIP(hipMemsetAsync(nnq, 0xff, sizeof(float4) * np, st));
+  InitArgs ia;
+  memcpy(ia.pose, pose, sizeof(ia.pose));
+  ia.mu0 = mu;
+  ia.need_centroid = 0;
+  ia.chain = 0;
+  ia.n = n;
+  k_init_state<<<1, kBS, 0, st>>>(slab, 0, nullptr, ia, ctx->d_state);
+  float* dsm = (float*)(totals + 48);
+  RST_HIP(hipMemcpyAsync(dsm, smean, sizeof(float) * 3, hipMemcpyHostToDevice, st));
+  k_debug_state<<<1, 64, 0, st>>>(ctx->d_state, dsm, mu, iter);
+  AccArgs aa;
+  aa.corr = nullptr;
+  aa.nrm = tgt->nrm;
+  aa.pmu = opts.p2plane_mu;
+  aa.max_d2 = opts.p2plane_max_dist > 0 ? opts.p2plane_max_dist * opts.p2plane_max_dist : FLT_MAX;
+  aa.pos0 = tgt->pos0;
+  const IcpParams prm = make_params(opts, n, n);
+  const BvhView bv = view_of(tgt);
+  const AdjView av = adj_of(tgt);
+  const size_t fb_lds = 2 * sizeof(int) * ((size_t)nblk + 1);
+  auto pass = [&](auto tag) {
+    using Acc = typename decltype(tag)::type;
+    if (n > 0) {
+      k_icp_nn<Acc><<<nblk, kBS, 0, st>>>(bv, av, aa, src->pts, n, ctx->d_state, nnq, cert, qbuf,
+                                          qcnt, slab);
+      k_icp_fb<Acc><<<fb_grid, kBS, fb_lds, st>>>(bv, av, aa, src->pts, ctx->d_state, nnq, cert,
+                                                   qbuf, qcnt, nblk, prm.lane_min, slab, slab2, n);
+      k_reduce_solve<Acc><<<1, kRedBS, 0, st>>>(slab, 0, slab2, fb_grid, prm, ctx->d_state, totals);
+    } else {
+      (void)hipMemsetAsync(totals, 0, sizeof(double) * Acc::NV, st);
+    }
+  };
+  if (p2plane)
+    pass(AccTag<P2PlaneAcc>{});
+  else
+    pass(AccTag<P2PointAcc>{});
+  RST_HIP(hipGetLastError());
+  RST_HIP(hipMemcpyAsync(out, totals, sizeof(double) * *nv, hipMemcpyDeviceToHost, st));
+  RST_HIP(hipMemcpyAsync(ctx->h_state, ctx->d_state, sizeof(IcpState), hipMemcpyDeviceToHost, st));
+  RST_HIP(hipStreamSynchronize(st));
+  if (ctx->h_state->guard) {
+    set_last_error(hipErrorIllegalAddress, "ICP index guard (partials)", __FILE__, __LINE__);
+    return RST_E_HIP;
+  }
+  return RST_OK;
+}
+
+int icp_debug_solve(rst_ctx* ctx, const rst_icp_opts* opts_in, int64_t n_total,
+                    const double* totals, const float smean[3], float pose_inout[16],
+                    float* mu_inout, int32_t* iter_inout) {
+  if (!ctx || !totals || !smean || !pose_inout || !mu_inout || !iter_inout) return RST_E_ARG;
+  rst_icp_opts opts;
+  if (opts_in)
+    opts = *opts_in;
+  else
+    rst_icp_opts_default(&opts);
+  const bool p2plane = opts.mode == RST_P2PLANE;
+  if (opts.mode != RST_P2POINT_REF && opts.mode != RST_P2PLANE) return RST_E_ARG;
+  const int nv = p2plane ? kNP2Plane : kNP2Point;
+  hipStream_t st = ctx->stream;
+  double* buf = nullptr;
+  RST_CHECK(ctx_slab(ctx, sizeof(double) * 64, &buf));
+  RST_HIP(hipMemcpyAsync(buf, totals, sizeof(double) * nv, hipMemcpyHostToDevice, st));
+  float* dsm = (float*)(buf + 48);
+  RST_HIP(hipMemcpyAsync(dsm, smean, sizeof(float) * 3, hipMemcpyHostToDevice, st));
+  InitArgs ia;
+  memcpy(ia.pose, pose_inout, sizeof(ia.pose));
+  ia.mu0 = *mu_inout;
+  ia.need_centroid = 0;
+  ia.chain = 0;
+  ia.n = n_total;
+  k_init_state<<<1, kBS, 0, st>>>(buf, 0, nullptr, ia, ctx->d_state);
+  k_debug_state<<<1, 64, 0, st>>>(ctx->d_state, dsm, *mu_inout, *iter_inout);
+  const IcpParams prm = make_params(opts, n_total, n_total);
+  if (p2plane)
+    k_solve_only<P2PlaneAcc><<<1, 64, 0, st>>>(buf, prm, ctx->d_state);
+  else
+    k_solve_only<P2PointAcc><<<1, 64, 0, st>>>(buf, prm, ctx->d_state);
+  RST_HIP(hipGetLastError());
+  RST_HIP(hipMemcpyAsync(ctx->h_state, ctx->d_state, sizeof(IcpState), hipMemcpyDeviceToHost, st));
+  RST_HIP(hipStreamSynchronize(st));
+  const IcpState& h = *ctx->h_state;
+  for (int c = 0; c < 3; ++c) {
+    for (int r = 0; r < 3; ++r) pose_inout[c * 4 + r] = h.R[c * 3 + r];
+    pose_inout[c * 4 + 3] = 0.f;
+  }
+  for (int r = 0; r < 3; ++r) pose_inout[12 + r] = h.t[r];
+  pose_inout[15] = 1.f;
+  *mu_inout = h.mu;
+  *iter_inout = h.iter;
+  return RST_OK;
 }
 
 int icp_align_prepared(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,

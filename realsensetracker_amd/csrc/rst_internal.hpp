@@ -77,6 +77,7 @@ struct IcpState : IcpCore {
                           // level that fails chains this on (host semantics)
   int32_t qlen[kQTrace];  // fallback-queue length per iteration (diagnostics)
   int32_t path[kQTrace][4];  // per-iteration diagnostics (rst_debug_queue_trace)
+  int32_t diag[kQTrace][4];  // RST_DIAG builds: far queue, ball chunks, ball aborts, deep searches
 };
 
 struct IcpParams {
@@ -202,6 +203,13 @@ int compute_grid_normals(rst_ctx* ctx, rst_target* tgt, int r, const float vp[3]
 int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
                const rst_icp_opts* opts, const float pose_in[16], rst_comm* comm,
                bool chain = false, int level = 0);
+// diagnostics (rst_debug.h): one iteration's partial sums; the solve step
+int icp_debug_partials(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
+                       const rst_icp_opts* opts, const float pose[16], float mu,
+                       const float smean[3], int32_t iter, double* out, int32_t* nv);
+int icp_debug_solve(rst_ctx* ctx, const rst_icp_opts* opts, int64_t n_total,
+                    const double* totals, const float smean[3], float pose_inout[16],
+                    float* mu_inout, int32_t* iter_inout);
 int icp_finish(rst_ctx* ctx, float pose_inout[16], float* mean_cost, int32_t* iters_run);
 int icp_align_prepared(rst_ctx* ctx, const rst_target* src,
                        const rst_target* tgt, const rst_icp_opts* opts,

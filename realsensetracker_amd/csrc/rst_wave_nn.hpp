@@ -1059,15 +1059,19 @@ __device__ __forceinline__ bool box_meets(const float4& lo, const float4& hi, fl
 // shrink to the lanes' new first distances (branch and bound for the whole
 // wave).  A node is dropped only when it misses the current B, which holds
 // every later B, so every target point inside the final B is scanned: each
-// lane's first is exact (its ball lies in B), and the distance Mq from q_i
-// to the outside of the final B bounds every unscanned point -- with the
-// second distance, the certificate min(r2, Mq).  Returns false (lanes keep a
+// distance Mq from q_i to the outside of the final B bounds every unscanned
+// point: the lane's first is exact when it lies within Mq (always, unless
+// the RST_BALL_CAP cap kept its ball out of B), and min(r2, Mq) is its
+// certificate.  Returns false (lanes keep a
 // valid but unfinished r) when the walk exceeds kBallMaxChunks chunks: the
 // caller finishes those lanes alone.
 constexpr int kBallChunk = 512;    // staged points per scan
 constexpr int kBallLeaves = 128;   // collected leaves (a round adds <= 64)
 constexpr int kBallStack = 320;    // node ids
-constexpr int kBallMaxChunks = 24;
+#ifndef RST_BALL_MAX_CHUNKS
+#define RST_BALL_MAX_CHUNKS 48
+#endif
+constexpr int kBallMaxChunks = RST_BALL_MAX_CHUNKS;
 struct BallScratch {               // per-wave LDS (~12.5 KB)
   float4 pts[kBallChunk];          // x, y, z, original index bits
   int pos[kBallChunk];             // sorted position
@@ -1088,10 +1092,18 @@ __device__ __forceinline__ float wave_max_f(float x) {
 }
 
 // The box of the active lanes' balls (radius: the first distance, rounded
-// up by the 1e-5 margins of every coverage test here).
+// up by the 1e-5 margins of every coverage test here, capped at
+// RST_BALL_CAP metres: a lane whose ball the box does not hold is answered
+// only if its first ends up inside the box -- the caller checks -- so the
+// cap bounds the work, never the exactness).
+#ifndef RST_BALL_CAP
+#define RST_BALL_CAP 0.10f  // r02z2: 0.10 m / 48 chunks 13.90 ms per pair, uncapped / 24 14.06
+#endif
 __device__ __forceinline__ void ball_box(bool act, float qx, float qy, float qz, const Best2& r,
                                          float4& lo, float4& hi) {
-  const float u = act ? margin_sqrt(r.d[0]) * 1.00001f + 1e-30f : 0.f;
+  // (+4 um: the box corners q -/+ u round to float at up to ~1 ulp of the
+  // coordinates, < 4 um for |q| < 32 m)
+  const float u = act ? fminf(margin_sqrt(r.d[0]) * 1.00001f + 4e-6f, RST_BALL_CAP) : 0.f;
   lo.x = wave_min_f(act ? qx - u : FLT_MAX);
   lo.y = wave_min_f(act ? qy - u : FLT_MAX);
   lo.z = wave_min_f(act ? qz - u : FLT_MAX);
@@ -1183,17 +1195,20 @@ __device__ __forceinline__ int ball_flush(const BvhView& bv, BallScratch& ts, in
 
 // act: the lane holds a query (r: its seeds, r.d[0] finite); inactive lanes
 // only help.  On true, Mq (per active lane) = the distance from q to the
-// outside of the final box, margins applied.  The whole wave calls it.
+// outside of the final box, margins applied: the lane's first is exact when
+// it lies within Mq (every point inside the box was scanned).  The whole
+// wave calls it.
 __device__ __forceinline__ bool ball_tile_search(const BvhView& bv, bool act, float qx, float qy,
                                                  float qz, Best2& r, float& mq, BallScratch& ts,
-                                                 int& gfail, int4& det) {
+                                                 int& gfail, int4& det, int& chunks) {
   const int lane = __lane_id();
   const int nl = bv.nleaves;
   const uint64_t lt = (1ull << lane) - 1ull;
   float4 lo, hi;
   ball_box(act, qx, qy, qz, r, lo, hi);
   if (lane == 0) ts.stack[0] = 1;
-  int sp = 1, nlv = 0, chunks = 0;
+  int sp = 1, nlv = 0;
+  chunks = 0;
   wave_sync();
   while (sp > 0 || nlv > 0) {
     if (sp > 0 && nlv <= kBallLeaves - kWave && sp <= kBallStack - 2 * kWave) {

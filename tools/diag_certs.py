@@ -27,8 +27,14 @@ for sm in (L.RST_SUM_FP64,):
     r = A.align_prepared(fb, fa, None, L.default_opts(sum_mode=sm))
     q = np.zeros((256, 5), np.int32)
     qt(ctx.handle, L.iptr(q), 256)
-    print(f"n={n} ok={r.ok}; iter: queue certified adj-exact (fractions of n), "
-          "solve kernel: reduce us, solve us")
+    dg = np.zeros((256, 4), np.int32)
+    dd = lib.rst_debug_iter_diag
+    dd.restype = C.c_int
+    dd.argtypes = [C.c_void_p, L.c_int32_p, C.c_int32]
+    dd(ctx.handle, L.iptr(dg), 256)
+    print(f"n={n} ok={r.ok}; iter: near-queue certified adj-exact (fractions of n), "
+          "solve kernel: reduce us, solve us | far queue, ball chunks/wave, ball aborts, deep")
     for it in list(range(12)) + [16, 24, 32, 48, 64, 96, 127]:
         print(f"{it:4d} {q[it, 0] / n:8.4f} {q[it, 1] / n:8.4f} {q[it, 2] / n:8.4f}"
-              f" {q[it, 3] * 0.01:7.2f} {q[it, 4] * 0.01:7.2f}")
+              f" {q[it, 3] * 0.01:7.2f} {q[it, 4] * 0.01:7.2f} | {dg[it, 0]:6d}"
+              f" {dg[it, 1] / max(1, (n + 63) // 64):7.2f} {dg[it, 2]:6d} {dg[it, 3]:6d}")
