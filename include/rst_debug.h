@@ -43,10 +43,17 @@ int rst_debug_query_nn_fallback(rst_ctx* ctx, const rst_target* tgt, const float
                                 int64_t nq, const int32_t* warm, int mode, int32_t* idx,
                                 float* d2, int32_t* path);
 
-/* The RST_SUM_REF loop's sequential-sum kernel on a host stream of n
+/* The RST_SUM_REF loop's sequential sums on a host stream of n
  * float4: out[c] = ((0 + x[0].c) + x[1].c) + ... in float32, i ascending --
  * the rounding of `dst_mean += dst.GetPoint(j)` (align_icp.cpp:120). */
 int rst_debug_seq_sum4(rst_ctx* ctx, const float* xyzw, int64_t n, float out[4]);
+
+/* The same sums by either kernel: serial = 0 the loop's parallel exact
+ * path (seqsum.hip: exponent-window run maps + one walking wavefront per
+ * component), serial = 1 the one-wavefront dependent chain (k_seq_sum4);
+ * reps launches back to back, *ms (optional) = device time per launch. */
+int rst_debug_seq_sum(rst_ctx* ctx, const float* xyzw, int64_t n, int serial, int reps,
+                      float out[4], float* ms);
 
 /* The target's leaf table: lstart[0 .. nleaves] (leaf L holds sorted
  * positions [lstart[L], lstart[L+1])) copied to the host when cap >=

@@ -28,7 +28,7 @@ INCLUDE = ROOT / "include"
 ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 ARCH = os.environ.get("RST_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["build.hip", "query.hip", "icp.hip", "capi.hip", "unproject.hip", "voxel.hip", "gicp.hip", "fpfh.hip", "comm.hip", "synth.cpp"]
+SOURCES = ["build.hip", "query.hip", "icp.hip", "seqsum.hip", "capi.hip", "unproject.hip", "voxel.hip", "gicp.hip", "fpfh.hip", "comm.hip", "synth.cpp"]
 LIB_NAME = "librst_align.so"
 
 # -ffp-contract=off: reference-exact rounding of the transform / distance /

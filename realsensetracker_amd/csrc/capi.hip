@@ -515,25 +515,45 @@ int rst_debug_target_leaves(rst_ctx* ctx, const rst_target* t, int32_t* lstart, 
   return RST_OK;
 }
 
-int rst_debug_seq_sum4(rst_ctx* ctx, const float* xyzw, int64_t n, float out[4]) {
-  if (!ctx || !out || n < 0 || (n > 0 && !xyzw)) return RST_E_ARG;
+int rst_debug_seq_sum(rst_ctx* ctx, const float* xyzw, int64_t n, int serial, int reps,
+                      float out[4], float* ms) {
+  if (!ctx || !out || n < 0 || (n > 0 && !xyzw) || reps < 1) return RST_E_ARG;
   RST_HIP(hipSetDevice(ctx->device));
   void* d = nullptr;
-  const size_t bytes = sizeof(float4) * (size_t)std::max<int64_t>(n, 1) + 64;
+  const size_t xb = (sizeof(float4) * (size_t)std::max<int64_t>(n, 1) + 255) & ~(size_t)255;
+  const size_t bytes = xb + 256 + seqsum_bytes(n);
   if (hipMalloc(&d, bytes) != hipSuccess) return RST_E_NOMEM;
-  float* dout = (float*)((char*)d + bytes - 64);
+  float* dout = (float*)((char*)d + xb);
+  void* ws = (char*)d + xb + 256;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
   int s = RST_OK;
   if (n > 0 && hipMemcpyAsync(d, xyzw, sizeof(float4) * n, hipMemcpyHostToDevice, ctx->stream) !=
                    hipSuccess)
     s = RST_E_HIP;
-  if (s >= 0) s = seq_sum4_device(ctx, (const float4*)d, n, dout);
+  if (s >= 0 && (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess)) s = RST_E_HIP;
+  if (s >= 0 && hipEventRecord(e0, ctx->stream) != hipSuccess) s = RST_E_HIP;
+  for (int r = 0; r < reps && s >= 0; ++r)
+    s = serial ? seq_sum4_device(ctx, (const float4*)d, n, dout)
+               : seqsum_enqueue((const float4*)d, n, 4, ws, dout, ctx->stream);
+  if (s >= 0 && hipEventRecord(e1, ctx->stream) != hipSuccess) s = RST_E_HIP;
   if (s >= 0 && (hipMemcpyAsync(out, dout, sizeof(float) * 4, hipMemcpyDeviceToHost, ctx->stream) !=
                      hipSuccess ||
                  hipStreamSynchronize(ctx->stream) != hipSuccess))
     s = RST_E_HIP;
+  if (s >= 0 && ms) {
+    float t = 0.f;
+    if (hipEventElapsedTime(&t, e0, e1) != hipSuccess) s = RST_E_HIP;
+    *ms = t / (float)reps;
+  }
   hipStreamSynchronize(ctx->stream);
+  if (e0) hipEventDestroy(e0);
+  if (e1) hipEventDestroy(e1);
   hipFree(d);
   return s;
+}
+
+int rst_debug_seq_sum4(rst_ctx* ctx, const float* xyzw, int64_t n, float out[4]) {
+  return rst_debug_seq_sum(ctx, xyzw, n, 0, 1, out, nullptr);
 }
 
 int rst_debug_icp_partials(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,

@@ -1470,12 +1470,14 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
   int32_t *qbuf = nullptr, *qcnt = nullptr;  // near queue, then far queue (k_icp_nn)
   float4* cert = nullptr;  // far-point certificates (read only under kCertBit)
   float4 *corr = nullptr, *srco = nullptr;
+  void* sqws = nullptr;  // seqsum.hip tables (RST_SUM_REF)
   {
     const size_t np = (size_t)std::max<int64_t>(n_local, 1);
     const size_t nq = (size_t)nblk * kBS;
     void* w = nullptr;
+    const size_t sqb = refsum ? seqsum_bytes(n_local) : 0;
     RST_CHECK(ctx_workspace(ctx, sizeof(float4) * np * (refsum ? 4 : 2) + sizeof(int4) * nq +
-                                     sizeof(int32_t) * (2 * nq + 2 * nblk + 64),
+                                     sizeof(int32_t) * (2 * nq + 2 * nblk + 64) + sqb + 256,
                             &w));
     cert = (float4*)w;
     nnq = cert + np;
@@ -1483,6 +1485,8 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
     srco = refsum ? cert + 3 * np : nullptr;
     qbuf = (int32_t*)(cert + np * (refsum ? 4 : 2));
     qcnt = qbuf + 2 * nq;
+    if (refsum)  // the sequential sums' tables (256-byte aligned)
+      sqws = (void*)(((uintptr_t)(qcnt + 2 * nblk + 64) + 255) & ~(uintptr_t)255);
     RST_HIP(hipMemsetAsync(nnq, 0xff, sizeof(float4) * np, st));
   }
 
@@ -1496,7 +1500,7 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
   float* fsum = (float*)totals;  // RST_SUM_REF: the centroid's sequential sums
   if (refsum) {
     k_gather_orig<<<blocks_for(n_local), kBS, 0, st>>>(src->pts, src->inv, n_local, srco);
-    k_seq_sum4<<<1, kWave, 0, st>>>(srco, n_local, fsum);  // point_cloud_utils.cpp:94-96
+    RST_CHECK(seqsum_enqueue(srco, n_local, 3, sqws, fsum, st));  // point_cloud_utils.cpp:94-96
     k_init_state<<<1, kBS, 0, st>>>(slab, 0, fsum, ia, ctx->d_state);
   } else if (!p2plane) {
     if (n_local > 0) {
@@ -1568,7 +1572,7 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
       } else if (refsum) {
         RST_CHECK(nn_pass(AccTag<RefAcc>{}));
         // align_icp.cpp:113,120: sum dst[nbr_i] and cost, i ascending, fp32
-        k_seq_sum4<<<1, kWave, 0, st>>>(corr, n_local, ctx->d_state->seq);
+        RST_CHECK(seqsum_enqueue(corr, n_local, 4, sqws, ctx->d_state->seq, st));
         k_cov_ref<<<kCovBlocks, kBS, 0, st>>>(srco, corr, n_local, ctx->d_state, slab2);
         k_reduce_solve<RefAcc><<<1, kRedBS, 0, st>>>(slab, 0, slab2, kCovBlocks, prm,
                                                      ctx->d_state, nullptr);

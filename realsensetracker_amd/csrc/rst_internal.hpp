@@ -220,6 +220,11 @@ int solve_kabsch_device(rst_ctx* ctx, const float* d_src, const float* d_dst,
 int centroid_device(rst_ctx* ctx, const float4* d_pts, int64_t n,
                     double* d_out3);
 int seq_sum4_device(rst_ctx* ctx, const float4* d_x, int64_t n, float* d_out);
+// the same sums, parallel and bit-exact (seqsum.hip): out[c] for c < nch;
+// ws holds seqsum_bytes(n)
+size_t seqsum_bytes(int64_t n);
+int seqsum_enqueue(const float4* d_x, int64_t n, int nch, void* ws, float* d_out,
+                   hipStream_t st);
 int kabsch_device(rst_ctx* ctx, const double cov[9], const float smean[3],
                   const float dmean[3], float pose_out[16]);
 

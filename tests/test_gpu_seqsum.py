@@ -1,0 +1,131 @@
+"""RST_SUM_REF's sequential float32 sums (align_icp.cpp:113,120-122;
+point_cloud_utils.cpp:94-96) -- the parallel exact kernels of seqsum.hip
+against numpy's sequential float32 accumulate (np.add.accumulate with a
+float32 dtype adds left to right, one rounding per element: the
+reference's `+=` loop), bit for bit, and against the one-wavefront serial
+chain (k_seq_sum4) they replace."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from realsensetracker_amd import _lib as L
+from realsensetracker_amd import align as A
+from realsensetracker_amd import driver
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    return A.get_context(0)
+
+
+def _fn():
+    f = L.lib().rst_debug_seq_sum
+    f.restype = C.c_int
+    f.argtypes = [C.c_void_p, L.c_float_p, C.c_int64, C.c_int, C.c_int, L.c_float_p,
+                  C.POINTER(C.c_float)]
+    return f
+
+
+def seq_sum(ctx, x, serial=0, reps=1):
+    x = np.ascontiguousarray(x, np.float32)
+    out = np.zeros(4, np.float32)
+    ms = C.c_float(0)
+    L.check(_fn()(ctx.handle, L.fptr(x), len(x), serial, reps, L.fptr(out), C.byref(ms)),
+            "seq_sum")
+    return out, ms.value
+
+
+def want(x):
+    # from a +0 start (the reference's Zero() vector): +0 + -0 = +0
+    x = np.concatenate([np.zeros((1, 4), np.float32), np.asarray(x, np.float32)])
+    return np.add.accumulate(x, axis=0, dtype=np.float32)[-1]
+
+
+def same(a, b):
+    a, b = np.asarray(a, np.float32), np.asarray(b, np.float32)
+    return np.array_equal(a.view(np.uint32), b.view(np.uint32)) or \
+        np.array_equal(np.isnan(a), np.isnan(b)) and np.array_equal(
+            np.where(np.isnan(a), 0, a).view(np.uint32), np.where(np.isnan(b), 0, b).view(np.uint32))
+
+
+def _cases():
+    rng = np.random.default_rng(7)
+    out = {}
+    for n in (1, 2, 63, 64, 65, 4095, 4096, 4097, 262144 + 17):
+        x = (rng.normal(size=(n, 4)) * 10 ** rng.uniform(-3, 2, size=(n, 4))).astype(np.float32)
+        x[:, 3] = np.abs(x[:, 3])
+        out[f"mixed_{n}"] = x
+    n = 200_000
+    # exact ties everywhere: small integers times powers of two
+    out["ties"] = (rng.integers(-64, 64, size=(n, 4)) *
+                   2.0 ** rng.integers(-12, 3, size=(n, 4))).astype(np.float32)
+    # a sum that oscillates through zero (many binade changes)
+    t = np.arange(n)
+    osc = np.sin(t * 2 * np.pi / 640.0) + 1e-3 * rng.normal(size=n)
+    out["zero_crossings"] = np.stack([osc, -osc, osc * 1e-3, np.abs(osc)], 1).astype(np.float32)
+    # alternating +-, a constant (every add rounds the same way), growth to 2^24 and past it
+    out["alternating"] = np.stack([(-1.0) ** t, (-1.0) ** t * 3.3, np.full(n, 0.1),
+                                   np.full(n, 1.0)], 1).astype(np.float32)
+    big = np.full((n, 4), 1e30, np.float32)
+    big[:, 1] = 3e38  # overflows to +inf
+    big[:, 2] = rng.normal(size=n) * 1e37
+    out["huge"] = big
+    tiny = (rng.normal(size=(n, 4)) * 1e-39).astype(np.float32)  # subnormals
+    tiny[::1000, 1] = 1.0
+    out["subnormal"] = tiny
+    nf = (rng.normal(size=(n, 4))).astype(np.float32)
+    nf[1000, 0] = np.nan
+    nf[5000, 1] = np.inf
+    nf[7000, 2] = np.inf
+    nf[9000, 2] = -np.inf
+    nf[150000, 3] = np.inf
+    out["nonfinite"] = nf
+    out["zeros"] = np.zeros((5000, 4), np.float32)
+    neg0 = np.full((100, 4), -0.0, np.float32)
+    out["neg_zeros"] = neg0
+    return out
+
+
+CASES = _cases()
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_parallel_seq_sum_bitexact(ctx, name):
+    x = CASES[name]
+    got, _ = seq_sum(ctx, x)
+    assert same(got, want(x)), (name, got, want(x))
+
+
+def test_parallel_seq_sum_frames(ctx):
+    """Real 640x480 clouds in pixel order (the order the reference sums:
+    the source in its original order, dst[nbr_i] for i ascending), both
+    frames of a pair and their squared ranges as a cost-like chain."""
+    K = driver.intrinsics(640, 480)
+    for seed in (10, 11):
+        da, db, _ = driver.make_pair(driver.SyntheticScene(0), K, seed=seed)
+        for d in (da, db):
+            p = driver.unproject(d, K)
+            x = np.concatenate([p, (p * p).sum(1, keepdims=True)], 1).astype(np.float32)
+            got, _ = seq_sum(ctx, x)
+            assert same(got, want(x)), (got, want(x))
+            # shifted so that the x chain starts far from zero, then crosses it
+            y = x.copy()
+            y[:, 0] -= np.float32(np.mean(x[:, 0]))
+            got, _ = seq_sum(ctx, y)
+            assert same(got, want(y))
+
+
+def test_parallel_matches_serial_kernel_and_is_faster(ctx):
+    K = driver.intrinsics(640, 480)
+    da, _, _ = driver.make_pair(driver.SyntheticScene(0), K, seed=10)
+    p = driver.unproject(da, K)
+    x = np.concatenate([p, (p * p).sum(1, keepdims=True)], 1).astype(np.float32)
+    a, ms_par = seq_sum(ctx, x, serial=0, reps=20)
+    b, ms_ser = seq_sum(ctx, x, serial=1, reps=3)
+    assert same(a, b)
+    print(f"\nseq sums of {len(x)} float4: parallel {ms_par * 1e3:.1f} us, "
+          f"serial {ms_ser * 1e3:.1f} us")
+    assert ms_par < ms_ser

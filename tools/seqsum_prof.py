@@ -1,0 +1,27 @@
+"""Time the RST_SUM_REF sequential sums (seqsum.hip) on a 640x480 frame:
+parallel path vs the serial chain; run under rocprofv3 --kernel-trace
+--stats for the per-kernel split."""
+import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "tests"))
+import numpy as np  # noqa: E402
+
+from realsensetracker_amd import align as A  # noqa: E402
+from realsensetracker_amd import driver  # noqa: E402
+from test_gpu_seqsum import seq_sum, want, same  # noqa: E402
+
+ctx = A.get_context(0)
+K = driver.intrinsics(640, 480)
+da, _, _ = driver.make_pair(driver.SyntheticScene(0), K, seed=10)
+p = driver.unproject(da, K)
+x = np.concatenate([p, (p * p).sum(1, keepdims=True)], 1).astype(np.float32)
+for serial, reps in ((0, 20), (1, 2)):
+    out, ms = seq_sum(ctx, x, serial=serial, reps=reps)
+    print("serial" if serial else "parallel", f"{ms * 1e3:.1f} us", same(out, want(x)))
+for c in range(4):
+    y = np.zeros_like(x)
+    y[:, c] = x[:, c]
+    out, ms = seq_sum(ctx, y, serial=0, reps=10)
+    print("chain", c, f"{ms * 1e3:.1f} us", same(out, want(y)))
