@@ -286,8 +286,12 @@ def main():
                          "frame-preparation stream and 4 pairs' streams on 4 hardware queues; "
                          "r02u/v: 2 pairs 16.2k, 4 pairs 15.8k it/s at 4 queues, 19.4k at 8; "
                          "0: leave the environment's value)")
-    ap.add_argument("--ref-steps", type=int, default=4,
+    ap.add_argument("--ref-steps", type=int, default=16,
                     help="frames timed in the reference-rounding mode (extra field; 0: skip)")
+    ap.add_argument("--ref-inflight", type=int, default=8,
+                    help="frame pairs in flight in the reference-rounding leg: its sequential "
+                         "sums run one wavefront per component for most of an iteration, so "
+                         "more pairs share the GPU")
     ap.add_argument("--roof-steps", type=int, default=4,
                     help="frames of the one-pair-in-flight kernel timing pass (roofline)")
     a = ap.parse_args()
@@ -470,18 +474,20 @@ def main():
     # ---- reference-rounding mode (RST_SUM_REF; extra field, not value) ----------
     refs = None
     if a.ref_steps > 0 and not pyr:
-        run(1, opts_exact, 0, None)
+        rctx = actx + [A.Context(local) for _ in range(max(0, a.ref_inflight - len(actx)))]
+        run(1, opts_exact, 0, None, rctx)
         sr = new_stats()
         barrier()
         sync_all()
         t4 = time.perf_counter()
-        run(a.ref_steps, opts_exact, 0, sr)
+        run(a.ref_steps, opts_exact, 0, sr, rctx)
         sync_all()
         barrier()
         dtr = max_over_ranks(time.perf_counter() - t4)
         refs = {"iterations_per_s": sum_over_ranks(sr["iters"]) / dtr,
                 "frames_per_s": sum_over_ranks(a.ref_steps) / dtr,
                 "ms_per_pair": 1000.0 * dtr / a.ref_steps, "steps": a.ref_steps,
+                "pairs_in_flight": len(rctx),
                 "pairs_ok": sr["ok"],
                 "note": "RST_SUM_REF (library default): source centroid, dst_mean and cost "
                         "as sequential fp32 sums in source order, the reference's rounding "

@@ -51,9 +51,13 @@ int rst_debug_seq_sum4(rst_ctx* ctx, const float* xyzw, int64_t n, float out[4])
 /* The same sums by either kernel: serial = 0 the loop's parallel exact
  * path (seqsum.hip: exponent-window run maps + one walking wavefront per
  * component), serial = 1 the one-wavefront dependent chain (k_seq_sum4);
- * reps launches back to back, *ms (optional) = device time per launch. */
+ * reps launches back to back, *ms (optional) = device time per launch;
+ * stats (optional, parallel path) = 8 int32 per component of the last
+ * launch's walk: superblock tries / jumps, block tries / jumps, serial
+ * blocks, zero blocks skipped, shader clocks in serial blocks, shader
+ * clocks of the whole walk. */
 int rst_debug_seq_sum(rst_ctx* ctx, const float* xyzw, int64_t n, int serial, int reps,
-                      float out[4], float* ms);
+                      float out[4], float* ms, int32_t* stats);
 
 /* The target's leaf table: lstart[0 .. nleaves] (leaf L holds sorted
  * positions [lstart[L], lstart[L+1])) copied to the host when cap >=

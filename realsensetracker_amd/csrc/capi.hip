@@ -516,15 +516,16 @@ int rst_debug_target_leaves(rst_ctx* ctx, const rst_target* t, int32_t* lstart, 
 }
 
 int rst_debug_seq_sum(rst_ctx* ctx, const float* xyzw, int64_t n, int serial, int reps,
-                      float out[4], float* ms) {
+                      float out[4], float* ms, int32_t* stats) {
   if (!ctx || !out || n < 0 || (n > 0 && !xyzw) || reps < 1) return RST_E_ARG;
   RST_HIP(hipSetDevice(ctx->device));
   void* d = nullptr;
   const size_t xb = (sizeof(float4) * (size_t)std::max<int64_t>(n, 1) + 255) & ~(size_t)255;
-  const size_t bytes = xb + 256 + seqsum_bytes(n);
+  const size_t bytes = xb + 256 + 256 + seqsum_bytes(n);
   if (hipMalloc(&d, bytes) != hipSuccess) return RST_E_NOMEM;
   float* dout = (float*)((char*)d + xb);
-  void* ws = (char*)d + xb + 256;
+  int* dstats = (int*)((char*)d + xb + 256);
+  void* ws = (char*)d + xb + 512;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   int s = RST_OK;
   if (n > 0 && hipMemcpyAsync(d, xyzw, sizeof(float4) * n, hipMemcpyHostToDevice, ctx->stream) !=
@@ -534,7 +535,8 @@ int rst_debug_seq_sum(rst_ctx* ctx, const float* xyzw, int64_t n, int serial, in
   if (s >= 0 && hipEventRecord(e0, ctx->stream) != hipSuccess) s = RST_E_HIP;
   for (int r = 0; r < reps && s >= 0; ++r)
     s = serial ? seq_sum4_device(ctx, (const float4*)d, n, dout)
-               : seqsum_enqueue((const float4*)d, n, 4, ws, dout, ctx->stream);
+               : seqsum_enqueue((const float4*)d, n, 4, ws, dout, ctx->stream,
+                                stats ? dstats : nullptr);
   if (s >= 0 && hipEventRecord(e1, ctx->stream) != hipSuccess) s = RST_E_HIP;
   if (s >= 0 && (hipMemcpyAsync(out, dout, sizeof(float) * 4, hipMemcpyDeviceToHost, ctx->stream) !=
                      hipSuccess ||
@@ -545,6 +547,9 @@ int rst_debug_seq_sum(rst_ctx* ctx, const float* xyzw, int64_t n, int serial, in
     if (hipEventElapsedTime(&t, e0, e1) != hipSuccess) s = RST_E_HIP;
     *ms = t / (float)reps;
   }
+  if (s >= 0 && stats && !serial &&
+      hipMemcpy(stats, dstats, sizeof(int) * 32, hipMemcpyDeviceToHost) != hipSuccess)
+    s = RST_E_HIP;
   hipStreamSynchronize(ctx->stream);
   if (e0) hipEventDestroy(e0);
   if (e1) hipEventDestroy(e1);
@@ -553,7 +558,7 @@ int rst_debug_seq_sum(rst_ctx* ctx, const float* xyzw, int64_t n, int serial, in
 }
 
 int rst_debug_seq_sum4(rst_ctx* ctx, const float* xyzw, int64_t n, float out[4]) {
-  return rst_debug_seq_sum(ctx, xyzw, n, 0, 1, out, nullptr);
+  return rst_debug_seq_sum(ctx, xyzw, n, 0, 1, out, nullptr, nullptr);
 }
 
 int rst_debug_icp_partials(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,

@@ -25,15 +25,16 @@ def _fn():
     f = L.lib().rst_debug_seq_sum
     f.restype = C.c_int
     f.argtypes = [C.c_void_p, L.c_float_p, C.c_int64, C.c_int, C.c_int, L.c_float_p,
-                  C.POINTER(C.c_float)]
+                  C.POINTER(C.c_float), C.c_void_p]
     return f
 
 
-def seq_sum(ctx, x, serial=0, reps=1):
+def seq_sum(ctx, x, serial=0, reps=1, stats=None):
     x = np.ascontiguousarray(x, np.float32)
     out = np.zeros(4, np.float32)
     ms = C.c_float(0)
-    L.check(_fn()(ctx.handle, L.fptr(x), len(x), serial, reps, L.fptr(out), C.byref(ms)),
+    sp = stats.ctypes.data if stats is not None else None
+    L.check(_fn()(ctx.handle, L.fptr(x), len(x), serial, reps, L.fptr(out), C.byref(ms), sp),
             "seq_sum")
     return out, ms.value
 
