@@ -198,8 +198,8 @@ def run_sharded(a, K, frames, d_depth, hip, world, rank, local, rdv, barrier, ma
     opts = L.default_opts(max_iter=a.iters, sum_mode=L.RST_SUM_FP64)
     ptr = d_src.value + 12 * lo
 
-    def step():
-        ok, pose, _ = sh.align(ptr, hi - lo, tgt, opts)
+    def step():  # every rank knows the global count: no host round trip per align
+        ok, pose, _ = sh.align(ptr, hi - lo, tgt, opts, n_total=n.value)
         return ok, pose
 
     for _ in range(a.warmup):

@@ -76,7 +76,12 @@ typedef struct {
   int32_t sum_mode;       /* rst_sum_mode (P2POINT_REF only; the sharded
                            * align always runs RST_SUM_FP64: a sequential
                            * sum has no shard decomposition) */
-  int32_t reserved[7];
+  int32_t n_total;        /* sharded align: the points of ALL shards when the
+                           * caller knows them (> 0: no count all-reduce and no
+                           * host round trip before the loop; must equal the
+                           * sum of n_shard over the ranks); 0 = all-reduce the
+                           * count (one host synchronisation per align) */
+  int32_t reserved[6];
 } rst_icp_opts;
 
 typedef struct {
@@ -405,6 +410,13 @@ int rst_icp_align_sharded_device(rst_ctx* ctx, rst_comm* comm,
                                  const rst_target* tgt,
                                  const rst_icp_opts* opts,
                                  float pose_inout[16], float* mean_cost);
+/* The same with a source shard prepared once (rst_target_build_device or
+ * rst_frame_prepare_device, with or without an index): no per-call Morton
+ * sort of the shard.  With opts->n_total set, the call enqueues the whole
+ * loop (RCCL all-reduces included) and synchronises only to read the pose. */
+int rst_icp_align_sharded_prepared(rst_ctx* ctx, rst_comm* comm, const rst_target* src_shard,
+                                   const rst_target* tgt, const rst_icp_opts* opts,
+                                   float pose_inout[16], float* mean_cost);
 
 #ifdef __cplusplus
 }

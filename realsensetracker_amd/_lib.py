@@ -32,7 +32,7 @@ class IcpOpts(C.Structure):
                 ("anneal_every", C.c_int32), ("anneal_div", C.c_float),
                 ("p2plane_eps", C.c_float), ("p2plane_mu", C.c_float),
                 ("p2plane_max_dist", C.c_float), ("sum_mode", C.c_int32),
-                ("reserved", C.c_int32 * 7)]
+                ("n_total", C.c_int32), ("reserved", C.c_int32 * 6)]
 
 
 class Intrinsics(C.Structure):
@@ -130,6 +130,8 @@ PROTOTYPES = {
     "rst_comm_destroy": (C.c_int, [_P]),
     "rst_icp_align_sharded_device": (C.c_int, [_P, _P, _P, C.c_int64, _P, C.POINTER(IcpOpts),
                                                c_float_p, c_float_p]),
+    "rst_icp_align_sharded_prepared": (C.c_int, [_P, _P, _P, _P, C.POINTER(IcpOpts),
+                                                 c_float_p, c_float_p]),
 }
 
 _lib = None

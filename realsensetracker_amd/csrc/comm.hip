@@ -95,4 +95,18 @@ int rst_icp_align_sharded_device(rst_ctx* ctx, rst_comm* comm, const float* d_sr
   return r;
 }
 
+int rst_icp_align_sharded_prepared(rst_ctx* ctx, rst_comm* comm, const rst_target* src_shard,
+                                   const rst_target* tgt, const rst_icp_opts* opts,
+                                   float pose_inout[16], float* mean_cost) {
+  if (!ctx || !comm || !src_shard || !tgt || !pose_inout) return RST_E_ARG;
+  RST_HIP(hipSetDevice(ctx->device));
+  rst_icp_opts o;
+  if (opts)
+    o = *opts;
+  else
+    rst_icp_opts_default(&o);
+  o.sum_mode = RST_SUM_FP64;
+  return icp_align_prepared(ctx, src_shard, tgt, &o, pose_inout, mean_cost, nullptr, comm);
+}
+
 }  // extern "C"

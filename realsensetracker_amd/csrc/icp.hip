@@ -1448,8 +1448,12 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
   double* slab2 = slab + rows1;
   double* totals = slab2 + (size_t)kFbBlocks * RS;  // 64 doubles
 
-  // n_total and the centroid are global quantities under sharding
-  if (comm) {
+  // n_total and the centroid are global quantities under sharding (the
+  // caller may know n_total: opts.n_total, no host round trip)
+  if (comm && opts.n_total > 0) {
+    if (opts.n_total < n_local) return RST_E_ARG;
+    n_total = opts.n_total;
+  } else if (comm) {
     double* cnt = totals;
     double h = (double)n_local;
     RST_HIP(hipMemcpyAsync(cnt, &h, sizeof(double), hipMemcpyHostToDevice, st));

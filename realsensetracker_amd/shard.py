@@ -91,15 +91,38 @@ class ShardedAligner:
         L.check(L.lib().rst_comm_create(ctx.handle, uid, self.world, self.rank,
                                         C.byref(self._comm)), "rst_comm_create")
 
-    def align(self, d_src_shard: int, n_shard: int, target, opts=None, pose=None):
+    def align(self, d_src_shard: int, n_shard: int, target, opts=None, pose=None,
+              n_total: int = 0):
+        """n_total > 0 (the points of all shards, when the caller knows it):
+        no count all-reduce and no host round trip before the loop."""
         pose = np.eye(4, dtype=np.float32) if pose is None else np.asarray(pose, np.float32)
         buf = L.pose_to_cm(pose)
         mc = C.c_float(0)
-        o = opts if opts is not None else L.default_opts(sum_mode=L.RST_SUM_FP64)
+        o = self._opts(opts, n_total)
         st = L.check(L.lib().rst_icp_align_sharded_device(
             self.ctx.handle, self._comm, C.c_void_p(d_src_shard), int(n_shard), target.handle,
             C.byref(o), L.fptr(buf), C.byref(mc)), "rst_icp_align_sharded_device")
         return st == L.RST_OK, L.cm_to_pose(buf), float(mc.value)
+
+    def align_prepared(self, src_shard, target, opts=None, pose=None, n_total: int = 0):
+        """The same with a prepared source shard (a Target): no per-call
+        Morton sort of the shard."""
+        pose = np.eye(4, dtype=np.float32) if pose is None else np.asarray(pose, np.float32)
+        buf = L.pose_to_cm(pose)
+        mc = C.c_float(0)
+        o = self._opts(opts, n_total)
+        st = L.check(L.lib().rst_icp_align_sharded_prepared(
+            self.ctx.handle, self._comm, src_shard.handle, target.handle, C.byref(o),
+            L.fptr(buf), C.byref(mc)), "rst_icp_align_sharded_prepared")
+        return st == L.RST_OK, L.cm_to_pose(buf), float(mc.value)
+
+    @staticmethod
+    def _opts(opts, n_total):
+        o = L.IcpOpts()
+        C.memmove(C.byref(o), C.byref(opts if opts is not None else
+                                      L.default_opts(sum_mode=L.RST_SUM_FP64)), C.sizeof(o))
+        o.n_total = int(n_total)
+        return o
 
     def close(self):
         if self._comm:

@@ -389,6 +389,24 @@ def test_sharded_single_rank_equals_unsharded(ctx):
         T = np.eye(4, dtype=np.float32)
         A.AlignIcp3d(g["src"], g["dst"], t, 128, T, opts=fp64_opts())
         assert np.array_equal(L.cm_to_pose(buf), T)
+        # the caller-known n_total (no count all-reduce, no host round trip)
+        # and a prepared shard: the same loop, the same bits
+        o.n_total = len(g["src"])
+        buf2 = L.pose_to_cm(np.eye(4))
+        assert L.lib().rst_icp_align_sharded_device(ctx.handle, comm, C.c_void_p(ds.ptr),
+                                                    len(g["src"]), t.handle, C.byref(o),
+                                                    L.fptr(buf2), C.byref(mc)) == 0
+        assert np.array_equal(L.cm_to_pose(buf2), T)
+        s = A.Target.build(g["src"], ctx)
+        buf3 = L.pose_to_cm(np.eye(4))
+        assert L.lib().rst_icp_align_sharded_prepared(ctx.handle, comm, s.handle, t.handle,
+                                                      C.byref(o), L.fptr(buf3),
+                                                      C.byref(mc)) == 0
+        assert np.array_equal(L.cm_to_pose(buf3), T)
+        o.n_total = len(g["src"]) - 1  # fewer than this rank's own shard: rejected
+        assert L.lib().rst_icp_align_sharded_device(ctx.handle, comm, C.c_void_p(ds.ptr),
+                                                    len(g["src"]), t.handle, C.byref(o),
+                                                    L.fptr(buf2), C.byref(mc)) == L.RST_E_ARG
     finally:
         L.lib().rst_comm_destroy(comm)
 
