@@ -62,6 +62,16 @@ constexpr int kCertBit = 1 << 30;
 #define RST_BALL_ITERS 4  // ... in the first iterations of a pair (r02r: iterations 0-3
                           // 1237/531/426/432 us vs 1668/674/568/492 per-lane; later ones lose)
 #endif
+#ifndef RST_PIX_TILES
+#define RST_PIX_TILES 1  // frame targets: exact searches in the target's pixel grid (k_icp_nn)
+#endif
+#ifndef RST_PIX_MIN_LANES
+#define RST_PIX_MIN_LANES 1  // k_icp_nn searches a wave's pixel windows when this many lanes need one
+#endif
+#ifndef RST_PIX_CHUNK
+#define RST_PIX_CHUNK 256  // pixels staged per wave and round (5 KB of LDS per wave)
+#endif
+constexpr int kPixChunk = RST_PIX_CHUNK;
 #ifndef RST_DIAG
 #define RST_DIAG 0  // 1: per-iteration certificate counters (rst_debug_queue_trace)
 #endif
@@ -575,6 +585,9 @@ __global__ __launch_bounds__(kBS) void k_icp_nn(BvhView bv, AdjView av, PixView 
   (void)av;
   __shared__ double lds[(kBS / kWave) * Acc::NV];
   __shared__ int wq[2][kBS / kWave];
+#if RST_PIX_TILES
+  __shared__ PixScratch<kPixChunk> pscr[kBS / kWave];
+#endif
   const int tb = xcd_tile(blockIdx.x, gridDim.x);
   // the far queue: the second half of qbuf / qcnt
   int32_t* __restrict__ qbuff = qbuf + (int64_t)gridDim.x * kBS;
@@ -606,10 +619,57 @@ __global__ __launch_bounds__(kBS) void k_icp_nn(BvhView bv, AdjView av, PixView 
     const float moved = margin_sqrt((dx * dx + dy * dy) + dz * dz) * 1.00001f;
     certified = margin_sqrt(dq) * 1.00001f + moved + 1e-30f < c.w;
   }
-  const bool need = act && fin && !certified;
+  bool need = act && fin && !certified;
   const bool far = wb >= 0 && (wb & kFarBit);
-  const uint64_t bm = __ballot(need && !far), fm = __ballot(need && far);
   const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+  // the search's seed: the last neighbour, or (cold: the pair's first
+  // iteration) the better of the projective and the Morton seed
+  float d0 = FLT_MAX;
+  float4 cq = make_float4(0.f, 0.f, 0.f, 0.f);
+  int cpos = -1;
+  if (need && wb < 0) {
+    Best2 sd;
+    sd.init();
+    proj_seed(bv, pv, px, py, pz, sd);
+    const int ms = morton_seed(bv, px, py, pz);
+    const float4 w = bv.pts[ms];
+    sd.offer(d2_ref(px, py, pz, w.x, w.y, w.z), f2i(w.w), ms);
+    cpos = sd.pos[0];
+    cq = bv.pts[cpos];
+    d0 = sd.d[0];
+  } else if (need) {
+    d0 = has_cert ? dq : d2_ref(px, py, pz, tq.x, tq.y, tq.z);
+  }
+#if RST_PIX_TILES
+  if (pv.map) {  // frame target (uniform): the pixel-window search, exact where it applies
+    Best2 pr;
+    pr.init();
+    float4 pq = make_float4(0.f, 0.f, 0.f, 0.f);
+    float prc = 0.f;
+    // a warm seed that moved away: the points around the query's projection
+    const float sp = (float)pv.s * pz / fminf(fabsf(pv.fx), fabsf(pv.fy));
+    const bool reseed = need && wb >= 0 && !(d0 <= 9.f * sp * sp);
+    if (__ballot(reseed) != 0 && reseed) d0 = fminf(d0, pix_seed_d2(pv, px, py, pz));
+    // (a wave with few searches leaves them to k_icp_fb's rows: one pass of
+    // this wave's staging would hold its whole block)
+    const bool dense = __popcll(__ballot(need)) >= RST_PIX_MIN_LANES;
+    if (pix_tile_search<kPixChunk, 2>(bv, pv, need && dense, px, py, pz, d0, pr, pq, pscr[wid],
+                                      prc)) {
+      const float g = cert_bound(pr, prc);
+      const int pos = pr.pos[0];
+      nnq[i] = make_float4(pq.x, pq.y, pq.z, i2f(pos | (g > 0.f ? kCertBit : 0)));
+      if (g > 0.f) cert[i] = make_float4(px, py, pz, g);
+      Acc::add(v, bv, aa, u, s, px, py, pz, pr.d[0], pos, pq);
+      need = false;
+    }
+#if RST_DIAG
+    const uint64_t pm = __ballot(act && fin && !certified && !need);
+    if (lane == 0 && st->iter < kQTrace)
+      atomicAdd(&const_cast<IcpState*>(st)->diag[st->iter][2], __popcll(pm));
+#endif
+  }
+#endif
+  const uint64_t bm = __ballot(need && !far), fm = __ballot(need && far);
 #if RST_DIAG
   {  // diagnostics build: per iteration, lanes certified
     const uint64_t cm = __ballot(act && certified);
@@ -632,19 +692,8 @@ __global__ __launch_bounds__(kBS) void k_icp_nn(BvhView bv, AdjView av, PixView 
   }
   const uint64_t lt = (1ull << lane) - 1ull;
   if (need && !far) qbuf[tb * (int64_t)kBS + before + __popcll(bm & lt)] = (int)i;
-  if (need && wb < 0) {
-    // cold (the pair's first iteration): seed the search with the better of
-    // the projective and the Morton seed (k_icp_fb starts from nnq's position)
-    Best2 sd;
-    sd.init();
-    proj_seed(bv, pv, px, py, pz, sd);
-    const int ms = morton_seed(bv, px, py, pz);
-    const float4 w = bv.pts[ms];
-    sd.offer(d2_ref(px, py, pz, w.x, w.y, w.z), f2i(w.w), ms);
-    const int p0 = sd.pos[0];
-    const float4 q = bv.pts[p0];
-    nnq[i] = make_float4(q.x, q.y, q.z, i2f(p0));
-  }
+  // cold: k_icp_fb starts from nnq's position
+  if (need && wb < 0) nnq[i] = make_float4(cq.x, cq.y, cq.z, i2f(cpos));
   if (need && far) qbuff[tb * (int64_t)kBS + beforef + __popcll(fm & lt)] = (int)i;
   if (threadIdx.x == 0) {
     qcnt[tb] = total;
@@ -1057,7 +1106,8 @@ union FbScratch {
 };
 
 template <class Acc>
-__global__ __launch_bounds__(kBS, Acc::kFbMinWaves) void k_icp_fb(BvhView bv, AdjView av, AccArgs aa,
+__global__ __launch_bounds__(kBS, Acc::kFbMinWaves) void k_icp_fb(BvhView bv, AdjView av, PixView pv,
+                                                AccArgs aa,
                                                 const float4* __restrict__ src,
                                                 IcpState* __restrict__ st,
                                                 float4* __restrict__ nnq,
@@ -1175,7 +1225,6 @@ __global__ __launch_bounds__(kBS, Acc::kFbMinWaves) void k_icp_fb(BvhView bv, Ad
 #if RST_DIAG
         if (lane == 0 && st->iter < kQTrace) {
           atomicAdd(&st->diag[st->iter][1], chunks);
-          if (!done) atomicAdd(&st->diag[st->iter][2], 1);
         }
 #endif
         if (gfail && lane == 0) {
@@ -1196,9 +1245,18 @@ __global__ __launch_bounds__(kBS, Acc::kFbMinWaves) void k_icp_fb(BvhView bv, Ad
         }
       } else {
         const bool act = has && fin;
-        const float rc = row_adj2(bv, av, act, r2.pos[0], px, py, pz, r2, rtags[wid][lane >> 4]);
-        exact = act && margin_sqrt(r2.d[0]) * 1.00001f + 1e-30f < rc;
-        if (exact) g = cert_bound(r2, rc);
+        // frame targets: the query's pixel window first (rows of 16 lanes)
+        float rcp = 0.f;
+        const bool pe = pv.map && row_pix(bv, pv, act, px, py, pz, r2, rcp);
+        const float rc =
+            row_adj2(bv, av, act && !pe, r2.pos[0], px, py, pz, r2, rtags[wid][lane >> 4]);
+        if (pe) {
+          exact = true;
+          g = cert_bound(r2, rcp);
+        } else {
+          exact = act && margin_sqrt(r2.d[0]) * 1.00001f + 1e-30f < rc;
+          if (exact) g = cert_bound(r2, rc);
+        }
       }
       if (has && lead && exact) fb_record<Acc>(v, bv, aa, u, nnq, cert, i, s, px, py, pz, r2, g, false);
       const bool unres = lead && has && fin && !exact;
@@ -1564,7 +1622,7 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
         k_icp_nn<Acc><<<nblk, kBS, 0, st>>>(bv, av, tgt->pix, aa, src->pts, n_local, ctx->d_state, nnq,
                                             cert, qbuf, qcnt, slab);
         RST_CHECK(mark(1));
-        k_icp_fb<Acc><<<fb_grid, kBS, fb_lds, st>>>(bv, av, aa, src->pts, ctx->d_state, nnq, cert,
+        k_icp_fb<Acc><<<fb_grid, kBS, fb_lds, st>>>(bv, av, tgt->pix, aa, src->pts, ctx->d_state, nnq, cert,
                                                      qbuf, qcnt, nblk, prm.lane_min, slab, slab2,
                                                      n_local);
         return mark(2);
@@ -1768,7 +1826,7 @@ int icp_debug_partials(rst_ctx* ctx, const rst_target* src, const rst_target* tg
     if (n > 0) {
       k_icp_nn<Acc><<<nblk, kBS, 0, st>>>(bv, av, tgt->pix, aa, src->pts, n, ctx->d_state, nnq, cert, qbuf,
                                           qcnt, slab);
-      k_icp_fb<Acc><<<fb_grid, kBS, fb_lds, st>>>(bv, av, aa, src->pts, ctx->d_state, nnq, cert,
+      k_icp_fb<Acc><<<fb_grid, kBS, fb_lds, st>>>(bv, av, tgt->pix, aa, src->pts, ctx->d_state, nnq, cert,
                                                    qbuf, qcnt, nblk, prm.lane_min, slab, slab2, n);
       k_reduce_solve<Acc><<<1, kRedBS, 0, st>>>(slab, 0, slab2, fb_grid, prm, ctx->d_state, totals);
     } else {

@@ -92,9 +92,13 @@ struct BvhView {
 // sorted position of grid pixel p's point (-1: no valid depth), p = vl * w +
 // ul on the level grid (pixel (s ul, s vl) of the full image, intrinsics of
 // the full image).  Projecting a query through it gives a candidate near its
-// nearest neighbour -- a warm start for the exact searches, never a result.
+// nearest neighbour (a warm start), and the grid's pixel windows answer exact
+// searches (pix_tile_search, rst_wave_nn.hpp).  pts[p] = the point of pixel p
+// (its sorted point, .w = original index bits; NaN where map[p] = -1), so a
+// window is staged with one load per pixel and map, in parallel.
 struct PixView {
   const int32_t* __restrict__ map;  // null: the target has no pixel grid
+  const float4* __restrict__ pts;   // [w h] grid pixel p's point (x, y, z, original index bits)
   float fx, fy, cx, cy;
   int32_t w, h, s;
   int32_t pad;

@@ -1262,6 +1262,213 @@ __device__ __forceinline__ bool ball_tile_search(const BvhView& bv, bool act, fl
   return true;
 }
 
+// ---- pixel tiles: exact searches through a frame target's pixel grid -------------------
+// A frame target's points come from its depth image (unproject.hip): point
+// (a, b) of the level grid (stride s) lies on the ray of full-resolution
+// pixel (a s, b s), P = z ((u - cx) / fx, (v - cy) / fy, 1), so
+// fx P.x / P.z + cx = u up to the float roundings of the unprojection
+// (relative 2e-7: < 3e-4 px).  For a query q with q.z > r, every x with
+// |x - q| <= r projects within
+//     |u_x - u_q| <= |fx| r sqrt(q.x^2 + q.z^2) / (q.z (q.z - r))
+// of q's projection u_q (the difference of ratios x.x / x.z - q.x / q.z has
+// numerator q.z d.x - q.x d.z <= r |(q.z, q.x)| and denominator
+// q.z x.z >= q.z (q.z - r)), likewise v with fy, q.y.  So the points of that
+// pixel window are every target point within r of q: a lane that scans the
+// window of a radius r at least the distance of some target point (its
+// seed) has its exact nearest, and min(second, r) is its certificate.  The
+// window is padded by 0.1 % and 0.02 px (the float arithmetic of the bound
+// and the projection).  The wave stages the union of its lanes' windows in
+// LDS, row-major, PixScratch<CH>::kN pixels at a time (PixView::pts and
+// map, one load each per pixel, all in flight), and each lane scans its own
+// window from LDS.  Lanes whose window exceeds RST_PIX_MAX_HALF pixels, or
+// whose query lies within 2 r of the camera plane, and waves whose union
+// exceeds kPixMaxW x 8 chunks, are left to the BVH searches (false).
+#ifndef RST_PIX_MAX_HALF
+#define RST_PIX_MAX_HALF 8.0f  // half-width cap of a lane's window (level pixels)
+#endif
+#ifndef RST_PIX_MIN_PX
+#define RST_PIX_MIN_PX 1.5f  // smallest window half-width: the certificate radius
+#endif
+constexpr int kPixMaxW = 64;
+
+template <int N>
+struct PixScratch {  // per-wave LDS
+  static constexpr int kN = N;
+  float4 pts[N];
+  int pos[N];
+};
+
+__device__ __forceinline__ int wave_min_i(int x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x = min(x, __shfl_xor(x, o, 64));
+  return x;
+}
+
+__device__ __forceinline__ int wave_max_i(int x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x = max(x, __shfl_xor(x, o, 64));
+  return x;
+}
+
+// The pixel window of the ball (q, r), r = max(the seed distance sqrt(d0)
+// with margins, RST_PIX_MIN_PX level pixels): false when it is too large
+// (or q too near the camera plane); rc = r.
+__device__ __forceinline__ bool pix_window(const PixView& pv, float qx, float qy, float qz,
+                                           float d0, float maxh, int& a0, int& a1, int& b0,
+                                           int& b1, float& rc) {
+  if (!(d0 < FLT_MAX) || !(qz > 0.f)) return false;
+  const float s = (float)pv.s;
+  const float afx = fabsf(pv.fx), afy = fabsf(pv.fy);
+  const float rw = fmaxf(margin_sqrt(d0) * 1.00001f + 4e-6f,
+                         RST_PIX_MIN_PX * s * qz / fminf(afx, afy));
+  if (!(qz > 2.0f * rw)) return false;
+  const float iz = 1.0f / qz;
+  const float uq = (pv.fx * qx * iz + pv.cx) / s, vq = (pv.fy * qy * iz + pv.cy) / s;
+  const float k = rw / (qz * (qz - rw)) / s;
+  const float bx = afx * k * sqrtf(qx * qx + qz * qz) * 1.001f + 0.02f;
+  const float by = afy * k * sqrtf(qy * qy + qz * qz) * 1.001f + 0.02f;
+  if (!(bx <= maxh && by <= maxh && fabsf(uq) < 1e6f && fabsf(vq) < 1e6f)) return false;
+  a0 = max(0, (int)ceilf(uq - bx));
+  a1 = min(pv.w - 1, (int)floorf(uq + bx));
+  b0 = max(0, (int)ceilf(vq - by));
+  b1 = min(pv.h - 1, (int)floorf(vq + by));
+  rc = rw;
+  return a0 <= a1 && b0 <= b1;  // (empty: the seed is off the grid -- never expected)
+}
+
+// The smallest squared distance from q to the points of the 3 x 3 pixels
+// around its projection (a seed for pix_window; FLT_MAX when none).
+__device__ __forceinline__ float pix_seed_d2(const PixView& pv, float qx, float qy, float qz) {
+  if (!(qz > 0.f)) return FLT_MAX;
+  const float iz = 1.0f / qz;
+  const float u = (pv.fx * qx * iz + pv.cx) / (float)pv.s;
+  const float v = (pv.fy * qy * iz + pv.cy) / (float)pv.s;
+  if (!(u > -2.f && v > -2.f && u < (float)pv.w + 1.f && v < (float)pv.h + 1.f)) return FLT_MAX;
+  const int uc = (int)floorf(u + 0.5f), vc = (int)floorf(v + 0.5f);
+  float4 p[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {  // all loads first: one latency
+    const int uu = uc + k % 3 - 1, vv = vc + k / 3 - 1;
+    const bool in = uu >= 0 && vv >= 0 && uu < pv.w && vv < pv.h;
+    p[k] = in ? pv.pts[(int64_t)vv * pv.w + uu] : make_float4(NAN, NAN, NAN, 0.f);
+  }
+  float d = FLT_MAX;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) d = fminf(d, d2_ref(qx, qy, qz, p[k].x, p[k].y, p[k].z));  // NaN: skipped
+  return d;
+}
+
+// act: the lane holds a finite query and d0 = the squared distance of some
+// target point (its seed).  On true, r (empty on entry) holds the lane's
+// exact two nearest within rc, the first's point in q0, and rc the covered
+// radius.  A wave whose union needs more than MaxChunks chunks leaves its
+// lanes (false).  The whole wave calls it.
+template <int N, int MaxChunks>
+__device__ __forceinline__ bool pix_tile_search(const BvhView& bv, const PixView& pv, bool act,
+                                                float qx, float qy, float qz, float d0, Best2& r,
+                                                float4& q0, PixScratch<N>& ts, float& rc) {
+  constexpr int kPer = N / kWave;
+  const int lane = __lane_id();
+  int a0 = 0, a1 = -1, b0 = 0, b1 = -1;
+  rc = 0.f;
+  const bool ok = act && pix_window(pv, qx, qy, qz, d0, RST_PIX_MAX_HALF, a0, a1, b0, b1, rc);
+  if (__ballot(ok) == 0) return false;
+  const int A0 = wave_min_i(ok ? a0 : INT_MAX), A1 = wave_max_i(ok ? a1 : INT_MIN);
+  const int B0 = wave_min_i(ok ? b0 : INT_MAX), B1 = wave_max_i(ok ? b1 : INT_MIN);
+  const int wu = A1 - A0 + 1, hu = B1 - B0 + 1;
+  const int rows = N / max(wu, 1);
+  if (wu > kPixMaxW || rows < 1 || hu > MaxChunks * rows) return false;
+  const float rwu = 1.0f / (float)wu;
+  for (int cb = B0; cb <= B1; cb += rows) {
+    const int ce = min(B1, cb + rows - 1);
+    const int cnt = (ce - cb + 1) * wu;
+    float4 pp[kPer];
+    int pk[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {  // every load of the chunk in flight
+      const int k = lane + j * kWave;
+      pk[j] = -1;
+      pp[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (k < cnt) {
+        const int rr = (int)(((float)k + 0.5f) * rwu);  // k / wu (exact: k, wu < 2^12)
+        const int64_t px = (int64_t)(cb + rr) * pv.w + (A0 + k - rr * wu);
+        pk[j] = pv.map[px];
+        pp[j] = pv.pts[px];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int k = lane + j * kWave;
+      if (k < cnt) {
+        ts.pts[k] = pp[j];
+        ts.pos[k] = (uint32_t)pk[j] < (uint32_t)bv.m ? pk[j] : -1;
+      }
+    }
+    wave_sync();
+    if (ok) {
+      const int sb0 = max(b0, cb), sb1 = min(b1, ce);
+      for (int b = sb0; b <= sb1; ++b) {
+        const int row = (b - cb) * wu - A0;
+        for (int a = a0; a <= a1; ++a) {
+          const int p = ts.pos[row + a];
+          if (p >= 0) {
+            const float4 t = ts.pts[row + a];
+            const float d = d2_ref(qx, qy, qz, t.x, t.y, t.z);
+            if (d <= r.d[1]) {  // (offer's own test, hoisted: most pixels are farther)
+              r.offer(d, f2i(t.w), p);
+              if (r.pos[0] == p) q0 = t;
+            }
+          }
+        }
+      }
+    }
+    wave_sync();
+  }
+  // (the seed lies in the window, so the first is within rc; checked anyway)
+  return ok && r.pos[0] >= 0 && margin_sqrt(r.d[0]) * 1.00001f + 1e-30f < rc;
+}
+
+// One query per row of 16 lanes (the fallback's short queues): the row's
+// lanes split the query's pixel window, then a row-wide (d2, index) merge.
+// r holds the seeds (r.d[0] = the seed distance); on true r is the exact two
+// nearest within rc.  Whole rows call it (act uniform per row).
+__device__ __forceinline__ bool row_pix(const BvhView& bv, const PixView& pv, bool act, float qx,
+                                        float qy, float qz, Best2& r, float& rc) {
+  const int sub = __lane_id() & 15;
+  int a0 = 0, a1 = -1, b0 = 0, b1 = -1;
+  rc = 0.f;
+  const bool ok = act && pix_window(pv, qx, qy, qz, r.d[0], RST_PIX_MAX_HALF, a0, a1, b0, b1, rc);
+  Best2 mine;
+  mine.init();
+  const int wa = a1 - a0 + 1;
+  const int cnt = ok ? wa * (b1 - b0 + 1) : 0;
+  const float rwa = 1.0f / (float)max(wa, 1);
+  for (int k0 = 0; k0 < cnt; k0 += 16 * 8) {
+    float4 p[8];
+    int pos[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {  // 8 pixels per lane in flight
+      const int k = k0 + sub + 16 * j;
+      pos[j] = -1;
+      p[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (k < cnt) {
+        const int rr = (int)(((float)k + 0.5f) * rwa);  // k / wa (exact)
+        const int64_t px = (int64_t)(b0 + rr) * pv.w + (a0 + k - rr * wa);
+        pos[j] = pv.map[px];
+        p[j] = pv.pts[px];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if ((uint32_t)pos[j] < (uint32_t)bv.m)
+        mine.offer(d2_ref(qx, qy, qz, p[j].x, p[j].y, p[j].z), f2i(p[j].w), pos[j]);
+  }
+  mine = wave_lex_min<8>(mine);
+  const bool ex = ok && mine.pos[0] >= 0 && margin_sqrt(mine.d[0]) * 1.00001f + 1e-30f < rc;
+  if (ex) r = mine;  // (else r keeps its seeds for the next search)
+  return ex;
+}
+
 // ---- the ICP loop's candidate lists ----------------------------------------------------
 // Exact K nearest of q (r empty: BestK keeps duplicate offers) through the
 // leaf adjacency of the leaf holding sorted position `start`: the entries in

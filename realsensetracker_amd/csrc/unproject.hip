@@ -112,13 +112,18 @@ __global__ __launch_bounds__(kBS) void k_write(const uint16_t* __restrict__ dept
   }
 }
 
-// pixel map: original point index -> sorted position of the built target
+// pixel map: original point index -> sorted position of the built target;
+// the grid's points in pixel order (PixView::pts)
 __global__ __launch_bounds__(kBS) void k_pixmap_sorted(int32_t* __restrict__ map, int64_t npx,
-                                                       const int32_t* __restrict__ inv) {
+                                                       const int32_t* __restrict__ inv,
+                                                       const float4* __restrict__ spts,
+                                                       float4* __restrict__ ppts) {
   const int64_t p = (int64_t)blockIdx.x * kBS + threadIdx.x;
   if (p < npx) {
     const int32_t o = map[p];
-    map[p] = o >= 0 ? inv[o] : -1;
+    const int32_t q = o >= 0 ? inv[o] : -1;
+    map[p] = q;
+    ppts[p] = q >= 0 ? spts[q] : make_float4(NAN, NAN, NAN, __int_as_float(-1));
   }
 }
 
@@ -250,9 +255,16 @@ static int frame_prepare(rst_ctx* ctx, const uint16_t* d_depth, const rst_intrin
   float* dx = nullptr;
   size_t dxc = 0, pmc = 0;
   int32_t* pm = nullptr;  // the level's pixel map (the target keeps it)
+  float4* pp = nullptr;   // ... and its points in pixel order
+  size_t ppc = 0;
   RST_CHECK(ctx_alloc(ctx, sizeof(float) * 3 * std::max<int64_t>(npx, 1), (void**)&dx, &dxc));
   if (ctx_alloc(ctx, sizeof(int32_t) * std::max<int64_t>(npl, 1), (void**)&pm, &pmc) < 0) {
     ctx_release(ctx, dx, dxc);
+    return RST_E_NOMEM;
+  }
+  if (ctx_alloc(ctx, sizeof(float4) * std::max<int64_t>(npl, 1), (void**)&pp, &ppc) < 0) {
+    ctx_release(ctx, dx, dxc);
+    ctx_release(ctx, pm, pmc);
     return RST_E_NOMEM;
   }
   int64_t n = 0;
@@ -260,10 +272,14 @@ static int frame_prepare(rst_ctx* ctx, const uint16_t* d_depth, const rst_intrin
   rst_target* t = nullptr;
   if (s >= 0) s = target_build_device(ctx, dx, n, true, &t);
   if (s >= 0) {
-    k_pixmap_sorted<<<(int)((npl + kBS - 1) / kBS), kBS, 0, ctx->stream>>>(pm, npl, t->inv);
+    k_pixmap_sorted<<<(int)((npl + kBS - 1) / kBS), kBS, 0, ctx->stream>>>(pm, npl, t->inv,
+                                                                            t->pts, pp);
     t->allocs.emplace_back(pm, pmc);  // freed with the target
+    t->allocs.emplace_back(pp, ppc);
+    t->pix.map = pm;
+    t->pix.pts = pp;
     pm = nullptr;
-    t->pix.map = t->allocs.back().first ? (const int32_t*)t->allocs.back().first : nullptr;
+    pp = nullptr;
     t->pix.fx = K->fx;
     t->pix.fy = K->fy;
     t->pix.cx = K->cx;
@@ -280,6 +296,7 @@ static int frame_prepare(rst_ctx* ctx, const uint16_t* d_depth, const rst_intrin
   hipStreamSynchronize(ctx->stream);
   ctx_release(ctx, dx, dxc);
   if (pm) ctx_release(ctx, pm, pmc);
+  if (pp) ctx_release(ctx, pp, ppc);
   if (s < 0) {
     if (t) rst_target_free(t);
     return s;

@@ -23,9 +23,15 @@ for name in ("rst_debug_queue_trace", "rst_debug_iter_diag"):
 ctx = A.get_context(0)
 K = driver.intrinsics(640, 480)
 da, db, _ = driver.make_pair(driver.SyntheticScene(0), K, seed=10)
-pa, pb = driver.unproject(da, K), driver.unproject(db, K)
-tgt = A.Target.build(pa, ctx)
-src = A.Target.build(pb, ctx)
+if "--host" in sys.argv:  # clouds built from host points (no pixel grid)
+    pa, pb = driver.unproject(da, K), driver.unproject(db, K)
+    tgt = A.Target.build(pa, ctx)
+    src = A.Target.build(pb, ctx)
+else:  # frame targets prepared from depth on the device (the bench path)
+    bufs = [A.DeviceBuffer.from_array(x, ctx) for x in (da, db)]
+    tgt = A.Target.from_depth_device(bufs[0].ptr, K, 0, ctx)
+    src = A.Target.from_depth_device(bufs[1].ptr, K, 0, ctx)
+    pa, pb = np.zeros((len(tgt), 3)), np.zeros((len(src), 3))
 opts = L.default_opts(max_iter=128, sum_mode=L.RST_SUM_FP64)
 for rep in range(2):
     T = np.eye(4, dtype=np.float32)
@@ -35,7 +41,7 @@ lib.rst_debug_queue_trace(ctx.handle, L.iptr(q), 256)
 d = np.zeros((256, 4), np.int32)
 lib.rst_debug_iter_diag(ctx.handle, L.iptr(d), 256)
 print("n", len(pb), "m", len(pa), "ok", r.ok)
-print("  it  certified   nearQ    farQ  adj_exact  ball_chunks  ball_abort   deep")
+print("  it  certified   nearQ    farQ  adj_exact  ball_chunks   pix_exact   deep  red_us solve_us")
 for it in list(range(0, 20)) + [24, 32, 48, 64, 96, 127]:
     print(f"{it:4d} {q[it,1]:10d} {q[it,0]:7d} {d[it,0]:7d} {q[it,2]:10d} {d[it,1]:12d} "
-          f"{d[it,2]:11d} {d[it,3]:6d}")
+          f"{d[it,2]:11d} {d[it,3]:6d} {q[it,3] / 100:7.2f} {q[it,4] / 100:8.2f}")
