@@ -65,8 +65,8 @@ constexpr int kCertBit = 1 << 30;
 #ifndef RST_PIX_TILES
 #define RST_PIX_TILES 1  // frame targets: exact searches in the target's pixel grid (k_icp_nn)
 #endif
-#ifndef RST_PIX_MIN_LANES
-#define RST_PIX_MIN_LANES 1  // k_icp_nn searches a wave's pixel windows when this many lanes need one
+#ifndef RST_ROW_PIX
+#define RST_ROW_PIX 1  // k_icp_fb's rows scan the pixel window before the leaf adjacency
 #endif
 #ifndef RST_PIX_CHUNK
 #define RST_PIX_CHUNK 256  // pixels staged per wave and round (5 KB of LDS per wave)
@@ -650,11 +650,7 @@ __global__ __launch_bounds__(kBS) void k_icp_nn(BvhView bv, AdjView av, PixView 
     const float sp = (float)pv.s * pz / fminf(fabsf(pv.fx), fabsf(pv.fy));
     const bool reseed = need && wb >= 0 && !(d0 <= 9.f * sp * sp);
     if (__ballot(reseed) != 0 && reseed) d0 = fminf(d0, pix_seed_d2(pv, px, py, pz));
-    // (a wave with few searches leaves them to k_icp_fb's rows: one pass of
-    // this wave's staging would hold its whole block)
-    const bool dense = __popcll(__ballot(need)) >= RST_PIX_MIN_LANES;
-    if (pix_tile_search<kPixChunk, 2>(bv, pv, need && dense, px, py, pz, d0, pr, pq, pscr[wid],
-                                      prc)) {
+    if (pix_tile_search<kPixChunk, 2>(bv, pv, need, px, py, pz, d0, pr, pq, pscr[wid], prc)) {
       const float g = cert_bound(pr, prc);
       const int pos = pr.pos[0];
       nnq[i] = make_float4(pq.x, pq.y, pq.z, i2f(pos | (g > 0.f ? kCertBit : 0)));
@@ -1247,7 +1243,7 @@ __global__ __launch_bounds__(kBS, Acc::kFbMinWaves) void k_icp_fb(BvhView bv, Ad
         const bool act = has && fin;
         // frame targets: the query's pixel window first (rows of 16 lanes)
         float rcp = 0.f;
-        const bool pe = pv.map && row_pix(bv, pv, act, px, py, pz, r2, rcp);
+        const bool pe = RST_ROW_PIX && pv.map && row_pix(bv, pv, act, px, py, pz, r2, rcp);
         const float rc =
             row_adj2(bv, av, act && !pe, r2.pos[0], px, py, pz, r2, rtags[wid][lane >> 4]);
         if (pe) {

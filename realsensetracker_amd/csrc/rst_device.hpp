@@ -200,6 +200,27 @@ __device__ __forceinline__ void block_sum_to_slab(double (&v)[NV],
   }
 }
 
+// block_sum_to_slab added onto the row's current values (a later kernel's
+// share of the same tile: fixed order, reproducible)
+template <int NV, int BS>
+__device__ __forceinline__ void block_sum_add_to_slab(double (&v)[NV], double* lds,
+                                                      double* slab_row) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wid = threadIdx.x / kWave;
+  constexpr int K = log2_exact(pow2_ceil(NV));
+  const double old = threadIdx.x < NV ? slab_row[threadIdx.x] : 0.0;  // in flight meanwhile
+  const double t = wave_sum_transpose<NV>(v, lane);
+  const int idx = lane >> (6 - K);
+  if ((lane & ((1 << (6 - K)) - 1)) == 0 && idx < NV) lds[wid * NV + idx] = t;
+  __syncthreads();
+  if (threadIdx.x < NV) {
+    double s = 0.0;
+#pragma unroll
+    for (int w = 0; w < BS / kWave; ++w) s += lds[w * NV + threadIdx.x];
+    slab_row[threadIdx.x] = old + s;
+  }
+}
+
 // block_sum_to_slab, then rows blk, blk + step, ... (< rows) of another slab
 // (row stride `stride`) added in increasing order: a grid of G blocks folds
 // an earlier kernel's rows into its own G, fixed order (reproducible).

@@ -17,13 +17,13 @@ for r in rows:
     if it < 0 or "P2Point" not in n:
         continue
     k = 0 if "k_icp_nn<" in n else (1 if "k_icp_fb<" in n else (
-        2 if "k_icp_wave<" in n else (3 if "k_reduce_solve<" in n else -1)))
+        2 if "k_icp_pix<" in n else (3 if "k_reduce_solve<" in n else -1)))
     if k < 0:
         continue
     per.setdefault(it, [0.0, 0.0, 0.0, 0.0])[k] += d
     if k == 3:
         it += 1
-print(f"pairs {pairs}; per-pair us: iter nn fb wave solve")
+print(f"pairs {pairs}; per-pair us: iter nn fb pix solve")
 for i in list(range(0, 8)) + [16, 32, 64, 127]:
     if i in per:
         print(i, " ".join(f"{x / pairs:8.1f}" for x in per[i]))

@@ -312,6 +312,34 @@ def test_icp_exact_recovery_property_full_size(ctx):
     assert max(e) <= 1e-4, e
 
 
+def test_frame_targets_640_pixel_windows(ctx):
+    """640x480 frames prepared from depth on the device: most searches are
+    answered in the targets' pixel windows (k_icp_nn, k_icp_fb's rows), the
+    rest by the BVH.  In the reference-rounding mode (sums in source order:
+    independent of which search answered) the pose equals the pose from
+    host-built clouds of the same points (BVH searches only) bit for bit,
+    and the reference arithmetic within the north_star gate."""
+    K = driver.intrinsics(640, 480)
+    sc = driver.SyntheticScene(5)
+    da, db, _ = driver.make_pair(sc, K, seed=17)
+    ba = A.DeviceBuffer.from_array(da, ctx)
+    bb = A.DeviceBuffer.from_array(db, ctx)
+    tf = A.Target.from_depth_device(ba.ptr, K, 0, ctx)
+    sf = A.Target.from_depth_device(bb.ptr, K, 0, ctx)
+    pa = driver.unproject(da, K, ctx=ctx)
+    pb = driver.unproject(db, K, ctx=ctx)
+    th, sh = A.Target.build(pa, ctx), A.Target.build(pb, ctx)
+    o = L.default_opts(max_iter=128)  # RST_SUM_REF
+    rf = A.align_prepared(sf, tf, None, o)
+    rh = A.align_prepared(sh, th, None, o)
+    assert rf.ok and rh.ok
+    assert np.array_equal(rf.pose, rh.pose), pose_err(rf.pose, rh.pose)
+    _, Tr, _, _ = O.align_icp(pb, pa, 128, tree=O.KDTree(pa), sum_mode=0)
+    e = pose_err(rf.pose, Tr)
+    print(f"640x480 frame targets vs reference arithmetic {e}")
+    assert max(e) <= 1e-4, e
+
+
 def test_icp_mid_size_lane_threshold(ctx):
     """A 320x240 pair (~75k source points: the RST_LANE_SMALL_N range of the
     fallback's lane-mode threshold, 3n/4) against the fp64-sum oracle, and
