@@ -14,6 +14,6 @@ step() {  # name, limit, command...
   [ $rc -eq 0 ] || exit $rc
 }
 [ -n "$SKIP_TESTS" ] || step pytest_gpu 600 python -u -m pytest tests/ -x -v -m gpu --timeout 120 --timeout-method thread
-step bench_pyramid 300 python bench.py --workload pyramid --no-p2plane
+step bench_pyramid 300 python bench.py --workload pyramid --graphs --no-p2plane
 step bench_sharded 300 python bench.py --workload sharded --steps 5 --warmup 1
 step bench_720p 300 python bench.py --width 1280 --height 720 --no-host-api --no-gicp
