@@ -281,14 +281,16 @@ def main():
                     help="replay each align's iteration loop as a hipGraph (no kernel timing)")
     ap.add_argument("--inflight", type=int, default=4,
                     help="frame pairs in flight per GPU (one HIP stream each)")
-    ap.add_argument("--hw-queues", type=int, default=8,
+    ap.add_argument("--hw-queues", type=int, default=24,
                     help="GPU_MAX_HW_QUEUES for this process (HIP's default, 4, puts the "
                          "frame-preparation stream and 4 pairs' streams on 4 hardware queues; "
                          "r02u/v: 2 pairs 16.2k, 4 pairs 15.8k it/s at 4 queues, 19.4k at 8; "
+                         "r02m: one queue per stream of the reference-rounding leg too "
+                         "(24 pairs: 7.1k vs 3.0k it/s at 8 queues, main leg unchanged); "
                          "0: leave the environment's value)")
-    ap.add_argument("--ref-steps", type=int, default=16,
+    ap.add_argument("--ref-steps", type=int, default=48,
                     help="frames timed in the reference-rounding mode (extra field; 0: skip)")
-    ap.add_argument("--ref-inflight", type=int, default=8,
+    ap.add_argument("--ref-inflight", type=int, default=24,
                     help="frame pairs in flight in the reference-rounding leg: its sequential "
                          "sums run one wavefront per component for most of an iteration, so "
                          "more pairs share the GPU")

@@ -1513,9 +1513,11 @@ static int gicp_lm_step(const double H[36], const double g[6], double lambda, do
  * (align_gicp.cpp:41-103): Ceres' Levenberg-Marquardt restated as the
  * build's own LM (DESIGN.md "GICP"): evaluate the candidate; accept when F
  * drops (lambda /= 3, floor 1e-12) else lambda *= 4; stop when the step norm
- * < 1e-10, the relative drop < 1e-12, lambda > 1e10, or after max_iter
- * evaluations.  Returns the final F (Ceres' final_cost); pose_out 4x4
+ * < 1e-10, the relative drop of an accepted step < 1e-6 (Ceres'
+ * Solver::Options::function_tolerance default: GetOptions(), align_gicp.cpp:13-37,
+ * sets no tolerance), lambda > 1e10, or after max_iter evaluations.  Returns the final F (Ceres' final_cost); pose_out 4x4
  * col-major float (R from the fp64 rotation, as q.toRotationMatrix()). */
+#define ORC_GICP_FTOL 1e-6 /* Ceres' default function_tolerance */
 double orc_gicp_solve(const float* src, int64_t n, const float* dst, const float* src_covs,
                       const float* dst_covs, const int32_t* dst_idx, const float seed[16],
                       int max_iter, float pose_out[16], int* iters_out) {
@@ -1557,7 +1559,7 @@ double orc_gicp_solve(const float* src, int64_t n, const float* dst, const float
       memcpy(g, g2, sizeof(g));
       F = F2;
       lambda = lambda / 3.0 > 1e-12 ? lambda / 3.0 : 1e-12;
-      if (drop < 1e-12) break;
+      if (drop < ORC_GICP_FTOL) break;
     } else {
       lambda *= 4.0;
       if (lambda > 1e10) break;

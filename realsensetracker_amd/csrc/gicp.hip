@@ -42,6 +42,10 @@ constexpr int kRedBS = 1024;
 constexpr int kNV = 28;  // H upper (21), g (6), cost
 constexpr int kRS = 32;  // slab row stride
 constexpr int kKnn = 33;
+// stop once an accepted step lowers the cost by less than this fraction:
+// Ceres' default Solver::Options::function_tolerance (the reference's
+// GetOptions(), align_gicp.cpp:13-37, sets none)
+constexpr double kGicpFtol = 1e-6;
 
 struct GicpState {
   double R[9], t[3];     // accepted pose (row-major R)
@@ -449,7 +453,7 @@ __global__ __launch_bounds__(kRedBS) void k_gicp_lm(const double* __restrict__ s
     s.F = F2;
     if (it > 0) {
       s.lambda = s.lambda / 3.0 > 1e-12 ? s.lambda / 3.0 : 1e-12;
-      if (drop < 1e-12) {
+      if (drop < kGicpFtol) {
         s.done = 1;
         return;
       }
@@ -566,18 +570,54 @@ int upload(hipStream_t st, void* d, const void* h, size_t bytes) {
   return RST_OK;
 }
 
-// max_inner LM evaluations on (src, dst, covs, idx) from st->est; result in st->est
+// max_inner LM evaluations on (src, dst, covs, idx) from st->est; result in
+// st->est.  The evaluations are enqueued kLmChunk at a time; after each
+// chunk the state's `done` flag is copied to pinned host memory, and the
+// host stops enqueueing once a finished chunk reports it (checked one chunk
+// behind, so the device never waits for the host): a solve that converges
+// after k evaluations launches about k + 2 kLmChunk of them, not max_inner
+// (every launch after `done` exits at once, so the result is the same).
+constexpr int kLmChunk = 4;
 int lm_solve(rst_ctx* ctx, const float* ds, int64_t n, const float* dd, const float* dcs,
              const float* dcd, const int32_t* didx, GicpState* dst_state, double* slab,
              int max_inner) {
   hipStream_t st = ctx->stream;
   const int nb = blocks_for(n);
+  void* pin = nullptr;
+  RST_CHECK(ctx_pinned(ctx, 64, &pin));
+  volatile int* hflag = (volatile int*)pin;
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  for (int k = 0; k < 2; ++k)
+    if (hipEventCreateWithFlags(&ev[k], hipEventDisableTiming) != hipSuccess) ev[k] = nullptr;
+  const bool early = ev[0] && ev[1];
   k_gicp_begin<<<1, 1, 0, st>>>(dst_state, max_inner);
-  for (int it = 0; it < max_inner; ++it) {
-    k_gicp_eval<<<nb, kBS, 0, st>>>(ds, n, dd, dcs, dcd, didx, dst_state, slab);
-    k_gicp_lm<<<1, kRedBS, 0, st>>>(slab, nb, dst_state);
+  int s = RST_OK;
+  for (int it = 0, c = 0; it < max_inner; ++c) {
+    for (int k = 0; k < kLmChunk && it < max_inner; ++k, ++it) {
+      k_gicp_eval<<<nb, kBS, 0, st>>>(ds, n, dd, dcs, dcd, didx, dst_state, slab);
+      k_gicp_lm<<<1, kRedBS, 0, st>>>(slab, nb, dst_state);
+    }
+    if (!early) continue;
+    if (hipMemcpyAsync((void*)(hflag + (c & 1)), &dst_state->done, sizeof(int),
+                       hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipEventRecord(ev[c & 1], st) != hipSuccess) {
+      s = RST_E_HIP;
+      break;
+    }
+    if (c >= 1) {
+      if (hipEventSynchronize(ev[(c - 1) & 1]) != hipSuccess) {
+        s = RST_E_HIP;
+        break;
+      }
+      if (hflag[(c - 1) & 1]) break;  // converged: the rest would exit at once
+    }
   }
   k_gicp_end<<<1, 1, 0, st>>>(dst_state);
+  // (a flag copy still pending is stream-ordered before the next solve's
+  // copies, and ctx_pinned synchronises before it frees the buffer)
+  for (int k = 0; k < 2; ++k)
+    if (ev[k]) (void)hipEventDestroy(ev[k]);
+  RST_CHECK(s);
   RST_HIP(hipGetLastError());
   return RST_OK;
 }

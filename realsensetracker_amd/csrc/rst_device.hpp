@@ -391,7 +391,10 @@ __device__ inline bool polar3(const double* a, double* Q) {
     double n2 = 0.0;
 #pragma unroll
     for (int i = 0; i < 9; ++i) n2 += X[i] * X[i];
-    const double nX = sqrt(n2);
+    // (norms and the scale in fp32: they only steer the convergence -- any
+    // g > 0 keeps the polar factor -- and the singularity test is a bound)
+    const float nXf = n2 < 1e30 ? sqrtf((float)n2) : (float)sqrt(n2);
+    const double nX = (double)nXf;
     // numerically singular (condition ~ nX^3 / |det| beyond ~1e12)
     if (!(fabs(det) > 1e-12 * nX * nX * nX)) return false;
     const double id = 1.0 / det;
@@ -401,7 +404,8 @@ __device__ inline bool polar3(const double* a, double* Q) {
       C[i] *= id;
       ni2 += C[i] * C[i];
     }
-    const double g = it < kPolarScaled ? sqrt(sqrt(ni2) / nX) : 1.0;
+    const double g =
+        it < kPolarScaled ? (double)sqrtf(sqrtf((float)fmin(ni2, 1e30)) / nXf) : 1.0;
     const double ig = 1.0 / g;
     double diff = 0.0;
 #pragma unroll
@@ -410,7 +414,9 @@ __device__ inline bool polar3(const double* a, double* Q) {
       diff += (xn - X[i]) * (xn - X[i]);
       X[i] = xn;
     }
-    if (it >= kPolarMinIt && diff <= 1e-30 * 3.0) {
+    // quadratic convergence: a step that moved X by <= ~1e-9 leaves it
+    // within ~1e-18 of the polar factor, below fp64 resolution
+    if (it >= kPolarMinIt && diff <= 1e-18) {
 #pragma unroll
       for (int i = 0; i < 9; ++i) Q[i] = X[i];
       return true;
