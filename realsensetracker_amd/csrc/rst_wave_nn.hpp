@@ -1468,19 +1468,27 @@ __device__ __forceinline__ bool pix_tile_search(const BvhView& bv, const PixView
     }
     wave_sync();
     if (ok) {
+      // four pixels' LDS reads in flight at a time (a dependent read per
+      // pixel would leave the scan bound by LDS latency); an invalid pixel
+      // is NaN, so its distance fails every test
       for (int b = b0; b <= b1; ++b) {
         const int row = moff + (b - my) * mw - mx - c0;
-        for (int a = a0; a <= a1; ++a) {
-          const int k = row + a;
-          if ((uint32_t)k < (uint32_t)cnt) {
-            const int p = ts.pos[k];
-            if (p >= 0) {
-              const float4 t = ts.pts[k];
-              const float d = d2_ref(qx, qy, qz, t.x, t.y, t.z);
-              if (d <= r.d[1]) {  // (offer's own test, hoisted: most pixels are farther)
-                r.offer(d, f2i(t.w), p);
-                if (r.pos[0] == p) q0 = t;
-              }
+        for (int a = a0; a <= a1; a += 4) {
+          float4 t[4];
+          int pp[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int k = row + a + j;
+            const bool in = a + j <= a1 && (uint32_t)k < (uint32_t)cnt;
+            t[j] = in ? ts.pts[k] : make_float4(NAN, NAN, NAN, 0.f);
+            pp[j] = in ? ts.pos[k] : -1;
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float d = d2_ref(qx, qy, qz, t[j].x, t[j].y, t[j].z);
+            if (pp[j] >= 0 && d <= r.d[1]) {  // (offer's own test, hoisted)
+              r.offer(d, f2i(t[j].w), pp[j]);
+              if (r.pos[0] == pp[j]) q0 = t[j];
             }
           }
         }
