@@ -550,6 +550,12 @@ def main():
     if rank != 0:
         rdv.close()
         return 0
+    # the measured HBM ceiling on this box (stream copy, read + write bytes),
+    # next to the spec peak the fraction is read against
+    gb = C.c_double(0.0)
+    cf = L.lib().rst_debug_stream_copy
+    cf.restype, cf.argtypes = C.c_int, [C.c_void_p, C.c_int64, C.c_int, C.POINTER(C.c_double)]
+    copy_gbps = gb.value if cf(actx[0].handle, 1 << 30, 5, C.byref(gb)) == 0 else None
     cpu = None
     if not a.no_cpu and world == 1:
         cpu = cpu_baseline(a.width, a.height, a.cpu_iters, pyr_iters if pyr else None)
@@ -581,6 +587,7 @@ def main():
         **({"iterations_all_levels_per_s": iters_raw / dt} if pyr else {}),
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "stream_copy_GBps": copy_gbps,
                      "kernel": "k_icp_nn+k_icp_fb (one ICP iteration's NN pass: certificate "
                                "stream + compacted searches)",
                      "avg_us": nn_us, "alg_bytes_per_launch": alg_bytes,

@@ -59,6 +59,12 @@ int rst_debug_seq_sum4(rst_ctx* ctx, const float* xyzw, int64_t n, float out[4])
 int rst_debug_seq_sum(rst_ctx* ctx, const float* xyzw, int64_t n, int serial, int reps,
                       float out[4], float* ms, int32_t* stats);
 
+/* A device stream copy (the measured HBM ceiling the rooflines are read
+ * against): `bytes` copied buffer to buffer by a float4 grid-stride kernel,
+ * reps launches timed with HIP events; *gbps = (read + write bytes) / the
+ * best launch's time. */
+int rst_debug_stream_copy(rst_ctx* ctx, int64_t bytes, int reps, double* gbps);
+
 /* The target's leaf table: lstart[0 .. nleaves] (leaf L holds sorted
  * positions [lstart[L], lstart[L+1])) copied to the host when cap >=
  * nleaves + 1, and pleaf[0 .. m) (the leaf of each sorted position) when

@@ -146,6 +146,18 @@ static int upload_xyz(rst_ctx* ctx, const float* h, int64_t n, float** d_out) {
   return RST_OK;
 }
 
+// the measured HBM ceiling (rst_debug_stream_copy): a grid-stride float4 copy,
+// nontemporal (streaming) loads and stores
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void k_stream_copy(const float4* __restrict__ a,
+                                                     float4* __restrict__ b, int64_t n4) {
+  const f32x4* __restrict__ av = reinterpret_cast<const f32x4*>(a);
+  f32x4* __restrict__ bv = reinterpret_cast<f32x4*>(b);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride)
+    __builtin_nontemporal_store(__builtin_nontemporal_load(av + i), bv + i);
+}
+
 }  // namespace rst
 
 using namespace rst;
@@ -512,6 +524,43 @@ int rst_debug_target_leaves(rst_ctx* ctx, const rst_target* t, int32_t* lstart, 
     RST_HIP(hipMemcpyAsync(pleaf, t->pleaf, sizeof(int32_t) * t->m, hipMemcpyDeviceToHost,
                            ctx->stream));
   RST_HIP(hipStreamSynchronize(ctx->stream));
+  return RST_OK;
+}
+
+int rst_debug_stream_copy(rst_ctx* ctx, int64_t bytes, int reps, double* gbps) {
+  if (!ctx || !gbps || bytes < 16 || reps < 1) return RST_E_ARG;
+  RST_HIP(hipSetDevice(ctx->device));
+  const int64_t n4 = bytes / 16;
+  float4 *a = nullptr, *b = nullptr;
+  if (hipMalloc(&a, 16 * n4) != hipSuccess) return RST_E_NOMEM;
+  if (hipMalloc(&b, 16 * n4) != hipSuccess) {
+    (void)hipFree(a);
+    return RST_E_NOMEM;
+  }
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  int s = RST_OK;
+  if (hipMemsetAsync(a, 0, 16 * n4, ctx->stream) != hipSuccess ||
+      hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess)
+    s = RST_E_HIP;
+  float best = 0.f;
+  for (int r = 0; r < reps && s >= 0; ++r) {
+    if (hipEventRecord(e0, ctx->stream) != hipSuccess) s = RST_E_HIP;
+    k_stream_copy<<<8192, 256, 0, ctx->stream>>>(a, b, n4);
+    if (s >= 0 && (hipGetLastError() != hipSuccess || hipEventRecord(e1, ctx->stream) != hipSuccess ||
+                   hipEventSynchronize(e1) != hipSuccess))
+      s = RST_E_HIP;
+    float ms = 0.f;
+    if (s >= 0 && hipEventElapsedTime(&ms, e0, e1) == hipSuccess && ms > 0.f &&
+        (best == 0.f || ms < best))
+      best = ms;
+  }
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
+  (void)hipStreamSynchronize(ctx->stream);
+  (void)hipFree(a);
+  (void)hipFree(b);
+  if (s < 0) return s;
+  *gbps = best > 0.f ? 2.0 * 16.0 * (double)n4 / (best * 1e-3) / 1e9 : 0.0;
   return RST_OK;
 }
 

@@ -21,11 +21,19 @@ def declared_functions() -> list[str]:
     return sorted(set(re.findall(r"\b(rst_[a-z0-9_]+)\s*\(", src)))
 
 
+def declared_debug_functions() -> list[str]:
+    src = (ROOT / "include" / "rst_debug.h").read_text()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(rst_[a-z0-9_]+)\s*\(", src)))
+
+
 def test_header_symbols_exported():
     names = declared_functions()
     assert len(names) >= 35
+    dbg = declared_debug_functions()
+    assert "rst_debug_stream_copy" in dbg
     lib = C.CDLL(str(L.LIB_PATH))
-    missing = [n for n in names if not hasattr(lib, n)]
+    missing = [n for n in names + dbg if not hasattr(lib, n)]
     assert not missing, missing
 
 
