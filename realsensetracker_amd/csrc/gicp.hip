@@ -61,20 +61,16 @@ struct GicpState {
 };
 
 // ---- ComputeCovariances ------------------------------------------------------------
-__global__ __launch_bounds__(kBS) void k_covariances(BvhView bv, int32_t pos0, int use_gicp,
-                                                     float* __restrict__ covs) {
-  const int64_t p = blockIdx.x * (int64_t)kBS + threadIdx.x;
-  if (p >= bv.m) return;
-  const float4 q = bv.pts[p];
-  BestK<kKnn> L;
-  L.init();
-  search(bv, (int)p, q.x, q.y, q.z, L);
-  // (:121-127) fp32 centroid of results 1..32 in result order; a slot the
-  // search could not fill is index 0, as the reference's out-parameters
+// (:121-158) the covariance of one point from its 33 nearest (sorted
+// positions in result order, < 0: a slot the search could not fill, which
+// the reference's out-parameters leave at index 0): fp32 centroid of results
+// 1..32, fp32 outer-product sums, then the GICP plane form or / 31
+__device__ __forceinline__ void cov_from_results(const BvhView& bv, int32_t pos0, int use_gicp,
+                                                 const int* pos, int orig, float* covs) {
   float cx = 0.f, cy = 0.f, cz = 0.f;
 #pragma unroll
   for (int j = 1; j < kKnn; ++j) {
-    const float4 o = bv.pts[L.pos[j] >= 0 ? L.pos[j] : pos0];
+    const float4 o = bv.pts[pos[j] >= 0 ? pos[j] : pos0];
     cx = cx + o.x;
     cy = cy + o.y;
     cz = cz + o.z;
@@ -87,14 +83,14 @@ __global__ __launch_bounds__(kBS) void k_covariances(BvhView bv, int32_t pos0, i
   for (int k = 0; k < 9; ++k) c[k] = 0.f;
 #pragma unroll
   for (int j = 1; j < kKnn; ++j) {  // (:130-135)
-    const float4 o = bv.pts[L.pos[j] >= 0 ? L.pos[j] : pos0];
+    const float4 o = bv.pts[pos[j] >= 0 ? pos[j] : pos0];
     const float d[3] = {o.x - cx, o.y - cy, o.z - cz};
 #pragma unroll
     for (int cc = 0; cc < 3; ++cc)
 #pragma unroll
       for (int r = 0; r < 3; ++r) c[cc * 3 + r] = c[cc * 3 + r] + d[r] * d[cc];
   }
-  float* out = covs + 9 * (int64_t)f2i(q.w);
+  float* out = covs + 9 * (int64_t)orig;
   if (use_gicp) {  // (:139-155): U diag(1, 1, 1e-2) U^T = I - 0.99 u3 u3^T
     double a[9], U[9], S[3], V[9];
 #pragma unroll
@@ -114,6 +110,106 @@ __global__ __launch_bounds__(kBS) void k_covariances(BvhView bv, int32_t pos0, i
 #pragma unroll
     for (int k = 0; k < 9; ++k) out[k] = c[k] / 31.0f;  // (:158)
   }
+}
+
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t y = ((uint64_t)(uint32_t)__shfl_xor((int)(x >> 32), o, 64) << 32) |
+                       (uint32_t)__shfl_xor((int)(uint32_t)x, o, 64);
+    x = y < x ? y : x;
+  }
+  return x;
+}
+
+// (d2, original index) as one ordered key: d2 >= 0 (or +inf), so its bits
+// order as the float; the lexicographic order of BestK / Best1
+__device__ __forceinline__ uint64_t nn_key(float d2, int id) {
+  return ((uint64_t)(uint32_t)f2i(d2) << 32) | (uint32_t)id;
+}
+
+// Small clouds (GICP's voxel-downsampled frames, a few thousand points):
+// one wavefront per point, every target point's key staged in LDS (the
+// lanes stride the cloud), then the 33 smallest keys extracted in order,
+// one wave minimum per result -- the same exact 33-NN in the same order as
+// the per-lane BVH search (k_covariances), on a wavefront per point instead
+// of a lane: the BVH kernel leaves a 4k-point cloud on 18 of 256 CUs.
+constexpr int kCovWaveMax = 8000;  // LDS keys per wavefront (< 64 KB with the result slots)
+__global__ __launch_bounds__(kWave) void k_covariances_wave(BvhView bv, int32_t pos0,
+                                                            int use_gicp,
+                                                            float* __restrict__ covs) {
+  extern __shared__ uint64_t keys[];  // [m]
+  __shared__ int res[kKnn];
+  const int p = blockIdx.x;  // sorted position of the point
+  const int lane = threadIdx.x;
+  const int m = bv.m;
+  const float4 q = bv.pts[p];
+  for (int j = lane; j < m; j += kWave) {
+    const float4 t = bv.pts[j];
+    keys[j] = nn_key(d2_ref(q.x, q.y, q.z, t.x, t.y, t.z), f2i(t.w));
+  }
+  __syncthreads();  // (one wavefront per block)
+  uint64_t last = 0;
+  for (int k = 0; k < kKnn; ++k) {
+    uint64_t best = ~0ull;
+    int bj = -1;
+    for (int j = lane; j < m; j += kWave) {
+      const uint64_t x = keys[j];
+      if ((k == 0 || x > last) && x < best) {
+        best = x;
+        bj = j;
+      }
+    }
+    const uint64_t w = wave_min_u64(best);
+    const uint64_t bm = __ballot(bj >= 0 && best == w);
+    const int src = bm ? __ffsll((long long)bm) - 1 : 0;
+    const int wj = __shfl(bj, src, kWave);
+    if (lane == 0) res[k] = bm ? wj : -1;
+    last = w;
+  }
+  __syncthreads();  // (one wavefront per block)
+  if (lane == 0) {
+    int pos[kKnn];
+#pragma unroll
+    for (int k = 0; k < kKnn; ++k) pos[k] = res[k];
+    cov_from_results(bv, pos0, use_gicp, pos, f2i(q.w), covs);
+  }
+}
+
+// Exact NN of each query over a small cloud, one wavefront per query (the
+// lanes stride the cloud, a wave minimum of the (d2, index) keys): GICP's
+// per-round correspondences, where the BVH kernel's one lane per query
+// leaves the GPU idle.
+__global__ __launch_bounds__(kBS) void k_query_nn_wave(BvhView bv, const float* __restrict__ q,
+                                                       int64_t nq, int32_t* __restrict__ idx,
+                                                       float* __restrict__ d2) {
+  const int64_t i = (int64_t)blockIdx.x * (kBS / kWave) + threadIdx.x / kWave;
+  if (i >= nq) return;  // (uniform per wave)
+  const int lane = threadIdx.x & (kWave - 1);
+  const float qx = q[3 * i], qy = q[3 * i + 1], qz = q[3 * i + 2];
+  uint64_t best = ~0ull;
+  for (int j = lane; j < bv.m; j += kWave) {
+    const float4 t = bv.pts[j];
+    const uint64_t x = nn_key(d2_ref(qx, qy, qz, t.x, t.y, t.z), f2i(t.w));
+    best = x < best ? x : best;
+  }
+  best = wave_min_u64(best);
+  if (lane == 0) {
+    idx[i] = best == ~0ull ? -1 : (int32_t)(uint32_t)best;
+    d2[i] = best == ~0ull ? FLT_MAX : i2f((int)(best >> 32));
+  }
+}
+
+
+__global__ __launch_bounds__(kBS) void k_covariances(BvhView bv, int32_t pos0, int use_gicp,
+                                                     float* __restrict__ covs) {
+  const int64_t p = blockIdx.x * (int64_t)kBS + threadIdx.x;
+  if (p >= bv.m) return;
+  const float4 q = bv.pts[p];
+  BestK<kKnn> L;
+  L.init();
+  search(bv, (int)p, q.x, q.y, q.z, L);
+  cov_from_results(bv, pos0, use_gicp, L.pos, f2i(q.w), covs);
 }
 
 // ---- per-correspondence evaluation ---------------------------------------------------
@@ -627,8 +723,12 @@ int lm_solve(rst_ctx* ctx, const float* ds, int64_t n, const float* dd, const fl
 int compute_covariances_device(rst_ctx* ctx, const rst_target* tgt, int use_gicp, float* d_covs) {
   if (!tgt->has_bvh) return RST_E_STATE;
   if (tgt->m == 0) return RST_OK;
-  k_covariances<<<blocks_for(tgt->m), kBS, 0, ctx->stream>>>(view_of(tgt), tgt->pos0, use_gicp,
-                                                             d_covs);
+  if (tgt->m <= kCovWaveMax)
+    k_covariances_wave<<<(unsigned)tgt->m, kWave, sizeof(uint64_t) * tgt->m, ctx->stream>>>(
+        view_of(tgt), tgt->pos0, use_gicp, d_covs);
+  else
+    k_covariances<<<blocks_for(tgt->m), kBS, 0, ctx->stream>>>(view_of(tgt), tgt->pos0, use_gicp,
+                                                               d_covs);
   RST_HIP(hipGetLastError());
   return RST_OK;
 }
@@ -734,7 +834,16 @@ int rst_gicp_align(rst_ctx* ctx, const float* src, int64_t n, const float* dst, 
   if (s >= 0) s = upload(st, gs, &h, sizeof(h));
   for (int o = 0; s >= 0 && o < outer_iters; ++o) {
     k_gicp_xform<<<blocks_for(n), kBS, 0, st>>>(ds, n, gs, dtmp);
-    s = query_nn_device(ctx, td, dtmp, n, di, dd2);  // FindCorrespondences (:140-141)
+    // FindCorrespondences (:140-141): exact NN, from the last round's
+    // neighbours after the first (the estimate moves little between rounds)
+    if (m <= kCovWaveMax) {
+      k_query_nn_wave<<<(unsigned)((n + kBS / kWave - 1) / (kBS / kWave)), kBS, 0, st>>>(
+          view_of(td), dtmp, n, di, dd2);
+      s = hipGetLastError() == hipSuccess ? RST_OK : RST_E_HIP;
+    } else {
+      s = o == 0 ? query_nn_device(ctx, td, dtmp, n, di, dd2)
+                 : query_nn_warm_device(ctx, td, dtmp, n, di, di, dd2);
+    }
     if (s >= 0) s = lm_solve(ctx, ds, n, dd, dcs, dcd, di, gs, slab, max_inner);
   }
   if (s >= 0 && hipMemcpyAsync(&h, gs, sizeof(h), hipMemcpyDeviceToHost, st) != hipSuccess)
