@@ -43,7 +43,7 @@ constexpr int kNP2Plane = 30;  // A (21), b (6), sum w r^2, count, sum d2
 // search.  nnq[i].w carries kCertBit while the certificate of its point
 // holds.  Kernel 1 makes certificates for near points too (adj_search2).
 #ifndef RST_FB_MIN_WAVES
-#define RST_FB_MIN_WAVES 4  // k_icp_fb<P2PointAcc>: 128 VGPRs (1 spill); r01h A/B 15.8k -> 16.2k it/s; r01k: 3 -> 16.7k, 5 -> 15.6k vs 17.1k
+#define RST_FB_MIN_WAVES 4  // k_icp_fb occupancy target (r01: 128 VGPRs, 4 waves/SIMD; r02: the kernel's paths need 201, the compiler settles at 2 waves/SIMD; forcing 3 spills: 22.8k vs 23.6k it/s)
 #endif
 constexpr int kCertBit = 1 << 30;
 #ifndef RST_NN_MIN_WAVES
