@@ -68,6 +68,9 @@ constexpr int kCertBit = 1 << 30;
 #ifndef RST_ROW_PIX
 #define RST_ROW_PIX 1  // k_icp_fb's rows scan the pixel window before the leaf adjacency
 #endif
+#ifndef RST_PIX_ITERS
+#define RST_PIX_ITERS (1 << 30)  // k_icp_nn's pixel windows in a pair's first iterations (r02: 24 -> 11.7 ms per pair alone vs 13.2, but 20.7k vs 23.6k it/s with 4 pairs in flight; default: all)
+#endif
 #ifndef RST_PIX_CHUNK
 #define RST_PIX_CHUNK 256  // pixels staged per wave and round (5 KB of LDS per wave)
 #endif
@@ -641,7 +644,11 @@ __global__ __launch_bounds__(kBS) void k_icp_nn(BvhView bv, AdjView av, PixView 
     d0 = has_cert ? dq : d2_ref(px, py, pz, tq.x, tq.y, tq.z);
   }
 #if RST_PIX_TILES
-  if (pv.map) {  // frame target (uniform): the pixel-window search, exact where it applies
+  // frame target (uniform): the pixel-window search, exact where it
+  // applies.  (RST_PIX_ITERS limits it to a pair's first iterations, the
+  // few uncertified points of the steady state then go to k_icp_fb's rows:
+  // a lower latency per pair, a lower throughput with pairs in flight.)
+  if (pv.map && st->iter < RST_PIX_ITERS) {
     Best2 pr;
     pr.init();
     float4 pq = make_float4(0.f, 0.f, 0.f, 0.f);
