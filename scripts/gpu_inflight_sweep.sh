@@ -3,7 +3,7 @@
 #   SWEEP="4:8 6:8 8:16" bash scripts/gpu_inflight_sweep.sh
 set -o pipefail
 mkdir -p gpurun_out
-for c in ${SWEEP:-4:8 6:12 8:16 12:16}; do
+for c in ${SWEEP:-4:24 6:24 8:24}; do
   inf=${c%%:*}; hq=${c#*:}
   f=gpurun_out/sweep_${inf}_${hq}.log
   timeout -k 10 300 python bench.py --inflight $inf --hw-queues $hq --no-cpu --no-p2plane --no-host-api --no-gicp --ref-steps 0 $EXTRA > $f 2>&1 || exit $?
