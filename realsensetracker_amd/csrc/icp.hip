@@ -110,7 +110,7 @@ __device__ __forceinline__ int xcd_tile(int b, int nb) {
 constexpr int kFarBit = 1 << 29;
 constexpr int kPosMask = kFarBit - 1;
 constexpr int kFbBlocks = 2048;  // largest fallback grid (RST_FB_BLOCKS)
-constexpr int kFbDefault = 1024;  // fallback grid (4096 waves; r01g sweep: 2048 / 512 lose)
+constexpr int kFbDefault = 384;  // fallback grid (r02 sweep, pixel windows in k_icp_nn: 384 -> 26.2k it/s, 256 26.3k, 512 25.8k, 1024 23.5k; 720p 7.0k vs 6.4k, 720p pyramid 137 vs 130 frames/s)
 // From a queue of lane_min entries (IcpParams: the cold first iterations,
 // where most lanes' last neighbour is far or missing) kernel 2 finishes the
 // queries its adjacency search leaves open one lane per query instead of
