@@ -176,6 +176,14 @@ __global__ __launch_bounds__(kWave) void k_covariances_wave(BvhView bv, int32_t 
   }
 }
 
+// A cloud as the brute-force kernels read it: (x, y, z, index bits) in input
+// order (sorted position = original index, so pos0 = 0)
+__global__ __launch_bounds__(kBS) void k_pack4(const float* __restrict__ xyz, int64_t n,
+                                               float4* __restrict__ out) {
+  const int64_t i = blockIdx.x * (int64_t)kBS + threadIdx.x;
+  if (i < n) out[i] = make_float4(xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2], i2f((int)i));
+}
+
 // Exact NN of each query over a small cloud, one wavefront per query (the
 // lanes stride the cloud, a wave minimum of the (d2, index) keys): GICP's
 // per-round correspondences, where the BVH kernel's one lane per query
@@ -647,8 +655,8 @@ inline int blocks_for(int64_t n, int per = kBS) {
 // device buffers of one GICP problem (all context-pool allocations)
 struct Bufs {
   rst_ctx* ctx = nullptr;
-  void* p[8] = {};
-  size_t c[8] = {};
+  void* p[12] = {};
+  size_t c[12] = {};
   int k = 0;
   int get(size_t bytes, void** out) {
     const int s = ctx_alloc(ctx, std::max<size_t>(bytes, 16), &p[k], &c[k]);
@@ -821,12 +829,40 @@ int rst_gicp_align(rst_ctx* ctx, const float* src, int64_t n, const float* dst, 
   slab = (double*)(gs + 1);
   RST_CHECK(upload(st, ds, src, sizeof(float) * 3 * n));
   RST_CHECK(upload(st, dd, dst, sizeof(float) * 3 * m));
-  // (:112-123) indices of both clouds, covariances (k = 32, use_gicp = false)
+  // (:112-123) indices of both clouds, covariances (k = 32, use_gicp = false).
+  // Small finite clouds (the downsampled frames) need no index: the
+  // wave-per-point kernels scan them whole, in input order
+  auto finite_all = [](const float* a, int64_t k) {
+    for (int64_t i = 0; i < 3 * k; ++i)
+      if (!std::isfinite(a[i])) return false;
+    return true;
+  };
+  const bool flat = n <= kCovWaveMax && m <= kCovWaveMax && finite_all(src, n) &&
+                    finite_all(dst, m);
   rst_target *ts = nullptr, *td = nullptr;
-  int s = target_build_device(ctx, ds, n, true, &ts);
-  if (s >= 0) s = target_build_device(ctx, dd, m, true, &td);
-  if (s >= 0) s = compute_covariances_device(ctx, ts, 0, dcs);
-  if (s >= 0) s = compute_covariances_device(ctx, td, 0, dcd);
+  BvhView vd = {};
+  int s = RST_OK;
+  if (flat) {
+    float4 *s4 = nullptr, *d4 = nullptr;
+    RST_CHECK(b.get(sizeof(float4) * n, (void**)&s4));
+    RST_CHECK(b.get(sizeof(float4) * m, (void**)&d4));
+    k_pack4<<<blocks_for(n), kBS, 0, st>>>(ds, n, s4);
+    k_pack4<<<blocks_for(m), kBS, 0, st>>>(dd, m, d4);
+    BvhView vs = {};
+    vs.pts = s4;
+    vs.m = (int32_t)n;
+    vd.pts = d4;
+    vd.m = (int32_t)m;
+    k_covariances_wave<<<(unsigned)n, kWave, sizeof(uint64_t) * n, st>>>(vs, 0, 0, dcs);
+    k_covariances_wave<<<(unsigned)m, kWave, sizeof(uint64_t) * m, st>>>(vd, 0, 0, dcd);
+    if (hipGetLastError() != hipSuccess) s = RST_E_HIP;
+  } else {
+    s = target_build_device(ctx, ds, n, true, &ts);
+    if (s >= 0) s = target_build_device(ctx, dd, m, true, &td);
+    if (s >= 0) s = compute_covariances_device(ctx, ts, 0, dcs);
+    if (s >= 0) s = compute_covariances_device(ctx, td, 0, dcd);
+    if (s >= 0) vd = view_of(td);
+  }
   // (:127-160) estimate = Identity; outer loop
   GicpState h;
   memset(&h, 0, sizeof(h));
@@ -838,7 +874,7 @@ int rst_gicp_align(rst_ctx* ctx, const float* src, int64_t n, const float* dst, 
     // neighbours after the first (the estimate moves little between rounds)
     if (m <= kCovWaveMax) {
       k_query_nn_wave<<<(unsigned)((n + kBS / kWave - 1) / (kBS / kWave)), kBS, 0, st>>>(
-          view_of(td), dtmp, n, di, dd2);
+          vd, dtmp, n, di, dd2);
       s = hipGetLastError() == hipSuccess ? RST_OK : RST_E_HIP;
     } else {
       s = o == 0 ? query_nn_device(ctx, td, dtmp, n, di, dd2)
