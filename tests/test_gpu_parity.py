@@ -856,6 +856,21 @@ def test_covariances_match_oracle(ctx, use_gicp):
         np.testing.assert_allclose(got, want, rtol=1e-6, atol=1e-12)
 
 
+@pytest.mark.parametrize("voxel", [0.03, 0.1])
+def test_covariances_both_kernels_match_oracle(ctx, voxel):
+    """ComputeCovariances on both sides of the kernel switch: clouds up to
+    8,000 points take the wavefront-per-point kernel (every key in LDS, 33
+    ordered wave minima), larger ones the per-lane BVH kNN; both must give
+    the oracle's neighbours in the oracle's order (fp32 sums equal)."""
+    g = load_golden("pair_160x120_s2")
+    src = O.downsample_voxel(g["src"], voxel)
+    assert (len(src) > 8000) == (voxel < 0.05), len(src)
+    t = A.Target.build(src, ctx)
+    got = A.ComputeCovariances(t, src, use_gicp=False)
+    want = O.compute_covariances(src, use_gicp=False)
+    np.testing.assert_allclose(got, want, rtol=1e-6, atol=1e-12)
+
+
 def test_gicp_solve_matches_oracle(ctx):
     src, dst, T = _gicp_pair()
     cs, cd = O.compute_covariances(src), O.compute_covariances(dst)
