@@ -899,6 +899,22 @@ def test_gicp_align_matches_oracle_and_motion(ctx):
     assert np.isfinite(cost)
 
 
+def test_gicp_align_indexed_path_matches_oracle(ctx):
+    """Clouds over 8,000 points keep the indexed path (BVH covariances,
+    cold then warm BVH correspondences): 3 rounds of up to 16 LM
+    evaluations against the C restatement."""
+    g = load_golden("pair_160x120_s2")
+    src, dst = O.downsample_voxel(g["src"], 0.05), O.downsample_voxel(g["dst"], 0.05)
+    assert len(src) > 8000 and len(dst) > 8000
+    out = np.zeros(16, np.float32)
+    c = C.c_double(0)
+    assert L.lib().rst_gicp_align(ctx.handle, L.fptr(src), len(src), L.fptr(dst), len(dst), 3,
+                                  16, L.fptr(out), C.byref(c)) == L.RST_OK
+    F, P = O.gicp_align(src, dst, 3, 16)
+    assert max(pose_err(L.cm_to_pose(out), P)) <= 1e-5
+    assert abs(c.value - F) <= 1e-6 * F
+
+
 def test_gicp_contract(ctx):
     src, dst, _ = _gicp_pair()
     cs = np.zeros((len(src), 9), np.float32)
