@@ -49,15 +49,24 @@ int rst_debug_query_nn_fallback(rst_ctx* ctx, const rst_target* tgt, const float
 int rst_debug_seq_sum4(rst_ctx* ctx, const float* xyzw, int64_t n, float out[4]);
 
 /* The same sums by either kernel: serial = 0 the loop's parallel exact
- * path (seqsum.hip: exponent-window run maps + one walking wavefront per
- * component), serial = 1 the one-wavefront dependent chain (k_seq_sum4);
- * reps launches back to back, *ms (optional) = device time per launch;
- * stats (optional, parallel path) = 8 int32 per component of the last
- * launch's walk: superblock tries / jumps, block tries / jumps, serial
- * blocks, zero blocks skipped, shader clocks in serial blocks, shader
- * clocks of the whole walk. */
+ * path (seqsum.hip: verified block / group / superblock maps, one walking
+ * wavefront per component), serial = 1 the one-wavefront dependent chain
+ * (k_seq_sum4); reps launches back to back, *ms (optional) = device time
+ * per launch; stats (optional, parallel path, 40 int32) = 8 per component
+ * of the last launch's walk: superblock tries / hits, group tries / hits,
+ * block tries / hits, blocks added serially, walker clocks; stats[32] =
+ * the map kernels' bound-check failure bits (0 = none). */
 int rst_debug_seq_sum(rst_ctx* ctx, const float* xyzw, int64_t n, int serial, int reps,
                       float out[4], float* ms, int32_t* stats);
+
+/* The sequential sums' kernels one at a time (stages: bit 0 the front
+ * kernel, bit 1 the maps, bit 2 the walk), each synchronised and checked
+ * before the next is launched; the workspace (rst_debug_seq_ws_bytes(n)
+ * bytes, zeroed first) is copied to ws_out (optional) afterwards, and
+ * *failed_stage names the first kernel that failed (0 = none). */
+int rst_debug_seq_stages(rst_ctx* ctx, const float* xyzw, int64_t n, int nch, int stages,
+                         float out[4], void* ws_out, int64_t ws_bytes, int* failed_stage);
+int64_t rst_debug_seq_ws_bytes(int64_t n);
 
 /* A device stream copy (the measured HBM ceiling the rooflines are read
  * against): `bytes` copied buffer to buffer by a float4 grid-stride kernel,

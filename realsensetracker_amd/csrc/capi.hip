@@ -597,7 +597,7 @@ int rst_debug_seq_sum(rst_ctx* ctx, const float* xyzw, int64_t n, int serial, in
     *ms = t / (float)reps;
   }
   if (s >= 0 && stats && !serial &&
-      hipMemcpy(stats, dstats, sizeof(int) * 32, hipMemcpyDeviceToHost) != hipSuccess)
+      hipMemcpy(stats, dstats, sizeof(int) * 40, hipMemcpyDeviceToHost) != hipSuccess)
     s = RST_E_HIP;
   hipStreamSynchronize(ctx->stream);
   if (e0) hipEventDestroy(e0);
@@ -605,6 +605,47 @@ int rst_debug_seq_sum(rst_ctx* ctx, const float* xyzw, int64_t n, int serial, in
   hipFree(d);
   return s;
 }
+
+int rst_debug_seq_stages(rst_ctx* ctx, const float* xyzw, int64_t n, int nch, int stages,
+                         float out[4], void* ws_out, int64_t ws_bytes, int* failed_stage) {
+  if (!ctx || !out || n < 1 || !xyzw || nch < 1 || nch > 4 || !failed_stage) return RST_E_ARG;
+  RST_HIP(hipSetDevice(ctx->device));
+  *failed_stage = 0;
+  const size_t sqb = seqsum_bytes(n);
+  if (ws_out && ws_bytes < (int64_t)sqb) return RST_E_ARG;
+  void* d = nullptr;
+  const size_t xb = (sizeof(float4) * (size_t)n + 255) & ~(size_t)255;
+  if (hipMalloc(&d, xb + 256 + sqb) != hipSuccess) return RST_E_NOMEM;
+  float* dout = (float*)((char*)d + xb);
+  void* ws = (char*)d + xb + 256;
+  int s = RST_OK;
+  if (hipMemsetAsync(d, 0, xb + 256 + sqb, ctx->stream) != hipSuccess ||
+      hipMemcpyAsync(d, xyzw, sizeof(float4) * n, hipMemcpyHostToDevice, ctx->stream) != hipSuccess ||
+      hipStreamSynchronize(ctx->stream) != hipSuccess)
+    s = RST_E_HIP;
+  // one kernel at a time, each checked before the next is launched
+  for (int b = 0; b < 3 && s >= 0; ++b) {
+    if (!(stages & (1 << b))) continue;
+    s = seqsum_enqueue((const float4*)d, n, nch, ws, dout, ctx->stream, nullptr, 1 << b);
+    if (s < 0) {
+      fprintf(stderr, "[rst] seq stage %d: launch failed: %s\n", b + 1, g_last_error);
+    } else {
+      const hipError_t e = hipStreamSynchronize(ctx->stream);
+      if (e != hipSuccess) {
+        fprintf(stderr, "[rst] seq stage %d: execution failed: %s (%s)\n", b + 1, hipGetErrorName(e),
+                hipGetErrorString(e));
+        s = RST_E_HIP;
+      }
+    }
+    if (s < 0) *failed_stage = b + 1;
+  }
+  if (s >= 0 && hipMemcpy(out, dout, sizeof(float) * 4, hipMemcpyDeviceToHost) != hipSuccess) s = RST_E_HIP;
+  if (s >= 0 && ws_out && hipMemcpy(ws_out, ws, sqb, hipMemcpyDeviceToHost) != hipSuccess) s = RST_E_HIP;
+  hipFree(d);
+  return s;
+}
+
+int64_t rst_debug_seq_ws_bytes(int64_t n) { return (int64_t)seqsum_bytes(std::max<int64_t>(n, 1)); }
 
 int rst_debug_seq_sum4(rst_ctx* ctx, const float* xyzw, int64_t n, float out[4]) {
   return rst_debug_seq_sum(ctx, xyzw, n, 0, 1, out, nullptr, nullptr);

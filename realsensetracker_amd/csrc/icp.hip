@@ -1637,7 +1637,9 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
       } else if (refsum) {
         RST_CHECK(nn_pass(AccTag<RefAcc>{}));
         // align_icp.cpp:113,120: sum dst[nbr_i] and cost, i ascending, fp32
-        RST_CHECK(seqsum_enqueue(corr, n_local, 4, sqws, ctx->d_state->seq, st));
+        // (the cost is only read after the last iteration, :104,157)
+        RST_CHECK(seqsum_enqueue(corr, n_local, it + 1 == opts.max_iter ? 4 : 3, sqws,
+                                 ctx->d_state->seq, st));
         k_cov_ref<<<kCovBlocks, kBS, 0, st>>>(srco, corr, n_local, ctx->d_state, slab2);
         k_reduce_solve<RefAcc><<<1, kRedBS, 0, st>>>(slab, 0, slab2, kCovBlocks, prm,
                                                      ctx->d_state, nullptr);

@@ -20,10 +20,11 @@ x = np.concatenate([p, (p * p).sum(1, keepdims=True)], 1).astype(np.float32)
 for serial, reps in ((0, 20), (1, 2)):
     out, ms = seq_sum(ctx, x, serial=serial, reps=reps)
     print("serial" if serial else "parallel", f"{ms * 1e3:.1f} us", same(out, want(x)))
-st = np.zeros((4, 8), np.int32)
+st = np.zeros((5, 8), np.int32)
 seq_sum(ctx, x, stats=st)
-print("walk stats per chain [l2 tries, l2 jumps, l1 tries, l1 jumps, serial, zero, -, -]")
-print(st)
+print("walk stats per chain [superblock tries, hits, group tries, hits, leaf tries, hits, serial blocks, walker clocks]")
+print(st[:4])
+print('bound-check error bits', st[4, 0])
 for c in range(4):
     y = np.zeros_like(x)
     y[:, c] = x[:, c]
