@@ -49,14 +49,54 @@ def rank_envs(nproc: int, port: int, base: dict | None = None,
     return out
 
 
-def launch(nproc: int, argv: list[str], script: str) -> int:
+def launch(nproc: int, argv: list[str], script: str, grace: float = 10.0,
+           poll: float = 0.05, timeout: float | None = None) -> int:
     """Run `script argv` as nproc rank processes; the job's exit status is
-    the worst rank's.  Called before anything touches the GPU."""
+    the first failing rank's (0 when all succeed).  Called before anything
+    touches the GPU.
+
+    All ranks are polled together: when one exits non-zero the others are
+    sent SIGTERM (a rank blocked in a collective would otherwise wait for
+    the dead peer until its own timeout), and whatever is still running
+    `grace` seconds later is killed.  `timeout` (seconds, None = none)
+    bounds the whole job the same way; the status is then 124."""
     envs = rank_envs(nproc, free_port())
     procs = [subprocess.Popen([sys.executable, script, *argv], env=e) for e in envs]
-    codes = [p.wait() for p in procs]
-    bad = [c for c in codes if c != 0]
-    return bad[0] if bad else 0
+    status = 0
+    t0 = time.monotonic()
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [c for c in codes if c is not None and c != 0]
+            if bad:
+                status = bad[0]
+                break
+            if all(c is not None for c in codes):
+                return 0
+            if timeout is not None and time.monotonic() - t0 > timeout:
+                status = 124
+                break
+            time.sleep(poll)
+    except BaseException:
+        _stop(procs, grace)
+        raise
+    _stop(procs, grace)
+    return status
+
+
+def _stop(procs: list[subprocess.Popen], grace: float) -> None:
+    """SIGTERM every rank still running, SIGKILL after `grace` seconds, and
+    reap them all."""
+    for p in procs:
+        if p.poll() is None:
+            p.terminate()
+    deadline = time.monotonic() + grace
+    for p in procs:
+        try:
+            p.wait(timeout=max(0.0, deadline - time.monotonic()))
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()
 
 
 def world_from_env() -> tuple[int, int, int]:

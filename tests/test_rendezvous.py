@@ -82,3 +82,48 @@ def test_launch_runs_every_rank(tmp_path):
         assert (tmp_path / f"rank{k}").read_text() == f"3 {k} 3.0"
     r = subprocess.run([sys.executable, "-c", code, "2", str(tmp_path), "fail"], timeout=120)
     assert r.returncode == 3
+
+
+def test_launch_stops_ranks_when_one_dies_early(tmp_path):
+    """A rank that exits non-zero before the collective: the launcher stops
+    the ranks blocked in it (they would otherwise wait out the rendezvous
+    timeout) and returns the failing rank's status promptly."""
+    import time
+
+    script = tmp_path / "early.py"
+    root = str(RV.__file__).rsplit("/realsensetracker_amd", 1)[0]
+    script.write_text(
+        "import sys\n"
+        f"sys.path.insert(0, {root!r})\n"
+        "from realsensetracker_amd import rendezvous as RV\n"
+        "w, r, lr = RV.world_from_env()\n"
+        "if r == 2:\n"
+        "    sys.exit(5)\n"
+        "rv = RV.Rendezvous(r, w, timeout=600)\n"
+        "rv.barrier()\n")
+    code = ("import sys; sys.path.insert(0, %r); from realsensetracker_amd import rendezvous as RV; "
+            "sys.exit(RV.launch(int(sys.argv[1]), sys.argv[2:], %r, grace=2.0))"
+            % (root, str(script)))
+    t0 = time.monotonic()
+    r = subprocess.run([sys.executable, "-c", code, "3"], timeout=120)
+    assert r.returncode == 5
+    assert time.monotonic() - t0 < 60
+
+
+def test_launch_kills_ranks_ignoring_sigterm(tmp_path):
+    """Ranks that ignore SIGTERM are killed after the grace period; the job
+    timeout reports 124."""
+    import time
+
+    script = tmp_path / "stubborn.py"
+    script.write_text(
+        "import signal, time\n"
+        "signal.signal(signal.SIGTERM, signal.SIG_IGN)\n"
+        "time.sleep(300)\n")
+    root = str(RV.__file__).rsplit("/realsensetracker_amd", 1)[0]
+    code = ("import sys; sys.path.insert(0, %r); from realsensetracker_amd import rendezvous as RV; "
+            "sys.exit(RV.launch(2, [], %r, grace=1.0, timeout=2.0))" % (root, str(script)))
+    t0 = time.monotonic()
+    r = subprocess.run([sys.executable, "-c", code], timeout=120)
+    assert r.returncode == 124
+    assert time.monotonic() - t0 < 30
