@@ -52,10 +52,13 @@ int rst_debug_seq_sum4(rst_ctx* ctx, const float* xyzw, int64_t n, float out[4])
  * path (seqsum.hip: verified block / group / superblock maps, one walking
  * wavefront per component), serial = 1 the one-wavefront dependent chain
  * (k_seq_sum4); reps launches back to back, *ms (optional) = device time
- * per launch; stats (optional, parallel path, 40 int32) = 8 per component
+ * per launch; stats (optional, parallel path, 64 int32) = 8 per component
  * of the last launch's walk: superblock tries / hits, group tries / hits,
  * block tries / hits, blocks added serially, walker clocks; stats[32] =
- * the map kernels' bound-check failure bits (0 = none). */
+ * the map kernels' bound-check failure bits (0 = none); stats[33 + c] =
+ * component c's walker clocks waiting for superblock maps; stats[40 + 4c
+ * + j] = its walker clock at the start of chunk j < 4 (16 superblocks a
+ * chunk). */
 int rst_debug_seq_sum(rst_ctx* ctx, const float* xyzw, int64_t n, int serial, int reps,
                       float out[4], float* ms, int32_t* stats);
 

@@ -168,6 +168,9 @@ def lib() -> C.CDLL:
             raise ImportError(
                 f"realsensetracker_amd: HIP library not built ({LIB_PATH}); run "
                 "`python -m realsensetracker_amd.build` (or __graft_entry__.build())")
+        # kernel arguments in device memory (the library's load-time default
+        # too; here for a runtime that initialises before the library loads)
+        os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
         L = C.CDLL(str(LIB_PATH), mode=C.RTLD_GLOBAL)
         rts = hip_runtimes_mapped()
         if len(rts) > 1:

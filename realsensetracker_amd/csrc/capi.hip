@@ -17,6 +17,13 @@ namespace rst {
 
 static thread_local char g_last_error[512] = {0};
 
+// Kernel arguments in device memory unless the environment says otherwise:
+// with the runtime's default (host memory) every kernel's first argument
+// load waited ~6k clocks on the host link (measured in k_sq_walk: its
+// prologue 7.7k -> 1.5k clocks).  Read by the HIP runtime when it
+// initialises, so set at load time, before this library's first HIP call.
+__attribute__((constructor)) static void rst_env_defaults() { setenv("HIP_FORCE_DEV_KERNARG", "1", 0); }
+
 void set_last_error(hipError_t e, const char* what, const char* file, int line) {
   snprintf(g_last_error, sizeof(g_last_error), "%s failed: %s (%s:%d)", what,
            hipGetErrorString(e), file, line);
@@ -597,7 +604,7 @@ int rst_debug_seq_sum(rst_ctx* ctx, const float* xyzw, int64_t n, int serial, in
     *ms = t / (float)reps;
   }
   if (s >= 0 && stats && !serial &&
-      hipMemcpy(stats, dstats, sizeof(int) * 40, hipMemcpyDeviceToHost) != hipSuccess)
+      hipMemcpy(stats, dstats, sizeof(int) * 64, hipMemcpyDeviceToHost) != hipSuccess)
     s = RST_E_HIP;
   hipStreamSynchronize(ctx->stream);
   if (e0) hipEventDestroy(e0);

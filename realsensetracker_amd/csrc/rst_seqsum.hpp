@@ -78,10 +78,13 @@ struct GroupMap {  // 4 + 48 = 52 dwords, padded to 64
   MapEnt e[kGroupR];
   int pad[12];
 };
-struct SbMap {  // 4 + 192 = 196 dwords, padded to 256
+struct SbMap {  // 4 + 192 + 6 = 202 dwords, padded to 256
   MapHdr h;
   MapEnt e[kSbR];
-  int pad[60];
+  // the superblock's group, block and element ranges [ga, gb), [ba, bb),
+  // [ea, eb): the walk's descent loads everything below it in one trip
+  int ga, gb, ba, bb, ea, eb;
+  int pad[54];
 };
 
 RST_SQ_HD uint32_t f2u(float f) {
@@ -230,13 +233,13 @@ RST_SQ_HD int hi_units(double hi, int e0) {
 // sign and binade (G normal, e0 its grid: the usual case), else in exact
 // double arithmetic.  False when v is not on the grid, non-finite, or
 // implausibly far from G.
-RST_SQ_HD bool offset_units(float v, const MapHdr& h, int& k) {
-  const uint32_t vb = f2u(v), gb = f2u(h.G);
-  if (((vb ^ gb) >> 23) == 0 && ((gb >> 23) & 0xffu) != 0) {
-    const int d = (int)(vb & 0x7fffffu) - (int)(gb & 0x7fffffu);
-    k = (gb >> 31) ? -d : d;
-    return true;
-  }
+// (the exact double path: v in another binade than G)
+#if defined(__HIPCC__)
+__host__ __device__ __noinline__
+#else
+inline
+#endif
+bool offset_units_slow(float v, const MapHdr& h, int& k) {
   if (!(v - v == 0.0f)) return false;
   const double kv = std::ldexp((double)v, -h.e0);
   const double kg = std::ldexp((double)h.G, -h.e0);
@@ -245,6 +248,25 @@ RST_SQ_HD bool offset_units(float v, const MapHdr& h, int& k) {
   if (!(std::fabs(kd) < 1073741824.0)) return false;
   k = (int)kd;
   return true;
+}
+RST_SQ_HD bool offset_units(float v, const MapHdr& h, int& k) {
+  const uint32_t vb = f2u(v), gb = f2u(h.G);
+  if (((vb ^ gb) >> 23) == 0) {
+    const int d = (int)(vb & 0x7fffffu) - (int)(gb & 0x7fffffu);
+    k = (gb >> 31) ? -d : d;
+    return true;
+  }
+  return offset_units_slow(v, h, k);
+}
+// the bits path only (false in another binade: the caller takes its slow path)
+RST_SQ_HD bool offset_units_fast(float v, const MapHdr& h, int& k) {
+  const uint32_t vb = f2u(v), gb = f2u(h.G);
+  if (((vb ^ gb) >> 23) == 0) {
+    const int d = (int)(vb & 0x7fffffu) - (int)(gb & 0x7fffffu);
+    k = (gb >> 31) ? -d : d;
+    return true;
+  }
+  return false;
 }
 
 // The end of a map run from the exact start G + k 2^e0: entry r = k mod

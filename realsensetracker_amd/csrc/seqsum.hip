@@ -65,7 +65,8 @@ struct SqView {
   GroupMap* grp;   // [nch][ng]
   SbMap* sbm;      // [nch][nk]
   int* stats;      // optional, 8 per chain
-  double* ttot;    // [nch][nk] fp64 tile totals
+  double* ttot;    // [nch][4 nk] fp64 totals of 1024-element quarter tiles
+  long long* clk;  // [nch][nk][8] shader clocks at the map kernel's phase boundaries
   int* err;        // bound-check failures (bits; 0 = none): a map kernel that
                    // meets a size its tables cannot hold stops instead of
                    // reading out of range
@@ -113,49 +114,91 @@ __device__ double block_scan_excl(double v, double* lds, double* total) {
 template <int BS>
 __device__ double block_sum_global(const double* a, int cnt, double* lds) {
   double s = 0.0;
-  for (int i = threadIdx.x; i < cnt; i += BS) s += a[i];
+  // (four loads in flight per round: a rolled loop waited one trip each)
+  for (int i0 = threadIdx.x; i0 < cnt; i0 += 4 * BS) {
+    double t[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) t[u] = i0 + u * BS < cnt ? a[i0 + u * BS] : 0.0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) s += t[u];
+  }
   double tot;
   (void)block_scan_excl<BS>(s, lds, &tot);
   return tot;
 }
 
-// ---- 1: SoA copy, window flags, fp64 tile totals --------------------------------
-// One 4096-element tile per workgroup, 16 consecutive elements (whole
-// float4 loads) per thread.
+// ---- 1: SoA copy, window flags, fp64 totals --------------------------------------
+// One 1024-element quarter tile per workgroup, four consecutive elements
+// per thread (64 contiguous bytes: coalesced float4 loads, one float4 SoA
+// store per component); a 16-element window is a lane quad, its flags
+// OR-ed across the quad by DPP.  The quarter tile's fp64 total per
+// component: the threads' 4-element sums (fixed order), reduced over the
+// block (fixed tree) -- four components in one reduction.
 constexpr int kFrontT = kTile / kW;  // 256
+constexpr int kTotE = 1024;          // elements per k_sq_tot workgroup
+constexpr int kTotQ = kTile / kTotE; // 4 per tile
+static_assert(kTotE == 4 * kFrontT, "k_sq_tot: four elements per thread");
+
+// quad_perm DPP: lane ^ 1 and lane ^ 2 within each lane quad
+__device__ __forceinline__ int quad_or(int a) {
+  a |= __builtin_amdgcn_mov_dpp(a, 0xB1, 0xF, 0xF, false);  // [1,0,3,2]
+  a |= __builtin_amdgcn_mov_dpp(a, 0x4E, 0xF, 0xF, false);  // [2,3,0,1]
+  return a;
+}
+
 __global__ __launch_bounds__(kFrontT) void k_sq_tot(const float4* __restrict__ x, SqView v) {
-  __shared__ double lds[kFrontT / kWave + 1];
-  const int t = blockIdx.x;
-  const int64_t i0 = (int64_t)t * kTile + (int64_t)threadIdx.x * kW;
-  const int b = t * kBlocksPerTile + threadIdx.x;
-  float4 q[kW];
+  __shared__ double red[kFrontT / kWave][4];
+  const int qt = blockIdx.x, tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid / kWave;
+  const int64_t i0 = (int64_t)qt * kTotE + 4 * tid;
+  float4 q[4];
 #pragma unroll
-  for (int j = 0; j < kW; ++j) q[j] = i0 + j < v.n ? x[i0 + j] : make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int c = 0; c < v.nch; ++c) {
-    double s = 0.0;
-    int fl = 0;
-    float e[kW];
+  for (int j = 0; j < 4; ++j) q[j] = i0 + j < v.n ? x[i0 + j] : make_float4(0.f, 0.f, 0.f, 0.f);
+  double part[4];
 #pragma unroll
-    for (int j = 0; j < kW; ++j) {
+  for (int c = 0; c < 4; ++c) {
+    float e[4];
+    int f = 0;
+    double ps = 0.0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
       e[j] = comp(q[j], c);
-      const int f = nf_flags(e[j]);
-      fl |= f;
-      if (!f) s += (double)e[j];
+      const int fj = nf_flags(e[j]);
+      f |= fj;
+      ps += fj ? 0.0 : (double)e[j];
     }
-    float* dst = v.soa + (int64_t)c * v.ns;
-    for (int j = 0; j < kW; ++j)
-      if (i0 + j < v.n) dst[i0 + j] = e[j];
-    if (b < v.nb) v.wflg[(int64_t)c * v.nb + b] = (uint8_t)fl;
-    double tot;
-    (void)block_scan_excl<kFrontT>(s, lds, &tot);
-    if (threadIdx.x == 0) v.ttot[(int64_t)c * v.nk + t] = tot;
+    part[c] = ps;
+    if (c < v.nch) {
+      float* dst = v.soa + (int64_t)c * v.ns;
+      // (ns is a multiple of 64 and i0 of 4: the float4 is in the row)
+      if (i0 < v.n) *reinterpret_cast<float4*>(dst + i0) = make_float4(e[0], e[1], e[2], e[3]);
+      f = quad_or(f);
+      const int64_t w = i0 / kW;
+      if ((tid & 3) == 0 && w < v.nb) v.wflg[(int64_t)c * v.nb + w] = (uint8_t)f;
+    }
+  }
+#pragma unroll
+  for (int o = kWave / 2; o > 0; o >>= 1)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) part[c] += __shfl_xor(part[c], o, kWave);
+  if (lane == 0)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) red[wv][c] = part[c];
+  __syncthreads();
+  if (tid < v.nch) {
+    double t = 0.0;
+#pragma unroll
+    for (int w = 0; w < kFrontT / kWave; ++w) t += red[w][tid];
+    v.ttot[(int64_t)tid * v.nk * kTotQ + qt] = t;
   }
 }
 
 // ---- 2: boundaries, unmonitored runs, increments ----------------------------------
 // One workgroup per (tile, chain); thread = one 16-element window.
 __global__ __launch_bounds__(kFrontT) void k_sq_front(SqView v) {
-  __shared__ float xs[kTile + kW];
+  // (one pad float per 16: thread t's window reads xs(16 t + j) at 17 t + j,
+  // every lane in its own bank)
+  __shared__ float xsp[(kTile + kW) + (kTile + kW) / kW];
+  auto xs = [&](int i) -> float& { return xsp[i + (i >> 4)]; };
   __shared__ int sbs[kFrontT + 1];
   __shared__ double sA[kFrontT];
   __shared__ double lds[kFrontT / kWave + 1];
@@ -167,16 +210,31 @@ __global__ __launch_bounds__(kFrontT) void k_sq_front(SqView v) {
   if (t == 0 && c == 0 && tid == 0) *v.err = 0;
   // the tile (and the next tile's first window) of component c
   const float* Xs = v.soa + (int64_t)c * v.ns;
-  for (int i = tid; i < kTile + kW; i += kFrontT) xs[i] = e0 + i < v.n ? Xs[e0 + i] : 0.0f;
-  // fp64 prefix at the tile start
-  const double P = block_sum_global<kFrontT>(v.ttot + (int64_t)c * v.nk, t, lds);
+  {
+    // (every load issued before the first LDS store: a rolled loop waited
+    // out one memory round trip per element)
+    constexpr int kJ = (kTile + kW + kFrontT - 1) / kFrontT;
+    float tv[kJ];
+#pragma unroll
+    for (int j = 0; j < kJ; ++j) {
+      const int i = tid + j * kFrontT;
+      tv[j] = i < kTile + kW && e0 + i < v.n ? Xs[e0 + i] : 0.0f;
+    }
+#pragma unroll
+    for (int j = 0; j < kJ; ++j) {
+      const int i = tid + j * kFrontT;
+      if (i < kTile + kW) xs(i) = tv[j];
+    }
+  }
+  // fp64 prefix at the tile start (the quarter tiles' totals before it)
+  const double P = block_sum_global<kFrontT>(v.ttot + (int64_t)c * v.nk * kTotQ, t * kTotQ, lds);
   __syncthreads();
   // the thread's window: fp64 total and prefix
   const int b = t * kBlocksPerTile + tid;
   double wsum = 0.0;
 #pragma unroll
   for (int j = 0; j < kW; ++j) {
-    const float e = xs[tid * kW + j];
+    const float e = xs(tid * kW + j);
     if (isfinite(e)) wsum += (double)e;
   }
   double ttotal;
@@ -192,7 +250,7 @@ __global__ __launch_bounds__(kFrontT) void k_sq_front(SqView v) {
       best = run;
       bj = j;
     }
-    const float e = xs[tid * kW + j];
+    const float e = xs(tid * kW + j);
     if (isfinite(e)) run += (double)e;
   }
   if (b == 0) {
@@ -210,7 +268,7 @@ __global__ __launch_bounds__(kFrontT) void k_sq_front(SqView v) {
         b2 = r2;
         j2 = j;
       }
-      const float e = xs[kTile + j];
+      const float e = xs(kTile + j);
       if (isfinite(e)) r2 += (double)e;
     }
     sbs[kFrontT] = kTile + j2;
@@ -265,7 +323,7 @@ __global__ __launch_bounds__(kFrontT) void k_sq_front(SqView v) {
     float s = G;
     double fsum = 0.0;
     for (int i = s0; i < s1; ++i) {
-      const float e = xs[i];
+      const float e = xs(i);
       s = s + e;
       if (isfinite(e)) fsum += (double)e;
     }
@@ -295,6 +353,8 @@ __global__ __launch_bounds__(kMapT) void k_sq_maps(SqView v) {
   __shared__ int sbad;
   const int k = blockIdx.x, c = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & (kWave - 1);
+  long long* clk = v.clk + ((int64_t)c * v.nk + k) * 8;
+  if (tid == 0) clk[0] = (long long)__builtin_amdgcn_s_memtime();
   const int* bsg = v.bs + (int64_t)c * (v.nb + 1);
   const int* gsg = v.gs + (int64_t)c * (v.ng + 1);
   const int* ksg = v.ks + (int64_t)c * (v.nk + 1);
@@ -318,9 +378,19 @@ __global__ __launch_bounds__(kMapT) void k_sq_maps(SqView v) {
   const int ngr = gb - ga, nblk = bb - ba, nel = eb - ea;
   const float* X = v.soa + (int64_t)c * v.ns;
   if (tid == 0) sbad = 0;
-  for (int i = tid; i < nel; i += kMapT) xs[i] = X[ea + i];
+  {
+    // (all loads in flight before the stores; nel <= kMaxSbElems)
+    constexpr int kJ = (kMaxSbElems + kMapT - 1) / kMapT;
+    float tv[kJ];
+#pragma unroll
+    for (int j = 0; j < kJ; ++j) tv[j] = tid + j * kMapT < nel ? X[ea + tid + j * kMapT] : 0.0f;
+#pragma unroll
+    for (int j = 0; j < kJ; ++j)
+      if (tid + j * kMapT < nel) xs[tid + j * kMapT] = tv[j];
+  }
   for (int i = tid; i <= nblk; i += kMapT) sbs[i] = bsg[ba + i] - ea;
   for (int i = tid; i <= ngr; i += kMapT) sgs[i] = gsg[ga + i] - ba;
+  if (tid == 0) clk[1] = (long long)__builtin_amdgcn_s_memtime();
   // refined guesses: the fp64 prefix of the blocks' float32 increments
   const double* inc = v.inc + (int64_t)c * v.nb;
   const int tb = ba / kBlocksPerTile;
@@ -336,6 +406,7 @@ __global__ __launch_bounds__(kMapT) void k_sq_maps(SqView v) {
     if (tid < nblk) Gd[tid] = ba + tid == 0 ? 0.0 : base + pre;
   }
   __syncthreads();
+  if (tid == 0) clk[2] = (long long)__builtin_amdgcn_s_memtime();
   // -- leaves: lane (block, residue pair): runs from candidates rp and rp + 2,
   // interleaved (two independent dependency chains per lane, one round for
   // up to 512 blocks)
@@ -403,6 +474,7 @@ __global__ __launch_bounds__(kMapT) void k_sq_maps(SqView v) {
   __syncthreads();
   for (int i = tid; i < nblk * (int)(sizeof(Leaf) / 4); i += kMapT)
     reinterpret_cast<int*>(leafg + ba)[i] = reinterpret_cast<const int*>(lf)[i];
+  if (tid == 0) clk[3] = (long long)__builtin_amdgcn_s_memtime();
   // -- groups: lane (group, residue), up to 16 residues
   GroupMap* grpg = v.grp + (int64_t)c * v.ng;
   {
@@ -459,7 +531,17 @@ __global__ __launch_bounds__(kMapT) void k_sq_maps(SqView v) {
   __syncthreads();
   for (int i = tid; i < ngr * (int)(sizeof(GroupMap) / 4); i += kMapT)
     reinterpret_cast<int*>(grpg + ga)[i] = reinterpret_cast<const int*>(gm)[i];
+  if (tid == 0) clk[4] = (long long)__builtin_amdgcn_s_memtime();
   // -- the superblock: lanes = residues, up to 64
+  if (tid == 0) {
+    SbMap* o = v.sbm + (int64_t)c * v.nk + k;
+    o->ga = ga;
+    o->gb = gb;
+    o->ba = ba;
+    o->bb = bb;
+    o->ea = ea;
+    o->eb = eb;
+  }
   if (tid < kWave && sbad) {
     SbMap* o = v.sbm + (int64_t)c * v.nk + k;
     if (tid == 0) o->h.flags = kOpaque;
@@ -503,28 +585,36 @@ __global__ __launch_bounds__(kMapT) void k_sq_maps(SqView v) {
       }
     }
     o->e[r] = en;
+    if (tid == 0) clk[5] = (long long)__builtin_amdgcn_s_memtime();
   }
 }
 
 // ---- 4: the walk -------------------------------------------------------------------
-// One wavefront per chain.  Superblock maps are staged into LDS in chunks of
-// kWalkC (the next chunk's loads in flight while the current one is
-// walked); a failed superblock check loads that superblock's group maps,
-// a failed group check the group's leaves, a failed leaf check the block's
-// elements -- the reference's own adds.
+// One wavefront per chain.  The superblock maps of a chunk of kWalkC
+// superblocks sit in registers -- lane r holds every superblock's entry r,
+// lane q < kWalkC superblock q's header -- so a step is a few scalar
+// reads (v_readlane) and integer / float ops on the exact running sum; the
+// next chunk's loads are in flight meanwhile.  A failed check descends
+// (from global memory) to the superblock's group maps, then a group's
+// leaf maps, then a block's own float adds.
 constexpr int kWalkC = 16;
-constexpr int kSbF4 = sizeof(SbMap) / 16;  // 64 float4 per superblock map
 
-struct WalkLds {
-  SbMap sb[2][kWalkC];
-  GroupMap g[kMaxSbGroups];
-  Leaf l[2 * kGW];
-  float x[2 * kW];
-  int gs[kMaxSbGroups + 1];
-  int bs[2 * kGW + 1];
+struct WalkStats {
+  int sb, sbh, g, gh, l, lh, ser;
 };
 
-// map (header h, entries e[]) applied to the exact s (all lanes agree)
+struct WalkLds {
+  GroupMap g[kMaxSbGroups];     // a descent's superblock, loaded in one trip:
+  Leaf l[kMaxSbBlocks];         // its group maps, leaf maps,
+  float x[kMaxSbElems + 8];     // elements (from a 16-byte boundary),
+  int gs[kWave];                // group and block starts
+  int bs[kMaxSbBlocks + 1 + 63];
+  WalkStats ws;   // the descent's counters (LDS: no stack slot in the walk)
+  long long tclk[8];  // (statistics) the first descent's phase clocks
+  int64_t pos_nf;  // element index where s became non-finite, else -1
+};
+
+// map (header h, entries e[] by residue) applied to the exact s (all lanes agree)
 __device__ __forceinline__ bool walk_try(float& s, const MapHdr& h, const MapEnt* e, int mmax) {
   if ((h.flags & kOpaque) || h.m < 0 || h.m > mmax) return false;
   int k;
@@ -536,126 +626,332 @@ __device__ __forceinline__ bool walk_try(float& s, const MapHdr& h, const MapEnt
   return true;
 }
 
+// superblock k by its group maps, leaf maps and own adds; pos_nf >= 0 when
+// the sum became inf / NaN (the element after the block that made it so)
+// (not inlined: the walk's unrolled fast path stays a few hundred
+// instructions; an inlined copy per step thrashed the instruction cache)
+// (the chain's tables as plain arguments: a reference to the kernel's view
+// would copy the view to a stack slot, and every walk would start with
+// scratch traffic)
+struct DescArgs {
+  const GroupMap* grp;
+  const Leaf* leaf;
+  const int* bsg;
+  const int* gsg;
+  const float* X;
+  int* err;
+  int64_t n;
+  int nb, ng;
+};
+
+// Steps over maps[0, nq) (nq < kWave, in LDS) from s, speculatively: the
+// offset units from the bits of s and G, the residue, the end E_r + du 2^e0
+// (the entry from LDS at a uniform address), unchecked; then the checks
+// lane-parallel, step q on lane q (s before step q is lane q of `hist`).
+// Returns the number of leading verified steps, s after them.
+template <class Map>
+__device__ __forceinline__ int spec_walk(float& s, const Map* maps, int nq, int mmax) {
+  const int lane = threadIdx.x;
+  nq = __builtin_amdgcn_readfirstlane(nq);  // (uniform: a scalar loop)
+  if (nq <= 0) return 0;
+  const int ql = min(lane, nq - 1);
+  const MapHdr hl = maps[ql].h;
+  const int gbl = (int)__float_as_uint(hl.G);
+  const int sgl = gbl >> 31;
+  const int mkl = (1 << min(hl.m & 7, mmax)) - 1;  // (clamped: r stays inside the entries)
+  int hist = 0;
+  for (int q = 0; q < nq; ++q) {
+    const int sbits = __builtin_amdgcn_readfirstlane((int)__float_as_uint(s));
+    hist = lane == q ? sbits : hist;
+    const int gb = __builtin_amdgcn_readlane(gbl, q);
+    const int sg = __builtin_amdgcn_readlane(sgl, q);
+    const int mk = __builtin_amdgcn_readlane(mkl, q);
+    const int e0 = __builtin_amdgcn_readlane(hl.e0, q);
+    const int kk = ((sbits - gb) ^ sg) - sg;
+    const int r = kk & mk;
+    s = maps[q].e[r].E - ldexpf((float)(r - kk), e0);
+  }
+  {
+    const int sfin = __builtin_amdgcn_readfirstlane((int)__float_as_uint(s));
+    hist = lane == nq ? sfin : hist;
+  }
+  const int nxb = __shfl(hist, lane + 1, kWave);
+  int okl;
+  {
+    const int kk = ((hist - gbl) ^ sgl) - sgl;
+    const int r = kk & mkl;
+    const MapEnt en = maps[ql].e[r];
+    const int du = kk - r;
+    const float a = en.E, b = -ldexpf((float)(r - kk), hl.e0);
+    const float o = en.E - ldexpf((float)(r - kk), hl.e0);
+    const bool abig = fabsf(a) >= fabsf(b);
+    const float big = abig ? a : b, sml = abig ? b : a;
+    okl = (lane < nq) & ((((uint32_t)hist ^ (uint32_t)gbl) >> 23) == 0u) & ((hl.flags & kOpaque) == 0) &
+          ((unsigned)hl.m <= (unsigned)mmax) & (en.LOu <= du) & (du <= en.HIu) & ((o - big) == sml) &
+          ((int)__float_as_uint(o) == nxb);
+  }
+  const uint64_t bad = __ballot(!okl) & ((1ull << nq) - 1);
+  const int qf = bad ? (int)__builtin_ctzll(bad) : nq;
+  s = __int_as_float(__builtin_amdgcn_readlane(hist, qf));
+  return qf;
+}
+
+// n pieces of kSz bytes from src (global) to dst (LDS) by LDS-DMA: no
+// registers staged, every piece in flight at once (the caller waits)
+#define RST_GLDS_COPY(NAME, SZ)                                                                            \
+  __device__ __forceinline__ void NAME(void* dst, const void* src, int n) {                               \
+    const int lane = threadIdx.x;                                                                         \
+    const char* sp = static_cast<const char*>(src);                                                       \
+    char* dp = static_cast<char*>(dst);                                                                   \
+    for (int j = 0; j * kWave < n; ++j) {                                                                 \
+      const int i = j * kWave + lane;                                                                     \
+      if (i < n)                                                                                          \
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(sp + (size_t)i * SZ), \
+                                         (__attribute__((address_space(3))) void*)(dp + (size_t)j * kWave * SZ), \
+                                         SZ, 0, 0);                                                       \
+    }                                                                                                     \
+  }
+RST_GLDS_COPY(glds_copy16, 16)
+RST_GLDS_COPY(glds_copy4, 4)
+#undef RST_GLDS_COPY
+
+__device__ __noinline__ float walk_descend(const DescArgs v, const int ga, const int gb, const int ba,
+                                           const int bb, const int ea, const int eb, float s, WalkLds& W) {
+  int64_t& pos_nf = W.pos_nf;
+  WalkStats& ws = W.ws;
+  const int lane = threadIdx.x;
+  const bool stamp = ws.g == 0 && lane == 0;  // (the first descent's phases)
+  if (stamp) W.tclk[0] = (long long)__builtin_amdgcn_s_memtime();
+  const int ngr = gb - ga, nblk = bb - ba, nel = eb - ea;
+  if (ngr < 1 || ngr > kMaxSbGroups || ga < 0 || gb > v.ng || nblk < 1 || nblk > kMaxSbBlocks || ba < 0 ||
+      bb > v.nb || nel < 1 || nel > kMaxSbElems || ea < 0 || eb > v.n) {
+    if (lane == 0) atomicOr(v.err, 4);
+    pos_nf = v.n;
+    return __int_as_float(0x7fc00000);
+  }
+  // the superblock's maps, starts and elements, one trip
+  const int e4 = ea & ~3, xo = ea - e4;
+  glds_copy16(W.g, v.grp + ga, ngr * (int)(sizeof(GroupMap) / 16));
+  glds_copy16(W.l, v.leaf + ba, nblk * (int)(sizeof(Leaf) / 16));
+  glds_copy16(W.x, v.X + e4, (eb - e4 + 3) >> 2);
+  glds_copy4(W.gs, v.gsg + ga, ngr + 1);
+  glds_copy4(W.bs, v.bsg + ba, nblk + 1);
+  __builtin_amdgcn_s_waitcnt(0);
+  if (stamp) W.tclk[1] = (long long)__builtin_amdgcn_s_memtime();
+  int q0 = 0;
+  while (q0 < ngr) {
+    const int qf = spec_walk(s, W.g + q0, ngr - q0, kGroupM);
+    ws.g += qf;
+    ws.gh += qf;
+    const int q = q0 + qf;
+    if (stamp && q0 == 0) W.tclk[2] = (long long)__builtin_amdgcn_s_memtime();
+    if (q >= ngr) break;
+    // group q by its leaves (block indices relative to ba)
+    ++ws.g;
+    const int b0 = W.gs[q] - ba, b1 = W.gs[q + 1] - ba;
+    if (b1 - b0 < 1 || b1 - b0 > 2 * kGW - 1 || b0 < 0 || b1 > nblk) {
+      if (lane == 0) atomicOr(v.err, 8);
+      pos_nf = v.n;
+      return __int_as_float(0x7fc00000);
+    }
+    const int nbl = b1 - b0;
+    int l0 = 0;
+    while (l0 < nbl) {
+      const int lf = spec_walk(s, W.l + b0 + l0, nbl - l0, kLeafM);
+      ws.l += lf;
+      ws.lh += lf;
+      const int bl = b0 + l0 + lf;
+      if (stamp && q0 == 0 && l0 == 0) W.tclk[4] = (long long)__builtin_amdgcn_s_memtime();
+      if (bl >= b1) break;
+      // the block by the reference's own adds (element indices relative to ea)
+      ++ws.l;
+      ++ws.ser;
+      const int e0 = W.bs[bl] - ea, e1 = W.bs[bl + 1] - ea;
+      if (e1 - e0 < 1 || e1 - e0 > 2 * kW - 1 || e0 < 0 || e1 > nel) {
+        if (lane == 0) atomicOr(v.err, 16);
+        pos_nf = v.n;
+        return __int_as_float(0x7fc00000);
+      }
+      for (int i = e0; i < e1; ++i) s = s + W.x[xo + i];
+      if (stamp && q0 == 0 && l0 == 0) W.tclk[5] = (long long)__builtin_amdgcn_s_memtime();
+      if (!isfinite(s)) {
+        pos_nf = (int64_t)ea + e1;
+        return s;
+      }
+      l0 = bl + 1 - b0;
+    }
+    q0 = q + 1;
+  }
+  if (stamp) W.tclk[6] = (long long)__builtin_amdgcn_s_memtime();
+  return s;
+}
+
+template <class T>
+__device__ __forceinline__ const __attribute__((address_space(1))) T* gptr(const T* p) {
+  return (const __attribute__((address_space(1))) T*)p;
+}
+
+// one superblock map in registers: lane r holds entry r, lanes < kWalkC
+// the header of superblock (chunk start + lane)
+struct SbRegs {
+  float E[kWalkC];
+  int LO[kWalkC], HI[kWalkC];
+  float G;
+  int e0, m, fl;
+  int ga, gb, ba, bb, ea, eb;  // lane q: superblock q's ranges (the descent's loads)
+};
+
+__device__ __forceinline__ void sb_fetch(const SbMap* __restrict__ sbm_, int nk, int k0, int lane,
+                                         SbRegs& R) {
+  // (global address space: generic loads would also count on lgkmcnt and
+  // serialise with every LDS / scalar wait of the walk)
+  const auto* sbm = gptr(sbm_);
+#pragma unroll
+  for (int q = 0; q < kWalkC; ++q) {
+    const int k = min(k0 + q, nk - 1);  // (clamped: a step past the end is never taken)
+    R.E[q] = sbm[k].e[lane].E;
+    R.LO[q] = sbm[k].e[lane].LOu;
+    R.HI[q] = sbm[k].e[lane].HIu;
+  }
+  const int kh = min(k0 + (lane & (kWalkC - 1)), nk - 1);
+  R.G = sbm[kh].h.G;
+  R.e0 = sbm[kh].h.e0;
+  R.m = sbm[kh].h.m;
+  R.fl = sbm[kh].h.flags;
+  R.ga = sbm[kh].ga;
+  R.gb = sbm[kh].gb;
+  R.ba = sbm[kh].ba;
+  R.bb = sbm[kh].bb;
+  R.ea = sbm[kh].ea;
+  R.eb = sbm[kh].eb;
+}
+
 __global__ __launch_bounds__(kWave) void k_sq_walk(SqView v, float* __restrict__ out) {
   __shared__ WalkLds W;
   const int c = blockIdx.x, lane = threadIdx.x;
   const SbMap* sbm = v.sbm + (int64_t)c * v.nk;
-  const GroupMap* grp = v.grp + (int64_t)c * v.ng;
-  const Leaf* leaf = v.leaf + (int64_t)c * v.nb;
-  const int* bsg = v.bs + (int64_t)c * (v.nb + 1);
-  const int* gsg = v.gs + (int64_t)c * (v.ng + 1);
-  const int* ksg = v.ks + (int64_t)c * (v.nk + 1);
   const float* X = v.soa + (int64_t)c * v.ns;
   int* st = v.stats ? v.stats + c * 8 : nullptr;
   const uint64_t t0 = st ? __builtin_amdgcn_s_memtime() : 0;
-  int n_sb = 0, n_sbh = 0, n_g = 0, n_gh = 0, n_l = 0, n_lh = 0, n_ser = 0;
-  float s = 0.0f;
-  int64_t pos_nf = -1;  // element index where s became non-finite
-  // chunk staging: lane copies float4 lane + 64 j of the chunk
-  float4 pre[kWalkC];
-  auto issue = [&](int ch) {
-    const float4* src = reinterpret_cast<const float4*>(sbm + (int64_t)ch * kWalkC);
-    const int cnt = min(kWalkC, v.nk - ch * kWalkC) * kSbF4;
-#pragma unroll
-    for (int j = 0; j < kWalkC; ++j) {
-      const int i = lane + j * kWave;
-      pre[j] = i < cnt ? src[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-  };
-  auto land = [&](int buf) {
-    float4* dst = reinterpret_cast<float4*>(&W.sb[buf][0]);
-#pragma unroll
-    for (int j = 0; j < kWalkC; ++j) dst[lane + j * kWave] = pre[j];
-  };
-  const int nchunk = (v.nk + kWalkC - 1) / kWalkC;
-  if (nchunk > 0) {
-    issue(0);
-    land(0);
+  if (lane == 0) {
+    W.ws = WalkStats{0, 0, 0, 0, 0, 0, 0};
+    for (int j = 0; j < 8; ++j) W.tclk[j] = 0;
+    W.pos_nf = -1;
   }
   __syncthreads();
-  for (int ch = 0; ch < nchunk && pos_nf < 0; ++ch) {
-    if (ch + 1 < nchunk) issue(ch + 1);
-    const int kend = min(v.nk, (ch + 1) * kWalkC);
-    for (int k = ch * kWalkC; k < kend && pos_nf < 0; ++k) {
-      const SbMap& M = W.sb[ch & 1][k - ch * kWalkC];
-      ++n_sb;
-      if (walk_try(s, M.h, M.e, kSbM)) {
-        ++n_sbh;
-        continue;
-      }
-      // descend: the superblock's groups
-      const int ga = ksg[k], gb = ksg[k + 1];
-      const int ngr = gb - ga;
-      if (ngr < 1 || ngr > kMaxSbGroups || ga < 0 || gb > v.ng) {
-        if (lane == 0) atomicOr(v.err, 4);
-        pos_nf = v.n;
-        s = __int_as_float(0x7fc00000);
-        break;
-      }
-      {
-        const int4* src = reinterpret_cast<const int4*>(grp + ga);
-        int4* dst = reinterpret_cast<int4*>(W.g);
-        for (int i = lane; i < ngr * (int)(sizeof(GroupMap) / 16); i += kWave) dst[i] = src[i];
-        for (int i = lane; i <= ngr; i += kWave) W.gs[i] = gsg[ga + i];
-      }
-      __syncthreads();
-      for (int q = 0; q < ngr && pos_nf < 0; ++q) {
-        ++n_g;
-        if (walk_try(s, W.g[q].h, W.g[q].e, kGroupM)) {
-          ++n_gh;
-          continue;
-        }
-        const int b0 = W.gs[q], b1 = W.gs[q + 1];
-        if (b1 - b0 < 1 || b1 - b0 > 2 * kGW - 1 || b0 < 0 || b1 > v.nb) {
-          if (lane == 0) atomicOr(v.err, 8);
-          pos_nf = v.n;
-          s = __int_as_float(0x7fc00000);
-          break;
-        }
-        __syncthreads();
-        {
-          const int4* src = reinterpret_cast<const int4*>(leaf + b0);
-          int4* dst = reinterpret_cast<int4*>(W.l);
-          for (int i = lane; i < (b1 - b0) * (int)(sizeof(Leaf) / 16); i += kWave) dst[i] = src[i];
-          for (int i = lane; i <= b1 - b0; i += kWave) W.bs[i] = bsg[b0 + i];
-        }
-        __syncthreads();
-        for (int bl = 0; bl < b1 - b0; ++bl) {
-          ++n_l;
-          if (walk_try(s, W.l[bl].h, W.l[bl].e, kLeafM)) {
-            ++n_lh;
-            continue;
-          }
-          // the block by the reference's own adds
-          ++n_ser;
-          const int e0 = W.bs[bl], e1 = W.bs[bl + 1];
-          if (e1 - e0 < 1 || e1 - e0 > 2 * kW - 1 || e0 < 0 || e1 > v.n) {
-            if (lane == 0) atomicOr(v.err, 16);
-            pos_nf = v.n;
-            s = __int_as_float(0x7fc00000);
-            break;
-          }
-          __syncthreads();
-          if (lane < e1 - e0) W.x[lane] = X[e0 + lane];
-          __syncthreads();
-          for (int i = 0; i < e1 - e0; ++i) s = s + W.x[i];
-          if (!isfinite(s)) {
-            pos_nf = e1;
-            break;
-          }
-        }
-        __syncthreads();
-      }
-      __syncthreads();
+  __shared__ MapEnt CE[kWalkC][kWave];  // the chunk's entries, for the checks
+  int nsb = 0, nsbh = 0;
+  float s = 0.0f;
+  bool nf = false;  // s became non-finite (W.pos_nf)
+  int k = 0;
+  SbRegs cur, nxt;
+  if (v.nk > 0) sb_fetch(sbm, v.nk, 0, lane, cur);
+  uint64_t wait_clk = 0;
+  while (k < v.nk && !nf) {
+    if (st) {  // (statistics: the time waiting for this chunk's maps)
+      const uint64_t ta = __builtin_amdgcn_s_memtime();
+      const int j = k / kWalkC;
+      if (c < 4 && j < 4 && lane == 0) v.stats[40 + c * 4 + j] = (int)(ta - t0);
+      __builtin_amdgcn_s_waitcnt(0);
+      wait_clk += __builtin_amdgcn_s_memtime() - ta;
     }
-    if (ch + 1 < nchunk) land((ch + 1) & 1);
-    __syncthreads();
+    // the next chunk in flight while this one is walked
+    sb_fetch(sbm, v.nk, k + kWalkC, lane, nxt);
+    k = __builtin_amdgcn_readfirstlane(k);  // (uniform: keep the chunk's bounds scalar)
+    const int qn = min(kWalkC, v.nk - k);
+#pragma unroll
+    for (int q = 0; q < kWalkC; ++q) CE[q][lane] = MapEnt{cur.E[q], cur.LO[q], cur.HI[q]};
+    // lane q: superblock k + q's header terms
+    const int gbl = (int)__float_as_uint(cur.G);
+    const int sgl = gbl >> 31;  // 0, or -1 for a negative G
+    const int mkl = ((1 << (cur.m & 7)) - 1) & (kWave - 1);
+    // The chunk's steps, speculatively and unchecked: offset units from the
+    // bits of s and G (s - G in G's grid when both share sign and binade),
+    // the residue r, the end E_r + du 2^e0 by v_readlane from registers.
+    // Eight dependent instructions a step; s before step q is kept in
+    // lane q of `hist`.
+    int hist = 0;
+#pragma unroll
+    for (int q = 0; q < kWalkC; ++q) {
+      const int sbits = __builtin_amdgcn_readfirstlane((int)__float_as_uint(s));
+      asm("v_writelane_b32 %0, %1, %2" : "+v"(hist) : "s"(sbits), "n"(q));
+      const int gb = __builtin_amdgcn_readlane(gbl, q);
+      const int sg = __builtin_amdgcn_readlane(sgl, q);
+      const int mk = __builtin_amdgcn_readlane(mkl, q);
+      const int e0 = __builtin_amdgcn_readlane(cur.e0, q);
+      const int kk = ((sbits - gb) ^ sg) - sg;
+      const int r = kk & mk;
+      const float E = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cur.E[q]), r));
+      // (E - (+0) keeps a -0 end; E + +0 would not)
+      s = E - ldexpf((float)(r - kk), e0);
+    }
+    {
+      const int sfin = __builtin_amdgcn_readfirstlane((int)__float_as_uint(s));
+      asm("v_writelane_b32 %0, %1, %2" : "+v"(hist) : "s"(sfin), "n"(kWalkC));
+    }
+    // The checks, step q on lane q: s and G share sign and binade (else the
+    // offset above is meaningless; G's grid is 2^e0, zero and subnormal G
+    // included, so the bits differ by the offset in units), the map is usable, the
+    // offset lies in the residue's window, E_r + du 2^e0 is exact
+    // (Fast2Sum) and is what the step produced.
+    const int nxb = __shfl(hist, lane + 1, kWave);
+    int okl;
+    {
+      const int kk = ((hist - gbl) ^ sgl) - sgl;
+      const int r = kk & mkl;
+      const MapEnt en = CE[min(lane, kWalkC - 1)][r];
+      const int du = kk - r;
+      const float a = en.E, b = -ldexpf((float)(r - kk), cur.e0);
+      const float o = en.E - ldexpf((float)(r - kk), cur.e0);
+      const bool abig = fabsf(a) >= fabsf(b);
+      const float big = abig ? a : b, sml = abig ? b : a;
+      okl = (lane < qn) & ((((uint32_t)hist ^ (uint32_t)gbl) >> 23) == 0u) &
+            ((cur.fl & kOpaque) == 0) & ((unsigned)cur.m <= (unsigned)kSbM) & (en.LOu <= du) & (du <= en.HIu) &
+            ((o - big) == sml) & ((int)__float_as_uint(o) == nxb);
+    }
+    const uint64_t bad = __ballot(!okl) & ((1ull << kWalkC) - 1);
+    int qf = kWalkC;
+    if (bad != 0) {
+      qf = (int)__builtin_ctzll(bad);
+      s = __int_as_float(__builtin_amdgcn_readlane(hist, qf));
+    }
+    nsb += qf;
+    nsbh += qf;
+    if (qf == kWalkC) {
+      k += kWalkC;
+      cur = nxt;
+      continue;
+    }
+    k += qf;
+    if (k >= v.nk) break;
+    // (rare) superblock k by its map's slow path or its groups, then a
+    // fresh chunk from k + 1
+    // (its map with the slow offset -- s in another binade than G -- from
+    // the chunk's registers and LDS copy, then the descent)
+    ++nsb;
+    MapHdr h;
+    h.G = __int_as_float(__builtin_amdgcn_readlane(gbl, qf));
+    h.e0 = __builtin_amdgcn_readlane(cur.e0, qf);
+    h.m = __builtin_amdgcn_readlane(cur.m, qf);
+    h.flags = __builtin_amdgcn_readlane(cur.fl, qf);
+    if (walk_try(s, h, CE[qf], kSbM)) {
+      ++nsbh;
+    } else {
+      const DescArgs da{v.grp + (int64_t)c * v.ng, v.leaf + (int64_t)c * v.nb, v.bs + (int64_t)c * (v.nb + 1),
+                        v.gs + (int64_t)c * (v.ng + 1), X, v.err, v.n, v.nb, v.ng};
+      s = walk_descend(da, __builtin_amdgcn_readlane(cur.ga, qf), __builtin_amdgcn_readlane(cur.gb, qf),
+                       __builtin_amdgcn_readlane(cur.ba, qf), __builtin_amdgcn_readlane(cur.bb, qf),
+                       __builtin_amdgcn_readlane(cur.ea, qf), __builtin_amdgcn_readlane(cur.eb, qf), s, W);
+      nf = W.pos_nf >= 0;
+    }
+    ++k;
+    sb_fetch(sbm, v.nk, k, lane, cur);  // (unconditional: cur is dead across the descent)
   }
-  if (pos_nf >= 0) {
+  if (nf) {
     // inf / NaN absorbs every finite element: only NaN or an opposite
     // infinity later can still change it.  Serial to the next window, then
     // the window flags.
-    int64_t i = pos_nf;
+    int64_t i = W.pos_nf;
     for (; i < v.n && (i % kW) != 0; ++i) s = s + X[i];
     int orf = 0;
     const uint8_t* wf = v.wflg + (int64_t)c * v.nb;
@@ -668,14 +964,17 @@ __global__ __launch_bounds__(kWave) void k_sq_walk(SqView v, float* __restrict__
     out[c] = s;
     if (c == 0 && v.stats) v.stats[32] = *v.err;
     if (st) {
-      st[0] = n_sb;
-      st[1] = n_sbh;
-      st[2] = n_g;
-      st[3] = n_gh;
-      st[4] = n_l;
-      st[5] = n_lh;
-      st[6] = n_ser;
+      st[0] = nsb;
+      st[1] = nsbh;
+      st[2] = W.ws.g;
+      st[3] = W.ws.gh;
+      st[4] = W.ws.l;
+      st[5] = W.ws.lh;
+      st[6] = W.ws.ser;
       st[7] = (int)min<uint64_t>(INT_MAX, __builtin_amdgcn_s_memtime() - t0);
+      if (c < 4) v.stats[33 + c] = (int)min<uint64_t>(INT_MAX, wait_clk);
+      if (c == 0)
+        for (int j = 1; j < 7; ++j) v.stats[56 + j] = W.tclk[j] ? (int)(W.tclk[j] - W.tclk[0]) : -1;
     }
   }
 }
@@ -699,7 +998,7 @@ static size_t sq_layout(SqView& v, int64_t n, int nch, char* base) {
   v.soa = (float*)take(sizeof(float) * nch * (size_t)v.ns);
   v.wflg = (uint8_t*)take((size_t)nch * v.nb);
   v.err = (int*)take(sizeof(int));
-  v.ttot = (double*)take(sizeof(double) * nch * (size_t)v.nk);
+  v.ttot = (double*)take(sizeof(double) * nch * 4 * (size_t)v.nk);
   v.bs = (int*)take(sizeof(int) * nch * (size_t)(v.nb + 1));
   v.gs = (int*)take(sizeof(int) * nch * (size_t)(v.ng + 1));
   v.ks = (int*)take(sizeof(int) * nch * (size_t)(v.nk + 1));
@@ -708,6 +1007,7 @@ static size_t sq_layout(SqView& v, int64_t n, int nch, char* base) {
   v.leaf = (Leaf*)take(sizeof(Leaf) * nch * (size_t)v.nb);
   v.grp = (GroupMap*)take(sizeof(GroupMap) * nch * (size_t)v.ng);
   v.sbm = (SbMap*)take(sizeof(SbMap) * nch * (size_t)v.nk);
+  v.clk = (long long*)take(sizeof(long long) * 8 * nch * (size_t)v.nk);
   return off;
 }
 
@@ -730,7 +1030,7 @@ int seqsum_enqueue(const float4* d_x, int64_t n, int nch, void* ws, float* d_out
   sq_layout(v, n, nch, (char*)ws);
   v.stats = d_stats;
   if (stages & 1) {
-    k_sq_tot<<<v.nk, kFrontT, 0, st>>>(d_x, v);
+    k_sq_tot<<<v.nk * kTotQ, kFrontT, 0, st>>>(d_x, v);
     k_sq_front<<<dim3(v.nk, nch), kFrontT, 0, st>>>(v);
   }
   if (stages & 2) k_sq_maps<<<dim3(v.nk, nch), kMapT, 0, st>>>(v);

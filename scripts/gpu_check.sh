@@ -1,0 +1,11 @@
+# GPU parity suite + the default bench (no CPU legs): a round-trip check
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+TAG=${TAG:-dev}
+timeout -k 10 900 python -u -m pytest tests/ -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/${TAG}_pytest_gpu.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -4 gpurun_out/${TAG}_pytest_gpu.log
+[ $rc -eq 0 ] || { grep -E "Error|assert|FAILED" gpurun_out/${TAG}_pytest_gpu.log | head -20; exit $rc; }
+timeout -k 10 400 python -u bench.py --no-cpu > gpurun_out/${TAG}_bench.log 2>&1
+rc=$?; echo "bench rc=$rc"; tail -3 gpurun_out/${TAG}_bench.log
+exit $rc

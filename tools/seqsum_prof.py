@@ -20,11 +20,13 @@ x = np.concatenate([p, (p * p).sum(1, keepdims=True)], 1).astype(np.float32)
 for serial, reps in ((0, 20), (1, 2)):
     out, ms = seq_sum(ctx, x, serial=serial, reps=reps)
     print("serial" if serial else "parallel", f"{ms * 1e3:.1f} us", same(out, want(x)))
-st = np.zeros((5, 8), np.int32)
+st = np.zeros((8, 8), np.int32)
 seq_sum(ctx, x, stats=st)
 print("walk stats per chain [superblock tries, hits, group tries, hits, leaf tries, hits, serial blocks, walker clocks]")
 print(st[:4])
-print('bound-check error bits', st[4, 0])
+print('bound-check error bits', st[4, 0], 'walker clocks waiting for map chunks', st[4, 1:5].tolist())
+print('walker clocks at the start of chunks 0-3 per chain', st[5:7].reshape(4, 4).tolist())
+print('chain 0 first descent phases (clocks from its start: groups loaded, group walk, leaves loaded, leaf walk, serial block, end)', st[7, 1:7].tolist())
 for c in range(4):
     y = np.zeros_like(x)
     y[:, c] = x[:, c]

@@ -29,9 +29,9 @@ def layout(n, nch=4):
     off = 0
     out = {}
     for name, size in (("soa", 4 * nch * ns), ("wflg", nch * nb),
-                       ("err", 4), ("ttot", 8 * nch * nk), ("bs", 4 * nch * (nb + 1)), ("gs", 4 * nch * (ng + 1)),
+                       ("err", 4), ("ttot", 8 * nch * 4 * nk), ("bs", 4 * nch * (nb + 1)), ("gs", 4 * nch * (ng + 1)),
                        ("ks", 4 * nch * (nk + 1)), ("inc", 8 * nch * nb), ("tinc", 8 * nch * nk),
-                       ("leaf", 64 * nch * nb), ("grp", 256 * nch * ng), ("sbm", 1024 * nch * nk)):
+                       ("leaf", 64 * nch * nb), ("grp", 256 * nch * ng), ("sbm", 1024 * nch * nk), ("clk", 64 * nch * nk)):
         out[name] = off
         off += (size + 255) & ~255
     return out, nb, ng, nk, off
@@ -60,13 +60,26 @@ def run(x, stages, nch=4):
 def main():
     stages = int(sys.argv[1]) if len(sys.argv) > 1 else 1
     case = sys.argv[2] if len(sys.argv) > 2 else "alternating"
-    from seqsum_cases import cases
-    x = cases()[case]
+    if case == "frame":
+        from realsensetracker_amd import driver
+        K = driver.intrinsics(640, 480)
+        da, _, _ = driver.make_pair(driver.SyntheticScene(0), K, seed=10)
+        p = driver.unproject(da, K)
+        x = np.concatenate([p, (p * p).sum(1, keepdims=True)], 1).astype(np.float32)
+    else:
+        from seqsum_cases import cases
+        x = cases()[case]
     st, failed, out, ws = run(x, stages)
     print(f"case {case} n={len(x)} stages {stages}: status {st}, failed stage {failed}, out {out}")
     off, nb, ng, nk, total = layout(len(x))
     err = ws[off["err"]:off["err"] + 4].view(np.int32)[0]
     print("err bits", err)
+    clk = ws[off["clk"]:off["clk"] + 64 * 4 * nk].view(np.int64).reshape(4, nk, 8)
+    if stages & 2:
+        d = np.diff(clk[:, :, :6], axis=2).astype(np.float64)
+        names = ["load+sizes", "guesses", "leaves", "groups", "superblock"]
+        print("map kernel phases (clocks, mean / max over superblocks):",
+              {nm: (round(d[:, :, i].mean()), int(d[:, :, i].max())) for i, nm in enumerate(names)})
     from seqsum_emu import emulate_tables
     for c in range(4):
         bs = ws[off["bs"]:].view(np.int32)[c * (nb + 1):(c + 1) * (nb + 1)]
