@@ -124,29 +124,38 @@ int ctx_slab(rst_ctx* ctx, size_t bytes, double** out) {
   return RST_OK;
 }
 
-// Upload host AoS xyz (n points) into a dedicated device buffer.
+// Upload host AoS xyz (n points) into a device buffer from the context's
+// size-class pool (no hipMalloc / hipFree per call: hipFree synchronises the
+// whole device); give it back with free_xyz.
+static size_t xyz_bytes(int64_t n) { return sizeof(float) * 3 * (size_t)std::max<int64_t>(n, 1); }
+
+static void free_xyz(rst_ctx* ctx, float* d, int64_t n) {
+  if (!d) return;
+  (void)hipStreamSynchronize(ctx->stream);  // no kernel may still read it
+  ctx_release(ctx, d, size_class(xyz_bytes(n)));
+}
+
 static int upload_xyz(rst_ctx* ctx, const float* h, int64_t n, float** d_out) {
   *d_out = nullptr;
-  const size_t bytes = sizeof(float) * 3 * (size_t)std::max<int64_t>(n, 1);
-  float* d = nullptr;
-  if (hipMalloc(&d, bytes) != hipSuccess) return RST_E_NOMEM;
+  const size_t bytes = xyz_bytes(n);
+  void* dv = nullptr;
+  size_t cls = 0;
+  RST_CHECK(ctx_alloc(ctx, bytes, &dv, &cls));
+  float* d = (float*)dv;
   if (n > 0) {
     void* pin = nullptr;
     int s = ctx_pinned(ctx, bytes, &pin);
-    if (s < 0) {
-      hipFree(d);
-      return s;
-    }
     // the staging buffer may still feed an earlier async copy
-    if (hipStreamSynchronize(ctx->stream) != hipSuccess) {
-      hipFree(d);
-      return RST_E_HIP;
+    if (s >= 0 && hipStreamSynchronize(ctx->stream) != hipSuccess) s = RST_E_HIP;
+    if (s >= 0) {
+      memcpy(pin, h, sizeof(float) * 3 * n);
+      if (hipMemcpyAsync(d, pin, sizeof(float) * 3 * n, hipMemcpyHostToDevice, ctx->stream) !=
+          hipSuccess)
+        s = RST_E_HIP;
     }
-    memcpy(pin, h, sizeof(float) * 3 * n);
-    if (hipMemcpyAsync(d, pin, sizeof(float) * 3 * n, hipMemcpyHostToDevice, ctx->stream) !=
-        hipSuccess) {
-      hipFree(d);
-      return RST_E_HIP;
+    if (s < 0) {
+      free_xyz(ctx, d, n);
+      return s;
     }
   }
   *d_out = d;
@@ -330,8 +339,7 @@ int rst_target_build(rst_ctx* ctx, const float* xyz, int64_t m, rst_target** out
   float* d = nullptr;
   RST_CHECK(upload_xyz(ctx, xyz, m, &d));
   int s = target_build_device(ctx, d, m, true, out);
-  hipStreamSynchronize(ctx->stream);
-  hipFree(d);
+  free_xyz(ctx, d, m);
   return s;
 }
 
@@ -423,8 +431,7 @@ int rst_target_query_nn(rst_ctx* ctx, const rst_target* t, const float* q, int64
         hipStreamSynchronize(ctx->stream) != hipSuccess)
       s = RST_E_HIP;
   }
-  hipStreamSynchronize(ctx->stream);
-  hipFree(dq);
+  free_xyz(ctx, dq, nq);
   return s < 0 ? s : RST_OK;
 }
 
@@ -478,7 +485,7 @@ int rst_debug_query_nn_warm_stats(rst_ctx* ctx, const rst_target* t, const float
   }
   if (e0) hipEventDestroy(e0);
   if (e1) hipEventDestroy(e1);
-  hipFree(dq);
+  free_xyz(ctx, dq, nq);
   return s < 0 ? s : RST_OK;
 }
 
@@ -513,8 +520,7 @@ int rst_debug_query_nn_fallback(rst_ctx* ctx, const rst_target* t, const float* 
        hipMemcpyAsync(path, dp, sizeof(int32_t) * nq, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
        hipStreamSynchronize(ctx->stream) != hipSuccess))
     s = RST_E_HIP;
-  hipStreamSynchronize(ctx->stream);
-  hipFree(dq);
+  free_xyz(ctx, dq, nq);
   return s < 0 ? s : RST_OK;
 }
 
@@ -710,8 +716,7 @@ int rst_target_query_knn(rst_ctx* ctx, const rst_target* t, const float* q, int6
         hipStreamSynchronize(ctx->stream) != hipSuccess)
       s = RST_E_HIP;
   }
-  hipStreamSynchronize(ctx->stream);
-  hipFree(dq);
+  free_xyz(ctx, dq, nq);
   return s < 0 ? s : RST_OK;
 }
 
@@ -801,8 +806,7 @@ int rst_icp_align(rst_ctx* ctx, const float* src, int64_t n, const rst_target* t
   float* d = nullptr;
   RST_CHECK(upload_xyz(ctx, src, n, &d));
   int r = rst_icp_align_device(ctx, d, n, tgt, opts, pose_inout, mean_cost);
-  hipStreamSynchronize(ctx->stream);
-  hipFree(d);
+  free_xyz(ctx, d, n);
   return r;
 }
 
@@ -845,55 +849,48 @@ int rst_solve_kabsch(rst_ctx* ctx, const float* src, int64_t n, const float* dst
       return RST_E_ARG;
   RST_HIP(hipSetDevice(ctx->device));
   float *ds = nullptr, *dd = nullptr;
-  void* dp = nullptr;
   RST_CHECK(upload_xyz(ctx, src, n, &ds));
   int r = upload_xyz(ctx, dst, m, &dd);
+  // pairs + weights through the pinned staging buffer into the workspace
   const size_t pb = sizeof(int32_t) * 2 * (size_t)k, wb = weights ? sizeof(float) * (size_t)k : 0;
-  if (r >= 0 && hipMalloc(&dp, pb + wb) != hipSuccess) r = RST_E_NOMEM;
-  if (r >= 0 && (hipMemcpyAsync(dp, pairs, pb, hipMemcpyHostToDevice, ctx->stream) != hipSuccess ||
-                 (weights && hipMemcpyAsync((char*)dp + pb, weights, wb, hipMemcpyHostToDevice,
-                                            ctx->stream) != hipSuccess)))
-    r = RST_E_HIP;
+  const size_t pwb = (pb + wb + 255) & ~(size_t)255;
+  void* ws = nullptr;
+  void* pin = nullptr;
+  if (r >= 0) r = ctx_workspace(ctx, pwb + solve_kabsch_ws_bytes(k), &ws);
+  // (the staging buffer may still feed the uploads above)
+  if (r >= 0 && hipStreamSynchronize(ctx->stream) != hipSuccess) r = RST_E_HIP;
+  if (r >= 0) r = ctx_pinned(ctx, pb + wb, &pin);
+  if (r >= 0) {
+    memcpy(pin, pairs, pb);
+    if (weights) memcpy((char*)pin + pb, weights, wb);
+    if (hipMemcpyAsync(ws, pin, pb + wb, hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
+      r = RST_E_HIP;
+  }
   if (r >= 0)
-    r = solve_kabsch_device(ctx, ds, dd, (const int32_t*)dp,
-                            weights ? (const float*)((char*)dp + pb) : nullptr, k, pose_out);
-  hipStreamSynchronize(ctx->stream);
-  if (dp) hipFree(dp);
-  if (dd) hipFree(dd);
-  hipFree(ds);
+    r = solve_kabsch_device(ctx, ds, dd, (const int32_t*)ws,
+                            weights ? (const float*)((char*)ws + pb) : nullptr, k,
+                            (char*)ws + pwb, pose_out);
+  free_xyz(ctx, dd, m);
+  free_xyz(ctx, ds, n);
   return r;
 }
 
+// ComputeCentroid (point_cloud_utils.cpp:92-98): the fp32 sequential sums in
+// input order (seqsum.hip, bit-exact), times float(1.0 / n)
 int rst_compute_centroid(rst_ctx* ctx, const float* xyz, int64_t n, float out[3]) {
   if (!ctx || !out || n <= 0 || !xyz) return RST_E_ARG;
   RST_HIP(hipSetDevice(ctx->device));
-  rst_target* s = nullptr;
   float* d = nullptr;
   RST_CHECK(upload_xyz(ctx, xyz, n, &d));
-  int r = target_build_device(ctx, d, n, false, &s);
-  if (r >= 0) {
-    double* slab = nullptr;
-    r = ctx_slab(ctx, sizeof(double) * 4 * 1100, &slab);
-    if (r >= 0) r = centroid_device(ctx, s->pts, n, slab);
-    if (r >= 0) {
-      std::vector<double> h((size_t)r * 4);
-      if (hipMemcpyAsync(h.data(), slab, sizeof(double) * 4 * r, hipMemcpyDeviceToHost,
-                         ctx->stream) != hipSuccess ||
-          hipStreamSynchronize(ctx->stream) != hipSuccess) {
-        r = RST_E_HIP;
-      } else {
-        double acc[4] = {0, 0, 0, 0};
-        for (int b = 0; b < (int)h.size() / 4; ++b)
-          for (int k = 0; k < 4; ++k) acc[k] += h[b * 4 + k];
-        for (int k = 0; k < 3; ++k) out[k] = (float)(acc[k] / (double)n);
-        r = RST_OK;
-      }
-    }
-  }
-  if (s) rst_target_free(s);
-  hipStreamSynchronize(ctx->stream);
-  hipFree(d);
-  return r;
+  void* ws = nullptr;
+  int r = ctx_workspace(ctx, centroid_ws_bytes(n), &ws);
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  if (r >= 0) r = centroid_seq_device(ctx, d, n, ws, s);
+  free_xyz(ctx, d, n);
+  if (r < 0) return r;
+  const float f = (float)(1.0 / (double)n);  // Vector3f *= double: the float Scalar
+  for (int k = 0; k < 3; ++k) out[k] = s[k] * f;
+  return RST_OK;
 }
 
 }  // extern "C"

@@ -46,9 +46,6 @@ constexpr int kNP2Plane = 30;  // A (21), b (6), sum w r^2, count, sum d2
 #define RST_FB_MIN_WAVES 4  // k_icp_fb occupancy target (r01: 128 VGPRs, 4 waves/SIMD; r02: the kernel's paths need 201, the compiler settles at 2 waves/SIMD; forcing 3 spills: 22.8k vs 23.6k it/s)
 #endif
 constexpr int kCertBit = 1 << 30;
-#ifndef RST_NN_MIN_WAVES
-#define RST_NN_MIN_WAVES 4  // k_icp_nn<P2PointAcc> (r02: Best2 certificate search, 96 VGPRs spilled at 5)
-#endif
 #ifndef RST_COLD_FAST
 #define RST_COLD_FAST 1
 #endif
@@ -287,7 +284,6 @@ struct AccArgs {
 struct P2PointAcc {
   static constexpr int NV = kNP2Point;  // sum w q u^T (9), sum w u (3), sum q (3), sum d2
   static constexpr int RS = 16;         // slab row stride (doubles; divides kRedBS)
-  static constexpr int kMinWaves = RST_NN_MIN_WAVES;  // k_icp_nn occupancy (waves/SIMD)
   static constexpr int kFbMinWaves = RST_FB_MIN_WAVES;  // k_icp_fb occupancy
   static constexpr bool kCanFinish = false;
   static constexpr bool kSums = true;  // the search kernels write slab rows
@@ -317,7 +313,6 @@ struct P2PointAcc {
 struct P2PlaneAcc {
   static constexpr int NV = kNP2Plane;  // A (21), b (6), sum w r^2, count, sum d2
   static constexpr int RS = 32;
-  static constexpr int kMinWaves = 4;
   static constexpr int kFbMinWaves = 1;
   static constexpr bool kCanFinish = true;
   static constexpr bool kSums = true;
@@ -358,7 +353,6 @@ struct P2PlaneAcc {
 struct RefAcc {
   static constexpr int NV = 9;   // k_cov_ref's rows: the 3x3 covariance
   static constexpr int RS = 16;
-  static constexpr int kMinWaves = RST_NN_MIN_WAVES;
   static constexpr int kFbMinWaves = RST_FB_MIN_WAVES;
   static constexpr bool kCanFinish = false;
   static constexpr bool kSums = false;
@@ -576,6 +570,8 @@ __device__ __forceinline__ void proj_seed(const BvhView& bv, const PixView& pv, 
 // lane goes to the search queue (in point order, one segment per block).
 // The searches run compacted in kernel 2, so no wavefront here waits on
 // one lane's search.
+// (no occupancy hint: the compiler's own register budget, measured best in
+// r02 -- a 5-waves/SIMD target spilled)
 template <class Acc>
 __global__ __launch_bounds__(kBS) void k_icp_nn(BvhView bv, AdjView av, PixView pv, AccArgs aa,
                                                 const float4* __restrict__ src, int64_t n,
@@ -754,35 +750,33 @@ __global__ void k_kabsch(const double* __restrict__ in /*cov[9] smean[3] dmean[3
 }
 
 // ---- SolveKabsch (align_icp.cpp:18-71): correspondences -> pose ----------------------
-// Pass 1: fp64 sums of src[pairs.first] and dst[pairs.second] (6 per block).
-__global__ __launch_bounds__(kBS) void k_pairs_sum(const float* __restrict__ src,
-                                                   const float* __restrict__ dst,
-                                                   const int32_t* __restrict__ pairs, int64_t k,
-                                                   double* __restrict__ slab) {
-  __shared__ double lds[(kBS / kWave) * 6];
-  double v[6] = {0, 0, 0, 0, 0, 0};
-  for (int64_t c = blockIdx.x * (int64_t)kBS + threadIdx.x; c < k;
-       c += (int64_t)gridDim.x * kBS) {
-    const int64_t i = pairs[2 * c], j = pairs[2 * c + 1];
-    v[0] += src[3 * i]; v[1] += src[3 * i + 1]; v[2] += src[3 * i + 2];
-    v[3] += dst[3 * j]; v[4] += dst[3 * j + 1]; v[5] += dst[3 * j + 2];
-  }
-  block_sum_to_slab<6, kBS>(v, lds, slab + blockIdx.x * 6);
+// Pass 1: the pairs' points in pair order, src[pairs.first] and
+// dst[pairs.second] as float4 streams for the sequential sums of :30-32.
+__global__ __launch_bounds__(kBS) void k_pairs_gather(const float* __restrict__ src,
+                                                      const float* __restrict__ dst,
+                                                      const int32_t* __restrict__ pairs, int64_t k,
+                                                      float4* __restrict__ gs,
+                                                      float4* __restrict__ gd) {
+  const int64_t c = blockIdx.x * (int64_t)kBS + threadIdx.x;
+  if (c >= k) return;
+  const int64_t i = pairs[2 * c], j = pairs[2 * c + 1];
+  gs[c] = make_float4(src[3 * i], src[3 * i + 1], src[3 * i + 2], 0.f);
+  gd[c] = make_float4(dst[3 * j], dst[3 * j + 1], dst[3 * j + 2], 0.f);
 }
 
-// Pass 2: the means (float, as src_mean /= indices.size() at :33-34), then
-// cov += w * double(float((q - dbar)(s - sbar)^T)) (:36-54) in fp64.
+// Pass 2: the means (float: src_mean /= indices.size() divides by the float
+// Scalar, :33-34), then cov += w * double(float((q - dbar)(s - sbar)^T))
+// (:36-54) in fp64.  sums = [src sums | dst sums] (the fp32 sequential sums).
 __global__ __launch_bounds__(kBS) void k_pairs_cov(const float* __restrict__ src,
                                                    const float* __restrict__ dst,
                                                    const int32_t* __restrict__ pairs,
                                                    const float* __restrict__ weights, int64_t k,
-                                                   const double* __restrict__ tot6,
+                                                   const float* __restrict__ sums,
                                                    double* __restrict__ slab) {
   __shared__ double lds[(kBS / kWave) * 9];
-  const float sm0 = (float)(tot6[0] / (double)k), sm1 = (float)(tot6[1] / (double)k),
-              sm2 = (float)(tot6[2] / (double)k);
-  const float dm0 = (float)(tot6[3] / (double)k), dm1 = (float)(tot6[4] / (double)k),
-              dm2 = (float)(tot6[5] / (double)k);
+  const float fk = (float)k;
+  const float sm0 = sums[0] / fk, sm1 = sums[1] / fk, sm2 = sums[2] / fk;
+  const float dm0 = sums[4] / fk, dm1 = sums[5] / fk, dm2 = sums[6] / fk;
   double v[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   for (int64_t c = blockIdx.x * (int64_t)kBS + threadIdx.x; c < k;
        c += (int64_t)gridDim.x * kBS) {
@@ -796,6 +790,13 @@ __global__ __launch_bounds__(kBS) void k_pairs_cov(const float* __restrict__ src
       for (int cc = 0; cc < 3; ++cc) v[r * 3 + cc] += w * (double)(q[r] * u[cc]);
   }
   block_sum_to_slab<9, kBS>(v, lds, slab + blockIdx.x * 9);
+}
+
+// ComputeCentroid's input: device xyz -> float4 (w = 0) for the sequential sums
+__global__ __launch_bounds__(kBS) void k_xyz_f4(const float* __restrict__ xyz, int64_t n,
+                                                float4* __restrict__ out) {
+  const int64_t i = blockIdx.x * (int64_t)kBS + threadIdx.x;
+  if (i < n) out[i] = make_float4(xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2], 0.f);
 }
 
 // Kabsch on the reduced sums (align_icp.cpp:122, 139-151).
@@ -1383,33 +1384,67 @@ int kabsch_device(rst_ctx* ctx, const double cov[9], const float smean[3], const
   return RST_OK;
 }
 
-// cov (row-major sums from k_pairs_cov) + means -> k_kabsch's input layout
-__global__ void k_pairs_pack(const double* __restrict__ tot6, const double* __restrict__ tot9,
+// cov (row-major sums from k_pairs_cov) + the float means -> k_kabsch's input layout
+__global__ void k_pairs_pack(const float* __restrict__ sums, const double* __restrict__ tot9,
                              int64_t k, double* __restrict__ out) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   for (int r = 0; r < 3; ++r)
     for (int c = 0; c < 3; ++c) RST_M3(out, r, c) = tot9[r * 3 + c];
-  for (int a = 0; a < 6; ++a) out[9 + a] = (double)(float)(tot6[a] / (double)k);
+  const float fk = (float)k;
+  for (int a = 0; a < 3; ++a) {
+    out[9 + a] = (double)(sums[a] / fk);
+    out[12 + a] = (double)(sums[4 + a] / fk);
+  }
+}
+
+static size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
+
+size_t solve_kabsch_ws_bytes(int64_t k) {
+  const size_t kk = (size_t)std::max<int64_t>(k, 1);
+  return 2 * align256(sizeof(float4) * kk) + 256 + seqsum_bytes(kk);
 }
 
 int solve_kabsch_device(rst_ctx* ctx, const float* d_src, const float* d_dst,
-                        const int32_t* d_pairs, const float* d_w, int64_t k,
+                        const int32_t* d_pairs, const float* d_w, int64_t k, void* ws,
                         float pose_out[16]) {
   const int nb = std::min(1024, blocks_for(k));
   double* slab = nullptr;
   RST_CHECK(ctx_slab(ctx, sizeof(double) * (9 * (size_t)nb + 64), &slab));
-  double* tot6 = slab + 9 * (size_t)nb;
-  double* tot9 = tot6 + 8;
+  double* tot9 = slab + 9 * (size_t)nb;
   double* packed = tot9 + 16;  // 15 in, 16 floats out
+  float4* gs = (float4*)ws;
+  float4* gd = (float4*)((char*)ws + align256(sizeof(float4) * (size_t)k));
+  float* sums = (float*)((char*)gd + align256(sizeof(float4) * (size_t)k));  // [src 4 | dst 4]
+  void* sqws = (char*)sums + 256;
   hipStream_t st = ctx->stream;
-  k_pairs_sum<<<nb, kBS, 0, st>>>(d_src, d_dst, d_pairs, k, slab);
-  k_slab_reduce<6><<<1, kRedBS, 0, st>>>(slab, nb, slab, 0, nullptr, tot6);
-  k_pairs_cov<<<nb, kBS, 0, st>>>(d_src, d_dst, d_pairs, d_w, k, tot6, slab);
+  k_pairs_gather<<<blocks_for(k), kBS, 0, st>>>(d_src, d_dst, d_pairs, k, gs, gd);
+  // src_mean += src.GetPoint(im.first), dst_mean += ... (:30-32), in pair order
+  RST_CHECK(seqsum_enqueue(gs, k, 3, sqws, sums, st));
+  RST_CHECK(seqsum_enqueue(gd, k, 3, sqws, sums + 4, st));
+  k_pairs_cov<<<nb, kBS, 0, st>>>(d_src, d_dst, d_pairs, d_w, k, sums, slab);
   k_slab_reduce<9><<<1, kRedBS, 0, st>>>(slab, nb, slab, 0, nullptr, tot9);
-  k_pairs_pack<<<1, 64, 0, st>>>(tot6, tot9, k, packed);
+  k_pairs_pack<<<1, 64, 0, st>>>(sums, tot9, k, packed);
   k_kabsch<<<1, 64, 0, st>>>(packed, (float*)(packed + 16));
   RST_HIP(hipGetLastError());
   RST_HIP(hipMemcpyAsync(pose_out, packed + 16, sizeof(float) * 16, hipMemcpyDeviceToHost, st));
+  RST_HIP(hipStreamSynchronize(st));
+  return RST_OK;
+}
+
+size_t centroid_ws_bytes(int64_t n) {
+  const size_t nn = (size_t)std::max<int64_t>(n, 1);
+  return align256(sizeof(float4) * nn) + 256 + seqsum_bytes(nn);
+}
+
+int centroid_seq_device(rst_ctx* ctx, const float* d_xyz, int64_t n, void* ws, float out[3]) {
+  float4* x4 = (float4*)ws;
+  float* sums = (float*)((char*)ws + align256(sizeof(float4) * (size_t)n));
+  void* sqws = (char*)sums + 256;
+  hipStream_t st = ctx->stream;
+  k_xyz_f4<<<blocks_for(n), kBS, 0, st>>>(d_xyz, n, x4);
+  RST_CHECK(seqsum_enqueue(x4, n, 3, sqws, sums, st));
+  RST_HIP(hipGetLastError());
+  RST_HIP(hipMemcpyAsync(out, sums, sizeof(float) * 3, hipMemcpyDeviceToHost, st));
   RST_HIP(hipStreamSynchronize(st));
   return RST_OK;
 }

@@ -215,8 +215,18 @@ int icp_align_prepared(rst_ctx* ctx, const rst_target* src,
                        const rst_target* tgt, const rst_icp_opts* opts,
                        float pose_inout[16], float* mean_cost,
                        int32_t* iters_run, rst_comm* comm);
+// SolveKabsch (align_icp.cpp:18-71) on device clouds: the means as the
+// reference's fp32 sequential sums over the pairs (seqsum.hip); ws holds
+// solve_kabsch_ws_bytes(k)
+size_t solve_kabsch_ws_bytes(int64_t k);
 int solve_kabsch_device(rst_ctx* ctx, const float* d_src, const float* d_dst,
-                        const int32_t* d_pairs, const float* d_w, int64_t k, float pose_out[16]);
+                        const int32_t* d_pairs, const float* d_w, int64_t k, void* ws,
+                        float pose_out[16]);
+// ComputeCentroid's sums (point_cloud_utils.cpp:94-96) of device xyz:
+// out[0..3) = the fp32 sequential sums (host memory); ws holds
+// centroid_ws_bytes(n)
+size_t centroid_ws_bytes(int64_t n);
+int centroid_seq_device(rst_ctx* ctx, const float* d_xyz, int64_t n, void* ws, float out[3]);
 int centroid_device(rst_ctx* ctx, const float4* d_pts, int64_t n,
                     double* d_out3);
 int seq_sum4_device(rst_ctx* ctx, const float4* d_x, int64_t n, float* d_out);

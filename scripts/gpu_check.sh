@@ -2,6 +2,9 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+# the queue count is read at the HIP runtime's first call, which rocprofv3's
+# preloaded library makes before bench.py runs: set it here, not in bench.py
+export GPU_MAX_HW_QUEUES=24
 TAG=${TAG:-dev}
 timeout -k 10 900 python -u -m pytest tests/ -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/${TAG}_pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -4 gpurun_out/${TAG}_pytest_gpu.log

@@ -6,6 +6,9 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+# the queue count is read at the HIP runtime's first call, which rocprofv3's
+# preloaded library makes before bench.py runs: set it here, not in bench.py
+export GPU_MAX_HW_QUEUES=24
 TAG=${TAG:-r02}
 step() {  # name, limit, command...
   local name=$1 lim=$2; shift 2

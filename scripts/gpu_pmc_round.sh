@@ -6,6 +6,9 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+# the queue count is read at the HIP runtime's first call, which rocprofv3's
+# preloaded library makes before bench.py runs: set it here, not in bench.py
+export GPU_MAX_HW_QUEUES=24
 TAG=${TAG:-pmc}
 SHORT="--inflight 1 --steps 6 --warmup 1 --no-cpu --no-p2plane --no-host-api --no-gicp --ref-steps 0 --roof-steps 0"
 run() {  # name, limit, rocprof args...

@@ -4,6 +4,9 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+# the queue count is read at the HIP runtime's first call, which rocprofv3's
+# preloaded library makes before bench.py runs: set it here, not in bench.py
+export GPU_MAX_HW_QUEUES=24
 TAG=${TAG:-sq}
 B="bench.py --steps 3 --warmup 1 --no-cpu --no-p2plane --no-host-api --no-gicp --ref-steps 0 --inflight 1"
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SALU --output-format csv -d gpurun_out/${TAG}_sq1 -o run -- python3 $B > gpurun_out/${TAG}_sq1.log 2>&1 || exit $?

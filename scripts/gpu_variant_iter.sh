@@ -4,6 +4,9 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+# the queue count is read at the HIP runtime's first call, which rocprofv3's
+# preloaded library makes before bench.py runs: set it here, not in bench.py
+export GPU_MAX_HW_QUEUES=24
 for v in default ${VARIANTS}; do
   lib=$PWD/realsensetracker_amd/lib/librst_align.so
   [ "$v" != default ] && lib=$PWD/realsensetracker_amd/lib/variants/$v.so

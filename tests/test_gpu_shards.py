@@ -65,6 +65,11 @@ def solve(ctx, opts, n_total, tot, smean, pose, mu, it):
     return L.cm_to_pose(buf), m.value, k.value
 
 
+def fp64_centroid(x):
+    """The RST_SUM_FP64 centroid: the fp64 sum / n rounded to float (k_init_state)."""
+    return (x.astype(np.float64).sum(0) / len(x)).astype(np.float32)
+
+
 def fp64(**kw):
     return L.default_opts(sum_mode=L.RST_SUM_FP64, **kw)
 
@@ -94,7 +99,7 @@ def test_shard_partials_sum_to_the_whole(ctx, pair640):
     h = len(pb) // 2
     s_all, s_a, s_b = (A.Target.build(x, ctx) for x in (pb, pb[:h], pb[h:]))
     o = fp64()
-    sm = A.ComputeCentroid(pb, ctx)
+    sm = fp64_centroid(pb)
     for pose in (np.eye(4, dtype=np.float32), D.astype(np.float32)):
         for it in (0, 40):
             full = partials(ctx, s_all, t, o, pose, o.mu0, sm, it)
@@ -124,7 +129,7 @@ def test_shard_partials_p2plane(ctx, pair640):
 def _host_two_shard_loop(ctx, src, tgt, iters, o):
     h = len(src) // 2
     sa, sb = A.Target.build(src[:h], ctx), A.Target.build(src[h:], ctx)
-    sm = A.ComputeCentroid(src, ctx)  # the all-reduced centroid (fp64 sums)
+    sm = fp64_centroid(src)  # the all-reduced centroid (fp64 sums)
     pose, mu, it = np.eye(4, dtype=np.float32), o.mu0, 0
     for _ in range(iters):
         tot = partials(ctx, sa, tgt, o, pose, mu, sm, it) + partials(ctx, sb, tgt, o, pose, mu, sm, it)
