@@ -195,7 +195,8 @@ def run_sharded(a, K, frames, d_depth, hip, world, rank, local, rdv, barrier, ma
                                          C.byref(n)), "rst_unproject_device")
     lo, hi = shard_bounds(n.value, world, rank)
     sh = ShardedAligner(ctx, rendezvous=rdv)
-    opts = L.default_opts(max_iter=a.iters, sum_mode=L.RST_SUM_FP64)
+    ref = a.sum_mode == "ref"
+    opts = L.default_opts(max_iter=a.iters, sum_mode=L.RST_SUM_REF if ref else L.RST_SUM_FP64)
     ptr = d_src.value + 12 * lo
 
     def step():  # every rank knows the global count: no host round trip per align
@@ -233,11 +234,16 @@ def run_sharded(a, K, frames, d_depth, hip, world, rank, local, rdv, barrier, ma
                     "~3% invalid)",
             "config": {"workload": f"{a.width}x{a.height} scan pair ({n.value} source points), "
                                    f"AlignIcp3d P2POINT_REF {a.iters} iters, source sharded "
-                                   f"over {world} rank(s), one RCCL all-reduce of 16 fp64 "
-                                   f"per iteration",
+                                   f"over {world} rank(s), " + (
+                                       "per iteration one RCCL all-gather of the "
+                                       "correspondences (16 B/pt), the sequential fp32 sums "
+                                       "on every rank, one all-reduce of 9 fp64" if ref else
+                                       "one RCCL all-reduce of 16 fp64 per iteration"),
                        "width": a.width, "height": a.height, "iters_per_pair": a.iters,
                        "points_per_frame": n.value, "target_points": len(tgt),
-                       "accumulation": "fp64 partial sums", "parallelism": f"shard{world}"},
+                       "accumulation": ("RST_SUM_REF: the reference's sequential fp32 sums, "
+                                        "bit-exact" if ref else "RST_SUM_FP64: fp64 partial sums"),
+                       "parallelism": f"shard{world}"},
             "frames_per_s": a.steps / dt, "pairs_ok": oks,
             "final_pose_t": [float(x) for x in pose[:3, 3]],
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,

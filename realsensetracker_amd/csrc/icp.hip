@@ -449,10 +449,11 @@ __global__ __launch_bounds__(kBS) void k_gather_orig(const float4* __restrict__ 
 constexpr int kCovBlocks = 1024;
 __global__ __launch_bounds__(kBS) void k_cov_ref(const float4* __restrict__ srco,
                                                  const float4* __restrict__ corr, int64_t n,
+                                                 int64_t n_total,
                                                  const IcpState* __restrict__ st,
                                                  double* __restrict__ slab) {
   __shared__ double lds[(kBS / kWave) * 9];
-  const float nf = (float)n;
+  const float nf = (float)n_total;  // dst_mean /= n (the whole source's n)
   const float dm0 = st->seq[0] / nf, dm1 = st->seq[1] / nf, dm2 = st->seq[2] / nf;
   const float sm0 = st->smean[0], sm1 = st->smean[1], sm2 = st->smean[2];
   const float mu = st->mu;
@@ -1517,10 +1518,9 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
   if (opts.mode != RST_P2POINT_REF && opts.mode != RST_P2PLANE) return RST_E_ARG;
   if (opts.max_iter < 0) return RST_E_ARG;
   if (opts.sum_mode != RST_SUM_REF && opts.sum_mode != RST_SUM_FP64) return RST_E_ARG;
-  // the reference's sequential sums (P2POINT_REF only; one ordered pass over
-  // the whole source has no shard decomposition)
+  // the reference's sequential sums (P2POINT_REF only; sharded: the chains
+  // are walked over the all-gathered correspondences, comm.hip)
   const bool refsum = !p2plane && opts.sum_mode == RST_SUM_REF;
-  if (refsum && comm) return RST_E_ARG;
   if (!tgt->has_bvh) return RST_E_ARG;
   if (tgt->m >= kCertBit) return RST_E_ARG;  // positions carry kCertBit
   if (p2plane && !tgt->nrm) return RST_E_STATE;
@@ -1544,20 +1544,11 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
   double* slab2 = slab + rows1;
   double* totals = slab2 + (size_t)kFbBlocks * RS;  // 64 doubles
 
-  // n_total and the centroid are global quantities under sharding (the
-  // caller may know n_total: opts.n_total, no host round trip)
-  if (comm && opts.n_total > 0) {
-    if (opts.n_total < n_local) return RST_E_ARG;
-    n_total = opts.n_total;
-  } else if (comm) {
-    double* cnt = totals;
-    double h = (double)n_local;
-    RST_HIP(hipMemcpyAsync(cnt, &h, sizeof(double), hipMemcpyHostToDevice, st));
-    RST_CHECK(comm_allreduce_sum_f64(comm, cnt, 1, st));
-    RST_HIP(hipMemcpyAsync(&h, cnt, sizeof(double), hipMemcpyDeviceToHost, st));
-    RST_HIP(hipStreamSynchronize(st));
-    n_total = (int64_t)h;
-  }
+  // n_total, this shard's offset in the source order and the centroid are
+  // global quantities under sharding: the shard layout is exchanged once
+  // and cached (a given opts.n_total is checked against it)
+  int64_t shard_off = 0;
+  if (comm) RST_CHECK(comm_shard_layout(comm, n_local, opts.n_total, st, &n_total, &shard_off, nullptr));
   // reference early return (:77-79): pose untouched
   if (n_total < 3 || tgt->m < 3) return RST_FALSE;
   if (p2plane && n_total < 6) return RST_FALSE;
@@ -1565,25 +1556,31 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
   // per source point: sorted target position of its last neighbour (warm
   // start of the next iteration's exact search; -1 = cold); the fallback
   // queue (one kBS segment per kernel-1 block) and its per-block counts;
-  // RST_SUM_REF: the correspondences and the source in original order
+  // RST_SUM_REF: the correspondences and the source in original order (the
+  // whole source's when sharded: this shard writes [shard_off, + n_local))
   float4* nnq = nullptr;  // last neighbour (p, pos | kCertBit), -1 = cold
   int32_t *qbuf = nullptr, *qcnt = nullptr;  // near queue, then far queue (k_icp_nn)
   float4* cert = nullptr;  // far-point certificates (read only under kCertBit)
-  float4 *corr = nullptr, *srco = nullptr;
+  float4 *corr = nullptr, *srco = nullptr, *corrg = nullptr, *srcog = nullptr;
   void* sqws = nullptr;  // seqsum.hip tables (RST_SUM_REF)
   {
     const size_t np = (size_t)std::max<int64_t>(n_local, 1);
+    const size_t ng = refsum ? (size_t)std::max<int64_t>(n_total, 1) : 0;
     const size_t nq = (size_t)nblk * kBS;
     void* w = nullptr;
-    const size_t sqb = refsum ? seqsum_bytes(n_local) : 0;
-    RST_CHECK(ctx_workspace(ctx, sizeof(float4) * np * (refsum ? 4 : 2) + sizeof(int4) * nq +
+    const size_t sqb = refsum ? seqsum_bytes(n_total) : 0;
+    RST_CHECK(ctx_workspace(ctx, sizeof(float4) * (2 * np + 2 * ng) + sizeof(int4) * nq +
                                      sizeof(int32_t) * (2 * nq + 2 * nblk + 64) + sqb + 256,
                             &w));
     cert = (float4*)w;
     nnq = cert + np;
-    corr = refsum ? cert + 2 * np : nullptr;
-    srco = refsum ? cert + 3 * np : nullptr;
-    qbuf = (int32_t*)(cert + np * (refsum ? 4 : 2));
+    if (refsum) {
+      corrg = nnq + np;
+      srcog = corrg + ng;
+      corr = corrg + shard_off;
+      srco = srcog + shard_off;
+    }
+    qbuf = (int32_t*)(cert + 2 * np + 2 * ng);
     qcnt = qbuf + 2 * nq;
     if (refsum)  // the sequential sums' tables (256-byte aligned)
       sqws = (void*)(((uintptr_t)(qcnt + 2 * nblk + 64) + 255) & ~(uintptr_t)255);
@@ -1599,8 +1596,9 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
   int crows = 0;
   float* fsum = (float*)totals;  // RST_SUM_REF: the centroid's sequential sums
   if (refsum) {
-    k_gather_orig<<<blocks_for(n_local), kBS, 0, st>>>(src->pts, src->inv, n_local, srco);
-    RST_CHECK(seqsum_enqueue(srco, n_local, 3, sqws, fsum, st));  // point_cloud_utils.cpp:94-96
+    if (n_local > 0) k_gather_orig<<<blocks_for(n_local), kBS, 0, st>>>(src->pts, src->inv, n_local, srco);
+    if (comm) RST_CHECK(comm_allgatherv_f4(comm, srcog, st));
+    RST_CHECK(seqsum_enqueue(srcog, n_total, 3, sqws, fsum, st));  // point_cloud_utils.cpp:94-96
     k_init_state<<<1, kBS, 0, st>>>(slab, 0, fsum, ia, ctx->d_state);
   } else if (!p2plane) {
     if (n_local > 0) {
@@ -1653,7 +1651,35 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
       return RST_OK;
     };
     RST_CHECK(mark(0));
-    if (n_local > 0) {
+    if (refsum) {
+      // align_icp.cpp:105-151 with the reference's rounding: the searches
+      // record (q, d2) at the original index, the sequential sums give
+      // dst_mean (:113,122) and -- last iteration only: the reference reads
+      // only that one (:104,157) -- the cost (:120), k_cov_ref the
+      // covariance of the float products (:125-136)
+      if (n_local > 0) {
+        k_icp_nn<RefAcc><<<nblk, kBS, 0, st>>>(bv, av, tgt->pix, aa, src->pts, n_local, ctx->d_state,
+                                               nnq, cert, qbuf, qcnt, slab);
+        RST_CHECK(mark(1));
+        k_icp_fb<RefAcc><<<fb_grid, kBS, fb_lds, st>>>(bv, av, tgt->pix, aa, src->pts, ctx->d_state, nnq,
+                                                       cert, qbuf, qcnt, nblk, prm.lane_min, slab, slab2,
+                                                       n_local);
+      } else {
+        RST_CHECK(mark(1));
+      }
+      RST_CHECK(mark(2));
+      if (comm) RST_CHECK(comm_allgatherv_f4(comm, corrg, st));
+      RST_CHECK(seqsum_enqueue(corrg, n_total, it + 1 == opts.max_iter ? 4 : 3, sqws,
+                               ctx->d_state->seq, st));
+      if (n_local > 0)
+        k_cov_ref<<<kCovBlocks, kBS, 0, st>>>(srco, corr, n_local, n_total, ctx->d_state, slab2);
+      k_reduce_solve<RefAcc><<<1, kRedBS, 0, st>>>(slab, 0, slab2, n_local > 0 ? kCovBlocks : 0, prm,
+                                                   ctx->d_state, red_out);
+      if (comm) {
+        RST_CHECK(comm_allreduce_sum_f64(comm, totals, RefAcc::NV, st));
+        k_solve_only<RefAcc><<<1, 64, 0, st>>>(totals, prm, ctx->d_state);
+      }
+    } else if (n_local > 0) {
       // kernel 1 (certificates), kernel 2 (the queued searches)
       auto nn_pass = [&](auto tag) -> int {
         using Acc = typename decltype(tag)::type;
@@ -1669,15 +1695,6 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
         RST_CHECK(nn_pass(AccTag<P2PlaneAcc>{}));
         k_reduce_solve<P2PlaneAcc><<<1, kRedBS, 0, st>>>(slab, 0, slab2, fb_grid, prm,
                                                          ctx->d_state, red_out);
-      } else if (refsum) {
-        RST_CHECK(nn_pass(AccTag<RefAcc>{}));
-        // align_icp.cpp:113,120: sum dst[nbr_i] and cost, i ascending, fp32
-        // (the cost is only read after the last iteration, :104,157)
-        RST_CHECK(seqsum_enqueue(corr, n_local, it + 1 == opts.max_iter ? 4 : 3, sqws,
-                                 ctx->d_state->seq, st));
-        k_cov_ref<<<kCovBlocks, kBS, 0, st>>>(srco, corr, n_local, ctx->d_state, slab2);
-        k_reduce_solve<RefAcc><<<1, kRedBS, 0, st>>>(slab, 0, slab2, kCovBlocks, prm,
-                                                     ctx->d_state, nullptr);
       } else {
         RST_CHECK(nn_pass(AccTag<P2PointAcc>{}));
         k_reduce_solve<P2PointAcc><<<1, kRedBS, 0, st>>>(slab, 0, slab2, fb_grid, prm,
@@ -1689,7 +1706,7 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
       // an empty shard still joins the all-reduce with zero partial sums
       RST_HIP(hipMemsetAsync(totals, 0, sizeof(double) * NV, st));
     }
-    if (comm) {
+    if (comm && !refsum) {
       RST_CHECK(comm_allreduce_sum_f64(comm, totals, NV, st));
       if (p2plane)
         k_solve_only<P2PlaneAcc><<<1, 64, 0, st>>>(totals, prm, ctx->d_state);

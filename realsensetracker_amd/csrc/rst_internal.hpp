@@ -258,5 +258,12 @@ int compute_covariances_device(rst_ctx* ctx, const rst_target* tgt, int use_gicp
 int comm_allreduce_sum_f64(rst_comm* comm, double* d_buf, size_t count,
                            hipStream_t stream);
 int comm_size(const rst_comm* comm);
+// every rank's shard size (exchanged once per layout): n_total, this rank's
+// offset in the whole source's order, the counts
+int comm_shard_layout(rst_comm* comm, int64_t n_local, int64_t n_total_hint, hipStream_t st,
+                      int64_t* n_total, int64_t* offset,
+                      const std::vector<int64_t>** counts);
+// in-place all-gather of every rank's stretch [off_r, off_r + n_r) of buf
+int comm_allgatherv_f4(rst_comm* comm, float4* buf, hipStream_t st);
 
 }  // namespace rst

@@ -7,15 +7,19 @@ scaling of AlignIcp3d (align_icp.cpp:92-153) to one node:
 * the source splits into contiguous shards, ``shard_bounds``;
 * per iteration every rank reduces its 16 (P2POINT_REF) / 30 (P2PLANE) fp64
   partial sums to one row and ONE RCCL all-reduce over xGMI makes them
-  global; every rank then solves the same pose (no broadcast).
+  global; every rank then solves the same pose (no broadcast);
+* the reference-rounding mode (RST_SUM_REF, the library default): the shards
+  are contiguous stretches of the source order, so each iteration every rank
+  all-gathers the correspondences (16 B per source point) into the whole
+  source's order and walks the sequential fp32 sums redundantly -- the same
+  bit-exact dst_mean and cost on every rank -- and the 9 covariance sums are
+  all-reduced.
 
 Host logic only: the RCCL communicator is created from a unique id that
 rank 0 draws and broadcasts -- through ``rendezvous.Rendezvous`` (TCP; what
 ``bench.py`` uses, no second HIP runtime in the process) or through a
 ``torch.distributed`` group (the gloo CPU tests).  The per-iteration
 exchange is inside librst_align.so (``rst_icp_align_sharded_device``).
-The sequential-sum mode (RST_SUM_REF) has no shard decomposition: the
-sharded align runs RST_SUM_FP64.
 """
 from __future__ import annotations
 
@@ -92,9 +96,11 @@ class ShardedAligner:
                                         C.byref(self._comm)), "rst_comm_create")
 
     def align(self, d_src_shard: int, n_shard: int, target, opts=None, pose=None,
-              n_total: int = 0):
-        """n_total > 0 (the points of all shards, when the caller knows it):
-        no count all-reduce and no host round trip before the loop."""
+              n_total: int | None = None):
+        """n_total (the points of all shards, when the caller knows it; by
+        default opts.n_total): after the communicator's first align, no count
+        exchange and no host round trip before the loop.  The library checks
+        it against the exchanged shard sizes."""
         pose = np.eye(4, dtype=np.float32) if pose is None else np.asarray(pose, np.float32)
         buf = L.pose_to_cm(pose)
         mc = C.c_float(0)
@@ -104,7 +110,7 @@ class ShardedAligner:
             C.byref(o), L.fptr(buf), C.byref(mc)), "rst_icp_align_sharded_device")
         return st == L.RST_OK, L.cm_to_pose(buf), float(mc.value)
 
-    def align_prepared(self, src_shard, target, opts=None, pose=None, n_total: int = 0):
+    def align_prepared(self, src_shard, target, opts=None, pose=None, n_total: int | None = None):
         """The same with a prepared source shard (a Target): no per-call
         Morton sort of the shard."""
         pose = np.eye(4, dtype=np.float32) if pose is None else np.asarray(pose, np.float32)
@@ -118,10 +124,12 @@ class ShardedAligner:
 
     @staticmethod
     def _opts(opts, n_total):
+        """A copy of opts (the library defaults when None); n_total only
+        overrides opts.n_total when given."""
         o = L.IcpOpts()
-        C.memmove(C.byref(o), C.byref(opts if opts is not None else
-                                      L.default_opts(sum_mode=L.RST_SUM_FP64)), C.sizeof(o))
-        o.n_total = int(n_total)
+        C.memmove(C.byref(o), C.byref(opts if opts is not None else L.default_opts()), C.sizeof(o))
+        if n_total is not None:
+            o.n_total = int(n_total)
         return o
 
     def close(self):

@@ -52,7 +52,44 @@ def sharded_icp(src, dst, tree, max_iter, lo, hi, allreduce):
     return T
 
 
-def _worker(rank, world, port, out):
+def seq_sum_f32(x):
+    """The reference's sequential float32 sum over axis 0 (ascending index)."""
+    return np.add.accumulate(np.asarray(x, np.float32), axis=0, dtype=np.float32)[-1]
+
+
+def sharded_icp_ref(src, dst, tree, max_iter, lo, hi, allgather, allreduce):
+    """RST_SUM_REF over shard [lo, hi) (the structure of icp.hip's sharded
+    refsum branch): the shards' source and, per iteration, their
+    correspondences (q, d2) are all-gathered into the whole source's order,
+    every rank takes the reference's sequential fp32 sums over them
+    (centroid :85-86, dst_mean :113,122, the same bits on every rank), and
+    the covariance of the reference's float products (:125-136) is a
+    sharded fp64 sum, all-reduced."""
+    n = len(src)
+    smean = seq_sum_f32(allgather(src[lo:hi])) * np.float32(1.0 / n)
+    T = np.eye(4, dtype=np.float32)
+    mu = np.float32(1.0)
+    b = (src[lo:hi] - smean).astype(np.float32)
+    for it in range(max_iter):
+        if it > 0 and it % 8 == 0:
+            mu = np.float32(mu / np.float32(1.4))
+        if hi > lo:
+            idx, d2 = tree.query(O.transform_points(T, src[lo:hi]))
+            corr = np.concatenate([dst[idx], d2[:, None]], 1).astype(np.float32)
+        else:
+            corr = np.zeros((0, 4), np.float32)
+        allc = allgather(corr)
+        dmean = (seq_sum_f32(allc[:, :3]) / np.float32(n)).astype(np.float32)
+        l = (mu / (corr[:, 3] + mu)).astype(np.float32)
+        w = (l * l).astype(np.float32)
+        a = (w[:, None] * (corr[:, :3] - dmean)).astype(np.float32)
+        part = (a[:, :, None] * b[:, None, :]).astype(np.float64).sum(0).ravel()
+        cov = allreduce(part).reshape(3, 3)
+        T = O.kabsch_pose(cov, smean, dmean)
+    return T
+
+
+def _worker(rank, world, port, out, mode="fp64"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -70,7 +107,15 @@ def _worker(rank, world, port, out):
             dist.all_reduce(t)
             return t.numpy()
 
-        T = sharded_icp(src, dst, tree, 32, lo, hi, allreduce)
+        def allgather(x):  # shards of different lengths, concatenated in rank order
+            parts = [None] * world
+            dist.all_gather_object(parts, np.ascontiguousarray(x))
+            return np.concatenate(parts, 0)
+
+        if mode == "ref":
+            T = sharded_icp_ref(src, dst, tree, 32, lo, hi, allgather, allreduce)
+        else:
+            T = sharded_icp(src, dst, tree, 32, lo, hi, allreduce)
         poses = [None] * world
         dist.all_gather_object(poses, T)
         if rank == 0:
@@ -97,6 +142,28 @@ def test_sharded_decomposition_gloo(world):
     assert max(pose_err(r["poses"][0], T1)) <= 1e-6
     _, To, _, _ = O.align_icp(g["src"], g["dst"], 32, sum_mode=1)
     assert max(pose_err(T1, To)) <= 2e-5
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_ref_decomposition_gloo(world):
+    """The sharded reference-rounding mode: all-gathered correspondences,
+    redundant sequential fp32 sums, all-reduced covariance.  Every rank ends
+    on the bitwise-same pose, that of the unsharded restatement, within 1e-6
+    of the reference-arithmetic oracle (the covariance's fp64 sum order)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    mp.start_processes(_worker, args=(world, port, q, "ref"), nprocs=world, start_method="spawn",
+                       join=True)
+    r = q.get()
+    assert all(np.array_equal(p, r["poses"][0]) for p in r["poses"])
+    g = load_golden("pair_80x60_s0")
+    tree = O.KDTree(g["dst"])
+    T1 = sharded_icp_ref(g["src"], g["dst"], tree, 32, 0, len(g["src"]), lambda x: x, lambda x: x)
+    assert max(pose_err(r["poses"][0], T1)) <= 1e-6
+    _, To, _, _ = O.align_icp(g["src"], g["dst"], 32, sum_mode=0)
+    e = pose_err(T1, To)
+    assert max(e) <= 1e-6, e
 
 
 def test_shard_bounds_tile():

@@ -403,7 +403,11 @@ def test_device_resident_path(ctx, sum_mode):
     assert np.array_equal(L.cm_to_pose(buf), T)
 
 
-def test_sharded_single_rank_equals_unsharded(ctx):
+@pytest.mark.parametrize("sum_mode", [REF, FP64])
+def test_sharded_single_rank_equals_unsharded(ctx, sum_mode):
+    """The sharded loop at one rank (RCCL in the loop: the correspondence
+    all-gather and the covariance all-reduce in the reference-rounding mode,
+    the 16-sum all-reduce in the fp64 mode) gives the unsharded loop's bits."""
     g = load_golden("pair_80x60_s0")
     uid = C.create_string_buffer(L.COMM_ID_BYTES)
     L.check(L.lib().rst_comm_get_unique_id(uid), "uid")
@@ -414,16 +418,21 @@ def test_sharded_single_rank_equals_unsharded(ctx):
         ds = A.DeviceBuffer.from_array(g["src"], ctx)
         buf = L.pose_to_cm(np.eye(4))
         mc = C.c_float(0)
-        o = L.default_opts()  # the sharded loop runs fp64 sums whatever sum_mode says
+        o = L.default_opts(sum_mode=sum_mode)
         st = L.lib().rst_icp_align_sharded_device(ctx.handle, comm, C.c_void_p(ds.ptr),
                                                   len(g["src"]), t.handle, C.byref(o),
                                                   L.fptr(buf), C.byref(mc))
         assert st == 0
         T = np.eye(4, dtype=np.float32)
-        A.AlignIcp3d(g["src"], g["dst"], t, 128, T, opts=fp64_opts())
+        A.AlignIcp3d(g["src"], g["dst"], t, 128, T, opts=L.default_opts(sum_mode=sum_mode))
         assert np.array_equal(L.cm_to_pose(buf), T)
-        # the caller-known n_total (no count all-reduce, no host round trip)
-        # and a prepared shard: the same loop, the same bits
+        if sum_mode == REF:
+            _, To, mco, _ = O.align_icp(g["src"], g["dst"], 128, sum_mode=0)
+            assert max(pose_err(T, To)) <= 1e-4
+            assert abs(mc.value - mco) <= 1e-5 * max(1.0, abs(mco))
+        # the caller-known n_total (no count exchange, no host round trip
+        # after the communicator's first align) and a prepared shard: the
+        # same loop, the same bits
         o.n_total = len(g["src"])
         buf2 = L.pose_to_cm(np.eye(4))
         assert L.lib().rst_icp_align_sharded_device(ctx.handle, comm, C.c_void_p(ds.ptr),
@@ -436,10 +445,12 @@ def test_sharded_single_rank_equals_unsharded(ctx):
                                                       C.byref(o), L.fptr(buf3),
                                                       C.byref(mc)) == 0
         assert np.array_equal(L.cm_to_pose(buf3), T)
-        o.n_total = len(g["src"]) - 1  # fewer than this rank's own shard: rejected
-        assert L.lib().rst_icp_align_sharded_device(ctx.handle, comm, C.c_void_p(ds.ptr),
-                                                    len(g["src"]), t.handle, C.byref(o),
-                                                    L.fptr(buf2), C.byref(mc)) == L.RST_E_ARG
+        # a wrong n_total is checked against the exchanged shard sizes
+        for bad in (len(g["src"]) - 1, len(g["src"]) + 5):
+            o.n_total = bad
+            assert L.lib().rst_icp_align_sharded_device(ctx.handle, comm, C.c_void_p(ds.ptr),
+                                                        len(g["src"]), t.handle, C.byref(o),
+                                                        L.fptr(buf2), C.byref(mc)) == L.RST_E_ARG
     finally:
         L.lib().rst_comm_destroy(comm)
 

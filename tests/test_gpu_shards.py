@@ -175,6 +175,15 @@ def test_configs3_1M_shards(ctx):
                                                      t.handle, C.byref(o), L.fptr(buf),
                                                      C.byref(mc)), "sharded")
         assert np.array_equal(L.cm_to_pose(buf), r.pose)
+        # the reference-rounding mode sharded (correspondence all-gather,
+        # sequential sums over the whole source, covariance all-reduce)
+        oref = L.default_opts(max_iter=16, sum_mode=L.RST_SUM_REF)
+        rr = A.align(pb, t, None, oref)
+        buf = L.pose_to_cm(np.eye(4))
+        L.check(L.lib().rst_icp_align_sharded_device(ctx.handle, comm, C.c_void_p(ds.ptr), len(pb),
+                                                     t.handle, C.byref(oref), L.fptr(buf),
+                                                     C.byref(mc)), "sharded ref")
+        assert np.array_equal(L.cm_to_pose(buf), rr.pose)
     finally:
         L.lib().rst_comm_destroy(comm)
 
