@@ -25,6 +25,16 @@ int rst_debug_query_nn_warm_stats(rst_ctx* ctx, const rst_target* tgt, const flo
  * solve kernel's reduction and solve times (10 ns ticks). */
 int rst_debug_queue_trace(rst_ctx* ctx, int32_t* out, int32_t n);
 
+/* RST_SUM_REF in-loop trace: with enable != 0, later aligns on ctx walk the
+ * cost chain every iteration (not only the last, the only one the
+ * reference reads, align_icp.cpp:104,157), and rst_debug_seq_trace gives, per
+ * iteration of the last align (first n <= 256), 4 floats: the sequential
+ * fp32 sums of the correspondences' x, y, z (dst_mean before the division,
+ * :113) and of their d2 (the cost, :120) -- bit for bit the reference's
+ * when every iteration's correspondences are. */
+int rst_debug_enable_seq_trace(rst_ctx* ctx, int enable);
+int rst_debug_seq_trace(rst_ctx* ctx, float* out, int32_t n);
+
 /* RST_DIAG builds, per iteration of the last align call on ctx (first n <=
  * 256), 4 int32: far-queue length, ball-tile chunks scanned (all waves),
  * ball-tile walks abandoned, deep (whole-wave) searches.  Zeros otherwise. */

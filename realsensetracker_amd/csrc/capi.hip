@@ -289,6 +289,19 @@ int rst_ctx_enable_graphs(rst_ctx* ctx, int enable) {
   return RST_OK;
 }
 
+int rst_debug_enable_seq_trace(rst_ctx* ctx, int enable) {
+  if (!ctx) return RST_E_ARG;
+  ctx->seq_trace = enable != 0;
+  return RST_OK;
+}
+
+int rst_debug_seq_trace(rst_ctx* ctx, float* out, int32_t n) {
+  if (!ctx || !out || n < 0) return RST_E_ARG;
+  for (int i = 0; i < n && i < kQTrace; ++i)
+    for (int j = 0; j < 4; ++j) out[4 * i + j] = ctx->h_state->seqtr[i][j];
+  return RST_OK;
+}
+
 int rst_ctx_enable_kernel_timing(rst_ctx* ctx, int enable) {
   if (!ctx) return RST_E_ARG;
   ctx->timing = enable != 0;

@@ -1006,6 +1006,8 @@ __global__ __launch_bounds__(kRedBS) void k_reduce_solve(const double* __restric
     if (it < kQTrace) {  // diagnostics (rst_debug_queue_trace): 10 ns ticks
       st->path[it][2] = (int)(t1 - t0);
       st->path[it][3] = (int)(t2 - t1);
+      if constexpr (std::is_same<Acc, RefAcc>::value)
+        for (int k = 0; k < 4; ++k) st->seqtr[it][k] = core.seq[k];
     }
   }
 }
@@ -1019,8 +1021,12 @@ __global__ void k_solve_only(const double* __restrict__ totals, IcpParams prm,
   if (Acc::kCanFinish && core.done) return;
   double tot[Acc::NV];
   for (int k = 0; k < Acc::NV; ++k) tot[k] = totals[k];
+  const int it = core.iter;
   acc_update<Acc>(tot, prm, &core);
   *static_cast<IcpCore*>(st) = core;
+  if constexpr (std::is_same<Acc, RefAcc>::value)
+    if (it < kQTrace)
+      for (int k = 0; k < 4; ++k) st->seqtr[it][k] = core.seq[k];
 }
 
 // ---- kernel 2: the searches of the queued queries -----------------------------------
@@ -1669,8 +1675,8 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
       }
       RST_CHECK(mark(2));
       if (comm) RST_CHECK(comm_allgatherv_f4(comm, corrg, st));
-      RST_CHECK(seqsum_enqueue(corrg, n_total, it + 1 == opts.max_iter ? 4 : 3, sqws,
-                               ctx->d_state->seq, st));
+      RST_CHECK(seqsum_enqueue(corrg, n_total, it + 1 == opts.max_iter || ctx->seq_trace ? 4 : 3,
+                               sqws, ctx->d_state->seq, st));
       if (n_local > 0)
         k_cov_ref<<<kCovBlocks, kBS, 0, st>>>(srco, corr, n_local, n_total, ctx->d_state, slab2);
       k_reduce_solve<RefAcc><<<1, kRedBS, 0, st>>>(slab, 0, slab2, n_local > 0 ? kCovBlocks : 0, prm,

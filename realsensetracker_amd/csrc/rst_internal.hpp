@@ -78,6 +78,8 @@ struct IcpState : IcpCore {
   int32_t qlen[kQTrace];  // fallback-queue length per iteration (diagnostics)
   int32_t path[kQTrace][4];  // per-iteration diagnostics (rst_debug_queue_trace)
   int32_t diag[kQTrace][4];  // RST_DIAG builds: far queue, ball chunks, ball aborts, deep searches
+  float seqtr[kQTrace][4];   // RST_SUM_REF: each iteration's sequential sums (sum q xyz, cost;
+                             // the cost every iteration only under rst_debug_enable_seq_trace)
 };
 
 struct IcpParams {
@@ -119,6 +121,7 @@ struct rst_ctx {
   // (pyramid level, iterations, P2PLANE, RST_SUM_REF) -> executable graph,
   // updated in place per align
   bool graphs = false;
+  bool seq_trace = false;  // RST_SUM_REF: walk the cost chain every iteration (diagnostics)
   std::map<std::tuple<int, int, int, int>, hipGraphExec_t> gexec;
   // device memory of freed targets, kept for the next build (hipFree
   // synchronises the whole device, which would stall every stream of a

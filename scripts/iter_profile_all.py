@@ -11,6 +11,7 @@ rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 
 
 def short(n: str) -> str:
+    n = n.replace("(anonymous namespace)::", "")
     n = re.sub(r"\(.*", "", n)
     n = re.sub(r"<.*", "", n)
     return n.split("::")[-1]

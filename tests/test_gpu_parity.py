@@ -487,7 +487,10 @@ def test_p2plane_matches_restatement(ctx, name):
     r = A.align_prepared(s, t, None, L.default_opts(mode=L.RST_P2PLANE, max_iter=30))
     assert r.ok
     e = pose_err(r.pose, g["p2plane_pose"])
+    print(f"P2PLANE {name} vs restatement {e}, vs truth {pose_err(r.pose, g['T_gt'])}")
     assert max(e) <= 1e-4, e
+    # (the ground truth of a few-thousand-point noisy fixture: the motion is
+    # recovered to ~1e-3; the parity gate is the restatement's above)
     assert max(pose_err(r.pose, g["T_gt"])) <= 3e-3
 
 
@@ -617,7 +620,7 @@ def test_p2plane_640_recovers_motion(ctx, normals_k):
     e = pose_err(r.pose, D)
     print(f"P2PLANE 640x480 normals_k={normals_k}: {r.iterations} iterations, error {e}")
     assert r.ok
-    assert e[0] < 5e-4 and e[1] < 5e-4, e  # measured ~3e-5 rad, ~1.1e-4 m
+    assert e[0] < 1e-4 and e[1] < 2.5e-4, e  # measured ~3e-5 rad, ~1.1e-4 m
 
 
 # ---- SolveKabsch (align_icp.cpp:18-71) -------------------------------------------------
