@@ -7,16 +7,18 @@ One step = one incoming frame of the stream, fully on the GPU:
     -> AlignIcp3d(curr, prev) with the reference's P2POINT_REF loop,
        128 fixed iterations (rs_replay_app.cpp:246-251).
 value = ICP iterations/s over all ranks (steps * 128 / time).  Frame
-preparation runs on its own HIP stream and --inflight frame pairs (default 4,
-on 8 hardware queues: --hw-queues) are aligned concurrently, each on its own context/stream: one pair's
-iteration chain is launch/latency-bound, so independent pairs overlap on the
-GPU.  A second timed loop runs the build's point-to-plane mode on the same
+preparation runs on its own HIP stream and --inflight frame pairs (default
+24 in the reference-rounding mode, 4 in the fp64 mode; 24 HIP hardware
+queues: --hw-queues) are aligned concurrently, each on its own
+context/stream: one pair's iteration chain is launch/latency-bound, so
+independent pairs overlap on the GPU.  A second timed loop runs the build's point-to-plane mode on the same
 frames (reported as extra fields).
 
-The value line runs the throughput mode (RST_SUM_FP64: fp64 partial sums);
-the reference-rounding mode (RST_SUM_REF, the library default: sequential
-fp32 sums exactly as align_icp.cpp rounds them) is timed on the same
-stream as the extra field "ref_sums".
+The value line runs the drop-in default, RST_SUM_REF: the reference's
+sequential fp32 sums exactly as align_icp.cpp rounds them, the mode within
+the north_star's 1e-4 gate (24 pairs in flight); the throughput mode
+RST_SUM_FP64 (fp64 partial sums, outside that gate) is timed on the same
+stream as the extra field "fp64_sums" (--sum-mode fp64 swaps them).
 
 roofline: the dominant kernel k_icp_nn (transform + exact NN + weighted
 partial sums of one ICP iteration), algorithmic bytes per launch
@@ -264,7 +266,7 @@ def run_sharded(a, K, frames, d_depth, hip, world, rank, local, rdv, barrier, ma
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=48)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="stream",
                     help="stream: configs[1] (configs[2] with --width 1280 --height 720); "
@@ -285,7 +287,7 @@ def main():
     ap.add_argument("--no-gicp", action="store_true")
     ap.add_argument("--graphs", action="store_true",
                     help="replay each align's iteration loop as a hipGraph (no kernel timing)")
-    ap.add_argument("--sum-mode", choices=["fp64", "ref"], default="fp64",
+    ap.add_argument("--sum-mode", choices=["fp64", "ref"], default="ref",
                     help="the value leg's sums: fp64 = RST_SUM_FP64 (fp64 partial sums), "
                          "ref = RST_SUM_REF (the drop-in default: the reference's sequential "
                          "fp32 sums, bit-exact); the other mode is timed as an extra field")
@@ -438,7 +440,9 @@ def main():
             c.synchronize()
 
     # ---- throughput mode (value): no events in the timed region -----------------
-    run(a.warmup, opts_main, 0, None)
+    # warm-up: W pairs, and at least one per context in flight, so that no
+    # context sizes its device workspace inside the timed region
+    run(max(a.warmup, len(actx)), opts_main, 0, None)
     st = new_stats()
     barrier()
     sync_all()
@@ -495,7 +499,7 @@ def main():
     if a.ref_steps > 0 and not pyr:
         n_other = 4 if main_ref else a.ref_inflight
         rctx = (actx + [A.Context(local) for _ in range(max(0, n_other - len(actx)))])[:n_other]
-        run(1, opts_other, 0, None, rctx)
+        run(len(rctx), opts_other, 0, None, rctx)  # every context warmed (as above)
         sr = new_stats()
         barrier()
         sync_all()
@@ -584,7 +588,8 @@ def main():
     value = iters_all / dt
     out = {
         "metric": METRIC, "value": value, "unit": "ICP iterations/s", "n_gpus": world,
-        "steps": a.steps, "warmup": a.warmup, "ms_per_step": 1000.0 * dt / a.steps,
+        "steps": a.steps, "warmup": a.warmup, "warmup_pairs": max(a.warmup, len(actx)),
+        "ms_per_step": 1000.0 * dt / a.steps,
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic (seeded procedural RGB-D room, ray-cast u16 depth, 1 mm noise, "
                 "~3% invalid)",

@@ -81,6 +81,12 @@ int rst_debug_seq_stages(rst_ctx* ctx, const float* xyzw, int64_t n, int nch, in
                          float out[4], void* ws_out, int64_t ws_bytes, int* failed_stage);
 int64_t rst_debug_seq_ws_bytes(int64_t n);
 
+/* The dispatch-rate probe: `launches` empty kernels (blocks x threads) on
+ * each of nstreams fresh streams, streams interleaved; *per_s = kernels
+ * completed per second (host clock, launch to the last stream's sync). */
+int rst_debug_launch_rate(rst_ctx* ctx, int nstreams, int launches, int blocks, int threads,
+                          double* per_s);
+
 /* A device stream copy (the measured HBM ceiling the rooflines are read
  * against): `bytes` copied buffer to buffer by a float4 grid-stride kernel,
  * reps launches timed with HIP events; *gbps = (read + write bytes) / the

@@ -415,7 +415,10 @@ int target_build_device(rst_ctx* ctx, const float* d_xyz, int64_t m, bool with_b
   rst_target* t = new rst_target();
   t->ctx = ctx;
   t->m = m;
-  ctx->live.push_back(t);
+  {
+    std::lock_guard<std::mutex> lk(ctx->pool_mu);
+    ctx->live.push_back(t);
+  }
   hipStream_t st = ctx->stream;
   const int64_t mp = std::max<int64_t>(m, 1);
   auto ta = [&](auto** p, size_t bytes) { return target_alloc(t, bytes, (void**)p) >= 0; };

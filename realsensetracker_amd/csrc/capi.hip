@@ -4,6 +4,8 @@
 // device workspace; *_device entry points take HBM pointers directly.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
+
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
@@ -42,6 +44,7 @@ constexpr size_t kPoolMaxBytes = (size_t)4 << 30;
 int ctx_alloc(rst_ctx* ctx, size_t bytes, void** out, size_t* class_bytes) {
   const size_t c = size_class(bytes);
   *class_bytes = c;
+  std::lock_guard<std::mutex> lk(ctx->pool_mu);
   auto it = ctx->pool.find(c);
   if (it != ctx->pool.end()) {
     *out = it->second;
@@ -61,12 +64,15 @@ int ctx_alloc(rst_ctx* ctx, size_t bytes, void** out, size_t* class_bytes) {
 
 void ctx_release(rst_ctx* ctx, void* p, size_t c) {
   if (!p) return;
-  if (ctx && ctx->pool_bytes + c <= kPoolMaxBytes) {
-    ctx->pool.emplace(c, p);
-    ctx->pool_bytes += c;
-  } else {
-    hipFree(p);
+  if (ctx) {
+    std::lock_guard<std::mutex> lk(ctx->pool_mu);
+    if (ctx->pool_bytes + c <= kPoolMaxBytes) {
+      ctx->pool.emplace(c, p);
+      ctx->pool_bytes += c;
+      return;
+    }
   }
+  hipFree(p);
 }
 
 int target_alloc(rst_target* t, size_t bytes, void** out) {
@@ -172,6 +178,12 @@ __global__ __launch_bounds__(256) void k_stream_copy(const float4* __restrict__ 
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride)
     __builtin_nontemporal_store(__builtin_nontemporal_load(av + i), bv + i);
+}
+
+// the dispatch-rate probe (rst_debug_launch_rate): a kernel that does
+// nothing but exist (one vector store per block to lane 0's slot)
+__global__ void k_nop(int* __restrict__ sink, int tag) {
+  if (threadIdx.x == 0 && tag < 0) sink[blockIdx.x] = tag;
 }
 
 }  // namespace rst
@@ -368,6 +380,7 @@ int rst_target_free(rst_target* t) {
   // context is gone, to the device
   rst_ctx* ctx = t->ctx;
   if (ctx) {
+    std::lock_guard<std::mutex> lk(ctx->pool_mu);
     auto& lv = ctx->live;
     for (size_t k = 0; k < lv.size(); ++k)
       if (lv[k] == t) {
@@ -588,6 +601,36 @@ int rst_debug_stream_copy(rst_ctx* ctx, int64_t bytes, int reps, double* gbps) {
   if (s < 0) return s;
   *gbps = best > 0.f ? 2.0 * 16.0 * (double)n4 / (best * 1e-3) / 1e9 : 0.0;
   return RST_OK;
+}
+
+int rst_debug_launch_rate(rst_ctx* ctx, int nstreams, int launches, int blocks, int threads,
+                          double* per_s) {
+  if (!ctx || !per_s || nstreams < 1 || nstreams > 64 || launches < 1 || blocks < 1 ||
+      threads < 1 || threads > 1024)
+    return RST_E_ARG;
+  RST_HIP(hipSetDevice(ctx->device));
+  std::vector<hipStream_t> ss(nstreams, nullptr);
+  int s = RST_OK;
+  for (auto& q : ss)
+    if (hipStreamCreateWithFlags(&q, hipStreamNonBlocking) != hipSuccess) s = RST_E_HIP;
+  int* sink = nullptr;
+  if (s >= 0 && hipMalloc(&sink, sizeof(int) * blocks) != hipSuccess) s = RST_E_NOMEM;
+  // warm-up, then the timed round: launches per stream, streams interleaved
+  for (int rep = 0; rep < 2 && s >= 0; ++rep) {
+    const int nl = rep == 0 ? 8 : launches;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int i = 0; i < nl; ++i)
+      for (auto q : ss) k_nop<<<blocks, threads, 0, q>>>(sink, 1);
+    for (auto q : ss)
+      if (hipStreamSynchronize(q) != hipSuccess) s = RST_E_HIP;
+    const double dt =
+        std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    *per_s = (double)nl * nstreams / dt;
+  }
+  for (auto q : ss)
+    if (q) (void)hipStreamDestroy(q);
+  if (sink) (void)hipFree(sink);
+  return s;
 }
 
 int rst_debug_seq_sum(rst_ctx* ctx, const float* xyzw, int64_t n, int serial, int reps,

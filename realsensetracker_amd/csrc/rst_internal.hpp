@@ -12,6 +12,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <map>
+#include <mutex>
 #include <tuple>
 #include <utility>
 #include <vector>
@@ -129,6 +130,9 @@ struct rst_ctx {
   std::multimap<size_t, void*> pool;
   size_t pool_bytes = 0;
   std::vector<rst_target*> live;  // targets built on this context
+  // guards pool / pool_bytes / live: a target may be freed on another host
+  // thread than the one building the next (a frame-preparation thread)
+  std::mutex pool_mu;
   // the align enqueued by icp_launch and not yet collected by icp_finish
   struct Pending {
     bool early_false = false;

@@ -60,6 +60,7 @@ struct SqView {
   int* gs;         // [nch][ng + 1]
   int* ks;         // [nch][nk + 1]
   double* inc;     // [nch][nb]
+  double* ipre;    // [nch][nb]: exclusive prefix of inc within the block's tile
   double* tinc;    // [nch][nk]
   Leaf* leaf;      // [nch][nb]
   GroupMap* grp;   // [nch][ng]
@@ -146,49 +147,62 @@ __device__ __forceinline__ int quad_or(int a) {
   return a;
 }
 
+// (one workgroup per tile, its four quarter tiles in turn: a quarter per
+// workgroup spent the workgroup dispatch rate the loop is bound by)
 __global__ __launch_bounds__(kFrontT) void k_sq_tot(const float4* __restrict__ x, SqView v) {
-  __shared__ double red[kFrontT / kWave][4];
-  const int qt = blockIdx.x, tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid / kWave;
-  const int64_t i0 = (int64_t)qt * kTotE + 4 * tid;
-  float4 q[4];
+  __shared__ double red[kTotQ][kFrontT / kWave][4];
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid / kWave;
+  float4 q[kTotQ][4];  // every load of the tile in flight first
 #pragma unroll
-  for (int j = 0; j < 4; ++j) q[j] = i0 + j < v.n ? x[i0 + j] : make_float4(0.f, 0.f, 0.f, 0.f);
-  double part[4];
+  for (int k = 0; k < kTotQ; ++k) {
+    const int64_t i0 = ((int64_t)blockIdx.x * kTotQ + k) * kTotE + 4 * tid;
 #pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    float e[4];
-    int f = 0;
-    double ps = 0.0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      e[j] = comp(q[j], c);
-      const int fj = nf_flags(e[j]);
-      f |= fj;
-      ps += fj ? 0.0 : (double)e[j];
-    }
-    part[c] = ps;
-    if (c < v.nch) {
-      float* dst = v.soa + (int64_t)c * v.ns;
-      // (ns is a multiple of 64 and i0 of 4: the float4 is in the row)
-      if (i0 < v.n) *reinterpret_cast<float4*>(dst + i0) = make_float4(e[0], e[1], e[2], e[3]);
-      f = quad_or(f);
-      const int64_t w = i0 / kW;
-      if ((tid & 3) == 0 && w < v.nb) v.wflg[(int64_t)c * v.nb + w] = (uint8_t)f;
-    }
+    for (int j = 0; j < 4; ++j) q[k][j] = i0 + j < v.n ? x[i0 + j] : make_float4(0.f, 0.f, 0.f, 0.f);
   }
 #pragma unroll
-  for (int o = kWave / 2; o > 0; o >>= 1)
+  for (int k = 0; k < kTotQ; ++k) {
+    const int qt = blockIdx.x * kTotQ + k;
+    const int64_t i0 = (int64_t)qt * kTotE + 4 * tid;
+    double part[4];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) part[c] += __shfl_xor(part[c], o, kWave);
-  if (lane == 0)
+    for (int c = 0; c < 4; ++c) {
+      float e[4];
+      int f = 0;
+      double ps = 0.0;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) red[wv][c] = part[c];
+      for (int j = 0; j < 4; ++j) {
+        e[j] = comp(q[k][j], c);
+        const int fj = nf_flags(e[j]);
+        f |= fj;
+        ps += fj ? 0.0 : (double)e[j];
+      }
+      part[c] = ps;
+      if (c < v.nch) {
+        float* dst = v.soa + (int64_t)c * v.ns;
+        // (ns is a multiple of 64 and i0 of 4: the float4 is in the row)
+        if (i0 < v.n) *reinterpret_cast<float4*>(dst + i0) = make_float4(e[0], e[1], e[2], e[3]);
+        f = quad_or(f);
+        const int64_t w = i0 / kW;
+        if ((tid & 3) == 0 && w < v.nb) v.wflg[(int64_t)c * v.nb + w] = (uint8_t)f;
+      }
+    }
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) part[c] += __shfl_xor(part[c], o, kWave);
+    if (lane == 0)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) red[k][wv][c] = part[c];
+  }
   __syncthreads();
-  if (tid < v.nch) {
-    double t = 0.0;
+  if (tid < kTotQ * 4) {
+    const int k = tid / 4, c = tid % 4;
+    if (c < v.nch) {
+      double t = 0.0;
 #pragma unroll
-    for (int w = 0; w < kFrontT / kWave; ++w) t += red[w][tid];
-    v.ttot[(int64_t)tid * v.nk * kTotQ + qt] = t;
+      for (int w = 0; w < kFrontT / kWave; ++w) t += red[k][w][c];
+      v.ttot[(int64_t)c * v.nk * kTotQ + blockIdx.x * kTotQ + k] = t;
+    }
   }
 }
 
@@ -331,19 +345,32 @@ __global__ __launch_bounds__(kFrontT) void k_sq_front(SqView v) {
     v.inc[(int64_t)c * v.nb + b] = incv;
   }
   double itot;
-  (void)block_scan_excl<kFrontT>(incv, lds, &itot);
+  const double ipv = block_scan_excl<kFrontT>(incv, lds, &itot);
+  if (b < v.nb) v.ipre[(int64_t)c * v.nb + b] = ipv;
   if (tid == 0) v.tinc[(int64_t)c * v.nk + t] = itot;
 }
 
 // ---- 3: leaf, group and superblock maps ------------------------------------------
-constexpr int kMapT = 1024;
+// threads per map workgroup: the leaf lanes take 2 * kMapT / 2 ... blocks in
+// rounds (the leaf phase is VALU-bound: fewer, busier waves take as long and
+// leave the CU's other wave slots to other kernels); a group's 16 residue
+// lanes need 31 * 16 <= kMapT
+#ifndef RST_SQ_MAP_T
+#define RST_SQ_MAP_T 512
+#endif
+constexpr int kMapT = RST_SQ_MAP_T;
+static_assert(kMapT >= kMaxSbGroups * kGroupR && kMapT % kWave == 0, "map workgroup size");
+constexpr int kLeafRounds = (2 * kMaxSbBlocks + kMapT - 1) / kMapT;
 
 __device__ __forceinline__ float cand(float G, int e0, int r) {
   return (float)((double)G + ldexp((double)r, e0));
 }
 
 __global__ __launch_bounds__(kMapT) void k_sq_maps(SqView v) {
-  __shared__ float xs[kMaxSbElems];
+  // (one pad float per 16: the leaf lanes' blocks start ~16 elements apart,
+  // padded they read distinct banks)
+  __shared__ float xsp[kMaxSbElems + kMaxSbElems / 16 + 1];
+  auto xs = [&](int i) -> float& { return xsp[i + (i >> 4)]; };
   __shared__ Leaf lf[kMaxSbBlocks];
   __shared__ GroupMap gm[kMaxSbGroups];
   __shared__ double Gd[kMaxSbBlocks + 1];
@@ -386,33 +413,33 @@ __global__ __launch_bounds__(kMapT) void k_sq_maps(SqView v) {
     for (int j = 0; j < kJ; ++j) tv[j] = tid + j * kMapT < nel ? X[ea + tid + j * kMapT] : 0.0f;
 #pragma unroll
     for (int j = 0; j < kJ; ++j)
-      if (tid + j * kMapT < nel) xs[tid + j * kMapT] = tv[j];
+      if (tid + j * kMapT < nel) xs(tid + j * kMapT) = tv[j];
   }
   for (int i = tid; i <= nblk; i += kMapT) sbs[i] = bsg[ba + i] - ea;
   for (int i = tid; i <= ngr; i += kMapT) sgs[i] = gsg[ga + i] - ba;
   if (tid == 0) clk[1] = (long long)__builtin_amdgcn_s_memtime();
-  // refined guesses: the fp64 prefix of the blocks' float32 increments
-  const double* inc = v.inc + (int64_t)c * v.nb;
-  const int tb = ba / kBlocksPerTile;
-  double base = block_sum_global<kMapT>(v.tinc + (int64_t)c * v.nk, tb, lds);
-  __syncthreads();
-  base += block_sum_global<kMapT>(inc + (int64_t)tb * kBlocksPerTile, ba - tb * kBlocksPerTile, lds);
-  __syncthreads();
+  // refined guesses: the fp64 prefix of the blocks' float32 increments --
+  // the tiles' totals before the superblock's first tile, plus each block's
+  // prefix within its tile (k_sq_front); a superblock spans <= 2 tiles
   {
-    // nblk <= 511 < kMapT: one increment per thread
-    const double iv = tid < nblk ? inc[ba + tid] : 0.0;
-    double tot;
-    const double pre = block_scan_excl<kMapT>(iv, lds, &tot);
-    if (tid < nblk) Gd[tid] = ba + tid == 0 ? 0.0 : base + pre;
+    const int tb = ba / kBlocksPerTile;
+    const double* tinc = v.tinc + (int64_t)c * v.nk;
+    const double iv = tid < nblk ? v.ipre[(int64_t)c * v.nb + ba + tid] : 0.0;  // (in flight)
+    const double next = tb < v.nk ? tinc[tb] : 0.0;
+    const double base = block_sum_global<kMapT>(tinc, tb, lds);
+    if (tid < nblk) {
+      const int b = ba + tid;
+      Gd[tid] = b == 0 ? 0.0 : (b / kBlocksPerTile == tb ? base : base + next) + iv;
+    }
   }
   __syncthreads();
   if (tid == 0) clk[2] = (long long)__builtin_amdgcn_s_memtime();
   // -- leaves: lane (block, residue pair): runs from candidates rp and rp + 2,
-  // interleaved (two independent dependency chains per lane, one round for
-  // up to 512 blocks)
+  // interleaved (two independent dependency chains per lane), kLeafRounds
+  // rounds of kMapT / 2 blocks
   Leaf* leafg = v.leaf + (int64_t)c * v.nb;
-  {
-    const int bl = tid >> 1, rp = tid & 1;
+  for (int round = 0; round < kLeafRounds; ++round) {
+    const int bl = (tid >> 1) + round * (kMapT / 2), rp = tid & 1;
     const bool act = bl < nblk;
     Run p0, p1;
     float G = 0.0f;
@@ -429,7 +456,7 @@ __global__ __launch_bounds__(kMapT) void k_sq_maps(SqView v) {
         s1 = s0;
       }
       for (int i = s0; i < s1; ++i) {
-        const float xv = xs[i];
+        const float xv = xs(i);
         run_step(p0, xv, e0);
         run_step(p1, xv, e0);
       }
@@ -1003,6 +1030,7 @@ static size_t sq_layout(SqView& v, int64_t n, int nch, char* base) {
   v.gs = (int*)take(sizeof(int) * nch * (size_t)(v.ng + 1));
   v.ks = (int*)take(sizeof(int) * nch * (size_t)(v.nk + 1));
   v.inc = (double*)take(sizeof(double) * nch * (size_t)v.nb);
+  v.ipre = (double*)take(sizeof(double) * nch * (size_t)v.nb);
   v.tinc = (double*)take(sizeof(double) * nch * (size_t)v.nk);
   v.leaf = (Leaf*)take(sizeof(Leaf) * nch * (size_t)v.nb);
   v.grp = (GroupMap*)take(sizeof(GroupMap) * nch * (size_t)v.ng);
@@ -1029,8 +1057,11 @@ int seqsum_enqueue(const float4* d_x, int64_t n, int nch, void* ws, float* d_out
   SqView v;
   sq_layout(v, n, nch, (char*)ws);
   v.stats = d_stats;
+#ifdef RST_SQ_ABLATE  // measurement only (wrong sums): skip kernels by bit
+  stages &= ~RST_SQ_ABLATE;
+#endif
   if (stages & 1) {
-    k_sq_tot<<<v.nk * kTotQ, kFrontT, 0, st>>>(d_x, v);
+    k_sq_tot<<<v.nk, kFrontT, 0, st>>>(d_x, v);
     k_sq_front<<<dim3(v.nk, nch), kFrontT, 0, st>>>(v);
   }
   if (stages & 2) k_sq_maps<<<dim3(v.nk, nch), kMapT, 0, st>>>(v);
