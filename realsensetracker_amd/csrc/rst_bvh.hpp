@@ -99,6 +99,7 @@ struct BvhView {
 struct PixView {
   const int32_t* __restrict__ map;  // null: the target has no pixel grid
   const float4* __restrict__ pts;   // [w h] grid pixel p's point (x, y, z, original index bits)
+  const int32_t* __restrict__ inv;  // [m] original index -> sorted position (the target's)
   float fx, fy, cx, cy;
   int32_t w, h, s;
   int32_t pad;

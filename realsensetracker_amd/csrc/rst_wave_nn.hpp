@@ -1292,11 +1292,20 @@ __device__ __forceinline__ bool ball_tile_search(const BvhView& bv, bool act, fl
 constexpr int kPixMaxW = 64;
 
 template <int N>
-struct PixScratch {  // per-wave LDS
+struct PixScratch {  // per-wave LDS: the staged pixels' points
   static constexpr int kN = N;
   float4 pts[N];
-  int pos[N];
 };
+
+// A window scan ranks candidates by (d2, original index) -- a frame's
+// original indices ascend with its pixels, and each staged pixel carries its
+// own (.w) -- and the winner's sorted position comes from the target's
+// inverse map once per lane afterwards: one 16-byte load per staged pixel.
+constexpr int kPosPending = 0;  // a candidate's position before pix_resolve
+__device__ __forceinline__ void pix_resolve(const BvhView& bv, const PixView& pv, Best2& r) {
+  if (r.pos[0] >= 0) r.pos[0] = (uint32_t)r.id[0] < (uint32_t)bv.m ? pv.inv[r.id[0]] : -1;
+  if (r.pos[1] >= 0) r.pos[1] = (uint32_t)r.id[1] < (uint32_t)bv.m ? pv.inv[r.id[1]] : -1;
+}
 
 __device__ __forceinline__ int wave_min_i(int x) {
 #pragma unroll
@@ -1432,12 +1441,10 @@ __device__ __forceinline__ bool pix_tile_search(const BvhView& bv, const PixView
   for (int c0 = 0; c0 < total; c0 += N) {
     const int cnt = min(N, total - c0);
     float4 pp[kPer];
-    int pk[kPer];
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {  // every load of the chunk in flight
       const int k = lane + j * kWave;
-      pk[j] = -1;
-      pp[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      pp[j] = make_float4(NAN, NAN, NAN, 0.f);
       if (k < cnt) {
         const int f = c0 + k;
         int g = 0;
@@ -1454,17 +1461,13 @@ __device__ __forceinline__ bool pix_tile_search(const BvhView& bv, const PixView
         const int kk = f - oo;
         const int rr = (int)(((float)kk + 0.5f) / (float)ow);  // kk / ow (exact: < 2^12)
         const int64_t px = (int64_t)(oy + rr) * pv.w + (ox + kk - rr * ow);
-        pk[j] = pv.map[px];
         pp[j] = pv.pts[px];
       }
     }
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
       const int k = lane + j * kWave;
-      if (k < cnt) {
-        ts.pts[k] = pp[j];
-        ts.pos[k] = (uint32_t)pk[j] < (uint32_t)bv.m ? pk[j] : -1;
-      }
+      if (k < cnt) ts.pts[k] = pp[j];
     }
     wave_sync();
     if (ok) {
@@ -1475,20 +1478,19 @@ __device__ __forceinline__ bool pix_tile_search(const BvhView& bv, const PixView
         const int row = moff + (b - my) * mw - mx - c0;
         for (int a = a0; a <= a1; a += 4) {
           float4 t[4];
-          int pp[4];
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const int k = row + a + j;
             const bool in = a + j <= a1 && (uint32_t)k < (uint32_t)cnt;
             t[j] = in ? ts.pts[k] : make_float4(NAN, NAN, NAN, 0.f);
-            pp[j] = in ? ts.pos[k] : -1;
           }
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const float d = d2_ref(qx, qy, qz, t[j].x, t[j].y, t[j].z);
-            if (pp[j] >= 0 && d <= r.d[1]) {  // (offer's own test, hoisted)
-              r.offer(d, f2i(t[j].w), pp[j]);
-              if (r.pos[0] == pp[j]) q0 = t[j];
+            if (d <= r.d[1]) {  // (offer's own test, hoisted; NaN: no point)
+              const int id = f2i(t[j].w);
+              r.offer(d, id, kPosPending);
+              if (r.id[0] == id) q0 = t[j];
             }
           }
         }
@@ -1496,6 +1498,7 @@ __device__ __forceinline__ bool pix_tile_search(const BvhView& bv, const PixView
     }
     wave_sync();
   }
+  if (ok) pix_resolve(bv, pv, r);
   // (the seed lies in the window, so the first is within rc; checked anyway)
   return ok && r.pos[0] >= 0 && margin_sqrt(r.d[0]) * 1.00001f + 1e-30f < rc;
 }
@@ -1517,25 +1520,24 @@ __device__ __forceinline__ bool row_pix(const BvhView& bv, const PixView& pv, bo
   const float rwa = 1.0f / (float)max(wa, 1);
   for (int k0 = 0; k0 < cnt; k0 += 16 * 8) {
     float4 p[8];
-    int pos[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {  // 8 pixels per lane in flight
       const int k = k0 + sub + 16 * j;
-      pos[j] = -1;
-      p[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      p[j] = make_float4(NAN, NAN, NAN, 0.f);
       if (k < cnt) {
         const int rr = (int)(((float)k + 0.5f) * rwa);  // k / wa (exact)
         const int64_t px = (int64_t)(b0 + rr) * pv.w + (a0 + k - rr * wa);
-        pos[j] = pv.map[px];
         p[j] = pv.pts[px];
       }
     }
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
-      if ((uint32_t)pos[j] < (uint32_t)bv.m)
-        mine.offer(d2_ref(qx, qy, qz, p[j].x, p[j].y, p[j].z), f2i(p[j].w), pos[j]);
+    for (int j = 0; j < 8; ++j) {
+      const float d = d2_ref(qx, qy, qz, p[j].x, p[j].y, p[j].z);
+      if (d <= mine.d[1]) mine.offer(d, f2i(p[j].w), kPosPending);  // (NaN: no point)
+    }
   }
   mine = wave_lex_min<8>(mine);
+  if (ok) pix_resolve(bv, pv, mine);
   const bool ex = ok && mine.pos[0] >= 0 && margin_sqrt(mine.d[0]) * 1.00001f + 1e-30f < rc;
   if (ex) r = mine;  // (else r keeps its seeds for the next search)
   return ex;

@@ -278,6 +278,7 @@ static int frame_prepare(rst_ctx* ctx, const uint16_t* d_depth, const rst_intrin
     t->allocs.emplace_back(pp, ppc);
     t->pix.map = pm;
     t->pix.pts = pp;
+    t->pix.inv = t->inv;
     pm = nullptr;
     pp = nullptr;
     t->pix.fx = K->fx;
