@@ -543,6 +543,36 @@ def main():
                 "note": "AlignIcp3d(src, dst, 128, T) with host clouds, one pair at a time: "
                         "PCIe-inclusive (upload, index build, ICP, readback)"}
 
+    # ---- the reference callers' own workload (extra fields) ----------------------
+    # rs_replay_app.cpp:229,246-251 per frame: RemoveNans(cloud_raw) ->
+    # DownsampleVoxel(curr, 0.05) and DownsampleVoxel(prev, 0.05) ->
+    # AlignIcp3d(curr_down, prev_down, 128, &xfm) (the 4-argument overload:
+    # the target's index built per call), host clouds, one pair at a time
+    callers = None
+    if not a.no_host_api and not pyr:
+        raw = [driver.unproject(frames[pingpong(k, nfr)], K, keep_invalid=True) for k in range(5)]
+        callers = {}
+        for name, sm in (("ref_sums", L.RST_SUM_REF), ("fp64_sums", L.RST_SUM_FP64)):
+            o = L.default_opts(sum_mode=sm)
+
+            def pair(k):
+                cur = A.DownsampleVoxel(A.RemoveNans(raw[k]), 0.05)
+                prv = A.DownsampleVoxel(A.RemoveNans(raw[k - 1]), 0.05)
+                T = np.eye(4, dtype=np.float32)
+                A.AlignIcp3d(cur, prv, a.iters, T, opts=o)
+                return len(cur)
+
+            pair(1)  # warm the context's pools
+            t5 = time.perf_counter()
+            npts = [pair(k) for k in range(2, 5)]
+            dtc = (time.perf_counter() - t5) / 3
+            callers[name] = {"ms_per_pair": 1000.0 * dtc, "pairs_per_s": 1.0 / dtc,
+                             "iterations_per_s": a.iters / dtc,
+                             "points_per_cloud": int(np.mean(npts))}
+        callers["note"] = ("rs_replay_app.cpp:229,246-251 per frame: RemoveNans, DownsampleVoxel "
+                           "0.05 of both clouds, AlignIcp3d(curr_down, prev_down, 128) with its "
+                           "index built per call; host clouds (PCIe-inclusive), one pair at a time")
+
     # ---- the tracker's GICP loop (rs_tracker.cpp:79-87; extra fields) ------------
     # per frame: DownsampleVoxel(curr, 0.1); ComputeAlignment(prev, curr, &T)
     # (16 rounds of exact NN + LM), host clouds, one pair at a time
@@ -640,6 +670,8 @@ def main():
         out["fp64_sums" if main_ref else "ref_sums"] = refs
     if host is not None:
         out["host_api"] = host
+    if callers is not None:
+        out["callers_workload"] = callers
     if gicp is not None:
         out["gicp"] = gicp
     if cpu is not None:

@@ -652,9 +652,9 @@ int rst_debug_seq_sum(rst_ctx* ctx, const float* xyzw, int64_t n, int serial, in
   if (s >= 0 && (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess)) s = RST_E_HIP;
   if (s >= 0 && hipEventRecord(e0, ctx->stream) != hipSuccess) s = RST_E_HIP;
   for (int r = 0; r < reps && s >= 0; ++r)
-    s = serial ? seq_sum4_device(ctx, (const float4*)d, n, dout)
-               : seqsum_enqueue((const float4*)d, n, 4, ws, dout, ctx->stream,
-                                stats ? dstats : nullptr);
+    s = serial == 1 ? seq_sum4_device(ctx, (const float4*)d, n, dout)
+                    : seqsum_enqueue((const float4*)d, n, 4, ws, dout, ctx->stream,
+                                     stats ? dstats : nullptr);
   if (s >= 0 && hipEventRecord(e1, ctx->stream) != hipSuccess) s = RST_E_HIP;
   if (s >= 0 && (hipMemcpyAsync(out, dout, sizeof(float) * 4, hipMemcpyDeviceToHost, ctx->stream) !=
                      hipSuccess ||
@@ -665,7 +665,7 @@ int rst_debug_seq_sum(rst_ctx* ctx, const float* xyzw, int64_t n, int serial, in
     if (hipEventElapsedTime(&t, e0, e1) != hipSuccess) s = RST_E_HIP;
     *ms = t / (float)reps;
   }
-  if (s >= 0 && stats && !serial &&
+  if (s >= 0 && stats && serial != 1 &&
       hipMemcpy(stats, dstats, sizeof(int) * 64, hipMemcpyDeviceToHost) != hipSuccess)
     s = RST_E_HIP;
   hipStreamSynchronize(ctx->stream);

@@ -36,6 +36,14 @@ def cases():
     nf[9000, 2] = -np.inf
     nf[150000, 3] = np.inf
     out["nonfinite"] = nf
+    # the reference callers' sizes (5 cm voxel clouds, ~15k points)
+    for name in ("ties", "zero_crossings", "alternating", "huge", "subnormal"):
+        out[f"{name}_small"] = out[name][:15239].copy()
+    nfs = out["nonfinite"][:16384].copy()
+    nfs[12000, 3] = np.nan
+    out["nonfinite_small"] = nfs
+    for n in (16384, 16385):
+        out[f"mixed_{n}"] = (rng.normal(size=(n, 4)) * 10 ** rng.uniform(-3, 2, size=(n, 4))).astype(np.float32)
     out["zeros"] = np.zeros((5000, 4), np.float32)
     neg0 = np.full((100, 4), -0.0, np.float32)
     out["neg_zeros"] = neg0

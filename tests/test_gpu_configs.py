@@ -155,3 +155,39 @@ def test_pyramid_720p_graphs(ctx, sum_mode):
     print(f"1280x720 pyramid (graphs, sum_mode {sum_mode}) vs oracle chain: {e}")
     assert ok == r.ok
     assert max(e) <= 1e-6, e  # gates 1e-4 / 2e-5 by contract; measured 0 (r03e)
+
+
+def test_callers_workload_ref_inloop(ctx):
+    """The reference callers' own sizes (rs_replay_app.cpp:229,246-251:
+    RemoveNans, DownsampleVoxel 0.05 of both clouds, the 4-argument
+    AlignIcp3d 128): ~15k points, where the sequential sums take the
+    one-workgroup path -- every iteration's sums bit-exact again."""
+    K = driver.intrinsics(640, 480)
+    da, db, _ = driver.make_pair(driver.SyntheticScene(0), K, seed=10)
+    # the recorded clouds keep every pixel, invalid ones at the origin
+    # (data_source_rs.cpp:89-90 writes 0 for NaN); a few NaNs as well
+    raw = [driver.unproject(d, K, keep_invalid=True) for d in (da, db)]
+    for r in raw:
+        r[::997] = np.nan
+    cur = A.DownsampleVoxel(A.RemoveNans(raw[1]), 0.05)
+    prv = A.DownsampleVoxel(A.RemoveNans(raw[0]), 0.05)
+    ocur = O.downsample_voxel(O.remove_nans(raw[1]), 0.05)
+    oprv = O.downsample_voxel(O.remove_nans(raw[0]), 0.05)
+    assert np.array_equal(cur, ocur) and np.array_equal(prv, oprv)
+    assert 5_000 < len(cur) <= 16384
+    hctx = A.get_context()
+    _enable_seq_trace(hctx, True)
+    try:
+        T = np.eye(4, dtype=np.float32)
+        assert A.AlignIcp3d(cur, prv, 128, T)
+        tr = _seq_trace(hctx, 128)
+    finally:
+        _enable_seq_trace(hctx, False)
+    ok, To, mco, otr = O.align_icp(cur, prv, 128, trace=True, sum_mode=0)
+    assert ok
+    dmean = (tr[:, :3] / np.float32(len(cur))).astype(np.float32)
+    assert np.array_equal(dmean.view(np.uint32), otr["dmean"].view(np.uint32))
+    assert np.array_equal(tr[:, 3].view(np.uint32), otr["cost"].view(np.uint32))
+    e = pose_err(T, To)
+    print(f"callers' workload ({len(cur)} points): 128/128 iterations bit-exact, pose {e}")
+    assert max(e) <= 1e-6, e
