@@ -458,11 +458,12 @@ def main():
     # ---- roofline: one pair in flight, events around every iteration's kernels --
     # (with two pairs in flight an event span also counts the CUs the other
     # pair holds; alone, the spans agree with rocprof's kernel durations)
+    # (under --graphs the timing pass runs its one context in stream mode:
+    # events cannot sit inside a replayed graph)
     sr1 = new_stats()
-    if not a.graphs:
-        timing(1, actx[:1])
-        run(a.roof_steps, opts_main, 0, sr1, ctxs=actx[:1])
-        timing(0, actx[:1])
+    actx[0].enable_kernel_timing(1)  # (a timed align runs in stream mode)
+    run(a.roof_steps, opts_main, 0, sr1, ctxs=actx[:1])
+    actx[0].enable_kernel_timing(0)
 
     # ---- point-to-plane mode (extra fields) ---------------------------------------
     def p2plane_leg(normals_k: int) -> dict:

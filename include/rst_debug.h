@@ -88,8 +88,9 @@ int rst_debug_launch_rate(rst_ctx* ctx, int nstreams, int launches, int blocks, 
                           double* per_s);
 
 /* A device stream copy (the measured HBM ceiling the rooflines are read
- * against): `bytes` copied buffer to buffer by a float4 grid-stride kernel,
- * reps launches timed with HIP events; *gbps = (read + write bytes) / the
+ * against): `bytes` copied buffer to buffer by float4 kernels (1-8 float4
+ * per thread in flight, nontemporal or default policy), reps launches of
+ * each variant timed with HIP events; *gbps = (read + write bytes) / the
  * best launch's time. */
 int rst_debug_stream_copy(rst_ctx* ctx, int64_t bytes, int reps, double* gbps);
 

@@ -21,18 +21,19 @@
 #define ORC_F 33
 #define ORC_PI 3.14159265358979323846 /* M_PI */
 
-/* ComputePfh (fpfh.cpp:20-64), kSymmetricPfh */
+/* ComputePfh (fpfh.cpp:20-64), kSymmetricPfh; Vector3f dot / norm in Eigen's
+ * unrolled redux order x0 + (x1 + x2), as mv_row (rst_oracle.c) */
 static int orc_pfh(const float* p1, const float* n1, const float* p2, const float* n2,
                    float f[3]) {
   float dx = p2[0] - p1[0], dy = p2[1] - p1[1], dz = p2[2] - p1[2];
-  const float distance = sqrtf((dx * dx + dy * dy) + dz * dz);
+  const float distance = sqrtf(dx * dx + (dy * dy + dz * dz));
   if (distance == 0.0f) return 0;
   const float id = 1.0f / distance;
   dx = dx * id;
   dy = dy * id;
   dz = dz * id;
-  const float n1_d = (n1[0] * dx + n1[1] * dy) + n1[2] * dz;
-  const float n2_d = (n2[0] * dx + n2[1] * dy) + n2[2] * dz;
+  const float n1_d = n1[0] * dx + (n1[1] * dy + n1[2] * dz);
+  const float n2_d = n2[0] * dx + (n2[1] * dy + n2[2] * dz);
   float u_d, nt_d;
   if (fabsf(n1_d) < fabsf(n2_d)) {
     u_d = -n2_d;
@@ -43,12 +44,12 @@ static int orc_pfh(const float* p1, const float* n1, const float* p2, const floa
   }
   if (fabsf(u_d) >= 1.0f) return 0;
   const float v_norm = sqrtf(1.0f - u_d * u_d);
-  const float n1n2 = (n1[0] * n2[0] + n1[1] * n2[1]) + n1[2] * n2[2];
+  const float n1n2 = n1[0] * n2[0] + (n1[1] * n2[1] + n1[2] * n2[2]);
   f[0] = atan2f(nt_d - n1n2 * u_d, n1n2 * v_norm);
   const float cx = n1[1] * n2[2] - n1[2] * n2[1];
   const float cy = n1[2] * n2[0] - n1[0] * n2[2];
   const float cz = n1[0] * n2[1] - n1[1] * n2[0];
-  f[1] = ((dx * cx + dy * cy) + dz * cz) / v_norm;
+  f[1] = (dx * cx + (dy * cy + dz * cz)) / v_norm;
   f[2] = u_d;
   return 1;
 }

@@ -168,16 +168,34 @@ static int upload_xyz(rst_ctx* ctx, const float* h, int64_t n, float** d_out) {
   return RST_OK;
 }
 
-// the measured HBM ceiling (rst_debug_stream_copy): a grid-stride float4 copy,
-// nontemporal (streaming) loads and stores
+// the measured HBM ceiling (rst_debug_stream_copy): a float4 copy, U float4
+// per thread in flight (all loads before the stores), nontemporal or default
+// cache policy; the best of the variants is the ceiling
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+template <int U, bool NT>
 __global__ __launch_bounds__(256) void k_stream_copy(const float4* __restrict__ a,
                                                      float4* __restrict__ b, int64_t n4) {
   const f32x4* __restrict__ av = reinterpret_cast<const f32x4*>(a);
   f32x4* __restrict__ bv = reinterpret_cast<f32x4*>(b);
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride)
-    __builtin_nontemporal_store(__builtin_nontemporal_load(av + i), bv + i);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x * U;
+  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x * U + threadIdx.x; i0 < n4; i0 += stride) {
+    f32x4 t[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + (int64_t)u * blockDim.x;
+      if (i < n4) t[u] = NT ? __builtin_nontemporal_load(av + i) : av[i];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + (int64_t)u * blockDim.x;
+      if (i < n4) {
+        if (NT)
+          __builtin_nontemporal_store(t[u], bv + i);
+        else
+          bv[i] = t[u];
+      }
+    }
+  }
 }
 
 // the dispatch-rate probe (rst_debug_launch_rate): a kernel that does
@@ -582,9 +600,16 @@ int rst_debug_stream_copy(rst_ctx* ctx, int64_t bytes, int reps, double* gbps) {
       hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess)
     s = RST_E_HIP;
   float best = 0.f;
-  for (int r = 0; r < reps && s >= 0; ++r) {
+  for (int r = 0; r < reps * 6 && s >= 0; ++r) {
     if (hipEventRecord(e0, ctx->stream) != hipSuccess) s = RST_E_HIP;
-    k_stream_copy<<<8192, 256, 0, ctx->stream>>>(a, b, n4);
+    switch (r % 6) {  // (variants interleaved: each gets reps launches)
+      case 0: k_stream_copy<1, true><<<8192, 256, 0, ctx->stream>>>(a, b, n4); break;
+      case 1: k_stream_copy<4, true><<<2048, 256, 0, ctx->stream>>>(a, b, n4); break;
+      case 2: k_stream_copy<4, false><<<2048, 256, 0, ctx->stream>>>(a, b, n4); break;
+      case 3: k_stream_copy<8, true><<<1024, 256, 0, ctx->stream>>>(a, b, n4); break;
+      case 4: k_stream_copy<4, true><<<4096, 256, 0, ctx->stream>>>(a, b, n4); break;
+      default: k_stream_copy<2, false><<<8192, 256, 0, ctx->stream>>>(a, b, n4); break;
+    }
     if (s >= 0 && (hipGetLastError() != hipSuccess || hipEventRecord(e1, ctx->stream) != hipSuccess ||
                    hipEventSynchronize(e1) != hipSuccess))
       s = RST_E_HIP;

@@ -33,20 +33,22 @@ constexpr int kBS = 128;
 constexpr int kBins = 11;
 constexpr int kF = 3 * kBins;
 
-// ComputePfh (fpfh.cpp:20-64), kSymmetricPfh: false (f zeroed) when the
+// ComputePfh (fpfh.cpp:20-64), kSymmetricPfh.  Vector3f dot / norm in
+// Eigen's unrolled redux order, x0 + (x1 + x2) (redux_novec_unroller splits a
+// length-3 sum 1 + 2; the same order as the oracle's mv_row).  False (f zeroed) when the
 // points coincide or |u . d| >= 1
 __device__ __forceinline__ bool pfh(float p1x, float p1y, float p1z, float n1x, float n1y,
                                     float n1z, float p2x, float p2y, float p2z, float n2x,
                                     float n2y, float n2z, float& f0, float& f1, float& f2) {
   float dx = p2x - p1x, dy = p2y - p1y, dz = p2z - p1z;
-  const float distance = sqrtf((dx * dx + dy * dy) + dz * dz);
+  const float distance = sqrtf(dx * dx + (dy * dy + dz * dz));
   if (distance == 0.0f) return false;
   const float id = 1.0f / distance;
   dx = dx * id;
   dy = dy * id;
   dz = dz * id;
-  const float n1_d = (n1x * dx + n1y * dy) + n1z * dz;
-  const float n2_d = (n2x * dx + n2y * dy) + n2z * dz;
+  const float n1_d = n1x * dx + (n1y * dy + n1z * dz);
+  const float n2_d = n2x * dx + (n2y * dy + n2z * dz);
   float u_d, nt_d;
   if (fabsf(n1_d) < fabsf(n2_d)) {
     u_d = -n2_d;
@@ -57,10 +59,10 @@ __device__ __forceinline__ bool pfh(float p1x, float p1y, float p1z, float n1x, 
   }
   if (fabsf(u_d) >= 1.0f) return false;
   const float v_norm = sqrtf(1.0f - u_d * u_d);
-  const float n1n2 = (n1x * n2x + n1y * n2y) + n1z * n2z;
+  const float n1n2 = n1x * n2x + (n1y * n2y + n1z * n2z);
   f0 = atan2f(nt_d - n1n2 * u_d, n1n2 * v_norm);
   const float cx = n1y * n2z - n1z * n2y, cy = n1z * n2x - n1x * n2z, cz = n1x * n2y - n1y * n2x;
-  f1 = ((dx * cx + dy * cy) + dz * cz) / v_norm;
+  f1 = (dx * cx + (dy * cy + dz * cz)) / v_norm;
   f2 = u_d;
   return true;
 }
