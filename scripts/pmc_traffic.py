@@ -1,24 +1,26 @@
-"""HBM traffic per ICP iteration of the NN pass -- k_icp_nn<P2PointAcc> and
-k_icp_fb<P2PointAcc>, per launch each and summed -- from two rocprofv3 --pmc
+"""HBM traffic per ICP iteration of the NN pass -- k_icp_nn<Acc> and
+k_icp_fb<Acc> (Acc = RefAcc, the bench value's mode, or P2PointAcc: the
+optional 4th argument), per launch each and summed -- from two rocprofv3 --pmc
 passes (FETCH_SIZE, WRITE_SIZE; counter_collection.csv each), corrected as
 /opt/skills/guides/MI355X_MICROARCH.md "HBM" prescribes: FETCH_SIZE (KiB) x 2
 on gfx950, WRITE_SIZE (KiB) as is.  Writes the JSON bench.py reads, stamped
 with the library's source hash (lib/BUILD_INFO.json): bench.py reports the
 traffic only while it matches the library it runs.
 
-  python scripts/pmc_traffic.py OUT.json FETCH.csv WRITE.csv"""
+  python scripts/pmc_traffic.py OUT.json FETCH.csv WRITE.csv [RefAcc|P2PointAcc]"""
 import csv
 import json
 import sys
 
 KERNELS = ("k_icp_nn<", "k_icp_fb<")
+ACC = sys.argv[4] if len(sys.argv) > 4 else "RefAcc"
 
 
 def per_dispatch(path, counter, kernel):
     vals = {}
     for r in csv.DictReader(open(path)):
         name = r["Kernel_Name"]
-        if r["Counter_Name"] != counter or kernel not in name or "P2PointAcc" not in name:
+        if r["Counter_Name"] != counter or kernel not in name or ACC not in name:
             continue
         # one row per (dispatch, counter); sum any per-dimension rows
         key = r.get("Dispatch_Id") or r.get("Correlation_Id") or len(vals)
@@ -30,13 +32,13 @@ def per_dispatch(path, counter, kernel):
 def main():
     out, fpath, wpath = sys.argv[1:4]
     d = {"kernels": {}, "note": "FETCH_SIZE x2 (gfx950), WRITE_SIZE as is; rocprofv3 --pmc, "
-                                "separate passes; per launch, P2PointAcc instances"}
+                                "separate passes; per launch, " + ACC + " instances"}
     tot = 0.0
     for k in KERNELS:
         f = per_dispatch(fpath, "FETCH_SIZE", k)
         w = per_dispatch(wpath, "WRITE_SIZE", k)
         if not f or not w:
-            raise SystemExit(f"no {k}P2PointAcc> rows")
+            raise SystemExit(f"no {k}{ACC}> rows")
         fm = sum(f) / len(f) * 1024.0 * 2.0  # KiB -> B, gfx950 half-count correction
         wm = sum(w) / len(w) * 1024.0
         d["kernels"][k.rstrip("<")] = {"dispatches": [len(f), len(w)],
