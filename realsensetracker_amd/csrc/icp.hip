@@ -446,11 +446,10 @@ __global__ __launch_bounds__(kBS) void k_gather_orig(const float4* __restrict__ 
 // order only moves the last bits of a double).  dbar = seq / float(n)
 // (:122); w_i = (mu / (d2_i + mu))^2 (:116-117).  Grid-stride over the
 // original order; one 9-double row (stride RefAcc::RS) per block.
-// (few, busy workgroups: the reference-rounding loop is bound by the
-// workgroup dispatch rate with many frame pairs in flight, ~45-50M WGs/s
-// measured over every kernel mix (r03j); 1024 -> RST_COV_BLOCKS)
+// (r03: 128 blocks measured no faster with pairs in flight and 1.6 us
+// slower alone)
 #ifndef RST_COV_BLOCKS
-#define RST_COV_BLOCKS 128
+#define RST_COV_BLOCKS 1024
 #endif
 constexpr int kCovBlocks = RST_COV_BLOCKS;
 __global__ __launch_bounds__(kBS) void k_cov_ref(const float4* __restrict__ srco,

@@ -147,62 +147,49 @@ __device__ __forceinline__ int quad_or(int a) {
   return a;
 }
 
-// (one workgroup per tile, its four quarter tiles in turn: a quarter per
-// workgroup spent the workgroup dispatch rate the loop is bound by)
 __global__ __launch_bounds__(kFrontT) void k_sq_tot(const float4* __restrict__ x, SqView v) {
-  __shared__ double red[kTotQ][kFrontT / kWave][4];
-  const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid / kWave;
-  float4 q[kTotQ][4];  // every load of the tile in flight first
+  __shared__ double red[kFrontT / kWave][4];
+  const int qt = blockIdx.x, tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid / kWave;
+  const int64_t i0 = (int64_t)qt * kTotE + 4 * tid;
+  float4 q[4];
 #pragma unroll
-  for (int k = 0; k < kTotQ; ++k) {
-    const int64_t i0 = ((int64_t)blockIdx.x * kTotQ + k) * kTotE + 4 * tid;
+  for (int j = 0; j < 4; ++j) q[j] = i0 + j < v.n ? x[i0 + j] : make_float4(0.f, 0.f, 0.f, 0.f);
+  double part[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) q[k][j] = i0 + j < v.n ? x[i0 + j] : make_float4(0.f, 0.f, 0.f, 0.f);
-  }
+  for (int c = 0; c < 4; ++c) {
+    float e[4];
+    int f = 0;
+    double ps = 0.0;
 #pragma unroll
-  for (int k = 0; k < kTotQ; ++k) {
-    const int qt = blockIdx.x * kTotQ + k;
-    const int64_t i0 = (int64_t)qt * kTotE + 4 * tid;
-    double part[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      float e[4];
-      int f = 0;
-      double ps = 0.0;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        e[j] = comp(q[k][j], c);
-        const int fj = nf_flags(e[j]);
-        f |= fj;
-        ps += fj ? 0.0 : (double)e[j];
-      }
-      part[c] = ps;
-      if (c < v.nch) {
-        float* dst = v.soa + (int64_t)c * v.ns;
-        // (ns is a multiple of 64 and i0 of 4: the float4 is in the row)
-        if (i0 < v.n) *reinterpret_cast<float4*>(dst + i0) = make_float4(e[0], e[1], e[2], e[3]);
-        f = quad_or(f);
-        const int64_t w = i0 / kW;
-        if ((tid & 3) == 0 && w < v.nb) v.wflg[(int64_t)c * v.nb + w] = (uint8_t)f;
-      }
+    for (int j = 0; j < 4; ++j) {
+      e[j] = comp(q[j], c);
+      const int fj = nf_flags(e[j]);
+      f |= fj;
+      ps += fj ? 0.0 : (double)e[j];
     }
-#pragma unroll
-    for (int o = kWave / 2; o > 0; o >>= 1)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) part[c] += __shfl_xor(part[c], o, kWave);
-    if (lane == 0)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) red[k][wv][c] = part[c];
-  }
-  __syncthreads();
-  if (tid < kTotQ * 4) {
-    const int k = tid / 4, c = tid % 4;
+    part[c] = ps;
     if (c < v.nch) {
-      double t = 0.0;
-#pragma unroll
-      for (int w = 0; w < kFrontT / kWave; ++w) t += red[k][w][c];
-      v.ttot[(int64_t)c * v.nk * kTotQ + blockIdx.x * kTotQ + k] = t;
+      float* dst = v.soa + (int64_t)c * v.ns;
+      // (ns is a multiple of 64 and i0 of 4: the float4 is in the row)
+      if (i0 < v.n) *reinterpret_cast<float4*>(dst + i0) = make_float4(e[0], e[1], e[2], e[3]);
+      f = quad_or(f);
+      const int64_t w = i0 / kW;
+      if ((tid & 3) == 0 && w < v.nb) v.wflg[(int64_t)c * v.nb + w] = (uint8_t)f;
     }
+  }
+#pragma unroll
+  for (int o = kWave / 2; o > 0; o >>= 1)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) part[c] += __shfl_xor(part[c], o, kWave);
+  if (lane == 0)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) red[wv][c] = part[c];
+  __syncthreads();
+  if (tid < v.nch) {
+    double t = 0.0;
+#pragma unroll
+    for (int w = 0; w < kFrontT / kWave; ++w) t += red[w][tid];
+    v.ttot[(int64_t)tid * v.nk * kTotQ + qt] = t;
   }
 }
 
@@ -351,12 +338,11 @@ __global__ __launch_bounds__(kFrontT) void k_sq_front(SqView v) {
 }
 
 // ---- 3: leaf, group and superblock maps ------------------------------------------
-// threads per map workgroup: the leaf lanes take 2 * kMapT / 2 ... blocks in
-// rounds (the leaf phase is VALU-bound: fewer, busier waves take as long and
-// leave the CU's other wave slots to other kernels); a group's 16 residue
-// lanes need 31 * 16 <= kMapT
+// threads per map workgroup: the leaf lanes take kMapT / 2 blocks per
+// round; a group's 16 residue lanes need 31 * 16 <= kMapT (r03: 512 threads
+// and two leaf rounds, same throughput with pairs in flight, 8 us slower alone)
 #ifndef RST_SQ_MAP_T
-#define RST_SQ_MAP_T 512
+#define RST_SQ_MAP_T 1024
 #endif
 constexpr int kMapT = RST_SQ_MAP_T;
 static_assert(kMapT >= kMaxSbGroups * kGroupR && kMapT % kWave == 0, "map workgroup size");
@@ -1061,7 +1047,7 @@ int seqsum_enqueue(const float4* d_x, int64_t n, int nch, void* ws, float* d_out
   stages &= ~RST_SQ_ABLATE;
 #endif
   if (stages & 1) {
-    k_sq_tot<<<v.nk, kFrontT, 0, st>>>(d_x, v);
+    k_sq_tot<<<v.nk * kTotQ, kFrontT, 0, st>>>(d_x, v);
     k_sq_front<<<dim3(v.nk, nch), kFrontT, 0, st>>>(v);
   }
   if (stages & 2) k_sq_maps<<<dim3(v.nk, nch), kMapT, 0, st>>>(v);
