@@ -72,6 +72,15 @@ constexpr int kCertBit = 1 << 30;
 #define RST_PIX_CHUNK 512  // pixels staged per wave and round (10 KB of LDS per wave; r02: 512 vs 256 same throughput, one pair 13.4 vs 13.9 ms)
 #endif
 constexpr int kPixChunk = RST_PIX_CHUNK;
+#ifndef RST_PIX_COLD_ITERS
+#define RST_PIX_COLD_ITERS 3  // iterations [1, RST_PIX_COLD_ITERS) take the cold windows below
+#endif
+#ifndef RST_PIX_COLD_HALF
+#define RST_PIX_COLD_HALF 16.0f  // their half-width cap (level pixels)
+#endif
+#ifndef RST_PIX_COLD_CHUNKS
+#define RST_PIX_COLD_CHUNKS 6  // their staging rounds per wave
+#endif
 #ifndef RST_DIAG
 #define RST_DIAG 0  // 1: per-iteration certificate counters (rst_debug_queue_trace)
 #endif
@@ -659,7 +668,18 @@ __global__ __launch_bounds__(kBS) void k_icp_nn(BvhView bv, AdjView av, PixView 
     const float sp = (float)pv.s * pz / fminf(fabsf(pv.fx), fabsf(pv.fy));
     const bool reseed = need && wb >= 0 && !(d0 <= 9.f * sp * sp);
     if (__ballot(reseed) != 0 && reseed) d0 = fminf(d0, pix_seed_d2(pv, px, py, pz));
-    if (pix_tile_search<kPixChunk, 2>(bv, pv, need, px, py, pz, d0, pr, pq, pscr[wid], prc)) {
+    // a pair's second and third iterations: larger windows over more
+    // staging rounds (the pose still moves by centimetres, beyond the steady
+    // state's cap, which would queue them for k_icp_fb's per-lane searches).
+    // Not the first: its seeds are the projective / Morton guesses, and
+    // k_icp_fb's ball tiles answer that whole queue faster (r03u: 1.06 vs
+    // 1.97 ms; iterations 1-2 0.65 -> 0.23-0.38 ms)
+    const bool cold = st->iter >= 1 && st->iter < RST_PIX_COLD_ITERS;
+    const bool pok =
+        cold ? pix_tile_search<kPixChunk, RST_PIX_COLD_CHUNKS>(bv, pv, need, px, py, pz, d0, pr, pq,
+                                                               pscr[wid], prc, RST_PIX_COLD_HALF)
+             : pix_tile_search<kPixChunk, 2>(bv, pv, need, px, py, pz, d0, pr, pq, pscr[wid], prc);
+    if (pok) {
       const float g = cert_bound(pr, prc);
       const int pos = pr.pos[0];
       nnq[i] = make_float4(pq.x, pq.y, pq.z, i2f(pos | (g > 0.f ? kCertBit : 0)));
@@ -713,23 +733,44 @@ __global__ __launch_bounds__(kBS) void k_icp_nn(BvhView bv, AdjView av, PixView 
 
 // Kabsch solve (align_icp.cpp:139-151; SolveKabsch :58-69): fp64 SVD,
 // R = float(U V^T), reflection fix, t = dmean - R smean, quaternion trip.
-__device__ void kabsch_solve(const double* cov, const float* smean, const float* dmean,
-                             float* Rq, float* t) {
+// (A warm start from the previous iteration's polar factor -- the polar
+// factor of Qp^T cov, near I -- took as many Newton steps: the scaled
+// iteration's step count follows the singular values' spread, r03w.)
+// (the rare Jacobi SVD fallback out of line, its 3x3s by value: inlined,
+// or called with array pointers, it would keep the solve's arrays in memory
+// -- one thread's whole solve then waits on LDS / scratch round trips)
+struct M3d {
+  double a[9];
+};
+struct M3f {
+  float a[9];
+};
+__device__ __noinline__ M3f kabsch_svd_r(M3d cov) {
+  double U[9], S[3], V[9];
+  svd3_jacobi(cov.a, U, S, V);
+  M3f R;
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < 3; ++c) {
+      const double a0 = RST_M3(U, r, 0) * RST_M3(V, c, 0);
+      const double a1 = RST_M3(U, r, 1) * RST_M3(V, c, 1);
+      const double a2 = RST_M3(U, r, 2) * RST_M3(V, c, 2);
+      RST_M3(R.a, r, c) = (float)(a0 + (a1 + a2));
+    }
+  return R;
+}
+
+__device__ __forceinline__ void kabsch_solve(const double* cov, const float* smean,
+                                             const float* dmean, float* Rq, float* t) {
   // R = U V^T: the polar factor (cheap, nonsingular cov), else Jacobi SVD
   double P[9];
   float R[9];
   if (polar3(cov, P)) {
     for (int k = 0; k < 9; ++k) R[k] = (float)P[k];
   } else {
-    double U[9], S[3], V[9];
-    svd3_jacobi(cov, U, S, V);
-    for (int r = 0; r < 3; ++r)
-      for (int c = 0; c < 3; ++c) {
-        const double a0 = RST_M3(U, r, 0) * RST_M3(V, c, 0);
-        const double a1 = RST_M3(U, r, 1) * RST_M3(V, c, 1);
-        const double a2 = RST_M3(U, r, 2) * RST_M3(V, c, 2);
-        RST_M3(R, r, c) = (float)(a0 + (a1 + a2));
-      }
+    M3d cv;
+    for (int k = 0; k < 9; ++k) cv.a[k] = cov[k];
+    const M3f Rs = kabsch_svd_r(cv);
+    for (int k = 0; k < 9; ++k) R[k] = Rs.a[k];
   }
   if (det3f(R) < 0) {  // :143-145 (non-standard fix kept on purpose)
     for (int r = 0; r < 3; ++r) RST_M3(R, r, 2) *= -1.0f;
@@ -806,7 +847,7 @@ __global__ __launch_bounds__(kBS) void k_xyz_f4(const float* __restrict__ xyz, i
 }
 
 // Kabsch on the reduced sums (align_icp.cpp:122, 139-151).
-__device__ void p2point_update(const double* tot, const IcpParams& prm, IcpCore* st) {
+__device__ __forceinline__ void p2point_update(const double* tot, const IcpParams& prm, IcpCore* st) {
   const double n = (double)prm.n;
   float dmean[3];
   for (int r = 0; r < 3; ++r) dmean[r] = (float)(tot[12 + r] / n);
@@ -926,7 +967,7 @@ __device__ void p2plane_update(const double* tot, const IcpParams& prm, IcpCore*
 // RST_SUM_REF: tot = the covariance (row-major sums of k_cov_ref), the means
 // and cost from this iteration's sequential sums (align_icp.cpp:122,
 // 139-151; `dst_mean /= n` divides by float(n)).
-__device__ void p2point_ref_update(const double* tot, const IcpParams& prm, IcpCore* st) {
+__device__ __forceinline__ void p2point_ref_update(const double* tot, const IcpParams& prm, IcpCore* st) {
   const float nf = (float)prm.n;
   float dmean[3];
   for (int r = 0; r < 3; ++r) dmean[r] = st->seq[r] / nf;
@@ -1000,8 +1041,8 @@ __global__ __launch_bounds__(kRedBS) void k_reduce_solve(const double* __restric
   if (totals) {
     if (t < Acc::NV) totals[t] = tot[t];
   } else if (t == 0) {
-    // (loaded here, not before the reduction: held across it, the state
-    // would be spilled to scratch and reloaded anyway)
+    // (loaded here, not before the reduction: staged through LDS during it,
+    // r03w, the solve took as long)
     IcpCore core = *static_cast<const IcpCore*>(st);
     const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
     const int it = core.iter;

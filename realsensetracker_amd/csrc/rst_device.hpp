@@ -364,7 +364,7 @@ __device__ inline void svd3_jacobi(const double* a_in, double* U, double* S,
 #endif
 constexpr int kPolarScaled = 6;                 // scaled Newton steps (then g = 1)
 constexpr int kPolarMinIt = RST_POLAR_MIN_IT;   // earliest converged exit
-__device__ inline bool polar3(const double* a, double* Q) {
+__device__ __forceinline__ bool polar3(const double* a, double* Q) {
   double X[9];
   double nx = 0.0;
 #pragma unroll
@@ -435,7 +435,7 @@ __device__ __forceinline__ float det3f(const float* m) {
 
 // Quaternionf(R) then toRotationMatrix() (align_icp.cpp:151; Eigen
 // quaternionbase_assign_impl<3x3> / toRotationMatrix op order).
-__device__ inline void quat_roundtrip(const float* R, float* Rq) {
+__device__ __forceinline__ void quat_roundtrip(const float* R, float* Rq) {
   float q[4];  // x y z w
   const float tr = (RST_M3(R, 0, 0) + RST_M3(R, 1, 1)) + RST_M3(R, 2, 2);
   if (tr > 0.0f) {

@@ -1391,12 +1391,13 @@ __device__ __forceinline__ int row_max_i(int x) {
 template <int N, int MaxChunks>
 __device__ __forceinline__ bool pix_tile_search(const BvhView& bv, const PixView& pv, bool act,
                                                 float qx, float qy, float qz, float d0, Best2& r,
-                                                float4& q0, PixScratch<N>& ts, float& rc) {
+                                                float4& q0, PixScratch<N>& ts, float& rc,
+                                                float maxh = RST_PIX_MAX_HALF) {
   constexpr int kPer = N / kWave;
   const int lane = __lane_id();
   int a0 = 0, a1 = -1, b0 = 0, b1 = -1;
   rc = 0.f;
-  const bool ok = act && pix_window(pv, qx, qy, qz, d0, RST_PIX_MAX_HALF, a0, a1, b0, b1, rc);
+  const bool ok = act && pix_window(pv, qx, qy, qz, d0, maxh, a0, a1, b0, b1, rc);
   if (__ballot(ok) == 0) return false;
   // the row boxes, then the wave box
   int gA0 = row_min_i(ok ? a0 : INT_MAX), gA1 = row_max_i(ok ? a1 : INT_MIN);
@@ -1473,8 +1474,13 @@ __device__ __forceinline__ bool pix_tile_search(const BvhView& bv, const PixView
     if (ok) {
       // four pixels' LDS reads in flight at a time (a dependent read per
       // pixel would leave the scan bound by LDS latency); an invalid pixel
-      // is NaN, so its distance fails every test
-      for (int b = b0; b <= b1; ++b) {
+      // is NaN, so its distance fails every test.  Only the window's rows
+      // that meet this chunk: the staged index of (a, b) is
+      // moff + (b - my) mw + (a - mx)
+      const int lo = c0 - moff + mx - a1, hi = c0 + cnt - 1 - moff + mx - a0;
+      const int rb0 = max(b0, my + (lo <= 0 ? -((-lo) / mw) : (lo + mw - 1) / mw));
+      const int rb1 = min(b1, my + (hi >= 0 ? hi / mw : -((-hi + mw - 1) / mw)));
+      for (int b = rb0; b <= rb1; ++b) {
         const int row = moff + (b - my) * mw - mx - c0;
         for (int a = a0; a <= a1; a += 4) {
           float4 t[4];
