@@ -51,6 +51,18 @@ constexpr int kMaxSbBlocks = 2 * kBlocksPerTile - 1;  // a superblock spans <= 5
 constexpr int kMaxSbElems = kMaxSbBlocks * kW + kW;   // ... and < 8208 elements
 constexpr int kMaxSbGroups = 2 * kKW - 1;             // ... and <= 31 groups
 
+// the positions of a 16-wide window a block / group / superblock may start
+// at (the largest |prefix| among them): the middle of the window, so sizes
+// stay within ~1.5x of the mean (r03: the map kernel follows its largest
+// superblock and group; 0..15, any position, measured slower)
+#ifndef RST_SQ_JLO
+#define RST_SQ_JLO 4
+#endif
+#ifndef RST_SQ_JHI
+#define RST_SQ_JHI 11
+#endif
+constexpr int kJLo = RST_SQ_JLO, kJHi = RST_SQ_JHI;
+
 constexpr int kLeafM = 2, kLeafR = 1 << kLeafM;     // residues of a block map
 constexpr int kGroupM = 4, kGroupR = 1 << kGroupM;  // of a group map
 constexpr int kSbM = 6, kSbR = 1 << kSbM;           // of a superblock map
@@ -234,8 +246,10 @@ RST_SQ_HD int hi_units(double hi, int e0) {
 // double arithmetic.  False when v is not on the grid, non-finite, or
 // implausibly far from G.
 // (the exact double path: v in another binade than G)
-#if defined(__HIPCC__)
+#if defined(__HIPCC__) && !defined(RST_SQ_SLOW_INLINE)
 __host__ __device__ __noinline__
+#elif defined(__HIPCC__)
+__host__ __device__ __forceinline__
 #else
 inline
 #endif

@@ -136,6 +136,7 @@ __device__ double block_sum_global(const double* a, int cnt, double* lds) {
 // component: the threads' 4-element sums (fixed order), reduced over the
 // block (fixed tree) -- four components in one reduction.
 constexpr int kFrontT = kTile / kW;  // 256
+
 constexpr int kTotE = 1024;          // elements per k_sq_tot workgroup
 constexpr int kTotQ = kTile / kTotE; // 4 per tile
 static_assert(kTotE == 4 * kFrontT, "k_sq_tot: four elements per thread");
@@ -240,19 +241,26 @@ __global__ __launch_bounds__(kFrontT) void k_sq_front(SqView v) {
   }
   double ttotal;
   const double wrel = block_scan_excl<kFrontT>(wsum, lds, &ttotal);
-  // block start: the element of largest |prefix| in the window (the prefix
-  // before the element: the value a block starting there starts from)
+  // block start: the element of largest |prefix| among positions
+  // [kJLo, kJHi] of the window (the prefix before the element: the value a
+  // block starting there starts from); the middle of the window only, so
+  // block, group and superblock sizes stay within ~1.5x of the mean (the
+  // map kernel's time follows its largest superblock and group)
   const double wpre = P + wrel;
   double best = wpre, run = wpre;
-  int bj = 0;
+  int bj = -1;
 #pragma unroll
   for (int j = 0; j < kW; ++j) {
-    if (j > 0 && fabs(run) > fabs(best) && e0 + tid * kW + j < v.n) {
+    if (j >= kJLo && j <= kJHi && (bj < 0 || fabs(run) > fabs(best)) && e0 + tid * kW + j < v.n) {
       best = run;
       bj = j;
     }
     const float e = xs(tid * kW + j);
     if (isfinite(e)) run += (double)e;
+  }
+  if (bj < 0) {  // (a last window shorter than kJLo + 1 elements)
+    best = wpre;
+    bj = 0;
   }
   if (b == 0) {
     best = 0.0;
@@ -263,24 +271,26 @@ __global__ __launch_bounds__(kFrontT) void k_sq_front(SqView v) {
   if (tid == kFrontT - 1) {
     // the next tile's first block start (same rule), for this tile's last block
     double r2 = P + ttotal, b2 = r2;
-    int j2 = 0;
+    int j2 = -1;
     for (int j = 0; j < kW; ++j) {
-      if (j > 0 && fabs(r2) > fabs(b2) && e0 + kTile + j < v.n) {
+      if (j >= kJLo && j <= kJHi && (j2 < 0 || fabs(r2) > fabs(b2)) && e0 + kTile + j < v.n) {
         b2 = r2;
         j2 = j;
       }
       const float e = xs(kTile + j);
       if (isfinite(e)) r2 += (double)e;
     }
-    sbs[kFrontT] = kTile + j2;
+    sbs[kFrontT] = kTile + (j2 < 0 ? 0 : j2);
   }
   __syncthreads();
   int* bsg = v.bs + (int64_t)c * (v.nb + 1);
   if (b < v.nb) bsg[b] = (int)(e0 + sbs[tid]);
   if (b == v.nb - 1) bsg[v.nb] = (int)v.n;
-  // group starts: the block of largest |start value| in each 16-block window
-  // (out-of-range blocks never win)
-  double key = b < v.nb ? fabs(sA[tid]) : -1.0;
+  // group starts: the block of largest |start value| among blocks [kJLo,
+  // kJHi] of each 16-block window (others only when none of those exists;
+  // out-of-range blocks never win)
+  const int wj = tid & (kGW - 1);
+  double key = b < v.nb ? (wj >= kJLo && wj <= kJHi ? fabs(sA[tid]) : -0.5) : -1.0;
   int kid = b < v.nb ? b : INT_MAX;
 #pragma unroll
   for (int o = 8; o > 0; o >>= 1) {
@@ -306,11 +316,13 @@ __global__ __launch_bounds__(kFrontT) void k_sq_front(SqView v) {
   if (tid == 0) {
     double bk = -2.0;
     int bq = 0;
-    for (int i = 0; i < kKW; ++i)
-      if (gkey[i] > bk) {
-        bk = gkey[i];
+    for (int i = 0; i < kKW; ++i) {
+      const double k = i >= kJLo && i <= kJHi ? gkey[i] : (gkey[i] >= 0.0 ? -0.5 : -1.0);
+      if (k > bk) {
+        bk = k;
         bq = gid[i];
       }
+    }
     int* ksg = v.ks + (int64_t)c * (v.nk + 1);
     ksg[t] = t == 0 ? 0 : bq;
     if (t == v.nk - 1) ksg[v.nk] = v.ng;

@@ -82,14 +82,19 @@ void front(Chain& C) {
       const double wpre = P + acc;
       acc += wsum.at(tid);
       double best = wpre, run = wpre;
-      int bj = 0;
+      int bj = -1;
       for (int j = 0; j < kW; ++j) {
-        if (j > 0 && std::fabs(run) > std::fabs(best) && e0 + tid * kW + j < n) {
+        if (j >= kJLo && j <= kJHi && (bj < 0 || std::fabs(run) > std::fabs(best)) &&
+            e0 + tid * kW + j < n) {
           best = run;
           bj = j;
         }
         const float e = xs.at(tid * kW + j);
         if (std::isfinite(e)) run += (double)e;
+      }
+      if (bj < 0) {
+        best = wpre;
+        bj = 0;
       }
       if (b == 0) {
         best = 0.0;
@@ -100,16 +105,17 @@ void front(Chain& C) {
     }
     {
       double r2 = P + ttotal, b2 = r2;
-      int j2 = 0;
+      int j2 = -1;
       for (int j = 0; j < kW; ++j) {
-        if (j > 0 && std::fabs(r2) > std::fabs(b2) && e0 + kTile + j < n) {
+        if (j >= kJLo && j <= kJHi && (j2 < 0 || std::fabs(r2) > std::fabs(b2)) &&
+            e0 + kTile + j < n) {
           b2 = r2;
           j2 = j;
         }
         const float e = xs.at(kTile + j);
         if (std::isfinite(e)) r2 += (double)e;
       }
-      sbs.at(kBlocksPerTile) = kTile + j2;
+      sbs.at(kBlocksPerTile) = kTile + (j2 < 0 ? 0 : j2);
     }
     for (int tid = 0; tid < kBlocksPerTile; ++tid) {
       const int b = t * kBlocksPerTile + tid;
@@ -125,7 +131,7 @@ void front(Chain& C) {
       for (int l = 0; l < kGW; ++l) {
         const int tid = gi * kGW + l;
         const int b = t * kBlocksPerTile + tid;
-        const double k2 = b < C.nb ? std::fabs(sA.at(tid)) : -1.0;
+        const double k2 = b < C.nb ? (l >= kJLo && l <= kJHi ? std::fabs(sA.at(tid)) : -0.5) : -1.0;
         const int i2 = b < C.nb ? b : INT32_MAX;
         if (k2 > key || (k2 == key && i2 < kid)) {
           key = k2;
@@ -142,11 +148,13 @@ void front(Chain& C) {
     }
     double bk = -2.0;
     int bq = 0;
-    for (int i = 0; i < kKW; ++i)
-      if (gkey.at(i) > bk) {
-        bk = gkey.at(i);
+    for (int i = 0; i < kKW; ++i) {
+      const double k = i >= kJLo && i <= kJHi ? gkey.at(i) : (gkey.at(i) >= 0.0 ? -0.5 : -1.0);
+      if (k > bk) {
+        bk = k;
         bq = gid.at(i);
       }
+    }
     C.ks.at(t) = t == 0 ? 0 : bq;
     if (t == C.nk - 1) C.ks.at(C.nk) = C.ng;
     double itot = 0.0;
