@@ -73,7 +73,7 @@ constexpr int kCertBit = 1 << 30;
 #endif
 constexpr int kPixChunk = RST_PIX_CHUNK;
 #ifndef RST_PIX_COLD_ITERS
-#define RST_PIX_COLD_ITERS 3  // iterations [1, RST_PIX_COLD_ITERS) take the cold windows below
+#define RST_PIX_COLD_ITERS 4  // iterations [1, RST_PIX_COLD_ITERS) take the cold windows below (r04a: 4 vs 3, +1.6 %)
 #endif
 #ifndef RST_PIX_COLD_HALF
 #define RST_PIX_COLD_HALF 16.0f  // their half-width cap (level pixels)
@@ -668,7 +668,7 @@ __global__ __launch_bounds__(kBS) void k_icp_nn(BvhView bv, AdjView av, PixView 
     const float sp = (float)pv.s * pz / fminf(fabsf(pv.fx), fabsf(pv.fy));
     const bool reseed = need && wb >= 0 && !(d0 <= 9.f * sp * sp);
     if (__ballot(reseed) != 0 && reseed) d0 = fminf(d0, pix_seed_d2(pv, px, py, pz));
-    // a pair's second and third iterations: larger windows over more
+    // a pair's iterations 1-3: larger windows over more
     // staging rounds (the pose still moves by centimetres, beyond the steady
     // state's cap, which would queue them for k_icp_fb's per-lane searches).
     // Not the first: its seeds are the projective / Morton guesses, and
