@@ -72,6 +72,9 @@ constexpr int kCertBit = 1 << 30;
 #define RST_PIX_CHUNK 512  // pixels staged per wave and round (10 KB of LDS per wave; r02: 512 vs 256 same throughput, one pair 13.4 vs 13.9 ms)
 #endif
 constexpr int kPixChunk = RST_PIX_CHUNK;
+#ifndef RST_SQ_FUSE_FRONT
+#define RST_SQ_FUSE_FRONT 0  // REF loop: the front kernel without the totals launch, the previous iteration's tile prefixes (r04b: front + totals 14.5 -> 13.3 us, but the walk +1 ms per pair: stale guesses in the first iterations)
+#endif
 #ifndef RST_PIX_COLD_ITERS
 #define RST_PIX_COLD_ITERS 4  // iterations [1, RST_PIX_COLD_ITERS) take the cold windows below (r04a: 4 vs 3, +1.6 %)
 #endif
@@ -1721,8 +1724,13 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
       }
       RST_CHECK(mark(2));
       if (comm) RST_CHECK(comm_allgatherv_f4(comm, corrg, st));
-      RST_CHECK(seqsum_enqueue(corrg, n_total, it + 1 == opts.max_iter || ctx->seq_trace ? 4 : 3,
-                               sqws, ctx->d_state->seq, st));
+      // (from the second iteration on, the same chains as the iteration before:
+      // no totals launch, the front kernel takes that iteration's tile
+      // prefixes; the last iteration adds the cost chain, which has none)
+      const int nch = it + 1 == opts.max_iter || ctx->seq_trace ? 4 : 3;
+      const int nch_prev = it == 0 ? 0 : (it == opts.max_iter || ctx->seq_trace ? 4 : 3);
+      RST_CHECK(seqsum_enqueue(corrg, n_total, nch, sqws, ctx->d_state->seq, st, nullptr, 7, it,
+                               it > 0 && nch <= nch_prev && RST_SQ_FUSE_FRONT));
       if (n_local > 0)
         k_cov_ref<<<kCovBlocks, kBS, 0, st>>>(srco, corr, n_local, n_total, ctx->d_state, slab2);
       k_reduce_solve<RefAcc><<<1, kRedBS, 0, st>>>(slab, 0, slab2, n_local > 0 ? kCovBlocks : 0, prm,

@@ -241,7 +241,8 @@ int seq_sum4_device(rst_ctx* ctx, const float4* d_x, int64_t n, float* d_out);
 // ws holds seqsum_bytes(n)
 size_t seqsum_bytes(int64_t n);
 int seqsum_enqueue(const float4* d_x, int64_t n, int nch, void* ws, float* d_out,
-                   hipStream_t st, int* d_stats = nullptr, int stages = 7);
+                   hipStream_t st, int* d_stats = nullptr, int stages = 7, int iter = -1,
+                   bool fused = false);
 int kabsch_device(rst_ctx* ctx, const double cov[9], const float smean[3],
                   const float dmean[3], float pose_out[16]);
 

@@ -66,7 +66,9 @@ struct SqView {
   GroupMap* grp;   // [nch][ng]
   SbMap* sbm;      // [nch][nk]
   int* stats;      // optional, 8 per chain
-  double* ttot;    // [nch][4 nk] fp64 totals of 1024-element quarter tiles
+  double* ttot;    // [nch][4 nk] fp64 totals of 1024-element quarter tiles (this call's)
+  double* ttot2;   // [2][4][4 nk] the same, by iteration parity (the fused front
+                   // reads the previous iteration's, writes its own)
   long long* clk;  // [nch][nk][8] shader clocks at the map kernel's phase boundaries
   int* err;        // bound-check failures (bits; 0 = none): a map kernel that
                    // meets a size its tables cannot hold stops instead of
@@ -196,7 +198,16 @@ __global__ __launch_bounds__(kFrontT) void k_sq_tot(const float4* __restrict__ x
 
 // ---- 2: boundaries, unmonitored runs, increments ----------------------------------
 // One workgroup per (tile, chain); thread = one 16-element window.
-__global__ __launch_bounds__(kFrontT) void k_sq_front(SqView v) {
+// FUSED (an ICP iteration after the first, the same chains as the one
+// before): no k_sq_tot launch -- the tile comes straight from the float4
+// stream, the SoA row, window flags and quarter totals are written here, and
+// the tile prefix P is the PREVIOUS iteration's (P only places the block
+// boundaries and seeds the guesses: a stale P costs map hits, never a bit
+// of the result).
+template <bool FUSED>
+__global__ __launch_bounds__(kFrontT) void k_sq_front(SqView v, const float4* __restrict__ x,
+                                                     const double* __restrict__ tprev,
+                                                     double* __restrict__ tnext) {
   // (one pad float per 16: thread t's window reads xs(16 t + j) at 17 t + j,
   // every lane in its own bank)
   __shared__ float xsp[(kTile + kW) + (kTile + kW) / kW];
@@ -220,7 +231,18 @@ __global__ __launch_bounds__(kFrontT) void k_sq_front(SqView v) {
 #pragma unroll
     for (int j = 0; j < kJ; ++j) {
       const int i = tid + j * kFrontT;
-      tv[j] = i < kTile + kW && e0 + i < v.n ? Xs[e0 + i] : 0.0f;
+      if (FUSED)
+        tv[j] = i < kTile + kW && e0 + i < v.n ? comp(x[e0 + i], c) : 0.0f;
+      else
+        tv[j] = i < kTile + kW && e0 + i < v.n ? Xs[e0 + i] : 0.0f;
+    }
+    if (FUSED) {
+      float* dst = v.soa + (int64_t)c * v.ns;
+#pragma unroll
+      for (int j = 0; j < kJ; ++j) {
+        const int i = tid + j * kFrontT;
+        if (i < kTile && e0 + i < v.n) dst[e0 + i] = tv[j];
+      }
     }
 #pragma unroll
     for (int j = 0; j < kJ; ++j) {
@@ -229,15 +251,27 @@ __global__ __launch_bounds__(kFrontT) void k_sq_front(SqView v) {
     }
   }
   // fp64 prefix at the tile start (the quarter tiles' totals before it)
-  const double P = block_sum_global<kFrontT>(v.ttot + (int64_t)c * v.nk * kTotQ, t * kTotQ, lds);
+  const double P = block_sum_global<kFrontT>((FUSED ? tprev : v.ttot) + (int64_t)c * v.nk * kTotQ,
+                                             t * kTotQ, lds);
   __syncthreads();
   // the thread's window: fp64 total and prefix
   const int b = t * kBlocksPerTile + tid;
   double wsum = 0.0;
+  int wfl = 0;
 #pragma unroll
   for (int j = 0; j < kW; ++j) {
     const float e = xs(tid * kW + j);
+    wfl |= nf_flags(e);
     if (isfinite(e)) wsum += (double)e;
+  }
+  if (FUSED) {
+    // the window's non-finite flags and this iteration's quarter totals (one
+    // quarter per wavefront: 64 windows of 16)
+    if (b < v.nb) v.wflg[(int64_t)c * v.nb + b] = (uint8_t)wfl;
+    double q = wsum;
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) q += __shfl_xor(q, o, kWave);
+    if ((tid & (kWave - 1)) == 0) tnext[(int64_t)c * v.nk * kTotQ + t * kTotQ + tid / kWave] = q;
   }
   double ttotal;
   const double wrel = block_scan_excl<kFrontT>(wsum, lds, &ttotal);
@@ -1020,6 +1054,9 @@ static size_t sq_layout(SqView& v, int64_t n, int nch, char* base) {
     off += (bytes + 255) & ~(size_t)255;
     return q;
   };
+  // (first: its place must not depend on nch -- consecutive calls with
+  // different chain counts share it)
+  v.ttot2 = (double*)take(sizeof(double) * 2 * 4 * 4 * (size_t)v.nk);
   v.soa = (float*)take(sizeof(float) * nch * (size_t)v.ns);
   v.wflg = (uint8_t*)take((size_t)nch * v.nb);
   v.err = (int*)take(sizeof(int));
@@ -1044,8 +1081,12 @@ size_t seqsum_bytes(int64_t n) {
 
 // out[c] for c < nch: the sequential float sum of component c of x[0..n).
 // stages (debug): bit 0 the front kernel, bit 1 the maps, bit 2 the walk.
+// iter >= 0 (an ICP loop's iteration on one workspace): the quarter totals
+// go to the iteration's parity buffer; fused (iter > 0, the same chains as
+// iteration iter - 1 summed on this workspace): no totals launch, the front
+// kernel takes the tile prefixes of iteration iter - 1.
 int seqsum_enqueue(const float4* d_x, int64_t n, int nch, void* ws, float* d_out, hipStream_t st,
-                   int* d_stats, int stages) {
+                   int* d_stats, int stages, int iter, bool fused) {
   if (nch < 1 || nch > 4 || n < 0) return RST_E_ARG;
   if (n == 0) {
     RST_HIP(hipMemsetAsync(d_out, 0, sizeof(float) * nch, st));
@@ -1058,9 +1099,16 @@ int seqsum_enqueue(const float4* d_x, int64_t n, int nch, void* ws, float* d_out
 #ifdef RST_SQ_ABLATE  // measurement only (wrong sums): skip kernels by bit
   stages &= ~RST_SQ_ABLATE;
 #endif
+  const size_t tq = (size_t)4 * kTotQ * v.nk;  // one parity buffer: 4 chains' quarter totals
+  if (iter >= 0) v.ttot = v.ttot2 + (size_t)(iter & 1) * tq;
   if (stages & 1) {
-    k_sq_tot<<<v.nk * kTotQ, kFrontT, 0, st>>>(d_x, v);
-    k_sq_front<<<dim3(v.nk, nch), kFrontT, 0, st>>>(v);
+    if (fused && iter > 0) {
+      k_sq_front<true><<<dim3(v.nk, nch), kFrontT, 0, st>>>(v, d_x, v.ttot2 + (size_t)((iter - 1) & 1) * tq,
+                                                            v.ttot);
+    } else {
+      k_sq_tot<<<v.nk * kTotQ, kFrontT, 0, st>>>(d_x, v);
+      k_sq_front<false><<<dim3(v.nk, nch), kFrontT, 0, st>>>(v, nullptr, nullptr, nullptr);
+    }
   }
   if (stages & 2) k_sq_maps<<<dim3(v.nk, nch), kMapT, 0, st>>>(v);
   if (stages & 4) k_sq_walk<<<nch, kWave, 0, st>>>(v, d_out);

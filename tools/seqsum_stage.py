@@ -28,7 +28,7 @@ def layout(n, nch=4):
     ns = (n + 63) & ~63
     off = 0
     out = {}
-    for name, size in (("soa", 4 * nch * ns), ("wflg", nch * nb),
+    for name, size in (("ttot2", 8 * 2 * 4 * 4 * nk), ("soa", 4 * nch * ns), ("wflg", nch * nb),
                        ("err", 4), ("ttot", 8 * nch * 4 * nk), ("bs", 4 * nch * (nb + 1)), ("gs", 4 * nch * (ng + 1)),
                        ("ks", 4 * nch * (nk + 1)), ("inc", 8 * nch * nb), ("ipre", 8 * nch * nb), ("tinc", 8 * nch * nk),
                        ("leaf", 64 * nch * nb), ("grp", 256 * nch * ng), ("sbm", 1024 * nch * nk), ("clk", 64 * nch * nk)):
