@@ -33,6 +33,11 @@ int rst_debug_queue_trace(rst_ctx* ctx, int32_t* out, int32_t n);
  * :113) and of their d2 (the cost, :120) -- bit for bit the reference's
  * when every iteration's correspondences are. */
 int rst_debug_enable_seq_trace(rst_ctx* ctx, int enable);
+/* With the trace enabled, per iteration of the last align (first n <= 256)
+ * the walks' statistics, 64 int32 each (the layout of rst_debug_seq_sum's
+ * stats: per chain superblock tries / hits, group tries / hits, leaf tries
+ * / hits, serial blocks, walker clocks). */
+int rst_debug_seq_walk_stats(rst_ctx* ctx, int32_t* out, int32_t n);
 int rst_debug_seq_trace(rst_ctx* ctx, float* out, int32_t n);
 
 /* RST_DIAG builds, per iteration of the last align call on ctx (first n <=

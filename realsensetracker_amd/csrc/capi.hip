@@ -280,6 +280,7 @@ int rst_ctx_destroy(rst_ctx* ctx) {
   if (ctx->d_state) hipFree(ctx->d_state);
   if (ctx->h_state) hipHostFree(ctx->h_state);
   if (ctx->d_slab) hipFree(ctx->d_slab);
+  if (ctx->d_sqstats) hipFree(ctx->d_sqstats);
   if (ctx->own_stream) hipStreamDestroy(ctx->own_stream);
   for (rst_target* t : ctx->live) t->ctx = nullptr;  // they free to the device
   for (auto& kv : ctx->pool) hipFree(kv.second);
@@ -322,6 +323,20 @@ int rst_ctx_enable_graphs(rst_ctx* ctx, int enable) {
 int rst_debug_enable_seq_trace(rst_ctx* ctx, int enable) {
   if (!ctx) return RST_E_ARG;
   ctx->seq_trace = enable != 0;
+  if (ctx->seq_trace && !ctx->d_sqstats) {
+    RST_HIP(hipSetDevice(ctx->device));
+    if (hipMalloc(&ctx->d_sqstats, sizeof(int32_t) * 64 * kQTrace) != hipSuccess) return RST_E_NOMEM;
+    RST_HIP(hipMemset(ctx->d_sqstats, 0, sizeof(int32_t) * 64 * kQTrace));
+  }
+  return RST_OK;
+}
+
+int rst_debug_seq_walk_stats(rst_ctx* ctx, int32_t* out, int32_t n) {
+  if (!ctx || !out || n < 0 || !ctx->d_sqstats) return RST_E_ARG;
+  RST_HIP(hipSetDevice(ctx->device));
+  RST_HIP(hipStreamSynchronize(ctx->stream));
+  RST_HIP(hipMemcpy(out, ctx->d_sqstats, sizeof(int32_t) * 64 * std::min<int32_t>(n, kQTrace),
+                    hipMemcpyDeviceToHost));
   return RST_OK;
 }
 

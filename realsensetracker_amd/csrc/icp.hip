@@ -1729,7 +1729,8 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
       // prefixes; the last iteration adds the cost chain, which has none)
       const int nch = it + 1 == opts.max_iter || ctx->seq_trace ? 4 : 3;
       const int nch_prev = it == 0 ? 0 : (it == opts.max_iter || ctx->seq_trace ? 4 : 3);
-      RST_CHECK(seqsum_enqueue(corrg, n_total, nch, sqws, ctx->d_state->seq, st, nullptr, 7, it,
+      int* sqstats = ctx->seq_trace && ctx->d_sqstats && it < kQTrace ? ctx->d_sqstats + 64 * it : nullptr;
+      RST_CHECK(seqsum_enqueue(corrg, n_total, nch, sqws, ctx->d_state->seq, st, sqstats, 7, it,
                                it > 0 && nch <= nch_prev && RST_SQ_FUSE_FRONT));
       if (n_local > 0)
         k_cov_ref<<<kCovBlocks, kBS, 0, st>>>(srco, corr, n_local, n_total, ctx->d_state, slab2);

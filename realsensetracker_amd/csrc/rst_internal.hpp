@@ -123,6 +123,7 @@ struct rst_ctx {
   // updated in place per align
   bool graphs = false;
   bool seq_trace = false;  // RST_SUM_REF: walk the cost chain every iteration (diagnostics)
+  int32_t* d_sqstats = nullptr;  // with seq_trace: the walks' statistics, 64 int32 per iteration
   std::map<std::tuple<int, int, int, int>, hipGraphExec_t> gexec;
   // device memory of freed targets, kept for the next build (hipFree
   // synchronises the whole device, which would stall every stream of a

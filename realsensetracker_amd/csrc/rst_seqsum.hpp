@@ -167,6 +167,9 @@ RST_SQ_HD void run_init(Run& p, float s0) {
   p.opaque = false;
 }
 
+// (branch-free: every case's bounds computed, then selected -- the leaf
+// runs of a wavefront take different cases in the same step; the values
+// are those of the case analysis in the comments)
 RST_SQ_HD void run_step(Run& p, float x, int e0) {
   const float s = p.s;
   const float r = s + x;
@@ -180,49 +183,41 @@ RST_SQ_HD void run_step(Run& p, float x, int e0) {
   const int Er = (int)((bits >> 23) & 0xffu);
   const uint32_t man = bits & 0x7fffffu;
   const bool neg = (bits >> 31) != 0;
-  if (r == 0.0f) {
-    // +-0 result: exact cancellation (anything else would be subnormal)
-    if (err != 0.0f) p.opaque = true;
-    const float B = pow2f(imin(e0 + 24, 127));
-    p.lo = fmaxf(p.lo, -B);
-    p.hi = fminf(p.hi, B);
-    return;
-  }
-  // |r| in [2^-99, 2^126): normal grids far from under/overflow, else no map
-  if (Er < 28 || Er > 252 || !(err == err)) {
-    p.opaque = true;
-    return;
-  }
+  // +-0 result: exact cancellation (anything else would be subnormal); the
+  // window +-2^(e0+24), no lattice need, opaque unless exact
+  const bool zero = r == 0.0f;
+  // else |r| in [2^-99, 2^126): normal grids far from under/overflow, else no map
+  const bool bad = !zero && (Er < 28 || Er > 252 || !(err == err));
+  const bool inexact = err != 0.0f;
   const int er = Er - 127;
   // y's binade: below |r| when r is a power of two rounded up from beneath
-  const bool below = man == 0 && err != 0.0f && ((f2u(err) >> 31) != (bits >> 31));
+  const bool below = man == 0 && inexact && ((f2u(err) >> 31) != (bits >> 31));
   const int ey = below ? er - 1 : er;
-  float wlo, whi;
-  if (err != 0.0f) {
-    const float gy = pow2f(ey - 23);
-    const float ra = fabsf(r);
-    const float ea = neg ? -err : err;   // |y| = ra + ea
-    const float D = pow2f(ey) - ra;      // <= 0
-    const float U = pow2f(ey + 1) - ra;  // >= 0
-    // magnitude offsets dm with |y| + dm in [2^ey, 2^(ey+1)), dm a multiple of gy
-    const float lo_m = ea > 0.0f ? D : D + gy;
-    const float hi_m = ea < 0.0f ? U : U - gy;
-    wlo = neg ? -hi_m : lo_m;
-    whi = neg ? -lo_m : hi_m;
-    const bool tie = fabsf(err) == 0.5f * gy;
-    p.need = imax(p.need, ey - 23 + (tie ? 1 : 0));
-  } else {
-    // exact: y + d stays representable while |y + d| <= 2^24 q,
-    // q = min(lsb(y), max(g0, grid(y))) (the lattice is raised to grid(y))
-    const int elsb = er - 23 + ctz32(man | 0x800000u);
-    const int eq = imin(elsb, imax(e0, ey - 23));
-    const float B = pow2f(imin(eq + 24, 127));
-    wlo = neg ? -B - r : -B;
-    whi = neg ? B : B - r;
-    p.need = imax(p.need, ey - 23);
-  }
-  p.lo = fmaxf(p.lo, wlo);
-  p.hi = fminf(p.hi, whi);
+  // inexact: magnitude offsets dm with |y| + dm in [2^ey, 2^(ey+1)), dm a
+  // multiple of gy
+  const float gy = pow2f(ey - 23);
+  const float ra = fabsf(r);
+  const float ea = neg ? -err : err;   // |y| = ra + ea
+  const float D = pow2f(ey) - ra;      // <= 0
+  const float U = pow2f(ey + 1) - ra;  // >= 0
+  const float lo_m = ea > 0.0f ? D : D + gy;
+  const float hi_m = ea < 0.0f ? U : U - gy;
+  const bool tie = fabsf(err) == 0.5f * gy;
+  // exact: y + d stays representable while |y + d| <= 2^24 q,
+  // q = min(lsb(y), max(g0, grid(y))) (the lattice is raised to grid(y))
+  const int elsb = er - 23 + ctz32(man | 0x800000u);
+  const int eq = imin(elsb, imax(e0, ey - 23));
+  const float B = pow2f(imin(eq + 24, 127));
+  const float B0 = pow2f(imin(e0 + 24, 127));
+  float wlo = inexact ? (neg ? -hi_m : lo_m) : (neg ? -B - r : -B);
+  float whi = inexact ? (neg ? -lo_m : hi_m) : (neg ? B : B - r);
+  wlo = zero ? -B0 : wlo;
+  whi = zero ? B0 : whi;
+  const int nd = ey - 23 + (inexact && tie ? 1 : 0);
+  p.opaque = p.opaque || bad || (zero && inexact);
+  p.lo = bad ? p.lo : fmaxf(p.lo, wlo);
+  p.hi = bad ? p.hi : fminf(p.hi, whi);
+  p.need = bad || zero ? p.need : imax(p.need, nd);
 }
 
 // Windows are stored in units of the map's grid 2^e0, clamped to
@@ -245,7 +240,12 @@ RST_SQ_HD int hi_units(double hi, int e0) {
 // sign and binade (G normal, e0 its grid: the usual case), else in exact
 // double arithmetic.  False when v is not on the grid, non-finite, or
 // implausibly far from G.
-// (the exact double path: v in another binade than G)
+// (the exact double path: v in another binade than G; by value in and out:
+// a reference argument to an out-of-line call would put the caller's
+// header and k on the stack)
+struct OffK {
+  int ok, k;
+};
 #if defined(__HIPCC__) && !defined(RST_SQ_SLOW_INLINE)
 __host__ __device__ __noinline__
 #elif defined(__HIPCC__)
@@ -253,15 +253,14 @@ __host__ __device__ __forceinline__
 #else
 inline
 #endif
-bool offset_units_slow(float v, const MapHdr& h, int& k) {
-  if (!(v - v == 0.0f)) return false;
-  const double kv = std::ldexp((double)v, -h.e0);
-  const double kg = std::ldexp((double)h.G, -h.e0);
-  if (kv != std::floor(kv)) return false;
+OffK offset_units_slow(float v, float G, int e0) {
+  if (!(v - v == 0.0f)) return OffK{0, 0};
+  const double kv = std::ldexp((double)v, -e0);
+  const double kg = std::ldexp((double)G, -e0);
+  if (kv != std::floor(kv)) return OffK{0, 0};
   const double kd = kv - kg;
-  if (!(std::fabs(kd) < 1073741824.0)) return false;
-  k = (int)kd;
-  return true;
+  if (!(std::fabs(kd) < 1073741824.0)) return OffK{0, 0};
+  return OffK{1, (int)kd};
 }
 RST_SQ_HD bool offset_units(float v, const MapHdr& h, int& k) {
   const uint32_t vb = f2u(v), gb = f2u(h.G);
@@ -270,7 +269,9 @@ RST_SQ_HD bool offset_units(float v, const MapHdr& h, int& k) {
     k = (gb >> 31) ? -d : d;
     return true;
   }
-  return offset_units_slow(v, h, k);
+  const OffK o = offset_units_slow(v, h.G, h.e0);
+  k = o.k;
+  return o.ok != 0;
 }
 // the bits path only (false in another binade: the caller takes its slow path)
 RST_SQ_HD bool offset_units_fast(float v, const MapHdr& h, int& k) {
@@ -306,19 +307,25 @@ RST_SQ_HD bool apply_ent(int du, int e0, const MapEnt& en, float& out) {
 // through a child map (header h, entries e[] by residue); the node's window
 // [clo, chi] (absolute offsets of the node's start) narrows.  False: this
 // candidate cannot pass the child.
-RST_SQ_HD bool through(float& v, double& clo, double& chi, const MapHdr& h, const MapEnt* e) {
-  if ((h.flags & kOpaque) || h.m < 0 || h.m > kSbM) return false;
-  int k;
-  if (!offset_units(v, h, k)) return false;
-  const int r = k & ((1 << h.m) - 1);
-  const MapEnt en = e[r];
-  const int du = k - r;
+// (in two parts for callers that fetch the entry themselves: the offset
+// k of v in the child's grid, then the child's entry r = k mod 2^m applied)
+RST_SQ_HD bool through_off(float v, const MapHdr& h, int mmax, int& k) {
+  if ((h.flags & kOpaque) || h.m < 0 || h.m > mmax) return false;
+  return offset_units(v, h, k);
+}
+RST_SQ_HD bool through_ent(float& v, double& clo, double& chi, const MapHdr& h, int k, const MapEnt& en) {
+  const int du = k - (k & ((1 << h.m) - 1));
   float out;
   if (!apply_ent(du, h.e0, en, out)) return false;
   clo = std::fmax(clo, std::ldexp((double)(en.LOu - du), h.e0));
   chi = std::fmin(chi, std::ldexp((double)(en.HIu - du), h.e0));
   v = out;
   return true;
+}
+RST_SQ_HD bool through(float& v, double& clo, double& chi, const MapHdr& h, const MapEnt* e) {
+  int k;
+  if (!through_off(v, h, kSbM, k)) return false;
+  return through_ent(v, clo, chi, h, k, e[k & ((1 << h.m) - 1)]);
 }
 
 }  // namespace sq

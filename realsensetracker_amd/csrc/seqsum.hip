@@ -383,35 +383,142 @@ __global__ __launch_bounds__(kFrontT) void k_sq_front(SqView v, const float4* __
   if (tid == 0) v.tinc[(int64_t)c * v.nk + t] = itot;
 }
 
-// ---- 3: leaf, group and superblock maps ------------------------------------------
-// threads per map workgroup: the leaf lanes take kMapT / 2 blocks per
-// round; a group's 16 residue lanes need 31 * 16 <= kMapT (r03: 512 threads
-// and two leaf rounds, same throughput with pairs in flight, 8 us slower alone)
-#ifndef RST_SQ_MAP_T
-#define RST_SQ_MAP_T 1024
-#endif
-constexpr int kMapT = RST_SQ_MAP_T;
-static_assert(kMapT >= kMaxSbGroups * kGroupR && kMapT % kWave == 0, "map workgroup size");
-constexpr int kLeafRounds = (2 * kMaxSbBlocks + kMapT - 1) / kMapT;
+// ---- 3a: leaf maps ----------------------------------------------------------------
+// One workgroup per 64 blocks of a tile and chain, one lane per (block,
+// candidate): a block's 4 candidate runs side by side in a lane quad.  The
+// guess of a block's start: the fp64 prefix of the float32 increments (the
+// tiles' totals before its tile, plus its prefix within the tile,
+// k_sq_front).  (r03: the leaves were a phase of the superblock workgroup --
+// 1024 threads, half of them idle on a 256-block superblock, one workgroup
+// per CU; 292 of them on 256 CUs ran in two rounds.  Alone the leaves fill
+// every CU.)
+constexpr int kLeafT = 256;
+constexpr int kLeafB = kLeafT / kLeafR;             // 64 blocks per workgroup
+constexpr int kLeafWg = kBlocksPerTile / kLeafB;    // 4 per tile
+constexpr int kLeafX = kLeafB * kW + 2 * kW;        // staged elements (the last block runs past)
+static_assert(kBlocksPerTile % kLeafB == 0, "leaf workgroups per tile");
+static_assert(sizeof(Leaf) == 64, "a leaf map is four int4 (k_sq_maps reads it so)");
+
+// A composite lane's step through a child map, without branches (the
+// lanes of a wavefront take different cases in the same step; a chain of
+// divergent branches cost ~1k clocks a step): comp_off the offset k of x in
+// the child's grid (`ok` cleared when the child is unusable or x is off its
+// grid), comp_apply the entry r = k mod 2^m -- the same arithmetic as
+// `through` (rst_seqsum.hpp); once `ok` is false nothing changes.
+__device__ __forceinline__ int comp_off(float x, const MapHdr& h, int mmax, bool& ok) {
+  const bool hv = !(h.flags & kOpaque) && h.m >= 0 && h.m <= mmax;
+  const uint32_t vb = __float_as_uint(x), gb = __float_as_uint(h.G);
+  const bool same = ((vb ^ gb) >> 23) == 0;
+  const int d = (int)(vb & 0x7fffffu) - (int)(gb & 0x7fffffu);
+  int k = (gb >> 31) ? -d : d;
+  bool kok = same;
+  const bool slow = ok && hv && !same;
+  if (__ballot(slow) != 0) {  // (rare: x in another binade than G)
+    if (slow) {
+      const OffK o = offset_units_slow(x, h.G, h.e0);
+      k = o.k;
+      kok = o.ok != 0;
+    }
+  }
+  ok = ok && hv && kok;
+  return k;
+}
+__device__ __forceinline__ void comp_apply(float& x, double& clo, double& chi, bool& ok, const MapHdr& h, int k,
+                                           const MapEnt& en) {
+  const int du = k - (k & ((1 << (ok ? h.m : 0)) - 1));
+  const bool inwin = en.LOu <= du && du <= en.HIu;
+  const float dd = ldexpf((float)du, h.e0);
+  const float o = en.E + dd;
+  const bool ebig = fabsf(en.E) >= fabsf(dd);
+  const bool exact = ebig ? (o - en.E == dd) : (o - dd == en.E);
+  ok = ok && inwin && (du == 0 || exact);
+  clo = ok ? fmax(clo, ldexp((double)(en.LOu - du), h.e0)) : clo;
+  chi = ok ? fmin(chi, ldexp((double)(en.HIu - du), h.e0)) : chi;
+  x = ok ? (du == 0 ? en.E : o) : x;
+}
 
 __device__ __forceinline__ float cand(float G, int e0, int r) {
   return (float)((double)G + ldexp((double)r, e0));
 }
 
+__global__ __launch_bounds__(kLeafT) void k_sq_leaves(SqView v) {
+  __shared__ float xs[kLeafX];
+  __shared__ double lds[kLeafT / kWave + 1];
+  const int t = blockIdx.x / kLeafWg, c = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), r = tid & (kLeafR - 1);
+  const int b0 = t * kBlocksPerTile + (blockIdx.x % kLeafWg) * kLeafB;
+  const int b = b0 + tid / kLeafR;
+  const bool act = b < v.nb;
+  const int* bsg = v.bs + (int64_t)c * (v.nb + 1);
+  const float* X = v.soa + (int64_t)c * v.ns;
+  // (in flight together: the block's bounds and prefix, the elements, the tiles' totals)
+  const int s0 = act ? bsg[b] : 0, s1 = act ? bsg[b + 1] : 0;
+  const double iv = act ? v.ipre[(int64_t)c * v.nb + b] : 0.0;
+  const int64_t x0 = (int64_t)b0 * kW;  // the first block's window: every start is at or after it
+  for (int i = tid; i < kLeafX; i += kLeafT) xs[i] = x0 + i < v.n ? X[x0 + i] : 0.0f;
+  const double base = block_sum_global<kLeafT>(v.tinc + (int64_t)c * v.nk, t, lds);  // (synchronises)
+  Run p;
+  float G = 0.0f;
+  int e0 = -149;
+  if (act) {
+    G = candidate_base(b == 0 ? 0.0f : (float)(base + iv), kLeafR);
+    e0 = grid_exp(G);
+    run_init(p, cand(G, e0, r));
+    int a0 = (int)(s0 - x0), a1 = (int)(s1 - x0);
+    if (a0 < 0 || a1 > kLeafX || a1 - a0 < 1 || a1 - a0 > 2 * kW - 1) {
+      atomicOr(v.err, 32);
+      p.opaque = true;
+      a0 = a1 = 0;
+    }
+    // (the elements in registers first: the run's chain waits on no LDS read)
+    float xr[2 * kW - 1];
+#pragma unroll
+    for (int i = 0; i < 2 * kW - 1; ++i) xr[i] = xs[min(a0 + i, kLeafX - 1)];
+#pragma unroll
+    for (int i = 0; i < 2 * kW - 1; ++i)
+      if (i < a1 - a0) run_step(p, xr[i], e0);
+  } else {
+    run_init(p, 0.0f);
+  }
+  // the block's lattice: the largest need over its 4 runs
+  int need = p.need;
+  need = max(need, __shfl_xor(need, 1, kWave));
+  need = max(need, __shfl_xor(need, 2, kWave));
+  const bool op0 = __shfl(p.opaque ? 1 : 0, lane & ~(kLeafR - 1), kWave) != 0;
+  if (!act) return;
+  const int mneed = need == kNoNeed ? 0 : max(0, need - e0);
+  const bool exact_only = mneed > kLeafM;
+  const int m = exact_only ? 0 : mneed;
+  Leaf& o = v.leaf[(int64_t)c * v.nb + b];
+  if (r == 0) o.h = MapHdr{G, e0, m, op0 ? kOpaque : 0};
+  MapEnt en;
+  en.E = p.s;
+  en.LOu = lo_units((double)p.lo, e0);
+  en.HIu = hi_units((double)p.hi, e0);
+  if (p.opaque || r >= (1 << m)) {
+    en.LOu = 1;
+    en.HIu = 0;
+  } else if (exact_only) {
+    en.LOu = max(en.LOu, 0);
+    en.HIu = min(en.HIu, 0);
+  }
+  o.e[r] = en;
+}
+
+// ---- 3b: group and superblock maps ------------------------------------------------
+// One workgroup per (superblock, chain): its leaf maps staged in LDS, then
+// lanes (group, residue) compose each group's leaves for up to 16
+// candidates, lanes 0..63 the superblock's groups for up to 64.
+constexpr int kMapT = 512;
+static_assert(kMapT >= kMaxSbGroups * kGroupR && kMapT % kWave == 0, "map workgroup size");
+
 __global__ __launch_bounds__(kMapT) void k_sq_maps(SqView v) {
-  // (one pad float per 16: the leaf lanes' blocks start ~16 elements apart,
-  // padded they read distinct banks)
-  __shared__ float xsp[kMaxSbElems + kMaxSbElems / 16 + 1];
-  auto xs = [&](int i) -> float& { return xsp[i + (i >> 4)]; };
   __shared__ Leaf lf[kMaxSbBlocks];
   __shared__ GroupMap gm[kMaxSbGroups];
-  __shared__ double Gd[kMaxSbBlocks + 1];
-  __shared__ int sbs[kMaxSbBlocks + 1];
   __shared__ int sgs[kMaxSbGroups + 1];
-  __shared__ double lds[kMapT / kWave + 1];
   __shared__ int sbad;
   const int k = blockIdx.x, c = blockIdx.y;
-  const int tid = threadIdx.x, lane = tid & (kWave - 1);
+  const int tid = threadIdx.x;
   long long* clk = v.clk + ((int64_t)c * v.nk + k) * 8;
   if (tid == 0) clk[0] = (long long)__builtin_amdgcn_s_memtime();
   const int* bsg = v.bs + (int64_t)c * (v.nb + 1);
@@ -434,106 +541,22 @@ __global__ __launch_bounds__(kMapT) void k_sq_maps(SqView v) {
     if (tid == 0) atomicOr(v.err, 1);
     return;
   }
-  const int ngr = gb - ga, nblk = bb - ba, nel = eb - ea;
-  const float* X = v.soa + (int64_t)c * v.ns;
+  const int ngr = gb - ga, nblk = bb - ba;
   if (tid == 0) sbad = 0;
   {
-    // (all loads in flight before the stores; nel <= kMaxSbElems)
-    constexpr int kJ = (kMaxSbElems + kMapT - 1) / kMapT;
-    float tv[kJ];
+    // the leaves (16 B pieces, all in flight before the stores)
+    constexpr int kP = sizeof(Leaf) / 16, kJ = (kMaxSbBlocks * kP + kMapT - 1) / kMapT;
+    const int4* src = reinterpret_cast<const int4*>(v.leaf + (int64_t)c * v.nb + ba);
+    int4 tv[kJ];
 #pragma unroll
-    for (int j = 0; j < kJ; ++j) tv[j] = tid + j * kMapT < nel ? X[ea + tid + j * kMapT] : 0.0f;
+    for (int j = 0; j < kJ; ++j) tv[j] = tid + j * kMapT < nblk * kP ? src[tid + j * kMapT] : int4{};
 #pragma unroll
     for (int j = 0; j < kJ; ++j)
-      if (tid + j * kMapT < nel) xs(tid + j * kMapT) = tv[j];
+      if (tid + j * kMapT < nblk * kP) reinterpret_cast<int4*>(lf)[tid + j * kMapT] = tv[j];
   }
-  for (int i = tid; i <= nblk; i += kMapT) sbs[i] = bsg[ba + i] - ea;
   for (int i = tid; i <= ngr; i += kMapT) sgs[i] = gsg[ga + i] - ba;
+  __syncthreads();
   if (tid == 0) clk[1] = (long long)__builtin_amdgcn_s_memtime();
-  // refined guesses: the fp64 prefix of the blocks' float32 increments --
-  // the tiles' totals before the superblock's first tile, plus each block's
-  // prefix within its tile (k_sq_front); a superblock spans <= 2 tiles
-  {
-    const int tb = ba / kBlocksPerTile;
-    const double* tinc = v.tinc + (int64_t)c * v.nk;
-    const double iv = tid < nblk ? v.ipre[(int64_t)c * v.nb + ba + tid] : 0.0;  // (in flight)
-    const double next = tb < v.nk ? tinc[tb] : 0.0;
-    const double base = block_sum_global<kMapT>(tinc, tb, lds);
-    if (tid < nblk) {
-      const int b = ba + tid;
-      Gd[tid] = b == 0 ? 0.0 : (b / kBlocksPerTile == tb ? base : base + next) + iv;
-    }
-  }
-  __syncthreads();
-  if (tid == 0) clk[2] = (long long)__builtin_amdgcn_s_memtime();
-  // -- leaves: lane (block, residue pair): runs from candidates rp and rp + 2,
-  // interleaved (two independent dependency chains per lane), kLeafRounds
-  // rounds of kMapT / 2 blocks
-  Leaf* leafg = v.leaf + (int64_t)c * v.nb;
-  for (int round = 0; round < kLeafRounds; ++round) {
-    const int bl = (tid >> 1) + round * (kMapT / 2), rp = tid & 1;
-    const bool act = bl < nblk;
-    Run p0, p1;
-    float G = 0.0f;
-    int e0 = -149;
-    if (act) {
-      G = candidate_base((float)Gd[bl], kLeafR);
-      e0 = grid_exp(G);
-      run_init(p0, cand(G, e0, rp));
-      run_init(p1, cand(G, e0, rp + 2));
-      int s0 = sbs[bl], s1 = sbs[bl + 1];
-      if (s0 < 0 || s1 > nel || s1 - s0 < 1 || s1 - s0 > 2 * kW - 1) {
-        atomicOr(v.err, 32);
-        p0.opaque = true;
-        s1 = s0;
-      }
-      for (int i = s0; i < s1; ++i) {
-        const float xv = xs(i);
-        run_step(p0, xv, e0);
-        run_step(p1, xv, e0);
-      }
-    } else {
-      run_init(p0, 0.0f);
-      run_init(p1, 0.0f);
-    }
-    // the block's lattice: the largest need over its 4 runs
-    int need = max(p0.need, p1.need);
-    need = max(need, __shfl_xor(need, 1, kWave));
-    const bool op0 = __shfl(p0.opaque ? 1 : 0, lane & ~1, kWave) != 0;
-    if (act) {
-      const int mneed = need == kNoNeed ? 0 : max(0, need - e0);
-      const bool exact_only = mneed > kLeafM;
-      const int m = exact_only ? 0 : mneed;
-      Leaf& o = lf[bl];
-      if (rp == 0) {
-        o.h.G = G;
-        o.h.e0 = e0;
-        o.h.m = m;
-        o.h.flags = op0 ? kOpaque : 0;
-      }
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const Run& p = h ? p1 : p0;
-        const int r = rp + 2 * h;
-        MapEnt en;
-        en.E = p.s;
-        en.LOu = lo_units((double)p.lo, e0);
-        en.HIu = hi_units((double)p.hi, e0);
-        if (p.opaque || r >= (1 << m)) {
-          en.LOu = 1;
-          en.HIu = 0;
-        } else if (exact_only) {
-          en.LOu = max(en.LOu, 0);
-          en.HIu = min(en.HIu, 0);
-        }
-        o.e[r] = en;
-      }
-    }
-  }
-  __syncthreads();
-  for (int i = tid; i < nblk * (int)(sizeof(Leaf) / 4); i += kMapT)
-    reinterpret_cast<int*>(leafg + ba)[i] = reinterpret_cast<const int*>(lf)[i];
-  if (tid == 0) clk[3] = (long long)__builtin_amdgcn_s_memtime();
   // -- groups: lane (group, residue), up to 16 residues
   GroupMap* grpg = v.grp + (int64_t)c * v.ng;
   {
@@ -549,9 +572,10 @@ __global__ __launch_bounds__(kMapT) void k_sq_maps(SqView v) {
       const MapHdr h0 = lf[c0].h;
       int lat = h0.e0 + h0.m;
       for (int j = c0 + 1; j < c1; ++j) {
-        const MapHdr hj = lf[j].h;
-        if (!(hj.flags & kOpaque)) lat = max(lat, hj.e0 + hj.m);
+        const int4 hj = *reinterpret_cast<const int4*>(&lf[j].h);  // (one read, no branch)
+        lat = (hj.w & kOpaque) ? lat : max(lat, hj.y + hj.z);
       }
+      if (tid == 0) clk[2] = (long long)__builtin_amdgcn_s_memtime();
       int m = max(0, lat - h0.e0);
       const bool exact_only = m > kGroupM;
       if (exact_only) m = 0;
@@ -573,7 +597,32 @@ __global__ __launch_bounds__(kMapT) void k_sq_maps(SqView v) {
         float x = cand(G, e0, r);
         double clo = -INFINITY, chi = INFINITY;
         bool ok = true;
-        for (int j = c0; j < c1 && ok; ++j) ok = through(x, clo, chi, lf[j].h, lf[j].e);
+        // (leaf j + 1 in flight while leaf j is applied; its entry picked
+        // from registers: no LDS trip in the chain)
+        // (as four int4: a select between struct members would go through
+        // the stack)
+        const int4* lq = reinterpret_cast<const int4*>(lf);
+        int4 q0 = lq[4 * c0], q1 = lq[4 * c0 + 1], q2 = lq[4 * c0 + 2], q3 = lq[4 * c0 + 3];
+        for (int j = c0; j < c1; ++j) {
+          const int jn = 4 * min(j + 1, c1 - 1);
+          const int4 n0 = lq[jn], n1 = lq[jn + 1], n2 = lq[jn + 2], n3 = lq[jn + 3];
+          const MapHdr h{__int_as_float(q0.x), q0.y, q0.z, q0.w};
+          const int kq = comp_off(x, h, kLeafM, ok);
+          const int rr = kq & ((1 << (ok ? h.m : 0)) - 1);  // (m <= kLeafM when ok)
+          // (selects on the residue's bits: a chain of rr == i tests became a
+          // switch, i.e. branches)
+          const bool r0 = (rr & 1) != 0, r1 = (rr & 2) != 0;
+          MapEnt en;
+          en.E = __int_as_float(r1 ? (r0 ? q3.y : q2.z) : (r0 ? q1.w : q1.x));
+          en.LOu = r1 ? (r0 ? q3.z : q2.w) : (r0 ? q2.x : q1.y);
+          en.HIu = r1 ? (r0 ? q3.w : q3.x) : (r0 ? q2.y : q1.z);
+          comp_apply(x, clo, chi, ok, h, kq, en);
+          q0 = n0;
+          q1 = n1;
+          q2 = n2;
+          q3 = n3;
+        }
+        if (tid == 0) clk[3] = (long long)__builtin_amdgcn_s_memtime();
         if (ok) {
           if (exact_only) {
             clo = fmax(clo, 0.0);
@@ -632,7 +681,14 @@ __global__ __launch_bounds__(kMapT) void k_sq_maps(SqView v) {
       float x = cand(G, e0, r);
       double clo = -INFINITY, chi = INFINITY;
       bool ok = true;
-      for (int j = 0; j < ngr && ok; ++j) ok = through(x, clo, chi, gm[j].h, gm[j].e);
+      // (group j + 1's header in flight while group j is applied)
+      MapHdr H = gm[0].h;
+      for (int j = 0; j < ngr; ++j) {
+        const MapHdr Hn = gm[min(j + 1, ngr - 1)].h;
+        const int kq = comp_off(x, H, kGroupM, ok);
+        comp_apply(x, clo, chi, ok, H, kq, gm[j].e[kq & ((1 << (ok ? H.m : 0)) - 1)]);
+        H = Hn;
+      }
       if (ok) {
         if (exact_only) {
           clo = fmax(clo, 0.0);
@@ -1110,7 +1166,10 @@ int seqsum_enqueue(const float4* d_x, int64_t n, int nch, void* ws, float* d_out
       k_sq_front<false><<<dim3(v.nk, nch), kFrontT, 0, st>>>(v, nullptr, nullptr, nullptr);
     }
   }
-  if (stages & 2) k_sq_maps<<<dim3(v.nk, nch), kMapT, 0, st>>>(v);
+  if (stages & 2) {
+    k_sq_leaves<<<dim3(v.nk * kLeafWg, nch), kLeafT, 0, st>>>(v);
+    k_sq_maps<<<dim3(v.nk, nch), kMapT, 0, st>>>(v);
+  }
   if (stages & 4) k_sq_walk<<<nch, kWave, 0, st>>>(v, d_out);
   RST_HIP(hipGetLastError());
   return RST_OK;
