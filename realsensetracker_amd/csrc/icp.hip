@@ -72,6 +72,12 @@ constexpr int kCertBit = 1 << 30;
 #define RST_PIX_CHUNK 512  // pixels staged per wave and round (10 KB of LDS per wave; r02: 512 vs 256 same throughput, one pair 13.4 vs 13.9 ms)
 #endif
 constexpr int kPixChunk = RST_PIX_CHUNK;
+#ifndef RST_NN_COMPACT
+#define RST_NN_COMPACT 0  // RST_SUM_REF: k_icp_nn's pixel-window searches compacted over the workgroup (r04h: nn 35.0 -> 38.6 us steady, fb queues longer -- larger union boxes; 15.1k -> 14.5k it/s)
+#endif
+#ifndef RST_NN_MIN_WAVES
+#define RST_NN_MIN_WAVES 1  // k_icp_nn occupancy hint (waves per SIMD)
+#endif
 #ifndef RST_SQ_FUSE_FRONT
 #define RST_SQ_FUSE_FRONT 0  // REF loop: the front kernel without the totals launch, the previous iteration's tile prefixes (r04b: front + totals 14.5 -> 13.3 us, but the walk +1 ms per pair: stale guesses in the first iterations)
 #endif
@@ -591,7 +597,7 @@ __device__ __forceinline__ void proj_seed(const BvhView& bv, const PixView& pv, 
 // (no occupancy hint: the compiler's own register budget, measured best in
 // r02 -- a 5-waves/SIMD target spilled)
 template <class Acc>
-__global__ __launch_bounds__(kBS) void k_icp_nn(BvhView bv, AdjView av, PixView pv, AccArgs aa,
+__global__ __launch_bounds__(kBS, RST_NN_MIN_WAVES) void k_icp_nn(BvhView bv, AdjView av, PixView pv, AccArgs aa,
                                                 const float4* __restrict__ src, int64_t n,
                                                 const IcpState* __restrict__ st,
                                                 float4* __restrict__ nnq,
@@ -657,6 +663,109 @@ __global__ __launch_bounds__(kBS) void k_icp_nn(BvhView bv, AdjView av, PixView 
   } else if (need) {
     d0 = has_cert ? dq : d2_ref(px, py, pz, tq.x, tq.y, tq.z);
   }
+#if RST_PIX_TILES && RST_NN_COMPACT
+  if constexpr (std::is_same<Acc, RefAcc>::value) {  // (RefAcc::add reads only s.w)
+    if (pv.map && st->iter < RST_PIX_ITERS && n < (int64_t)1 << 30) {  // (i and two flags in 32 bits)
+      // The pixel-window searches compacted over the workgroup: the lanes
+      // that still need a search (a few per wavefront in the steady state)
+      // listed in point order in LDS, the list searched by as many whole
+      // wavefronts as it fills -- one, mostly; the others only stream.
+      // (r04: a wavefront per 64 points each searching for its own few
+      // lanes kept the pass at ~36 us where its stream takes ~8.)
+      __shared__ float4 cl_q[kBS];  // query, seed distance
+      __shared__ float4 cl_c[kBS];  // cold seed (point, position)
+      __shared__ int cl_i[kBS], cl_o[kBS];
+      const float sp = (float)pv.s * pz / fminf(fabsf(pv.fx), fabsf(pv.fy));
+      const bool reseed = need && wb >= 0 && !(d0 <= 9.f * sp * sp);
+      if (__ballot(reseed) != 0 && reseed) d0 = fminf(d0, pix_seed_d2(pv, px, py, pz));
+      const uint64_t nm = __ballot(need);
+      if (lane == 0) wq[0][wid] = __popcll(nm);
+      __syncthreads();
+      int slot = 0, tot = 0;
+#pragma unroll
+      for (int w = 0; w < kBS / kWave; ++w) {
+        slot += w < wid ? wq[0][w] : 0;
+        tot += wq[0][w];
+      }
+      const uint64_t lt = (1ull << lane) - 1ull;
+      if (need) {
+        slot += __popcll(nm & lt);
+        cl_q[slot] = make_float4(px, py, pz, d0);
+        cl_c[slot] = make_float4(cq.x, cq.y, cq.z, i2f(cpos));
+        // (bit 31: far queue; bit 30: cold)
+        cl_i[slot] = (int)i | (far ? (int)0x80000000 : 0) | (wb < 0 ? 0x40000000 : 0);
+        cl_o[slot] = f2i(s.w);
+      }
+      // the certified and the non-finite queries' outputs (their own lanes)
+      if (certified)
+        Acc::add(v, bv, aa, u, s, px, py, pz, dq, f2i(tq.w) & kPosMask, tq);
+      else if (act && !fin)
+        Acc::add(v, bv, aa, u, s, px, py, pz, FLT_MAX, -1, tq);
+      __syncthreads();
+      const int j = wid * kWave + lane;
+      bool fail = false, jfar = false;
+      int ji = 0;
+      if (wid * kWave < tot) {  // (uniform per wavefront)
+        const bool ea = j < tot;
+        const float4 q = ea ? cl_q[j] : make_float4(0.f, 0.f, 0.f, FLT_MAX);
+        const int code = ea ? cl_i[j] : 0;
+        ji = code & 0x3fffffff;
+        jfar = code < 0;
+        Best2 pr;
+        pr.init();
+        float4 pq = make_float4(0.f, 0.f, 0.f, 0.f);
+        float prc = 0.f;
+        const bool cold = st->iter >= 1 && st->iter < RST_PIX_COLD_ITERS;
+        const bool pok =
+            cold ? pix_tile_search<kPixChunk, RST_PIX_COLD_CHUNKS>(bv, pv, ea, q.x, q.y, q.z, q.w, pr, pq,
+                                                                   pscr[wid], prc, RST_PIX_COLD_HALF)
+                 : pix_tile_search<kPixChunk, 2>(bv, pv, ea, q.x, q.y, q.z, q.w, pr, pq, pscr[wid], prc);
+        if (pok) {
+          const float g = cert_bound(pr, prc);
+          const int pos = pr.pos[0];
+          nnq[ji] = make_float4(pq.x, pq.y, pq.z, i2f(pos | (g > 0.f ? kCertBit : 0)));
+          if (g > 0.f) cert[ji] = make_float4(q.x, q.y, q.z, g);
+          const float4 so = make_float4(0.f, 0.f, 0.f, i2f(cl_o[j]));  // (RefAcc: the original index)
+          Acc::add(v, bv, aa, u, so, q.x, q.y, q.z, pr.d[0], pos, pq);
+        }
+        fail = ea && !pok;
+        // cold: k_icp_fb starts from nnq's position
+        if (fail && (code & 0x40000000)) nnq[ji] = cl_c[j];
+#if RST_DIAG
+        const uint64_t pm = __ballot(pok);
+        if (lane == 0 && st->iter < kQTrace)
+          atomicAdd(&const_cast<IcpState*>(st)->diag[st->iter][2], __popcll(pm));
+#endif
+      }
+      // the failures to the queues, in point order
+      const uint64_t bm = __ballot(fail && !jfar), fm = __ballot(fail && jfar);
+      if (lane == 0) {
+        wq[0][wid] = __popcll(bm);
+        wq[1][wid] = __popcll(fm);
+      }
+      __syncthreads();
+      int before = 0, total = 0, beforef = 0, totalf = 0;
+#pragma unroll
+      for (int w = 0; w < kBS / kWave; ++w) {
+        before += w < wid ? wq[0][w] : 0;
+        total += wq[0][w];
+        beforef += w < wid ? wq[1][w] : 0;
+        totalf += wq[1][w];
+      }
+      if (fail && !jfar) qbuf[tb * (int64_t)kBS + before + __popcll(bm & lt)] = ji;
+      if (fail && jfar) qbuff[tb * (int64_t)kBS + beforef + __popcll(fm & lt)] = ji;
+      if (threadIdx.x == 0) {
+        qcnt[tb] = total;
+        qcntf[tb] = totalf;
+      }
+#if RST_DIAG
+      const uint64_t cm = __ballot(act && certified);
+      if (lane == 0 && st->iter < kQTrace) atomicAdd(&const_cast<IcpState*>(st)->path[st->iter][0], __popcll(cm));
+#endif
+      return;
+    }
+  }
+#endif
 #if RST_PIX_TILES
   // frame target (uniform): the pixel-window search, exact where it
   // applies.  (RST_PIX_ITERS limits it to a pair's first iterations, the
