@@ -38,6 +38,9 @@ int rst_debug_enable_seq_trace(rst_ctx* ctx, int enable);
  * stats: per chain superblock tries / hits, group tries / hits, leaf tries
  * / hits, serial blocks, walker clocks). */
 int rst_debug_seq_walk_stats(rst_ctx* ctx, int32_t* out, int32_t n);
+/* The context's reduction slab (first n doubles) as the last align left
+ * it: diagnostics builds write kernel clocks there (tools/nn_clock.py). */
+int rst_debug_slab(rst_ctx* ctx, double* out, int64_t n);
 int rst_debug_seq_trace(rst_ctx* ctx, float* out, int32_t n);
 
 /* RST_DIAG builds, per iteration of the last align call on ctx (first n <=

@@ -776,6 +776,15 @@ int rst_debug_icp_solve(rst_ctx* ctx, const rst_icp_opts* opts, int64_t n_total,
   return icp_debug_solve(ctx, opts, n_total, totals, smean, pose_inout, mu_inout, iter_inout);
 }
 
+int rst_debug_slab(rst_ctx* ctx, double* out, int64_t n) {
+  if (!ctx || !out || n < 0) return RST_E_ARG;
+  if (!ctx->d_slab || (size_t)n * sizeof(double) > ctx->slab_bytes) return RST_E_ARG;
+  RST_HIP(hipSetDevice(ctx->device));
+  RST_HIP(hipStreamSynchronize(ctx->stream));
+  RST_HIP(hipMemcpy(out, ctx->d_slab, sizeof(double) * n, hipMemcpyDeviceToHost));
+  return RST_OK;
+}
+
 int rst_debug_iter_diag(rst_ctx* ctx, int32_t* out, int32_t n) {
   if (!ctx || !out || n < 0) return RST_E_ARG;
   for (int i = 0; i < n && i < kQTrace; ++i)

@@ -75,6 +75,12 @@ constexpr int kPixChunk = RST_PIX_CHUNK;
 #ifndef RST_NN_COMPACT
 #define RST_NN_COMPACT 0  // RST_SUM_REF: k_icp_nn's pixel-window searches compacted over the workgroup (r04h: nn 35.0 -> 38.6 us steady, fb queues longer -- larger union boxes; 15.1k -> 14.5k it/s)
 #endif
+#ifndef RST_NN_CLK
+#define RST_NN_CLK 0  // diagnostics build: k_icp_nn's wave latencies (tools/nn_clock.py)
+#endif
+#ifndef RST_NN_CLK_ITER
+#define RST_NN_CLK_ITER 64
+#endif
 #ifndef RST_NN_MIN_WAVES
 #define RST_NN_MIN_WAVES 1  // k_icp_nn occupancy hint (waves per SIMD)
 #endif
@@ -83,6 +89,12 @@ constexpr int kPixChunk = RST_PIX_CHUNK;
 #endif
 #ifndef RST_PIX_COLD_ITERS
 #define RST_PIX_COLD_ITERS 4  // iterations [1, RST_PIX_COLD_ITERS) take the cold windows below (r04a: 4 vs 3, +1.6 %)
+#endif
+#ifndef RST_PIX_MAX_HALF_REF
+#define RST_PIX_MAX_HALF_REF 4.0f  // RST_SUM_REF's k_icp_nn window cap (level pixels; RST_PIX_MAX_HALF elsewhere)
+#endif
+#ifndef RST_PIX_CHUNKS
+#define RST_PIX_CHUNKS 2  // staging rounds per wave of the steady-state pixel windows
 #endif
 #ifndef RST_PIX_COLD_HALF
 #define RST_PIX_COLD_HALF 16.0f  // their half-width cap (level pixels)
@@ -611,6 +623,10 @@ __global__ __launch_bounds__(kBS, RST_NN_MIN_WAVES) void k_icp_nn(BvhView bv, Ad
 #if RST_PIX_TILES
   __shared__ PixScratch<kPixChunk> pscr[kBS / kWave];
 #endif
+#if RST_NN_CLK  // diagnostics build: per wave latency and phases (diag[it][0..3])
+  const uint64_t ck0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
+  uint64_t ck1 = 0, ck2 = 0;
+#endif
   const int tb = xcd_tile(blockIdx.x, gridDim.x);
   // the far queue: the second half of qbuf / qcnt
   int32_t* __restrict__ qbuff = qbuf + (int64_t)gridDim.x * kBS;
@@ -644,6 +660,9 @@ __global__ __launch_bounds__(kBS, RST_NN_MIN_WAVES) void k_icp_nn(BvhView bv, Ad
   }
   bool need = act && fin && !certified;
   const bool far = wb >= 0 && (wb & kFarBit);
+#if RST_NN_CLK
+  ck1 = __builtin_amdgcn_s_memtime();
+#endif
   const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
   // the search's seed: the last neighbour, or (cold: the pair's first
   // iteration) the better of the projective and the Morton seed
@@ -719,7 +738,7 @@ __global__ __launch_bounds__(kBS, RST_NN_MIN_WAVES) void k_icp_nn(BvhView bv, Ad
         const bool pok =
             cold ? pix_tile_search<kPixChunk, RST_PIX_COLD_CHUNKS>(bv, pv, ea, q.x, q.y, q.z, q.w, pr, pq,
                                                                    pscr[wid], prc, RST_PIX_COLD_HALF)
-                 : pix_tile_search<kPixChunk, 2>(bv, pv, ea, q.x, q.y, q.z, q.w, pr, pq, pscr[wid], prc);
+                 : pix_tile_search<kPixChunk, RST_PIX_CHUNKS>(bv, pv, ea, q.x, q.y, q.z, q.w, pr, pq, pscr[wid], prc);
         if (pok) {
           const float g = cert_bound(pr, prc);
           const int pos = pr.pos[0];
@@ -787,10 +806,19 @@ __global__ __launch_bounds__(kBS, RST_NN_MIN_WAVES) void k_icp_nn(BvhView bv, Ad
     // k_icp_fb's ball tiles answer that whole queue faster (r03u: 1.06 vs
     // 1.97 ms; iterations 1-2 0.65 -> 0.23-0.38 ms)
     const bool cold = st->iter >= 1 && st->iter < RST_PIX_COLD_ITERS;
+    // (the REF loop's steady-state windows capped smaller: the pass waits on
+    // its slowest wavefronts, whose few wide windows the queue's row
+    // searches take in parallel instead; r04j: nn 35 -> 25 us, same
+    // throughput.  The fp64 loop keeps the wider cap, r02's throughput best)
+    constexpr float kPixHalf = std::is_same<Acc, RefAcc>::value ? RST_PIX_MAX_HALF_REF : RST_PIX_MAX_HALF;
     const bool pok =
         cold ? pix_tile_search<kPixChunk, RST_PIX_COLD_CHUNKS>(bv, pv, need, px, py, pz, d0, pr, pq,
                                                                pscr[wid], prc, RST_PIX_COLD_HALF)
-             : pix_tile_search<kPixChunk, 2>(bv, pv, need, px, py, pz, d0, pr, pq, pscr[wid], prc);
+             : pix_tile_search<kPixChunk, RST_PIX_CHUNKS>(bv, pv, need, px, py, pz, d0, pr, pq, pscr[wid], prc,
+                                                                 kPixHalf);
+#if RST_NN_CLK
+    ck2 = __builtin_amdgcn_s_memtime();
+#endif
     if (pok) {
       const float g = cert_bound(pr, prc);
       const int pos = pr.pos[0];
@@ -841,6 +869,20 @@ __global__ __launch_bounds__(kBS, RST_NN_MIN_WAVES) void k_icp_nn(BvhView bv, Ad
   else if (act && !fin)  // no neighbour: the query's untouched outputs
     Acc::add(v, bv, aa, u, s, px, py, pz, FLT_MAX, -1, tq);
   if constexpr (Acc::kSums) block_sum_to_slab<Acc::NV, kBS>(v, lds, slab + (int64_t)tb * Acc::RS);
+#if RST_NN_CLK
+  // (iteration RST_NN_CLK_ITER only, per wave into the slab -- unused by
+  // RefAcc's nn pass: four clocks and the realtime start / end;
+  // rst_debug_slab reads it.  Same-address atomics from every wave would
+  // serialise and dominate the pass.)
+  if (lane == 0 && st->iter == RST_NN_CLK_ITER) {
+    const uint64_t ck3 = __builtin_amdgcn_s_memtime(), rt3 = __builtin_amdgcn_s_memrealtime();
+    int64_t* o = reinterpret_cast<int64_t*>(slab) + (int64_t)tb * 16 + wid * 4;
+    o[0] = (int64_t)rt0;
+    o[1] = (int64_t)rt3;
+    o[2] = (int64_t)(ck1 - ck0);
+    o[3] = (int64_t)((ck2 ? ck2 - ck1 : 0) | ((ck3 - ck0) << 32));
+  }
+#endif
 }
 
 // Kabsch solve (align_icp.cpp:139-151; SolveKabsch :58-69): fp64 SVD,
