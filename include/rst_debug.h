@@ -66,11 +66,14 @@ int rst_debug_query_nn_fallback(rst_ctx* ctx, const rst_target* tgt, const float
  * the rounding of `dst_mean += dst.GetPoint(j)` (align_icp.cpp:120). */
 int rst_debug_seq_sum4(rst_ctx* ctx, const float* xyzw, int64_t n, float out[4]);
 
-/* The same sums by either kernel: serial = 0 the loop's parallel exact
- * path (seqsum.hip: verified block / group / superblock maps, one walking
- * wavefront per component), serial = 1 the one-wavefront dependent chain
- * (k_seq_sum4); reps launches back to back, *ms (optional) = device time
- * per launch; stats (optional, parallel path, 64 int32) = 8 per component
+/* The same sums by either kernel: serial = 0 the loop's own choice by size
+ * (seqsum_enqueue: the one-wavefront replay k_sq_serial up to
+ * RST_SQ_SERIAL_MAX elements, else the parallel exact path -- verified
+ * block / group / superblock maps, one walking wavefront per component),
+ * 1 the older one-wavefront dependent chain (k_seq_sum4), 2 the map path
+ * at any size, 3 k_sq_serial at any size; reps launches back to back, *ms
+ * (optional) = device time per launch; stats (optional, map path, 64
+ * int32; zero when the replay ran) = 8 per component
  * of the last launch's walk: superblock tries / hits, group tries / hits,
  * block tries / hits, blocks added serially, walker clocks; stats[32] =
  * the map kernels' bound-check failure bits (0 = none); stats[33 + c] =

@@ -87,6 +87,9 @@ constexpr int kPixChunk = RST_PIX_CHUNK;
 #ifndef RST_SQ_FUSE_FRONT
 #define RST_SQ_FUSE_FRONT 0  // REF loop: the front kernel without the totals launch, the previous iteration's tile prefixes (r04b: front + totals 14.5 -> 13.3 us, but the walk +1 ms per pair: stale guesses in the first iterations)
 #endif
+#ifndef RST_SQ_FUSE_FROM
+#define RST_SQ_FUSE_FROM 0  // ... from this iteration on only (0: never; RST_SQ_FUSE_FROM env overrides), once the pose barely moves
+#endif
 #ifndef RST_PIX_COLD_ITERS
 #define RST_PIX_COLD_ITERS 4  // iterations [1, RST_PIX_COLD_ITERS) take the cold windows below (r04a: 4 vs 3, +1.6 %)
 #endif
@@ -1675,6 +1678,17 @@ int centroid_device(rst_ctx* ctx, const float4* d_pts, int64_t n, double* d_out)
 // when enqueued, RST_FALSE for the reference's early false (nothing
 // enqueued), or an error.
 // fallback grid (RST_FB_BLOCKS: tuning knob, <= kFbBlocks)
+// the first iteration whose sequential sums take the fused front (no
+// totals launch; RST_SQ_FUSE_FROM: tuning knob, <= 0 never)
+static int sq_fuse_from() {
+  static const int g = [] {
+    const char* e = getenv("RST_SQ_FUSE_FROM");
+    const int v = e ? atoi(e) : (RST_SQ_FUSE_FRONT ? 1 : RST_SQ_FUSE_FROM);
+    return v > 0 ? v : INT_MAX;
+  }();
+  return g;
+}
+
 static int fb_grid_size() {
   static const int g = [] {
     const char* e = getenv("RST_FB_BLOCKS");
@@ -1882,7 +1896,7 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
       const int nch_prev = it == 0 ? 0 : (it == opts.max_iter || ctx->seq_trace ? 4 : 3);
       int* sqstats = ctx->seq_trace && ctx->d_sqstats && it < kQTrace ? ctx->d_sqstats + 64 * it : nullptr;
       RST_CHECK(seqsum_enqueue(corrg, n_total, nch, sqws, ctx->d_state->seq, st, sqstats, 7, it,
-                               it > 0 && nch <= nch_prev && RST_SQ_FUSE_FRONT));
+                               it > 0 && it >= sq_fuse_from() && nch <= nch_prev));
       if (n_local > 0)
         k_cov_ref<<<kCovBlocks, kBS, 0, st>>>(srco, corr, n_local, n_total, ctx->d_state, slab2);
       k_reduce_solve<RefAcc><<<1, kRedBS, 0, st>>>(slab, 0, slab2, n_local > 0 ? kCovBlocks : 0, prm,

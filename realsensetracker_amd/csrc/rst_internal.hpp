@@ -239,7 +239,11 @@ int centroid_device(rst_ctx* ctx, const float4* d_pts, int64_t n,
                     double* d_out3);
 int seq_sum4_device(rst_ctx* ctx, const float4* d_x, int64_t n, float* d_out);
 // the same sums, parallel and bit-exact (seqsum.hip): out[c] for c < nch;
-// ws holds seqsum_bytes(n)
+// ws holds seqsum_bytes(n).  stages: bits 1 / 2 / 4 the map pipeline's
+// front / maps / walk; with all three, streams of <= RST_SQ_SERIAL_MAX
+// elements take the one-wavefront replay (k_sq_serial) instead, unless
+// kSqForceMaps; kSqForceSerial takes it at any size.
+constexpr int kSqForceSerial = 16, kSqForceMaps = 32;
 size_t seqsum_bytes(int64_t n);
 int seqsum_enqueue(const float4* d_x, int64_t n, int nch, void* ws, float* d_out,
                    hipStream_t st, int* d_stats = nullptr, int stages = 7, int iter = -1,

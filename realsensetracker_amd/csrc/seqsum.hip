@@ -130,6 +130,101 @@ __device__ double block_sum_global(const double* a, int cnt, double* lds) {
   return tot;
 }
 
+// ---- 0: small streams, the chains replayed ----------------------------------------
+// Below RST_SQ_SERIAL_MAX elements the map pipeline's five dependent
+// launches (~50 us of fixed latency however short the stream) cost more
+// than replaying the chains: lane c < 4 carries chain c through s = fl(s + x_i), i
+// ascending from +0 -- the reference's loop itself, so inf / NaN / subnormal
+// need no case analysis -- one dependent v_add_f32 per element.  The
+// wavefront only keeps it fed: tiles of 64 x kSerT float4 loaded coalesced
+// a tile ahead, transposed through LDS so lane c reads four of its values
+// per ds_read_b128, kSerG reads in flight ahead of the adds.  A tile's tail
+// past n is +0: s is never -0 (from +0, fl(a + b) = -0 needs a = b = -0),
+// so fl(s + 0) = s and the padded adds change no bit.
+constexpr int kSerT = 16;                   // float4 per lane per tile (1024 elements)
+constexpr int kSerRow = kSerT * kWave + 4;  // floats per chain row (+4: rows on distinct banks)
+constexpr int kSerG = 8;                    // ds_read_b128 per group (32 elements)
+// RST_SQ_SERIAL_MAX default.  A lone wavefront's dependent v_add_f32 costs
+// ~12 clocks (the ISA is 32 back-to-back adds per group): 5.0 ns an element
+// against the pipeline's ~53 us flat (r05a, tools/seq_serial_sweep.py:
+// 2k / 4k / 8k / 15k / 33k elements 13 / 23 / 43 / 77 / 163 us replayed vs
+// 64 / 50 / 55 / 53 / 53 us mapped) -- the callers' ~15k-point clouds stay
+// on the pipeline
+constexpr int kSerDefault = 8192;
+
+__device__ __forceinline__ void ser_load(const float4* __restrict__ x, int64_t n, int64_t base,
+                                         float4 (&v)[kSerT]) {
+#pragma unroll
+  for (int t = 0; t < kSerT; ++t) {
+    const int64_t i = base + (int64_t)t * kWave + threadIdx.x;
+    v[t] = i < n ? x[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+__device__ __forceinline__ void ser_group(const float* row, float4 (&q)[kSerG]) {
+#pragma unroll
+  for (int k = 0; k < kSerG; ++k) q[k] = *reinterpret_cast<const float4*>(row + 4 * k);
+}
+
+__device__ __forceinline__ void ser_add(const float4 (&q)[kSerG], float& s) {
+#pragma unroll
+  for (int k = 0; k < kSerG; ++k) {
+    s = s + q[k].x;
+    s = s + q[k].y;
+    s = s + q[k].z;
+    s = s + q[k].w;
+  }
+}
+
+// one tile: transpose, then lane c's chain over its first cnt values
+// (rounded up to a group: the rest are +0)
+__device__ __forceinline__ void ser_tile(const float4 (&v)[kSerT], int cnt, float* tile, float& s) {
+  const int lane = threadIdx.x;
+  __syncthreads();  // (the previous tile's reads are done)
+#pragma unroll
+  for (int t = 0; t < kSerT; ++t) {
+    tile[0 * kSerRow + t * kWave + lane] = v[t].x;
+    tile[1 * kSerRow + t * kWave + lane] = v[t].y;
+    tile[2 * kSerRow + t * kWave + lane] = v[t].z;
+    tile[3 * kSerRow + t * kWave + lane] = v[t].w;
+  }
+  __syncthreads();
+  if (lane < 4) {
+    const float* row = tile + lane * kSerRow;
+    constexpr int kGE = 4 * kSerG;  // elements per group
+    const int ng = (cnt + kGE - 1) / kGE;
+    float4 q[kSerG], r[kSerG];
+    ser_group(row, q);
+    int g = 0;
+    // two groups per trip: one group's reads in flight during the other's adds
+    for (; g + 2 <= ng; g += 2) {
+      ser_group(row + (g + 1) * kGE, r);
+      ser_add(q, s);
+      if (g + 2 < ng) ser_group(row + (g + 2) * kGE, q);
+      ser_add(r, s);
+    }
+    if (g < ng) ser_add(q, s);
+  }
+}
+
+__global__ __launch_bounds__(kWave) void k_sq_serial(const float4* __restrict__ x, int64_t n, int nch,
+                                                     float* __restrict__ out) {
+  __shared__ float4 tile4[kSerRow];  // 4 rows of kSerRow floats
+  float* tile = reinterpret_cast<float*>(tile4);
+  constexpr int64_t kT = (int64_t)kSerT * kWave;
+  float s = 0.0f;
+  float4 a[kSerT], b[kSerT];
+  ser_load(x, n, 0, a);
+  for (int64_t base = 0; base < n; base += 2 * kT) {
+    ser_load(x, n, base + kT, b);  // in flight during a's chain
+    ser_tile(a, (int)min<int64_t>(n - base, kT), tile, s);
+    if (base + kT >= n) break;
+    ser_load(x, n, base + 2 * kT, a);
+    ser_tile(b, (int)min<int64_t>(n - base - kT, kT), tile, s);
+  }
+  if ((int)threadIdx.x < nch) out[threadIdx.x] = s;
+}
+
 // ---- 1: SoA copy, window flags, fp64 totals --------------------------------------
 // One 1024-element quarter tile per workgroup, four consecutive elements
 // per thread (64 contiguous bytes: coalesced float4 loads, one float4 SoA
@@ -1141,6 +1236,16 @@ size_t seqsum_bytes(int64_t n) {
 // go to the iteration's parity buffer; fused (iter > 0, the same chains as
 // iteration iter - 1 summed on this workspace): no totals launch, the front
 // kernel takes the tile prefixes of iteration iter - 1.
+// the replay's ceiling (elements; RST_SQ_SERIAL_MAX: tuning knob, 0 = never)
+static int64_t serial_max() {
+  static const int64_t g = [] {
+    const char* e = getenv("RST_SQ_SERIAL_MAX");
+    const long long v = e ? atoll(e) : (long long)kSerDefault;
+    return (int64_t)(v < 0 ? 0 : v);
+  }();
+  return g;
+}
+
 int seqsum_enqueue(const float4* d_x, int64_t n, int nch, void* ws, float* d_out, hipStream_t st,
                    int* d_stats, int stages, int iter, bool fused) {
   if (nch < 1 || nch > 4 || n < 0) return RST_E_ARG;
@@ -1149,6 +1254,14 @@ int seqsum_enqueue(const float4* d_x, int64_t n, int nch, void* ws, float* d_out
     return RST_OK;
   }
   if (n > (int64_t)INT_MAX - 2 * kTile) return RST_E_ARG;
+  // small streams: one wavefront replays the chains (the whole sum, no stats)
+  const bool whole = (stages & 7) == 7;
+  if (whole && !(stages & kSqForceMaps) && ((stages & kSqForceSerial) || n <= serial_max())) {
+    k_sq_serial<<<1, kWave, 0, st>>>(d_x, n, nch, d_out);
+    RST_HIP(hipGetLastError());
+    return RST_OK;
+  }
+  stages &= 7;
   SqView v;
   sq_layout(v, n, nch, (char*)ws);
   v.stats = d_stats;

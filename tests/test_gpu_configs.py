@@ -157,11 +157,14 @@ def test_pyramid_720p_graphs(ctx, sum_mode):
     assert max(e) <= 1e-6, e  # gates 1e-4 / 2e-5 by contract; measured 0 (r03e)
 
 
-def test_callers_workload_ref_inloop(ctx):
+@pytest.mark.parametrize("voxel", [0.05, 0.1])
+def test_callers_workload_ref_inloop(ctx, voxel):
     """The reference callers' own sizes (rs_replay_app.cpp:229,246-251:
     RemoveNans, DownsampleVoxel 0.05 of both clouds, the 4-argument
-    AlignIcp3d 128): ~15k points, where the sequential sums take the
-    one-workgroup path -- every iteration's sums bit-exact again."""
+    AlignIcp3d 128): ~15k points, four superblocks of the map pipeline
+    per chain -- every iteration's sums bit-exact again; at 10 cm (~4k
+    points, the tracker's voxel, rs_tracker.cpp) the one-wavefront replay
+    k_sq_serial takes the sums instead, bit-exact the same way."""
     K = driver.intrinsics(640, 480)
     da, db, _ = driver.make_pair(driver.SyntheticScene(0), K, seed=10)
     # the recorded clouds keep every pixel, invalid ones at the origin
@@ -169,12 +172,13 @@ def test_callers_workload_ref_inloop(ctx):
     raw = [driver.unproject(d, K, keep_invalid=True) for d in (da, db)]
     for r in raw:
         r[::997] = np.nan
-    cur = A.DownsampleVoxel(A.RemoveNans(raw[1]), 0.05)
-    prv = A.DownsampleVoxel(A.RemoveNans(raw[0]), 0.05)
-    ocur = O.downsample_voxel(O.remove_nans(raw[1]), 0.05)
-    oprv = O.downsample_voxel(O.remove_nans(raw[0]), 0.05)
+    cur = A.DownsampleVoxel(A.RemoveNans(raw[1]), voxel)
+    prv = A.DownsampleVoxel(A.RemoveNans(raw[0]), voxel)
+    ocur = O.downsample_voxel(O.remove_nans(raw[1]), voxel)
+    oprv = O.downsample_voxel(O.remove_nans(raw[0]), voxel)
     assert np.array_equal(cur, ocur) and np.array_equal(prv, oprv)
-    assert 5_000 < len(cur) <= 16384
+    # 5 cm: above the replay's 8192 (the map pipeline); 10 cm: below it
+    assert (8192 < len(cur) <= 16384) if voxel == 0.05 else (1000 < len(cur) <= 8192), len(cur)
     hctx = A.get_context()
     _enable_seq_trace(hctx, True)
     try:

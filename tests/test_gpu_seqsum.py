@@ -56,11 +56,31 @@ def same(a, b):
 CASES = cases()
 
 
+PATHS = {"auto": 0, "maps": 2, "replay": 3}
+
+
+@pytest.mark.parametrize("path", sorted(PATHS))
 @pytest.mark.parametrize("name", sorted(CASES))
-def test_parallel_seq_sum_bitexact(ctx, name):
+def test_parallel_seq_sum_bitexact(ctx, name, path):
+    """Every edge case by both paths (the map pipeline and the one-wavefront
+    replay k_sq_serial, forced at any size) and by the size rule."""
     x = CASES[name]
-    got, _ = seq_sum(ctx, x)
-    assert same(got, want(x)), (name, got, want(x))
+    got, _ = seq_sum(ctx, x, serial=PATHS[path])
+    assert same(got, want(x)), (name, path, got, want(x))
+
+
+@pytest.mark.parametrize("n", [1, 31, 1023, 1024, 1025, 2047, 2048, 2049, 15_237, 40_000])
+def test_replay_tile_edges(ctx, n):
+    """k_sq_serial around its 1024-element tiles and 32-element groups (the
+    padded tail), with large-magnitude, cancelling and non-finite-free
+    chains: bit-exact against numpy's sequential float32 sums, and equal to
+    the map pipeline's."""
+    rng = np.random.default_rng(n)
+    x = (rng.standard_normal((n, 4)) * np.array([1e3, 1e-3, 1.0, 1e6])).astype(np.float32)
+    x[:, 2] -= np.float32(0.25)
+    a, _ = seq_sum(ctx, x, serial=3)
+    b, _ = seq_sum(ctx, x, serial=2)
+    assert same(a, want(x)) and same(b, want(x)), (n, a, b, want(x))
 
 
 def test_parallel_seq_sum_frames(ctx):
@@ -89,7 +109,24 @@ def test_parallel_matches_serial_kernel_and_is_faster(ctx):
     x = np.concatenate([p, (p * p).sum(1, keepdims=True)], 1).astype(np.float32)
     a, ms_par = seq_sum(ctx, x, serial=0, reps=20)
     b, ms_ser = seq_sum(ctx, x, serial=1, reps=3)
-    assert same(a, b)
+    c, ms_rep = seq_sum(ctx, x, serial=3, reps=3)
+    assert same(a, b) and same(a, c)
     print(f"\nseq sums of {len(x)} float4: parallel {ms_par * 1e3:.1f} us, "
-          f"serial {ms_ser * 1e3:.1f} us")
-    assert ms_par < ms_ser
+          f"serial {ms_ser * 1e3:.1f} us, replay {ms_rep * 1e3:.1f} us")
+    assert ms_par < ms_ser and ms_par < ms_rep
+
+
+def test_replay_chosen_where_faster(ctx):
+    """The size rule: at 4096 elements (below RST_SQ_SERIAL_MAX's 8192) the
+    replay, the product's choice there, is faster than the map pipeline
+    (measured 23 vs 50 us, r05a); at 640x480 sizes the map pipeline is (the
+    test above)."""
+    rng = np.random.default_rng(5)
+    x = rng.standard_normal((4096, 4)).astype(np.float32)
+    a, ms_auto = seq_sum(ctx, x, serial=0, reps=20)
+    b, ms_maps = seq_sum(ctx, x, serial=2, reps=20)
+    c, ms_rep = seq_sum(ctx, x, serial=3, reps=20)
+    assert same(a, want(x)) and same(b, a) and same(c, a)
+    print(f"\nseq sums of 4096 float4: auto {ms_auto * 1e3:.1f} us, maps {ms_maps * 1e3:.1f} us, "
+          f"replay {ms_rep * 1e3:.1f} us")
+    assert ms_rep < ms_maps
