@@ -26,6 +26,7 @@
 #include <algorithm>
 #include <climits>
 #include <cmath>
+#include <cstring>
 
 #include "rst_device.hpp"
 #include "rst_internal.hpp"
@@ -377,7 +378,13 @@ using namespace rst;
 
 namespace {
 
-// host-buffer entry points: upload, run `fn` on device buffers, download
+// host-buffer entry points: upload, run `fn` on device buffers, download --
+// both copies through the context's pinned staging buffer (as capi.hip's
+// uploads).  A copy straight from / to pageable memory leaves the pinning to
+// the runtime, which measured 20-28 ms on a frame not copied recently
+// (profiles/r05_callers_prof.txt: the first RemoveNans of each pair of the
+// callers' workload, 0.4 ms otherwise); a staged copy is a host memcpy plus
+// a pinned DMA every time.
 template <class Fn>
 int run_host(rst_ctx* ctx, const float* xyz, int64_t n, float* out, int64_t* n_out, Fn fn) {
   float *din = nullptr, *dout = nullptr;
@@ -385,16 +392,25 @@ int run_host(rst_ctx* ctx, const float* xyz, int64_t n, float* out, int64_t* n_o
   const size_t bytes = sizeof(float) * 3 * (size_t)std::max<int64_t>(n, 1);
   RST_CHECK(ctx_alloc(ctx, bytes, (void**)&din, &cin));
   int s = ctx_alloc(ctx, bytes, (void**)&dout, &cout);
-  if (s >= 0 && n > 0 &&
-      hipMemcpyAsync(din, xyz, sizeof(float) * 3 * n, hipMemcpyHostToDevice, ctx->stream) !=
-          hipSuccess)
-    s = RST_E_HIP;
-  if (s >= 0) s = fn(din, dout);
-  if (s >= 0 && *n_out > 0 &&
-      (hipMemcpyAsync(out, dout, sizeof(float) * 3 * (*n_out), hipMemcpyDeviceToHost,
-                      ctx->stream) != hipSuccess ||
-       hipStreamSynchronize(ctx->stream) != hipSuccess))
-    s = RST_E_HIP;
+  void* pin = nullptr;
+  if (s >= 0) s = ctx_pinned(ctx, bytes, &pin);
+  // the staging buffer may still feed an earlier async copy
+  if (s >= 0 && hipStreamSynchronize(ctx->stream) != hipSuccess) s = RST_E_HIP;
+  if (s >= 0 && n > 0) {
+    memcpy(pin, xyz, sizeof(float) * 3 * n);
+    if (hipMemcpyAsync(din, pin, sizeof(float) * 3 * n, hipMemcpyHostToDevice, ctx->stream) !=
+        hipSuccess)
+      s = RST_E_HIP;
+  }
+  if (s >= 0) s = fn(din, dout);  // (stream-ordered after the upload: pin is free again once it returns a count)
+  if (s >= 0 && *n_out > 0) {
+    if (hipMemcpyAsync(pin, dout, sizeof(float) * 3 * (*n_out), hipMemcpyDeviceToHost, ctx->stream) !=
+            hipSuccess ||
+        hipStreamSynchronize(ctx->stream) != hipSuccess)
+      s = RST_E_HIP;
+    else
+      memcpy(out, pin, sizeof(float) * 3 * (*n_out));
+  }
   hipStreamSynchronize(ctx->stream);
   ctx_release(ctx, din, cin);
   if (dout) ctx_release(ctx, dout, cout);
