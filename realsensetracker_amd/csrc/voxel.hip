@@ -588,10 +588,15 @@ int rst_accum_add(rst_accum* a, const float pose[16], const float* xyz, int64_t 
   float* d = nullptr;
   size_t c = 0;
   RST_CHECK(ctx_alloc(a->ctx, sizeof(float) * 3 * n, (void**)&d, &c));
-  int s = hipMemcpyAsync(d, xyz, sizeof(float) * 3 * n, hipMemcpyHostToDevice, a->ctx->stream) ==
-                  hipSuccess
-              ? RST_OK
-              : RST_E_HIP;
+  // staged through pinned memory (run_host above: no pageable-copy stall)
+  void* pin = nullptr;
+  int s = ctx_pinned(a->ctx, sizeof(float) * 3 * n, &pin);
+  if (s >= 0 && hipStreamSynchronize(a->ctx->stream) != hipSuccess) s = RST_E_HIP;
+  if (s >= 0) {
+    memcpy(pin, xyz, sizeof(float) * 3 * n);
+    if (hipMemcpyAsync(d, pin, sizeof(float) * 3 * n, hipMemcpyHostToDevice, a->ctx->stream) != hipSuccess)
+      s = RST_E_HIP;
+  }
   if (s >= 0) s = accum_add_device(a, pose, d, n);
   hipStreamSynchronize(a->ctx->stream);
   ctx_release(a->ctx, d, c);
@@ -608,9 +613,12 @@ int rst_accum_extract(rst_accum* a, float* out, int64_t* n_out) {
   if (!a || !n_out || (a->count > 0 && !out)) return RST_E_ARG;
   RST_HIP(hipSetDevice(a->ctx->device));
   if (a->count > 0) {
-    RST_HIP(hipMemcpyAsync(out, a->list, sizeof(float) * 3 * a->count, hipMemcpyDeviceToHost,
+    void* pin = nullptr;
+    RST_CHECK(ctx_pinned(a->ctx, sizeof(float) * 3 * a->count, &pin));
+    RST_HIP(hipMemcpyAsync(pin, a->list, sizeof(float) * 3 * a->count, hipMemcpyDeviceToHost,
                            a->ctx->stream));
     RST_HIP(hipStreamSynchronize(a->ctx->stream));
+    memcpy(out, pin, sizeof(float) * 3 * a->count);
   }
   *n_out = a->count;
   return RST_OK;
