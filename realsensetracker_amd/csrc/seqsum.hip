@@ -478,21 +478,37 @@ __global__ __launch_bounds__(kFrontT) void k_sq_front(SqView v, const float4* __
   if (tid == 0) v.tinc[(int64_t)c * v.nk + t] = itot;
 }
 
-// ---- 3a: leaf maps ----------------------------------------------------------------
-// One workgroup per 64 blocks of a tile and chain, one lane per (block,
-// candidate): a block's 4 candidate runs side by side in a lane quad.  The
-// guess of a block's start: the fp64 prefix of the float32 increments (the
-// tiles' totals before its tile, plus its prefix within the tile,
-// k_sq_front).  (r03: the leaves were a phase of the superblock workgroup --
-// 1024 threads, half of them idle on a 256-block superblock, one workgroup
-// per CU; 292 of them on 256 CUs ran in two rounds.  Alone the leaves fill
-// every CU.)
-constexpr int kLeafT = 256;
-constexpr int kLeafB = kLeafT / kLeafR;             // 64 blocks per workgroup
-constexpr int kLeafWg = kBlocksPerTile / kLeafB;    // 4 per tile
-constexpr int kLeafX = kLeafB * kW + 2 * kW;        // staged elements (the last block runs past)
-static_assert(kBlocksPerTile % kLeafB == 0, "leaf workgroups per tile");
-static_assert(sizeof(Leaf) == 64, "a leaf map is four int4 (k_sq_maps reads it so)");
+// ---- 3: leaf, group and superblock maps, one workgroup per superblock -------------
+// One workgroup per (superblock, chain) builds every map of the superblock:
+//   leaves      one lane per block (<= 511 blocks: one round of 512 lanes) runs
+//               candidate 0 -- the block's guess G -- through the block's
+//               elements (staged in LDS).  When that run rounds on no grid
+//               coarser than G's own (its lattice need <= e0: m = 0), the map
+//               needs no other candidate: any start on G's grid is G + d, d a
+//               multiple of every step's grid, and the run's window says which
+//               d keep every step's rounding.  That is ~99.7% of an ICP loop's
+//               blocks (tools/seqsum_incr_sim.py's leaf histogram: m = 0
+//               1,295,842 / m = 1 3,751 / m = 2 296 / exact-only 111 over 24
+//               iterations at 640x480); the rest list their candidates 1..3 in
+//               LDS and run them in one extra round, then m is the largest need
+//               over the four runs as before.  (r05: four lanes per block,
+//               every block, in a kernel of its own -- 5.3M VALU instructions
+//               an iteration, three quarters of them for entries m = 0 drops.)
+//   groups      lanes (group, candidate) listed compactly: every group's
+//               candidate 0, then the candidates 1..R-1 of groups whose
+//               lattice needs them (97.7% need none), composed through the
+//               group's leaf maps from LDS;
+//   superblock  lanes r < R (R = 1 for 87% of superblocks, 2 for 11%)
+//               composed through the group maps.
+// Every map is a valid statement about its own runs whatever the guess (a
+// wrong guess only costs hits), so the walk's results never depend on this
+// kernel's choices.  Leaf and group maps go to global memory for the walk's
+// descents.
+constexpr int kBuildT = 512;
+static_assert(kBuildT >= kMaxSbBlocks + 1 && kBuildT >= kMaxSbGroups * kGroupR && kBuildT % kWave == 0,
+              "map workgroup size");
+static_assert(sizeof(Leaf) == 64, "a leaf map is four int4");
+constexpr int kXPad = kMaxSbElems + kMaxSbElems / kW + 2 * kW;  // padded staging (see xp)
 
 // A composite lane's step through a child map, without branches (the
 // lanes of a wavefront take different cases in the same step; a chain of
@@ -536,84 +552,57 @@ __device__ __forceinline__ float cand(float G, int e0, int r) {
   return (float)((double)G + ldexp((double)r, e0));
 }
 
-__global__ __launch_bounds__(kLeafT) void k_sq_leaves(SqView v) {
-  __shared__ float xs[kLeafX];
-  __shared__ double lds[kLeafT / kWave + 1];
-  const int t = blockIdx.x / kLeafWg, c = blockIdx.y;
-  const int tid = threadIdx.x, lane = tid & (kWave - 1), r = tid & (kLeafR - 1);
-  const int b0 = t * kBlocksPerTile + (blockIdx.x % kLeafWg) * kLeafB;
-  const int b = b0 + tid / kLeafR;
-  const bool act = b < v.nb;
-  const int* bsg = v.bs + (int64_t)c * (v.nb + 1);
-  const float* X = v.soa + (int64_t)c * v.ns;
-  // (in flight together: the block's bounds and prefix, the elements, the tiles' totals)
-  const int s0 = act ? bsg[b] : 0, s1 = act ? bsg[b + 1] : 0;
-  const double iv = act ? v.ipre[(int64_t)c * v.nb + b] : 0.0;
-  const int64_t x0 = (int64_t)b0 * kW;  // the first block's window: every start is at or after it
-  for (int i = tid; i < kLeafX; i += kLeafT) xs[i] = x0 + i < v.n ? X[x0 + i] : 0.0f;
-  const double base = block_sum_global<kLeafT>(v.tinc + (int64_t)c * v.nk, t, lds);  // (synchronises)
-  Run p;
-  float G = 0.0f;
-  int e0 = -149;
-  if (act) {
-    G = candidate_base(b == 0 ? 0.0f : (float)(base + iv), kLeafR);
-    e0 = grid_exp(G);
-    run_init(p, cand(G, e0, r));
-    int a0 = (int)(s0 - x0), a1 = (int)(s1 - x0);
-    if (a0 < 0 || a1 > kLeafX || a1 - a0 < 1 || a1 - a0 > 2 * kW - 1) {
-      atomicOr(v.err, 32);
-      p.opaque = true;
-      a0 = a1 = 0;
-    }
-    // (the elements in registers first: the run's chain waits on no LDS read)
-    float xr[2 * kW - 1];
+// staged element a of the superblock at a + a / 16: lane j's block starts
+// near 16 j, so the lanes of a step read 17 words apart -- distinct banks
+// (r05: unpadded, stride 16, 3.3 conflicts per LDS instruction)
+__device__ __forceinline__ int xp(int a) { return a + (a >> 4); }
+
+struct BuildLds {
+  float x[kXPad];
+  Leaf lf[kMaxSbBlocks];
+  GroupMap gm[kMaxSbGroups];
+  int sbs[kMaxSbBlocks + 1];   // block starts, relative to the superblock's first element
+  int sgs[kMaxSbGroups + 1];   // group starts, relative to its first block
+  int xneed[kMaxSbBlocks][kLeafR - 1];  // the extra candidates' lattice needs
+  int list[kBuildT];           // extra leaf candidates (block << 2 | r), then (group << 4 | r)
+  int nlist;
+  int bad;
+  double base[2];              // fp64 increments of the tiles before the superblock's first
+                               // tile and before the next
+};
+
+// one monitored run of block bl from candidate r (the elements from LDS into
+// registers first: the run's chain waits on no LDS read), at most `wmax`
+// steps (the wavefront's longest block, uniform)
+__device__ __forceinline__ void leaf_run(Run& p, const BuildLds& W, int a0, int len, int wmax, float G, int e0,
+                                         int r) {
+  run_init(p, cand(G, e0, r));
+  float xr[2 * kW - 1];
 #pragma unroll
-    for (int i = 0; i < 2 * kW - 1; ++i) xr[i] = xs[min(a0 + i, kLeafX - 1)];
+  for (int i = 0; i < 2 * kW - 1; ++i) xr[i] = W.x[xp(min(a0 + i, kMaxSbElems - 1))];
 #pragma unroll
-    for (int i = 0; i < 2 * kW - 1; ++i)
-      if (i < a1 - a0) run_step(p, xr[i], e0);
-  } else {
-    run_init(p, 0.0f);
+  for (int i = 0; i < 2 * kW - 1; ++i) {
+    if (i >= wmax) break;
+    if (i < len) run_step(p, xr[i], e0);
   }
-  // the block's lattice: the largest need over its 4 runs
-  int need = p.need;
-  need = max(need, __shfl_xor(need, 1, kWave));
-  need = max(need, __shfl_xor(need, 2, kWave));
-  const bool op0 = __shfl(p.opaque ? 1 : 0, lane & ~(kLeafR - 1), kWave) != 0;
-  if (!act) return;
-  const int mneed = need == kNoNeed ? 0 : max(0, need - e0);
-  const bool exact_only = mneed > kLeafM;
-  const int m = exact_only ? 0 : mneed;
-  Leaf& o = v.leaf[(int64_t)c * v.nb + b];
-  if (r == 0) o.h = MapHdr{G, e0, m, op0 ? kOpaque : 0};
+}
+
+__device__ __forceinline__ MapEnt leaf_ent(const Run& p, int e0) {
   MapEnt en;
   en.E = p.s;
   en.LOu = lo_units((double)p.lo, e0);
   en.HIu = hi_units((double)p.hi, e0);
-  if (p.opaque || r >= (1 << m)) {
+  if (p.opaque) {
     en.LOu = 1;
     en.HIu = 0;
-  } else if (exact_only) {
-    en.LOu = max(en.LOu, 0);
-    en.HIu = min(en.HIu, 0);
   }
-  o.e[r] = en;
+  return en;
 }
 
-// ---- 3b: group and superblock maps ------------------------------------------------
-// One workgroup per (superblock, chain): its leaf maps staged in LDS, then
-// lanes (group, residue) compose each group's leaves for up to 16
-// candidates, lanes 0..63 the superblock's groups for up to 64.
-constexpr int kMapT = 512;
-static_assert(kMapT >= kMaxSbGroups * kGroupR && kMapT % kWave == 0, "map workgroup size");
-
-__global__ __launch_bounds__(kMapT) void k_sq_maps(SqView v) {
-  __shared__ Leaf lf[kMaxSbBlocks];
-  __shared__ GroupMap gm[kMaxSbGroups];
-  __shared__ int sgs[kMaxSbGroups + 1];
-  __shared__ int sbad;
+__global__ __launch_bounds__(kBuildT) void k_sq_build(SqView v) {
+  __shared__ BuildLds W;
   const int k = blockIdx.x, c = blockIdx.y;
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & (kWave - 1);
   long long* clk = v.clk + ((int64_t)c * v.nk + k) * 8;
   if (tid == 0) clk[0] = (long long)__builtin_amdgcn_s_memtime();
   const int* bsg = v.bs + (int64_t)c * (v.nb + 1);
@@ -636,152 +625,266 @@ __global__ __launch_bounds__(kMapT) void k_sq_maps(SqView v) {
     if (tid == 0) atomicOr(v.err, 1);
     return;
   }
-  const int ngr = gb - ga, nblk = bb - ba;
-  if (tid == 0) sbad = 0;
+  const int ngr = gb - ga, nblk = bb - ba, nel = eb - ea;
+  const float* X = v.soa + (int64_t)c * v.ns;
+  // (in flight together: the elements, the block's bounds and prefix)
   {
-    // the leaves (16 B pieces, all in flight before the stores)
-    constexpr int kP = sizeof(Leaf) / 16, kJ = (kMaxSbBlocks * kP + kMapT - 1) / kMapT;
-    const int4* src = reinterpret_cast<const int4*>(v.leaf + (int64_t)c * v.nb + ba);
-    int4 tv[kJ];
+    constexpr int kJ = (kMaxSbElems + kBuildT - 1) / kBuildT;
+    float tv[kJ];
 #pragma unroll
-    for (int j = 0; j < kJ; ++j) tv[j] = tid + j * kMapT < nblk * kP ? src[tid + j * kMapT] : int4{};
+    for (int j = 0; j < kJ; ++j) tv[j] = tid + j * kBuildT < nel ? X[ea + tid + j * kBuildT] : 0.0f;
 #pragma unroll
     for (int j = 0; j < kJ; ++j)
-      if (tid + j * kMapT < nblk * kP) reinterpret_cast<int4*>(lf)[tid + j * kMapT] = tv[j];
+      if (tid + j * kBuildT < nel) W.x[xp(tid + j * kBuildT)] = tv[j];
   }
-  for (int i = tid; i <= ngr; i += kMapT) sgs[i] = gsg[ga + i] - ba;
+  const bool act = tid < nblk;
+  const int b = ba + tid;
+  const double iv = act ? v.ipre[(int64_t)c * v.nb + b] : 0.0;
+  if (tid <= nblk) W.sbs[tid] = bsg[ba + tid] - ea;
+  if (tid <= ngr) W.sgs[tid] = gsg[ga + tid] - ba;
+  if (tid == 0) {
+    W.nlist = 0;
+    W.bad = 0;
+  }
+  if (tid < kWave) {  // the tiles' increments before tile k (fixed order)
+    const double* ti = v.tinc + (int64_t)c * v.nk;
+    double s = 0.0;
+    for (int i = lane; i < k; i += kWave) s += ti[i];
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, kWave);
+    if (lane == 0) {
+      W.base[0] = s;
+      W.base[1] = s + (k < v.nk ? ti[k] : 0.0);
+    }
+  }
   __syncthreads();
   if (tid == 0) clk[1] = (long long)__builtin_amdgcn_s_memtime();
-  // -- groups: lane (group, residue), up to 16 residues
-  GroupMap* grpg = v.grp + (int64_t)c * v.ng;
+  // -- leaves: candidate 0 per block
+  Run p;
+  float G = 0.0f;
+  int e0 = -149, a0 = 0, len = 0;
+  bool more = false;
   {
-    const int gi = tid / kGroupR, r = tid % kGroupR;
-    const int c0 = gi < ngr ? sgs[gi] : 0, c1 = gi < ngr ? sgs[gi + 1] : 0;
-    const bool gok = c0 >= 0 && c1 > c0 && c1 <= nblk && c1 - c0 <= 2 * kGW - 1;
-    if (gi < ngr && !gok) {
-      atomicOr(v.err, 2);
-      sbad = 1;
+    if (act) {
+      a0 = W.sbs[tid];
+      len = W.sbs[tid + 1] - a0;
+      if (a0 < 0 || len < 1 || len > 2 * kW - 1 || a0 + len > nel) {
+        atomicOr(v.err, 32);
+        a0 = len = 0;
+      }
+      // a superblock's blocks lie in tile k and tile k + 1
+      const double base = (b / kBlocksPerTile) == k ? W.base[0] : W.base[1];
+      G = candidate_base(b == 0 ? 0.0f : (float)(base + iv), kLeafR);
+      e0 = grid_exp(G);
     }
-    if (gi < ngr && gok) {
-      // lattice over the children
-      const MapHdr h0 = lf[c0].h;
-      int lat = h0.e0 + h0.m;
-      for (int j = c0 + 1; j < c1; ++j) {
-        const int4 hj = *reinterpret_cast<const int4*>(&lf[j].h);  // (one read, no branch)
-        lat = (hj.w & kOpaque) ? lat : max(lat, hj.y + hj.z);
-      }
-      if (tid == 0) clk[2] = (long long)__builtin_amdgcn_s_memtime();
-      int m = max(0, lat - h0.e0);
-      const bool exact_only = m > kGroupM;
-      if (exact_only) m = 0;
-      const int R = 1 << m;
-      const float G = candidate_base(h0.G, R);
-      const int e0 = grid_exp(G);
-      GroupMap& o = gm[gi];
-      if (r == 0) {
-        o.h.G = G;
-        o.h.e0 = e0;
-        o.h.m = m;
-        o.h.flags = 0;
-      }
-      MapEnt en;
-      en.E = 0.0f;
-      en.LOu = 1;
-      en.HIu = 0;
-      if (r < R) {
-        float x = cand(G, e0, r);
-        double clo = -INFINITY, chi = INFINITY;
-        bool ok = true;
-        // (leaf j + 1 in flight while leaf j is applied; its entry picked
-        // from registers: no LDS trip in the chain)
-        // (as four int4: a select between struct members would go through
-        // the stack)
-        const int4* lq = reinterpret_cast<const int4*>(lf);
-        int4 q0 = lq[4 * c0], q1 = lq[4 * c0 + 1], q2 = lq[4 * c0 + 2], q3 = lq[4 * c0 + 3];
-        for (int j = c0; j < c1; ++j) {
-          const int jn = 4 * min(j + 1, c1 - 1);
-          const int4 n0 = lq[jn], n1 = lq[jn + 1], n2 = lq[jn + 2], n3 = lq[jn + 3];
-          const MapHdr h{__int_as_float(q0.x), q0.y, q0.z, q0.w};
-          const int kq = comp_off(x, h, kLeafM, ok);
-          const int rr = kq & ((1 << (ok ? h.m : 0)) - 1);  // (m <= kLeafM when ok)
-          // (selects on the residue's bits: a chain of rr == i tests became a
-          // switch, i.e. branches)
-          const bool r0 = (rr & 1) != 0, r1 = (rr & 2) != 0;
-          MapEnt en;
-          en.E = __int_as_float(r1 ? (r0 ? q3.y : q2.z) : (r0 ? q1.w : q1.x));
-          en.LOu = r1 ? (r0 ? q3.z : q2.w) : (r0 ? q2.x : q1.y);
-          en.HIu = r1 ? (r0 ? q3.w : q3.x) : (r0 ? q2.y : q1.z);
-          comp_apply(x, clo, chi, ok, h, kq, en);
-          q0 = n0;
-          q1 = n1;
-          q2 = n2;
-          q3 = n3;
-        }
-        if (tid == 0) clk[3] = (long long)__builtin_amdgcn_s_memtime();
-        if (ok) {
-          if (exact_only) {
-            clo = fmax(clo, 0.0);
-            chi = fmin(chi, 0.0);
-          }
-          en.E = x;
-          en.LOu = lo_units(clo, e0);
-          en.HIu = hi_units(chi, e0);
-        }
-      }
-      o.e[r] = en;
+    // the wavefront's longest block bounds the unrolled steps
+    int wl = len;
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) wl = max(wl, __shfl_xor(wl, o, kWave));
+    const int wmax = __builtin_amdgcn_readfirstlane(wl);
+    if (wmax > 0) {
+      leaf_run(p, W, a0, len, wmax, G, e0, 0);
+    } else {
+      run_init(p, 0.0f);
+    }
+    if (act && len == 0) p.opaque = true;  // (a bad block: no map)
+    const int m0 = p.need == kNoNeed ? 0 : max(0, p.need - e0);
+    more = act && !p.opaque && m0 >= 1 && m0 <= kLeafM;
+    if (more) {
+      const int at = atomicAdd(&W.nlist, kLeafR - 1);
+#pragma unroll
+      for (int r = 1; r < kLeafR; ++r) W.list[at + r - 1] = tid << 2 | r;
     }
   }
   __syncthreads();
-  for (int i = tid; i < ngr * (int)(sizeof(GroupMap) / 4); i += kMapT)
-    reinterpret_cast<int*>(grpg + ga)[i] = reinterpret_cast<const int*>(gm)[i];
-  if (tid == 0) clk[4] = (long long)__builtin_amdgcn_s_memtime();
-  // -- the superblock: lanes = residues, up to 64
-  if (tid == 0) {
-    SbMap* o = v.sbm + (int64_t)c * v.nk + k;
-    o->ga = ga;
-    o->gb = gb;
-    o->ba = ba;
-    o->bb = bb;
-    o->ea = ea;
-    o->eb = eb;
+  {
+    // the listed extra candidates, one lane each (rare; uniform skip)
+    const int nl = W.nlist;
+    for (int j0 = 0; j0 < nl; j0 += kBuildT) {
+      const int j = j0 + tid;
+      const int code = j < nl ? W.list[j] : 0;
+      const int bl = code >> 2, r = code & 3;
+      const int xa = j < nl ? W.sbs[bl] : 0, xl = j < nl ? W.sbs[bl + 1] - xa : 0;
+      const int xb = ba + bl;
+      const double base = (xb / kBlocksPerTile) == k ? W.base[0] : W.base[1];
+      const float xG = j < nl ? candidate_base(xb == 0 ? 0.0f : (float)(base + v.ipre[(int64_t)c * v.nb + xb]),
+                                               kLeafR)
+                              : 0.0f;
+      const int xe0 = grid_exp(xG);
+      int wl = xl;
+#pragma unroll
+      for (int o = kWave / 2; o > 0; o >>= 1) wl = max(wl, __shfl_xor(wl, o, kWave));
+      const int wmax = __builtin_amdgcn_readfirstlane(wl);
+      if (wmax > 0) {
+        Run q;
+        leaf_run(q, W, xa, xl, wmax, xG, xe0, r);
+        if (j < nl) {
+          W.lf[bl].e[r] = leaf_ent(q, xe0);
+          W.xneed[bl][r - 1] = q.need;
+        }
+      }
+    }
   }
-  if (tid < kWave && sbad) {
-    SbMap* o = v.sbm + (int64_t)c * v.nk + k;
-    if (tid == 0) o->h.flags = kOpaque;
+  __syncthreads();
+  if (act) {
+    int need = p.need;
+    if (more)
+#pragma unroll
+      for (int r = 1; r < kLeafR; ++r) need = max(need, W.xneed[tid][r - 1]);
+    const int mneed = need == kNoNeed ? 0 : max(0, need - e0);
+    const bool exact_only = mneed > kLeafM;
+    const int m = exact_only ? 0 : mneed;
+    Leaf o;
+    o.h = MapHdr{G, e0, m, p.opaque ? kOpaque : 0};
+    o.e[0] = leaf_ent(p, e0);
+#pragma unroll
+    for (int r = 1; r < kLeafR; ++r) o.e[r] = more ? W.lf[tid].e[r] : MapEnt{0.0f, 1, 0};
+#pragma unroll
+    for (int r = 0; r < kLeafR; ++r) {
+      if (r >= (1 << m)) {
+        o.e[r].LOu = 1;
+        o.e[r].HIu = 0;
+      } else if (exact_only) {
+        o.e[r].LOu = max(o.e[r].LOu, 0);
+        o.e[r].HIu = min(o.e[r].HIu, 0);
+      }
+    }
+    W.lf[tid] = o;
+    v.leaf[(int64_t)c * v.nb + b] = o;
+  }
+  if (tid == 0) W.nlist = ngr;  // the group list: every group's candidate 0 first
+  __syncthreads();
+  if (tid == 0) clk[2] = (long long)__builtin_amdgcn_s_memtime();
+  // -- groups: the lattice (lane per group), then lanes (group, candidate)
+  if (tid < ngr) {
+    const int gi = tid;
+    const int c0 = W.sgs[gi], c1 = W.sgs[gi + 1];
+    const bool gok = c0 >= 0 && c1 > c0 && c1 <= nblk && c1 - c0 <= 2 * kGW - 1;
+    GroupMap& o = W.gm[gi];
+    int R = 1;
+    if (!gok) {
+      atomicOr(v.err, 2);
+      W.bad = 1;
+      o.h = MapHdr{0.0f, 0, 0, kOpaque};
+    } else {
+      const MapHdr h0 = W.lf[c0].h;
+      int lat = h0.e0 + h0.m;
+      for (int j = c0 + 1; j < c1; ++j) {
+        const int4 hj = *reinterpret_cast<const int4*>(&W.lf[j].h);  // (one read, no branch)
+        lat = (hj.w & kOpaque) ? lat : max(lat, hj.y + hj.z);
+      }
+      int m = max(0, lat - h0.e0);
+      const bool exact_only = m > kGroupM;  // (the windows clamped to 0 below)
+      if (exact_only) m = 0;
+      R = 1 << m;
+      const float Gg = candidate_base(h0.G, R);
+      o.h = MapHdr{Gg, grid_exp(Gg), m, 0};
+      o.pad[0] = exact_only ? 1 : 0;
+    }
+    for (int r = 0; r < kGroupR; ++r) o.e[r] = MapEnt{0.0f, 1, 0};
+    if (R > 1) {
+      const int at = atomicAdd(&W.nlist, R - 1);
+      for (int r = 1; r < R; ++r) W.list[at + r - 1] = gi << 4 | r;
+    }
+  }
+  __syncthreads();
+  {
+    const int nl = W.nlist;  // <= 31 x 16 <= kBuildT
+    const int j = tid;
+    if (j - lane < nl) {  // (uniform per wavefront: waves past the list skip)
+      const bool ea_ = j < nl;
+      const int code = !ea_ ? 0 : (j < ngr ? j << 4 : W.list[j]);
+      const int gi = code >> 4, r = code & (kGroupR - 1);
+      const int c0 = W.sgs[gi], c1 = W.sgs[gi + 1];
+      const bool gok = ea_ && c0 >= 0 && c1 > c0 && c1 <= nblk && c1 - c0 <= 2 * kGW - 1;
+      const MapHdr gh = W.gm[gi].h;
+      const bool exact_only = W.gm[gi].pad[0] != 0;  // (a lattice beyond kGroupM)
+      float x = cand(gh.G, gh.e0, r);
+      double clo = -INFINITY, chi = INFINITY;
+      bool ok = gok && !(gh.flags & kOpaque);
+      // (leaf j + 1 in flight while leaf j is applied; its entry picked
+      // from registers: no LDS trip in the chain)
+      // (as four int4: a select between struct members would go through
+      // the stack)
+      const int4* lq = reinterpret_cast<const int4*>(W.lf);
+      const int cc0 = gok ? c0 : 0, cc1 = gok ? c1 : 1;
+      int4 q0 = lq[4 * cc0], q1 = lq[4 * cc0 + 1], q2 = lq[4 * cc0 + 2], q3 = lq[4 * cc0 + 3];
+      int nst = cc1 - cc0;
+#pragma unroll
+      for (int o = kWave / 2; o > 0; o >>= 1) nst = max(nst, __shfl_xor(nst, o, kWave));
+      nst = __builtin_amdgcn_readfirstlane(nst);
+      for (int s = 0; s < nst; ++s) {
+        const int jl = cc0 + s;
+        const int jn = 4 * min(jl + 1, cc1 - 1);
+        const int4 n0 = lq[jn], n1 = lq[jn + 1], n2 = lq[jn + 2], n3 = lq[jn + 3];
+        const MapHdr h{__int_as_float(q0.x), q0.y, q0.z, q0.w};
+        bool okj = ok && jl < cc1;
+        const int kq = comp_off(x, h, kLeafM, okj);
+        const int rr = kq & ((1 << (okj ? h.m : 0)) - 1);  // (m <= kLeafM when ok)
+        // (selects on the residue's bits: a chain of rr == i tests became a
+        // switch, i.e. branches)
+        const bool r0 = (rr & 1) != 0, r1 = (rr & 2) != 0;
+        MapEnt en;
+        en.E = __int_as_float(r1 ? (r0 ? q3.y : q2.z) : (r0 ? q1.w : q1.x));
+        en.LOu = r1 ? (r0 ? q3.z : q2.w) : (r0 ? q2.x : q1.y);
+        en.HIu = r1 ? (r0 ? q3.w : q3.x) : (r0 ? q2.y : q1.z);
+        comp_apply(x, clo, chi, okj, h, kq, en);
+        ok = jl < cc1 ? okj : ok;
+        q0 = n0;
+        q1 = n1;
+        q2 = n2;
+        q3 = n3;
+      }
+      if (ea_ && ok) {
+        if (exact_only) {
+          clo = fmax(clo, 0.0);
+          chi = fmin(chi, 0.0);
+        }
+        W.gm[gi].e[r] = MapEnt{x, lo_units(clo, gh.e0), hi_units(chi, gh.e0)};
+      }
+    }
+  }
+  __syncthreads();
+  if (tid == 0) clk[3] = (long long)__builtin_amdgcn_s_memtime();
+  GroupMap* grpg = v.grp + (int64_t)c * v.ng;
+  for (int i = tid; i < ngr * (int)(sizeof(GroupMap) / 4); i += kBuildT)
+    reinterpret_cast<int*>(grpg + ga)[i] = reinterpret_cast<const int*>(W.gm)[i];
+  if (tid == 0) clk[4] = (long long)__builtin_amdgcn_s_memtime();
+  // -- the superblock: lanes = candidates, up to 64
+  SbMap* so = v.sbm + (int64_t)c * v.nk + k;
+  if (tid == 0) {
+    so->ga = ga;
+    so->gb = gb;
+    so->ba = ba;
+    so->bb = bb;
+    so->ea = ea;
+    so->eb = eb;
+  }
+  if (tid < kWave && W.bad) {
+    if (tid == 0) so->h.flags = kOpaque;
   } else if (tid < kWave) {
     const int r = tid;
-    const MapHdr h0 = gm[0].h;
+    const MapHdr h0 = W.gm[0].h;
     int lat = h0.e0 + h0.m;
-    for (int j = 1; j < ngr; ++j) lat = max(lat, gm[j].h.e0 + gm[j].h.m);
+    for (int j = 1; j < ngr; ++j) lat = max(lat, W.gm[j].h.e0 + W.gm[j].h.m);
     int m = max(0, lat - h0.e0);
     const bool exact_only = m > kSbM;
     if (exact_only) m = 0;
     const int R = 1 << m;
-    const float G = candidate_base(h0.G, R);
-    const int e0 = grid_exp(G);
-    SbMap* o = v.sbm + (int64_t)c * v.nk + k;
-    if (r == 0) {
-      MapHdr h;
-      h.G = G;
-      h.e0 = e0;
-      h.m = m;
-      h.flags = 0;
-      o->h = h;
-    }
-    MapEnt en;
-    en.E = 0.0f;
-    en.LOu = 1;
-    en.HIu = 0;
+    const float Gs = candidate_base(h0.G, R);
+    const int se0 = grid_exp(Gs);
+    if (r == 0) so->h = MapHdr{Gs, se0, m, 0};
+    MapEnt en{0.0f, 1, 0};
     if (r < R) {
-      float x = cand(G, e0, r);
+      float x = cand(Gs, se0, r);
       double clo = -INFINITY, chi = INFINITY;
       bool ok = true;
       // (group j + 1's header in flight while group j is applied)
-      MapHdr H = gm[0].h;
+      MapHdr H = W.gm[0].h;
       for (int j = 0; j < ngr; ++j) {
-        const MapHdr Hn = gm[min(j + 1, ngr - 1)].h;
+        const MapHdr Hn = W.gm[min(j + 1, ngr - 1)].h;
         const int kq = comp_off(x, H, kGroupM, ok);
-        comp_apply(x, clo, chi, ok, H, kq, gm[j].e[kq & ((1 << (ok ? H.m : 0)) - 1)]);
+        comp_apply(x, clo, chi, ok, H, kq, W.gm[j].e[kq & ((1 << (ok ? H.m : 0)) - 1)]);
         H = Hn;
       }
       if (ok) {
@@ -789,15 +892,14 @@ __global__ __launch_bounds__(kMapT) void k_sq_maps(SqView v) {
           clo = fmax(clo, 0.0);
           chi = fmin(chi, 0.0);
         }
-        en.E = x;
-        en.LOu = lo_units(clo, e0);
-        en.HIu = hi_units(chi, e0);
+        en = MapEnt{x, lo_units(clo, se0), hi_units(chi, se0)};
       }
     }
-    o->e[r] = en;
+    so->e[r] = en;
     if (tid == 0) clk[5] = (long long)__builtin_amdgcn_s_memtime();
   }
 }
+
 
 // ---- 4: the walk -------------------------------------------------------------------
 // One wavefront per chain.  The superblock maps of a chunk of kWalkC
@@ -1279,10 +1381,7 @@ int seqsum_enqueue(const float4* d_x, int64_t n, int nch, void* ws, float* d_out
       k_sq_front<false><<<dim3(v.nk, nch), kFrontT, 0, st>>>(v, nullptr, nullptr, nullptr);
     }
   }
-  if (stages & 2) {
-    k_sq_leaves<<<dim3(v.nk * kLeafWg, nch), kLeafT, 0, st>>>(v);
-    k_sq_maps<<<dim3(v.nk, nch), kMapT, 0, st>>>(v);
-  }
+  if (stages & 2) k_sq_build<<<dim3(v.nk, nch), kBuildT, 0, st>>>(v);
   if (stages & 4) k_sq_walk<<<nch, kWave, 0, st>>>(v, d_out);
   RST_HIP(hipGetLastError());
   return RST_OK;

@@ -39,6 +39,8 @@ struct Chain {
   std::vector<GroupMap> grp;
   std::vector<SbMap> sbm;
   int stats[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int work[3] = {0, 0, 0};  // leaf maps, group maps, superblock maps built
+  bool fresh = false;       // incremental with a fresh front (reuse needs the same base)
 };
 
 void front(Chain& C) {
@@ -179,10 +181,19 @@ void front(Chain& C) {
   }
 }
 
-void maps(Chain& C) {
+// dirty: per block, 1 = its elements changed since the maps were built
+// (nullptr: build everything).  Clean blocks keep their leaf maps, groups of
+// clean blocks their group maps, superblocks of clean groups their maps --
+// seqsum.hip's incremental rebuild (the guesses, boundaries and candidate
+// bases stay those of the last full build).
+void maps(Chain& C, const std::vector<uint8_t>* dirty = nullptr) {
   for (int k = 0; k < C.nk; ++k) {
     const int ga = C.ks.at(k), gb = C.ks.at(k + 1);
     const int ba = C.gs.at(ga), bb = C.gs.at(gb);
+    bool sb_dirty = dirty == nullptr || C.fresh;
+    if (dirty)
+      for (int b = ba; b < bb; ++b) sb_dirty = sb_dirty || dirty->at(b);
+    if (!sb_dirty) continue;
     const int ea = C.bs.at(ba), eb = C.bs.at(bb);
     const int ngr = gb - ga, nblk = bb - ba, nel = eb - ea;
     if (ngr < 1 || ngr > kMaxSbGroups || nblk < 1 || nblk > kMaxSbBlocks || nel < 1 || nel > kMaxSbElems)
@@ -203,19 +214,40 @@ void maps(Chain& C) {
       pre += C.inc.at(ba + i);
     }
     std::vector<Leaf> lf(kMaxSbBlocks);
+    std::vector<uint8_t> dirty_leaf(kMaxSbBlocks, 0);
     for (int bl = 0; bl < nblk; ++bl) {
       const float G = candidate_base((float)Gd.at(bl), kLeafR);
+      if (dirty && !dirty->at(ba + bl) && (!C.fresh || std::memcmp(&G, &C.leaf.at(ba + bl).h.G, 4) == 0)) {
+        lf.at(bl) = C.leaf.at(ba + bl);
+        continue;
+      }
+      if (dirty) dirty_leaf.at(bl) = 1;
+      C.work[0] += 1;
       const int e0 = grid_exp(G);
+      // candidate 0 first: when its run rounds on no grid coarser than G's
+      // (m = 0, ~99.7% of an ICP loop's blocks) it alone is the map; else
+      // all kLeafR candidates as before
       Run p[kLeafR];
-      for (int r = 0; r < kLeafR; ++r) {
+      run_init(p[0], cand(G, e0, 0));
+      for (int i = sbs.at(bl); i < sbs.at(bl + 1); ++i) run_step(p[0], xs.at(i), e0);
+      const bool more = p[0].need != kNoNeed && p[0].need > e0;
+      for (int r = 1; r < kLeafR; ++r) {
         run_init(p[r], cand(G, e0, r));
-        for (int i = sbs.at(bl); i < sbs.at(bl + 1); ++i) run_step(p[r], xs.at(i), e0);
+        if (more)
+          for (int i = sbs.at(bl); i < sbs.at(bl + 1); ++i) run_step(p[r], xs.at(i), e0);
       }
       int need = kNoNeed;
-      for (int r = 0; r < kLeafR; ++r) need = imax(need, p[r].need);
+      for (int r = 0; r < (more ? kLeafR : 1); ++r) need = imax(need, p[r].need);
       const int mneed = need == kNoNeed ? 0 : imax(0, need - e0);
       const bool exact_only = mneed > kLeafM;
       const int m = exact_only ? 0 : mneed;
+      if (getenv("EMU_MHIST")) {  // (statistics) leaf lattice: m 0..kLeafM, exact-only, opaque
+        static long long h[8];
+        static int calls;
+        h[p[0].opaque ? 7 : (exact_only ? 6 : m)]++;
+        if (++calls % 100000 == 0)
+          std::fprintf(stderr, "mhist m0 %lld m1 %lld m2 %lld exact_only %lld opaque %lld\n", h[0], h[1], h[2], h[6], h[7]);
+      }
       Leaf& o = lf.at(bl);
       o.h.G = G;
       o.h.e0 = e0;
@@ -238,9 +270,19 @@ void maps(Chain& C) {
       C.leaf.at(ba + bl) = o;
     }
     std::vector<GroupMap> gm(kMaxSbGroups);
+    bool any_group = false;
     for (int gi = 0; gi < ngr; ++gi) {
       const int c0 = sgs.at(gi), c1 = sgs.at(gi + 1);
       if (c1 - c0 < 1 || c1 - c0 > 2 * kGW - 1) throw std::runtime_error("group size out of range");
+      bool g_dirty = dirty == nullptr;
+      if (dirty)
+        for (int j = c0; j < c1; ++j) g_dirty = g_dirty || dirty_leaf.at(j);
+      if (!g_dirty) {
+        gm.at(gi) = C.grp.at(ga + gi);
+        continue;
+      }
+      C.work[1] += 1;
+      any_group = true;
       const MapHdr h0 = lf.at(c0).h;
       int lat = h0.e0 + h0.m;
       for (int j = c0 + 1; j < c1; ++j) {
@@ -249,6 +291,13 @@ void maps(Chain& C) {
       }
       int m = imax(0, lat - h0.e0);
       const bool exact_only = m > kGroupM;
+      if (getenv("EMU_MHIST")) {
+        static long long h[8];
+        static int calls;
+        h[exact_only ? 7 : m]++;
+        if (++calls % 10000 == 0)
+          std::fprintf(stderr, "ghist %lld %lld %lld %lld %lld exact_only %lld\n", h[0], h[1], h[2], h[3], h[4], h[7]);
+      }
       if (exact_only) m = 0;
       const int R = 1 << m;
       const float G = candidate_base(h0.G, R);
@@ -282,12 +331,21 @@ void maps(Chain& C) {
       }
       C.grp.at(ga + gi) = o;
     }
+    if (dirty && !any_group) continue;
+    C.work[2] += 1;
     {
       const MapHdr h0 = gm.at(0).h;
       int lat = h0.e0 + h0.m;
       for (int j = 1; j < ngr; ++j) lat = imax(lat, gm.at(j).h.e0 + gm.at(j).h.m);
       int m = imax(0, lat - h0.e0);
       const bool exact_only = m > kSbM;
+      if (getenv("EMU_MHIST")) {
+        static long long h[8];
+        static int calls;
+        h[exact_only ? 7 : m]++;
+        if (++calls % 1000 == 0)
+          std::fprintf(stderr, "sbhist %lld %lld %lld %lld %lld %lld %lld exact_only %lld\n", h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7]);
+      }
       if (exact_only) m = 0;
       const int R = 1 << m;
       const float G = candidate_base(h0.G, R);
@@ -380,14 +438,22 @@ float walk(Chain& C) {
 
 }  // namespace
 
+// seqsum_emu <in.f32> <n> <nch> [nstreams [incremental]]: nstreams float4
+// streams of n rows back to back (an ICP loop's iterations); incremental: a
+// stream after the first rebuilds only the maps of blocks whose windows
+// changed (the GPU's rule: block b is dirty when window b or b + 1 is).
+// One line per stream and chain: sum bits, walk stats, maps built.
 int main(int argc, char** argv) {
   if (argc < 4) {
-    std::fprintf(stderr, "usage: seqsum_emu <in.f32> <n> <nch>\n");
+    std::fprintf(stderr, "usage: seqsum_emu <in.f32> <n> <nch> [nstreams [incremental]]\n");
     return 2;
   }
   const int64_t n = std::atoll(argv[2]);
   const int nch = std::atoi(argv[3]);
-  std::vector<float> raw((size_t)n * 4);
+  const int ns = argc > 4 ? std::atoi(argv[4]) : 1;
+  const int incr_mode = argc > 5 ? std::atoi(argv[5]) : 0;  // 1 stale front, 2 fresh front
+  const bool incr = incr_mode != 0;
+  std::vector<float> raw((size_t)n * 4 * ns);
   FILE* f = std::fopen(argv[1], "rb");
   if (!f || std::fread(raw.data(), 4, raw.size(), f) != raw.size()) {
     std::fprintf(stderr, "read failed\n");
@@ -395,44 +461,75 @@ int main(int argc, char** argv) {
   }
   std::fclose(f);
   try {
-    for (int c = 0; c < nch; ++c) {
-      Chain C;
-      C.n = n;
-      C.nb = (int)((n + kW - 1) / kW);
-      C.ng = (C.nb + kGW - 1) / kGW;
-      C.nk = (C.ng + kKW - 1) / kKW;
-      C.x.resize(n);
-      for (int64_t i = 0; i < n; ++i) C.x[i] = raw[(size_t)i * 4 + c];
-      C.wflg.assign(C.nb, 0);
-      C.inc.assign(C.nb, 0.0);
-      C.tinc.assign(C.nk, 0.0);
-      C.bs.assign(C.nb + 1, -1);
-      C.gs.assign(C.ng + 1, -1);
-      C.ks.assign(C.nk + 1, -1);
-      C.leaf.resize(C.nb);
-      C.grp.resize(C.ng);
-      C.sbm.resize(C.nk);
-      float s = 0.0f;
-      if (n > 0) {
-        front(C);
-        if (const char* dump = getenv("EMU_DUMP")) {
-          // the front kernel's tables of chain c: bs, gs, ks (int32), inc (f64)
-          char path[512];
-          std::snprintf(path, sizeof(path), "%s.%d", dump, c);
-          FILE* g = std::fopen(path, "wb");
-          std::fwrite(C.bs.data(), 4, C.bs.size(), g);
-          std::fwrite(C.gs.data(), 4, C.gs.size(), g);
-          std::fwrite(C.ks.data(), 4, C.ks.size(), g);
-          std::fwrite(C.inc.data(), 8, C.inc.size(), g);
-          std::fclose(g);
+    std::vector<Chain> chains(nch);
+    for (int si = 0; si < ns; ++si) {
+      for (int c = 0; c < nch; ++c) {
+        Chain& C = chains[c];
+        const bool inc_now = incr && si > 0 && n > 0;
+        std::vector<uint8_t> dirty;
+        if (inc_now) {
+          std::vector<uint8_t> dw(C.nb + 1, 0);
+          for (int64_t i = 0; i < n; ++i) {
+            const float v = raw[((size_t)si * n + i) * 4 + c];
+            uint32_t a, b;
+            std::memcpy(&a, &v, 4);
+            std::memcpy(&b, &C.x.at(i), 4);
+            if (a != b) dw.at(i / kW) = 1;
+            C.x.at(i) = v;
+          }
+          dirty.assign(C.nb, 0);
+          for (int b = 0; b < C.nb; ++b) dirty.at(b) = dw.at(b) | dw.at(b + 1);
+          for (int w = 0; w < C.nb; ++w) {  // the window flags stay current
+            int fl = 0;
+            for (int64_t i = (int64_t)w * kW; i < std::min<int64_t>(n, (int64_t)(w + 1) * kW); ++i)
+              fl |= nf_flags(C.x.at(i));
+            C.wflg.at(w) = (uint8_t)fl;
+          }
+        } else {
+          C = Chain();
+          C.n = n;
+          C.nb = (int)((n + kW - 1) / kW);
+          C.ng = (C.nb + kGW - 1) / kGW;
+          C.nk = (C.ng + kKW - 1) / kKW;
+          C.x.resize(n);
+          for (int64_t i = 0; i < n; ++i) C.x[i] = raw[((size_t)si * n + i) * 4 + c];
+          C.wflg.assign(C.nb, 0);
+          C.inc.assign(C.nb, 0.0);
+          C.tinc.assign(C.nk, 0.0);
+          C.bs.assign(C.nb + 1, -1);
+          C.gs.assign(C.ng + 1, -1);
+          C.ks.assign(C.nk + 1, -1);
+          C.leaf.resize(C.nb);
+          C.grp.resize(C.ng);
+          C.sbm.resize(C.nk);
         }
-        maps(C);
-        s = walk(C);
+        for (int j = 0; j < 8; ++j) C.stats[j] = 0;
+        for (int j = 0; j < 3; ++j) C.work[j] = 0;
+        float s = 0.0f;
+        if (n > 0) {
+          C.fresh = inc_now && incr_mode == 2;
+          if (!inc_now || C.fresh) {
+            front(C);
+            if (const char* dump = getenv("EMU_DUMP")) {
+              // the front kernel's tables of chain c: bs, gs, ks (int32), inc (f64)
+              char path[512];
+              std::snprintf(path, sizeof(path), "%s.%d", dump, c);
+              FILE* g = std::fopen(path, "wb");
+              std::fwrite(C.bs.data(), 4, C.bs.size(), g);
+              std::fwrite(C.gs.data(), 4, C.gs.size(), g);
+              std::fwrite(C.ks.data(), 4, C.ks.size(), g);
+              std::fwrite(C.inc.data(), 8, C.inc.size(), g);
+              std::fclose(g);
+            }
+          }
+          maps(C, inc_now ? &dirty : nullptr);
+          s = walk(C);
+        }
+        uint32_t u;
+        std::memcpy(&u, &s, 4);
+        std::printf("%08x %d %d %d %d %d %d %d %d %d %d\n", u, C.stats[0], C.stats[1], C.stats[2],
+                    C.stats[3], C.stats[4], C.stats[5], C.stats[6], C.work[0], C.work[1], C.work[2]);
       }
-      uint32_t u;
-      std::memcpy(&u, &s, 4);
-      std::printf("%08x %d %d %d %d %d %d %d\n", u, C.stats[0], C.stats[1], C.stats[2], C.stats[3],
-                  C.stats[4], C.stats[5], C.stats[6]);
     }
   } catch (const std::exception& e) {
     std::printf("ERROR %s\n", e.what());
