@@ -31,9 +31,10 @@ struct rst_comm {
   int device = 0;
   // the shard layout of the last count exchange (rst::comm_shard_layout)
   bool have_layout = false;
-  int64_t layout_local = -1, layout_total = -1;
+  int64_t layout_total = -1;
   std::vector<int64_t> counts, offsets;
-  int64_t* d_cnt = nullptr;  // device scratch of the count all-gather
+  int64_t* d_cnt = nullptr;     // device scratch of the count all-gather [R + 1]
+  int64_t* d_layout = nullptr;  // the exchanged counts on the device [R]
 };
 
 namespace rst {
@@ -47,47 +48,86 @@ int comm_allreduce_sum_f64(rst_comm* comm, double* d_buf, size_t count, hipStrea
 
 int comm_size(const rst_comm* comm) { return comm ? comm->nranks : 1; }
 
-// Every rank's shard size.  The exchange (one all-gather of one int64 per
-// rank and a host synchronisation) runs on the first align of a
-// communicator, whenever the caller passes no n_total, and whenever this
-// rank's n_local or the caller's n_total differ from the cached layout's
-// (a shard-size change must therefore reach every rank in the same align,
-// or the caller passes n_total = 0 on every rank); a given n_total is
-// checked against the exchanged counts, so a wrong or rank-dependent value
-// fails with RST_E_ARG instead of skewing the means.
+namespace {
+__global__ void k_put_i64(int64_t* __restrict__ p, int64_t v) {
+  if (threadIdx.x == 0) *p = v;
+}
+// this align's all-gathered counts against the cached layout: a rank whose
+// shard size changed without an n_total change shows up in every rank's
+// copy of the gathered counts, so every rank flags the same align
+__global__ void k_layout_check(const int64_t* __restrict__ got, const int64_t* __restrict__ want, int R,
+                               int32_t* __restrict__ guard) {
+  bool bad = false;
+  for (int r = threadIdx.x; r < R; r += blockDim.x) bad = bad || got[r] != want[r];
+  if (__syncthreads_or(bad) && threadIdx.x == 0) atomicOr(guard, kGuardLayout);
+}
+}  // namespace
+
+// Every rank's shard size.  Whether the sizes are exchanged (one all-gather
+// of an int64 per rank and a host synchronisation) depends only on values
+// every rank holds alike -- the communicator's first align, a caller's
+// n_total of 0, or an n_total other than the cached layout's -- so the ranks
+// always issue the same collectives (the caller passes the same n_total on
+// every rank: include/rst_align.h).  An exchange whose total differs from a
+// given n_total fails with RST_E_ARG on every rank (they all see the same
+// counts) before any further collective.  With the cached layout, every
+// align still all-gathers the ranks' counts (no host wait) and
+// comm_layout_check compares them with the cache on the device: a shard
+// size changed at an unchanged n_total fails that align on every rank at
+// icp_finish (RST_E_ARG).  *n_eff is the source count this rank runs with
+// (0 when its size left the layout), so a stale layout never moves a kernel
+// out of its buffers.
 int comm_shard_layout(rst_comm* comm, int64_t n_local, int64_t n_total_hint, hipStream_t st,
-                      int64_t* n_total, int64_t* offset, const std::vector<int64_t>** counts) {
+                      int64_t* n_total, int64_t* offset, int64_t* n_eff,
+                      const std::vector<int64_t>** counts) {
   if (!comm || !comm->comm) return RST_E_ARG;
-  const bool cached = comm->have_layout && n_total_hint > 0 && n_local == comm->layout_local &&
-                      n_total_hint == comm->layout_total;
-  if (!cached) {
-    const int R = comm->nranks;
-    if (!comm->d_cnt && hipMalloc(&comm->d_cnt, sizeof(int64_t) * (R + 1)) != hipSuccess)
-      return RST_E_NOMEM;
-    RST_HIP(hipMemcpyAsync(comm->d_cnt + R, &n_local, sizeof(int64_t), hipMemcpyHostToDevice, st));
-    if (ncclAllGather(comm->d_cnt + R, comm->d_cnt, 1, ncclInt64, comm->comm, st) != ncclSuccess)
-      return RST_E_COMM;
+  const int R = comm->nranks;
+  if (!comm->d_cnt) {
+    if (hipMalloc(&comm->d_cnt, sizeof(int64_t) * (2 * R + 1)) != hipSuccess) return RST_E_NOMEM;
+    comm->d_layout = comm->d_cnt + R + 1;
+  }
+  const bool exchange = !comm->have_layout || n_total_hint <= 0 || n_total_hint != comm->layout_total;
+  k_put_i64<<<1, 64, 0, st>>>(comm->d_cnt + R, n_local);
+  RST_HIP(hipGetLastError());
+  if (ncclAllGather(comm->d_cnt + R, comm->d_cnt, 1, ncclInt64, comm->comm, st) != ncclSuccess)
+    return RST_E_COMM;
+  if (exchange) {
     std::vector<int64_t> c(R);
     RST_HIP(hipMemcpyAsync(c.data(), comm->d_cnt, sizeof(int64_t) * R, hipMemcpyDeviceToHost, st));
     RST_HIP(hipStreamSynchronize(st));
     std::vector<int64_t> o(R);
     int64_t tot = 0;
+    bool neg = false;
     for (int r = 0; r < R; ++r) {
-      if (c[r] < 0) return RST_E_ARG;
+      neg = neg || c[r] < 0;
       o[r] = tot;
       tot += c[r];
     }
-    if (c[comm->rank] != n_local) return RST_E_ARG;
+    comm->have_layout = false;
+    if (neg) return RST_E_ARG;  // (every rank sees the same counts)
     comm->counts = c;
     comm->offsets = o;
-    comm->layout_local = n_local;
     comm->layout_total = tot;
     comm->have_layout = true;
+    RST_HIP(hipMemcpyAsync(comm->d_layout, comm->counts.data(), sizeof(int64_t) * R, hipMemcpyHostToDevice,
+                           st));
+    RST_HIP(hipStreamSynchronize(st));
   }
   if (n_total_hint > 0 && n_total_hint != comm->layout_total) return RST_E_ARG;
   *n_total = comm->layout_total;
   *offset = comm->offsets[comm->rank];
+  // (a rank whose size left the cached layout runs no points: its searches
+  // scatter to original indices up to its own size, which the layout would
+  // not hold; the align is flagged on every rank by comm_layout_check)
+  *n_eff = n_local == comm->counts[comm->rank] ? n_local : 0;
   if (counts) *counts = &comm->counts;
+  return RST_OK;
+}
+
+int comm_layout_check(rst_comm* comm, hipStream_t st, int32_t* d_guard) {
+  if (!comm || !comm->d_cnt) return RST_E_ARG;
+  k_layout_check<<<1, 64, 0, st>>>(comm->d_cnt, comm->d_layout, comm->nranks, d_guard);
+  RST_HIP(hipGetLastError());
   return RST_OK;
 }
 

@@ -1744,9 +1744,15 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
   if (!tgt->has_bvh) return RST_E_ARG;
   if (tgt->m >= kCertBit) return RST_E_ARG;  // positions carry kCertBit
   if (p2plane && !tgt->nrm) return RST_E_STATE;
-  const int64_t n_local = src->m;
+  int64_t n_local = src->m;
   int64_t n_total = n_local;
   hipStream_t st = ctx->stream;
+  // n_total, this shard's offset in the source order and the centroid are
+  // global quantities under sharding: the shard layout is exchanged when the
+  // caller's n_total asks for it and checked on the device every align
+  // (comm.hip); this rank runs with its count of the layout
+  int64_t shard_off = 0;
+  if (comm) RST_CHECK(comm_shard_layout(comm, src->m, opts.n_total, st, &n_total, &shard_off, &n_local, nullptr));
   // one scratch buffer: [centroid / kernel-1 slab | kernel-2 slab | totals]
   const int nblk = blocks_for(n_local);
   // k_icp_fb scans both queues' per-block counts into dynamic LDS, on top of
@@ -1764,11 +1770,6 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
   double* slab2 = slab + rows1;
   double* totals = slab2 + (size_t)kFbBlocks * RS;  // 64 doubles
 
-  // n_total, this shard's offset in the source order and the centroid are
-  // global quantities under sharding: the shard layout is exchanged once
-  // and cached (a given opts.n_total is checked against it)
-  int64_t shard_off = 0;
-  if (comm) RST_CHECK(comm_shard_layout(comm, n_local, opts.n_total, st, &n_total, &shard_off, nullptr));
   // reference early return (:77-79): pose untouched
   if (n_total < 3 || tgt->m < 3) return RST_FALSE;
   if (p2plane && n_total < 6) return RST_FALSE;
@@ -1835,6 +1836,7 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
   } else {
     k_init_state<<<1, kBS, 0, st>>>(slab, 0, nullptr, ia, ctx->d_state);
   }
+  if (comm) RST_CHECK(comm_layout_check(comm, st, &ctx->d_state->guard));
   AccArgs aa;
   aa.corr = corr;
   aa.nrm = tgt->nrm;
@@ -1999,6 +2001,11 @@ int icp_finish(rst_ctx* ctx, float pose_inout[16], float* mean_cost, int32_t* it
     ctx->last_kernel_launches = cnt;
   }
   const IcpState& h = *ctx->h_state;
+  if (h.guard & kGuardLayout) {  // (every rank of the communicator alike)
+    set_last_error(hipSuccess, "sharded align: a shard size changed while n_total did not (pass the new "
+                   "n_total, or 0, on every rank)", __FILE__, __LINE__);
+    return RST_E_ARG;
+  }
   if (h.guard) {  // an index guard tripped: corrupted queue / neighbour state
     static thread_local char msg[160];
     const int32_t* d = h.path[kQTrace - 1];  // the first trip's details (kernel-specific)

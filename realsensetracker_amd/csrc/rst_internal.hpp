@@ -47,6 +47,8 @@ void set_last_error(hipError_t e, const char* what, const char* file,
 // Written only by the single-block solve kernels, read (uniformly) by the
 // per-point kernels.  Plain POD; lives in the context's workspace.
 constexpr int kQTrace = 256;
+// IcpCore::guard bit of a shard layout that changed at an unchanged n_total
+constexpr int32_t kGuardLayout = 1 << 16;
 
 // The part of the state the solve reads and writes: copied to registers at
 // the start of the solve kernel (its loads overlap the slab reduction) and
@@ -69,7 +71,9 @@ struct IcpCore {
   int32_t fb_e;      // fallback-queue entries of the current iteration
   float seq[4];      // RST_SUM_REF: this iteration's sequential fp32 sums
                      // (sum dst[nbr_i] xyz, cost), align_icp.cpp:113,120
-  int32_t guard;     // bit mask of index guards that tripped (0: none; diagnostics)
+  int32_t guard;     // bit mask of index guards that tripped (0: none; diagnostics);
+                     // kGuardLayout: a sharded align's shard sizes changed at an
+                     // unchanged n_total (comm.hip)
   int32_t pad1;
 };
 
@@ -271,11 +275,15 @@ int compute_covariances_device(rst_ctx* ctx, const rst_target* tgt, int use_gicp
 int comm_allreduce_sum_f64(rst_comm* comm, double* d_buf, size_t count,
                            hipStream_t stream);
 int comm_size(const rst_comm* comm);
-// every rank's shard size (exchanged once per layout): n_total, this rank's
-// offset in the whole source's order, the counts
+// every rank's shard size (exchanged per layout, checked on the device every
+// align): n_total, this rank's offset in the whole source's order, the count
+// it runs with, the counts
 int comm_shard_layout(rst_comm* comm, int64_t n_local, int64_t n_total_hint, hipStream_t st,
-                      int64_t* n_total, int64_t* offset,
+                      int64_t* n_total, int64_t* offset, int64_t* n_eff,
                       const std::vector<int64_t>** counts);
+// after k_init_state: this align's gathered counts against the cached
+// layout, kGuardLayout into *d_guard on a mismatch (every rank alike)
+int comm_layout_check(rst_comm* comm, hipStream_t st, int32_t* d_guard);
 // in-place all-gather of every rank's stretch [off_r, off_r + n_r) of buf
 int comm_allgatherv_f4(rst_comm* comm, float4* buf, hipStream_t st);
 
