@@ -170,7 +170,8 @@ def lib() -> C.CDLL:
                 "`python -m realsensetracker_amd.build` (or __graft_entry__.build())")
         # kernel arguments in device memory (the library's load-time default
         # too; here for a runtime that initialises before the library loads)
-        os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
+        if os.environ.get("RST_NO_ENV_DEFAULTS", "0") in ("", "0"):
+            os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
         L = C.CDLL(str(LIB_PATH), mode=C.RTLD_GLOBAL)
         rts = hip_runtimes_mapped()
         if len(rts) > 1:

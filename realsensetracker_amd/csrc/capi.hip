@@ -24,7 +24,17 @@ static thread_local char g_last_error[512] = {0};
 // load waited ~6k clocks on the host link (measured in k_sq_walk: its
 // prologue 7.7k -> 1.5k clocks).  Read by the HIP runtime when it
 // initialises, so set at load time, before this library's first HIP call.
-__attribute__((constructor)) static void rst_env_defaults() { setenv("HIP_FORCE_DEV_KERNARG", "1", 0); }
+// The variable is process-wide: it also places the kernel arguments of any
+// other HIP code in the process that initialises the runtime afterwards
+// (INTEGRATION.md).  A set value is never overridden, and
+// RST_NO_ENV_DEFAULTS=1 leaves the environment untouched (the loader sets
+// nothing either; a host that initialises HIP before loading this library
+// keeps its own placement).
+__attribute__((constructor)) static void rst_env_defaults() {
+  const char* off = getenv("RST_NO_ENV_DEFAULTS");
+  if (off && *off && *off != '0') return;
+  setenv("HIP_FORCE_DEV_KERNARG", "1", 0);
+}
 
 void set_last_error(hipError_t e, const char* what, const char* file, int line) {
   snprintf(g_last_error, sizeof(g_last_error), "%s failed: %s (%s:%d)", what,
@@ -98,19 +108,61 @@ int ctx_workspace(rst_ctx* ctx, size_t bytes, void** out) {
   return RST_OK;
 }
 
-int ctx_pinned(rst_ctx* ctx, size_t bytes, void** out) {
-  if (bytes > ctx->pinned_bytes) {
-    if (ctx->pinned) {
-      RST_HIP(hipStreamSynchronize(ctx->stream));
-      RST_HIP(hipHostFree(ctx->pinned));
-      ctx->pinned = nullptr;
-      ctx->pinned_bytes = 0;
-    }
-    const size_t sz = std::max<size_t>(bytes + bytes / 4, 1 << 20);
-    if (hipHostMalloc(&ctx->pinned, sz, hipHostMallocDefault) != hipSuccess) return RST_E_NOMEM;
-    ctx->pinned_bytes = sz;
+static int stage_init(rst_ctx* ctx) {
+  if (ctx->pinned) return RST_OK;
+  const size_t sz = 2 * kStageChunk + kPinnedSmall;
+  if (hipHostMalloc(&ctx->pinned, sz, hipHostMallocDefault) != hipSuccess) return RST_E_NOMEM;
+  ctx->pinned_bytes = sz;
+  for (int k = 0; k < 2; ++k) {
+    RST_HIP(hipEventCreateWithFlags(&ctx->stage_ev[k], hipEventDisableTiming));
+    RST_HIP(hipEventRecord(ctx->stage_ev[k], ctx->stream));
   }
-  *out = ctx->pinned;
+  return RST_OK;
+}
+
+int ctx_pinned_small(rst_ctx* ctx, size_t bytes, void** out) {
+  if (bytes > kPinnedSmall) return RST_E_ARG;
+  RST_CHECK(stage_init(ctx));
+  *out = (char*)ctx->pinned + 2 * kStageChunk;
+  return RST_OK;
+}
+
+int stage_h2d(rst_ctx* ctx, void* d, const void* h, size_t bytes) {
+  if (bytes == 0) return RST_OK;
+  RST_CHECK(stage_init(ctx));
+  for (size_t off = 0, i = 0; off < bytes; off += kStageChunk, ++i) {
+    const int k = (int)(i & 1);
+    const size_t len = std::min(kStageChunk, bytes - off);
+    char* pin = (char*)ctx->pinned + k * kStageChunk;
+    RST_HIP(hipEventSynchronize(ctx->stage_ev[k]));  // the half's previous DMA is done
+    memcpy(pin, (const char*)h + off, len);
+    RST_HIP(hipMemcpyAsync((char*)d + off, pin, len, hipMemcpyHostToDevice, ctx->stream));
+    RST_HIP(hipEventRecord(ctx->stage_ev[k], ctx->stream));
+  }
+  return RST_OK;
+}
+
+int stage_d2h(rst_ctx* ctx, void* h, const void* d, size_t bytes) {
+  if (bytes == 0) return RST_OK;
+  RST_CHECK(stage_init(ctx));
+  const size_t nc = (bytes + kStageChunk - 1) / kStageChunk;
+  auto issue = [&](size_t i) -> int {
+    const int k = (int)(i & 1);
+    const size_t off = i * kStageChunk, len = std::min(kStageChunk, bytes - off);
+    RST_HIP(hipEventSynchronize(ctx->stage_ev[k]));
+    RST_HIP(hipMemcpyAsync((char*)ctx->pinned + k * kStageChunk, (const char*)d + off, len,
+                           hipMemcpyDeviceToHost, ctx->stream));
+    RST_HIP(hipEventRecord(ctx->stage_ev[k], ctx->stream));
+    return RST_OK;
+  };
+  RST_CHECK(issue(0));
+  for (size_t i = 0; i < nc; ++i) {
+    const int k = (int)(i & 1);
+    const size_t off = i * kStageChunk, len = std::min(kStageChunk, bytes - off);
+    if (i + 1 < nc) RST_CHECK(issue(i + 1));  // (the other half: in flight meanwhile)
+    RST_HIP(hipEventSynchronize(ctx->stage_ev[k]));
+    memcpy((char*)h + off, (const char*)ctx->pinned + k * kStageChunk, len);
+  }
   return RST_OK;
 }
 
@@ -149,16 +201,7 @@ static int upload_xyz(rst_ctx* ctx, const float* h, int64_t n, float** d_out) {
   RST_CHECK(ctx_alloc(ctx, bytes, &dv, &cls));
   float* d = (float*)dv;
   if (n > 0) {
-    void* pin = nullptr;
-    int s = ctx_pinned(ctx, bytes, &pin);
-    // the staging buffer may still feed an earlier async copy
-    if (s >= 0 && hipStreamSynchronize(ctx->stream) != hipSuccess) s = RST_E_HIP;
-    if (s >= 0) {
-      memcpy(pin, h, sizeof(float) * 3 * n);
-      if (hipMemcpyAsync(d, pin, sizeof(float) * 3 * n, hipMemcpyHostToDevice, ctx->stream) !=
-          hipSuccess)
-        s = RST_E_HIP;
-    }
+    const int s = stage_h2d(ctx, d, h, sizeof(float) * 3 * n);
     if (s < 0) {
       free_xyz(ctx, d, n);
       return s;
@@ -277,6 +320,8 @@ int rst_ctx_destroy(rst_ctx* ctx) {
   for (auto& kv : ctx->gexec) hipGraphExecDestroy(kv.second);
   if (ctx->ws) hipFree(ctx->ws);
   if (ctx->pinned) hipHostFree(ctx->pinned);
+  for (hipEvent_t e : ctx->stage_ev)
+    if (e) hipEventDestroy(e);
   if (ctx->d_state) hipFree(ctx->d_state);
   if (ctx->h_state) hipHostFree(ctx->h_state);
   if (ctx->d_slab) hipFree(ctx->d_slab);
@@ -964,17 +1009,9 @@ int rst_solve_kabsch(rst_ctx* ctx, const float* src, int64_t n, const float* dst
   const size_t pb = sizeof(int32_t) * 2 * (size_t)k, wb = weights ? sizeof(float) * (size_t)k : 0;
   const size_t pwb = (pb + wb + 255) & ~(size_t)255;
   void* ws = nullptr;
-  void* pin = nullptr;
   if (r >= 0) r = ctx_workspace(ctx, pwb + solve_kabsch_ws_bytes(k), &ws);
-  // (the staging buffer may still feed the uploads above)
-  if (r >= 0 && hipStreamSynchronize(ctx->stream) != hipSuccess) r = RST_E_HIP;
-  if (r >= 0) r = ctx_pinned(ctx, pb + wb, &pin);
-  if (r >= 0) {
-    memcpy(pin, pairs, pb);
-    if (weights) memcpy((char*)pin + pb, weights, wb);
-    if (hipMemcpyAsync(ws, pin, pb + wb, hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
-      r = RST_E_HIP;
-  }
+  if (r >= 0) r = stage_h2d(ctx, ws, pairs, pb);
+  if (r >= 0 && weights) r = stage_h2d(ctx, (char*)ws + pb, weights, wb);
   if (r >= 0)
     r = solve_kabsch_device(ctx, ds, dd, (const int32_t*)ws,
                             weights ? (const float*)((char*)ws + pb) : nullptr, k,

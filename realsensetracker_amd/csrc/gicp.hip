@@ -688,7 +688,7 @@ int lm_solve(rst_ctx* ctx, const float* ds, int64_t n, const float* dd, const fl
   hipStream_t st = ctx->stream;
   const int nb = blocks_for(n);
   void* pin = nullptr;
-  RST_CHECK(ctx_pinned(ctx, 64, &pin));
+  RST_CHECK(ctx_pinned_small(ctx, 64, &pin));
   volatile int* hflag = (volatile int*)pin;
   hipEvent_t ev[2] = {nullptr, nullptr};
   for (int k = 0; k < 2; ++k)
@@ -718,7 +718,7 @@ int lm_solve(rst_ctx* ctx, const float* ds, int64_t n, const float* dd, const fl
   }
   k_gicp_end<<<1, 1, 0, st>>>(dst_state);
   // (a flag copy still pending is stream-ordered before the next solve's
-  // copies, and ctx_pinned synchronises before it frees the buffer)
+  // copies; the small pinned area lives as long as the context)
   for (int k = 0; k < 2; ++k)
     if (ev[k]) (void)hipEventDestroy(ev[k]);
   RST_CHECK(s);

@@ -109,8 +109,9 @@ struct rst_ctx {
   // workspaces (grow-only)
   void* ws = nullptr;
   size_t ws_bytes = 0;
-  void* pinned = nullptr;
+  void* pinned = nullptr;     // host staging: two halves of kStageChunk bytes
   size_t pinned_bytes = 0;
+  hipEvent_t stage_ev[2] = {nullptr, nullptr};  // the last copy through each half
   rst::IcpState* d_state = nullptr;
   rst::IcpState* h_state = nullptr;   // pinned mirror
   double* d_slab = nullptr;           // per-block partial sums
@@ -186,7 +187,18 @@ int target_alloc(rst_target* t, size_t bytes, void** out);
 
 // workspace helpers (implemented in capi.hip)
 int ctx_workspace(rst_ctx* ctx, size_t bytes, void** out);
-int ctx_pinned(rst_ctx* ctx, size_t bytes, void** out);
+// host <-> device copies through the context's pinned staging buffer, in
+// chunks of at most kStageChunk bytes through two alternating halves (one
+// half's DMA in flight while the other is filled): the pinned memory stays
+// 2 x kStageChunk however large the copy.  h2d returns with the copies
+// enqueued on the context's stream (h may be reused at once); d2h returns
+// with h written.
+constexpr size_t kStageChunk = (size_t)8 << 20;
+// a separate small pinned area past the halves (device -> host flags)
+constexpr size_t kPinnedSmall = 4096;
+int ctx_pinned_small(rst_ctx* ctx, size_t bytes, void** out);
+int stage_h2d(rst_ctx* ctx, void* d, const void* h, size_t bytes);
+int stage_d2h(rst_ctx* ctx, void* h, const void* d, size_t bytes);
 int ctx_slab(rst_ctx* ctx, size_t bytes, double** out);
 
 // target build (build.hip)

@@ -379,8 +379,8 @@ using namespace rst;
 namespace {
 
 // host-buffer entry points: upload, run `fn` on device buffers, download --
-// both copies through the context's pinned staging buffer (as capi.hip's
-// uploads).  A copy straight from / to pageable memory leaves the pinning to
+// both copies through the context's pinned staging buffer (stage_h2d /
+// stage_d2h: bounded chunks, as capi.hip's uploads).  A copy straight from / to pageable memory leaves the pinning to
 // the runtime, which measured 20-28 ms on a frame not copied recently
 // (profiles/r05_callers_prof.txt: the first RemoveNans of each pair of the
 // callers' workload, 0.4 ms otherwise); a staged copy is a host memcpy plus
@@ -392,25 +392,9 @@ int run_host(rst_ctx* ctx, const float* xyz, int64_t n, float* out, int64_t* n_o
   const size_t bytes = sizeof(float) * 3 * (size_t)std::max<int64_t>(n, 1);
   RST_CHECK(ctx_alloc(ctx, bytes, (void**)&din, &cin));
   int s = ctx_alloc(ctx, bytes, (void**)&dout, &cout);
-  void* pin = nullptr;
-  if (s >= 0) s = ctx_pinned(ctx, bytes, &pin);
-  // the staging buffer may still feed an earlier async copy
-  if (s >= 0 && hipStreamSynchronize(ctx->stream) != hipSuccess) s = RST_E_HIP;
-  if (s >= 0 && n > 0) {
-    memcpy(pin, xyz, sizeof(float) * 3 * n);
-    if (hipMemcpyAsync(din, pin, sizeof(float) * 3 * n, hipMemcpyHostToDevice, ctx->stream) !=
-        hipSuccess)
-      s = RST_E_HIP;
-  }
-  if (s >= 0) s = fn(din, dout);  // (stream-ordered after the upload: pin is free again once it returns a count)
-  if (s >= 0 && *n_out > 0) {
-    if (hipMemcpyAsync(pin, dout, sizeof(float) * 3 * (*n_out), hipMemcpyDeviceToHost, ctx->stream) !=
-            hipSuccess ||
-        hipStreamSynchronize(ctx->stream) != hipSuccess)
-      s = RST_E_HIP;
-    else
-      memcpy(out, pin, sizeof(float) * 3 * (*n_out));
-  }
+  if (s >= 0 && n > 0) s = stage_h2d(ctx, din, xyz, sizeof(float) * 3 * n);
+  if (s >= 0) s = fn(din, dout);
+  if (s >= 0 && *n_out > 0) s = stage_d2h(ctx, out, dout, sizeof(float) * 3 * (*n_out));
   hipStreamSynchronize(ctx->stream);
   ctx_release(ctx, din, cin);
   if (dout) ctx_release(ctx, dout, cout);
@@ -589,14 +573,7 @@ int rst_accum_add(rst_accum* a, const float pose[16], const float* xyz, int64_t 
   size_t c = 0;
   RST_CHECK(ctx_alloc(a->ctx, sizeof(float) * 3 * n, (void**)&d, &c));
   // staged through pinned memory (run_host above: no pageable-copy stall)
-  void* pin = nullptr;
-  int s = ctx_pinned(a->ctx, sizeof(float) * 3 * n, &pin);
-  if (s >= 0 && hipStreamSynchronize(a->ctx->stream) != hipSuccess) s = RST_E_HIP;
-  if (s >= 0) {
-    memcpy(pin, xyz, sizeof(float) * 3 * n);
-    if (hipMemcpyAsync(d, pin, sizeof(float) * 3 * n, hipMemcpyHostToDevice, a->ctx->stream) != hipSuccess)
-      s = RST_E_HIP;
-  }
+  int s = stage_h2d(a->ctx, d, xyz, sizeof(float) * 3 * n);
   if (s >= 0) s = accum_add_device(a, pose, d, n);
   hipStreamSynchronize(a->ctx->stream);
   ctx_release(a->ctx, d, c);
@@ -612,14 +589,7 @@ int rst_accum_size(const rst_accum* a, int64_t* n) {
 int rst_accum_extract(rst_accum* a, float* out, int64_t* n_out) {
   if (!a || !n_out || (a->count > 0 && !out)) return RST_E_ARG;
   RST_HIP(hipSetDevice(a->ctx->device));
-  if (a->count > 0) {
-    void* pin = nullptr;
-    RST_CHECK(ctx_pinned(a->ctx, sizeof(float) * 3 * a->count, &pin));
-    RST_HIP(hipMemcpyAsync(pin, a->list, sizeof(float) * 3 * a->count, hipMemcpyDeviceToHost,
-                           a->ctx->stream));
-    RST_HIP(hipStreamSynchronize(a->ctx->stream));
-    memcpy(out, pin, sizeof(float) * 3 * a->count);
-  }
+  if (a->count > 0) RST_CHECK(stage_d2h(a->ctx, out, a->list, sizeof(float) * 3 * a->count));
   *n_out = a->count;
   return RST_OK;
 }

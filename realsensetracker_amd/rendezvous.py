@@ -19,8 +19,10 @@ from __future__ import annotations
 import os
 import socket
 import struct
+import signal
 import subprocess
 import sys
+import threading
 import time
 
 import numpy as np
@@ -64,12 +66,20 @@ def launch(nproc: int, argv: list[str], script: str, grace: float = 10.0,
     procs = [subprocess.Popen([sys.executable, script, *argv], env=e) for e in envs]
     status = 0
     t0 = time.monotonic()
+    # a SIGTERM to the launcher stops the ranks too (no orphans); the
+    # handler raises, and the except clause below reaps them
+    prev_term = None
+    if threading.current_thread() is threading.main_thread():
+        def _on_term(signum, frame):
+            raise SystemExit(128 + signum)
+        prev_term = signal.signal(signal.SIGTERM, _on_term)
     try:
         while True:
             codes = [p.poll() for p in procs]
             bad = [c for c in codes if c is not None and c != 0]
             if bad:
-                status = bad[0]
+                # a rank killed by signal N reports -N: the shell's 128 + N
+                status = 128 - bad[0] if bad[0] < 0 else bad[0]
                 break
             if all(c is not None for c in codes):
                 return 0
@@ -80,6 +90,9 @@ def launch(nproc: int, argv: list[str], script: str, grace: float = 10.0,
     except BaseException:
         _stop(procs, grace)
         raise
+    finally:
+        if prev_term is not None:
+            signal.signal(signal.SIGTERM, prev_term)
     _stop(procs, grace)
     return status
 

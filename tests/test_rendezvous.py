@@ -4,6 +4,7 @@ environments and the TCP collectives at world size 2 and 3."""
 from __future__ import annotations
 
 import multiprocessing as mp
+import os
 import subprocess
 import sys
 
@@ -127,3 +128,50 @@ def test_launch_kills_ranks_ignoring_sigterm(tmp_path):
     r = subprocess.run([sys.executable, "-c", code], timeout=120)
     assert r.returncode == 124
     assert time.monotonic() - t0 < 30
+
+
+def test_launch_reports_a_signalled_rank_as_128_plus_n(tmp_path):
+    """A rank killed by a signal (Popen's -N) is reported as the shell's
+    128 + N, not as sys.exit(-N)'s 256 - N."""
+    script = tmp_path / "killed.py"
+    script.write_text(
+        "import os, signal, sys, time\n"
+        "if os.environ['RANK'] == '1':\n"
+        "    os.kill(os.getpid(), signal.SIGKILL)\n"
+        "time.sleep(300)\n")
+    root = str(RV.__file__).rsplit("/realsensetracker_amd", 1)[0]
+    code = ("import sys; sys.path.insert(0, %r); from realsensetracker_amd import rendezvous as RV; "
+            "sys.exit(RV.launch(2, [], %r, grace=1.0))" % (root, str(script)))
+    r = subprocess.run([sys.executable, "-c", code], timeout=120)
+    assert r.returncode == 128 + 9
+
+
+def test_launch_stops_ranks_on_sigterm(tmp_path):
+    """SIGTERM to the launcher stops every rank (no orphans) and exits
+    128 + 15."""
+    import signal
+    import time
+
+    script = tmp_path / "sleeper.py"
+    script.write_text(
+        "import os, sys, time\n"
+        "open(sys.argv[1] + '/pid' + os.environ['RANK'], 'w').write(str(os.getpid()))\n"
+        "time.sleep(300)\n")
+    root = str(RV.__file__).rsplit("/realsensetracker_amd", 1)[0]
+    code = ("import sys; sys.path.insert(0, %r); from realsensetracker_amd import rendezvous as RV; "
+            "sys.exit(RV.launch(2, [sys.argv[1]], %r, grace=1.0))" % (root, str(script)))
+    p = subprocess.Popen([sys.executable, "-c", code, str(tmp_path)])
+    t0 = time.monotonic()
+    while not all((tmp_path / f"pid{k}").exists() for k in range(2)):
+        assert time.monotonic() - t0 < 60
+        time.sleep(0.1)
+    pids = [int((tmp_path / f"pid{k}").read_text()) for k in range(2)]
+    p.send_signal(signal.SIGTERM)
+    assert p.wait(timeout=60) == 128 + 15
+    for pid in pids:
+        try:
+            os.kill(pid, 0)
+            alive = True
+        except ProcessLookupError:
+            alive = False
+        assert not alive, pid
