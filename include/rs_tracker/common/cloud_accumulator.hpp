@@ -2,7 +2,8 @@
 // (rs_replay_app.cpp:76-129: AddCloud, GetVoxelIndex, ExtractPointCloud) on
 // the device, header-only over the C ABI (rst_accum_*).  Same voxel rule
 // ((xfm * p) * (1 / voxel), truncated; the first point of a voxel stays);
-// ExtractPointCloud returns the points in insertion order.
+// ExtractPointCloud returns the points in the reference's std::unordered_map
+// iteration order (rs_replay_app.cpp:112-121).
 #pragma once
 
 #include "rs_tracker/common/types.hpp"

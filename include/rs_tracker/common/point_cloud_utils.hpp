@@ -11,8 +11,8 @@
 namespace rs_tracker {
 
 // point_cloud_utils.cpp:34-68: the first point of every voxel
-// floor(p / voxel_size), in ascending input order (the reference's order is
-// its unordered_map's; the point set is the same).
+// floor(p / voxel_size), in the reference's order: its std::unordered_map's
+// iteration (point_cloud_utils.cpp:54-57), replayed on the device.
 inline void DownsampleVoxel(const Cloud3f& cloud_in, const float voxel_size,
                             Cloud3f* const cloud_out) {
   Cloud3f tmp(cloud_in.cols());

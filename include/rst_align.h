@@ -304,9 +304,10 @@ int rst_remove_nans(rst_ctx* ctx, const float* xyz, int64_t n, float* out,
 int rst_remove_nans_device(rst_ctx* ctx, const float* d_xyz, int64_t n,
                            float* d_out, int64_t* n_out);
 /* DownsampleVoxel (point_cloud_utils.cpp:34-68): the first point (lowest
- * input index) of every voxel (int)floor(p / voxel_size), emitted in
- * ascending input index (the reference's order is its unordered_map's,
- * i.e. unspecified; the point SET is identical).  NaN / out-of-int-range
+ * input index) of every voxel (int)floor(p / voxel_size), emitted in the
+ * reference's order: the iteration order of its std::unordered_map (:54-57),
+ * libstdc++'s container with the classic boost::hash_combine (Boost <= 1.80)
+ * replayed on the device (voxel.hip).  NaN / out-of-int-range
  * coordinates key to INT_MIN as the reference's float->int cast does on
  * x86-64.  voxel_size must be > 0 and n < 2^30 (RST_E_ARG otherwise);
  * out holds >= n points. */
@@ -338,8 +339,9 @@ int rst_compute_matches(rst_ctx* ctx, const float* src_feat, int64_t n,
 /* A voxel map on the device: AddCloud(xfm, cloud) inserts xfm * p for
  * every point whose voxel (int)(p * inv) -- inv = float(1.0 / voxel_size),
  * truncation, NaN / out-of-range -> INT_MIN -- is new; the first point added
- * to a voxel stays.  Extract returns the points in insertion order (the
- * reference returns them in unordered_map order: same set). */
+ * to a voxel stays.  Extract returns the points in the reference's order,
+ * its std::unordered_map's iteration (rs_replay_app.cpp:112-121; as
+ * rst_downsample_voxel). */
 typedef struct rst_accum rst_accum;
 int rst_accum_create(rst_ctx* ctx, float voxel_size, rst_accum** out);
 int rst_accum_destroy(rst_accum* a);

@@ -134,6 +134,14 @@ int rst_debug_icp_solve(rst_ctx* ctx, const rst_icp_opts* opts, int64_t n_total,
                         const double* totals, const float smean[3], float pose_inout[16],
                         float* mu_inout, int32_t* iter_inout);
 
+/* The rehash schedule DownsampleVoxel / ExtractPointCloud's reference order
+ * is replayed from (voxel.hip umap_schedule: libstdc++'s _Prime_rehash_policy
+ * for a default-constructed std::unordered_map receiving n distinct keys):
+ * out[2k] = elements before the insert that rehashed, out[2k + 1] = the new
+ * bucket count, at most cap pairs; *count = the number of rehashes.  Host
+ * only (no GPU call). */
+int rst_debug_umap_schedule(int64_t n, int64_t* out, int64_t cap, int64_t* count);
+
 #ifdef __cplusplus
 }
 #endif

@@ -84,6 +84,9 @@ def lib():
         L.orc_accum_add.argtypes = [P, _f, _f, C.c_int64]
         L.orc_accum_extract.restype = C.c_int64
         L.orc_accum_extract.argtypes = [P, _f]
+        L.orc_umap_order.argtypes = [_i, C.c_int64, C.POINTER(C.c_int64)]
+        L.orc_umap_schedule.restype = C.c_int64
+        L.orc_umap_schedule.argtypes = [C.c_int64, C.POINTER(C.c_int64), C.c_int64]
         L.orc_unproject.argtypes = [_u16, C.c_int, C.c_int, _f, C.c_float, C.c_int, _f]
         L.orc_unproject_strided.argtypes = [_u16, C.c_int, C.c_int, C.c_int, _f, C.c_float,
                                             C.c_int, _f]
@@ -290,12 +293,52 @@ def remove_nans(cloud):
     return out[:n].copy()
 
 
-def downsample_voxel(cloud, voxel_size):
-    """DownsampleVoxel (point_cloud_utils.cpp:34-68), ascending input order."""
+def downsample_voxel(cloud, voxel_size, order: str = "reference"):
+    """DownsampleVoxel (point_cloud_utils.cpp:34-68): the first point of each
+    voxel, in the reference's std::unordered_map iteration order (:54-57;
+    rst_oracle_umap.cpp), or order="input" for ascending input index."""
     a = _cloud(cloud)
     out = np.zeros_like(a)
     n = lib().orc_downsample_voxel(_fp(a), a.shape[0], float(voxel_size), _fp(out))
-    return out[:n].copy()
+    out = out[:n].copy()
+    if order == "input":
+        return out
+    return out[umap_order(vox_keys(out, voxel_size, 0))]
+
+
+def vox_keys(points, voxel_size, kind: int):
+    """The reference's voxel keys, int32 (n, 3): kind 0 DownsampleVoxel's
+    (p / v).floor().cast<int>() (point_cloud_utils.cpp:41-42), kind 1
+    CloudAccumulator's (p * float(1.0 / v)).cast<int>() (rs_replay_app.cpp:
+    91-92,108-110); NaN / out of int range -> INT_MIN (x86-64 cvttss2si)."""
+    a = _cloud(points)
+    with np.errstate(invalid="ignore", divide="ignore", over="ignore"):
+        if kind == 0:
+            q = np.floor(a / np.float32(voxel_size))
+        else:
+            q = np.trunc(a * np.float32(1.0 / float(voxel_size)))
+        ok = (q >= np.float32(-2147483648.0)) & (q < np.float32(2147483648.0))
+        return np.where(ok, np.where(ok, q, 0).astype(np.int64), np.iinfo(np.int32).min).astype(np.int32)
+
+
+def umap_order(keys):
+    """keys: (n, 3) int32, distinct, insertion order.  The insertion indices
+    in the order a real std::unordered_map (this toolchain's libstdc++, the
+    reference's classic boost::hash_combine) iterates them."""
+    k = np.ascontiguousarray(np.asarray(keys, np.int32).reshape(-1, 3))
+    out = np.zeros(len(k), np.int64)
+    lib().orc_umap_order(k.ctypes.data_as(_i), len(k), out.ctypes.data_as(C.POINTER(C.c_int64)))
+    return out
+
+
+def umap_schedule(n: int):
+    """(elements before the insert that rehashed, new bucket count) of a
+    default-constructed std::unordered_map receiving n distinct keys."""
+    cap = 128
+    out = np.zeros(2 * cap, np.int64)
+    k = lib().orc_umap_schedule(int(n), out.ctypes.data_as(C.POINTER(C.c_int64)), cap)
+    assert k <= cap
+    return [tuple(int(v) for v in out[2 * j:2 * j + 2]) for j in range(k)]
 
 
 def compute_covariances(cloud, use_gicp=False, tree: KDTree | None = None):
@@ -370,20 +413,25 @@ def compute_matches(src_feat, dst_feat, k=2):
 
 
 class Accumulator:
-    """CloudAccumulator (rs_replay_app.cpp:76-129), insertion order."""
+    """CloudAccumulator (rs_replay_app.cpp:76-129)."""
 
     def __init__(self, voxel_size=0.05):
+        self.voxel_size = float(voxel_size)
         self.h = lib().orc_accum_create(float(voxel_size))
 
     def add(self, T, cloud):
         a = _cloud(cloud)
         lib().orc_accum_add(self.h, _fp(_cm(T)), _fp(a), a.shape[0])
 
-    def extract(self):
+    def extract(self, order: str = "reference"):
+        """ExtractPointCloud (rs_replay_app.cpp:112-121): the reference's
+        std::unordered_map iteration order, or order="input" (insertion)."""
         n = lib().orc_accum_extract(self.h, None)
         out = np.zeros((n, 3), np.float32)
         lib().orc_accum_extract(self.h, _fp(out))
-        return out
+        if order == "input":
+            return out
+        return out[umap_order(vox_keys(out, self.voxel_size, 1))]
 
     def __del__(self):
         try:

@@ -460,8 +460,8 @@ def RemoveNans(cloud, ctx: Context | None = None) -> np.ndarray:
 
 def DownsampleVoxel(cloud, voxel_size: float, ctx: Context | None = None) -> np.ndarray:
     """point_cloud_utils.cpp:34-68: the first point of every voxel
-    floor(p / voxel_size).  Returned in ascending input index; the reference
-    returns the same points in its unordered_map's order (unspecified)."""
+    floor(p / voxel_size), in the reference's order: its std::unordered_map's
+    iteration (:54-57), replayed on the device (voxel.hip)."""
     ctx = ctx or get_context()
     a = L.as_cloud(cloud)
     out = np.zeros_like(a)
@@ -528,8 +528,8 @@ def PruneMatchesLowe(matches, src_fpfh, dst_fpfh, lowe_ratio: float = 0.9):
 class CloudAccumulator:
     """rs_replay_app.cpp:76-129 on the device: AddCloud(xfm, cloud) keeps
     the first point (after xfm) of every voxel (int)(p / voxel_size);
-    ExtractPointCloud() returns them in insertion order (the reference's
-    order is its unordered_map's: same set)."""
+    ExtractPointCloud() returns them in the reference's order, its
+    std::unordered_map's iteration (:112-121)."""
 
     def __init__(self, voxel_size: float = 0.05, ctx: Context | None = None):
         self.ctx = ctx or get_context()

@@ -7,9 +7,8 @@
 //   DownsampleVoxel (point_cloud_utils.cpp:34-68): one point per voxel
 //                   floor(p / voxel_size) -- the FIRST point (lowest index)
 //                   of each voxel, since the reference emplaces only when the
-//                   key is new.  The reference emits them in unordered_map
-//                   order (implementation-defined); here they come out in
-//                   ascending input index (deterministic).  The voxel key is
+//                   key is new -- emitted in the reference's order, its
+//                   std::unordered_map's iteration (k_umap_order).  The voxel key is
 //                   (int)floorf(p / v) per axis; a NaN / out-of-int-range
 //                   value maps to INT_MIN, what x86-64's cvttss2si yields
 //                   for the reference's cast (so NaN points share one voxel).
@@ -27,6 +26,7 @@
 #include <climits>
 #include <cmath>
 #include <cstring>
+#include <unordered_map>  // (libstdc++'s _Prime_rehash_policy: umap_schedule)
 
 #include "rst_device.hpp"
 #include "rst_internal.hpp"
@@ -226,6 +226,204 @@ int compact(rst_ctx* ctx, const float* d_xyz, int64_t n, int mode, const uint8_t
   return RST_OK;
 }
 
+// ---- the reference's std::unordered_map iteration order ------------------------------
+// DownsampleVoxel (point_cloud_utils.cpp:54-57,63-66) and
+// CloudAccumulator::ExtractPointCloud (rs_replay_app.cpp:112-121) emit their
+// points by iterating a std::unordered_map that received the distinct voxel
+// keys in input order (find, then emplace).  libstdc++'s table keeps one
+// singly-linked list: an insert into an empty bucket goes to the list's
+// front, any other to the front of its bucket's run; a rehash walks the old
+// list and re-inserts each node the same way.  So between rehashes the list
+// is one run per bucket, the bucket created later first, the later arrival
+// first inside a bucket, and at every level the order sorts by (creation of
+// the element's bucket, arrival), both descending -- arrival being the
+// element's position in the list the last rehash walked, or its insertion
+// index when it came after it.  k_umap_order replays that level by level
+// from the container's rehash schedule (umap_schedule: libstdc++'s own
+// _Prime_rehash_policy), with no list: per level the buckets' creation times
+// (atomicMin of arrival), their sizes, one suffix scan over arrivals for the
+// runs' starts, and each bucket's members ranked by arrival.  The hash is
+// the reference's boost::hash_combine over std::hash<int> / hash_value(int)
+// (both size_t(k)), Boost <= 1.80's classic form (oracle/rst_oracle_umap.cpp
+// pins the model against a real std::unordered_map, tests/test_oracle.py).
+constexpr int kUmapT = 1024;
+constexpr int kUmapMaxLevels = 48;
+struct UmapSched {
+  int nl;
+  int64_t r[kUmapMaxLevels];  // elements before the insert that rehashed
+  int64_t B[kUmapMaxLevels];  // the bucket count it rehashed to
+};
+
+__device__ __forceinline__ uint64_t boost_combine3(const Vox& k) {
+  uint64_t seed = 0;
+  const int v[3] = {k.x, k.y, k.z};
+#pragma unroll
+  for (int i = 0; i < 3; ++i) seed ^= (uint64_t)(int64_t)v[i] + 0x9e3779b9ull + (seed << 6) + (seed >> 2);
+  return seed;
+}
+
+// cross-wave reads of the scratch arrays at agent scope: some are written by
+// atomics, which act in L2 (no stale vL1 line is ever read)
+template <class T>
+__device__ __forceinline__ T ld(const T* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// one workgroup: exclusive scan of a[0, n) in place (forward) or the suffix
+// form s[i] = sum of a[j > i] (backward); returns the total
+__device__ int64_t wg_scan(int32_t* a, int64_t n, bool suffix, int64_t* part) {
+  const int t = threadIdx.x;
+  const int64_t per = (n + kUmapT - 1) / kUmapT;
+  const int64_t b0 = t * per, b1 = min(n, b0 + per);
+  int64_t sum = 0;
+  for (int64_t i = b0; i < b1; ++i) sum += ld(a + (suffix ? n - 1 - i : i));
+  part[t] = sum;
+  __syncthreads();
+  if (t == 0) {
+    int64_t run = 0;
+    for (int k = 0; k < kUmapT; ++k) {
+      const int64_t v = part[k];
+      part[k] = run;
+      run += v;
+    }
+    part[kUmapT] = run;
+  }
+  __syncthreads();
+  int64_t run = part[t];
+  for (int64_t i = b0; i < b1; ++i) {
+    const int64_t j = suffix ? n - 1 - i : i;
+    const int32_t v = ld(a + j);
+    __hip_atomic_store(a + j, (int32_t)run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    run += v;
+  }
+  const int64_t tot = part[kUmapT];
+  __syncthreads();
+  return tot;
+}
+
+struct UmapWs {
+  uint64_t* h;
+  int32_t *pos, *arr, *bk, *mem, *hs;     // [n]
+  int32_t *ctime, *cnt, *start, *fill;  // [B max]
+};
+
+__global__ __launch_bounds__(kUmapT) void k_umap_order(const float* __restrict__ pts, int64_t n, float v,
+                                                       int kind, UmapSched sc, UmapWs w,
+                                                       float* __restrict__ out) {
+  __shared__ int64_t part[kUmapT + 1];
+  const int t = threadIdx.x;
+  auto st = [](int32_t* p, int32_t x) { __hip_atomic_store(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+  for (int64_t e = t; e < n; e += kUmapT) w.h[e] = boost_combine3(vox_of(pts, e, v, kind));
+  __syncthreads();
+  for (int l = 0; l < sc.nl; ++l) {
+    const int64_t r = sc.r[l], B = sc.B[l];
+    const int64_t nl = l + 1 < sc.nl ? sc.r[l + 1] : n;
+    for (int64_t b = t; b < B; b += kUmapT) {
+      st(w.ctime + b, INT_MAX);
+      st(w.cnt + b, 0);
+      st(w.fill + b, 0);
+    }
+    for (int64_t a = t; a < nl; a += kUmapT) st(w.hs + a, 0);
+    __syncthreads();
+    // arrival (the walked list's position, or the insertion index), bucket
+    for (int64_t e = t; e < nl; e += kUmapT) {
+      const int32_t a = e < r ? ld(w.pos + e) : (int32_t)e;
+      const int32_t b = (int32_t)(ld(w.h + e) % (uint64_t)B);
+      st(w.arr + e, a);
+      st(w.bk + e, b);
+      atomicMin(w.ctime + b, a);
+      atomicAdd(w.cnt + b, 1);
+    }
+    __syncthreads();
+    // the buckets' member ranges, and each bucket's size at its creation's arrival
+    for (int64_t b = t; b < B; b += kUmapT) st(w.start + b, ld(w.cnt + b));
+    __syncthreads();
+    wg_scan(w.start, B, false, part);
+    for (int64_t e = t; e < nl; e += kUmapT) {
+      const int32_t b = ld(w.bk + e), a = ld(w.arr + e);
+      const int32_t slot = ld(w.start + b) + atomicAdd(w.fill + b, 1);
+      st(w.mem + slot, (int32_t)e);
+      if (a == ld(w.ctime + b)) st(w.hs + a, ld(w.cnt + b));
+    }
+    __syncthreads();
+    // hs[a] = the elements of buckets created after arrival a: a run's start
+    wg_scan(w.hs, nl, true, part);
+    // each bucket's members by arrival, descending, from its run's start
+    for (int64_t b = t; b < B; b += kUmapT) {
+      const int32_t c = ld(w.cnt + b);
+      if (c == 0) continue;
+      const int32_t s0 = ld(w.start + b), base = ld(w.hs + ld(w.ctime + b));
+      for (int32_t i = 0; i < c; ++i) {
+        const int32_t ei = ld(w.mem + s0 + i), ai = ld(w.arr + ei);
+        int32_t rank = 0;  // members arriving later come first
+        for (int32_t j = 0; j < c; ++j) rank += ld(w.arr + ld(w.mem + s0 + j)) > ai ? 1 : 0;
+        st(w.pos + ei, base + rank);
+      }
+    }
+    __syncthreads();
+  }
+  for (int64_t e = t; e < n; e += kUmapT) {
+    const int64_t o = ld(w.pos + e);
+    out[3 * o + 0] = pts[3 * e + 0];
+    out[3 * o + 1] = pts[3 * e + 1];
+    out[3 * o + 2] = pts[3 * e + 2];
+  }
+}
+
+// the rehash points of a default-constructed std::unordered_map receiving
+// n distinct keys one by one, from libstdc++'s own policy (max load 1, one
+// bucket before the first insert): (elements before the insert, new count)
+int umap_schedule(int64_t n, UmapSched* sc) {
+  std::__detail::_Prime_rehash_policy pol;
+  std::size_t nb = 1;
+  sc->nl = 0;
+  for (int64_t e = 0; e < n;) {
+    const auto rh = pol._M_need_rehash(nb, (std::size_t)e, 1);
+    if (rh.first) {
+      if (sc->nl >= kUmapMaxLevels) return RST_E_ARG;
+      sc->r[sc->nl] = e;
+      sc->B[sc->nl] = (int64_t)rh.second;
+      ++sc->nl;
+      nb = rh.second;
+    }
+    // no rehash check fires before the element count passes _M_next_resize
+    e = std::max<int64_t>(e + 1, std::min<int64_t>(n, (int64_t)pol._M_next_resize));
+  }
+  return RST_OK;
+}
+
+// out[0, n) = pts[0, n) (distinct voxels, insertion order) in the
+// reference's unordered_map iteration order; kind / v as vox_coord
+int umap_order_device(rst_ctx* ctx, const float* d_pts, int64_t n, float v, int kind, float* d_out) {
+  if (n <= 0) return RST_OK;
+  if (n >= ((int64_t)1 << 31) - 1) return RST_E_ARG;
+  UmapSched sc;
+  RST_CHECK(umap_schedule(n, &sc));
+  const int64_t bmax = sc.B[sc.nl - 1];
+  const size_t bytes = sizeof(uint64_t) * n + sizeof(int32_t) * (6 * (size_t)n + 4 * (size_t)bmax) + 256;
+  void* p = nullptr;
+  size_t cls = 0;
+  RST_CHECK(ctx_alloc(ctx, bytes, &p, &cls));
+  UmapWs w;
+  w.h = (uint64_t*)p;
+  int32_t* q = (int32_t*)(w.h + n);
+  w.pos = q;
+  w.arr = q + n;
+  w.bk = q + 2 * n;
+  w.mem = q + 3 * n;
+  w.hs = q + 4 * n;
+  w.ctime = q + 6 * n;
+  w.cnt = w.ctime + bmax;
+  w.start = w.cnt + bmax;
+  w.fill = w.start + bmax;
+  k_umap_order<<<1, kUmapT, 0, ctx->stream>>>(d_pts, n, v, kind, sc, w, d_out);
+  const hipError_t e = hipGetLastError();
+  hipStreamSynchronize(ctx->stream);
+  ctx_release(ctx, p, cls);
+  RST_HIP(e);
+  return RST_OK;
+}
+
 }  // namespace
 
 int remove_nans_device(rst_ctx* ctx, const float* d_xyz, int64_t n, float* d_out,
@@ -286,7 +484,16 @@ int downsample_voxel_device(rst_ctx* ctx, const float* d_xyz, int64_t n, float v
   }
   VoxWs w;
   RST_CHECK(first_per_voxel(ctx, d_xyz, n, voxel, 0, &w));
-  return compact(ctx, d_xyz, n, 1, w.flag, w.counts, w.counts + w.nb + 16, d_out, n_out);
+  // the first point of each voxel in input order, then the reference's
+  // unordered_map order (:54-57)
+  float* tmp = nullptr;
+  size_t cls = 0;
+  RST_CHECK(ctx_alloc(ctx, sizeof(float) * 3 * (size_t)n, (void**)&tmp, &cls));
+  int s = compact(ctx, d_xyz, n, 1, w.flag, w.counts, w.counts + w.nb + 16, tmp, n_out);
+  if (s >= 0) s = umap_order_device(ctx, tmp, *n_out, voxel, 0, d_out);
+  hipStreamSynchronize(ctx->stream);
+  ctx_release(ctx, tmp, cls);
+  return s;
 }
 
 // ---- CloudAccumulator (rs_replay_app.cpp:76-129) --------------------------------------
@@ -589,9 +796,32 @@ int rst_accum_size(const rst_accum* a, int64_t* n) {
 int rst_accum_extract(rst_accum* a, float* out, int64_t* n_out) {
   if (!a || !n_out || (a->count > 0 && !out)) return RST_E_ARG;
   RST_HIP(hipSetDevice(a->ctx->device));
-  if (a->count > 0) RST_CHECK(stage_d2h(a->ctx, out, a->list, sizeof(float) * 3 * a->count));
+  if (a->count > 0) {
+    // the insertion-ordered list in the reference's unordered_map order
+    // (rs_replay_app.cpp:112-121), then to the host
+    float* tmp = nullptr;
+    size_t cls = 0;
+    RST_CHECK(ctx_alloc(a->ctx, sizeof(float) * 3 * (size_t)a->count, (void**)&tmp, &cls));
+    int s = umap_order_device(a->ctx, a->list, a->count, a->inv, 1, tmp);
+    if (s >= 0) s = stage_d2h(a->ctx, out, tmp, sizeof(float) * 3 * a->count);
+    hipStreamSynchronize(a->ctx->stream);
+    ctx_release(a->ctx, tmp, cls);
+    RST_CHECK(s);
+  }
   *n_out = a->count;
   return RST_OK;
 }
 
 }  // extern "C"
+
+extern "C" int rst_debug_umap_schedule(int64_t n, int64_t* out, int64_t cap, int64_t* count) {
+  if (n < 0 || !count || (cap > 0 && !out)) return RST_E_ARG;
+  rst::UmapSched sc;
+  RST_CHECK(rst::umap_schedule(n, &sc));
+  for (int k = 0; k < sc.nl && k < cap; ++k) {
+    out[2 * k] = sc.r[k];
+    out[2 * k + 1] = sc.B[k];
+  }
+  *count = sc.nl;
+  return RST_OK;
+}

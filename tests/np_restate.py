@@ -199,3 +199,44 @@ def downsample_voxel(cloud: np.ndarray, voxel_size: float) -> np.ndarray:
     k = voxel_keys(a, voxel_size).astype(np.int32)
     _, first = np.unique(k, axis=0, return_index=True)
     return a[np.sort(first)]
+
+
+def boost_classic_hash(keys: np.ndarray) -> np.ndarray:
+    """seed = 0; per coordinate seed ^= size_t(k) + 0x9e3779b9 + (seed << 6)
+    + (seed >> 2) -- MatrixHash (point_cloud_utils.cpp:13-22) and VoxelHash
+    (rs_replay_app.cpp:78-84) with Boost <= 1.80's hash_combine, uint64."""
+    k = np.asarray(keys, np.int32).reshape(-1, 3).astype(np.int64).view(np.uint64)
+    seed = np.zeros(len(k), np.uint64)
+    with np.errstate(over="ignore"):
+        for c in range(3):
+            seed ^= k[:, c] + np.uint64(0x9E3779B9) + (seed << np.uint64(6)) + (seed >> np.uint64(2))
+    return seed
+
+
+def umap_order_model(keys: np.ndarray, schedule) -> np.ndarray:
+    """The iteration order of a libstdc++ std::unordered_map that received
+    `keys` (distinct, in order), from its rehash schedule alone (the model
+    voxel.hip's k_umap_order computes):  between rehashes the list is one run
+    per bucket, a bucket created later first, inside a bucket the later
+    arrival first (an insert into an empty bucket goes to the list's front,
+    any other to its bucket's front); a rehash walks the old list and
+    re-inserts each node the same way.  So at every level the order sorts
+    by (bucket's creation, arrival), both descending, where arrival = the
+    node's position in the list the rehash walked, or its insertion index for
+    keys inserted after it."""
+    h = boost_classic_hash(keys)
+    n = len(h)
+    pos = np.zeros(0, np.int64)
+    for lvl, (r, B) in enumerate(schedule):
+        nl = schedule[lvl + 1][0] if lvl + 1 < len(schedule) else n
+        a = np.arange(nl, dtype=np.int64)
+        a[:r] = pos[:r]
+        b = (h[:nl] % np.uint64(B)).astype(np.int64)
+        ctime = np.full(B, np.iinfo(np.int64).max)
+        np.minimum.at(ctime, b, a)
+        order = np.lexsort((-a, -ctime[b]))
+        pos = np.empty(nl, np.int64)
+        pos[order] = np.arange(nl)
+    out = np.empty(n, np.int64)
+    out[pos] = np.arange(n)
+    return out

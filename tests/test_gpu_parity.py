@@ -825,8 +825,23 @@ def test_downsample_voxel_full_frame_and_repeat(ctx):
     ref = O.downsample_voxel(cloud, PC.VOXEL)
     for _ in range(3):
         np.testing.assert_array_equal(A.DownsampleVoxel(cloud, PC.VOXEL, ctx), ref)
-    # idempotent: every kept point is the first of its voxel already
-    np.testing.assert_array_equal(A.DownsampleVoxel(ref, PC.VOXEL, ctx), ref)
+    # twice: every kept point is the first of its voxel already, the set is
+    # the same; the order is the container's over the new input order
+    # (the reference is not idempotent in order either)
+    np.testing.assert_array_equal(A.DownsampleVoxel(ref, PC.VOXEL, ctx), O.downsample_voxel(ref, PC.VOXEL))
+    assert len(O.downsample_voxel(ref, PC.VOXEL)) == len(ref)
+
+
+def test_downsample_voxel_reference_order_not_input_order(ctx):
+    """The output is the reference's std::unordered_map iteration order
+    (point_cloud_utils.cpp:54-57), which differs from the input order."""
+    K = driver.intrinsics(320, 240)
+    sc = driver.SyntheticScene(1)
+    cloud = driver.unproject(sc.render(sc.trajectory(2), K, noise_seed=3), K)
+    got = A.DownsampleVoxel(cloud, 0.05, ctx)
+    inp = O.downsample_voxel(cloud, 0.05, order="input")
+    assert not np.array_equal(got, inp)
+    np.testing.assert_array_equal(got, O.downsample_voxel(cloud, 0.05))
 
 
 def test_preprocess_device_entry_points(ctx):

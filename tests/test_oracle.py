@@ -278,18 +278,61 @@ def test_remove_nans_oracle_matches_numpy(name):
 @pytest.mark.parametrize("name", sorted(PC.cases()))
 def test_downsample_voxel_oracle_matches_numpy(name):
     cloud, v = PC.cases()[name]
-    got = O.downsample_voxel(cloud, v)
+    got = O.downsample_voxel(cloud, v, order="input")
     np.testing.assert_array_equal(got, NPR.downsample_voxel(cloud, v))
     # one point per occupied voxel, each the first of its voxel
     k = NPR.voxel_keys(cloud, v)
     assert len(got) == (len(np.unique(k, axis=0)) if len(cloud) else 0)
+    # the reference's order: the container's iteration over those points
+    ref = O.downsample_voxel(cloud, v)
+    keys = NPR.voxel_keys(got, v)
+    np.testing.assert_array_equal(ref, got[NPR.umap_order_model(keys, O.umap_schedule(len(got)))])
 
 
 def test_downsample_voxel_oracle_on_frame():
     cloud = PC.frame_cloud()
-    got = O.downsample_voxel(cloud, PC.VOXEL)
+    got = O.downsample_voxel(cloud, PC.VOXEL, order="input")
     np.testing.assert_array_equal(got, NPR.downsample_voxel(cloud, PC.VOXEL))
     assert 0 < len(got) < len(cloud)
+    ref = O.downsample_voxel(cloud, PC.VOXEL)
+    assert not np.array_equal(ref, got)  # (the container's order is not the input's)
+    np.testing.assert_array_equal(np.sort(ref.view(np.uint32).reshape(-1, 3), axis=0),
+                                  np.sort(got.view(np.uint32).reshape(-1, 3), axis=0))
+
+
+# ---- the reference's std::unordered_map order (rst_oracle_umap.cpp) ----------
+@pytest.mark.parametrize("n", [0, 1, 2, 13, 14, 29, 30, 59, 60, 127, 1000, 4099, 20000, 70000])
+def test_umap_order_model_matches_the_real_container(n):
+    """The level model (np_restate.umap_order_model: what voxel.hip's
+    k_umap_order computes) reproduces a real libstdc++ std::unordered_map's
+    iteration order with the classic boost::hash_combine, across every
+    rehash up to n -- negative, zero and INT_MIN coordinates included."""
+    rng = np.random.default_rng(n)
+    k = rng.integers(-40, 40, size=(3 * n + 64, 3)).astype(np.int32)
+    k[::7, 1] = np.iinfo(np.int32).min
+    k[::11] = 0
+    _, first = np.unique(k, axis=0, return_index=True)
+    k = k[np.sort(first)][:n]
+    assert len(k) == n
+    sch = O.umap_schedule(n)
+    np.testing.assert_array_equal(O.umap_order(k), NPR.umap_order_model(k, sch))
+
+
+def test_umap_schedule_of_the_library_matches_the_container():
+    """voxel.hip's rehash schedule (libstdc++'s _Prime_rehash_policy, host
+    code, rst_debug_umap_schedule) equals the bucket counts a real
+    std::unordered_map goes through (no GPU call)."""
+    import ctypes as C
+    from realsensetracker_amd import _lib as L
+    f = L.lib().rst_debug_umap_schedule
+    f.restype = C.c_int
+    f.argtypes = [C.c_int64, C.POINTER(C.c_int64), C.c_int64, C.POINTER(C.c_int64)]
+    for n in [0, 1, 13, 14, 29, 30, 1000, 123457, 2000000]:
+        out = np.zeros(256, np.int64)
+        cnt = C.c_int64(0)
+        assert f(n, out.ctypes.data_as(C.POINTER(C.c_int64)), 128, C.byref(cnt)) == 0
+        got = [tuple(int(v) for v in out[2 * j:2 * j + 2]) for j in range(cnt.value)]
+        assert got == O.umap_schedule(n), n
 
 
 # ---- f2: GICP oracle (point_cloud_utils.cpp:100-161, align_gicp.cpp:41-163) ----
@@ -379,7 +422,11 @@ def test_accumulator_oracle_matches_numpy():
     acc = O.Accumulator(0.05)
     for T, c in seq:
         acc.add(T, c)
-    np.testing.assert_array_equal(acc.extract(), _accum_numpy(seq, 0.05))
+    ins = _accum_numpy(seq, 0.05)
+    np.testing.assert_array_equal(acc.extract(order="input"), ins)
+    # ExtractPointCloud (:112-121): the container's iteration order
+    keys = O.vox_keys(ins, 0.05, 1)
+    np.testing.assert_array_equal(acc.extract(), ins[NPR.umap_order_model(keys, O.umap_schedule(len(ins)))])
 
 
 # ---- f3: FPFH oracle (fpfh.cpp:20-165,248-300) ----------------------------------
