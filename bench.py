@@ -150,6 +150,30 @@ def cpu_baseline(width: int, height: int, iters: int, levels: list | None = None
                                   "result); secondary baseline, for context"}}
 
 
+def callers_cpu_baseline(raw, iters: int):
+    """The reference callers' sequence (rs_replay_app.cpp:229,246-251) on the
+    oracle, 1 core: RemoveNans, DownsampleVoxel 0.05 of both clouds (the
+    reference's unordered_map order), AlignIcp3d(curr_down, prev_down, iters)
+    with its kd-tree built per call (the 4-argument overload,
+    align_icp.cpp:163-167) -- the same frames as the GPU leg, pairs 2-3."""
+    from oracle import oracle as O
+    O.set_threads(1)
+    ts, npts = [], []
+    for k in (2, 3):
+        t0 = time.perf_counter()
+        cur = O.downsample_voxel(O.remove_nans(raw[k]), 0.05)
+        prv = O.downsample_voxel(O.remove_nans(raw[k - 1]), 0.05)
+        O.align_icp(cur, prv, iters, tree=O.KDTree(prv, 16))
+        ts.append(time.perf_counter() - t0)
+        npts.append(len(cur))
+    ms = 1000.0 * float(np.mean(ts))
+    return {"ms_per_pair": ms, "iterations_per_s": iters / (ms * 1e-3), "cores": 1, "kind": "port",
+            "points_per_cloud": int(np.mean(npts)), "cpu": cpu_model(),
+            "sample": f"2 frame pairs of the callers' workload, {iters} P2POINT_REF iterations each, "
+                      "oracle/rst_oracle.c -O3 (reference arithmetic, nanoflann-style kd-tree "
+                      "leaf 16 built per call), preprocessing included"}
+
+
 def load_traffic():
     """HBM bytes per iteration of the NN pass (k_icp_nn + k_icp_fb) from a
     committed PMC summary (profiles/pmc_*.json, scripts/pmc_traffic.py) --
@@ -573,6 +597,11 @@ def main():
         callers["note"] = ("rs_replay_app.cpp:229,246-251 per frame: RemoveNans, DownsampleVoxel "
                            "0.05 of both clouds, AlignIcp3d(curr_down, prev_down, 128) with its "
                            "index built per call; host clouds (PCIe-inclusive), one pair at a time")
+        if not a.no_cpu and world == 1:
+            callers["cpu_baseline"] = callers_cpu_baseline(raw, a.iters)
+            for name in ("ref_sums", "fp64_sums"):
+                callers[name]["speedup_vs_cpu"] = (callers["cpu_baseline"]["ms_per_pair"] /
+                                                   callers[name]["ms_per_pair"])
 
     # ---- the tracker's GICP loop (rs_tracker.cpp:79-87; extra fields) ------------
     # per frame: DownsampleVoxel(curr, 0.1); ComputeAlignment(prev, curr, &T)
