@@ -307,6 +307,7 @@ struct AccArgs {
   float pmu;                       // P2PLANE: Geman-McClure scale on r^2
   float max_d2;                    // P2PLANE: correspondence rejection
   int32_t pos0;                    // sorted position of dst[0]
+  int32_t full;                    // RST_SUM_REF: every lane writes its record (q, d2)
 };
 
 // P2POINT_REF.  Single pass over the correspondences with the source
@@ -324,7 +325,7 @@ struct P2PointAcc {
   // position; no neighbour (bp < 0) -> dst[0], d2 = FLT_MAX
   __device__ static void add(double (&v)[NV], const BvhView& bv, const AccArgs& a, const Uni& u,
                              const float4& s, float px, float py, float pz, float bd, int bp,
-                             float4 q) {
+                             float4 q, bool same = false) {
     (void)px; (void)py; (void)pz;
     const float l = u.mu / (bd + u.mu);  // :116-117
     const float w = l * l;
@@ -351,7 +352,7 @@ struct P2PlaneAcc {
   static constexpr bool kSums = true;
   __device__ static void add(double (&v)[NV], const BvhView& bv, const AccArgs& a, const Uni& u,
                              const float4& s, float px, float py, float pz, float bd, int bp,
-                             float4 q) {
+                             float4 q, bool same = false) {
     (void)u; (void)s; (void)bv;
     if (bp < 0 || !(bd <= a.max_d2)) return;
     const float4 nn = a.nrm[bp];
@@ -391,8 +392,14 @@ struct RefAcc {
   static constexpr bool kSums = false;
   __device__ static void add(double (&v)[NV], const BvhView& bv, const AccArgs& a, const Uni& u,
                              const float4& s, float px, float py, float pz, float bd, int bp,
-                             float4 q) {
+                             float4 q, bool same = false) {
     (void)v; (void)u; (void)px; (void)py; (void)pz;
+    // a lane whose neighbour is the one it had (certified, or found again)
+    // leaves its record alone: q is there already, and k_cov_ref recomputes
+    // d2 from the pose (every iteration writing every record was 16 B per
+    // point of scattered writes, ~26 B per point of write traffic, r05 PMC);
+    // the last iteration writes them all, the cost chain reads d2
+    if (same && !a.full) return;
     if (bp < 0) q = bv.pts[a.pos0];
     a.corr[f2i(s.w)] = make_float4(q.x, q.y, q.z, bd);
   }
@@ -495,6 +502,7 @@ __global__ __launch_bounds__(kBS) void k_cov_ref(const float4* __restrict__ srco
   const float dm0 = st->seq[0] / nf, dm1 = st->seq[1] / nf, dm2 = st->seq[2] / nf;
   const float sm0 = st->smean[0], sm1 = st->smean[1], sm2 = st->smean[2];
   const float mu = st->mu;
+  const Pose3 P = load_pose(st);
   double v[9];
 #pragma unroll
   for (int k = 0; k < 9; ++k) v[k] = 0.0;
@@ -502,7 +510,13 @@ __global__ __launch_bounds__(kBS) void k_cov_ref(const float4* __restrict__ srco
        i += (int64_t)gridDim.x * kBS) {
     const float4 s = srco[i];
     const float4 c = corr[i];
-    const float l = mu / (c.w + mu);
+    // d2 of the search (:112), recomputed: the records of lanes that kept
+    // their neighbour are not rewritten (RefAcc::add); the same transform and
+    // distance arithmetic, so the same bits; no neighbour -> FLT_MAX
+    float px, py, pz;
+    xform(P, s.x, s.y, s.z, px, py, pz);
+    const float d2 = finite3(px, py, pz) ? d2_ref(px, py, pz, c.x, c.y, c.z) : FLT_MAX;
+    const float l = mu / (d2 + mu);
     const float w = l * l;
     const float a0 = w * (c.x - dm0), a1 = w * (c.y - dm1), a2 = w * (c.z - dm2);
     const float b0 = s.x - sm0, b1 = s.y - sm1, b2 = s.z - sm2;
@@ -720,7 +734,7 @@ __global__ __launch_bounds__(kBS, RST_NN_MIN_WAVES) void k_icp_nn(BvhView bv, Ad
       }
       // the certified and the non-finite queries' outputs (their own lanes)
       if (certified)
-        Acc::add(v, bv, aa, u, s, px, py, pz, dq, f2i(tq.w) & kPosMask, tq);
+        Acc::add(v, bv, aa, u, s, px, py, pz, dq, f2i(tq.w) & kPosMask, tq, true);
       else if (act && !fin)
         Acc::add(v, bv, aa, u, s, px, py, pz, FLT_MAX, -1, tq);
       __syncthreads();
@@ -827,7 +841,7 @@ __global__ __launch_bounds__(kBS, RST_NN_MIN_WAVES) void k_icp_nn(BvhView bv, Ad
       const int pos = pr.pos[0];
       nnq[i] = make_float4(pq.x, pq.y, pq.z, i2f(pos | (g > 0.f ? kCertBit : 0)));
       if (g > 0.f) cert[i] = make_float4(px, py, pz, g);
-      Acc::add(v, bv, aa, u, s, px, py, pz, pr.d[0], pos, pq);
+      Acc::add(v, bv, aa, u, s, px, py, pz, pr.d[0], pos, pq, wb >= 0 && pos == (wb & kPosMask));
       need = false;
     }
 #if RST_DIAG
@@ -868,7 +882,7 @@ __global__ __launch_bounds__(kBS, RST_NN_MIN_WAVES) void k_icp_nn(BvhView bv, Ad
     qcntf[tb] = totalf;
   }
   if (certified)
-    Acc::add(v, bv, aa, u, s, px, py, pz, dq, f2i(tq.w) & kPosMask, tq);
+    Acc::add(v, bv, aa, u, s, px, py, pz, dq, f2i(tq.w) & kPosMask, tq, true);
   else if (act && !fin)  // no neighbour: the query's untouched outputs
     Acc::add(v, bv, aa, u, s, px, py, pz, FLT_MAX, -1, tq);
   if constexpr (Acc::kSums) block_sum_to_slab<Acc::NV, kBS>(v, lds, slab + (int64_t)tb * Acc::RS);
@@ -1843,6 +1857,7 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
   aa.pmu = opts.p2plane_mu;
   aa.max_d2 = opts.p2plane_max_dist > 0 ? opts.p2plane_max_dist * opts.p2plane_max_dist : FLT_MAX;
   aa.pos0 = tgt->pos0;
+  aa.full = 1;
   const AdjView av = adj_of(tgt);
   const size_t fb_lds = 2 * sizeof(int) * ((size_t)nblk + 1);
 
@@ -1879,6 +1894,8 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
       // dst_mean (:113,122) and -- last iteration only: the reference reads
       // only that one (:104,157) -- the cost (:120), k_cov_ref the
       // covariance of the float products (:125-136)
+      // (the last iteration's records all written: its cost chain reads d2)
+      aa.full = it + 1 == opts.max_iter || ctx->seq_trace ? 1 : 0;
       if (n_local > 0) {
         k_icp_nn<RefAcc><<<nblk, kBS, 0, st>>>(bv, av, tgt->pix, aa, src->pts, n_local, ctx->d_state,
                                                nnq, cert, qbuf, qcnt, slab);
@@ -2103,6 +2120,7 @@ int icp_debug_partials(rst_ctx* ctx, const rst_target* src, const rst_target* tg
   k_debug_state<<<1, 64, 0, st>>>(ctx->d_state, dsm, mu, iter);
   AccArgs aa;
   aa.corr = nullptr;
+  aa.full = 1;
   aa.nrm = tgt->nrm;
   aa.pmu = opts.p2plane_mu;
   aa.max_d2 = opts.p2plane_max_dist > 0 ? opts.p2plane_max_dist * opts.p2plane_max_dist : FLT_MAX;
