@@ -40,6 +40,11 @@ struct Chain {
   std::vector<SbMap> sbm;
   int stats[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   int work[3] = {0, 0, 0};  // leaf maps, group maps, superblock maps built
+  // a stretch of a longer chain (the sharded loop: seqsum.hip's p0 / s_in):
+  // the fp64 prefix before it (the guesses' offset) and the chain's value
+  // where it starts (the walk's start)
+  double p0 = 0.0;
+  float s0 = 0.0f;
   bool fresh = false;       // incremental with a fresh front (reuse needs the same base)
 };
 
@@ -57,7 +62,7 @@ void front(Chain& C) {
     const int64_t e0 = (int64_t)t * kTile;
     std::vector<float> xs(kTile + kW);
     for (int i = 0; i < kTile + kW; ++i) xs.at(i) = e0 + i < n ? C.x.at(e0 + i) : 0.0f;
-    double P = 0.0;
+    double P = C.p0;
     for (int i = 0; i < t; ++i)
       if (std::isfinite(tf.at(i))) P += (double)tf.at(i);
     std::vector<double> wsum(kBlocksPerTile);
@@ -204,7 +209,7 @@ void maps(Chain& C, const std::vector<uint8_t>* dirty = nullptr) {
     for (int i = 0; i <= nblk; ++i) sbs.at(i) = C.bs.at(ba + i) - ea;
     for (int i = 0; i <= ngr; ++i) sgs.at(i) = C.gs.at(ga + i) - ba;
     const int tb = ba / kBlocksPerTile;
-    double base = 0.0;
+    double base = C.p0;
     for (int i = 0; i < tb; ++i) base += C.tinc.at(i);
     for (int b = tb * kBlocksPerTile; b < ba; ++b) base += C.inc.at(b);
     std::vector<double> Gd(kMaxSbBlocks + 1);
@@ -394,7 +399,7 @@ bool walk_try(float& s, const MapHdr& h, const MapEnt* e, int nent) {
 }
 
 float walk(Chain& C) {
-  float s = 0.0f;
+  float s = C.s0;
   int64_t pos_nf = -1;
   for (int k = 0; k < C.nk && pos_nf < 0; ++k) {
     ++C.stats[0];
@@ -505,7 +510,20 @@ int main(int argc, char** argv) {
         }
         for (int j = 0; j < 8; ++j) C.stats[j] = 0;
         for (int j = 0; j < 3; ++j) C.work[j] = 0;
-        float s = 0.0f;
+        // EMU_P0="p,p,p,p" (fp64) / EMU_S0="hex,hex,hex,hex" (float bits): a stretch
+        // of a longer chain, per chain
+        if (const char* e = getenv("EMU_P0")) {
+          const char* q = e;
+          for (int j = 0; j < c && q; ++j) q = std::strchr(q, ',') ? std::strchr(q, ',') + 1 : nullptr;
+          C.p0 = q ? std::strtod(q, nullptr) : 0.0;
+        }
+        if (const char* e = getenv("EMU_S0")) {
+          const char* q = e;
+          for (int j = 0; j < c && q; ++j) q = std::strchr(q, ',') ? std::strchr(q, ',') + 1 : nullptr;
+          const uint32_t u = q ? (uint32_t)std::strtoul(q, nullptr, 16) : 0u;
+          std::memcpy(&C.s0, &u, 4);
+        }
+        float s = C.s0;
         if (n > 0) {
           C.fresh = inc_now && incr_mode == 2;
           if (!inc_now || C.fresh) {

@@ -27,14 +27,22 @@ def binary(sanitize: bool = False) -> Path:
     return out
 
 
-def emulate(x, sanitize=False):
-    """(sums as uint32 bits [4], walk stats [4][7]) of a float4 stream"""
+def emulate(x, sanitize=False, p0=None, s0=None):
+    """(sums as uint32 bits [4], walk stats [4][10]) of a float4 stream.
+    p0 (4 fp64) / s0 (4 float32): the stream is a stretch of a longer chain
+    -- the fp64 prefix before it (the guesses' offset) and the chain's value
+    where it starts (the walk's start), as the sharded loop's relay runs it."""
     x = np.ascontiguousarray(x, np.float32).reshape(-1, 4)
+    env = dict(os.environ)
+    if p0 is not None:
+        env["EMU_P0"] = ",".join(repr(float(v)) for v in p0)
+    if s0 is not None:
+        env["EMU_S0"] = ",".join("%08x" % int(v) for v in np.asarray(s0, np.float32).view(np.uint32))
     with tempfile.TemporaryDirectory() as d:
         f = Path(d) / "in.f32"
         x.tofile(f)
         r = subprocess.run([str(binary(sanitize)), str(f), str(len(x)), "4"], capture_output=True,
-                           text=True)
+                           text=True, env=env)
     if r.returncode != 0:
         raise RuntimeError(f"emulation failed: {r.stdout[-500:]} {r.stderr[-2000:]}")
     rows = [ln.split() for ln in r.stdout.splitlines() if ln.strip()]

@@ -176,3 +176,68 @@ def test_shard_bounds_tile():
             assert max(sizes) - min(sizes) <= 1
     with pytest.raises(ValueError):
         shard_bounds(10, 2, 2)
+
+
+# ---- RST_SUM_REF sharded by relay ----------------------------------
+def _relay_worker(rank, world, port, out, x):
+    """Rank r holds the contiguous stretch [lo, hi) of the correspondence
+    stream.  One all-gather of the ranks' fp64 totals gives the fp64 prefix
+    before the stretch (its guesses' offset); the chain's value at the
+    stretch start comes from rank r - 1, the stretch is mapped and walked
+    locally (the kernels' arithmetic: tests/cpp/seqsum_emu.cpp), its end goes
+    to rank r + 1, and the last rank broadcasts the sums."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sys
+        from pathlib import Path
+        sys.path.insert(0, str(Path(__file__).resolve().parent))
+        from seqsum_emu import emulate
+        lo, hi = shard_bounds(len(x), world, rank)
+        mine = x[lo:hi]
+        tot = torch.tensor(np.where(np.isfinite(mine), mine, 0).astype(np.float64).sum(0))
+        tots = [torch.zeros(4, dtype=torch.float64) for _ in range(world)]
+        dist.all_gather(tots, tot)
+        p0 = sum((t.numpy() for t in tots[:rank]), np.zeros(4))
+        s_in = torch.zeros(4, dtype=torch.float32)
+        if rank > 0:
+            dist.recv(s_in, src=rank - 1)
+        bits, st = emulate(mine, p0=p0, s0=s_in.numpy())
+        s_out = torch.from_numpy(bits.view(np.float32).copy())
+        if rank + 1 < world:
+            dist.send(s_out, dst=rank + 1)
+        dist.broadcast(s_out, src=world - 1)
+        got = [None] * world
+        dist.all_gather_object(got, (s_out.numpy().view(np.uint32).tolist(), st[:, :2].tolist()))
+        if rank == 0:
+            out.put(got)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_ref_sums_relay_gloo(world):
+    """The sharded loop's sequential sums without moving correspondences:
+    every rank gets the unsharded chain's bits (numpy's sequential float32
+    accumulate), and the stretches' superblock maps hit with only the fp64
+    prefix as the guesses' offset.  xGMI bytes per iteration: R x 32 B of
+    totals, 16 B per relay hop, 16 B broadcast."""
+    rng = np.random.default_rng(world)
+    n = 120000
+    u = np.tile(np.arange(400), n // 400 + 1)[:n]
+    x = np.stack([(u - 200) / 385.0 * 2.0, np.full(n, 1.0) + rng.normal(size=n) * 0.1,
+                  2.0 + rng.normal(size=n) * 0.01, rng.random(n)], 1).astype(np.float32)
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    mp.start_processes(_relay_worker, args=(world, port, q, x), nprocs=world, start_method="spawn",
+                       join=True)
+    got = q.get()
+    want = np.add.accumulate(np.concatenate([np.zeros((1, 4), np.float32), x]), axis=0,
+                             dtype=np.float32)[-1].view(np.uint32).tolist()
+    assert all(g[0] == want for g in got), (got, want)
+    # (every rank's superblock jumps: most hit with the fp64-prefix guesses)
+    hits = sum(sum(h for _, h in g[1]) for g in got)
+    tries = sum(sum(t for t, _ in g[1]) for g in got)
+    assert hits >= 0.8 * tries, (hits, tries)
