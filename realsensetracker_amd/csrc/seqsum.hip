@@ -509,6 +509,8 @@ static_assert(kBuildT >= kMaxSbBlocks + 1 && kBuildT >= kMaxSbGroups * kGroupR &
               "map workgroup size");
 static_assert(sizeof(Leaf) == 64, "a leaf map is four int4");
 constexpr int kXPad = kMaxSbElems + kMaxSbElems / kW + 2 * kW;  // padded staging (see xp)
+constexpr int kListCap = (kLeafR - 1) * kMaxSbBlocks;
+static_assert(kListCap >= kMaxSbGroups * kGroupR, "the group list shares the leaf list's storage");
 
 // A composite lane's step through a child map, without branches (the
 // lanes of a wavefront take different cases in the same step; a chain of
@@ -564,7 +566,10 @@ struct BuildLds {
   int sbs[kMaxSbBlocks + 1];   // block starts, relative to the superblock's first element
   int sgs[kMaxSbGroups + 1];   // group starts, relative to its first block
   int xneed[kMaxSbBlocks][kLeafR - 1];  // the extra candidates' lattice needs
-  int list[kBuildT];           // extra leaf candidates (block << 2 | r), then (group << 4 | r)
+  // extra leaf candidates (block << 2 | r): up to kLeafR - 1 per block (a
+  // stream of exact ties needs them for most blocks); then the group list
+  // (group << 4 | r), at most kMaxSbGroups x kGroupR
+  int list[kListCap];
   int nlist;
   int bad;
   double base[2];              // fp64 increments of the tiles before the superblock's first
@@ -692,18 +697,22 @@ __global__ __launch_bounds__(kBuildT) void k_sq_build(SqView v) {
     more = act && !p.opaque && m0 >= 1 && m0 <= kLeafM;
     if (more) {
       const int at = atomicAdd(&W.nlist, kLeafR - 1);
+      if (at + kLeafR - 1 <= kListCap) {  // (always: kListCap covers every block)
 #pragma unroll
-      for (int r = 1; r < kLeafR; ++r) W.list[at + r - 1] = tid << 2 | r;
+        for (int r = 1; r < kLeafR; ++r) W.list[at + r - 1] = tid << 2 | r;
+      } else {
+        atomicOr(v.err, 64);
+      }
     }
   }
   __syncthreads();
   {
     // the listed extra candidates, one lane each (rare; uniform skip)
-    const int nl = W.nlist;
+    const int nl = min(W.nlist, kListCap);
     for (int j0 = 0; j0 < nl; j0 += kBuildT) {
       const int j = j0 + tid;
       const int code = j < nl ? W.list[j] : 0;
-      const int bl = code >> 2, r = code & 3;
+      const int bl = min(code >> 2, nblk - 1), r = code & 3;
       const int xa = j < nl ? W.sbs[bl] : 0, xl = j < nl ? W.sbs[bl + 1] - xa : 0;
       const int xb = ba + bl;
       const double base = (xb / kBlocksPerTile) == k ? W.base[0] : W.base[1];
@@ -784,12 +793,13 @@ __global__ __launch_bounds__(kBuildT) void k_sq_build(SqView v) {
     for (int r = 0; r < kGroupR; ++r) o.e[r] = MapEnt{0.0f, 1, 0};
     if (R > 1) {
       const int at = atomicAdd(&W.nlist, R - 1);
-      for (int r = 1; r < R; ++r) W.list[at + r - 1] = gi << 4 | r;
+      for (int r = 1; r < R; ++r)
+        if (at + r - 1 < kListCap) W.list[at + r - 1] = gi << 4 | r;  // (<= 496 entries: always)
     }
   }
   __syncthreads();
   {
-    const int nl = W.nlist;  // <= 31 x 16 <= kBuildT
+    const int nl = min(W.nlist, kBuildT);  // <= 31 x 16 <= kBuildT
     const int j = tid;
     if (j - lane < nl) {  // (uniform per wavefront: waves past the list skip)
       const bool ea_ = j < nl;

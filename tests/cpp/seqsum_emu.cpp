@@ -250,7 +250,7 @@ void maps(Chain& C, const std::vector<uint8_t>* dirty = nullptr) {
         static long long h[8];
         static int calls;
         h[p[0].opaque ? 7 : (exact_only ? 6 : m)]++;
-        if (++calls % 100000 == 0)
+        if (++calls % 1000 == 0)
           std::fprintf(stderr, "mhist m0 %lld m1 %lld m2 %lld exact_only %lld opaque %lld\n", h[0], h[1], h[2], h[6], h[7]);
       }
       Leaf& o = lf.at(bl);
