@@ -10,12 +10,11 @@
 //
 // RST_SUM_REF (the reference's sequential fp32 sums) shards too: the shards
 // are contiguous stretches of the reference's source order, rank r holding
-// [off_r, off_r + n_r).  Each iteration every rank all-gathers the
-// correspondences (q, d2 per source point, 16 B) into the whole source's
-// order -- one grouped set of broadcasts, ranks' counts may differ -- and
-// walks the global chains redundantly (seqsum.hip), so every rank holds the
-// same bit-exact dst_mean and cost; the covariance stays a sharded fp64
-// partial sum (9 doubles all-reduced).
+// [off_r, off_r + n_r).  Each iteration every rank maps the chains of its own
+// stretch and the chains' values travel rank to rank (comm_relay_seqsum:
+// < 1 KB per iteration), so every rank holds the same bit-exact dst_mean and
+// cost; the covariance stays a sharded fp64 partial sum (9 doubles
+// all-reduced).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -35,6 +34,7 @@ struct rst_comm {
   std::vector<int64_t> counts, offsets;
   int64_t* d_cnt = nullptr;     // device scratch of the count all-gather [R + 1]
   int64_t* d_layout = nullptr;  // the exchanged counts on the device [R]
+  double* d_relay = nullptr;    // comm_relay_seqsum's exchange buffers
 };
 
 namespace rst {
@@ -131,19 +131,72 @@ int comm_layout_check(rst_comm* comm, hipStream_t st, int32_t* d_guard) {
   return RST_OK;
 }
 
-// buf[off_r, off_r + n_r) of rank r to every rank (in place; counts may
-// differ): grouped broadcasts, one per non-empty shard
-int comm_allgatherv_f4(rst_comm* comm, float4* buf, hipStream_t st) {
-  if (!comm || !comm->comm || !comm->have_layout) return RST_E_ARG;
-  if (ncclGroupStart() != ncclSuccess) return RST_E_COMM;
-  ncclResult_t e = ncclSuccess;
-  for (int r = 0; r < comm->nranks && e == ncclSuccess; ++r) {
-    const size_t cnt = (size_t)comm->counts[r] * 4;
-    if (cnt == 0) continue;
-    float* p = reinterpret_cast<float*>(buf + comm->offsets[r]);
-    e = ncclBroadcast(p, p, cnt, ncclFloat32, r, comm->comm, st);
+namespace {
+// the relay's guesses: the fp64 prefix of the ranks before this one (their
+// chain totals), plus the drift the previous iteration's true start showed
+__global__ void k_relay_p0(const double* __restrict__ tots, int R, int rank, const double* __restrict__ drift,
+                           double* __restrict__ p0raw, double* __restrict__ p0) {
+  const int c = threadIdx.x;
+  if (c >= 4) return;
+  double s = 0.0;
+  for (int r = 0; r < rank && r < R; ++r) s += tots[r * 4 + c];
+  p0raw[c] = s;
+  p0[c] = s + (drift ? drift[c] : 0.0);
+}
+// the float chain's value at the stretch start against the fp64 prefix there
+// (the next iteration's guesses start from it; the chains move little)
+__global__ void k_relay_drift(const float* __restrict__ s_in, const double* __restrict__ p0raw,
+                              double* __restrict__ drift) {
+  const int c = threadIdx.x;
+  if (c >= 4) return;
+  const float v = s_in[c];
+  drift[c] = isfinite(v) && isfinite(p0raw[c]) ? (double)v - p0raw[c] : 0.0;
+}
+}  // namespace
+
+// The reference's sequential fp32 sums over the ranks' stretches, in order
+// (align_icp.cpp:113,120; point_cloud_utils.cpp:94-96), without moving the
+// stretches: every rank maps its own stretch (seqsum.hip) with the fp64
+// prefix of the ranks before it as the guesses' offset (one all-gather of
+// the ranks' fp64 totals, 32 B each), rank r - 1 hands rank r the chains'
+// value at the stretch start (ncclRecv / ncclSend, 16 B), rank r walks its
+// stretch from it, and the last rank broadcasts the sums (16 B).  The walks
+// follow one another -- a sequential sum has no other decomposition -- but
+// each covers n / R elements, with its own descents, and the maps, the
+// bulk of the work, shrink by R.  d_out: 4 floats on every rank; d_drift (4
+// doubles, zero at an align's start, or null) carries the start's drift
+// from one iteration to the next.
+int comm_relay_seqsum(rst_comm* comm, const float4* d_x, int64_t n_local, int nch, void* sqws,
+                      float* d_out, hipStream_t st, double* d_drift, int* d_stats, int iter) {
+  if (!comm || !comm->comm || nch < 1 || nch > 4) return RST_E_ARG;
+  const int R = comm->nranks, rank = comm->rank;
+  if (!comm->d_relay) {
+    const size_t b = sizeof(double) * (4 + 4 * (size_t)R + 8) + sizeof(float) * 4;
+    if (hipMalloc(&comm->d_relay, b) != hipSuccess) return RST_E_NOMEM;
   }
-  if (ncclGroupEnd() != ncclSuccess || e != ncclSuccess) return RST_E_COMM;
+  double* tot4 = comm->d_relay;
+  double* tots = tot4 + 4;
+  double* p0raw = tots + 4 * R;
+  double* p0 = p0raw + 4;
+  float* s_in = (float*)(p0 + 4);
+  RST_CHECK(seqsum_totals(d_x, n_local, nch, sqws, tot4, st, iter));
+  if (ncclAllGather(tot4, tots, 4, ncclFloat64, comm->comm, st) != ncclSuccess) return RST_E_COMM;
+  k_relay_p0<<<1, 64, 0, st>>>(tots, R, rank, d_drift, p0raw, p0);
+  RST_HIP(hipGetLastError());
+  if (rank > 0) {
+    if (ncclRecv(s_in, 4, ncclFloat32, rank - 1, comm->comm, st) != ncclSuccess) return RST_E_COMM;
+  } else {
+    RST_HIP(hipMemsetAsync(s_in, 0, sizeof(float) * 4, st));
+  }
+  const SqStretch sx{p0, s_in, true};
+  RST_CHECK(seqsum_enqueue(d_x, n_local, nch, sqws, d_out, st, d_stats, 7, iter, false, &sx));
+  if (rank + 1 < R && ncclSend(d_out, 4, ncclFloat32, rank + 1, comm->comm, st) != ncclSuccess)
+    return RST_E_COMM;
+  if (ncclBroadcast(d_out, d_out, 4, ncclFloat32, R - 1, comm->comm, st) != ncclSuccess) return RST_E_COMM;
+  if (d_drift) {
+    k_relay_drift<<<1, 64, 0, st>>>(s_in, p0raw, d_drift);
+    RST_HIP(hipGetLastError());
+  }
   return RST_OK;
 }
 
@@ -184,9 +237,10 @@ int rst_comm_create(rst_ctx* ctx, const char id[RST_COMM_ID_BYTES], int nranks, 
 int rst_comm_destroy(rst_comm* comm) {
   if (!comm) return RST_OK;
   if (comm->comm) ncclCommDestroy(comm->comm);
-  if (comm->d_cnt) {
+  if (comm->d_cnt || comm->d_relay) {
     (void)hipSetDevice(comm->device);
-    (void)hipFree(comm->d_cnt);
+    if (comm->d_cnt) (void)hipFree(comm->d_cnt);
+    if (comm->d_relay) (void)hipFree(comm->d_relay);
   }
   delete comm;
   return RST_OK;

@@ -1765,7 +1765,7 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
   // global quantities under sharding: the shard layout is exchanged when the
   // caller's n_total asks for it and checked on the device every align
   // (comm.hip); this rank runs with its count of the layout
-  int64_t shard_off = 0;
+  int64_t shard_off = 0;  // (the relay needs no offset: every rank keeps its own stretch)
   if (comm) RST_CHECK(comm_shard_layout(comm, src->m, opts.n_total, st, &n_total, &shard_off, &n_local, nullptr));
   // one scratch buffer: [centroid / kernel-1 slab | kernel-2 slab | totals]
   const int nblk = blocks_for(n_local);
@@ -1791,29 +1791,27 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
   // per source point: sorted target position of its last neighbour (warm
   // start of the next iteration's exact search; -1 = cold); the fallback
   // queue (one kBS segment per kernel-1 block) and its per-block counts;
-  // RST_SUM_REF: the correspondences and the source in original order (the
-  // whole source's when sharded: this shard writes [shard_off, + n_local))
+  // RST_SUM_REF: the correspondences and the source in original order (this
+  // shard's stretch when sharded: the chains relay rank to rank, comm.hip)
   float4* nnq = nullptr;  // last neighbour (p, pos | kCertBit), -1 = cold
   int32_t *qbuf = nullptr, *qcnt = nullptr;  // near queue, then far queue (k_icp_nn)
   float4* cert = nullptr;  // far-point certificates (read only under kCertBit)
-  float4 *corr = nullptr, *srco = nullptr, *corrg = nullptr, *srcog = nullptr;
+  float4 *corr = nullptr, *srco = nullptr;
   void* sqws = nullptr;  // seqsum.hip tables (RST_SUM_REF)
   {
     const size_t np = (size_t)std::max<int64_t>(n_local, 1);
-    const size_t ng = refsum ? (size_t)std::max<int64_t>(n_total, 1) : 0;
+    const size_t ng = refsum ? np : 0;
     const size_t nq = (size_t)nblk * kBS;
     void* w = nullptr;
-    const size_t sqb = refsum ? seqsum_bytes(n_total) : 0;
+    const size_t sqb = refsum ? seqsum_bytes(n_local) : 0;
     RST_CHECK(ctx_workspace(ctx, sizeof(float4) * (2 * np + 2 * ng) + sizeof(int4) * nq +
                                      sizeof(int32_t) * (2 * nq + 2 * nblk + 64) + sqb + 256,
                             &w));
     cert = (float4*)w;
     nnq = cert + np;
     if (refsum) {
-      corrg = nnq + np;
-      srcog = corrg + ng;
-      corr = corrg + shard_off;
-      srco = srcog + shard_off;
+      corr = nnq + np;
+      srco = corr + ng;
     }
     qbuf = (int32_t*)(cert + 2 * np + 2 * ng);
     qcnt = qbuf + 2 * nq;
@@ -1830,11 +1828,16 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
   ia.n = n_total;
   int crows = 0;
   float* fsum = (float*)totals;  // RST_SUM_REF: the centroid's sequential sums
+  double* drift = totals + 40;   // sharded RST_SUM_REF: the relay's start drift (comm.hip)
   if (refsum) {
     if (n_local > 0) k_gather_orig<<<blocks_for(n_local), kBS, 0, st>>>(src->pts, src->inv, n_local, srco);
-    if (comm) RST_CHECK(comm_allgatherv_f4(comm, srcog, st));
-    RST_CHECK(seqsum_enqueue(srcog, n_total, 3, sqws, fsum, st));  // point_cloud_utils.cpp:94-96
+    // point_cloud_utils.cpp:94-96 (sharded: the stretches' chains relayed)
+    if (comm)
+      RST_CHECK(comm_relay_seqsum(comm, srco, n_local, 3, sqws, fsum, st, nullptr, nullptr, -1));
+    else
+      RST_CHECK(seqsum_enqueue(srco, n_local, 3, sqws, fsum, st));
     k_init_state<<<1, kBS, 0, st>>>(slab, 0, fsum, ia, ctx->d_state);
+    if (comm) RST_HIP(hipMemsetAsync(drift, 0, sizeof(double) * 4, st));
   } else if (!p2plane) {
     if (n_local > 0) {
       crows = centroid_device(ctx, src->pts, n_local, slab);
@@ -1907,15 +1910,17 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
         RST_CHECK(mark(1));
       }
       RST_CHECK(mark(2));
-      if (comm) RST_CHECK(comm_allgatherv_f4(comm, corrg, st));
       // (from the second iteration on, the same chains as the iteration before:
       // no totals launch, the front kernel takes that iteration's tile
       // prefixes; the last iteration adds the cost chain, which has none)
       const int nch = it + 1 == opts.max_iter || ctx->seq_trace ? 4 : 3;
       const int nch_prev = it == 0 ? 0 : (it == opts.max_iter || ctx->seq_trace ? 4 : 3);
       int* sqstats = ctx->seq_trace && ctx->d_sqstats && it < kQTrace ? ctx->d_sqstats + 64 * it : nullptr;
-      RST_CHECK(seqsum_enqueue(corrg, n_total, nch, sqws, ctx->d_state->seq, st, sqstats, 7, it,
-                               it > 0 && it >= sq_fuse_from() && nch <= nch_prev));
+      if (comm)
+        RST_CHECK(comm_relay_seqsum(comm, corr, n_local, nch, sqws, ctx->d_state->seq, st, drift, sqstats, it));
+      else
+        RST_CHECK(seqsum_enqueue(corr, n_local, nch, sqws, ctx->d_state->seq, st, sqstats, 7, it,
+                                 it > 0 && it >= sq_fuse_from() && nch <= nch_prev));
       if (n_local > 0)
         k_cov_ref<<<kCovBlocks, kBS, 0, st>>>(srco, corr, n_local, n_total, ctx->d_state, slab2);
       k_reduce_solve<RefAcc><<<1, kRedBS, 0, st>>>(slab, 0, slab2, n_local > 0 ? kCovBlocks : 0, prm,

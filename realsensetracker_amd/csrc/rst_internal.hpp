@@ -261,9 +261,22 @@ int seq_sum4_device(rst_ctx* ctx, const float4* d_x, int64_t n, float* d_out);
 // kSqForceMaps; kSqForceSerial takes it at any size.
 constexpr int kSqForceSerial = 16, kSqForceMaps = 32;
 size_t seqsum_bytes(int64_t n);
+// a stretch of a longer chain (the sharded loop's relay, comm.hip): per chain
+// the fp64 prefix before the stretch (guesses only) and the chain's value at
+// its start (device pointers, 4 each); tot_done: seqsum_totals ran on this
+// workspace for the same iteration
+struct SqStretch {
+  const double* p0;
+  const float* s0;
+  bool tot_done;
+};
 int seqsum_enqueue(const float4* d_x, int64_t n, int nch, void* ws, float* d_out,
                    hipStream_t st, int* d_stats = nullptr, int stages = 7, int iter = -1,
-                   bool fused = false);
+                   bool fused = false, const SqStretch* stretch = nullptr);
+// a stretch's fp64 chain totals (d_tot4[4], non-finite elements skipped)
+// for the relay's exchange; leaves the quarter totals for seqsum_enqueue
+int seqsum_totals(const float4* d_x, int64_t n, int nch, void* ws, double* d_tot4, hipStream_t st,
+                  int iter);
 int kabsch_device(rst_ctx* ctx, const double cov[9], const float smean[3],
                   const float dmean[3], float pose_out[16]);
 
@@ -296,7 +309,10 @@ int comm_shard_layout(rst_comm* comm, int64_t n_local, int64_t n_total_hint, hip
 // after k_init_state: this align's gathered counts against the cached
 // layout, kGuardLayout into *d_guard on a mismatch (every rank alike)
 int comm_layout_check(rst_comm* comm, hipStream_t st, int32_t* d_guard);
-// in-place all-gather of every rank's stretch [off_r, off_r + n_r) of buf
-int comm_allgatherv_f4(rst_comm* comm, float4* buf, hipStream_t st);
+// the sequential sums of the ranks' consecutive stretches (d_x: this rank's,
+// n_local elements) relayed rank to rank: d_out[0..nch) the whole chains'
+// sums on every rank; d_drift: 4 doubles carried between iterations (or null)
+int comm_relay_seqsum(rst_comm* comm, const float4* d_x, int64_t n_local, int nch, void* sqws,
+                      float* d_out, hipStream_t st, double* d_drift, int* d_stats, int iter);
 
 }  // namespace rst

@@ -73,6 +73,11 @@ struct SqView {
   int* err;        // bound-check failures (bits; 0 = none): a map kernel that
                    // meets a size its tables cannot hold stops instead of
                    // reading out of range
+  // a stretch of a longer chain (the sharded loop's relay, comm.hip): per
+  // chain the fp64 prefix before the stretch (the guesses' offset) and the
+  // chain's value where it starts (the walk's start); null = a whole chain
+  const double* p0;
+  const float* s0;
 };
 
 __device__ __forceinline__ float comp(const float4& v, int c) {
@@ -208,11 +213,11 @@ __device__ __forceinline__ void ser_tile(const float4 (&v)[kSerT], int cnt, floa
 }
 
 __global__ __launch_bounds__(kWave) void k_sq_serial(const float4* __restrict__ x, int64_t n, int nch,
-                                                     float* __restrict__ out) {
+                                                     const float* __restrict__ s0, float* __restrict__ out) {
   __shared__ float4 tile4[kSerRow];  // 4 rows of kSerRow floats
   float* tile = reinterpret_cast<float*>(tile4);
   constexpr int64_t kT = (int64_t)kSerT * kWave;
-  float s = 0.0f;
+  float s = s0 && (int)threadIdx.x < nch ? s0[threadIdx.x] : 0.0f;
   float4 a[kSerT], b[kSerT];
   ser_load(x, n, 0, a);
   for (int64_t base = 0; base < n; base += 2 * kT) {
@@ -347,7 +352,8 @@ __global__ __launch_bounds__(kFrontT) void k_sq_front(SqView v, const float4* __
   }
   // fp64 prefix at the tile start (the quarter tiles' totals before it)
   const double P = block_sum_global<kFrontT>((FUSED ? tprev : v.ttot) + (int64_t)c * v.nk * kTotQ,
-                                             t * kTotQ, lds);
+                                             t * kTotQ, lds) +
+                   (v.p0 ? v.p0[c] : 0.0);
   __syncthreads();
   // the thread's window: fp64 total and prefix
   const int b = t * kBlocksPerTile + tid;
@@ -391,8 +397,8 @@ __global__ __launch_bounds__(kFrontT) void k_sq_front(SqView v, const float4* __
     best = wpre;
     bj = 0;
   }
-  if (b == 0) {
-    best = 0.0;
+  if (b == 0) {  // the chain's first element (a stretch: its fp64 prefix, P)
+    best = v.p0 ? P : 0.0;
     bj = 0;
   }
   sbs[tid] = tid * kW + bj;  // tile-relative start
@@ -461,7 +467,7 @@ __global__ __launch_bounds__(kFrontT) void k_sq_front(SqView v, const float4* __
   if (b < v.nb) {
     const int s0 = sbs[tid];
     const int s1 = b == v.nb - 1 ? (int)(v.n - e0) : sbs[tid + 1];
-    const float G = b == 0 ? 0.0f : (float)sA[tid];
+    const float G = b == 0 && !v.p0 ? 0.0f : (float)sA[tid];
     float s = G;
     double fsum = 0.0;
     for (int i = s0; i < s1; ++i) {
@@ -658,8 +664,9 @@ __global__ __launch_bounds__(kBuildT) void k_sq_build(SqView v) {
 #pragma unroll
     for (int o = kWave / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, kWave);
     if (lane == 0) {
-      W.base[0] = s;
-      W.base[1] = s + (k < v.nk ? ti[k] : 0.0);
+      const double q = v.p0 ? v.p0[c] : 0.0;  // (a stretch of a longer chain)
+      W.base[0] = s + q;
+      W.base[1] = s + q + (k < v.nk ? ti[k] : 0.0);
     }
   }
   __syncthreads();
@@ -679,7 +686,7 @@ __global__ __launch_bounds__(kBuildT) void k_sq_build(SqView v) {
       }
       // a superblock's blocks lie in tile k and tile k + 1
       const double base = (b / kBlocksPerTile) == k ? W.base[0] : W.base[1];
-      G = candidate_base(b == 0 ? 0.0f : (float)(base + iv), kLeafR);
+      G = candidate_base(b == 0 && !v.p0 ? 0.0f : (float)(base + iv), kLeafR);
       e0 = grid_exp(G);
     }
     // the wavefront's longest block bounds the unrolled steps
@@ -716,7 +723,7 @@ __global__ __launch_bounds__(kBuildT) void k_sq_build(SqView v) {
       const int xa = j < nl ? W.sbs[bl] : 0, xl = j < nl ? W.sbs[bl + 1] - xa : 0;
       const int xb = ba + bl;
       const double base = (xb / kBlocksPerTile) == k ? W.base[0] : W.base[1];
-      const float xG = j < nl ? candidate_base(xb == 0 ? 0.0f : (float)(base + v.ipre[(int64_t)c * v.nb + xb]),
+      const float xG = j < nl ? candidate_base(xb == 0 && !v.p0 ? 0.0f : (float)(base + v.ipre[(int64_t)c * v.nb + xb]),
                                                kLeafR)
                               : 0.0f;
       const int xe0 = grid_exp(xG);
@@ -1163,7 +1170,7 @@ __global__ __launch_bounds__(kWave) void k_sq_walk(SqView v, float* __restrict__
   __syncthreads();
   __shared__ MapEnt CE[kWalkC][kWave];  // the chunk's entries, for the checks
   int nsb = 0, nsbh = 0;
-  float s = 0.0f;
+  float s = v.s0 ? v.s0[c] : 0.0f;  // (a stretch: the chain's value at its start)
   bool nf = false;  // s became non-finite (W.pos_nf)
   int k = 0;
   SbRegs cur, nxt;
@@ -1358,18 +1365,56 @@ static int64_t serial_max() {
   return g;
 }
 
-int seqsum_enqueue(const float4* d_x, int64_t n, int nch, void* ws, float* d_out, hipStream_t st,
-                   int* d_stats, int stages, int iter, bool fused) {
+namespace {
+// a stretch's chain totals: the quarter tiles' fp64 totals (k_sq_tot), per
+// chain in a fixed order (block 0 of the relay's exchange)
+__global__ __launch_bounds__(kFrontT) void k_sq_sumq(SqView v, double* __restrict__ tot4) {
+  __shared__ double lds[kFrontT / kWave + 1];
+  for (int c = 0; c < 4; ++c) {
+    double t = 0.0;
+    if (c < v.nch) t = block_sum_global<kFrontT>(v.ttot + (int64_t)c * v.nk * kTotQ, v.nk * kTotQ, lds);
+    if (threadIdx.x == 0) tot4[c] = t;
+    __syncthreads();
+  }
+}
+__global__ void k_sq_copy4(const float* __restrict__ s0, int nch, float* __restrict__ out) {
+  if ((int)threadIdx.x < nch) out[threadIdx.x] = s0 ? s0[threadIdx.x] : 0.0f;
+}
+}  // namespace
+
+int seqsum_totals(const float4* d_x, int64_t n, int nch, void* ws, double* d_tot4, hipStream_t st, int iter) {
   if (nch < 1 || nch > 4 || n < 0) return RST_E_ARG;
   if (n == 0) {
-    RST_HIP(hipMemsetAsync(d_out, 0, sizeof(float) * nch, st));
+    RST_HIP(hipMemsetAsync(d_tot4, 0, sizeof(double) * 4, st));
+    return RST_OK;
+  }
+  if (n > (int64_t)INT_MAX - 2 * kTile) return RST_E_ARG;
+  SqView v;
+  sq_layout(v, n, nch, (char*)ws);
+  v.p0 = nullptr;
+  v.s0 = nullptr;
+  const size_t tq = (size_t)4 * kTotQ * v.nk;
+  if (iter >= 0) v.ttot = v.ttot2 + (size_t)(iter & 1) * tq;
+  k_sq_tot<<<v.nk * kTotQ, kFrontT, 0, st>>>(d_x, v);
+  k_sq_sumq<<<1, kFrontT, 0, st>>>(v, d_tot4);
+  RST_HIP(hipGetLastError());
+  return RST_OK;
+}
+
+int seqsum_enqueue(const float4* d_x, int64_t n, int nch, void* ws, float* d_out, hipStream_t st,
+                   int* d_stats, int stages, int iter, bool fused, const SqStretch* stretch) {
+  if (nch < 1 || nch > 4 || n < 0) return RST_E_ARG;
+  const float* s0 = stretch ? stretch->s0 : nullptr;
+  if (n == 0) {  // (a stretch: the chain's value at its start, unchanged)
+    k_sq_copy4<<<1, kWave, 0, st>>>(s0, nch, d_out);
+    RST_HIP(hipGetLastError());
     return RST_OK;
   }
   if (n > (int64_t)INT_MAX - 2 * kTile) return RST_E_ARG;
   // small streams: one wavefront replays the chains (the whole sum, no stats)
   const bool whole = (stages & 7) == 7;
   if (whole && !(stages & kSqForceMaps) && ((stages & kSqForceSerial) || n <= serial_max())) {
-    k_sq_serial<<<1, kWave, 0, st>>>(d_x, n, nch, d_out);
+    k_sq_serial<<<1, kWave, 0, st>>>(d_x, n, nch, s0, d_out);
     RST_HIP(hipGetLastError());
     return RST_OK;
   }
@@ -1377,17 +1422,20 @@ int seqsum_enqueue(const float4* d_x, int64_t n, int nch, void* ws, float* d_out
   SqView v;
   sq_layout(v, n, nch, (char*)ws);
   v.stats = d_stats;
+  v.p0 = stretch ? stretch->p0 : nullptr;
+  v.s0 = s0;
 #ifdef RST_SQ_ABLATE  // measurement only (wrong sums): skip kernels by bit
   stages &= ~RST_SQ_ABLATE;
 #endif
   const size_t tq = (size_t)4 * kTotQ * v.nk;  // one parity buffer: 4 chains' quarter totals
   if (iter >= 0) v.ttot = v.ttot2 + (size_t)(iter & 1) * tq;
   if (stages & 1) {
-    if (fused && iter > 0) {
+    if (fused && iter > 0 && !stretch) {
       k_sq_front<true><<<dim3(v.nk, nch), kFrontT, 0, st>>>(v, d_x, v.ttot2 + (size_t)((iter - 1) & 1) * tq,
                                                             v.ttot);
     } else {
-      k_sq_tot<<<v.nk * kTotQ, kFrontT, 0, st>>>(d_x, v);
+      // (a stretch's totals are in place: seqsum_totals ran for the exchange)
+      if (!(stretch && stretch->tot_done)) k_sq_tot<<<v.nk * kTotQ, kFrontT, 0, st>>>(d_x, v);
       k_sq_front<false><<<dim3(v.nk, nch), kFrontT, 0, st>>>(v, nullptr, nullptr, nullptr);
     }
   }
