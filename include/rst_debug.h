@@ -97,6 +97,12 @@ int64_t rst_debug_seq_ws_bytes(int64_t n);
  * completed per second (host clock, launch to the last stream's sync). */
 int rst_debug_launch_rate(rst_ctx* ctx, int nstreams, int launches, int blocks, int threads,
                           double* per_s);
+/* The concurrency probe: `launches` kernels per stream on nstreams fresh
+ * streams, each kernel's waves waiting spin_us on the real-time clock with
+ * lds_bytes of dynamic LDS; *overlap = kernels running at once on average
+ * (their busy time over the wall time). */
+int rst_debug_kernel_overlap(rst_ctx* ctx, int nstreams, int launches, int blocks, int threads,
+                             int spin_us, int lds_bytes, double* overlap);
 
 /* A device stream copy (the measured HBM ceiling the rooflines are read
  * against): `bytes` copied buffer to buffer by float4 kernels (1-8 float4

@@ -247,6 +247,17 @@ __global__ void k_nop(int* __restrict__ sink, int tag) {
   if (threadIdx.x == 0 && tag < 0) sink[blockIdx.x] = tag;
 }
 
+// the concurrency probe (rst_debug_kernel_overlap): every wave waits
+// `ticks` of the 100 MHz real-time clock (no memory traffic, no ALU
+// pressure), holding `lds` bytes of dynamic LDS -- how many such kernels
+// from independent streams the GPU runs at once
+__global__ void k_spin(int* __restrict__ sink, int tag, int ticks) {
+  extern __shared__ int spin_lds[];
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) < ticks) __builtin_amdgcn_s_sleep(2);
+  if (threadIdx.x == 0 && tag < 0) sink[blockIdx.x] = tag + spin_lds[0];
+}
+
 }  // namespace rst
 
 using namespace rst;
@@ -711,6 +722,41 @@ int rst_debug_launch_rate(rst_ctx* ctx, int nstreams, int launches, int blocks, 
     const double dt =
         std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     *per_s = (double)nl * nstreams / dt;
+  }
+  for (auto q : ss)
+    if (q) (void)hipStreamDestroy(q);
+  if (sink) (void)hipFree(sink);
+  return s;
+}
+
+int rst_debug_kernel_overlap(rst_ctx* ctx, int nstreams, int launches, int blocks, int threads,
+                             int spin_us, int lds_bytes, double* overlap) {
+  if (!ctx || !overlap || nstreams < 1 || nstreams > 64 || launches < 1 || blocks < 1 ||
+      threads < 1 || threads > 1024 || spin_us < 1 || lds_bytes < 0 || lds_bytes > 160 * 1024)
+    return RST_E_ARG;
+  RST_HIP(hipSetDevice(ctx->device));
+  std::vector<hipStream_t> ss(nstreams, nullptr);
+  int s = RST_OK;
+  for (auto& q : ss)
+    if (hipStreamCreateWithFlags(&q, hipStreamNonBlocking) != hipSuccess) s = RST_E_HIP;
+  int* sink = nullptr;
+  if (s >= 0 && hipMalloc(&sink, sizeof(int) * blocks) != hipSuccess) s = RST_E_NOMEM;
+  if (s >= 0 && lds_bytes > 64 * 1024 &&
+      hipFuncSetAttribute((const void*)k_spin, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes) !=
+          hipSuccess)
+    s = RST_E_HIP;
+  const int ticks = spin_us * 100;  // s_memrealtime: 100 MHz
+  for (int rep = 0; rep < 2 && s >= 0; ++rep) {
+    const int nl = rep == 0 ? 4 : launches;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int i = 0; i < nl; ++i)
+      for (auto q : ss) k_spin<<<blocks, threads, lds_bytes, q>>>(sink, 1, ticks);
+    for (auto q : ss)
+      if (hipStreamSynchronize(q) != hipSuccess) s = RST_E_HIP;
+    const double dt =
+        std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    // kernels running at once, on average: their busy time over the wall time
+    *overlap = (double)nl * nstreams * spin_us * 1e-6 / dt;
   }
   for (auto q : ss)
     if (q) (void)hipStreamDestroy(q);

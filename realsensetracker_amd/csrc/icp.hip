@@ -105,6 +105,12 @@ constexpr int kPixChunk = RST_PIX_CHUNK;
 #ifndef RST_PIX_COLD_CHUNKS
 #define RST_PIX_COLD_CHUNKS 6  // their staging rounds per wave
 #endif
+#ifndef RST_PIX_I0_HALF
+#define RST_PIX_I0_HALF 0.0f  // > 0: a pair's first iteration takes windows of this cap (level pixels)
+#endif
+#ifndef RST_PIX_I0_CHUNKS
+#define RST_PIX_I0_CHUNKS 2  // ... over this many staging rounds per wave
+#endif
 #ifndef RST_DIAG
 #define RST_DIAG 0  // 1: per-iteration certificate counters (rst_debug_queue_trace)
 #endif
@@ -828,11 +834,15 @@ __global__ __launch_bounds__(kBS, RST_NN_MIN_WAVES) void k_icp_nn(BvhView bv, Ad
     // searches take in parallel instead; r04j: nn 35 -> 25 us, same
     // throughput.  The fp64 loop keeps the wider cap, r02's throughput best)
     constexpr float kPixHalf = std::is_same<Acc, RefAcc>::value ? RST_PIX_MAX_HALF_REF : RST_PIX_MAX_HALF;
-    const bool pok =
-        cold ? pix_tile_search<kPixChunk, RST_PIX_COLD_CHUNKS>(bv, pv, need, px, py, pz, d0, pr, pq,
-                                                               pscr[wid], prc, RST_PIX_COLD_HALF)
-             : pix_tile_search<kPixChunk, RST_PIX_CHUNKS>(bv, pv, need, px, py, pz, d0, pr, pq, pscr[wid], prc,
-                                                                 kPixHalf);
+    bool pok;
+    if (RST_PIX_I0_HALF > 0.0f && st->iter == 0)  // (uniform)
+      pok = pix_tile_search<kPixChunk, RST_PIX_I0_CHUNKS>(bv, pv, need, px, py, pz, d0, pr, pq, pscr[wid], prc,
+                                                           RST_PIX_I0_HALF);
+    else
+      pok = cold ? pix_tile_search<kPixChunk, RST_PIX_COLD_CHUNKS>(bv, pv, need, px, py, pz, d0, pr, pq,
+                                                                   pscr[wid], prc, RST_PIX_COLD_HALF)
+                 : pix_tile_search<kPixChunk, RST_PIX_CHUNKS>(bv, pv, need, px, py, pz, d0, pr, pq, pscr[wid],
+                                                              prc, kPixHalf);
 #if RST_NN_CLK
     ck2 = __builtin_amdgcn_s_memtime();
 #endif
