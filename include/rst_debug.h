@@ -97,6 +97,13 @@ int64_t rst_debug_seq_ws_bytes(int64_t n);
  * completed per second (host clock, launch to the last stream's sync). */
 int rst_debug_launch_rate(rst_ctx* ctx, int nstreams, int launches, int blocks, int threads,
                           double* per_s);
+/* RST_TIMELINE builds (RST_DEFINES=-DRST_TIMELINE=1): the context's last
+ * ICP align, per iteration and loop kernel (k_icp_nn, k_icp_fb, k_sq_tot,
+ * k_sq_front, k_sq_build, k_sq_walk, k_cov_ref, k_reduce_solve) the
+ * earliest wave start and the latest wave end on the 100 MHz device clock:
+ * out[(iter * 8 + kernel) * 2 + {0, 1}], at most cap values; *iters = the
+ * iterations run.  RST_E_STATE in other builds. */
+int rst_debug_timeline(rst_ctx* ctx, uint64_t* out, int32_t cap, int32_t* iters);
 /* The concurrency probe: `launches` kernels per stream on nstreams fresh
  * streams, each kernel's waves waiting spin_us on the real-time clock with
  * lds_bytes of dynamic LDS; *overlap = kernels running at once on average

@@ -729,6 +729,22 @@ int rst_debug_launch_rate(rst_ctx* ctx, int nstreams, int launches, int blocks, 
   return s;
 }
 
+int rst_debug_timeline(rst_ctx* ctx, uint64_t* out, int32_t cap, int32_t* iters) {
+  if (!ctx || !iters || (cap > 0 && !out)) return RST_E_ARG;
+#if RST_TIMELINE
+  RST_HIP(hipSetDevice(ctx->device));
+  RST_HIP(hipStreamSynchronize(ctx->stream));
+  const int n = std::min<int>(cap, kQTrace * kTlKernels * 2);
+  memcpy(out, &ctx->h_state->tl[0][0][0], sizeof(uint64_t) * (size_t)std::max(n, 0));
+  *iters = ctx->h_state->iter;
+  return RST_OK;
+#else
+  (void)out;
+  (void)cap;
+  return RST_E_STATE;
+#endif
+}
+
 int rst_debug_kernel_overlap(rst_ctx* ctx, int nstreams, int launches, int blocks, int threads,
                              int spin_us, int lds_bytes, double* overlap) {
   if (!ctx || !overlap || nstreams < 1 || nstreams > 64 || launches < 1 || blocks < 1 ||

@@ -244,6 +244,12 @@ __global__ __launch_bounds__(kBS) void k_init_state(const double* __restrict__ c
                                                     IcpState* __restrict__ st) {
   __shared__ double red[(kBS / kWave) * 4];
   __shared__ double tot[4];
+#if RST_TIMELINE
+  for (int i = threadIdx.x; i < kQTrace * kTlKernels; i += blockDim.x) {
+    st->tl[0][0][2 * i] = ~0ull;
+    st->tl[0][0][2 * i + 1] = 0ull;
+  }
+#endif
   if (a.need_centroid == 1) reduce_slab_rows<4>(cslab, rows, cslab, 0, nullptr, red, tot);
   if (threadIdx.x == 0) {
     float P[12];  // R col-major, t
@@ -504,6 +510,9 @@ __global__ __launch_bounds__(kBS) void k_cov_ref(const float4* __restrict__ srco
                                                  const IcpState* __restrict__ st,
                                                  double* __restrict__ slab) {
   __shared__ double lds[(kBS / kWave) * 9];
+#if RST_TIMELINE
+  RST_TL(const_cast<IcpState*>(st)->tl[0][0], st->iter, 6);
+#endif
   const float nf = (float)n_total;  // dst_mean /= n (the whole source's n)
   const float dm0 = st->seq[0] / nf, dm1 = st->seq[1] / nf, dm2 = st->seq[2] / nf;
   const float sm0 = st->smean[0], sm1 = st->smean[1], sm2 = st->smean[2];
@@ -641,6 +650,9 @@ __global__ __launch_bounds__(kBS, RST_NN_MIN_WAVES) void k_icp_nn(BvhView bv, Ad
                                                 int32_t* __restrict__ qcnt,
                                                 double* __restrict__ slab) {
   (void)av;
+#if RST_TIMELINE
+  RST_TL(const_cast<IcpState*>(st)->tl[0][0], st->iter, 0);
+#endif
   __shared__ double lds[(kBS / kWave) * Acc::NV];
   __shared__ int wq[2][kBS / kWave];
 #if RST_PIX_TILES
@@ -1195,6 +1207,9 @@ __global__ __launch_bounds__(kRedBS) void k_reduce_solve(const double* __restric
   static_assert((RS & (RS - 1)) == 0 && RS <= kWave, "rows: a power of two <= 64 doubles");
   __shared__ double red[NW * RS];
   __shared__ double tot[RS];
+#if RST_TIMELINE
+  RST_TL(st->tl[0][0], st->iter, 7);
+#endif
   if (Acc::kCanFinish && st->done) return;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   const int rows2 = rows2max;  // every fallback block writes its row (kernel 1's folded in)
@@ -1355,6 +1370,9 @@ __global__ __launch_bounds__(kBS, Acc::kFbMinWaves) void k_icp_fb(BvhView bv, Ad
                                                 int lane_min, const double* __restrict__ slab1,
                                                 double* __restrict__ slab2, int64_t n) {
   extern __shared__ int pref[];  // [2 (nb1 + 1)]: near prefix, far prefix
+#if RST_TIMELINE
+  RST_TL(st->tl[0][0], st->iter, 1);
+#endif
   int* preff = pref + nb1 + 1;
   const int32_t* __restrict__ qbuff = qbuf + (int64_t)nb1 * kBS;
   const int32_t* __restrict__ qcntf = qcnt + nb1;
@@ -1930,7 +1948,13 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
         RST_CHECK(comm_relay_seqsum(comm, corr, n_local, nch, sqws, ctx->d_state->seq, st, drift, sqstats, it));
       else
         RST_CHECK(seqsum_enqueue(corr, n_local, nch, sqws, ctx->d_state->seq, st, sqstats, 7, it,
-                                 it > 0 && it >= sq_fuse_from() && nch <= nch_prev));
+                                 it > 0 && it >= sq_fuse_from() && nch <= nch_prev, nullptr,
+#if RST_TIMELINE
+                                 &ctx->d_state->tl[0][0][0]
+#else
+                                 nullptr
+#endif
+                                 ));
       if (n_local > 0)
         k_cov_ref<<<kCovBlocks, kBS, 0, st>>>(srco, corr, n_local, n_total, ctx->d_state, slab2);
       k_reduce_solve<RefAcc><<<1, kRedBS, 0, st>>>(slab, 0, slab2, n_local > 0 ? kCovBlocks : 0, prm,

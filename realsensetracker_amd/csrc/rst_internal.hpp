@@ -47,6 +47,27 @@ void set_last_error(hipError_t e, const char* what, const char* file,
 // Written only by the single-block solve kernels, read (uniformly) by the
 // per-point kernels.  Plain POD; lives in the context's workspace.
 constexpr int kQTrace = 256;
+#ifndef RST_TIMELINE
+#define RST_TIMELINE 0  // diagnostics build: device-side kernel timeline of the ICP loop
+#endif
+// the loop's kernels in the timeline: nn, fb, sq_tot, sq_front, sq_build,
+// sq_walk, cov_ref, reduce_solve
+constexpr int kTlKernels = 8;
+#if RST_TIMELINE && defined(__HIPCC__)
+struct TlGuard {
+  unsigned long long* p;
+  __device__ TlGuard(unsigned long long* base, int it, int kid)
+      : p(base && it >= 0 && it < kQTrace ? base + ((size_t)it * kTlKernels + kid) * 2 : nullptr) {
+    if (p && (threadIdx.x & 63) == 0) atomicMin(p, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+  }
+  __device__ ~TlGuard() {
+    if (p && (threadIdx.x & 63) == 0) atomicMax(p + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+  }
+};
+#define RST_TL(base, it, kid) rst::TlGuard rst_tl_guard_((base), (it), (kid))
+#else
+#define RST_TL(base, it, kid) (void)0
+#endif
 // IcpCore::guard bit of a shard layout that changed at an unchanged n_total
 constexpr int32_t kGuardLayout = 1 << 16;
 
@@ -85,6 +106,11 @@ struct IcpState : IcpCore {
   int32_t diag[kQTrace][4];  // RST_DIAG builds: far queue, ball chunks, ball aborts, deep searches
   float seqtr[kQTrace][4];   // RST_SUM_REF: each iteration's sequential sums (sum q xyz, cost;
                              // the cost every iteration only under rst_debug_enable_seq_trace)
+#if RST_TIMELINE
+  // diagnostics build: per iteration and loop kernel, the earliest wave start
+  // and the latest wave end (100 MHz real-time clock; rst_debug_timeline)
+  unsigned long long tl[kQTrace][kTlKernels][2];
+#endif
 };
 
 struct IcpParams {
@@ -272,7 +298,8 @@ struct SqStretch {
 };
 int seqsum_enqueue(const float4* d_x, int64_t n, int nch, void* ws, float* d_out,
                    hipStream_t st, int* d_stats = nullptr, int stages = 7, int iter = -1,
-                   bool fused = false, const SqStretch* stretch = nullptr);
+                   bool fused = false, const SqStretch* stretch = nullptr,
+                   unsigned long long* tl = nullptr);
 // a stretch's fp64 chain totals (d_tot4[4], non-finite elements skipped)
 // for the relay's exchange; leaves the quarter totals for seqsum_enqueue
 int seqsum_totals(const float4* d_x, int64_t n, int nch, void* ws, double* d_tot4, hipStream_t st,

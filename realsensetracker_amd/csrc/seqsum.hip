@@ -78,6 +78,8 @@ struct SqView {
   // chain's value where it starts (the walk's start); null = a whole chain
   const double* p0;
   const float* s0;
+  unsigned long long* tl;  // RST_TIMELINE builds: the ICP loop's kernel timeline
+  int it;                  // ... and this iteration
 };
 
 __device__ __forceinline__ float comp(const float4& v, int c) {
@@ -251,6 +253,7 @@ __device__ __forceinline__ int quad_or(int a) {
 }
 
 __global__ __launch_bounds__(kFrontT) void k_sq_tot(const float4* __restrict__ x, SqView v) {
+  RST_TL(v.tl, v.it, 2);
   __shared__ double red[kFrontT / kWave][4];
   const int qt = blockIdx.x, tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid / kWave;
   const int64_t i0 = (int64_t)qt * kTotE + 4 * tid;
@@ -308,6 +311,7 @@ template <bool FUSED>
 __global__ __launch_bounds__(kFrontT) void k_sq_front(SqView v, const float4* __restrict__ x,
                                                      const double* __restrict__ tprev,
                                                      double* __restrict__ tnext) {
+  RST_TL(v.tl, v.it, 3);
   // (one pad float per 16: thread t's window reads xs(16 t + j) at 17 t + j,
   // every lane in its own bank)
   __shared__ float xsp[(kTile + kW) + (kTile + kW) / kW];
@@ -611,6 +615,7 @@ __device__ __forceinline__ MapEnt leaf_ent(const Run& p, int e0) {
 }
 
 __global__ __launch_bounds__(kBuildT) void k_sq_build(SqView v) {
+  RST_TL(v.tl, v.it, 4);
   __shared__ BuildLds W;
   const int k = blockIdx.x, c = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & (kWave - 1);
@@ -1156,6 +1161,7 @@ __device__ __forceinline__ void sb_fetch(const SbMap* __restrict__ sbm_, int nk,
 }
 
 __global__ __launch_bounds__(kWave) void k_sq_walk(SqView v, float* __restrict__ out) {
+  RST_TL(v.tl, v.it, 5);
   __shared__ WalkLds W;
   const int c = blockIdx.x, lane = threadIdx.x;
   const SbMap* sbm = v.sbm + (int64_t)c * v.nk;
@@ -1391,8 +1397,11 @@ int seqsum_totals(const float4* d_x, int64_t n, int nch, void* ws, double* d_tot
   if (n > (int64_t)INT_MAX - 2 * kTile) return RST_E_ARG;
   SqView v;
   sq_layout(v, n, nch, (char*)ws);
+  v.stats = nullptr;
   v.p0 = nullptr;
   v.s0 = nullptr;
+  v.tl = nullptr;
+  v.it = iter;
   const size_t tq = (size_t)4 * kTotQ * v.nk;
   if (iter >= 0) v.ttot = v.ttot2 + (size_t)(iter & 1) * tq;
   k_sq_tot<<<v.nk * kTotQ, kFrontT, 0, st>>>(d_x, v);
@@ -1402,7 +1411,8 @@ int seqsum_totals(const float4* d_x, int64_t n, int nch, void* ws, double* d_tot
 }
 
 int seqsum_enqueue(const float4* d_x, int64_t n, int nch, void* ws, float* d_out, hipStream_t st,
-                   int* d_stats, int stages, int iter, bool fused, const SqStretch* stretch) {
+                   int* d_stats, int stages, int iter, bool fused, const SqStretch* stretch,
+                   unsigned long long* tl) {
   if (nch < 1 || nch > 4 || n < 0) return RST_E_ARG;
   const float* s0 = stretch ? stretch->s0 : nullptr;
   if (n == 0) {  // (a stretch: the chain's value at its start, unchanged)
@@ -1424,6 +1434,8 @@ int seqsum_enqueue(const float4* d_x, int64_t n, int nch, void* ws, float* d_out
   v.stats = d_stats;
   v.p0 = stretch ? stretch->p0 : nullptr;
   v.s0 = s0;
+  v.tl = tl;
+  v.it = iter;
 #ifdef RST_SQ_ABLATE  // measurement only (wrong sums): skip kernels by bit
   stages &= ~RST_SQ_ABLATE;
 #endif
