@@ -54,14 +54,20 @@ constexpr int kQTrace = 256;
 // sq_walk, cov_ref, reduce_solve
 constexpr int kTlKernels = 8;
 #if RST_TIMELINE && defined(__HIPCC__)
+// (light: the start from block 0's first wave, the end from the first wave of
+// the grid's last four blocks -- dispatched last, done about last; one
+// atomic per wave on one address serialised the kernels it measured)
 struct TlGuard {
   unsigned long long* p;
+  bool first, last;
   __device__ TlGuard(unsigned long long* base, int it, int kid)
-      : p(base && it >= 0 && it < kQTrace ? base + ((size_t)it * kTlKernels + kid) * 2 : nullptr) {
-    if (p && (threadIdx.x & 63) == 0) atomicMin(p, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+      : p(base && it >= 0 && it < kQTrace ? base + ((size_t)it * kTlKernels + kid) * 2 : nullptr),
+        first(blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0),
+        last(blockIdx.x + 4 >= gridDim.x && threadIdx.x == 0) {
+    if (p && first) atomicMin(p, (unsigned long long)__builtin_amdgcn_s_memrealtime());
   }
   __device__ ~TlGuard() {
-    if (p && (threadIdx.x & 63) == 0) atomicMax(p + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    if (p && last) atomicMax(p + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
   }
 };
 #define RST_TL(base, it, kid) rst::TlGuard rst_tl_guard_((base), (it), (kid))

@@ -77,7 +77,10 @@ def main():
     clk = ws[off["clk"]:off["clk"] + 64 * 4 * nk].view(np.int64).reshape(4, nk, 8)
     if stages & 2:
         d = np.diff(clk[:, :, :6], axis=2).astype(np.float64)
-        names = ["leaf loads", "group lattice", "group runs (group 0)", "groups rest", "superblock"]  # (the leaves: k_sq_leaves)
+        # k_sq_build's stamps: start, staged, leaves done, group composites done,
+        # group maps stored, superblock done
+        names = ["staging", "leaves (+ extra candidates)", "group lattice + composites", "group store",
+                 "superblock"]
         print("map kernel phases (clocks, mean / max over superblocks):",
               {nm: (round(d[:, :, i].mean()), int(d[:, :, i].max())) for i, nm in enumerate(names)})
     from seqsum_emu import emulate_tables

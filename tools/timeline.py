@@ -76,9 +76,12 @@ for t in tls:
         for i in range(len(t)):
             if t[i, k, 1] > 0:
                 ivals.append((t[i, k, 0] - t0, t[i, k, 1] - t0, k))
-# the window where every context's last align runs
-lo = max(t[0, 0, 0] for t in tls) - t0
-hi = min(t[-1, 7, 1] for t in tls) - t0
+# the window where most contexts' last aligns run (the middle half of their span)
+st0 = sorted(t[0, 0, 0] - t0 for t in tls)
+en0 = sorted(t[-1, 7, 1] - t0 for t in tls)
+lo, hi = st0[-1] if len(tls) == 1 else st0[len(tls) // 2], en0[0] if len(tls) == 1 else en0[len(tls) // 2]
+if hi <= lo:
+    lo, hi = min(st0), max(en0)
 print(f"{len(tls)} aligns side by side; common window {lo / 1e3:.0f} .. {hi / 1e3:.0f} us")
 if hi > lo:
     pts = sorted([(max(s, lo), 1) for s, e, _ in ivals if e > lo and s < hi] +
