@@ -223,6 +223,23 @@ int rst_icp_align_prepared_async(rst_ctx* ctx, const rst_target* src,
 int rst_icp_align_wait(rst_ctx* ctx, float pose_inout[16], float* mean_cost,
                        int32_t* iterations_run);
 
+/* A batch of nb independent frame pairs aligned in lockstep on one context:
+ * AlignIcp3d(src[p], tgt[p]) from pose_in[16 p .. 16 p + 16) for every p,
+ * each result bit-identical to aligning the pair alone, but one launch of
+ * each loop kernel covers the whole batch (the GPU runs only a few kernels
+ * of independent streams at once; a batch hands it nb pairs' work per
+ * launch).  Pairs with the reference's early false (< 3 points; < 6 for
+ * RST_P2PLANE) are left out and report it.  One align or batch in flight
+ * per context (RST_E_STATE otherwise); the targets must stay alive until
+ * _wait.  _wait: poses_inout (nb x 16), mean_costs (nb, may be NULL),
+ * status (nb: RST_OK / RST_FALSE per pair), iterations (nb, may be NULL);
+ * returns RST_OK or the first error. */
+int rst_icp_align_batch_async(rst_ctx* ctx, int32_t nb, const rst_target* const* src,
+                              const rst_target* const* tgt, const rst_icp_opts* opts,
+                              const float* poses_in);
+int rst_icp_align_batch_wait(rst_ctx* ctx, float* poses_inout, float* mean_costs,
+                             int32_t* status, int32_t* iterations);
+
 /* Coarse-to-fine ICP over pyramid levels (BASELINE configs[4]; the
  * reference has no pyramid): level 0 is the finest, nlevels-1 the coarsest.
  * Runs levels nlevels-1 .. 0, iters[l] iterations each, every level starting

@@ -84,6 +84,9 @@ PROTOTYPES = {
                                    c_float_p, C.c_int64, c_float_p]),
     "rst_icp_align_prepared_async": (C.c_int, [_P, _P, _P, C.POINTER(IcpOpts), c_float_p]),
     "rst_icp_align_wait": (C.c_int, [_P, c_float_p, c_float_p, c_int32_p]),
+    "rst_icp_align_batch_async": (C.c_int, [_P, C.c_int32, C.POINTER(_P), C.POINTER(_P),
+                                            C.POINTER(IcpOpts), c_float_p]),
+    "rst_icp_align_batch_wait": (C.c_int, [_P, c_float_p, c_float_p, c_int32_p, c_int32_p]),
     "rst_ctx_enable_graphs": (C.c_int, [_P, C.c_int]),
     "rst_icp_align_pyramid_async": (C.c_int, [_P, C.POINTER(_P), C.POINTER(_P), C.c_int,
                                               c_int32_p, C.POINTER(IcpOpts), c_float_p]),

@@ -351,6 +351,47 @@ def align_prepared_async(src: Target, target: Target, ctx: Context, pose=None,
     return p
 
 
+class PendingBatch:
+    """A batch enqueued with align_batch_async; .wait() -> [IcpResult]."""
+
+    def __init__(self, ctx: Context, poses: np.ndarray, refs):
+        self.ctx = ctx
+        self._buf = np.ascontiguousarray(np.stack([L.pose_to_cm(p) for p in poses]), np.float32)
+        self._refs = refs  # sources / targets stay alive until wait()
+
+    def wait(self) -> list:
+        nb = len(self._buf)
+        mc = np.zeros(nb, np.float32)
+        st = np.zeros(nb, np.int32)
+        it = np.zeros(nb, np.int32)
+        L.check(L.lib().rst_icp_align_batch_wait(self.ctx.handle, L.fptr(self._buf), L.fptr(mc),
+                                                 st.ctypes.data_as(L.c_int32_p),
+                                                 it.ctypes.data_as(L.c_int32_p)),
+                "rst_icp_align_batch_wait")
+        self._refs = None
+        return [IcpResult(int(st[k]) == L.RST_OK, L.cm_to_pose(self._buf[k]), float(mc[k]), int(it[k]))
+                for k in range(nb)]
+
+
+def align_batch_async(srcs, targets, ctx: Context, poses=None,
+                      opts: "L.IcpOpts | None" = None) -> PendingBatch:
+    """Enqueue AlignIcp3d(srcs[k], targets[k]) for a batch of independent
+    frame pairs on ctx's stream, in lockstep (rst_icp_align_batch_async):
+    one launch per loop kernel for the whole batch, every result
+    bit-identical to aligning the pair alone.  .wait() -> [IcpResult]."""
+    nb = len(srcs)
+    if len(targets) != nb or nb < 1:
+        raise ValueError("srcs and targets need one entry per pair")
+    poses = [np.eye(4, dtype=np.float32)] * nb if poses is None else [np.asarray(p, np.float32) for p in poses]
+    o = opts if opts is not None else L.default_opts()
+    sh = (C.c_void_p * nb)(*[t.handle.value for t in srcs])
+    th = (C.c_void_p * nb)(*[t.handle.value for t in targets])
+    p = PendingBatch(ctx, poses, (list(srcs), list(targets)))
+    L.check(L.lib().rst_icp_align_batch_async(ctx.handle, nb, sh, th, C.byref(o), L.fptr(p._buf)),
+            "rst_icp_align_batch_async")
+    return p
+
+
 def align_pyramid_async(src_levels, tgt_levels, ctx: Context, iters, pose=None,
                         opts: "L.IcpOpts | None" = None) -> PendingAlign:
     """Enqueue the coarse-to-fine ICP (rst_icp_align_pyramid_async): levels

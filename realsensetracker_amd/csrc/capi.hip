@@ -335,6 +335,8 @@ int rst_ctx_destroy(rst_ctx* ctx) {
     if (e) hipEventDestroy(e);
   if (ctx->d_state) hipFree(ctx->d_state);
   if (ctx->h_state) hipHostFree(ctx->h_state);
+  if (ctx->d_bstate) hipFree(ctx->d_bstate);
+  if (ctx->h_bstate) hipHostFree(ctx->h_bstate);
   if (ctx->d_slab) hipFree(ctx->d_slab);
   if (ctx->d_sqstats) hipFree(ctx->d_sqstats);
   if (ctx->own_stream) hipStreamDestroy(ctx->own_stream);
@@ -993,6 +995,21 @@ int rst_icp_align_pyramid_async(rst_ctx* ctx, const rst_target* const* src,
   }
   ctx->pend.pyramid = true;
   return RST_OK;
+}
+
+int rst_icp_align_batch_async(rst_ctx* ctx, int32_t nb, const rst_target* const* src,
+                              const rst_target* const* tgt, const rst_icp_opts* opts,
+                              const float* poses_in) {
+  if (!ctx || nb < 1 || !src || !tgt || !poses_in) return RST_E_ARG;
+  RST_HIP(hipSetDevice(ctx->device));
+  return icp_launch_batch(ctx, nb, src, tgt, opts, poses_in);
+}
+
+int rst_icp_align_batch_wait(rst_ctx* ctx, float* poses_inout, float* mean_costs, int32_t* status,
+                             int32_t* iterations) {
+  if (!ctx || !poses_inout || !status) return RST_E_ARG;
+  RST_HIP(hipSetDevice(ctx->device));
+  return icp_finish_batch(ctx, poses_inout, mean_costs, status, iterations);
 }
 
 int rst_icp_align_wait(rst_ctx* ctx, float pose_inout[16], float* mean_cost,

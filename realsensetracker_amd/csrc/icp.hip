@@ -301,6 +301,7 @@ struct Uni {  // uniform per-iteration values of the device state
   Pose3 P;
   float mu;
   float sm0, sm1, sm2;
+  int it;  // the iteration
 };
 
 __device__ __forceinline__ Uni load_uni(const IcpState* __restrict__ st) {
@@ -310,6 +311,7 @@ __device__ __forceinline__ Uni load_uni(const IcpState* __restrict__ st) {
   u.sm0 = st->smean[0];
   u.sm1 = st->smean[1];
   u.sm2 = st->smean[2];
+  u.it = st->iter;
   return u;
 }
 
@@ -319,7 +321,8 @@ struct AccArgs {
   float pmu;                       // P2PLANE: Geman-McClure scale on r^2
   float max_d2;                    // P2PLANE: correspondence rejection
   int32_t pos0;                    // sorted position of dst[0]
-  int32_t full;                    // RST_SUM_REF: every lane writes its record (q, d2)
+  int32_t full_from;               // RST_SUM_REF: from this iteration on every lane writes
+                                   // its record (q, d2): the last one, whose cost chain reads d2
 };
 
 // P2POINT_REF.  Single pass over the correspondences with the source
@@ -405,13 +408,13 @@ struct RefAcc {
   __device__ static void add(double (&v)[NV], const BvhView& bv, const AccArgs& a, const Uni& u,
                              const float4& s, float px, float py, float pz, float bd, int bp,
                              float4 q, bool same = false) {
-    (void)v; (void)u; (void)px; (void)py; (void)pz;
+    (void)v; (void)px; (void)py; (void)pz;
     // a lane whose neighbour is the one it had (certified, or found again)
     // leaves its record alone: q is there already, and k_cov_ref recomputes
     // d2 from the pose (every iteration writing every record was 16 B per
     // point of scattered writes, ~26 B per point of write traffic, r05 PMC);
     // the last iteration writes them all, the cost chain reads d2
-    if (same && !a.full) return;
+    if (same && u.it < a.full_from) return;
     if (bp < 0) q = bv.pts[a.pos0];
     a.corr[f2i(s.w)] = make_float4(q.x, q.y, q.z, bd);
   }
@@ -504,11 +507,9 @@ __global__ __launch_bounds__(kBS) void k_gather_orig(const float4* __restrict__ 
 #define RST_COV_BLOCKS 1024
 #endif
 constexpr int kCovBlocks = RST_COV_BLOCKS;
-__global__ __launch_bounds__(kBS) void k_cov_ref(const float4* __restrict__ srco,
-                                                 const float4* __restrict__ corr, int64_t n,
-                                                 int64_t n_total,
-                                                 const IcpState* __restrict__ st,
-                                                 double* __restrict__ slab) {
+__device__ __forceinline__ void cov_ref_body(const float4* __restrict__ srco, const float4* __restrict__ corr,
+                                             int64_t n, int64_t n_total, const IcpState* __restrict__ st,
+                                             double* __restrict__ slab) {
   __shared__ double lds[(kBS / kWave) * 9];
 #if RST_TIMELINE
   RST_TL(const_cast<IcpState*>(st)->tl[0][0], st->iter, 6);
@@ -540,6 +541,14 @@ __global__ __launch_bounds__(kBS) void k_cov_ref(const float4* __restrict__ srco
     v[6] += (double)(a2 * b0); v[7] += (double)(a2 * b1); v[8] += (double)(a2 * b2);
   }
   block_sum_to_slab<9, kBS>(v, lds, slab + (int64_t)blockIdx.x * RefAcc::RS);
+}
+
+__global__ __launch_bounds__(kBS) void k_cov_ref(const float4* __restrict__ srco,
+                                                 const float4* __restrict__ corr, int64_t n,
+                                                 int64_t n_total,
+                                                 const IcpState* __restrict__ st,
+                                                 double* __restrict__ slab) {
+  cov_ref_body(srco, corr, n, n_total, st, slab);
 }
 
 // ---- kernel 1: adjacency search, one point per thread ----------------------------------
@@ -640,15 +649,15 @@ __device__ __forceinline__ void proj_seed(const BvhView& bv, const PixView& pv, 
 // one lane's search.
 // (no occupancy hint: the compiler's own register budget, measured best in
 // r02 -- a 5-waves/SIMD target spilled)
+// (the body of k_icp_nn / k_icp_nn_b: nbk = this pair's grid, the queue
+// segments' count)
 template <class Acc>
-__global__ __launch_bounds__(kBS, RST_NN_MIN_WAVES) void k_icp_nn(BvhView bv, AdjView av, PixView pv, AccArgs aa,
-                                                const float4* __restrict__ src, int64_t n,
-                                                const IcpState* __restrict__ st,
-                                                float4* __restrict__ nnq,
-                                                float4* __restrict__ cert,
-                                                int32_t* __restrict__ qbuf,
-                                                int32_t* __restrict__ qcnt,
-                                                double* __restrict__ slab) {
+__device__ __forceinline__ void icp_nn_body(const BvhView& bv, const AdjView& av, const PixView& pv,
+                                            const AccArgs& aa, const float4* __restrict__ src, int64_t n,
+                                            const IcpState* __restrict__ st, float4* __restrict__ nnq,
+                                            float4* __restrict__ cert, int32_t* __restrict__ qbuf,
+                                            int32_t* __restrict__ qcnt, double* __restrict__ slab,
+                                            const int nbk) {
   (void)av;
 #if RST_TIMELINE
   RST_TL(const_cast<IcpState*>(st)->tl[0][0], st->iter, 0);
@@ -662,10 +671,10 @@ __global__ __launch_bounds__(kBS, RST_NN_MIN_WAVES) void k_icp_nn(BvhView bv, Ad
   const uint64_t ck0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
   uint64_t ck1 = 0, ck2 = 0;
 #endif
-  const int tb = xcd_tile(blockIdx.x, gridDim.x);
+  const int tb = xcd_tile(blockIdx.x, nbk);
   // the far queue: the second half of qbuf / qcnt
-  int32_t* __restrict__ qbuff = qbuf + (int64_t)gridDim.x * kBS;
-  int32_t* __restrict__ qcntf = qcnt + gridDim.x;
+  int32_t* __restrict__ qbuff = qbuf + (int64_t)nbk * kBS;
+  int32_t* __restrict__ qcntf = qcnt + nbk;
   if (Acc::kCanFinish && st->done) {  // converged: uniform early exit
     if (threadIdx.x == 0) qcnt[tb] = qcntf[tb] = 0;
     return;
@@ -922,6 +931,54 @@ __global__ __launch_bounds__(kBS, RST_NN_MIN_WAVES) void k_icp_nn(BvhView bv, Ad
     o[3] = (int64_t)((ck2 ? ck2 - ck1 : 0) | ((ck3 - ck0) << 32));
   }
 #endif
+}
+
+template <class Acc>
+__global__ __launch_bounds__(kBS, RST_NN_MIN_WAVES) void k_icp_nn(BvhView bv, AdjView av, PixView pv, AccArgs aa,
+                                                const float4* __restrict__ src, int64_t n,
+                                                const IcpState* __restrict__ st,
+                                                float4* __restrict__ nnq,
+                                                float4* __restrict__ cert,
+                                                int32_t* __restrict__ qbuf,
+                                                int32_t* __restrict__ qcnt,
+                                                double* __restrict__ slab) {
+  icp_nn_body<Acc>(bv, av, pv, aa, src, n, st, nnq, cert, qbuf, qcnt, slab, (int)gridDim.x);
+}
+
+// A batch of independent frame pairs in lockstep (icp_launch_batch): one
+// launch per loop kernel for the whole batch, pair = blockIdx.z, its
+// arguments from a device array.  (The GPU overlaps only a few kernels from
+// independent streams -- its dispatch path, tools/kernel_overlap2.py -- so
+// pairs in flight on their own streams leave most of the chip idle between
+// small latency-bound kernels; one launch over B pairs gives the chip B
+// pairs' work at once.)
+struct PairArgs {
+  BvhView bv;
+  AdjView av;
+  PixView pv;
+  AccArgs aa;
+  const float4* src;  // the prepared (sorted) source
+  int64_t n;          // its points (this pair's, this rank's)
+  int64_t n_total;
+  IcpState* st;
+  float4* nnq;
+  float4* cert;
+  int32_t* qbuf;
+  int32_t* qcnt;
+  double* slab;   // kernel 1's rows
+  double* slab2;  // the fallback grid's / the covariance's rows
+  const float4* srco;  // RST_SUM_REF: the source in original order
+  float4* corr;        // ... the correspondences
+  IcpParams prm;
+  int32_t nb1;  // k_icp_nn's grid for this pair
+  int32_t lane_min;
+};
+
+template <class Acc>
+__global__ __launch_bounds__(kBS, RST_NN_MIN_WAVES) void k_icp_nn_b(const PairArgs* __restrict__ pa) {
+  const PairArgs& A = pa[blockIdx.z];
+  if ((int)blockIdx.x >= A.nb1) return;  // (uniform: the grid fits the batch's largest pair)
+  icp_nn_body<Acc>(A.bv, A.av, A.pv, A.aa, A.src, A.n, A.st, A.nnq, A.cert, A.qbuf, A.qcnt, A.slab, A.nb1);
 }
 
 // Kabsch solve (align_icp.cpp:139-151; SolveKabsch :58-69): fp64 SVD,
@@ -1197,12 +1254,10 @@ __device__ __forceinline__ void acc_update(const double* tot, const IcpParams& p
 // solves (align_icp.cpp:122-151); multi-GPU: the row goes to `totals` for
 // the RCCL all-reduce and k_solve_only follows.
 template <class Acc>
-__global__ __launch_bounds__(kRedBS) void k_reduce_solve(const double* __restrict__ slab1,
-                                                         int rows1,
-                                                         const double* __restrict__ slab2,
-                                                         int rows2max, IcpParams prm,
-                                                         IcpState* __restrict__ st,
-                                                         double* __restrict__ totals) {
+__device__ __forceinline__ void reduce_solve_body(const double* __restrict__ slab1, int rows1,
+                                                  const double* __restrict__ slab2, int rows2max,
+                                                  const IcpParams& prm, IcpState* __restrict__ st,
+                                                  double* __restrict__ totals) {
   constexpr int RS = Acc::RS, PER = kRedBS / RS, NW = kRedBS / kWave;
   static_assert((RS & (RS - 1)) == 0 && RS <= kWave, "rows: a power of two <= 64 doubles");
   __shared__ double red[NW * RS];
@@ -1252,6 +1307,16 @@ __global__ __launch_bounds__(kRedBS) void k_reduce_solve(const double* __restric
         for (int k = 0; k < 4; ++k) st->seqtr[it][k] = core.seq[k];
     }
   }
+}
+
+template <class Acc>
+__global__ __launch_bounds__(kRedBS) void k_reduce_solve(const double* __restrict__ slab1,
+                                                         int rows1,
+                                                         const double* __restrict__ slab2,
+                                                         int rows2max, IcpParams prm,
+                                                         IcpState* __restrict__ st,
+                                                         double* __restrict__ totals) {
+  reduce_solve_body<Acc>(slab1, rows1, slab2, rows2max, prm, st, totals);
 }
 
 // Multi-GPU: the all-reduced row -> the same solve on every rank.
@@ -1359,16 +1424,13 @@ union FbScratch {
 };
 
 template <class Acc>
-__global__ __launch_bounds__(kBS, Acc::kFbMinWaves) void k_icp_fb(BvhView bv, AdjView av, PixView pv,
-                                                AccArgs aa,
-                                                const float4* __restrict__ src,
-                                                IcpState* __restrict__ st,
-                                                float4* __restrict__ nnq,
-                                                float4* __restrict__ cert,
-                                                const int32_t* __restrict__ qbuf,
-                                                const int32_t* __restrict__ qcnt, int nb1,
-                                                int lane_min, const double* __restrict__ slab1,
-                                                double* __restrict__ slab2, int64_t n) {
+__device__ __forceinline__ void icp_fb_body(const BvhView& bv, const AdjView& av, const PixView& pv,
+                                            const AccArgs& aa, const float4* __restrict__ src,
+                                            IcpState* __restrict__ st, float4* __restrict__ nnq,
+                                            float4* __restrict__ cert, const int32_t* __restrict__ qbuf,
+                                            const int32_t* __restrict__ qcnt, int nb1, int lane_min,
+                                            const double* __restrict__ slab1, double* __restrict__ slab2,
+                                            int64_t n) {
   extern __shared__ int pref[];  // [2 (nb1 + 1)]: near prefix, far prefix
 #if RST_TIMELINE
   RST_TL(st->tl[0][0], st->iter, 1);
@@ -1606,6 +1668,39 @@ __global__ __launch_bounds__(kBS, Acc::kFbMinWaves) void k_icp_fb(BvhView bv, Ad
   if constexpr (Acc::kSums)
     block_sum_to_slab_fold<Acc::NV, kBS>(v, lds, slab2 + (int64_t)blockIdx.x * Acc::RS, slab1, nb1,
                                          Acc::RS, blockIdx.x, gridDim.x);
+}
+
+template <class Acc>
+__global__ __launch_bounds__(kBS, Acc::kFbMinWaves) void k_icp_fb(BvhView bv, AdjView av, PixView pv,
+                                                AccArgs aa,
+                                                const float4* __restrict__ src,
+                                                IcpState* __restrict__ st,
+                                                float4* __restrict__ nnq,
+                                                float4* __restrict__ cert,
+                                                const int32_t* __restrict__ qbuf,
+                                                const int32_t* __restrict__ qcnt, int nb1,
+                                                int lane_min, const double* __restrict__ slab1,
+                                                double* __restrict__ slab2, int64_t n) {
+  icp_fb_body<Acc>(bv, av, pv, aa, src, st, nnq, cert, qbuf, qcnt, nb1, lane_min, slab1, slab2, n);
+}
+
+// the batch forms (PairArgs, pair = blockIdx.z)
+template <class Acc>
+__global__ __launch_bounds__(kBS, Acc::kFbMinWaves) void k_icp_fb_b(const PairArgs* __restrict__ pa) {
+  const PairArgs& A = pa[blockIdx.z];
+  icp_fb_body<Acc>(A.bv, A.av, A.pv, A.aa, A.src, A.st, A.nnq, A.cert, A.qbuf, A.qcnt, A.nb1, A.lane_min,
+                   A.slab, A.slab2, A.n);
+}
+
+__global__ __launch_bounds__(kBS) void k_cov_ref_b(const PairArgs* __restrict__ pa) {
+  const PairArgs& A = pa[blockIdx.z];
+  cov_ref_body(A.srco, A.corr, A.n, A.n_total, A.st, A.slab2);
+}
+
+template <class Acc>
+__global__ __launch_bounds__(kRedBS) void k_reduce_solve_b(const PairArgs* __restrict__ pa, int rows2max) {
+  const PairArgs& A = pa[blockIdx.z];
+  reduce_solve_body<Acc>(A.slab, 0, A.slab2, rows2max, A.prm, A.st, nullptr);
 }
 
 template <class A>
@@ -1888,7 +1983,9 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
   aa.pmu = opts.p2plane_mu;
   aa.max_d2 = opts.p2plane_max_dist > 0 ? opts.p2plane_max_dist * opts.p2plane_max_dist : FLT_MAX;
   aa.pos0 = tgt->pos0;
-  aa.full = 1;
+  // (the last iteration's records all written: its cost chain reads d2;
+  // every iteration's under the sums' trace)
+  aa.full_from = ctx->seq_trace ? 0 : opts.max_iter - 1;
   const AdjView av = adj_of(tgt);
   const size_t fb_lds = 2 * sizeof(int) * ((size_t)nblk + 1);
 
@@ -1925,8 +2022,6 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
       // dst_mean (:113,122) and -- last iteration only: the reference reads
       // only that one (:104,157) -- the cost (:120), k_cov_ref the
       // covariance of the float products (:125-136)
-      // (the last iteration's records all written: its cost chain reads d2)
-      aa.full = it + 1 == opts.max_iter || ctx->seq_trace ? 1 : 0;
       if (n_local > 0) {
         k_icp_nn<RefAcc><<<nblk, kBS, 0, st>>>(bv, av, tgt->pix, aa, src->pts, n_local, ctx->d_state,
                                                nnq, cert, qbuf, qcnt, slab);
@@ -2103,6 +2198,291 @@ int icp_finish(rst_ctx* ctx, float pose_inout[16], float* mean_cost, int32_t* it
   return (mc < 10000.0f) ? RST_OK : RST_FALSE;  // :160 (NaN -> false)
 }
 
+// ---- a batch of frame pairs in lockstep -----------------------------------------------
+// The same loop as icp_launch for nb independent pairs at once: per pair its
+// own state, workspace and slab; per iteration ONE launch of each loop
+// kernel for the whole batch (pair = blockIdx.z, its arguments from a
+// device array of PairArgs; the sequential sums from one of SqPair
+// records).  Each pair's arithmetic is exactly its icp_launch's (the same
+// kernels' bodies, the same grids), so each result is bit-identical to
+// aligning it alone.  No RCCL, no hipGraph (plain stream launches).
+int icp_launch_batch(rst_ctx* ctx, int nb, const rst_target* const* src, const rst_target* const* tgt,
+                     const rst_icp_opts* opts_in, const float* poses_in) {
+  if (!ctx || nb < 1 || !src || !tgt || !poses_in) return RST_E_ARG;
+  if (ctx->bpend.active || ctx->pend.active) return RST_E_STATE;
+  rst_icp_opts opts;
+  if (opts_in)
+    opts = *opts_in;
+  else
+    rst_icp_opts_default(&opts);
+  const bool p2plane = opts.mode == RST_P2PLANE;
+  if (opts.mode != RST_P2POINT_REF && opts.mode != RST_P2PLANE) return RST_E_ARG;
+  if (opts.max_iter < 0) return RST_E_ARG;
+  if (opts.sum_mode != RST_SUM_REF && opts.sum_mode != RST_SUM_FP64) return RST_E_ARG;
+  const bool refsum = !p2plane && opts.sum_mode == RST_SUM_REF;
+  hipStream_t st = ctx->stream;
+  // the pairs that run (the reference's early false, align_icp.cpp:77-79: left out)
+  std::vector<int32_t> slot(nb, -1);
+  std::vector<int> run;
+  for (int p = 0; p < nb; ++p) {
+    if (!src[p] || !tgt[p]) return RST_E_ARG;
+    if (!tgt[p]->has_bvh || tgt[p]->m >= kCertBit) return RST_E_ARG;
+    if (p2plane && !tgt[p]->nrm) return RST_E_STATE;
+    const int64_t n = src[p]->m;
+    if (n < 3 || tgt[p]->m < 3 || (p2plane && n < 6)) continue;
+    slot[p] = (int32_t)run.size();
+    run.push_back(p);
+  }
+  const int B = (int)run.size();
+  ctx->bpend = {};
+  ctx->bpend.nb = nb;
+  ctx->bpend.slot = slot;
+  ctx->bpend.n_total.assign(nb, 0);
+  ctx->bpend.max_iter = opts.max_iter;
+  ctx->bpend.p2plane = p2plane;
+  for (int p = 0; p < nb; ++p) ctx->bpend.n_total[p] = src[p]->m;
+  if (B == 0) {
+    ctx->bpend.active = true;
+    return RST_OK;
+  }
+  // per pair: states
+  if (ctx->bcap < B) {
+    RST_HIP(hipStreamSynchronize(st));
+    if (ctx->d_bstate) hipFree(ctx->d_bstate);
+    if (ctx->h_bstate) hipHostFree(ctx->h_bstate);
+    ctx->d_bstate = nullptr;
+    ctx->h_bstate = nullptr;
+    ctx->bcap = 0;
+    if (hipMalloc(&ctx->d_bstate, sizeof(IcpState) * B) != hipSuccess ||
+        hipHostMalloc(&ctx->h_bstate, sizeof(IcpState) * B, hipHostMallocDefault) != hipSuccess)
+      return RST_E_NOMEM;
+    ctx->bcap = B;
+  }
+  // per pair: slab and workspace sizes (as icp_launch), carved from one of each
+  const int NVmode = p2plane ? kNP2Plane : kNP2Point;
+  (void)NVmode;
+  const int RS = p2plane ? P2PlaneAcc::RS : P2PointAcc::RS;
+  const int fb_grid = fb_grid_size();
+  std::vector<size_t> slab_off(B), ws_off(B);
+  std::vector<int> nblk(B);
+  size_t slab_tot = 0, ws_tot = 0;
+  int nblk_max = 0;
+  int64_t nmax = 1;
+  auto a256 = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  for (int b = 0; b < B; ++b) {
+    const int64_t n = src[run[b]]->m;
+    nblk[b] = blocks_for(n);
+    nblk_max = std::max(nblk_max, nblk[b]);
+    nmax = std::max(nmax, n);
+    const int ncb = std::min(1024, blocks_for(n));
+    const size_t rows1 = (size_t)std::max(nblk[b] * RS, ncb * 4);
+    slab_off[b] = slab_tot;
+    slab_tot += a256(sizeof(double) * (rows1 + (size_t)kFbBlocks * RS + 64));
+    const size_t np = (size_t)n, ng = refsum ? np : 0, nq = (size_t)nblk[b] * kBS;
+    ws_off[b] = ws_tot;
+    ws_tot += a256(sizeof(float4) * (2 * np + 2 * ng) + sizeof(int4) * nq + sizeof(int32_t) * (2 * nq + 2 * nblk[b] + 64)) +
+              (refsum ? a256(seqsum_bytes(n)) : 0) + 256;
+  }
+  const size_t fb_lds = 2 * sizeof(int) * ((size_t)nblk_max + 1);
+  if (fb_lds > (size_t)96 * 1024) return RST_E_ARG;
+  const size_t pa_off = ws_tot, sq_off = a256(pa_off + sizeof(PairArgs) * B);
+  const size_t ws_all = a256(sq_off + seqsum_pair_bytes() * B);
+  double* slab_all = nullptr;
+  void* ws_all_p = nullptr;
+  RST_CHECK(ctx_slab(ctx, slab_tot, &slab_all));
+  RST_CHECK(ctx_workspace(ctx, ws_all, &ws_all_p));
+  char* W = (char*)ws_all_p;
+  std::vector<PairArgs> pa(B);
+  std::vector<char> sqrec(seqsum_pair_bytes() * B);
+  const IcpParams prm0 = make_params(opts, nmax, nmax);
+  for (int b = 0; b < B; ++b) {
+    const rst_target* S = src[run[b]];
+    const rst_target* T = tgt[run[b]];
+    const int64_t n = S->m;
+    IcpState* dst = ctx->d_bstate + b;
+    double* slab = (double*)((char*)slab_all + slab_off[b]);
+    const int ncb = std::min(1024, blocks_for(n));
+    const size_t rows1 = (size_t)std::max(nblk[b] * RS, ncb * 4);
+    double* slab2 = slab + rows1;
+    double* totals = slab2 + (size_t)kFbBlocks * RS;
+    char* w = W + ws_off[b];
+    const size_t np = (size_t)n, ng = refsum ? np : 0, nq = (size_t)nblk[b] * kBS;
+    float4* cert = (float4*)w;
+    float4* nnq = cert + np;
+    float4* corr = refsum ? nnq + np : nullptr;
+    float4* srco = refsum ? corr + ng : nullptr;
+    int32_t* qbuf = (int32_t*)(cert + 2 * np + 2 * ng);
+    int32_t* qcnt = qbuf + 2 * nq;
+    void* sqws = refsum ? (void*)(((uintptr_t)(qcnt + 2 * nblk[b] + 64) + 255) & ~(uintptr_t)255) : nullptr;
+    RST_HIP(hipMemsetAsync(nnq, 0xff, sizeof(float4) * np, st));
+    // init (per pair, once): the source centroid, the state
+    InitArgs ia;
+    memcpy(ia.pose, poses_in + 16 * run[b], sizeof(ia.pose));
+    ia.mu0 = opts.mu0;
+    ia.need_centroid = p2plane ? 0 : (refsum ? 2 : 1);
+    ia.chain = 0;
+    ia.n = n;
+    float* fsum = (float*)totals;
+    if (refsum) {
+      k_gather_orig<<<blocks_for(n), kBS, 0, st>>>(S->pts, S->inv, n, srco);
+      RST_CHECK(seqsum_enqueue(srco, n, 3, sqws, fsum, st));  // point_cloud_utils.cpp:94-96
+      k_init_state<<<1, kBS, 0, st>>>(slab, 0, fsum, ia, dst);
+    } else if (!p2plane) {
+      const int crows = centroid_device(ctx, S->pts, n, slab);
+      if (crows < 0) return crows;
+      k_init_state<<<1, kBS, 0, st>>>(slab, crows, nullptr, ia, dst);
+    } else {
+      k_init_state<<<1, kBS, 0, st>>>(slab, 0, nullptr, ia, dst);
+    }
+    PairArgs& A = pa[b];
+    A.bv = view_of(T);
+    A.av = adj_of(T);
+    A.pv = T->pix;
+    A.aa.nrm = T->nrm;
+    A.aa.corr = corr;
+    A.aa.pmu = opts.p2plane_mu;
+    A.aa.max_d2 = opts.p2plane_max_dist > 0 ? opts.p2plane_max_dist * opts.p2plane_max_dist : FLT_MAX;
+    A.aa.pos0 = T->pos0;
+    A.aa.full_from = opts.max_iter - 1;
+    A.src = S->pts;
+    A.n = n;
+    A.n_total = n;
+    A.st = dst;
+    A.nnq = nnq;
+    A.cert = cert;
+    A.qbuf = qbuf;
+    A.qcnt = qcnt;
+    A.slab = slab;
+    A.slab2 = slab2;
+    A.srco = srco;
+    A.corr = corr;
+    A.prm = make_params(opts, n, n);
+    A.nb1 = nblk[b];
+    A.lane_min = A.prm.lane_min;
+    if (refsum)
+      seqsum_pair_fill(sqrec.data() + seqsum_pair_bytes() * b, corr, n, sqws, dst->seq,
+#if RST_TIMELINE
+                       &dst->tl[0][0][0]
+#else
+                       nullptr
+#endif
+      );
+  }
+  (void)prm0;
+  const PairArgs* d_pa = (const PairArgs*)(W + pa_off);
+  const void* d_sq = W + sq_off;
+  RST_CHECK(stage_h2d(ctx, (void*)d_pa, pa.data(), sizeof(PairArgs) * B));
+  if (refsum) RST_CHECK(stage_h2d(ctx, (void*)d_sq, sqrec.data(), sqrec.size()));
+  const bool timing = ctx->timing && opts.max_iter > 0;
+  if (timing) {
+    const size_t need = 4 * (size_t)opts.max_iter;
+    while (ctx->ev.size() < need) {
+      hipEvent_t e;
+      RST_HIP(hipEventCreate(&e));
+      ctx->ev.push_back(e);
+    }
+  }
+  const dim3 gnn(nblk_max, 1, B), gfb(fb_grid, 1, B), gone(1, 1, B);
+  for (int it = 0; it < opts.max_iter; ++it) {
+    const bool tm = timing && it % ctx->timing_stride == 0;
+    auto mark = [&](int k) -> int {
+      if (tm) RST_HIP(hipEventRecord(ctx->ev[4 * it + k], st));
+      return RST_OK;
+    };
+    RST_CHECK(mark(0));
+    if (refsum) {
+      k_icp_nn_b<RefAcc><<<gnn, kBS, 0, st>>>(d_pa);
+      RST_CHECK(mark(1));
+      k_icp_fb_b<RefAcc><<<gfb, kBS, fb_lds, st>>>(d_pa);
+      RST_CHECK(mark(2));
+      RST_CHECK(seqsum_enqueue_batch(d_sq, B, nmax, it + 1 == opts.max_iter ? 4 : 3, it, st));
+      k_cov_ref_b<<<dim3(kCovBlocks, 1, B), kBS, 0, st>>>(d_pa);
+      k_reduce_solve_b<RefAcc><<<gone, kRedBS, 0, st>>>(d_pa, kCovBlocks);
+    } else if (p2plane) {
+      k_icp_nn_b<P2PlaneAcc><<<gnn, kBS, 0, st>>>(d_pa);
+      RST_CHECK(mark(1));
+      k_icp_fb_b<P2PlaneAcc><<<gfb, kBS, fb_lds, st>>>(d_pa);
+      RST_CHECK(mark(2));
+      k_reduce_solve_b<P2PlaneAcc><<<gone, kRedBS, 0, st>>>(d_pa, fb_grid);
+    } else {
+      k_icp_nn_b<P2PointAcc><<<gnn, kBS, 0, st>>>(d_pa);
+      RST_CHECK(mark(1));
+      k_icp_fb_b<P2PointAcc><<<gfb, kBS, fb_lds, st>>>(d_pa);
+      RST_CHECK(mark(2));
+      k_reduce_solve_b<P2PointAcc><<<gone, kRedBS, 0, st>>>(d_pa, fb_grid);
+    }
+    RST_CHECK(mark(3));
+  }
+  RST_HIP(hipGetLastError());
+  RST_HIP(hipMemcpyAsync(ctx->h_bstate, ctx->d_bstate, sizeof(IcpState) * B, hipMemcpyDeviceToHost, st));
+  ctx->bpend.active = true;
+  ctx->bpend.timing = timing;
+  return RST_OK;
+}
+
+// one pair's result from its final state (icp_finish's rules)
+static int state_result(const IcpState& h, bool p2plane, int max_iter, int64_t n_total, float pose_inout[16],
+                        float* mean_cost, int32_t* iters_run) {
+  if (h.guard) {
+    static thread_local char msg[160];
+    const int32_t* d = h.path[kQTrace - 1];
+    snprintf(msg, sizeof(msg), "ICP index guard bits %d (detail %d %d %d %d)", h.guard, d[0], d[1], d[2], d[3]);
+    set_last_error(hipErrorIllegalAddress, msg, __FILE__, __LINE__);
+    return RST_E_HIP;
+  }
+  if (iters_run) *iters_run = h.iter;
+  if (p2plane && h.fail) return RST_FALSE;
+  if (max_iter > 0 || p2plane) {
+    for (int c = 0; c < 3; ++c) {
+      for (int r = 0; r < 3; ++r) pose_inout[c * 4 + r] = h.R[c * 3 + r];
+      pose_inout[c * 4 + 3] = 0.f;
+    }
+    for (int r = 0; r < 3; ++r) pose_inout[12 + r] = h.t[r];
+    pose_inout[15] = 1.f;
+  }
+  const float mc = p2plane ? (h.last_cnt > 0 ? (float)sqrt(h.last_d2 / h.last_cnt) : 0.f)
+                           : sqrtf(h.last_cost / (float)n_total);  // :157
+  if (mean_cost) *mean_cost = mc;
+  if (p2plane) return RST_OK;
+  return (mc < 10000.0f) ? RST_OK : RST_FALSE;  // :160 (NaN -> false)
+}
+
+int icp_finish_batch(rst_ctx* ctx, float* poses_inout, float* mean_costs, int32_t* status, int32_t* iters) {
+  if (!ctx || !poses_inout || !status) return RST_E_ARG;
+  if (!ctx->bpend.active) return RST_E_STATE;
+  const auto pd = ctx->bpend;
+  ctx->bpend.active = false;
+  RST_HIP(hipStreamSynchronize(ctx->stream));
+  if (pd.timing) {
+    float tot[3] = {0.f, 0.f, 0.f};
+    int cnt = 0;
+    for (int it = 0; it < pd.max_iter; it += ctx->timing_stride) {
+      for (int k = 0; k < 3; ++k) {
+        float ms = 0.f;
+        RST_HIP(hipEventElapsedTime(&ms, ctx->ev[4 * it + k], ctx->ev[4 * it + k + 1]));
+        tot[k] += ms;
+      }
+      ++cnt;
+    }
+    ctx->last_kernel_ms = cnt ? tot[0] / cnt : 0.f;
+    for (int k = 0; k < 3; ++k) ctx->last_iter_ms[k] = cnt ? tot[k] / cnt : 0.f;
+    ctx->last_kernel_launches = cnt;
+  }
+  int worst = RST_OK;
+  for (int p = 0; p < pd.nb; ++p) {
+    if (mean_costs) mean_costs[p] = 0.f;
+    if (iters) iters[p] = 0;
+    if (pd.slot[p] < 0) {  // pose untouched (align_icp.cpp:77-79)
+      status[p] = RST_FALSE;
+      continue;
+    }
+    status[p] = state_result(ctx->h_bstate[pd.slot[p]], pd.p2plane, pd.max_iter, pd.n_total[p],
+                             poses_inout + 16 * p, mean_costs ? mean_costs + p : nullptr, iters ? iters + p : nullptr);
+    if (status[p] < 0) worst = status[p];
+  }
+  return worst;
+}
+
 // ---- diagnostics: the sharded loop's two halves (rst_debug.h) ------------------------
 // The state a sharded iteration starts from: pose, mu, source centroid and
 // iteration count set directly (k_init_state, then these).
@@ -2159,7 +2539,7 @@ int icp_debug_partials(rst_ctx* ctx, const rst_target* src, const rst_target* tg
   k_debug_state<<<1, 64, 0, st>>>(ctx->d_state, dsm, mu, iter);
   AccArgs aa;
   aa.corr = nullptr;
-  aa.full = 1;
+  aa.full_from = 0;
   aa.nrm = tgt->nrm;
   aa.pmu = opts.p2plane_mu;
   aa.max_d2 = opts.p2plane_max_dist > 0 ? opts.p2plane_max_dist * opts.p2plane_max_dist : FLT_MAX;

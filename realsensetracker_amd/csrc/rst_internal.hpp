@@ -181,6 +181,20 @@ struct rst_ctx {
     int32_t max_iter = 0;
     int64_t n_total = 0;
   } pend;
+  // a batch of frame pairs aligned in lockstep (rst_icp_align_batch_async):
+  // one IcpState per pair, device and pinned host mirrors, grown on demand
+  rst::IcpState* d_bstate = nullptr;
+  rst::IcpState* h_bstate = nullptr;
+  int32_t bcap = 0;
+  struct PendingBatch {
+    bool active = false;
+    bool p2plane = false;
+    bool timing = false;
+    int32_t nb = 0;        // pairs in the call
+    int32_t max_iter = 0;
+    std::vector<int32_t> slot;     // per pair: its state slot, -1 = the reference's early false
+    std::vector<int64_t> n_total;  // per pair
+  } bpend;
 };
 
 struct rst_target {
@@ -267,6 +281,13 @@ int icp_debug_solve(rst_ctx* ctx, const rst_icp_opts* opts, int64_t n_total,
                     const double* totals, const float smean[3], float pose_inout[16],
                     float* mu_inout, int32_t* iter_inout);
 int icp_finish(rst_ctx* ctx, float pose_inout[16], float* mean_cost, int32_t* iters_run);
+// a batch of nb independent pairs in lockstep: one launch per loop kernel for
+// the whole batch (pairs with the reference's early false are left out and
+// reported so by icp_finish_batch); then per pair the same results as
+// icp_finish (status RST_OK / RST_FALSE per pair)
+int icp_launch_batch(rst_ctx* ctx, int nb, const rst_target* const* src, const rst_target* const* tgt,
+                     const rst_icp_opts* opts, const float* poses_in);
+int icp_finish_batch(rst_ctx* ctx, float* poses_inout, float* mean_costs, int32_t* status, int32_t* iters);
 int icp_align_prepared(rst_ctx* ctx, const rst_target* src,
                        const rst_target* tgt, const rst_icp_opts* opts,
                        float pose_inout[16], float* mean_cost,
@@ -306,6 +327,14 @@ int seqsum_enqueue(const float4* d_x, int64_t n, int nch, void* ws, float* d_out
                    hipStream_t st, int* d_stats = nullptr, int stages = 7, int iter = -1,
                    bool fused = false, const SqStretch* stretch = nullptr,
                    unsigned long long* tl = nullptr);
+// a batch of streams summed by one set of launches (the batched ICP loop):
+// a device array of records, one per stream (seqsum_pair_fill writes one
+// into host memory: the stream, its length, its workspace of
+// seqsum_bytes(n), its 4-float output), the chains' count and iteration per
+// launch; nmax = the longest stream.  Always the map pipeline.
+size_t seqsum_pair_bytes();
+void seqsum_pair_fill(void* rec, const float4* d_x, int64_t n, void* ws, float* d_out, unsigned long long* tl);
+int seqsum_enqueue_batch(const void* d_pairs, int nbatch, int64_t nmax, int nch, int iter, hipStream_t st);
 // a stretch's fp64 chain totals (d_tot4[4], non-finite elements skipped)
 // for the relay's exchange; leaves the quarter totals for seqsum_enqueue
 int seqsum_totals(const float4* d_x, int64_t n, int nch, void* ws, double* d_tot4, hipStream_t st,

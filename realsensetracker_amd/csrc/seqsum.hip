@@ -39,6 +39,7 @@
 #include <climits>
 #include <cmath>
 #include <cstdint>
+#include <cstring>
 
 #include "rst_device.hpp"
 #include "rst_internal.hpp"
@@ -252,10 +253,10 @@ __device__ __forceinline__ int quad_or(int a) {
   return a;
 }
 
-__global__ __launch_bounds__(kFrontT) void k_sq_tot(const float4* __restrict__ x, SqView v) {
+__device__ __forceinline__ void sq_tot_body(const float4* __restrict__ x, const SqView& v, const int qt) {
   RST_TL(v.tl, v.it, 2);
   __shared__ double red[kFrontT / kWave][4];
-  const int qt = blockIdx.x, tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid / kWave;
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid / kWave;
   const int64_t i0 = (int64_t)qt * kTotE + 4 * tid;
   float4 q[4];
 #pragma unroll
@@ -308,9 +309,9 @@ __global__ __launch_bounds__(kFrontT) void k_sq_tot(const float4* __restrict__ x
 // boundaries and seeds the guesses: a stale P costs map hits, never a bit
 // of the result).
 template <bool FUSED>
-__global__ __launch_bounds__(kFrontT) void k_sq_front(SqView v, const float4* __restrict__ x,
-                                                     const double* __restrict__ tprev,
-                                                     double* __restrict__ tnext) {
+__device__ __forceinline__ void sq_front_body(const SqView& v, const float4* __restrict__ x,
+                                              const double* __restrict__ tprev, double* __restrict__ tnext,
+                                              const int t, const int c) {
   RST_TL(v.tl, v.it, 3);
   // (one pad float per 16: thread t's window reads xs(16 t + j) at 17 t + j,
   // every lane in its own bank)
@@ -321,7 +322,6 @@ __global__ __launch_bounds__(kFrontT) void k_sq_front(SqView v, const float4* __
   __shared__ double lds[kFrontT / kWave + 1];
   __shared__ double gkey[kKW];
   __shared__ int gid[kKW];
-  const int t = blockIdx.x, c = blockIdx.y;
   const int tid = threadIdx.x;
   const int64_t e0 = (int64_t)t * kTile;
   if (t == 0 && c == 0 && tid == 0) *v.err = 0;
@@ -614,10 +614,9 @@ __device__ __forceinline__ MapEnt leaf_ent(const Run& p, int e0) {
   return en;
 }
 
-__global__ __launch_bounds__(kBuildT) void k_sq_build(SqView v) {
+__device__ __forceinline__ void sq_build_body(const SqView& v, const int k, const int c) {
   RST_TL(v.tl, v.it, 4);
   __shared__ BuildLds W;
-  const int k = blockIdx.x, c = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & (kWave - 1);
   long long* clk = v.clk + ((int64_t)c * v.nk + k) * 8;
   if (tid == 0) clk[0] = (long long)__builtin_amdgcn_s_memtime();
@@ -1160,10 +1159,10 @@ __device__ __forceinline__ void sb_fetch(const SbMap* __restrict__ sbm_, int nk,
   R.eb = sbm[kh].eb;
 }
 
-__global__ __launch_bounds__(kWave) void k_sq_walk(SqView v, float* __restrict__ out) {
+__device__ __forceinline__ void sq_walk_body(const SqView& v, float* __restrict__ out, const int c) {
   RST_TL(v.tl, v.it, 5);
   __shared__ WalkLds W;
-  const int c = blockIdx.x, lane = threadIdx.x;
+  const int lane = threadIdx.x;
   const SbMap* sbm = v.sbm + (int64_t)c * v.nk;
   const float* X = v.soa + (int64_t)c * v.ns;
   int* st = v.stats ? v.stats + c * 8 : nullptr;
@@ -1314,6 +1313,60 @@ __global__ __launch_bounds__(kWave) void k_sq_walk(SqView v, float* __restrict__
   }
 }
 
+// ---- the kernels: one stream (SqView by value), or a batch of streams -----------
+__global__ __launch_bounds__(kFrontT) void k_sq_tot(const float4* __restrict__ x, SqView v) {
+  sq_tot_body(x, v, blockIdx.x);
+}
+template <bool FUSED>
+__global__ __launch_bounds__(kFrontT) void k_sq_front(SqView v, const float4* __restrict__ x,
+                                                     const double* __restrict__ tprev,
+                                                     double* __restrict__ tnext) {
+  sq_front_body<FUSED>(v, x, tprev, tnext, blockIdx.x, blockIdx.y);
+}
+__global__ __launch_bounds__(kBuildT) void k_sq_build(SqView v) { sq_build_body(v, blockIdx.x, blockIdx.y); }
+__global__ __launch_bounds__(kWave) void k_sq_walk(SqView v, float* __restrict__ out) {
+  sq_walk_body(v, out, blockIdx.x);
+}
+
+// A batch of streams (the batched ICP loop, icp.hip): stream = blockIdx.z,
+// its tables from a device array of SqPair records (seqsum_pair_fill); the
+// grids fit the batch's longest stream, the other streams' extra blocks
+// return at once.  nch and iter are the launch's (the records are laid out
+// for 4 chains).
+struct SqPair {
+  const float4* x;
+  float* out;
+  SqView v;
+};
+__device__ __forceinline__ SqView sq_at(const SqPair& P, int nch, int iter) {
+  SqView v = P.v;
+  v.nch = nch;
+  v.it = iter;
+  if (iter >= 0) v.ttot = v.ttot2 + (size_t)(iter & 1) * 4 * kTotQ * v.nk;
+  return v;
+}
+__global__ __launch_bounds__(kFrontT) void k_sq_tot_b(const SqPair* __restrict__ P, int nch, int iter) {
+  const SqPair& p = P[blockIdx.z];
+  const SqView v = sq_at(p, nch, iter);
+  if ((int)blockIdx.x >= v.nk * kTotQ) return;
+  sq_tot_body(p.x, v, blockIdx.x);
+}
+__global__ __launch_bounds__(kFrontT) void k_sq_front_b(const SqPair* __restrict__ P, int nch, int iter) {
+  const SqView v = sq_at(P[blockIdx.z], nch, iter);
+  if ((int)blockIdx.x >= v.nk) return;
+  sq_front_body<false>(v, nullptr, nullptr, nullptr, blockIdx.x, blockIdx.y);
+}
+__global__ __launch_bounds__(kBuildT) void k_sq_build_b(const SqPair* __restrict__ P, int nch, int iter) {
+  const SqView v = sq_at(P[blockIdx.z], nch, iter);
+  if ((int)blockIdx.x >= v.nk) return;
+  sq_build_body(v, blockIdx.x, blockIdx.y);
+}
+__global__ __launch_bounds__(kWave) void k_sq_walk_b(const SqPair* __restrict__ P, int nch, int iter) {
+  const SqPair& p = P[blockIdx.z];
+  const SqView v = sq_at(p, nch, iter);
+  sq_walk_body(v, p.out, blockIdx.x);
+}
+
 }  // namespace
 
 // the workspace layout (seqsum_bytes sizes it for 4 chains)
@@ -1387,6 +1440,34 @@ __global__ void k_sq_copy4(const float* __restrict__ s0, int nch, float* __restr
   if ((int)threadIdx.x < nch) out[threadIdx.x] = s0 ? s0[threadIdx.x] : 0.0f;
 }
 }  // namespace
+
+size_t seqsum_pair_bytes() { return sizeof(SqPair); }
+
+void seqsum_pair_fill(void* rec, const float4* d_x, int64_t n, void* ws, float* d_out, unsigned long long* tl) {
+  SqPair p;
+  p.x = d_x;
+  p.out = d_out;
+  sq_layout(p.v, std::max<int64_t>(n, 1), 4, (char*)ws);
+  p.v.n = n;
+  p.v.stats = nullptr;
+  p.v.p0 = nullptr;
+  p.v.s0 = nullptr;
+  p.v.tl = tl;
+  p.v.it = -1;
+  memcpy(rec, &p, sizeof(p));
+}
+
+int seqsum_enqueue_batch(const void* d_pairs, int nbatch, int64_t nmax, int nch, int iter, hipStream_t st) {
+  if (nch < 1 || nch > 4 || nbatch < 1 || nmax < 1 || nmax > (int64_t)INT_MAX - 2 * kTile) return RST_E_ARG;
+  const int nb = (int)((nmax + kW - 1) / kW), ng = (nb + kGW - 1) / kGW, nk = (ng + kKW - 1) / kKW;
+  const SqPair* P = (const SqPair*)d_pairs;
+  k_sq_tot_b<<<dim3(nk * kTotQ, 1, nbatch), kFrontT, 0, st>>>(P, nch, iter);
+  k_sq_front_b<<<dim3(nk, nch, nbatch), kFrontT, 0, st>>>(P, nch, iter);
+  k_sq_build_b<<<dim3(nk, nch, nbatch), kBuildT, 0, st>>>(P, nch, iter);
+  k_sq_walk_b<<<dim3(nch, 1, nbatch), kWave, 0, st>>>(P, nch, iter);
+  RST_HIP(hipGetLastError());
+  return RST_OK;
+}
 
 int seqsum_totals(const float4* d_x, int64_t n, int nch, void* ws, double* d_tot4, hipStream_t st, int iter) {
   if (nch < 1 || nch > 4 || n < 0) return RST_E_ARG;
