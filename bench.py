@@ -331,6 +331,9 @@ def main():
                     help="frame pairs in flight in the reference-rounding leg: its sequential "
                          "sums run one wavefront per component for most of an iteration, so "
                          "more pairs share the GPU")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="frame pairs per batched align (rst_icp_align_batch_async: one launch of "
+                         "each loop kernel for the whole batch); 0 = one pair per align")
     ap.add_argument("--roof-steps", type=int, default=4,
                     help="frames of the one-pair-in-flight kernel timing pass (roofline)")
     a = ap.parse_args()
@@ -447,6 +450,49 @@ def main():
         for t in prev:
             t.free()
 
+    def run_batched(nsteps: int, opts, normals_k: int, stats: dict | None, ctxs, B: int):
+        # B consecutive frame pairs per align call, in lockstep (one launch of
+        # each loop kernel covers the batch); len(ctxs) batches in flight
+        pending = deque()
+
+        def prep(f):
+            return A.Target.from_depth_device(d_depth[f].value, K, normals_k, pctx)
+
+        def finish_one():
+            pb, c, curs, prevs = pending.popleft()
+            rs = pb.wait()
+            if stats is not None:
+                for r, cur, tg in zip(rs, curs, prevs):
+                    stats["iters"] += r.iterations
+                    stats["iters_all"] += r.iterations
+                    stats["n"] += len(cur)
+                    stats["m"] += len(tg)
+                    stats["ok"] += int(r.ok)
+            for tg in prevs:  # each a target here and a source of a finished pair
+                tg.free()
+
+        prev = prep(0)
+        k, s, nbatch = 1, 0, 0
+        while s < nsteps:
+            nb = min(B, nsteps - s)
+            curs, prevs = [], []
+            for _ in range(nb):
+                cur = prep(pingpong(k, nfr))
+                curs.append(cur)
+                prevs.append(prev)
+                prev = cur
+                k += 1
+            if len(pending) == len(ctxs):
+                finish_one()
+            c = ctxs[nbatch % len(ctxs)]
+            # AlignIcp3d(curr, prev, 128, &xfm), xfm = Identity per pair (rs_replay_app.cpp:235,251)
+            pending.append((A.align_batch_async(curs, prevs, c, None, opts), c, curs, prevs))
+            s += nb
+            nbatch += 1
+        while pending:
+            finish_one()
+        prev.free()
+
     def new_stats():
         return {"iters": 0.0, "iters_all": 0, "n": 0, "m": 0, "ok": 0, "kernel_ms": 0.0,
                 "launches": 0, "iter_ms": [0.0, 0.0, 0.0]}
@@ -466,12 +512,19 @@ def main():
     # ---- throughput mode (value): no events in the timed region -----------------
     # warm-up: W pairs, and at least one per context in flight, so that no
     # context sizes its device workspace inside the timed region
-    run(max(a.warmup, len(actx)), opts_main, 0, None)
+    batched = a.batch > 0 and not pyr
+    if batched:
+        run_batched(max(a.warmup, len(actx) * a.batch), opts_main, 0, None, actx, a.batch)
+    else:
+        run(max(a.warmup, len(actx)), opts_main, 0, None)
     st = new_stats()
     barrier()
     sync_all()
     t0 = time.perf_counter()
-    run(a.steps, opts_main, 0, st)
+    if batched:
+        run_batched(a.steps, opts_main, 0, st, actx, a.batch)
+    else:
+        run(a.steps, opts_main, 0, st)
     sync_all()
     barrier()
     dt = max_over_ranks(time.perf_counter() - t0)
@@ -676,7 +729,9 @@ def main():
                                     "default; outside the 1e-4 gate of the reference's fp32 "
                                     "sums, see ref_sums)"),
                    "parallelism": f"replica{world}",
-                   "pairs_in_flight_per_gpu": len(actx), "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
+                   "pairs_in_flight_per_gpu": len(actx) * (a.batch if a.batch > 0 and not pyr else 1),
+                   "pairs_per_batch": a.batch if a.batch > 0 and not pyr else 1,
+                   "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
                    "hipgraph": bool(a.graphs)},
         "frames_per_s": frames_all / dt,
         "pairs_ok": st["ok"],
