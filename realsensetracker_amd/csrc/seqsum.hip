@@ -520,6 +520,8 @@ static_assert(kBuildT >= kMaxSbBlocks + 1 && kBuildT >= kMaxSbGroups * kGroupR &
 static_assert(sizeof(Leaf) == 64, "a leaf map is four int4");
 constexpr int kXPad = kMaxSbElems + kMaxSbElems / kW + 2 * kW;  // padded staging (see xp)
 constexpr int kListCap = (kLeafR - 1) * kMaxSbBlocks;
+constexpr int16_t kNeedNone = INT16_MIN;  // kNoNeed in 16 bits
+static_assert((kMaxSbBlocks << 2 | 3) <= 0xffff && (kMaxSbGroups << 4 | 15) <= 0xffff, "list codes in 16 bits");
 static_assert(kListCap >= kMaxSbGroups * kGroupR, "the group list shares the leaf list's storage");
 
 // A composite lane's step through a child map, without branches (the
@@ -569,17 +571,22 @@ __device__ __forceinline__ float cand(float G, int e0, int r) {
 // (r05: unpadded, stride 16, 3.3 conflicts per LDS instruction)
 __device__ __forceinline__ int xp(int a) { return a + (a >> 4); }
 
+// (<= 80 KB: two workgroups per CU -- one's composites, a wavefront or two,
+// beside the other's leaves; the group maps reuse the elements' space, done
+// with once the leaves are)
 struct BuildLds {
-  float x[kXPad];
+  union {
+    float x[kXPad];
+    GroupMap gm[kMaxSbGroups];
+  };
   Leaf lf[kMaxSbBlocks];
-  GroupMap gm[kMaxSbGroups];
   int sbs[kMaxSbBlocks + 1];   // block starts, relative to the superblock's first element
   int sgs[kMaxSbGroups + 1];   // group starts, relative to its first block
-  int xneed[kMaxSbBlocks][kLeafR - 1];  // the extra candidates' lattice needs
+  int16_t xneed[kMaxSbBlocks][kLeafR - 1];  // the extra candidates' lattice needs (kNeedNone: none)
   // extra leaf candidates (block << 2 | r): up to kLeafR - 1 per block (a
   // stream of exact ties needs them for most blocks); then the group list
   // (group << 4 | r), at most kMaxSbGroups x kGroupR
-  int list[kListCap];
+  uint16_t list[kListCap];
   int nlist;
   int bad;
   double base[2];              // fp64 increments of the tiles before the superblock's first
@@ -710,7 +717,7 @@ __device__ __forceinline__ void sq_build_body(const SqView& v, const int k, cons
       const int at = atomicAdd(&W.nlist, kLeafR - 1);
       if (at + kLeafR - 1 <= kListCap) {  // (always: kListCap covers every block)
 #pragma unroll
-        for (int r = 1; r < kLeafR; ++r) W.list[at + r - 1] = tid << 2 | r;
+        for (int r = 1; r < kLeafR; ++r) W.list[at + r - 1] = (uint16_t)(tid << 2 | r);
       } else {
         atomicOr(v.err, 64);
       }
@@ -740,7 +747,7 @@ __device__ __forceinline__ void sq_build_body(const SqView& v, const int k, cons
         leaf_run(q, W, xa, xl, wmax, xG, xe0, r);
         if (j < nl) {
           W.lf[bl].e[r] = leaf_ent(q, xe0);
-          W.xneed[bl][r - 1] = q.need;
+          W.xneed[bl][r - 1] = q.need == kNoNeed ? kNeedNone : (int16_t)max(-32767, min(32767, q.need));
         }
       }
     }
@@ -750,7 +757,10 @@ __device__ __forceinline__ void sq_build_body(const SqView& v, const int k, cons
     int need = p.need;
     if (more)
 #pragma unroll
-      for (int r = 1; r < kLeafR; ++r) need = max(need, W.xneed[tid][r - 1]);
+      for (int r = 1; r < kLeafR; ++r) {
+        const int xn = W.xneed[tid][r - 1];
+        need = max(need, xn == kNeedNone ? kNoNeed : xn);
+      }
     const int mneed = need == kNoNeed ? 0 : max(0, need - e0);
     const bool exact_only = mneed > kLeafM;
     const int m = exact_only ? 0 : mneed;
@@ -805,7 +815,7 @@ __device__ __forceinline__ void sq_build_body(const SqView& v, const int k, cons
     if (R > 1) {
       const int at = atomicAdd(&W.nlist, R - 1);
       for (int r = 1; r < R; ++r)
-        if (at + r - 1 < kListCap) W.list[at + r - 1] = gi << 4 | r;  // (<= 496 entries: always)
+        if (at + r - 1 < kListCap) W.list[at + r - 1] = (uint16_t)(gi << 4 | r);  // (<= 496 entries: always)
     }
   }
   __syncthreads();
