@@ -175,7 +175,8 @@ def callers_cpu_baseline(raw, iters: int):
 
 
 def load_traffic():
-    """HBM bytes per iteration of the NN pass (k_icp_nn + k_icp_fb) from a
+    """HBM bytes per pair iteration of the NN pass (k_icp_nn + k_icp_fb, or
+    a batched launch's share per pair) from a
     committed PMC summary (profiles/pmc_*.json, scripts/pmc_traffic.py) --
     only one stamped with this library's source hash (lib/BUILD_INFO.json):
     a pass of other code is not reported.  Returns (bytes | None, origin)."""
@@ -189,8 +190,8 @@ def load_traffic():
             d = json.loads(f.read_text())
         except ValueError:
             continue
-        if cur and d.get("source_hash") == cur and "nn_pass_bytes_per_iteration" in d:
-            return d["nn_pass_bytes_per_iteration"], f.name
+        if cur and d.get("source_hash") == cur and "nn_pass_bytes_per_pair_iteration" in d:
+            return d["nn_pass_bytes_per_pair_iteration"], f.name
     return None, f"no PMC pass of this build (source hash {cur}) under profiles/"
 
 
@@ -316,8 +317,9 @@ def main():
                          "ref = RST_SUM_REF (the drop-in default: the reference's sequential "
                          "fp32 sums, bit-exact); the other mode is timed as an extra field")
     ap.add_argument("--inflight", type=int, default=0,
-                    help="frame pairs in flight per GPU (one HIP stream each; 0: 4 in the "
-                         "fp64 mode, --ref-inflight in the ref mode)")
+                    help="aligns in flight per GPU, one HIP stream each (a batched align "
+                         "carries --batch pairs); 0: 4 batched, else 4 in the fp64 mode and "
+                         "--ref-inflight in the ref mode")
     ap.add_argument("--hw-queues", type=int, default=24,
                     help="GPU_MAX_HW_QUEUES for this process (HIP's default, 4, puts the "
                          "frame-preparation stream and 4 pairs' streams on 4 hardware queues; "
@@ -331,11 +333,13 @@ def main():
                     help="frame pairs in flight in the reference-rounding leg: its sequential "
                          "sums run one wavefront per component for most of an iteration, so "
                          "more pairs share the GPU")
-    ap.add_argument("--batch", type=int, default=0,
+    ap.add_argument("--batch", type=int, default=8,
                     help="frame pairs per batched align (rst_icp_align_batch_async: one launch of "
-                         "each loop kernel for the whole batch); 0 = one pair per align")
+                         "each loop kernel for the whole batch, r06h: 8 x 4 in flight 23.0k it/s "
+                         "vs 15.1k for 24 single aligns); 0 = one pair per align")
     ap.add_argument("--roof-steps", type=int, default=4,
-                    help="frames of the one-pair-in-flight kernel timing pass (roofline)")
+                    help="frames of the one-pair-in-flight kernel timing pass (roofline; "
+                         "batched: the value leg's --steps pairs, one batch in flight)")
     a = ap.parse_args()
     if a.hw_queues > 0:  # read by the HIP runtime at its first call (none yet)
         os.environ["GPU_MAX_HW_QUEUES"] = str(a.hw_queues)
@@ -387,8 +391,9 @@ def main():
     opts_exact = L.default_opts(max_iter=a.iters, sum_mode=L.RST_SUM_REF)
     main_ref = a.sum_mode == "ref"
     opts_main, opts_other = (opts_exact, opts_fp64) if main_ref else (opts_fp64, opts_exact)
+    batched = a.batch > 0 and not pyr
     if a.inflight <= 0:
-        a.inflight = a.ref_inflight if main_ref else 4
+        a.inflight = 4 if batched or not main_ref else a.ref_inflight
     opts_pl = L.default_opts(mode=L.RST_P2PLANE, max_iter=30)
     # frame preparation on its own context (stream); each frame pair in
     # flight on its own context, so the latency-bound per-iteration chains
@@ -462,6 +467,15 @@ def main():
             pb, c, curs, prevs = pending.popleft()
             rs = pb.wait()
             if stats is not None:
+                ms, nl = c.last_kernel_time()
+                stats["kernel_ms"] += ms * nl
+                stats["launches"] += nl
+                if nl:
+                    it3, _ = c.last_iteration_times()
+                    for k in range(3):
+                        stats["iter_ms"][k] += it3[k] * nl
+                stats["batches"] += 1
+                stats["batch_pairs"] += len(rs)
                 for r, cur, tg in zip(rs, curs, prevs):
                     stats["iters"] += r.iterations
                     stats["iters_all"] += r.iterations
@@ -495,7 +509,7 @@ def main():
 
     def new_stats():
         return {"iters": 0.0, "iters_all": 0, "n": 0, "m": 0, "ok": 0, "kernel_ms": 0.0,
-                "launches": 0, "iter_ms": [0.0, 0.0, 0.0]}
+                "launches": 0, "iter_ms": [0.0, 0.0, 0.0], "batches": 0, "batch_pairs": 0}
 
     if a.graphs:
         for c in actx:
@@ -512,7 +526,6 @@ def main():
     # ---- throughput mode (value): no events in the timed region -----------------
     # warm-up: W pairs, and at least one per context in flight, so that no
     # context sizes its device workspace inside the timed region
-    batched = a.batch > 0 and not pyr
     if batched:
         run_batched(max(a.warmup, len(actx) * a.batch), opts_main, 0, None, actx, a.batch)
     else:
@@ -537,9 +550,15 @@ def main():
     # pair holds; alone, the spans agree with rocprof's kernel durations)
     # (under --graphs the timing pass runs its one context in stream mode:
     # events cannot sit inside a replayed graph)
+    # (batched: one batch in flight, its launches cover the batch's pairs; the
+    # value leg's frame pairs, whose difficulty varies along the trajectory:
+    # r06 first 8 pairs nn+fb 281 us, pairs 25-32 126 us per batched launch)
     sr1 = new_stats()
     actx[0].enable_kernel_timing(1)  # (a timed align runs in stream mode)
-    run(a.roof_steps, opts_main, 0, sr1, ctxs=actx[:1])
+    if batched:
+        run_batched(a.steps, opts_main, 0, sr1, actx[:1], a.batch)
+    else:
+        run(a.roof_steps, opts_main, 0, sr1, ctxs=actx[:1])
     actx[0].enable_kernel_timing(0)
 
     # ---- point-to-plane mode (extra fields) ---------------------------------------
@@ -578,21 +597,28 @@ def main():
     # leg: RST_SUM_FP64 as "fp64_sums"
     refs = None
     if a.ref_steps > 0 and not pyr:
-        n_other = 4 if main_ref else a.ref_inflight
+        n_other = 4 if main_ref or batched else a.ref_inflight
         rctx = (actx + [A.Context(local) for _ in range(max(0, n_other - len(actx)))])[:n_other]
-        run(len(rctx), opts_other, 0, None, rctx)  # every context warmed (as above)
+        if batched:
+            run_batched(len(rctx) * a.batch, opts_other, 0, None, rctx, a.batch)
+        else:
+            run(len(rctx), opts_other, 0, None, rctx)  # every context warmed (as above)
         sr = new_stats()
         barrier()
         sync_all()
         t4 = time.perf_counter()
-        run(a.ref_steps, opts_other, 0, sr, rctx)
+        if batched:
+            run_batched(a.ref_steps, opts_other, 0, sr, rctx, a.batch)
+        else:
+            run(a.ref_steps, opts_other, 0, sr, rctx)
         sync_all()
         barrier()
         dtr = max_over_ranks(time.perf_counter() - t4)
         refs = {"iterations_per_s": sum_over_ranks(sr["iters"]) / dtr,
                 "frames_per_s": sum_over_ranks(a.ref_steps) / dtr,
                 "ms_per_pair": 1000.0 * dtr / a.ref_steps, "steps": a.ref_steps,
-                "pairs_in_flight": len(rctx),
+                "pairs_in_flight": len(rctx) * (a.batch if batched else 1),
+                "pairs_per_batch": a.batch if batched else 1,
                 "pairs_ok": sr["ok"],
                 "note": ("RST_SUM_FP64 (throughput mode, not the drop-in default): fp64 "
                          "partial sums, pose within 2e-5 of the fp64-sum oracle but not "
@@ -683,11 +709,15 @@ def main():
     nn_us = kern_us[0] + kern_us[1]
     n_avg = st["n"] / max(1, a.steps)
     m_avg = st["m"] / max(1, a.steps)
-    alg_bytes = p2point_alg_bytes(n_avg, m_avg)
+    # a batched launch covers the batch's pairs: per-pair bytes x pairs per launch
+    pairs_per_launch = sr1["batch_pairs"] / max(1, sr1["batches"]) if batched else 1.0
+    alg_bytes = p2point_alg_bytes(n_avg, m_avg) * pairs_per_launch
     achieved = alg_bytes / (nn_us * 1e-6) / 1e9 if nn_us > 0 else 0.0
     # the committed PMC pass is of the default workload only
     traffic, traffic_src = (load_traffic() if (a.workload, a.width, a.height) ==
                             ("stream", 640, 480) else (None, "PMC pass is of the 640x480 stream"))
+    if traffic is not None:
+        traffic *= pairs_per_launch
 
     if rank != 0:
         rdv.close()
@@ -729,8 +759,8 @@ def main():
                                     "default; outside the 1e-4 gate of the reference's fp32 "
                                     "sums, see ref_sums)"),
                    "parallelism": f"replica{world}",
-                   "pairs_in_flight_per_gpu": len(actx) * (a.batch if a.batch > 0 and not pyr else 1),
-                   "pairs_per_batch": a.batch if a.batch > 0 and not pyr else 1,
+                   "pairs_in_flight_per_gpu": len(actx) * (a.batch if batched else 1),
+                   "pairs_per_batch": a.batch if batched else 1,
                    "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
                    "hipgraph": bool(a.graphs)},
         "frames_per_s": frames_all / dt,
@@ -739,13 +769,19 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "stream_copy_GBps": copy_gbps,
-                     "kernel": "k_icp_nn+k_icp_fb (one ICP iteration's NN pass: certificate "
-                               "stream + compacted searches)",
+                     "kernel": ("k_icp_nn_b+k_icp_fb_b (one ICP iteration's NN pass of a batch "
+                                f"of {pairs_per_launch:g} pairs: certificate stream + compacted "
+                                "searches)" if batched else
+                                "k_icp_nn+k_icp_fb (one ICP iteration's NN pass: certificate "
+                                "stream + compacted searches)"),
+                     "pairs_per_launch": pairs_per_launch,
                      "avg_us": nn_us, "alg_bytes_per_launch": alg_bytes,
                      "kernels_avg_us": {"k_icp_nn": kern_us[0], "k_icp_fb": kern_us[1],
                                         "rest_of_iteration": kern_us[2]},
-                     "timing": f"HIP events around every iteration's kernels, one pair in "
-                               f"flight, {a.roof_steps} frames ({sr1['launches']} iterations)",
+                     "timing": (f"HIP events around every iteration's kernels, one "
+                                f"{'batch' if batched else 'pair'} in flight, "
+                                f"{sr1['batch_pairs'] if batched else a.roof_steps} frame pairs "
+                                f"({sr1['launches']} iterations)"),
                      "traffic_source": traffic_src},
         "cpu_baseline": cpu,
     }

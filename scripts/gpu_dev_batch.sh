@@ -25,7 +25,7 @@ if [ -n "${PROF:-1}" ]; then
 import csv, glob, re
 f = glob.glob("gpurun_out/prof_${TAG}/**/*kernel_stats.csv", recursive=True)[0]
 for r in list(csv.DictReader(open(f)))[:10]:
-    n = re.sub(r"\(.*", "", r["Name"]).replace("rst::(anonymous namespace)::", "")
+    n = re.sub(r"\(.*", "", r["Name"].replace("rst::(anonymous namespace)::", ""))
     print(f"{n[:60]:<60} {int(r['Calls']):6d} {float(r['AverageNs']) / 1e3:9.1f} us")
 PY
 fi

@@ -7,13 +7,17 @@ on gfx950, WRITE_SIZE (KiB) as is.  Writes the JSON bench.py reads, stamped
 with the library's source hash (lib/BUILD_INFO.json): bench.py reports the
 traffic only while it matches the library it runs.
 
-  python scripts/pmc_traffic.py OUT.json FETCH.csv WRITE.csv [RefAcc|P2PointAcc]"""
+A batched run (k_icp_nn_b / k_icp_fb_b: one launch per batch of PAIRS frame
+pairs, every batch full) is divided by PAIRS: the JSON holds bytes per pair
+iteration, bench.py scales them by its pairs per launch.
+
+  python scripts/pmc_traffic.py OUT.json FETCH.csv WRITE.csv [RefAcc|P2PointAcc] [PAIRS]"""
 import csv
 import json
 import sys
 
-KERNELS = ("k_icp_nn<", "k_icp_fb<")
 ACC = sys.argv[4] if len(sys.argv) > 4 else "RefAcc"
+PAIRS = int(sys.argv[5]) if len(sys.argv) > 5 else 1
 
 
 def per_dispatch(path, counter, kernel):
@@ -34,7 +38,10 @@ def main():
     d = {"kernels": {}, "note": "FETCH_SIZE x2 (gfx950), WRITE_SIZE as is; rocprofv3 --pmc, "
                                 "separate passes; per launch, " + ACC + " instances"}
     tot = 0.0
-    for k in KERNELS:
+    batched = any("k_icp_nn_b<" in r["Kernel_Name"] for r in csv.DictReader(open(fpath)))
+    kernels = ("k_icp_nn_b<", "k_icp_fb_b<") if batched else ("k_icp_nn<", "k_icp_fb<")
+    d["pairs_per_launch"] = PAIRS if batched else 1
+    for k in kernels:
         f = per_dispatch(fpath, "FETCH_SIZE", k)
         w = per_dispatch(wpath, "WRITE_SIZE", k)
         if not f or not w:
@@ -46,7 +53,8 @@ def main():
                                        "bytes_per_launch": fm + wm,
                                        "fetch_size_kib_median_raw": f[len(f) // 2]}
         tot += fm + wm
-    d["nn_pass_bytes_per_iteration"] = tot
+    d["nn_pass_bytes_per_iteration"] = tot  # per launch
+    d["nn_pass_bytes_per_pair_iteration"] = tot / d["pairs_per_launch"]
     try:
         d["source_hash"] = json.load(open("realsensetracker_amd/lib/BUILD_INFO.json"))["source_hash"]
     except (OSError, KeyError, ValueError):

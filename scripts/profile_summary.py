@@ -24,5 +24,5 @@ for line in open(log):
         d = json.loads(line)
         rf = d["roofline"]
         print(f"\nsame command's bench line: value {d['value']:.1f} {d['unit']}, "
-              f"{rf['kernel']} avg {rf['avg_us']:.2f} us (HIP events, every 8th iteration), "
+              f"{rf['kernel']} avg {rf['avg_us']:.2f} us (HIP events: {rf.get('timing', '')}), "
               f"achieved {rf['achieved']:.1f} GB/s = {100*rf['frac']:.2f}% of {rf['peak']} GB/s")
