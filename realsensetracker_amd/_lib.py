@@ -12,8 +12,8 @@ from pathlib import Path
 
 import numpy as np
 
-LIB_PATH = Path(os.environ.get(
-    "RST_LIB", Path(__file__).resolve().parent / "lib" / "librst_align.so"))
+LIB_PATH = Path(os.environ.get("RST_LIB")  # (an empty value: the default)
+                or Path(__file__).resolve().parent / "lib" / "librst_align.so")
 
 RST_OK, RST_FALSE = 0, 1
 RST_E_ARG, RST_E_HIP, RST_E_NOMEM, RST_E_NODEVICE, RST_E_COMM, RST_E_STATE = -1, -2, -3, -4, -5, -6

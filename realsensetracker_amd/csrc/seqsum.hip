@@ -566,10 +566,196 @@ __device__ __forceinline__ float cand(float G, int e0, int r) {
   return (float)((double)G + ldexp((double)r, e0));
 }
 
+// One speculative step in the integers (scalar ALU): the end E_r + du 2^e0
+// as E_r's bits plus du in E_r's grid -- what the float formula gives
+// whenever the step is valid (the offset rule keeps E_r + d in E_r's binade,
+// d a multiple of its grid), up to a power-of-two E_r, which the lanes'
+// checks (the float formula) catch like any unverified step.  sh = e0 minus
+// E_r's grid exponent, per entry, computed lane-parallel beside the entries
+// (step_shift).  r06: the float formula's VALU round trip (v_readfirstlane,
+// cvt, ldexp, sub) made a step ~250 clocks.
+__device__ __forceinline__ int step_shift(float E, int e0) {
+  return e0 - (max((int)((__float_as_uint(E) >> 23) & 0xffu), 1) - 150);
+}
+__device__ __forceinline__ int step_bits(int Eb, int du, int sh) {
+  // (shift counts masked to 5 bits as the scalar shifts take them: a clamp
+  // selects v_med3 and moves the whole chain to vector registers; an
+  // out-of-range shift only yields a value the checks reject)
+  const int l = max(sh, 0) & 31, rr = max(-sh, 0) & 31;
+  const int u = (du << l) >> rr;
+  return Eb >= 0 ? Eb + u : Eb - u;  // (a negative float's bits are a negative int)
+}
+
+// The speculative chain of a run of maps as a parallel prefix (r06: a
+// step-by-step scalar chain cost ~250 clocks a step, its dependent
+// scalar / v_readlane round trips).  For a fixed residue r the step of
+// lane q's map is affine in the input's bits x (same sign and binade as G,
+// what the checks verify): x' = Eb + sE 2^sh (sG (x - gb) - r) =
+// A_q + B_q x, B_q = sE sG 2^sh.  An inclusive scan of (A, B) over the
+// chunk's lanes (DPP row shifts, lanes < 16: kWalkC) composes the steps;
+// lane q's input is the composition of the steps before it applied to
+// sb0.  A, B are dyadic rationals far inside double's 53 bits (x < 2^31,
+// |sh| small), so the prefix is exact wherever the steps are valid; a value
+// that is not an int32 becomes NaN bits, which no check accepts.
+template <int CTRL>
+__device__ __forceinline__ int dpp_row(int old, int x) {
+  return __builtin_amdgcn_update_dpp(old, x, CTRL, 0xf, 0xf, false);
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_row(double old, double x) {
+  const uint2 o = __builtin_bit_cast(uint2, old), u = __builtin_bit_cast(uint2, x);
+  const int lo = __builtin_amdgcn_update_dpp((int)o.x, (int)u.x, CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp((int)o.y, (int)u.y, CTRL, 0xf, 0xf, false);
+  return __builtin_bit_cast(double, make_uint2((unsigned)lo, (unsigned)hi));
+}
+template <int D>
+__device__ __forceinline__ void affine_scan_step(double& A, int& e, int& sg) {
+  constexpr int kRowShr = 0x110 + D;  // DPP row_shr:D (lanes below D in their row keep `old`)
+  const double Ap = dpp_row<kRowShr>(0.0, A);  // (identity: A = 0, B = +1)
+  const int ep = dpp_row<kRowShr>(0, e);
+  const int sp = dpp_row<kRowShr>(1, sg);
+  A = A + (double)sg * ldexp(Ap, e);
+  e += ep;
+  sg *= sp;
+}
+// lane q (< nq <= 16): Eb, sh, gb, r of its map's step; returns lane q's
+// input (lane 0: sb0), lane nq the chunk's end
+__device__ __forceinline__ int affine_hist(int sb0, int Eb, int sh, int gb, int r, int nq) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const bool on = lane < nq;
+  const int sgG = (gb >> 31) | 1, sgE = (Eb >> 31) | 1;
+  double A = on ? (double)Eb - (double)sgE * ldexp((double)((int64_t)sgG * gb + r), sh) : 0.0;
+  int e = on ? sh : 0;
+  int sg = on ? sgE * sgG : 1;
+  affine_scan_step<1>(A, e, sg);
+  affine_scan_step<2>(A, e, sg);
+  affine_scan_step<4>(A, e, sg);
+  affine_scan_step<8>(A, e, sg);
+  const double val = A + (double)sg * ldexp((double)sb0, e);
+  const bool okv = val == rint(val) && val >= -2147483648.0 && val < 2147483648.0;
+  const int vi = okv ? (int)(int64_t)val : 0x7fc00000;
+  const int h = __shfl(vi, (lane + kWave - 1) & (kWave - 1), kWave);
+  return lane == 0 ? sb0 : h;
+}
+
+// A chunk's speculative inputs from sb0 (lane q < nq: map maps[ql], ql = q):
+// every step with residue 0 first; when a map of the chunk has several
+// residues, again with each lane's residue from the first pass's input (right
+// whenever the steps before it were)
+template <class Map>
+__device__ __forceinline__ int spec_hist(int sb0, const Map* maps, int ql, const MapHdr& hl, int gbl, int sgl,
+                                         int mkl, int nq) {
+  const int lane = threadIdx.x & (kWave - 1);
+  float El = maps[ql].e[0].E;
+  int hist = affine_hist(sb0, (int)__float_as_uint(El), step_shift(El, hl.e0), gbl, 0, nq);
+  if (__ballot(lane < nq && mkl != 0) != 0) {
+    const int rl = (((hist - gbl) ^ sgl) - sgl) & mkl;
+    El = maps[ql].e[rl].E;
+    hist = affine_hist(sb0, (int)__float_as_uint(El), step_shift(El, hl.e0), gbl, rl, nq);
+  }
+  return hist;
+}
+
+
+// One candidate x through maps[0, n) (LDS) -- the same statement as
+// comp_off / comp_apply map after map, made by the whole wavefront: up to
+// kChainC maps a round, the values speculated in scalar registers
+// (step_bits, the entries by v_readlane), then every step checked on its
+// own lane (same binade, usable header, in window, exact, the value the
+// speculation carried on) and the window narrowed by a reduction over the
+// verified lanes.  A step that fails its check -- x in another binade than
+// the map's G, or a power-of-two end -- is taken by comp_off / comp_apply
+// themselves, so the result is theirs, bit for bit.  False: the candidate
+// cannot pass (no map for it).  r06: a lane stepping through the maps with
+// an LDS read per step took ~13k clocks for a superblock's 16 groups.
+constexpr int kChainC = 16;
+constexpr int kSbChainR = 4;
+#ifndef RST_SQ_GROUP_CHAIN
+#define RST_SQ_GROUP_CHAIN 0  // the group composites by comp_chain (else a lane each)
+#endif  // superblock candidates taken by comp_chain (more: a lane each)
+template <class Map>
+__device__ __forceinline__ bool comp_chain(float& x, double& clo, double& chi, const Map* maps, int n, int mmax) {
+  const int lane = threadIdx.x & (kWave - 1);
+  n = __builtin_amdgcn_readfirstlane(n);  // (every lane's alike: a scalar loop)
+  int q0 = 0;
+  while (q0 < n) {
+    const int nq = __builtin_amdgcn_readfirstlane(min(n - q0, kChainC));
+    const Map* mp = maps + q0;
+    const int ql = min(lane, nq - 1);
+    const MapHdr hl = mp[ql].h;
+    const int gbl = (int)__float_as_uint(hl.G);
+    const int sgl = gbl >> 31;
+    const int mkl = (1 << min(hl.m & 7, mmax)) - 1;
+    const int sb0 = __builtin_amdgcn_readfirstlane((int)__float_as_uint(x));
+    int hist = spec_hist(sb0, mp, ql, hl, gbl, sgl, mkl, nq);
+    const int nxb = __shfl(hist, lane + 1, kWave);
+    bool okl;
+    double lo, hi;
+    {
+      const bool same = (((uint32_t)hist ^ (uint32_t)gbl) >> 23) == 0u;
+      const bool hv = !(hl.flags & kOpaque) && hl.m >= 0 && hl.m <= mmax;
+      const int kk = ((hist - gbl) ^ sgl) - sgl;
+      const int r = kk & mkl;
+      const MapEnt en = mp[ql].e[r];
+      const int du = kk - r;
+      const bool inwin = en.LOu <= du && du <= en.HIu;
+      const float dd = ldexpf((float)du, hl.e0);
+      const float o = en.E + dd;
+      const bool ebig = fabsf(en.E) >= fabsf(dd);
+      const bool exact = ebig ? (o - en.E == dd) : (o - dd == en.E);
+      const float xo = du == 0 ? en.E : o;
+      okl = lane < nq && same && hv && inwin && (du == 0 || exact) && (int)__float_as_uint(xo) == nxb;
+      lo = ldexp((double)(en.LOu - du), hl.e0);
+      hi = ldexp((double)(en.HIu - du), hl.e0);
+    }
+    const uint64_t bad = __ballot(!okl) & ((1ull << nq) - 1);
+    const int qf = bad ? (int)__builtin_ctzll(bad) : nq;
+    // the verified steps' windows (lanes < qf < kChainC <= 16: one row)
+    lo = lane < qf ? lo : -INFINITY;
+    hi = lane < qf ? hi : INFINITY;
+#pragma unroll
+    for (int o = kChainC / 2; o > 0; o >>= 1) {
+      lo = fmax(lo, __shfl_xor(lo, o, kWave));
+      hi = fmin(hi, __shfl_xor(hi, o, kWave));
+    }
+    clo = fmax(clo, __shfl(lo, 0, kWave));
+    chi = fmin(chi, __shfl(hi, 0, kWave));
+    x = __int_as_float(__builtin_amdgcn_readlane(hist, qf));
+    if (qf == nq) {
+      q0 += nq;
+      continue;
+    }
+    // step q0 + qf by the lane statement itself (every lane alike)
+    const MapHdr H = mp[qf].h;
+    bool ok = true;
+    const int kq = comp_off(x, H, mmax, ok);
+    if (!ok) return false;
+    comp_apply(x, clo, chi, ok, H, kq, mp[qf].e[kq & ((1 << H.m) - 1)]);
+    if (!ok) return false;
+    q0 += qf + 1;
+  }
+  return true;
+}
+
 // staged element a of the superblock at a + a / 16: lane j's block starts
 // near 16 j, so the lanes of a step read 17 words apart -- distinct banks
 // (r05: unpadded, stride 16, 3.3 conflicts per LDS instruction)
 __device__ __forceinline__ int xp(int a) { return a + (a >> 4); }
+
+// the wavefront's largest v, v in [lo, lo + 2^B): B ballots, most significant
+// bit first -- no cross-lane data move (a shuffle butterfly is six LDS-unit
+// round trips, ~600 clocks)
+template <int B>
+__device__ __forceinline__ int wave_max_small(int v, int lo = 0) {
+  const int u = v - lo;
+  int hi = 0;
+#pragma unroll
+  for (int b = B - 1; b >= 0; --b) {
+    const int t = hi | (1 << b);
+    hi = __ballot(u >= t) != 0 ? t : hi;
+  }
+  return hi + lo;
+}
 
 // (<= 80 KB: two workgroups per CU -- one's composites, a wavefront or two,
 // beside the other's leaves; the group maps reuse the elements' space, done
@@ -596,16 +782,25 @@ struct BuildLds {
 // one monitored run of block bl from candidate r (the elements from LDS into
 // registers first: the run's chain waits on no LDS read), at most `wmax`
 // steps (the wavefront's longest block, uniform)
+template <bool UNROLL>
 __device__ __forceinline__ void leaf_run(Run& p, const BuildLds& W, int a0, int len, int wmax, float G, int e0,
                                          int r) {
   run_init(p, cand(G, e0, r));
-  float xr[2 * kW - 1];
+  if constexpr (UNROLL) {
+    float xr[2 * kW - 1];
 #pragma unroll
-  for (int i = 0; i < 2 * kW - 1; ++i) xr[i] = W.x[xp(min(a0 + i, kMaxSbElems - 1))];
+    for (int i = 0; i < 2 * kW - 1; ++i) xr[i] = W.x[xp(min(a0 + i, kMaxSbElems - 1))];
+    // (predicated, not a break: the loop unrolls, xr[i] stays a register --
+    // a rolled loop indexed xr through s_set_gpr_idx)
 #pragma unroll
-  for (int i = 0; i < 2 * kW - 1; ++i) {
-    if (i >= wmax) break;
-    if (i < len) run_step(p, xr[i], e0);
+    for (int i = 0; i < 2 * kW - 1; ++i) {
+      if (i < wmax) {
+        if (i < len) run_step(p, xr[i], e0);
+      }
+    }
+  } else {  // (the rare extra candidates: compact code)
+    for (int i = 0; i < wmax; ++i)
+      if (i < len) run_step(p, W.x[xp(min(a0 + i, kMaxSbElems - 1))], e0);
   }
 }
 
@@ -701,12 +896,9 @@ __device__ __forceinline__ void sq_build_body(const SqView& v, const int k, cons
       e0 = grid_exp(G);
     }
     // the wavefront's longest block bounds the unrolled steps
-    int wl = len;
-#pragma unroll
-    for (int o = kWave / 2; o > 0; o >>= 1) wl = max(wl, __shfl_xor(wl, o, kWave));
-    const int wmax = __builtin_amdgcn_readfirstlane(wl);
+    const int wmax = wave_max_small<5>(len);  // (a block <= 2 kW - 1 elements)
     if (wmax > 0) {
-      leaf_run(p, W, a0, len, wmax, G, e0, 0);
+      leaf_run<true>(p, W, a0, len, wmax, G, e0, 0);
     } else {
       run_init(p, 0.0f);
     }
@@ -738,13 +930,10 @@ __device__ __forceinline__ void sq_build_body(const SqView& v, const int k, cons
                                                kLeafR)
                               : 0.0f;
       const int xe0 = grid_exp(xG);
-      int wl = xl;
-#pragma unroll
-      for (int o = kWave / 2; o > 0; o >>= 1) wl = max(wl, __shfl_xor(wl, o, kWave));
-      const int wmax = __builtin_amdgcn_readfirstlane(wl);
+      const int wmax = wave_max_small<5>(xl);
       if (wmax > 0) {
         Run q;
-        leaf_run(q, W, xa, xl, wmax, xG, xe0, r);
+        leaf_run<false>(q, W, xa, xl, wmax, xG, xe0, r);
         if (j < nl) {
           W.lf[bl].e[r] = leaf_ent(q, xe0);
           W.xneed[bl][r - 1] = q.need == kNoNeed ? kNeedNone : (int16_t)max(-32767, min(32767, q.need));
@@ -799,9 +988,14 @@ __device__ __forceinline__ void sq_build_body(const SqView& v, const int k, cons
     } else {
       const MapHdr h0 = W.lf[c0].h;
       int lat = h0.e0 + h0.m;
-      for (int j = c0 + 1; j < c1; ++j) {
-        const int4 hj = *reinterpret_cast<const int4*>(&W.lf[j].h);  // (one read, no branch)
-        lat = (hj.w & kOpaque) ? lat : max(lat, hj.y + hj.z);
+      // (unrolled and predicated: every header read in flight at once --
+      // a rolled loop waited on each)
+#pragma unroll
+      for (int j = 1; j < 2 * kGW - 1; ++j) {
+        if (c0 + j < c1) {
+          const int4 hj = *reinterpret_cast<const int4*>(&W.lf[c0 + j].h);  // (one read, no branch)
+          lat = (hj.w & kOpaque) ? lat : max(lat, hj.y + hj.z);
+        }
       }
       int m = max(0, lat - h0.e0);
       const bool exact_only = m > kGroupM;  // (the windows clamped to 0 below)
@@ -819,6 +1013,33 @@ __device__ __forceinline__ void sq_build_body(const SqView& v, const int k, cons
     }
   }
   __syncthreads();
+#if RST_SQ_GROUP_CHAIN
+  {
+    // the listed (group, candidate) composites, one at a time per wavefront
+    // (comp_chain: the wavefront steps one candidate through the group's
+    // leaf maps), wavefront w taking list entries w, w + 8, ...
+    const int nl = min(W.nlist, kBuildT);
+    const int wv = tid / kWave;
+    for (int j = wv; j < nl; j += kBuildT / kWave) {
+      const int code = j < ngr ? j << 4 : W.list[j];
+      const int gi = min(code >> 4, ngr - 1), r = code & (kGroupR - 1);
+      const int c0 = W.sgs[gi], c1 = W.sgs[gi + 1];
+      const bool gok = c0 >= 0 && c1 > c0 && c1 <= nblk && c1 - c0 <= 2 * kGW - 1;
+      const MapHdr gh = W.gm[gi].h;
+      const bool exact_only = W.gm[gi].pad[0] != 0;  // (a lattice beyond kGroupM)
+      if (!gok || (gh.flags & kOpaque)) continue;
+      float x = cand(gh.G, gh.e0, r);
+      double clo = -INFINITY, chi = INFINITY;
+      if (comp_chain<Leaf>(x, clo, chi, W.lf + c0, c1 - c0, kLeafM) && lane == 0) {
+        if (exact_only) {
+          clo = fmax(clo, 0.0);
+          chi = fmin(chi, 0.0);
+        }
+        W.gm[gi].e[r] = MapEnt{x, lo_units(clo, gh.e0), hi_units(chi, gh.e0)};
+      }
+    }
+  }
+#else
   {
     const int nl = min(W.nlist, kBuildT);  // <= 31 x 16 <= kBuildT
     const int j = tid;
@@ -840,10 +1061,7 @@ __device__ __forceinline__ void sq_build_body(const SqView& v, const int k, cons
       const int4* lq = reinterpret_cast<const int4*>(W.lf);
       const int cc0 = gok ? c0 : 0, cc1 = gok ? c1 : 1;
       int4 q0 = lq[4 * cc0], q1 = lq[4 * cc0 + 1], q2 = lq[4 * cc0 + 2], q3 = lq[4 * cc0 + 3];
-      int nst = cc1 - cc0;
-#pragma unroll
-      for (int o = kWave / 2; o > 0; o >>= 1) nst = max(nst, __shfl_xor(nst, o, kWave));
-      nst = __builtin_amdgcn_readfirstlane(nst);
+      const int nst = wave_max_small<5>(cc1 - cc0);  // (a group <= 2 kGW - 1 blocks)
       for (int s = 0; s < nst; ++s) {
         const int jl = cc0 + s;
         const int jn = 4 * min(jl + 1, cc1 - 1);
@@ -875,6 +1093,7 @@ __device__ __forceinline__ void sq_build_body(const SqView& v, const int k, cons
       }
     }
   }
+#endif
   __syncthreads();
   if (tid == 0) clk[3] = (long long)__builtin_amdgcn_s_memtime();
   GroupMap* grpg = v.grp + (int64_t)c * v.ng;
@@ -896,8 +1115,9 @@ __device__ __forceinline__ void sq_build_body(const SqView& v, const int k, cons
   } else if (tid < kWave) {
     const int r = tid;
     const MapHdr h0 = W.gm[0].h;
-    int lat = h0.e0 + h0.m;
-    for (int j = 1; j < ngr; ++j) lat = max(lat, W.gm[j].h.e0 + W.gm[j].h.m);
+    // the lattice: the groups' e0 + m, lane per group, max over the wavefront
+    // (e0 + m in [-149, 105 + kGroupM]: 9 bits above -160)
+    const int lat = wave_max_small<9>(tid < ngr ? W.gm[tid].h.e0 + W.gm[tid].h.m : h0.e0 + h0.m, -160);
     int m = max(0, lat - h0.e0);
     const bool exact_only = m > kSbM;
     if (exact_only) m = 0;
@@ -906,7 +1126,21 @@ __device__ __forceinline__ void sq_build_body(const SqView& v, const int k, cons
     const int se0 = grid_exp(Gs);
     if (r == 0) so->h = MapHdr{Gs, se0, m, 0};
     MapEnt en{0.0f, 1, 0};
-    if (r < R) {
+    if (R <= kSbChainR) {
+      // few candidates (R = 1 for ~87% of superblocks): one after another,
+      // each by the whole wavefront (comp_chain)
+      for (int rc = 0; rc < R; ++rc) {
+        float x = cand(Gs, se0, rc);
+        double clo = -INFINITY, chi = INFINITY;
+        if (comp_chain<GroupMap>(x, clo, chi, W.gm, ngr, kGroupM)) {
+          if (exact_only) {
+            clo = fmax(clo, 0.0);
+            chi = fmin(chi, 0.0);
+          }
+          if (r == rc) en = MapEnt{x, lo_units(clo, se0), hi_units(chi, se0)};
+        }
+      }
+    } else if (r < R) {
       float x = cand(Gs, se0, r);
       double clo = -INFINITY, chi = INFINITY;
       bool ok = true;
@@ -946,12 +1180,17 @@ struct WalkStats {
   int sb, sbh, g, gh, l, lh, ser;
 };
 
+// A descent loads its superblock's group maps and block starts in one trip;
+// a group its maps miss loads that group's leaf maps and elements in a
+// second (r06: the whole superblock at once, ~72 KB through one wavefront,
+// took 8.5k clocks before the first group was tried).
+constexpr int kGrpElems = (2 * kGW - 1) * (2 * kW - 1);  // a group's elements, bound
 struct WalkLds {
-  GroupMap g[kMaxSbGroups];     // a descent's superblock, loaded in one trip:
-  Leaf l[kMaxSbBlocks];         // its group maps, leaf maps,
-  float x[kMaxSbElems + 8];     // elements (from a 16-byte boundary),
-  int gs[kWave];                // group and block starts
-  int bs[kMaxSbBlocks + 1 + 63];
+  GroupMap g[kMaxSbGroups];      // the descent's superblock: its group maps,
+  int gs[kWave];                 // group starts,
+  int bs[kMaxSbBlocks + 1 + 63]; // block starts;
+  Leaf l[2 * kGW - 1];           // the missed group's leaf maps
+  float x[kGrpElems + 8];        // and elements (from a 16-byte boundary)
   WalkStats ws;   // the descent's counters (LDS: no stack slot in the walk)
   long long tclk[8];  // (statistics) the first descent's phase clocks
   int64_t pos_nf;  // element index where s became non-finite, else -1
@@ -987,37 +1226,20 @@ struct DescArgs {
   int nb, ng;
 };
 
-// Steps over maps[0, nq) (nq < kWave, in LDS) from s, speculatively: the
-// offset units from the bits of s and G, the residue, the end E_r + du 2^e0
-// (the entry from LDS at a uniform address), unchecked; then the checks
-// lane-parallel, step q on lane q (s before step q is lane q of `hist`).
-// Returns the number of leading verified steps, s after them.
+// Steps over maps[0, nq) (in LDS; at most kWalkC per call) from s,
+// speculatively -- every step's input at once, the steps composed as a
+// parallel prefix (spec_hist) -- then the checks lane-parallel, step q on
+// lane q (s before step q is lane q of `hist`).  Returns the number of
+// leading verified steps, s after them.
 template <class Map>
-__device__ __forceinline__ int spec_walk(float& s, const Map* maps, int nq, int mmax) {
+__device__ __forceinline__ int spec_chunk(float& s, const Map* maps, int nq, int mmax) {
   const int lane = threadIdx.x;
-  nq = __builtin_amdgcn_readfirstlane(nq);  // (uniform: a scalar loop)
-  if (nq <= 0) return 0;
   const int ql = min(lane, nq - 1);
   const MapHdr hl = maps[ql].h;
   const int gbl = (int)__float_as_uint(hl.G);
   const int sgl = gbl >> 31;
   const int mkl = (1 << min(hl.m & 7, mmax)) - 1;  // (clamped: r stays inside the entries)
-  int hist = 0;
-  for (int q = 0; q < nq; ++q) {
-    const int sbits = __builtin_amdgcn_readfirstlane((int)__float_as_uint(s));
-    hist = lane == q ? sbits : hist;
-    const int gb = __builtin_amdgcn_readlane(gbl, q);
-    const int sg = __builtin_amdgcn_readlane(sgl, q);
-    const int mk = __builtin_amdgcn_readlane(mkl, q);
-    const int e0 = __builtin_amdgcn_readlane(hl.e0, q);
-    const int kk = ((sbits - gb) ^ sg) - sg;
-    const int r = kk & mk;
-    s = maps[q].e[r].E - ldexpf((float)(r - kk), e0);
-  }
-  {
-    const int sfin = __builtin_amdgcn_readfirstlane((int)__float_as_uint(s));
-    hist = lane == nq ? sfin : hist;
-  }
+  const int hist = spec_hist(__builtin_amdgcn_readfirstlane((int)__float_as_uint(s)), maps, ql, hl, gbl, sgl, mkl, nq);
   const int nxb = __shfl(hist, lane + 1, kWave);
   int okl;
   {
@@ -1037,6 +1259,21 @@ __device__ __forceinline__ int spec_walk(float& s, const Map* maps, int nq, int 
   const int qf = bad ? (int)__builtin_ctzll(bad) : nq;
   s = __int_as_float(__builtin_amdgcn_readlane(hist, qf));
   return qf;
+}
+template <class Map>
+__device__ __forceinline__ int spec_walk(float& s, const Map* maps, int nq, int mmax) {
+  nq = __builtin_amdgcn_readfirstlane(min(nq, kWalkC));  // (uniform: a scalar loop)
+  int done = 0;
+  while (done < nq) {
+    done += spec_chunk(s, maps + done, nq - done, mmax);
+    if (done >= nq) break;
+    // the step the speculation could not verify -- often only a residue the
+    // prefix took from a wrong input, or s in another binade than G -- by the
+    // map itself; a true miss ends the run
+    if (!walk_try(s, maps[done].h, maps[done].e, mmax)) break;
+    ++done;
+  }
+  return done;
 }
 
 // n pieces of kSz bytes from src (global) to dst (LDS) by LDS-DMA: no
@@ -1058,8 +1295,25 @@ RST_GLDS_COPY(glds_copy16, 16)
 RST_GLDS_COPY(glds_copy4, 4)
 #undef RST_GLDS_COPY
 
-__device__ __noinline__ float walk_descend(const DescArgs v, const int ga, const int gb, const int ba,
-                                           const int bb, const int ea, const int eb, float s, WalkLds& W) {
+// a value every lane holds alike, made scalar: a non-inlined function's
+// arguments arrive in vector registers, and the compiler then treats every
+// branch and loop on them as divergent (r06: exec-mask loops throughout
+// the descent)
+__device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ int64_t uni64(int64_t x) {
+  const uint64_t u = (uint64_t)x;
+  return (int64_t)(((uint64_t)(uint32_t)uni((int)(u >> 32)) << 32) | (uint32_t)uni((int)(uint32_t)u));
+}
+template <class T>
+__device__ __forceinline__ T* uni_ptr(T* p) {
+  return reinterpret_cast<T*>(uni64(reinterpret_cast<int64_t>(p)));
+}
+
+__device__ __noinline__ float walk_descend(const DescArgs va, const int ga_, const int gb_, const int ba_,
+                                           const int bb_, const int ea_, const int eb_, float s, WalkLds& W) {
+  const DescArgs v{uni_ptr(va.grp), uni_ptr(va.leaf), uni_ptr(va.bsg), uni_ptr(va.gsg), uni_ptr(va.X),
+                   uni_ptr(va.err), uni64(va.n), uni(va.nb), uni(va.ng)};
+  const int ga = uni(ga_), gb = uni(gb_), ba = uni(ba_), bb = uni(bb_), ea = uni(ea_), eb = uni(eb_);
   int64_t& pos_nf = W.pos_nf;
   WalkStats& ws = W.ws;
   const int lane = threadIdx.x;
@@ -1072,56 +1326,80 @@ __device__ __noinline__ float walk_descend(const DescArgs v, const int ga, const
     pos_nf = v.n;
     return __int_as_float(0x7fc00000);
   }
-  // the superblock's maps, starts and elements, one trip
-  const int e4 = ea & ~3, xo = ea - e4;
+  // the superblock's group maps and starts, one trip
   glds_copy16(W.g, v.grp + ga, ngr * (int)(sizeof(GroupMap) / 16));
-  glds_copy16(W.l, v.leaf + ba, nblk * (int)(sizeof(Leaf) / 16));
-  glds_copy16(W.x, v.X + e4, (eb - e4 + 3) >> 2);
   glds_copy4(W.gs, v.gsg + ga, ngr + 1);
   glds_copy4(W.bs, v.bsg + ba, nblk + 1);
   __builtin_amdgcn_s_waitcnt(0);
   if (stamp) W.tclk[1] = (long long)__builtin_amdgcn_s_memtime();
   int q0 = 0;
   while (q0 < ngr) {
-    const int qf = spec_walk(s, W.g + q0, ngr - q0, kGroupM);
+    const int qf = spec_walk<GroupMap>(s, W.g + q0, ngr - q0, kGroupM);
     ws.g += qf;
     ws.gh += qf;
     const int q = q0 + qf;
     if (stamp && q0 == 0) W.tclk[2] = (long long)__builtin_amdgcn_s_memtime();
     if (q >= ngr) break;
-    // group q by its leaves (block indices relative to ba)
+    if (qf == min(kWalkC, ngr - q0)) {  // a full chunk verified: the next one
+      q0 = q;
+      continue;
+    }
+    // group q by its leaves (block indices relative to ba): its leaf maps
+    // and elements, one trip
     ++ws.g;
-    const int b0 = W.gs[q] - ba, b1 = W.gs[q + 1] - ba;
+    const int b0 = uni(W.gs[q]) - ba, b1 = uni(W.gs[q + 1]) - ba;
     if (b1 - b0 < 1 || b1 - b0 > 2 * kGW - 1 || b0 < 0 || b1 > nblk) {
       if (lane == 0) atomicOr(v.err, 8);
       pos_nf = v.n;
       return __int_as_float(0x7fc00000);
     }
     const int nbl = b1 - b0;
+    const int ga0 = uni(W.bs[b0]), gb0 = uni(W.bs[b1]);  // the group's elements [ga0, gb0)
+    if (gb0 - ga0 < 1 || gb0 - ga0 > kGrpElems || ga0 < ea || gb0 > eb) {
+      if (lane == 0) atomicOr(v.err, 16);
+      pos_nf = v.n;
+      return __int_as_float(0x7fc00000);
+    }
+    const int e4 = ga0 & ~3, xo = ga0 - e4;
+    glds_copy16(W.l, v.leaf + ba + b0, nbl * (int)(sizeof(Leaf) / 16));
+    glds_copy16(W.x, v.X + e4, (gb0 - e4 + 3) >> 2);
+    __builtin_amdgcn_s_waitcnt(0);
+    if (stamp && q0 == 0) W.tclk[3] = (long long)__builtin_amdgcn_s_memtime();
     int l0 = 0;
     while (l0 < nbl) {
-      const int lf = spec_walk(s, W.l + b0 + l0, nbl - l0, kLeafM);
+      const int lf = spec_walk<Leaf>(s, W.l + l0, nbl - l0, kLeafM);
       ws.l += lf;
       ws.lh += lf;
-      const int bl = b0 + l0 + lf;
+      const int bl = l0 + lf;  // (relative to b0)
       if (stamp && q0 == 0 && l0 == 0) W.tclk[4] = (long long)__builtin_amdgcn_s_memtime();
-      if (bl >= b1) break;
-      // the block by the reference's own adds (element indices relative to ea)
+      if (bl >= nbl) break;
+      if (lf == min(kWalkC, nbl - l0)) {
+        l0 = bl;
+        continue;
+      }
+      // the block by the reference's own adds: its elements from a register
+      // (lane i = element i), one dependent v_add_f32 each
       ++ws.l;
       ++ws.ser;
-      const int e0 = W.bs[bl] - ea, e1 = W.bs[bl + 1] - ea;
-      if (e1 - e0 < 1 || e1 - e0 > 2 * kW - 1 || e0 < 0 || e1 > nel) {
+      const int e0 = uni(W.bs[b0 + bl]) - ga0, e1 = uni(W.bs[b0 + bl + 1]) - ga0;
+      if (e1 - e0 < 1 || e1 - e0 > 2 * kW - 1 || e0 < 0 || e1 > gb0 - ga0) {
         if (lane == 0) atomicOr(v.err, 16);
         pos_nf = v.n;
         return __int_as_float(0x7fc00000);
       }
-      for (int i = e0; i < e1; ++i) s = s + W.x[xo + i];
+      const int cnt = __builtin_amdgcn_readfirstlane(e1 - e0);
+      const float xv = W.x[xo + e0 + min(lane, cnt - 1)];
+#pragma unroll
+      for (int i = 0; i < 2 * kW - 1; ++i) {
+        if (i >= cnt) break;
+        s = s + __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xv), i));
+      }
       if (stamp && q0 == 0 && l0 == 0) W.tclk[5] = (long long)__builtin_amdgcn_s_memtime();
       if (!isfinite(s)) {
-        pos_nf = (int64_t)ea + e1;
+        pos_nf = (int64_t)ga0 + e1;
         return s;
       }
-      l0 = bl + 1 - b0;
+      l0 = bl + 1;
     }
     q0 = q + 1;
   }
@@ -1177,6 +1455,7 @@ __device__ __forceinline__ void sq_walk_body(const SqView& v, float* __restrict_
   const float* X = v.soa + (int64_t)c * v.ns;
   int* st = v.stats ? v.stats + c * 8 : nullptr;
   const uint64_t t0 = st ? __builtin_amdgcn_s_memtime() : 0;
+  const uint64_t rt0 = st ? __builtin_amdgcn_s_memrealtime() : 0;  // (100 MHz: calibrates the clocks)
   if (lane == 0) {
     W.ws = WalkStats{0, 0, 0, 0, 0, 0, 0};
     for (int j = 0; j < 8; ++j) W.tclk[j] = 0;
@@ -1209,30 +1488,21 @@ __device__ __forceinline__ void sq_walk_body(const SqView& v, float* __restrict_
     const int gbl = (int)__float_as_uint(cur.G);
     const int sgl = gbl >> 31;  // 0, or -1 for a negative G
     const int mkl = ((1 << (cur.m & 7)) - 1) & (kWave - 1);
-    // The chunk's steps, speculatively and unchecked: offset units from the
-    // bits of s and G (s - G in G's grid when both share sign and binade),
-    // the residue r, the end E_r + du 2^e0 by v_readlane from registers.
-    // Eight dependent instructions a step; s before step q is kept in
-    // lane q of `hist`.
-    int hist = 0;
-#pragma unroll
-    for (int q = 0; q < kWalkC; ++q) {
-      const int sbits = __builtin_amdgcn_readfirstlane((int)__float_as_uint(s));
-      asm("v_writelane_b32 %0, %1, %2" : "+v"(hist) : "s"(sbits), "n"(q));
-      const int gb = __builtin_amdgcn_readlane(gbl, q);
-      const int sg = __builtin_amdgcn_readlane(sgl, q);
-      const int mk = __builtin_amdgcn_readlane(mkl, q);
-      const int e0 = __builtin_amdgcn_readlane(cur.e0, q);
-      const int kk = ((sbits - gb) ^ sg) - sg;
-      const int r = kk & mk;
-      const float E = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cur.E[q]), r));
-      // (E - (+0) keeps a -0 end; E + +0 would not)
-      s = E - ldexpf((float)(r - kk), e0);
+    // The chunk's steps, speculatively and unchecked: lane q's input from
+    // the steps before it composed as a parallel prefix (affine_hist: the
+    // offset units from the bits of s and G, s - G in G's grid when both
+    // share sign and binade; the residue's end E_r + du 2^e0 in E_r's bits);
+    // s before step q is lane q of `hist`, lane qn the chunk's end.
+    const int ql = min(lane, kWalkC - 1);
+    const int sb0 = __builtin_amdgcn_readfirstlane((int)__float_as_uint(s));
+    float El = CE[ql][0].E;
+    int hist = affine_hist(sb0, (int)__float_as_uint(El), step_shift(El, cur.e0), gbl, 0, qn);
+    if (__ballot(lane < qn && mkl != 0) != 0) {  // (a map with several residues: again with each lane's)
+      const int rl = (((hist - gbl) ^ sgl) - sgl) & mkl;
+      El = CE[ql][rl].E;
+      hist = affine_hist(sb0, (int)__float_as_uint(El), step_shift(El, cur.e0), gbl, rl, qn);
     }
-    {
-      const int sfin = __builtin_amdgcn_readfirstlane((int)__float_as_uint(s));
-      asm("v_writelane_b32 %0, %1, %2" : "+v"(hist) : "s"(sfin), "n"(kWalkC));
-    }
+    s = __int_as_float(__builtin_amdgcn_readlane(hist, qn));
     // The checks, step q on lane q: s and G share sign and binade (else the
     // offset above is meaningless; G's grid is 2^e0, zero and subnormal G
     // included, so the bits differ by the offset in units), the map is usable, the
@@ -1316,6 +1586,7 @@ __device__ __forceinline__ void sq_walk_body(const SqView& v, float* __restrict_
       st[5] = W.ws.lh;
       st[6] = W.ws.ser;
       st[7] = (int)min<uint64_t>(INT_MAX, __builtin_amdgcn_s_memtime() - t0);
+      if (c < 4) v.stats[c < 3 ? 37 + c : 56] = (int)min<uint64_t>(INT_MAX, __builtin_amdgcn_s_memrealtime() - rt0);
       if (c < 4) v.stats[33 + c] = (int)min<uint64_t>(INT_MAX, wait_clk);
       if (c == 0)
         for (int j = 1; j < 7; ++j) v.stats[56 + j] = W.tclk[j] ? (int)(W.tclk[j] - W.tclk[0]) : -1;

@@ -403,9 +403,20 @@ float walk(Chain& C) {
   int64_t pos_nf = -1;
   for (int k = 0; k < C.nk && pos_nf < 0; ++k) {
     ++C.stats[0];
+    const float s_in = s;
     if (walk_try(s, C.sbm.at(k).h, C.sbm.at(k).e, kSbR)) {
       ++C.stats[1];
       continue;
+    }
+    if (getenv("EMU_MISS")) {  // (statistics) why superblock k's map missed
+      const MapHdr& h = C.sbm.at(k).h;
+      const double du = ((double)s_in - (double)h.G) / std::ldexp(1.0, h.e0);
+      int kk = 0;
+      const bool off = offset_units(s_in, h, kk);
+      const int r = off ? (kk & ((1 << h.m) - 1)) : -1;
+      std::fprintf(stderr, "miss k=%d s=%.9g G=%.9g e0=%d m=%d fl=%d units=%.1f off=%d r=%d win=[%d,%d] du=%d\n", k,
+                   (double)s_in, (double)h.G, h.e0, h.m, h.flags, du, (int)off, r,
+                   r >= 0 ? C.sbm.at(k).e[r].LOu : 0, r >= 0 ? C.sbm.at(k).e[r].HIu : 0, off ? kk - r : 0);
     }
     const int ga = C.ks.at(k), gb = C.ks.at(k + 1);
     for (int q = ga; q < gb && pos_nf < 0; ++q) {
