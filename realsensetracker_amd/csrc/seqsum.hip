@@ -515,10 +515,11 @@ __device__ __forceinline__ void sq_front_body(const SqView& v, const float4* __r
 // kernel's choices.  Leaf and group maps go to global memory for the walk's
 // descents.
 constexpr int kBuildT = 512;
+// three workgroups per CU: 24 waves, 6 per SIMD (<= 80 registers)
+constexpr int kBuildWaves = 3 * kBuildT / kWave / 4;
 static_assert(kBuildT >= kMaxSbBlocks + 1 && kBuildT >= kMaxSbGroups * kGroupR && kBuildT % kWave == 0,
               "map workgroup size");
 static_assert(sizeof(Leaf) == 64, "a leaf map is four int4");
-constexpr int kXPad = kMaxSbElems + kMaxSbElems / kW + 2 * kW;  // padded staging (see xp)
 constexpr int kListCap = (kLeafR - 1) * kMaxSbBlocks;
 constexpr int16_t kNeedNone = INT16_MIN;  // kNoNeed in 16 bits
 static_assert((kMaxSbBlocks << 2 | 3) <= 0xffff && (kMaxSbGroups << 4 | 15) <= 0xffff, "list codes in 16 bits");
@@ -737,11 +738,6 @@ __device__ __forceinline__ bool comp_chain(float& x, double& clo, double& chi, c
   return true;
 }
 
-// staged element a of the superblock at a + a / 16: lane j's block starts
-// near 16 j, so the lanes of a step read 17 words apart -- distinct banks
-// (r05: unpadded, stride 16, 3.3 conflicts per LDS instruction)
-__device__ __forceinline__ int xp(int a) { return a + (a >> 4); }
-
 // the wavefront's largest v, v in [lo, lo + 2^B): B ballots, most significant
 // bit first -- no cross-lane data move (a shuffle butterfly is six LDS-unit
 // round trips, ~600 clocks)
@@ -757,14 +753,11 @@ __device__ __forceinline__ int wave_max_small(int v, int lo = 0) {
   return hi + lo;
 }
 
-// (<= 80 KB: two workgroups per CU -- one's composites, a wavefront or two,
-// beside the other's leaves; the group maps reuse the elements' space, done
-// with once the leaves are)
+// (<= 53 KB: three workgroups per CU -- the composites, a wavefront or two
+// each, beside other workgroups' leaves.  The leaves read their elements
+// from global memory themselves: r06, staged in LDS, 76 KB and two per CU)
 struct BuildLds {
-  union {
-    float x[kXPad];
-    GroupMap gm[kMaxSbGroups];
-  };
+  GroupMap gm[kMaxSbGroups];
   Leaf lf[kMaxSbBlocks];
   int sbs[kMaxSbBlocks + 1];   // block starts, relative to the superblock's first element
   int sgs[kMaxSbGroups + 1];   // group starts, relative to its first block
@@ -779,28 +772,39 @@ struct BuildLds {
                                // tile and before the next
 };
 
-// one monitored run of block bl from candidate r (the elements from LDS into
-// registers first: the run's chain waits on no LDS read), at most `wmax`
-// steps (the wavefront's longest block, uniform)
-template <bool UNROLL>
-__device__ __forceinline__ void leaf_run(Run& p, const BuildLds& W, int a0, int len, int wmax, float G, int e0,
-                                         int r) {
+// one monitored run of a block from candidate r: its len <= 2 kW - 1
+// elements X[a], X[a + 1], ... (the chain's SoA row, rows padded to 64
+// floats) into registers first -- nine 16-byte loads from a's 16-byte
+// boundary, clamped inside the row -- so the run's chain waits on no load;
+// register j is step j - a mod 4 (steps predicated per lane: a select by the
+// lane's offset became an indexed scratch access); at most `wmax` + 3 steps
+// (the wavefront's longest block, uniform)
+__device__ __forceinline__ void leaf_run(Run& p, const float* __restrict__ X, int64_t ns, int64_t a, int len,
+                                         int wmax, float G, int e0, int r) {
+  constexpr int kL4 = (2 * kW - 1 + 3 + 3) / 4;  // float4 loads covering a mod 4 + len
   run_init(p, cand(G, e0, r));
-  if constexpr (UNROLL) {
-    float xr[2 * kW - 1];
+  const int64_t a4 = a >> 2, last4 = (ns >> 2) - 1;
+#if defined(__HIP_DEVICE_COMPILE__)
+  const auto* X4 = (const __attribute__((address_space(1))) float4*)X;  // (global loads, not flat)
+#else
+  const float4* X4 = reinterpret_cast<const float4*>(X);
+#endif
+  float w[4 * kL4];
 #pragma unroll
-    for (int i = 0; i < 2 * kW - 1; ++i) xr[i] = W.x[xp(min(a0 + i, kMaxSbElems - 1))];
-    // (predicated, not a break: the loop unrolls, xr[i] stays a register --
-    // a rolled loop indexed xr through s_set_gpr_idx)
+  for (int j = 0; j < kL4; ++j) {
+    const float4 t = X4[min(a4 + j, last4)];
+    w[4 * j] = t.x;
+    w[4 * j + 1] = t.y;
+    w[4 * j + 2] = t.z;
+    w[4 * j + 3] = t.w;
+  }
+  const int off = (int)(a & 3);
+  // (unrolled and predicated, not a break: w[j] stays a register)
 #pragma unroll
-    for (int i = 0; i < 2 * kW - 1; ++i) {
-      if (i < wmax) {
-        if (i < len) run_step(p, xr[i], e0);
-      }
+  for (int j = 0; j < 2 * kW - 1 + 3; ++j) {
+    if (j < wmax + 3) {
+      if (j >= off && j < off + len) run_step(p, w[j], e0);
     }
-  } else {  // (the rare extra candidates: compact code)
-    for (int i = 0; i < wmax; ++i)
-      if (i < len) run_step(p, W.x[xp(min(a0 + i, kMaxSbElems - 1))], e0);
   }
 }
 
@@ -844,16 +848,6 @@ __device__ __forceinline__ void sq_build_body(const SqView& v, const int k, cons
   }
   const int ngr = gb - ga, nblk = bb - ba, nel = eb - ea;
   const float* X = v.soa + (int64_t)c * v.ns;
-  // (in flight together: the elements, the block's bounds and prefix)
-  {
-    constexpr int kJ = (kMaxSbElems + kBuildT - 1) / kBuildT;
-    float tv[kJ];
-#pragma unroll
-    for (int j = 0; j < kJ; ++j) tv[j] = tid + j * kBuildT < nel ? X[ea + tid + j * kBuildT] : 0.0f;
-#pragma unroll
-    for (int j = 0; j < kJ; ++j)
-      if (tid + j * kBuildT < nel) W.x[xp(tid + j * kBuildT)] = tv[j];
-  }
   const bool act = tid < nblk;
   const int b = ba + tid;
   const double iv = act ? v.ipre[(int64_t)c * v.nb + b] : 0.0;
@@ -898,7 +892,7 @@ __device__ __forceinline__ void sq_build_body(const SqView& v, const int k, cons
     // the wavefront's longest block bounds the unrolled steps
     const int wmax = wave_max_small<5>(len);  // (a block <= 2 kW - 1 elements)
     if (wmax > 0) {
-      leaf_run<true>(p, W, a0, len, wmax, G, e0, 0);
+      leaf_run(p, X, v.ns, (int64_t)ea + a0, len, wmax, G, e0, 0);
     } else {
       run_init(p, 0.0f);
     }
@@ -933,7 +927,7 @@ __device__ __forceinline__ void sq_build_body(const SqView& v, const int k, cons
       const int wmax = wave_max_small<5>(xl);
       if (wmax > 0) {
         Run q;
-        leaf_run<false>(q, W, xa, xl, wmax, xG, xe0, r);
+        leaf_run(q, X, v.ns, (int64_t)ea + xa, xl, wmax, xG, xe0, r);
         if (j < nl) {
           W.lf[bl].e[r] = leaf_ent(q, xe0);
           W.xneed[bl][r - 1] = q.need == kNoNeed ? kNeedNone : (int16_t)max(-32767, min(32767, q.need));
@@ -1193,6 +1187,9 @@ struct WalkLds {
   float x[kGrpElems + 8];        // and elements (from a 16-byte boundary)
   WalkStats ws;   // the descent's counters (LDS: no stack slot in the walk)
   long long tclk[8];  // (statistics) the first descent's phase clocks
+  long long tph[6];   // (statistics) every descent's clocks by phase: group load, group steps,
+                      // leaf load, leaf steps, own adds, whole descents
+  int tph_on;
   int64_t pos_nf;  // element index where s became non-finite, else -1
 };
 
@@ -1319,6 +1316,15 @@ __device__ __noinline__ float walk_descend(const DescArgs va, const int ga_, con
   const int lane = threadIdx.x;
   const bool stamp = ws.g == 0 && lane == 0;  // (the first descent's phases)
   if (stamp) W.tclk[0] = (long long)__builtin_amdgcn_s_memtime();
+  const bool ph = uni(W.tph_on) != 0;
+  long long tp0 = ph ? (long long)__builtin_amdgcn_s_memtime() : 0, tpl = tp0;
+  auto phase = [&](int j) {  // (statistics: the clocks since the last mark to phase j)
+    if (ph) {
+      const long long t = (long long)__builtin_amdgcn_s_memtime();
+      if (lane == 0) W.tph[j] += t - tpl;
+      tpl = t;
+    }
+  };
   const int ngr = gb - ga, nblk = bb - ba, nel = eb - ea;
   if (ngr < 1 || ngr > kMaxSbGroups || ga < 0 || gb > v.ng || nblk < 1 || nblk > kMaxSbBlocks || ba < 0 ||
       bb > v.nb || nel < 1 || nel > kMaxSbElems || ea < 0 || eb > v.n) {
@@ -1332,9 +1338,11 @@ __device__ __noinline__ float walk_descend(const DescArgs va, const int ga_, con
   glds_copy4(W.bs, v.bsg + ba, nblk + 1);
   __builtin_amdgcn_s_waitcnt(0);
   if (stamp) W.tclk[1] = (long long)__builtin_amdgcn_s_memtime();
+  phase(0);
   int q0 = 0;
   while (q0 < ngr) {
     const int qf = spec_walk<GroupMap>(s, W.g + q0, ngr - q0, kGroupM);
+    phase(1);
     ws.g += qf;
     ws.gh += qf;
     const int q = q0 + qf;
@@ -1365,9 +1373,11 @@ __device__ __noinline__ float walk_descend(const DescArgs va, const int ga_, con
     glds_copy16(W.x, v.X + e4, (gb0 - e4 + 3) >> 2);
     __builtin_amdgcn_s_waitcnt(0);
     if (stamp && q0 == 0) W.tclk[3] = (long long)__builtin_amdgcn_s_memtime();
+    phase(2);
     int l0 = 0;
     while (l0 < nbl) {
       const int lf = spec_walk<Leaf>(s, W.l + l0, nbl - l0, kLeafM);
+      phase(3);
       ws.l += lf;
       ws.lh += lf;
       const int bl = l0 + lf;  // (relative to b0)
@@ -1395,6 +1405,7 @@ __device__ __noinline__ float walk_descend(const DescArgs va, const int ga_, con
         s = s + __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xv), i));
       }
       if (stamp && q0 == 0 && l0 == 0) W.tclk[5] = (long long)__builtin_amdgcn_s_memtime();
+      phase(4);
       if (!isfinite(s)) {
         pos_nf = (int64_t)ga0 + e1;
         return s;
@@ -1404,6 +1415,7 @@ __device__ __noinline__ float walk_descend(const DescArgs va, const int ga_, con
     q0 = q + 1;
   }
   if (stamp) W.tclk[6] = (long long)__builtin_amdgcn_s_memtime();
+  if (ph && lane == 0) W.tph[5] += (long long)__builtin_amdgcn_s_memtime() - tp0;
   return s;
 }
 
@@ -1459,6 +1471,8 @@ __device__ __forceinline__ void sq_walk_body(const SqView& v, float* __restrict_
   if (lane == 0) {
     W.ws = WalkStats{0, 0, 0, 0, 0, 0, 0};
     for (int j = 0; j < 8; ++j) W.tclk[j] = 0;
+    for (int j = 0; j < 6; ++j) W.tph[j] = 0;
+    W.tph_on = st != nullptr;
     W.pos_nf = -1;
   }
   __syncthreads();
@@ -1474,7 +1488,7 @@ __device__ __forceinline__ void sq_walk_body(const SqView& v, float* __restrict_
     if (st) {  // (statistics: the time waiting for this chunk's maps)
       const uint64_t ta = __builtin_amdgcn_s_memtime();
       const int j = k / kWalkC;
-      if (c < 4 && j < 4 && lane == 0) v.stats[40 + c * 4 + j] = (int)(ta - t0);
+      (void)j;
       __builtin_amdgcn_s_waitcnt(0);
       wait_clk += __builtin_amdgcn_s_memtime() - ta;
     }
@@ -1587,6 +1601,8 @@ __device__ __forceinline__ void sq_walk_body(const SqView& v, float* __restrict_
       st[6] = W.ws.ser;
       st[7] = (int)min<uint64_t>(INT_MAX, __builtin_amdgcn_s_memtime() - t0);
       if (c < 4) v.stats[c < 3 ? 37 + c : 56] = (int)min<uint64_t>(INT_MAX, __builtin_amdgcn_s_memrealtime() - rt0);
+      if (c < 2)
+        for (int j = 0; j < 6; ++j) v.stats[40 + 6 * c + j] = (int)min<long long>(INT_MAX, W.tph[j]);
       if (c < 4) v.stats[33 + c] = (int)min<uint64_t>(INT_MAX, wait_clk);
       if (c == 0)
         for (int j = 1; j < 7; ++j) v.stats[56 + j] = W.tclk[j] ? (int)(W.tclk[j] - W.tclk[0]) : -1;
@@ -1604,7 +1620,7 @@ __global__ __launch_bounds__(kFrontT) void k_sq_front(SqView v, const float4* __
                                                      double* __restrict__ tnext) {
   sq_front_body<FUSED>(v, x, tprev, tnext, blockIdx.x, blockIdx.y);
 }
-__global__ __launch_bounds__(kBuildT) void k_sq_build(SqView v) { sq_build_body(v, blockIdx.x, blockIdx.y); }
+__global__ __launch_bounds__(kBuildT, kBuildWaves) void k_sq_build(SqView v) { sq_build_body(v, blockIdx.x, blockIdx.y); }
 __global__ __launch_bounds__(kWave) void k_sq_walk(SqView v, float* __restrict__ out) {
   sq_walk_body(v, out, blockIdx.x);
 }
@@ -1637,7 +1653,7 @@ __global__ __launch_bounds__(kFrontT) void k_sq_front_b(const SqPair* __restrict
   if ((int)blockIdx.x >= v.nk) return;
   sq_front_body<false>(v, nullptr, nullptr, nullptr, blockIdx.x, blockIdx.y);
 }
-__global__ __launch_bounds__(kBuildT) void k_sq_build_b(const SqPair* __restrict__ P, int nch, int iter) {
+__global__ __launch_bounds__(kBuildT, kBuildWaves) void k_sq_build_b(const SqPair* __restrict__ P, int nch, int iter) {
   const SqView v = sq_at(P[blockIdx.z], nch, iter);
   if ((int)blockIdx.x >= v.nk) return;
   sq_build_body(v, blockIdx.x, blockIdx.y);

@@ -2,7 +2,9 @@
 RST_DIAG library variant (RST_LIB=.../diag.so): points certified by
 k_icp_nn, near / far queue lengths, queued entries the leaf adjacency
 answered, ball-tile chunks, deep searches, and the kernel times (timing
-pass on the same pair)."""
+pass on the same pair).
+
+    RST_LIB=.../diag.so python tools/diag_fb.py [--host] [--bench-pair K] [--ref]"""
 import ctypes as C
 import sys
 from pathlib import Path
@@ -22,7 +24,13 @@ for name in ("rst_debug_queue_trace", "rst_debug_iter_diag"):
     f.argtypes = [C.c_void_p, L.c_int32_p, C.c_int32]
 ctx = A.get_context(0)
 K = driver.intrinsics(640, 480)
-da, db, _ = driver.make_pair(driver.SyntheticScene(0), K, seed=10)
+if "--bench-pair" in sys.argv:  # the bench stream's pair k: frames k-1 (target) and k (source)
+    kp = int(sys.argv[sys.argv.index("--bench-pair") + 1])
+    sc = driver.SyntheticScene(0)
+    da = sc.render(sc.trajectory(kp - 1), K, noise_seed=kp - 1)
+    db = sc.render(sc.trajectory(kp), K, noise_seed=kp)
+else:
+    da, db, _ = driver.make_pair(driver.SyntheticScene(0), K, seed=10)
 if "--host" in sys.argv:  # clouds built from host points (no pixel grid)
     pa, pb = driver.unproject(da, K), driver.unproject(db, K)
     tgt = A.Target.build(pa, ctx)
@@ -32,7 +40,7 @@ else:  # frame targets prepared from depth on the device (the bench path)
     tgt = A.Target.from_depth_device(bufs[0].ptr, K, 0, ctx)
     src = A.Target.from_depth_device(bufs[1].ptr, K, 0, ctx)
     pa, pb = np.zeros((len(tgt), 3)), np.zeros((len(src), 3))
-opts = L.default_opts(max_iter=128, sum_mode=L.RST_SUM_FP64)
+opts = L.default_opts(max_iter=128, sum_mode=L.RST_SUM_REF if "--ref" in sys.argv else L.RST_SUM_FP64)
 for rep in range(2):
     T = np.eye(4, dtype=np.float32)
     r = A.align_prepared_async(src, tgt, ctx, T, opts).wait()  # (second run: warm pools)
