@@ -502,9 +502,11 @@ __global__ __launch_bounds__(kBS) void k_gather_orig(const float4* __restrict__ 
 // (:122); w_i = (mu / (d2_i + mu))^2 (:116-117).  Grid-stride over the
 // original order; one 9-double row (stride RefAcc::RS) per block.
 // (r03: 128 blocks measured no faster with pairs in flight and 1.6 us
-// slower alone)
+// slower alone; r06o, batched: 256 blocks 25.6k vs 25.2k ICP it/s -- a
+// batch's launch is 256 x B blocks, and the solve reduces 256 rows, not
+// 1024; every GPU test bit-identical)
 #ifndef RST_COV_BLOCKS
-#define RST_COV_BLOCKS 1024
+#define RST_COV_BLOCKS 256
 #endif
 constexpr int kCovBlocks = RST_COV_BLOCKS;
 __device__ __forceinline__ void cov_ref_body(const float4* __restrict__ srco, const float4* __restrict__ corr,
