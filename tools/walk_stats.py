@@ -50,6 +50,11 @@ for pi in range(a.first, a.first + a.pairs):
         clk = tot[:, :, 7].astype(np.float64)
         ok = rt > 0
         print(f"  walker clock rate {np.median(clk[ok] / rt[ok]) * 0.1:.2f} GHz (s_memtime / s_memrealtime)")
+        tp = st[:, 40:52].reshape(-1, 2, 6).astype(np.int64).sum(0)
+        for c in range(2):
+            print(f"  chain {c} descents, clocks over the align: group load {tp[c, 0]}, group steps {tp[c, 1]}, "
+                  f"leaf load {tp[c, 2]}, leaf steps {tp[c, 3]}, own adds {tp[c, 4]}, whole {tp[c, 5]} "
+                  f"(of walks {int(tot[:, c, 7].sum())})")
         tot_all += tot.sum(0)
         for b in bufs:
             b.free()
