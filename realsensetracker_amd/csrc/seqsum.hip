@@ -1179,6 +1179,32 @@ struct WalkStats {
 // second (r06: the whole superblock at once, ~72 KB through one wavefront,
 // took 8.5k clocks before the first group was tried).
 constexpr int kGrpElems = (2 * kGW - 1) * (2 * kW - 1);  // a group's elements, bound
+// A group its map misses: its leaf maps, or with RST_SQ_GROUP_SERIAL the
+// reference's own adds over the whole group -- measured slower (r07b, bench
+// pair 14's x chain over an align: 60.8M walker clocks vs 50.8M; the adds
+// ran ~53 clocks an element inside the walk, k_sq_serial's 12 not reached).
+#ifndef RST_SQ_GROUP_SERIAL
+#define RST_SQ_GROUP_SERIAL 0
+#endif
+
+// s <- the reference's adds over xl[0, cnt) (LDS), in order: 32 elements a
+// round read by every lane at the same addresses (broadcast) into 32
+// registers, then 32 dependent v_add_f32 -- no cross-lane move in the chain
+// (r07a: a v_readlane per element cost ~78 clocks an element).  Past cnt
+// the round adds +0, which changes no bit: s, a chain value from +0, is
+// never -0 (k_sq_serial's argument).
+__device__ __forceinline__ void serial_adds(float& s, const float* xl, int cnt) {
+  constexpr int kR = 32;
+  cnt = __builtin_amdgcn_readfirstlane(cnt);
+  for (int c0 = 0; c0 < cnt; c0 += kR) {
+    float xr[kR];
+#pragma unroll
+    for (int i = 0; i < kR; ++i) xr[i] = c0 + i < cnt ? xl[c0 + i] : 0.0f;
+#pragma unroll
+    for (int i = 0; i < kR; ++i) s = s + xr[i];
+  }
+}
+
 struct WalkLds {
   GroupMap g[kMaxSbGroups];      // the descent's superblock: its group maps,
   int gs[kWave];                 // group starts,
@@ -1369,6 +1395,22 @@ __device__ __noinline__ float walk_descend(const DescArgs va, const int ga_, con
       return __int_as_float(0x7fc00000);
     }
     const int e4 = ga0 & ~3, xo = ga0 - e4;
+#if RST_SQ_GROUP_SERIAL
+    (void)nbl;
+    glds_copy16(W.x, v.X + e4, (gb0 - e4 + 3) >> 2);
+    __builtin_amdgcn_s_waitcnt(0);
+    if (stamp && q0 == 0) W.tclk[3] = (long long)__builtin_amdgcn_s_memtime();
+    phase(2);
+    ws.ser += 1;
+    serial_adds(s, W.x + xo, gb0 - ga0);
+    phase(4);
+    if (!isfinite(s)) {
+      pos_nf = (int64_t)gb0;
+      return s;
+    }
+    q0 = q + 1;
+    continue;
+#endif
     glds_copy16(W.l, v.leaf + ba + b0, nbl * (int)(sizeof(Leaf) / 16));
     glds_copy16(W.x, v.X + e4, (gb0 - e4 + 3) >> 2);
     __builtin_amdgcn_s_waitcnt(0);
@@ -1387,8 +1429,8 @@ __device__ __noinline__ float walk_descend(const DescArgs va, const int ga_, con
         l0 = bl;
         continue;
       }
-      // the block by the reference's own adds: its elements from a register
-      // (lane i = element i), one dependent v_add_f32 each
+      // the block by the reference's own adds (serial_adds: r07b, half the
+      // clocks of a v_readlane per element)
       ++ws.l;
       ++ws.ser;
       const int e0 = uni(W.bs[b0 + bl]) - ga0, e1 = uni(W.bs[b0 + bl + 1]) - ga0;
@@ -1397,13 +1439,7 @@ __device__ __noinline__ float walk_descend(const DescArgs va, const int ga_, con
         pos_nf = v.n;
         return __int_as_float(0x7fc00000);
       }
-      const int cnt = __builtin_amdgcn_readfirstlane(e1 - e0);
-      const float xv = W.x[xo + e0 + min(lane, cnt - 1)];
-#pragma unroll
-      for (int i = 0; i < 2 * kW - 1; ++i) {
-        if (i >= cnt) break;
-        s = s + __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xv), i));
-      }
+      serial_adds(s, W.x + xo + e0, e1 - e0);
       if (stamp && q0 == 0 && l0 == 0) W.tclk[5] = (long long)__builtin_amdgcn_s_memtime();
       phase(4);
       if (!isfinite(s)) {
