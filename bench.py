@@ -34,6 +34,9 @@ rendezvous (no torch in the process: the library is its only HIP runtime).
 
 Other BASELINE configs (extra bench lines, same JSON contract):
     --width 1280 --height 720     configs[2]: the stream at 720p
+    --mode p2plane                the value leg in the build's point-to-plane mode
+                                  to convergence (configs[1-2] name point-to-plane;
+                                  the reference's own loop is P2POINT_REF, the default)
     --workload pyramid            configs[4]: 3-level coarse-to-fine ICP on a
                                   1280x720 stream, pose chained on the device
     --workload sharded            configs[3]: a 1000x1000 (~1M-point) pair, the
@@ -262,9 +265,11 @@ def run_sharded(a, K, frames, d_depth, hip, world, rank, local, rdv, barrier, ma
             "config": {"workload": f"{a.width}x{a.height} scan pair ({n.value} source points), "
                                    f"AlignIcp3d P2POINT_REF {a.iters} iters, source sharded "
                                    f"over {world} rank(s), " + (
-                                       "per iteration one RCCL all-gather of the "
-                                       "correspondences (16 B/pt), the sequential fp32 sums "
-                                       "on every rank, one all-reduce of 9 fp64" if ref else
+                                       "per iteration the sequential fp32 sums relayed rank "
+                                       "to rank (an all-gather of 32 B fp64 totals per rank, "
+                                       "16 B chain values sent on, a 16 B broadcast; each "
+                                       "rank maps and walks its own stretch), one all-reduce "
+                                       "of 9 fp64" if ref else
                                        "one RCCL all-reduce of 16 fp64 per iteration"),
                        "width": a.width, "height": a.height, "iters_per_pair": a.iters,
                        "points_per_frame": n.value, "target_points": len(tgt),
@@ -312,6 +317,11 @@ def main():
     ap.add_argument("--no-gicp", action="store_true")
     ap.add_argument("--graphs", action="store_true",
                     help="replay each align's iteration loop as a hipGraph (no kernel timing)")
+    ap.add_argument("--mode", choices=["p2point_ref", "p2plane"], default="p2point_ref",
+                    help="the value leg's ICP: the reference's loop (AlignIcp3d P2POINT_REF, "
+                         "--iters fixed iterations) or the build's point-to-plane mode to "
+                         "convergence (<= 30 iterations, image-grid normals; BASELINE configs[1-2] "
+                         "name point-to-plane)")
     ap.add_argument("--sum-mode", choices=["fp64", "ref"], default="ref",
                     help="the value leg's sums: fp64 = RST_SUM_FP64 (fp64 partial sums), "
                          "ref = RST_SUM_REF (the drop-in default: the reference's sequential "
@@ -395,6 +405,12 @@ def main():
     if a.inflight <= 0:
         a.inflight = 4 if batched or not main_ref else a.ref_inflight
     opts_pl = L.default_opts(mode=L.RST_P2PLANE, max_iter=30)
+    plane = a.mode == "p2plane"
+    nk_main = -2 if plane else 0  # the value leg's normals (image-grid PCA 5x5 for P2PLANE)
+    if plane:
+        opts_main = opts_pl
+        a.ref_steps = 0  # (the sum modes are the point-to-point loop's)
+        a.no_p2plane = True  # (the value is that leg)
     # frame preparation on its own context (stream); each frame pair in
     # flight on its own context, so the latency-bound per-iteration chains
     # of independent pairs overlap on the GPU
@@ -527,17 +543,17 @@ def main():
     # warm-up: W pairs, and at least one per context in flight, so that no
     # context sizes its device workspace inside the timed region
     if batched:
-        run_batched(max(a.warmup, len(actx) * a.batch), opts_main, 0, None, actx, a.batch)
+        run_batched(max(a.warmup, len(actx) * a.batch), opts_main, nk_main, None, actx, a.batch)
     else:
-        run(max(a.warmup, len(actx)), opts_main, 0, None)
+        run(max(a.warmup, len(actx)), opts_main, nk_main, None)
     st = new_stats()
     barrier()
     sync_all()
     t0 = time.perf_counter()
     if batched:
-        run_batched(a.steps, opts_main, 0, st, actx, a.batch)
+        run_batched(a.steps, opts_main, nk_main, st, actx, a.batch)
     else:
-        run(a.steps, opts_main, 0, st)
+        run(a.steps, opts_main, nk_main, st)
     sync_all()
     barrier()
     dt = max_over_ranks(time.perf_counter() - t0)
@@ -556,9 +572,9 @@ def main():
     sr1 = new_stats()
     actx[0].enable_kernel_timing(1)  # (a timed align runs in stream mode)
     if batched:
-        run_batched(a.steps, opts_main, 0, sr1, actx[:1], a.batch)
+        run_batched(a.steps, opts_main, nk_main, sr1, actx[:1], a.batch)
     else:
-        run(a.roof_steps, opts_main, 0, sr1, ctxs=actx[:1])
+        run(a.roof_steps, opts_main, nk_main, sr1, ctxs=actx[:1])
     actx[0].enable_kernel_timing(0)
 
     # ---- point-to-plane mode (extra fields) ---------------------------------------
@@ -711,11 +727,13 @@ def main():
     m_avg = st["m"] / max(1, a.steps)
     # a batched launch covers the batch's pairs: per-pair bytes x pairs per launch
     pairs_per_launch = sr1["batch_pairs"] / max(1, sr1["batches"]) if batched else 1.0
-    alg_bytes = p2point_alg_bytes(n_avg, m_avg) * pairs_per_launch
+    # (point-to-plane also reads the target normals: 12 m more)
+    alg_bytes = (p2point_alg_bytes(n_avg, m_avg) + (12 * m_avg if plane else 0)) * pairs_per_launch
     achieved = alg_bytes / (nn_us * 1e-6) / 1e9 if nn_us > 0 else 0.0
     # the committed PMC pass is of the default workload only
-    traffic, traffic_src = (load_traffic() if (a.workload, a.width, a.height) ==
-                            ("stream", 640, 480) else (None, "PMC pass is of the 640x480 stream"))
+    traffic, traffic_src = (load_traffic() if (a.workload, a.width, a.height, plane) ==
+                            ("stream", 640, 480, False) else
+                            (None, "the PMC pass is of the 640x480 P2POINT_REF stream"))
     if traffic is not None:
         traffic *= pairs_per_launch
 
@@ -745,14 +763,23 @@ def main():
                                 f"level {pyr_iters} (finest first), pose chained on the device"
                                 if pyr else
                                 f"{a.width}x{a.height} synthetic RGB-D stream, per frame: "
+                                f"unproject + image-grid normals (5x5 PCA) + index build + "
+                                f"point-to-plane ICP to convergence (<= 30 iterations, 6x6 "
+                                f"Gauss-Newton)"
+                                if plane else
+                                f"{a.width}x{a.height} synthetic RGB-D stream, per frame: "
                                 f"unproject + index build + AlignIcp3d P2POINT_REF "
                                 f"{a.iters} iters (reference loop)"),
                    "width": a.width, "height": a.height,
-                   "iters_per_pair": sum(pyr_iters) if pyr else a.iters,
+                   "mode": "P2PLANE" if plane else "P2POINT_REF",
+                   "iters_per_pair": (round(st["iters"] / max(1, a.steps), 2) if plane else
+                                      sum(pyr_iters) if pyr else a.iters),
                    "iteration_unit": ("level-0 equivalents: a level-l iteration counts n_l / n_0"
                                       if pyr else "full-resolution ICP iteration"),
                    "points_per_frame": round(n_avg), "frames_cycled": nfr,
-                   "accumulation": ("RST_SUM_REF: the reference's sequential fp32 sums, "
+                   "accumulation": ("fp64 6x6 normal equations (point-to-plane; absent in the "
+                                    "reference, SURVEY.md §8 a11)" if plane else
+                                    "RST_SUM_REF: the reference's sequential fp32 sums, "
                                     "bit-exact (the drop-in default; within the 1e-4 gate)"
                                     if main_ref else
                                     "RST_SUM_FP64: fp64 partial sums (not the drop-in "

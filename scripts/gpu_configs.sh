@@ -20,3 +20,5 @@ step() {  # name, limit, command...
 step bench_pyramid 300 python bench.py --workload pyramid --graphs --no-p2plane
 step bench_sharded 300 python bench.py --workload sharded --steps 5 --warmup 1
 step bench_720p 300 python bench.py --width 1280 --height 720 --no-host-api --no-gicp
+step bench_720p_p2plane 300 python bench.py --width 1280 --height 720 --mode p2plane --no-host-api --no-gicp
+step bench_p2plane 300 python bench.py --mode p2plane --no-host-api --no-gicp
