@@ -605,6 +605,26 @@ __device__ void queue_prefix(const int32_t* __restrict__ qcnt, int nb, int32_t* 
   }
 }
 
+// Both fallback queues' prefixes, once per pair and iteration, into gpref
+// (near [0, nb], far [nb + 1, 2 nb + 1]) with the queue trace -- a launch of
+// its own between k_icp_nn and k_icp_fb, so that k_icp_fb's blocks do not
+// each rebuild them (r07: 384 blocks a pair, most without an entry in the
+// steady state, each scanning 2 x 1164 counts).  (A last-block ticket in
+// k_icp_nn instead needed an agent-scope release per block -- an L2
+// write-back each: k_icp_nn_b 94 -> 950 us, r07d.)
+__device__ __forceinline__ void queue_prefix_body(const int32_t* __restrict__ qcnt, int nb,
+                                                  IcpState* __restrict__ st) {
+  if (st->done) return;  // (converged: k_icp_fb returns at once)
+  int32_t* gpref = const_cast<int32_t*>(qcnt) + 2 * nb + 64;
+  queue_prefix(qcnt, nb, gpref, st);
+  __syncthreads();
+  queue_prefix(qcnt + nb, nb, gpref + nb + 1, nullptr);
+}
+__global__ __launch_bounds__(kBS) void k_queue_prefix(const int32_t* __restrict__ qcnt, int nb,
+                                                      IcpState* __restrict__ st) {
+  queue_prefix_body(qcnt, nb, st);
+}
+
 // Projective seeds (frame targets, cold queries): the query projected
 // through the target's pixel grid, the valid points of the 3 x 3 level
 // pixels around it offered to r -- candidates near the query where Morton
@@ -1445,11 +1465,10 @@ __device__ __forceinline__ void icp_fb_body(const BvhView& bv, const AdjView& av
   __shared__ FbScratch scr[kBS / kWave];
   __shared__ int4 left[kBS / kWave][kWave / 16];  // a round's leftovers (i, seeds)
   if (Acc::kCanFinish && st->done) return;  // converged: nothing reads the slabs
-  queue_prefix(qcnt, nb1, pref, blockIdx.x == 0 ? st : nullptr);
-  __syncthreads();
-  queue_prefix(qcntf, nb1, preff, nullptr);
-  __syncthreads();
-  const int E = pref[nb1], EF = preff[nb1];
+  // the queues' prefixes as k_queue_prefix published them (near [0, nb1],
+  // far [nb1 + 1, 2 nb1 + 1])
+  const int32_t* __restrict__ gpref = qcnt + 2 * nb1 + 64;
+  const int E = gpref[nb1], EF = gpref[2 * nb1 + 1];
 #if RST_DIAG
   if (blockIdx.x == 0 && threadIdx.x == 0 && st->iter < kQTrace) st->diag[st->iter][0] = EF;
 #endif
@@ -1477,6 +1496,14 @@ __device__ __forceinline__ void icp_fb_body(const BvhView& bv, const AdjView& av
   // round of entries, else this wave's next far entry.  All uniform.
   const int fg0 = W - 1 - gw;  // this wave's far entries: fg0, fg0 + W, ...
   const int nfar = (!many && fg0 < EF) ? (EF - fg0 + W - 1) / W : 0;
+  // a block without an entry (most of the grid in the steady state) loads no
+  // prefix; without sums to fold (RST_SUM_REF) it is done
+  if (__syncthreads_or(e0 < e1 || nfar > 0)) {
+    for (int j = threadIdx.x; j < 2 * (nb1 + 1); j += kBS) pref[j] = gpref[j];
+    __syncthreads();
+  } else if constexpr (!Acc::kSums) {
+    return;
+  }
   int r0 = e0, nleft = 0, fdone = 0;
   while (true) {
     bool deep = false, try1 = false;
@@ -1687,6 +1714,11 @@ __global__ __launch_bounds__(kBS, Acc::kFbMinWaves) void k_icp_fb(BvhView bv, Ad
 }
 
 // the batch forms (PairArgs, pair = blockIdx.z)
+__global__ __launch_bounds__(kBS) void k_queue_prefix_b(const PairArgs* __restrict__ pa) {
+  const PairArgs& A = pa[blockIdx.z];
+  queue_prefix_body(A.qcnt, A.nb1, A.st);
+}
+
 template <class Acc>
 __global__ __launch_bounds__(kBS, Acc::kFbMinWaves) void k_icp_fb_b(const PairArgs* __restrict__ pa) {
   const PairArgs& A = pa[blockIdx.z];
@@ -1930,7 +1962,7 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
     void* w = nullptr;
     const size_t sqb = refsum ? seqsum_bytes(n_local) : 0;
     RST_CHECK(ctx_workspace(ctx, sizeof(float4) * (2 * np + 2 * ng) + sizeof(int4) * nq +
-                                     sizeof(int32_t) * (2 * nq + 2 * nblk + 64) + sqb + 256,
+                                     sizeof(int32_t) * (2 * nq + 4 * nblk + 192) + sqb + 256,
                             &w));
     cert = (float4*)w;
     nnq = cert + np;
@@ -1941,7 +1973,7 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
     qbuf = (int32_t*)(cert + 2 * np + 2 * ng);
     qcnt = qbuf + 2 * nq;
     if (refsum)  // the sequential sums' tables (256-byte aligned)
-      sqws = (void*)(((uintptr_t)(qcnt + 2 * nblk + 64) + 255) & ~(uintptr_t)255);
+      sqws = (void*)(((uintptr_t)(qcnt + 4 * nblk + 192) + 255) & ~(uintptr_t)255);
     RST_HIP(hipMemsetAsync(nnq, 0xff, sizeof(float4) * np, st));
   }
 
@@ -2028,6 +2060,7 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
         k_icp_nn<RefAcc><<<nblk, kBS, 0, st>>>(bv, av, tgt->pix, aa, src->pts, n_local, ctx->d_state,
                                                nnq, cert, qbuf, qcnt, slab);
         RST_CHECK(mark(1));
+        k_queue_prefix<<<1, kBS, 0, st>>>(qcnt, nblk, ctx->d_state);
         k_icp_fb<RefAcc><<<fb_grid, kBS, fb_lds, st>>>(bv, av, tgt->pix, aa, src->pts, ctx->d_state, nnq,
                                                        cert, qbuf, qcnt, nblk, prm.lane_min, slab, slab2,
                                                        n_local);
@@ -2067,7 +2100,8 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
         k_icp_nn<Acc><<<nblk, kBS, 0, st>>>(bv, av, tgt->pix, aa, src->pts, n_local, ctx->d_state, nnq,
                                             cert, qbuf, qcnt, slab);
         RST_CHECK(mark(1));
-        k_icp_fb<Acc><<<fb_grid, kBS, fb_lds, st>>>(bv, av, tgt->pix, aa, src->pts, ctx->d_state, nnq, cert,
+        k_queue_prefix<<<1, kBS, 0, st>>>(qcnt, nblk, ctx->d_state);
+      k_icp_fb<Acc><<<fb_grid, kBS, fb_lds, st>>>(bv, av, tgt->pix, aa, src->pts, ctx->d_state, nnq, cert,
                                                      qbuf, qcnt, nblk, prm.lane_min, slab, slab2,
                                                      n_local);
         return mark(2);
@@ -2282,7 +2316,7 @@ int icp_launch_batch(rst_ctx* ctx, int nb, const rst_target* const* src, const r
     slab_tot += a256(sizeof(double) * (rows1 + (size_t)kFbBlocks * RS + 64));
     const size_t np = (size_t)n, ng = refsum ? np : 0, nq = (size_t)nblk[b] * kBS;
     ws_off[b] = ws_tot;
-    ws_tot += a256(sizeof(float4) * (2 * np + 2 * ng) + sizeof(int4) * nq + sizeof(int32_t) * (2 * nq + 2 * nblk[b] + 64)) +
+    ws_tot += a256(sizeof(float4) * (2 * np + 2 * ng) + sizeof(int4) * nq + sizeof(int32_t) * (2 * nq + 4 * nblk[b] + 192)) +
               (refsum ? a256(seqsum_bytes(n)) : 0) + 256;
   }
   const size_t fb_lds = 2 * sizeof(int) * ((size_t)nblk_max + 1);
@@ -2315,7 +2349,7 @@ int icp_launch_batch(rst_ctx* ctx, int nb, const rst_target* const* src, const r
     float4* srco = refsum ? corr + ng : nullptr;
     int32_t* qbuf = (int32_t*)(cert + 2 * np + 2 * ng);
     int32_t* qcnt = qbuf + 2 * nq;
-    void* sqws = refsum ? (void*)(((uintptr_t)(qcnt + 2 * nblk[b] + 64) + 255) & ~(uintptr_t)255) : nullptr;
+    void* sqws = refsum ? (void*)(((uintptr_t)(qcnt + 4 * nblk[b] + 192) + 255) & ~(uintptr_t)255) : nullptr;
     RST_HIP(hipMemsetAsync(nnq, 0xff, sizeof(float4) * np, st));
     // init (per pair, once): the source centroid, the state
     InitArgs ia;
@@ -2395,6 +2429,7 @@ int icp_launch_batch(rst_ctx* ctx, int nb, const rst_target* const* src, const r
     if (refsum) {
       k_icp_nn_b<RefAcc><<<gnn, kBS, 0, st>>>(d_pa);
       RST_CHECK(mark(1));
+      k_queue_prefix_b<<<gone, kBS, 0, st>>>(d_pa);
       k_icp_fb_b<RefAcc><<<gfb, kBS, fb_lds, st>>>(d_pa);
       RST_CHECK(mark(2));
       RST_CHECK(seqsum_enqueue_batch(d_sq, B, nmax, it + 1 == opts.max_iter ? 4 : 3, it, st));
@@ -2403,12 +2438,14 @@ int icp_launch_batch(rst_ctx* ctx, int nb, const rst_target* const* src, const r
     } else if (p2plane) {
       k_icp_nn_b<P2PlaneAcc><<<gnn, kBS, 0, st>>>(d_pa);
       RST_CHECK(mark(1));
+      k_queue_prefix_b<<<gone, kBS, 0, st>>>(d_pa);
       k_icp_fb_b<P2PlaneAcc><<<gfb, kBS, fb_lds, st>>>(d_pa);
       RST_CHECK(mark(2));
       k_reduce_solve_b<P2PlaneAcc><<<gone, kRedBS, 0, st>>>(d_pa, fb_grid);
     } else {
       k_icp_nn_b<P2PointAcc><<<gnn, kBS, 0, st>>>(d_pa);
       RST_CHECK(mark(1));
+      k_queue_prefix_b<<<gone, kBS, 0, st>>>(d_pa);
       k_icp_fb_b<P2PointAcc><<<gfb, kBS, fb_lds, st>>>(d_pa);
       RST_CHECK(mark(2));
       k_reduce_solve_b<P2PointAcc><<<gone, kRedBS, 0, st>>>(d_pa, fb_grid);
@@ -2523,7 +2560,7 @@ int icp_debug_partials(rst_ctx* ctx, const rst_target* src, const rst_target* tg
   double* totals = slab2 + (size_t)kFbBlocks * RS;
   void* w = nullptr;
   const size_t np = (size_t)std::max<int64_t>(n, 1), nq = (size_t)nblk * kBS;
-  RST_CHECK(ctx_workspace(ctx, sizeof(float4) * np * 2 + sizeof(int32_t) * (2 * nq + 2 * nblk + 64), &w));
+  RST_CHECK(ctx_workspace(ctx, sizeof(float4) * np * 2 + sizeof(int32_t) * (2 * nq + 4 * nblk + 192), &w));
   float4* cert = (float4*)w;
   float4* nnq = cert + np;
   int32_t* qbuf = (int32_t*)(cert + 2 * np);
@@ -2555,6 +2592,7 @@ int icp_debug_partials(rst_ctx* ctx, const rst_target* src, const rst_target* tg
     if (n > 0) {
       k_icp_nn<Acc><<<nblk, kBS, 0, st>>>(bv, av, tgt->pix, aa, src->pts, n, ctx->d_state, nnq, cert, qbuf,
                                           qcnt, slab);
+      k_queue_prefix<<<1, kBS, 0, st>>>(qcnt, nblk, ctx->d_state);
       k_icp_fb<Acc><<<fb_grid, kBS, fb_lds, st>>>(bv, av, tgt->pix, aa, src->pts, ctx->d_state, nnq, cert,
                                                    qbuf, qcnt, nblk, prm.lane_min, slab, slab2, n);
       k_reduce_solve<Acc><<<1, kRedBS, 0, st>>>(slab, 0, slab2, fb_grid, prm, ctx->d_state, totals);
