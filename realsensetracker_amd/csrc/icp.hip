@@ -2432,7 +2432,7 @@ int icp_launch_batch(rst_ctx* ctx, int nb, const rst_target* const* src, const r
       k_queue_prefix_b<<<gone, kBS, 0, st>>>(d_pa);
       k_icp_fb_b<RefAcc><<<gfb, kBS, fb_lds, st>>>(d_pa);
       RST_CHECK(mark(2));
-      RST_CHECK(seqsum_enqueue_batch(d_sq, B, nmax, it + 1 == opts.max_iter ? 4 : 3, it, st));
+      RST_CHECK(seqsum_enqueue_batch(d_sq, B, nmax, it + 1 == opts.max_iter ? 4 : 3, it, st, it > 0 ? 3 : 0));
       k_cov_ref_b<<<dim3(kCovBlocks, 1, B), kBS, 0, st>>>(d_pa);
       k_reduce_solve_b<RefAcc><<<gone, kRedBS, 0, st>>>(d_pa, kCovBlocks);
     } else if (p2plane) {

@@ -334,7 +334,8 @@ int seqsum_enqueue(const float4* d_x, int64_t n, int nch, void* ws, float* d_out
 // launch; nmax = the longest stream.  Always the map pipeline.
 size_t seqsum_pair_bytes();
 void seqsum_pair_fill(void* rec, const float4* d_x, int64_t n, void* ws, float* d_out, unsigned long long* tl);
-int seqsum_enqueue_batch(const void* d_pairs, int nbatch, int64_t nmax, int nch, int iter, hipStream_t st);
+int seqsum_enqueue_batch(const void* d_pairs, int nbatch, int64_t nmax, int nch, int iter, hipStream_t st,
+                         int nch_prev);
 // a stretch's fp64 chain totals (d_tot4[4], non-finite elements skipped)
 // for the relay's exchange; leaves the quarter totals for seqsum_enqueue
 int seqsum_totals(const float4* d_x, int64_t n, int nch, void* ws, double* d_tot4, hipStream_t st,

@@ -1684,10 +1684,17 @@ __global__ __launch_bounds__(kFrontT) void k_sq_tot_b(const SqPair* __restrict__
   if ((int)blockIdx.x >= v.nk * kTotQ) return;
   sq_tot_body(p.x, v, blockIdx.x);
 }
+template <bool FUSED>
 __global__ __launch_bounds__(kFrontT) void k_sq_front_b(const SqPair* __restrict__ P, int nch, int iter) {
-  const SqView v = sq_at(P[blockIdx.z], nch, iter);
+  const SqPair& p = P[blockIdx.z];
+  const SqView v = sq_at(p, nch, iter);
   if ((int)blockIdx.x >= v.nk) return;
-  sq_front_body<false>(v, nullptr, nullptr, nullptr, blockIdx.x, blockIdx.y);
+  if constexpr (FUSED) {  // (iter >= 1: the previous iteration's totals by parity)
+    const double* tprev = v.ttot2 + (size_t)((iter - 1) & 1) * 4 * kTotQ * v.nk;
+    sq_front_body<true>(v, p.x, tprev, v.ttot, blockIdx.x, blockIdx.y);
+  } else {
+    sq_front_body<false>(v, nullptr, nullptr, nullptr, blockIdx.x, blockIdx.y);
+  }
 }
 __global__ __launch_bounds__(kBuildT, kBuildWaves) void k_sq_build_b(const SqPair* __restrict__ P, int nch, int iter) {
   const SqView v = sq_at(P[blockIdx.z], nch, iter);
@@ -1790,12 +1797,26 @@ void seqsum_pair_fill(void* rec, const float4* d_x, int64_t n, void* ws, float* 
   memcpy(rec, &p, sizeof(p));
 }
 
-int seqsum_enqueue_batch(const void* d_pairs, int nbatch, int64_t nmax, int nch, int iter, hipStream_t st) {
+// (measured r08: the batched value 26.4k fused vs 26.9k not -- a one-batch
+// iteration's sums 266 vs 227 us; the fused front redoes the quarter totals
+// once per chain: off)
+#ifndef RST_SQ_FUSE_BATCH
+#define RST_SQ_FUSE_BATCH 0
+#endif
+int seqsum_enqueue_batch(const void* d_pairs, int nbatch, int64_t nmax, int nch, int iter, hipStream_t st,
+                         int nch_prev) {
   if (nch < 1 || nch > 4 || nbatch < 1 || nmax < 1 || nmax > (int64_t)INT_MAX - 2 * kTile) return RST_E_ARG;
   const int nb = (int)((nmax + kW - 1) / kW), ng = (nb + kGW - 1) / kGW, nk = (ng + kKW - 1) / kKW;
   const SqPair* P = (const SqPair*)d_pairs;
-  k_sq_tot_b<<<dim3(nk * kTotQ, 1, nbatch), kFrontT, 0, st>>>(P, nch, iter);
-  k_sq_front_b<<<dim3(nk, nch, nbatch), kFrontT, 0, st>>>(P, nch, iter);
+  // (fused: an iteration after the first whose chains the previous one ran
+  // too -- not the last, which adds the cost chain -- takes its tile
+  // prefixes from the previous iteration's totals, no k_sq_tot_b launch)
+  if (RST_SQ_FUSE_BATCH && iter >= 1 && nch == 3 && nch_prev == 3) {
+    k_sq_front_b<true><<<dim3(nk, nch, nbatch), kFrontT, 0, st>>>(P, nch, iter);
+  } else {
+    k_sq_tot_b<<<dim3(nk * kTotQ, 1, nbatch), kFrontT, 0, st>>>(P, nch, iter);
+    k_sq_front_b<false><<<dim3(nk, nch, nbatch), kFrontT, 0, st>>>(P, nch, iter);
+  }
   k_sq_build_b<<<dim3(nk, nch, nbatch), kBuildT, 0, st>>>(P, nch, iter);
   k_sq_walk_b<<<dim3(nch, 1, nbatch), kWave, 0, st>>>(P, nch, iter);
   RST_HIP(hipGetLastError());
