@@ -334,6 +334,7 @@ struct P2PointAcc {
   static constexpr int NV = kNP2Point;  // sum w q u^T (9), sum w u (3), sum q (3), sum d2
   static constexpr int RS = 16;         // slab row stride (doubles; divides kRedBS)
   static constexpr int kFbMinWaves = RST_FB_MIN_WAVES;  // k_icp_fb occupancy
+  static constexpr bool kPubPrefix = true;  // k_queue_prefix publishes the queues' prefixes
   static constexpr bool kCanFinish = false;
   static constexpr bool kSums = true;  // the search kernels write slab rows
   // q = the neighbour's coordinates (the caller has them), bp its sorted
@@ -363,6 +364,7 @@ struct P2PlaneAcc {
   static constexpr int NV = kNP2Plane;  // A (21), b (6), sum w r^2, count, sum d2
   static constexpr int RS = 32;
   static constexpr int kFbMinWaves = 1;
+  static constexpr bool kPubPrefix = false;  // k_icp_fb scans the queue counts per block (see there)
   static constexpr bool kCanFinish = true;
   static constexpr bool kSums = true;
   __device__ static void add(double (&v)[NV], const BvhView& bv, const AccArgs& a, const Uni& u,
@@ -403,6 +405,7 @@ struct RefAcc {
   static constexpr int NV = 9;   // k_cov_ref's rows: the 3x3 covariance
   static constexpr int RS = 16;
   static constexpr int kFbMinWaves = RST_FB_MIN_WAVES;
+  static constexpr bool kPubPrefix = true;
   static constexpr bool kCanFinish = false;
   static constexpr bool kSums = false;
   __device__ static void add(double (&v)[NV], const BvhView& bv, const AccArgs& a, const Uni& u,
@@ -1465,10 +1468,24 @@ __device__ __forceinline__ void icp_fb_body(const BvhView& bv, const AdjView& av
   __shared__ FbScratch scr[kBS / kWave];
   __shared__ int4 left[kBS / kWave][kWave / 16];  // a round's leftovers (i, seeds)
   if (Acc::kCanFinish && st->done) return;  // converged: nothing reads the slabs
-  // the queues' prefixes as k_queue_prefix published them (near [0, nb1],
-  // far [nb1 + 1, 2 nb1 + 1])
-  const int32_t* __restrict__ gpref = qcnt + 2 * nb1 + 64;
-  const int E = gpref[nb1], EF = gpref[2 * nb1 + 1];
+  // The queues' prefixes as k_queue_prefix published them (near [0, nb1],
+  // far [nb1 + 1, 2 nb1 + 1]); P2PLANE scans them per block instead (r08:
+  // with the published prefixes its k_icp_fb_b took 256 VGPRs, one wave a
+  // SIMD, 117.6 -> 195 us; the fp64 P2POINT loop measured 45.4k vs 40.9k
+  // it/s for publishing)
+  int E, EF;
+  if constexpr (!Acc::kPubPrefix) {
+    queue_prefix(qcnt, nb1, pref, blockIdx.x == 0 ? st : nullptr);
+    __syncthreads();
+    queue_prefix(qcntf, nb1, preff, nullptr);
+    __syncthreads();
+    E = pref[nb1];
+    EF = preff[nb1];
+  } else {
+    const int32_t* __restrict__ gpref = qcnt + 2 * nb1 + 64;
+    E = gpref[nb1];
+    EF = gpref[2 * nb1 + 1];
+  }
 #if RST_DIAG
   if (blockIdx.x == 0 && threadIdx.x == 0 && st->iter < kQTrace) st->diag[st->iter][0] = EF;
 #endif
@@ -1498,11 +1515,14 @@ __device__ __forceinline__ void icp_fb_body(const BvhView& bv, const AdjView& av
   const int nfar = (!many && fg0 < EF) ? (EF - fg0 + W - 1) / W : 0;
   // a block without an entry (most of the grid in the steady state) loads no
   // prefix; without sums to fold (RST_SUM_REF) it is done
-  if (__syncthreads_or(e0 < e1 || nfar > 0)) {
-    for (int j = threadIdx.x; j < 2 * (nb1 + 1); j += kBS) pref[j] = gpref[j];
-    __syncthreads();
-  } else if constexpr (!Acc::kSums) {
-    return;
+  if constexpr (Acc::kPubPrefix) {
+    if (__syncthreads_or(e0 < e1 || nfar > 0)) {
+      const int32_t* __restrict__ gpref = qcnt + 2 * nb1 + 64;
+      for (int j = threadIdx.x; j < 2 * (nb1 + 1); j += kBS) pref[j] = gpref[j];
+      __syncthreads();
+    } else if constexpr (!Acc::kSums) {
+      return;
+    }
   }
   int r0 = e0, nleft = 0, fdone = 0;
   while (true) {
@@ -2100,8 +2120,8 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
         k_icp_nn<Acc><<<nblk, kBS, 0, st>>>(bv, av, tgt->pix, aa, src->pts, n_local, ctx->d_state, nnq,
                                             cert, qbuf, qcnt, slab);
         RST_CHECK(mark(1));
-        k_queue_prefix<<<1, kBS, 0, st>>>(qcnt, nblk, ctx->d_state);
-      k_icp_fb<Acc><<<fb_grid, kBS, fb_lds, st>>>(bv, av, tgt->pix, aa, src->pts, ctx->d_state, nnq, cert,
+        if constexpr (Acc::kPubPrefix) k_queue_prefix<<<1, kBS, 0, st>>>(qcnt, nblk, ctx->d_state);
+        k_icp_fb<Acc><<<fb_grid, kBS, fb_lds, st>>>(bv, av, tgt->pix, aa, src->pts, ctx->d_state, nnq, cert,
                                                      qbuf, qcnt, nblk, prm.lane_min, slab, slab2,
                                                      n_local);
         return mark(2);
@@ -2438,7 +2458,6 @@ int icp_launch_batch(rst_ctx* ctx, int nb, const rst_target* const* src, const r
     } else if (p2plane) {
       k_icp_nn_b<P2PlaneAcc><<<gnn, kBS, 0, st>>>(d_pa);
       RST_CHECK(mark(1));
-      k_queue_prefix_b<<<gone, kBS, 0, st>>>(d_pa);
       k_icp_fb_b<P2PlaneAcc><<<gfb, kBS, fb_lds, st>>>(d_pa);
       RST_CHECK(mark(2));
       k_reduce_solve_b<P2PlaneAcc><<<gone, kRedBS, 0, st>>>(d_pa, fb_grid);
@@ -2592,7 +2611,7 @@ int icp_debug_partials(rst_ctx* ctx, const rst_target* src, const rst_target* tg
     if (n > 0) {
       k_icp_nn<Acc><<<nblk, kBS, 0, st>>>(bv, av, tgt->pix, aa, src->pts, n, ctx->d_state, nnq, cert, qbuf,
                                           qcnt, slab);
-      k_queue_prefix<<<1, kBS, 0, st>>>(qcnt, nblk, ctx->d_state);
+      if constexpr (Acc::kPubPrefix) k_queue_prefix<<<1, kBS, 0, st>>>(qcnt, nblk, ctx->d_state);
       k_icp_fb<Acc><<<fb_grid, kBS, fb_lds, st>>>(bv, av, tgt->pix, aa, src->pts, ctx->d_state, nnq, cert,
                                                    qbuf, qcnt, nblk, prm.lane_min, slab, slab2, n);
       k_reduce_solve<Acc><<<1, kRedBS, 0, st>>>(slab, 0, slab2, fb_grid, prm, ctx->d_state, totals);

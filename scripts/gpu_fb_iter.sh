@@ -14,7 +14,7 @@ import csv, glob, re, numpy as np
 f = glob.glob("gpurun_out/fbit_${TAG}_$V/**/*kernel_trace.csv", recursive=True)[0]
 rows = [r for r in csv.DictReader(open(f))]
 def nm(r): return re.sub(r"\(.*", "", r["Kernel_Name"].replace("rst::(anonymous namespace)::", "").replace("void ", ""))
-for k in ("k_icp_nn_b<RefAcc>", "k_icp_fb_b<RefAcc>"):
+for k in sorted({nm(r) for r in rows if re.search(r"_b(<|$)", nm(r))}) if "${ALLK:-}" else ("k_icp_nn_b<RefAcc>", "k_icp_fb_b<RefAcc>"):
     d = np.array([(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows if nm(r) == k])
     d = d[-128:]  # the last align: the roofline pass's batch
     print("$V", k, "total", round(d.sum()), "it 0-7", [round(x) for x in d[:8]], "8-31", round(d[8:32].mean(), 1), "32-127", round(d[32:].mean(), 1))
