@@ -21,12 +21,15 @@ SHORT="--steps 6 --warmup 1 --no-cpu --no-p2plane --no-host-api --no-gicp --ref-
 PMCB="--steps 48 --warmup 1 --batch 8 --inflight 1 --no-cpu --no-p2plane --no-host-api --no-gicp --ref-steps 0"
 step pytest_gpu 600 python -u -m pytest tests/ -x -v -m gpu --timeout 120 --timeout-method thread
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-step bench 600 python bench.py
-step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${TAG} -o run -- python3 bench.py
-python3 scripts/profile_summary.py $(find gpurun_out/prof_${TAG} -name "*kernel_stats.csv") gpurun_out/${TAG}_prof.log > gpurun_out/${TAG}_profile_summary.txt
+# the PMC passes first, so that the bench line below carries this build's
+# traffic (bench.py reads profiles/pmc_*.json; the copy stays on the box)
 step pmc_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcf_${TAG} -o run -- python3 bench.py $PMCB
 step pmc_write 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcw_${TAG} -o run -- python3 bench.py $PMCB
 python3 scripts/pmc_traffic.py gpurun_out/pmc_${TAG}.json $(find gpurun_out/pmcf_${TAG} -name "*counter_collection.csv") $(find gpurun_out/pmcw_${TAG} -name "*counter_collection.csv") RefAcc 8
+cp gpurun_out/pmc_${TAG}.json profiles/pmc_${TAG}.json
+step bench 600 python bench.py
+step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${TAG} -o run -- python3 bench.py
+python3 scripts/profile_summary.py $(find gpurun_out/prof_${TAG} -name "*kernel_stats.csv") gpurun_out/${TAG}_prof.log > gpurun_out/${TAG}_profile_summary.txt
 step iter 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/iter_${TAG} -o run -- python3 bench.py --batch 0 --inflight 1 $SHORT --steps 3
 python3 scripts/iter_profile_all.py $(find gpurun_out/iter_${TAG} -name "*kernel_trace.csv") > gpurun_out/${TAG}_iteration_profile.txt
 step diag 200 env RST_LIB=realsensetracker_amd/lib/variants/diag.so python tools/diag_fb.py
