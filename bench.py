@@ -1,12 +1,15 @@
 """Benchmark: ICP iterations/s + frames/s on a 640x480 synthetic RGB-D stream
 (BASELINE.json metric, configs[1]).
 
-One step = one incoming frame of the stream, fully on the GPU:
+One step = one batch of --batch (8) incoming frames of the stream, fully on
+the GPU, per frame:
     u16 depth (already in HBM) -> unprojection -> Morton sort + BVH build
     (the frame's index, reused as the next pair's target)
     -> AlignIcp3d(curr, prev) with the reference's P2POINT_REF loop,
-       128 fixed iterations (rs_replay_app.cpp:246-251).
-value = ICP iterations/s over all ranks (steps * 128 / time).  Frame
+       128 fixed iterations (rs_replay_app.cpp:246-251),
+the batch's 8 frame pairs aligned in lockstep by one
+rst_icp_align_batch_async (--batch 0: a step is one frame pair, one align).
+value = ICP iterations/s over all ranks (pairs * 128 / time).  Frame
 preparation runs on its own HIP stream and --inflight frame pairs (default
 24 in the reference-rounding mode, 4 in the fp64 mode; 24 HIP hardware
 queues: --hw-queues) are aligned concurrently, each on its own
@@ -143,7 +146,9 @@ def cpu_baseline(width: int, height: int, iters: int, levels: list | None = None
         O.set_threads(1)
     what = (f"{nlev}-level pyramid {width}x{height}, iterations {its} (finest first), "
             f"{eq:.1f} level-0-equivalent iterations" if levels else
-            f"first {iters} of 128 P2POINT_REF iterations")
+            f"all {iters} P2POINT_REF iterations" if iters >= 128 else
+            f"first {iters} of 128 P2POINT_REF iterations (the early iterations are the "
+            f"costliest for a kd-tree: biased low)")
     return {"value": eq / dt1, "unit": "ICP iterations/s", "cores": 1, "kind": "port",
             "sample": f"1 frame pair {width}x{height} (n={len(pb[0])}, m={len(pa[0])}), {what}, "
                       f"oracle/rst_oracle.c -O3, kd-tree leaf 16 prebuilt ({t1 - t0:.3f} s)",
@@ -296,8 +301,10 @@ def run_sharded(a, K, frames, d_depth, hip, world, rank, local, rdv, barrier, ma
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=48)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=20,
+                    help="timed steps: batches of --batch frame pairs (one frame pair each with "
+                         "--batch 0, and for the pyramid / point-to-plane / sharded workloads)")
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="stream",
                     help="stream: configs[1] (configs[2] with --width 1280 --height 720); "
                          "pyramid: configs[4]; sharded: configs[3]")
@@ -311,7 +318,9 @@ def main():
     ap.add_argument("--stride", type=int, default=1, help="trajectory frames between frames")
     ap.add_argument("--iters", type=int, default=128)
     ap.add_argument("--no-p2plane", action="store_true")
-    ap.add_argument("--cpu-iters", type=int, default=24)
+    ap.add_argument("--cpu-iters", type=int, default=128,
+                    help="CPU baseline sample: the first N of the pair's 128 iterations (all "
+                         "128 by default: the early iterations are the costliest for a kd-tree)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-host-api", action="store_true")
     ap.add_argument("--no-gicp", action="store_true")
@@ -337,8 +346,9 @@ def main():
                          "r02m: one queue per stream of the reference-rounding leg too "
                          "(24 pairs: 7.1k vs 3.0k it/s at 8 queues, main leg unchanged); "
                          "0: leave the environment's value)")
-    ap.add_argument("--ref-steps", type=int, default=48,
-                    help="frames timed in the reference-rounding mode (extra field; 0: skip)")
+    ap.add_argument("--ref-steps", type=int, default=-1,
+                    help="frame pairs timed in the other sum mode (extra field; -1: as many as "
+                         "the value leg, 0: skip)")
     ap.add_argument("--ref-inflight", type=int, default=24,
                     help="frame pairs in flight in the reference-rounding leg: its sequential "
                          "sums run one wavefront per component for most of an iteration, so "
@@ -378,7 +388,10 @@ def main():
         return float(rdv.allreduce([x], "sum")[0])
 
     K = driver.intrinsics(a.width, a.height)
-    nfr = max(2, a.frames if a.frames > 0 else min(512, max(a.steps, a.warmup) + 1))
+    batched = a.batch > 0 and not pyr and a.workload == "stream"
+    pps = a.batch if batched else 1  # frame pairs per step
+    npairs = a.steps * pps  # timed pairs
+    nfr = max(2, a.frames if a.frames > 0 else min(512, max(npairs, a.warmup * pps) + 1))
     if a.workload == "sharded":
         nfr = 2  # one pair, aligned every step
     frames = render_frames(seed=rank, n=nfr, K=K, stride=a.stride)
@@ -401,7 +414,6 @@ def main():
     opts_exact = L.default_opts(max_iter=a.iters, sum_mode=L.RST_SUM_REF)
     main_ref = a.sum_mode == "ref"
     opts_main, opts_other = (opts_exact, opts_fp64) if main_ref else (opts_fp64, opts_exact)
-    batched = a.batch > 0 and not pyr
     if a.inflight <= 0:
         a.inflight = 4 if batched or not main_ref else a.ref_inflight
     opts_pl = L.default_opts(mode=L.RST_P2PLANE, max_iter=30)
@@ -540,26 +552,27 @@ def main():
             c.synchronize()
 
     # ---- throughput mode (value): no events in the timed region -----------------
-    # warm-up: W pairs, and at least one per context in flight, so that no
+    # warm-up: W steps, and at least one per context in flight, so that no
     # context sizes its device workspace inside the timed region
+    warm_steps = max(a.warmup, len(actx))
     if batched:
-        run_batched(max(a.warmup, len(actx) * a.batch), opts_main, nk_main, None, actx, a.batch)
+        run_batched(warm_steps * a.batch, opts_main, nk_main, None, actx, a.batch)
     else:
-        run(max(a.warmup, len(actx)), opts_main, nk_main, None)
+        run(warm_steps, opts_main, nk_main, None)
     st = new_stats()
     barrier()
     sync_all()
     t0 = time.perf_counter()
     if batched:
-        run_batched(a.steps, opts_main, nk_main, st, actx, a.batch)
+        run_batched(npairs, opts_main, nk_main, st, actx, a.batch)
     else:
-        run(a.steps, opts_main, nk_main, st)
+        run(npairs, opts_main, nk_main, st)
     sync_all()
     barrier()
     dt = max_over_ranks(time.perf_counter() - t0)
     iters_all = sum_over_ranks(st["iters"])
     iters_raw = sum_over_ranks(st["iters_all"])  # pyramid: every level's iteration counted once
-    frames_all = sum_over_ranks(a.steps)
+    frames_all = sum_over_ranks(npairs)
 
     # ---- roofline: one pair in flight, events around every iteration's kernels --
     # (with two pairs in flight an event span also counts the CUs the other
@@ -567,36 +580,47 @@ def main():
     # (under --graphs the timing pass runs its one context in stream mode:
     # events cannot sit inside a replayed graph)
     # (batched: one batch in flight, its launches cover the batch's pairs; the
-    # value leg's frame pairs, whose difficulty varies along the trajectory:
-    # r06 first 8 pairs nn+fb 281 us, pairs 25-32 126 us per batched launch)
+    # value leg's frame pairs -- the same full batches --, whose difficulty
+    # varies along the trajectory: r06 first 8 pairs nn+fb 281 us, pairs 25-32
+    # 126 us per batched launch)
     sr1 = new_stats()
     actx[0].enable_kernel_timing(1)  # (a timed align runs in stream mode)
     if batched:
-        run_batched(a.steps, opts_main, nk_main, sr1, actx[:1], a.batch)
+        run_batched(npairs, opts_main, nk_main, sr1, actx[:1], a.batch)
     else:
         run(a.roof_steps, opts_main, nk_main, sr1, ctxs=actx[:1])
     actx[0].enable_kernel_timing(0)
 
     # ---- point-to-plane mode (extra fields) ---------------------------------------
     def p2plane_leg(normals_k: int) -> dict:
-        # 4 pairs in flight: a ~7-iteration pair is bound by its frame's
-        # preparation, which a deeper queue of aligns only delays
+        # 4 aligns in flight, batched as the value leg (8 pairs each) unless
+        # --batch 0: a ~7-iteration pair is bound by its frame's preparation,
+        # which a deeper queue of aligns only delays
         pctxs = actx[:4]
-        run(max(a.warmup, len(pctxs)), opts_pl, normals_k, None, pctxs)
+        B = a.batch if a.batch > 0 else 0
+        np_pl = max(a.steps * max(1, B), 8)
+
+        def go(k, stats):
+            if B:
+                run_batched(k, opts_pl, normals_k, stats, pctxs, B)
+            else:
+                run(k, opts_pl, normals_k, stats, pctxs)
+        go(max(a.warmup, len(pctxs)) * max(1, B), None)
         timing(8, pctxs)
         sp = new_stats()
         barrier()
         sync_all()
         t1 = time.perf_counter()
-        run(a.steps, opts_pl, normals_k, sp, pctxs)
+        go(np_pl, sp)
         sync_all()
         barrier()
         timing(0, pctxs)
         dtp = max_over_ranks(time.perf_counter() - t1)
-        return {"iterations_per_s": sum_over_ranks(sp["iters"]) / dtp, "pairs_in_flight": len(pctxs),
-                "frames_per_s": sum_over_ranks(a.steps) / dtp,
-                "mean_iterations_per_pair": sp["iters"] / max(1, a.steps),
-                "ms_per_pair": 1000.0 * dtp / a.steps,
+        return {"iterations_per_s": sum_over_ranks(sp["iters"]) / dtp,
+                "pairs_in_flight": len(pctxs) * max(1, B), "pairs_per_batch": max(1, B),
+                "pairs": np_pl, "frames_per_s": sum_over_ranks(np_pl) / dtp,
+                "mean_iterations_per_pair": sp["iters"] / max(1, np_pl),
+                "ms_per_pair": 1000.0 * dtp / np_pl,
                 "k_p2plane_avg_us": 1000.0 * sp["kernel_ms"] / max(1, sp["launches"]),
                 "normals": ("image-grid PCA, %dx%d window (rst_target_compute_grid_normals)"
                             % (1 - 2 * normals_k, 1 - 2 * normals_k)) if normals_k < 0 else
@@ -612,6 +636,8 @@ def main():
     # fp64 value leg: RST_SUM_REF (the drop-in default) as "ref_sums"; ref value
     # leg: RST_SUM_FP64 as "fp64_sums"
     refs = None
+    if a.ref_steps < 0:
+        a.ref_steps = npairs
     if a.ref_steps > 0 and not pyr:
         n_other = 4 if main_ref or batched else a.ref_inflight
         rctx = (actx + [A.Context(local) for _ in range(max(0, n_other - len(actx)))])[:n_other]
@@ -723,8 +749,8 @@ def main():
     nl1 = max(1, sr1["launches"])
     kern_us = [1000.0 * x / nl1 for x in sr1["iter_ms"]]  # nn | fb | rest, per iteration
     nn_us = kern_us[0] + kern_us[1]
-    n_avg = st["n"] / max(1, a.steps)
-    m_avg = st["m"] / max(1, a.steps)
+    n_avg = st["n"] / max(1, npairs)
+    m_avg = st["m"] / max(1, npairs)
     # a batched launch covers the batch's pairs: per-pair bytes x pairs per launch
     pairs_per_launch = sr1["batch_pairs"] / max(1, sr1["batches"]) if batched else 1.0
     # (point-to-plane also reads the target normals: 12 m more)
@@ -752,7 +778,8 @@ def main():
     value = iters_all / dt
     out = {
         "metric": METRIC, "value": value, "unit": "ICP iterations/s", "n_gpus": world,
-        "steps": a.steps, "warmup": a.warmup, "warmup_pairs": max(a.warmup, len(actx)),
+        "steps": a.steps, "warmup": a.warmup, "warmup_pairs": warm_steps * pps,
+        "pairs": npairs, "pairs_per_step": pps,
         "ms_per_step": 1000.0 * dt / a.steps,
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic (seeded procedural RGB-D room, ray-cast u16 depth, 1 mm noise, "
@@ -772,7 +799,9 @@ def main():
                                 f"{a.iters} iters (reference loop)"),
                    "width": a.width, "height": a.height,
                    "mode": "P2PLANE" if plane else "P2POINT_REF",
-                   "iters_per_pair": (round(st["iters"] / max(1, a.steps), 2) if plane else
+                   "step": (f"one batch of {pps} consecutive frame pairs, aligned in lockstep "
+                            f"(rst_icp_align_batch_async)" if batched else "one frame pair"),
+                   "iters_per_pair": (round(st["iters"] / max(1, npairs), 2) if plane else
                                       sum(pyr_iters) if pyr else a.iters),
                    "iteration_unit": ("level-0 equivalents: a level-l iteration counts n_l / n_0"
                                       if pyr else "full-resolution ICP iteration"),

@@ -38,10 +38,19 @@ int rst_debug_enable_seq_trace(rst_ctx* ctx, int enable);
  * stats: per chain superblock tries / hits, group tries / hits, leaf tries
  * / hits, serial blocks, walker clocks). */
 int rst_debug_seq_walk_stats(rst_ctx* ctx, int32_t* out, int32_t n);
+/* Test hook: every sequential-sum walk after this call ORs `bits` (1..127,
+ * 0 = off; process-wide) into its table bound-check word, as a corrupted map
+ * would.  An align whose sums tripped a check returns RST_E_HIP (with
+ * rst_last_error's detail), never the reference's false. */
+int rst_debug_seqsum_fault(rst_ctx* ctx, int32_t bits);
 /* The context's reduction slab (first n doubles) as the last align left
  * it: diagnostics builds write kernel clocks there (tools/nn_clock.py). */
 int rst_debug_slab(rst_ctx* ctx, double* out, int64_t n);
 int rst_debug_seq_trace(rst_ctx* ctx, float* out, int32_t n);
+/* The same for pair `pair` of the context's last collected batch
+ * (rst_icp_align_batch_wait): per iteration its three dst sums; the cost
+ * (column 3) only in the last iteration, where the batched loop walks it. */
+int rst_debug_batch_seq_trace(rst_ctx* ctx, int32_t pair, float* out, int32_t n);
 
 /* RST_DIAG builds, per iteration of the last align call on ctx (first n <=
  * 256), 4 int32: far-queue length, ball-tile chunks scanned (all waves),

@@ -354,13 +354,16 @@ def align_prepared_async(src: Target, target: Target, ctx: Context, pose=None,
 class PendingBatch:
     """A batch enqueued with align_batch_async; .wait() -> [IcpResult]."""
 
-    def __init__(self, ctx: Context, poses: np.ndarray, refs):
+    def __init__(self, ctx: Context, poses: np.ndarray, refs, nb: int):
         self.ctx = ctx
         self._buf = np.ascontiguousarray(np.stack([L.pose_to_cm(p) for p in poses]), np.float32)
+        if len(self._buf) != nb:  # the C side reads and writes nb poses
+            raise ValueError("one pose per pair")
+        self._nb = nb
         self._refs = refs  # sources / targets stay alive until wait()
 
     def wait(self) -> list:
-        nb = len(self._buf)
+        nb = self._nb  # the count the C call was given: it writes nb of each
         mc = np.zeros(nb, np.float32)
         st = np.zeros(nb, np.int32)
         it = np.zeros(nb, np.int32)
@@ -383,10 +386,12 @@ def align_batch_async(srcs, targets, ctx: Context, poses=None,
     if len(targets) != nb or nb < 1:
         raise ValueError("srcs and targets need one entry per pair")
     poses = [np.eye(4, dtype=np.float32)] * nb if poses is None else [np.asarray(p, np.float32) for p in poses]
+    if len(poses) != nb:
+        raise ValueError("poses needs one 4x4 pose per pair")
     o = opts if opts is not None else L.default_opts()
     sh = (C.c_void_p * nb)(*[t.handle.value for t in srcs])
     th = (C.c_void_p * nb)(*[t.handle.value for t in targets])
-    p = PendingBatch(ctx, poses, (list(srcs), list(targets)))
+    p = PendingBatch(ctx, poses, (list(srcs), list(targets)), nb)
     L.check(L.lib().rst_icp_align_batch_async(ctx.handle, nb, sh, th, C.byref(o), L.fptr(p._buf)),
             "rst_icp_align_batch_async")
     return p

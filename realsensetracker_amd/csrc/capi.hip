@@ -389,6 +389,13 @@ int rst_debug_enable_seq_trace(rst_ctx* ctx, int enable) {
   return RST_OK;
 }
 
+int rst_debug_seqsum_fault(rst_ctx* ctx, int32_t bits) {
+  if (!ctx || bits < 0 || bits > 127) return RST_E_ARG;
+  RST_HIP(hipSetDevice(ctx->device));
+  RST_HIP(hipStreamSynchronize(ctx->stream));
+  return seqsum_debug_fault((int)bits);
+}
+
 int rst_debug_seq_walk_stats(rst_ctx* ctx, int32_t* out, int32_t n) {
   if (!ctx || !out || n < 0 || !ctx->d_sqstats) return RST_E_ARG;
   RST_HIP(hipSetDevice(ctx->device));
@@ -402,6 +409,18 @@ int rst_debug_seq_trace(rst_ctx* ctx, float* out, int32_t n) {
   if (!ctx || !out || n < 0) return RST_E_ARG;
   for (int i = 0; i < n && i < kQTrace; ++i)
     for (int j = 0; j < 4; ++j) out[4 * i + j] = ctx->h_state->seqtr[i][j];
+  return RST_OK;
+}
+
+// the last batch's pair `pair` (its index in the call): its per-iteration
+// sequential sums (rst_debug_seq_trace's layout; the batched loop walks the
+// cost chain in the last iteration only, so column 3 is valid there alone)
+int rst_debug_batch_seq_trace(rst_ctx* ctx, int32_t pair, float* out, int32_t n) {
+  if (!ctx || !out || n < 0 || pair < 0 || pair >= ctx->bpend.nb || ctx->bpend.active) return RST_E_ARG;
+  const int slot = ctx->bpend.slot[pair];
+  if (slot < 0 || !ctx->h_bstate) return RST_E_STATE;
+  for (int i = 0; i < n && i < kQTrace; ++i)
+    for (int j = 0; j < 4; ++j) out[4 * i + j] = ctx->h_bstate[slot].seqtr[i][j];
   return RST_OK;
 }
 

@@ -163,11 +163,12 @@ __global__ void k_relay_drift(const float* __restrict__ s_in, const double* __re
 // stretch from it, and the last rank broadcasts the sums (16 B).  The walks
 // follow one another -- a sequential sum has no other decomposition -- but
 // each covers n / R elements, with its own descents, and the maps, the
-// bulk of the work, shrink by R.  d_out: 4 floats on every rank; d_drift (4
+// bulk of the work, shrink by R and run on every rank at once (enqueued
+// ahead of the receive: only the walk waits on the rank before).  d_out: 4 floats on every rank; d_drift (4
 // doubles, zero at an align's start, or null) carries the start's drift
 // from one iteration to the next.
 int comm_relay_seqsum(rst_comm* comm, const float4* d_x, int64_t n_local, int nch, void* sqws,
-                      float* d_out, hipStream_t st, double* d_drift, int* d_stats, int iter) {
+                      float* d_out, hipStream_t st, double* d_drift, int* d_stats, int iter, int* d_guard) {
   if (!comm || !comm->comm || nch < 1 || nch > 4) return RST_E_ARG;
   const int R = comm->nranks, rank = comm->rank;
   if (!comm->d_relay) {
@@ -183,13 +184,19 @@ int comm_relay_seqsum(rst_comm* comm, const float4* d_x, int64_t n_local, int nc
   if (ncclAllGather(tot4, tots, 4, ncclFloat64, comm->comm, st) != ncclSuccess) return RST_E_COMM;
   k_relay_p0<<<1, 64, 0, st>>>(tots, R, rank, d_drift, p0raw, p0);
   RST_HIP(hipGetLastError());
+  const SqStretch sx{p0, s_in, true};
+  // the maps need only the guesses (p0): enqueued before the receive, so rank
+  // r maps its stretch while the ranks before it walk theirs; only the walk
+  // (which alone reads s_in) waits for rank r - 1's chain values
+  const bool split = n_local > 0;
+  if (split) RST_CHECK(seqsum_enqueue(d_x, n_local, nch, sqws, d_out, st, d_stats, 3, iter, false, &sx, nullptr, d_guard));
   if (rank > 0) {
     if (ncclRecv(s_in, 4, ncclFloat32, rank - 1, comm->comm, st) != ncclSuccess) return RST_E_COMM;
   } else {
     RST_HIP(hipMemsetAsync(s_in, 0, sizeof(float) * 4, st));
   }
-  const SqStretch sx{p0, s_in, true};
-  RST_CHECK(seqsum_enqueue(d_x, n_local, nch, sqws, d_out, st, d_stats, 7, iter, false, &sx));
+  RST_CHECK(seqsum_enqueue(d_x, n_local, nch, sqws, d_out, st, d_stats, split ? 4 : 7, iter, false, &sx, nullptr,
+                           d_guard));
   if (rank + 1 < R && ncclSend(d_out, 4, ncclFloat32, rank + 1, comm->comm, st) != ncclSuccess)
     return RST_E_COMM;
   if (ncclBroadcast(d_out, d_out, 4, ncclFloat32, R - 1, comm->comm, st) != ncclSuccess) return RST_E_COMM;

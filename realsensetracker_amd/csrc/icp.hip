@@ -292,7 +292,8 @@ __global__ __launch_bounds__(kBS) void k_init_state(const double* __restrict__ c
     st->last_cnt = 0;
     st->last_d2 = 0;
     for (int k = 0; k < 4; ++k) st->seq[k] = 0.f;
-    st->guard = 0;
+    // (guard: cleared by the launch before the centroid's sums, which may
+    // already have set a bit; a chained pyramid level keeps the levels before)
   }
 }
 
@@ -1919,6 +1920,7 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
                const rst_icp_opts* opts_in, const float pose_in[16], rst_comm* comm,
                bool chain, int level) {
   if (!ctx || !src || !tgt || !pose_in) return RST_E_ARG;
+  if (ctx->bpend.active) return RST_E_STATE;  // one align or batch in flight per context (rst_align.h)
   ctx->pend = {};
   rst_icp_opts opts;
   if (opts_in)
@@ -1997,6 +1999,7 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
     RST_HIP(hipMemsetAsync(nnq, 0xff, sizeof(float4) * np, st));
   }
 
+  if (!chain) RST_HIP(hipMemsetAsync(&ctx->d_state->guard, 0, sizeof(int32_t), st));
   InitArgs ia;
   memcpy(ia.pose, pose_in, sizeof(ia.pose));
   ia.mu0 = opts.mu0;
@@ -2010,9 +2013,11 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
     if (n_local > 0) k_gather_orig<<<blocks_for(n_local), kBS, 0, st>>>(src->pts, src->inv, n_local, srco);
     // point_cloud_utils.cpp:94-96 (sharded: the stretches' chains relayed)
     if (comm)
-      RST_CHECK(comm_relay_seqsum(comm, srco, n_local, 3, sqws, fsum, st, nullptr, nullptr, -1));
+      RST_CHECK(comm_relay_seqsum(comm, srco, n_local, 3, sqws, fsum, st, nullptr, nullptr, -1,
+                                  &ctx->d_state->guard));
     else
-      RST_CHECK(seqsum_enqueue(srco, n_local, 3, sqws, fsum, st));
+      RST_CHECK(seqsum_enqueue(srco, n_local, 3, sqws, fsum, st, nullptr, 7, -1, false, nullptr, nullptr,
+                               &ctx->d_state->guard));
     k_init_state<<<1, kBS, 0, st>>>(slab, 0, fsum, ia, ctx->d_state);
     if (comm) RST_HIP(hipMemsetAsync(drift, 0, sizeof(double) * 4, st));
   } else if (!p2plane) {
@@ -2095,16 +2100,17 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
       const int nch_prev = it == 0 ? 0 : (it == opts.max_iter || ctx->seq_trace ? 4 : 3);
       int* sqstats = ctx->seq_trace && ctx->d_sqstats && it < kQTrace ? ctx->d_sqstats + 64 * it : nullptr;
       if (comm)
-        RST_CHECK(comm_relay_seqsum(comm, corr, n_local, nch, sqws, ctx->d_state->seq, st, drift, sqstats, it));
+        RST_CHECK(comm_relay_seqsum(comm, corr, n_local, nch, sqws, ctx->d_state->seq, st, drift, sqstats, it,
+                                    &ctx->d_state->guard));
       else
         RST_CHECK(seqsum_enqueue(corr, n_local, nch, sqws, ctx->d_state->seq, st, sqstats, 7, it,
                                  it > 0 && it >= sq_fuse_from() && nch <= nch_prev, nullptr,
 #if RST_TIMELINE
-                                 &ctx->d_state->tl[0][0][0]
+                                 &ctx->d_state->tl[0][0][0],
 #else
-                                 nullptr
+                                 nullptr,
 #endif
-                                 ));
+                                 &ctx->d_state->guard));
       if (n_local > 0)
         k_cov_ref<<<kCovBlocks, kBS, 0, st>>>(srco, corr, n_local, n_total, ctx->d_state, slab2);
       k_reduce_solve<RefAcc><<<1, kRedBS, 0, st>>>(slab, 0, slab2, n_local > 0 ? kCovBlocks : 0, prm,
@@ -2185,6 +2191,17 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
   return RST_OK;
 }
 
+// a sequential-sum table's bound check tripped (seqsum.hip err bits): the
+// sums -- NaN by then -- would read as the reference's false; an internal
+// error instead
+static int seqsum_guard_error(int32_t guard) {
+  static thread_local char msg[160];
+  snprintf(msg, sizeof(msg), "sequential-sum bound check tripped (err bits %d): sums not computed",
+           (int)((uint32_t)guard >> kGuardSeqsumShift));
+  set_last_error(hipErrorIllegalAddress, msg, __FILE__, __LINE__);
+  return RST_E_HIP;
+}
+
 int icp_finish(rst_ctx* ctx, float pose_inout[16], float* mean_cost, int32_t* iters_run) {
   if (!ctx || !pose_inout) return RST_E_ARG;
   if (!ctx->pend.active) return RST_E_STATE;
@@ -2213,6 +2230,7 @@ int icp_finish(rst_ctx* ctx, float pose_inout[16], float* mean_cost, int32_t* it
                    "n_total, or 0, on every rank)", __FILE__, __LINE__);
     return RST_E_ARG;
   }
+  if (h.guard & kGuardSeqsum) return seqsum_guard_error(h.guard);
   if (h.guard) {  // an index guard tripped: corrupted queue / neighbour state
     static thread_local char msg[160];
     const int32_t* d = h.path[kQTrace - 1];  // the first trip's details (kernel-specific)
@@ -2314,6 +2332,7 @@ int icp_launch_batch(rst_ctx* ctx, int nb, const rst_target* const* src, const r
       return RST_E_NOMEM;
     ctx->bcap = B;
   }
+  RST_HIP(hipMemsetAsync(ctx->d_bstate, 0, sizeof(IcpState) * B, st));  // (every guard word cleared)
   // per pair: slab and workspace sizes (as icp_launch), carved from one of each
   const int NVmode = p2plane ? kNP2Plane : kNP2Point;
   (void)NVmode;
@@ -2381,7 +2400,8 @@ int icp_launch_batch(rst_ctx* ctx, int nb, const rst_target* const* src, const r
     float* fsum = (float*)totals;
     if (refsum) {
       k_gather_orig<<<blocks_for(n), kBS, 0, st>>>(S->pts, S->inv, n, srco);
-      RST_CHECK(seqsum_enqueue(srco, n, 3, sqws, fsum, st));  // point_cloud_utils.cpp:94-96
+      RST_CHECK(seqsum_enqueue(srco, n, 3, sqws, fsum, st, nullptr, 7, -1, false, nullptr, nullptr,
+                               &dst->guard));  // point_cloud_utils.cpp:94-96
       k_init_state<<<1, kBS, 0, st>>>(slab, 0, fsum, ia, dst);
     } else if (!p2plane) {
       const int crows = centroid_device(ctx, S->pts, n, slab);
@@ -2418,11 +2438,11 @@ int icp_launch_batch(rst_ctx* ctx, int nb, const rst_target* const* src, const r
     if (refsum)
       seqsum_pair_fill(sqrec.data() + seqsum_pair_bytes() * b, corr, n, sqws, dst->seq,
 #if RST_TIMELINE
-                       &dst->tl[0][0][0]
+                       &dst->tl[0][0][0],
 #else
-                       nullptr
+                       nullptr,
 #endif
-      );
+                       &dst->guard);
   }
   (void)prm0;
   const PairArgs* d_pa = (const PairArgs*)(W + pa_off);
@@ -2481,6 +2501,7 @@ int icp_launch_batch(rst_ctx* ctx, int nb, const rst_target* const* src, const r
 // one pair's result from its final state (icp_finish's rules)
 static int state_result(const IcpState& h, bool p2plane, int max_iter, int64_t n_total, float pose_inout[16],
                         float* mean_cost, int32_t* iters_run) {
+  if (h.guard & kGuardSeqsum) return seqsum_guard_error(h.guard);
   if (h.guard) {
     static thread_local char msg[160];
     const int32_t* d = h.path[kQTrace - 1];
@@ -2591,6 +2612,7 @@ int icp_debug_partials(rst_ctx* ctx, const rst_target* src, const rst_target* tg
   ia.need_centroid = 0;
   ia.chain = 0;
   ia.n = n;
+  RST_HIP(hipMemsetAsync(&ctx->d_state->guard, 0, sizeof(int32_t), st));
   k_init_state<<<1, kBS, 0, st>>>(slab, 0, nullptr, ia, ctx->d_state);
   float* dsm = (float*)(totals + 48);
   RST_HIP(hipMemcpyAsync(dsm, smean, sizeof(float) * 3, hipMemcpyHostToDevice, st));
@@ -2658,6 +2680,7 @@ int icp_debug_solve(rst_ctx* ctx, const rst_icp_opts* opts_in, int64_t n_total,
   ia.need_centroid = 0;
   ia.chain = 0;
   ia.n = n_total;
+  RST_HIP(hipMemsetAsync(&ctx->d_state->guard, 0, sizeof(int32_t), st));
   k_init_state<<<1, kBS, 0, st>>>(buf, 0, nullptr, ia, ctx->d_state);
   k_debug_state<<<1, 64, 0, st>>>(ctx->d_state, dsm, *mu_inout, *iter_inout);
   const IcpParams prm = make_params(opts, n_total, n_total);

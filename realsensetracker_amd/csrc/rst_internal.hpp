@@ -76,6 +76,9 @@ struct TlGuard {
 #endif
 // IcpCore::guard bit of a shard layout that changed at an unchanged n_total
 constexpr int32_t kGuardLayout = 1 << 16;
+// ... and of a sequential-sum table bound check that tripped (seqsum.hip
+// err bits above kGuardSeqsumShift): the sums are not trusted
+constexpr int32_t kGuardSeqsum = 1 << 17, kGuardSeqsumShift = 20;
 
 // The part of the state the solve reads and writes: copied to registers at
 // the start of the solve kernel (its loads overlap the slab reduction) and
@@ -326,14 +329,17 @@ struct SqStretch {
 int seqsum_enqueue(const float4* d_x, int64_t n, int nch, void* ws, float* d_out,
                    hipStream_t st, int* d_stats = nullptr, int stages = 7, int iter = -1,
                    bool fused = false, const SqStretch* stretch = nullptr,
-                   unsigned long long* tl = nullptr);
+                   unsigned long long* tl = nullptr, int* d_guard = nullptr);
+// diagnostics: err bits every walk adds (0 = off), to test the guard path
+int seqsum_debug_fault(int bits);
 // a batch of streams summed by one set of launches (the batched ICP loop):
 // a device array of records, one per stream (seqsum_pair_fill writes one
 // into host memory: the stream, its length, its workspace of
 // seqsum_bytes(n), its 4-float output), the chains' count and iteration per
 // launch; nmax = the longest stream.  Always the map pipeline.
 size_t seqsum_pair_bytes();
-void seqsum_pair_fill(void* rec, const float4* d_x, int64_t n, void* ws, float* d_out, unsigned long long* tl);
+void seqsum_pair_fill(void* rec, const float4* d_x, int64_t n, void* ws, float* d_out, unsigned long long* tl,
+                      int* d_guard = nullptr);
 int seqsum_enqueue_batch(const void* d_pairs, int nbatch, int64_t nmax, int nch, int iter, hipStream_t st,
                          int nch_prev);
 // a stretch's fp64 chain totals (d_tot4[4], non-finite elements skipped)
@@ -376,6 +382,7 @@ int comm_layout_check(rst_comm* comm, hipStream_t st, int32_t* d_guard);
 // n_local elements) relayed rank to rank: d_out[0..nch) the whole chains'
 // sums on every rank; d_drift: 4 doubles carried between iterations (or null)
 int comm_relay_seqsum(rst_comm* comm, const float4* d_x, int64_t n_local, int nch, void* sqws,
-                      float* d_out, hipStream_t st, double* d_drift, int* d_stats, int iter);
+                      float* d_out, hipStream_t st, double* d_drift, int* d_stats, int iter,
+                      int* d_guard = nullptr);
 
 }  // namespace rst

@@ -81,7 +81,14 @@ struct SqView {
   const float* s0;
   unsigned long long* tl;  // RST_TIMELINE builds: the ICP loop's kernel timeline
   int it;                  // ... and this iteration
+  int* guard;              // optional: the ICP state's guard word -- a tripped bound
+                           // check (err) reaches the align's result as an
+                           // internal error, not as the reference's false
 };
+
+// diagnostics (rst_debug_seqsum_fault): bits OR-ed into err by every walk,
+// so a test can trip the guard path without corrupting a table
+__device__ int g_sq_fault = 0;
 
 __device__ __forceinline__ float comp(const float4& v, int c) {
   return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w));
@@ -1626,7 +1633,12 @@ __device__ __forceinline__ void sq_walk_body(const SqView& v, float* __restrict_
   }
   if (lane == 0) {
     out[c] = s;
-    if (c == 0 && v.stats) v.stats[32] = *v.err;
+    // every chain reads err after its own walk: its descents' trips and the
+    // map kernels' (an atomic read: the trips are L2 atomics)
+    if (g_sq_fault) atomicOr(v.err, g_sq_fault);
+    const int ev = atomicOr(v.err, 0);
+    if (ev && v.guard) atomicOr(v.guard, kGuardSeqsum | (ev << kGuardSeqsumShift));
+    if (c == 0 && v.stats) v.stats[32] = ev;
     if (st) {
       st[0] = nsb;
       st[1] = nsbh;
@@ -1783,12 +1795,14 @@ __global__ void k_sq_copy4(const float* __restrict__ s0, int nch, float* __restr
 
 size_t seqsum_pair_bytes() { return sizeof(SqPair); }
 
-void seqsum_pair_fill(void* rec, const float4* d_x, int64_t n, void* ws, float* d_out, unsigned long long* tl) {
+void seqsum_pair_fill(void* rec, const float4* d_x, int64_t n, void* ws, float* d_out, unsigned long long* tl,
+                      int* d_guard) {
   SqPair p;
   p.x = d_x;
   p.out = d_out;
   sq_layout(p.v, std::max<int64_t>(n, 1), 4, (char*)ws);
   p.v.n = n;
+  p.v.guard = d_guard;
   p.v.stats = nullptr;
   p.v.p0 = nullptr;
   p.v.s0 = nullptr;
@@ -1823,6 +1837,11 @@ int seqsum_enqueue_batch(const void* d_pairs, int nbatch, int64_t nmax, int nch,
   return RST_OK;
 }
 
+int seqsum_debug_fault(int bits) {
+  RST_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_sq_fault), &bits, sizeof(int)));
+  return RST_OK;
+}
+
 int seqsum_totals(const float4* d_x, int64_t n, int nch, void* ws, double* d_tot4, hipStream_t st, int iter) {
   if (nch < 1 || nch > 4 || n < 0) return RST_E_ARG;
   if (n == 0) {
@@ -1837,6 +1856,7 @@ int seqsum_totals(const float4* d_x, int64_t n, int nch, void* ws, double* d_tot
   v.s0 = nullptr;
   v.tl = nullptr;
   v.it = iter;
+  v.guard = nullptr;
   const size_t tq = (size_t)4 * kTotQ * v.nk;
   if (iter >= 0) v.ttot = v.ttot2 + (size_t)(iter & 1) * tq;
   k_sq_tot<<<v.nk * kTotQ, kFrontT, 0, st>>>(d_x, v);
@@ -1847,7 +1867,7 @@ int seqsum_totals(const float4* d_x, int64_t n, int nch, void* ws, double* d_tot
 
 int seqsum_enqueue(const float4* d_x, int64_t n, int nch, void* ws, float* d_out, hipStream_t st,
                    int* d_stats, int stages, int iter, bool fused, const SqStretch* stretch,
-                   unsigned long long* tl) {
+                   unsigned long long* tl, int* d_guard) {
   if (nch < 1 || nch > 4 || n < 0) return RST_E_ARG;
   const float* s0 = stretch ? stretch->s0 : nullptr;
   if (n == 0) {  // (a stretch: the chain's value at its start, unchanged)
@@ -1871,6 +1891,7 @@ int seqsum_enqueue(const float4* d_x, int64_t n, int nch, void* ws, float* d_out
   v.s0 = s0;
   v.tl = tl;
   v.it = iter;
+  v.guard = d_guard;
 #ifdef RST_SQ_ABLATE  // measurement only (wrong sums): skip kernels by bit
   stages &= ~RST_SQ_ABLATE;
 #endif

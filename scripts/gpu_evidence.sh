@@ -18,7 +18,7 @@ step() {  # name, limit, command...
   [ $rc -eq 0 ] || exit $rc
 }
 SHORT="--steps 6 --warmup 1 --no-cpu --no-p2plane --no-host-api --no-gicp --ref-steps 0"
-PMCB="--steps 48 --warmup 1 --batch 8 --inflight 1 --no-cpu --no-p2plane --no-host-api --no-gicp --ref-steps 0"
+PMCB="--steps 6 --warmup 1 --batch 8 --inflight 1 --no-cpu --no-p2plane --no-host-api --no-gicp --ref-steps 0"
 step pytest_gpu 600 python -u -m pytest tests/ -x -v -m gpu --timeout 120 --timeout-method thread
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 # the PMC passes first, so that the bench line below carries this build's

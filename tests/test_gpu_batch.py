@@ -81,3 +81,95 @@ def test_batch_of_one_and_reuse(ctx, frames):
     assert np.array_equal(b[0].pose, one.pose)
     for x in t:
         x.free()
+
+
+# ---- the bench's value path at its own size ------------------------------------------
+# bench.py's value leg: consecutive 640x480 frames of the seeded trajectory
+# (render_frames(seed=0): trajectory(i), noise_seed i), frame k the source of
+# pair k and the target of pair k + 1, 8 pairs per rst_icp_align_batch_async,
+# 128 RST_SUM_REF iterations (align_icp.cpp:92-153 as rs_replay_app.cpp:246-251
+# calls it); here also a ragged 4-pair batch (the tail of a run whose pair
+# count is not a multiple of 8).
+
+
+def _batch_seq_trace(ctx, pair, n):
+    import ctypes as C
+    out = np.zeros((n, 4), np.float32)
+    f = L.lib().rst_debug_batch_seq_trace
+    f.restype, f.argtypes = C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_int32]
+    L.check(f(ctx.handle, pair, out.ctypes.data, n), "rst_debug_batch_seq_trace")
+    return out
+
+
+@pytest.fixture(scope="module")
+def bench_frames():
+    K = driver.intrinsics(640, 480)
+    sc = driver.SyntheticScene(0)  # bench.py render_frames(seed=rank 0, stride 1)
+    return K, [sc.render(sc.trajectory(i), K, noise_seed=i) for i in range(13)]
+
+
+@pytest.mark.parametrize("first,nb,traced", [(1, 8, (0, 7)), (9, 4, (3,))])
+def test_bench_batch_640_ref_bitexact(ctx, bench_frames, first, nb, traced):
+    """Pairs (frame k, frame k - 1), k = first .. first + nb - 1, in one
+    lockstep batch: every pair's pose, mean cost, status and iteration count
+    bit-identical to its single align; for the traced pairs every
+    iteration's dst sums (dst_mean, :113,122) and the last iteration's cost
+    (:120, :157) bit-exact against the reference arithmetic (the oracle)."""
+    from oracle import oracle as O
+    K, deps = bench_frames
+    idx = list(range(first - 1, first + nb))
+    t = _targets(ctx, K, [deps[i] for i in idx])
+    srcs, dsts = t[1:], t[:-1]
+    opts = L.default_opts(max_iter=128, sum_mode=L.RST_SUM_REF)
+    got = A.align_batch_async(srcs, dsts, ctx, None, opts).wait()
+    traces = {p: _batch_seq_trace(ctx, p, 128) for p in traced}
+    assert len(got) == nb
+    for k in range(nb):
+        one = A.align_prepared_async(srcs[k], dsts[k], ctx, None, opts).wait()
+        assert got[k].ok and one.ok and got[k].iterations == one.iterations == 128
+        assert np.array_equal(got[k].pose, one.pose), (k, got[k].pose, one.pose)
+        assert got[k].mean_cost == one.mean_cost, k
+    K4 = [K.fx, K.fy, K.cx, K.cy]
+    O.set_threads(16)
+    try:
+        for p, tr in traces.items():
+            pb = O.unproject(deps[idx[p + 1]], K4)  # source: frame first + p
+            pa = O.unproject(deps[idx[p]], K4)
+            assert len(pb) == len(srcs[p]) and len(pa) == len(dsts[p])
+            ok, To, mco, otr = O.align_icp(pb, pa, 128, tree=O.KDTree(pa), trace=True, sum_mode=0)
+            dmean = (tr[:, :3] / np.float32(len(pb))).astype(np.float32)  # dst_mean /= n (:122)
+            bad = np.flatnonzero(np.any(dmean.view(np.uint32) != otr["dmean"].view(np.uint32), axis=1))
+            assert bad.size == 0, f"pair {p}: dst_mean differs from iteration {bad[:5]}"
+            assert tr[127, 3].view(np.uint32) == otr["cost"][127].view(np.uint32), p
+            assert ok and got[p].mean_cost == np.float32(mco), (p, got[p].mean_cost, mco)
+            assert np.array_equal(got[p].pose, To) or np.abs(got[p].pose - To).max() <= 1e-6, p
+    finally:
+        O.set_threads(1)
+    for x in t:
+        x.free()
+
+
+def test_seqsum_guard_is_an_error(ctx, frames):
+    """A tripped bound check of the sequential sums' tables (seqsum.hip err
+    bits; forced by the rst_debug_seqsum_fault hook) is an internal error of
+    the align (RST_E_HIP), single and batched -- never the reference's false
+    that NaN sums would otherwise read as (align_icp.cpp:157-160)."""
+    import ctypes as C
+    K, deps = frames
+    t = _targets(ctx, K, deps[:2])
+    opts = L.default_opts(max_iter=8, sum_mode=L.RST_SUM_REF)
+    f = L.lib().rst_debug_seqsum_fault
+    f.restype, f.argtypes = C.c_int, [C.c_void_p, C.c_int32]
+    L.check(f(ctx.handle, 4), "rst_debug_seqsum_fault")
+    try:
+        with pytest.raises(L.RstError) as ei:
+            A.align_prepared(t[1], t[0], None, opts)
+        assert "sequential-sum" in str(ei.value)
+        with pytest.raises(L.RstError):
+            A.align_batch_async([t[1]], [t[0]], ctx, None, opts).wait()
+    finally:
+        L.check(f(ctx.handle, 0), "rst_debug_seqsum_fault")
+    r = A.align_prepared(t[1], t[0], None, opts)  # the hook off: the same align is fine
+    assert r.ok
+    for x in t:
+        x.free()
