@@ -77,10 +77,12 @@ int rst_debug_seq_sum4(rst_ctx* ctx, const float* xyzw, int64_t n, float out[4])
 
 /* The same sums by either kernel: serial = 0 the loop's own choice by size
  * (seqsum_enqueue: the one-wavefront replay k_sq_serial up to
- * RST_SQ_SERIAL_MAX elements, else the parallel exact path -- verified
+ * RST_SQ_SERIAL_MAX elements, the one-workgroup-per-component k_sq_small up
+ * to RST_SQ_SMALL_MAX (<= 16384), else the parallel exact path -- verified
  * block / group / superblock maps, one walking wavefront per component),
  * 1 the older one-wavefront dependent chain (k_seq_sum4), 2 the map path
- * at any size, 3 k_sq_serial at any size; reps launches back to back, *ms
+ * at any size, 3 k_sq_serial at any size, 4 k_sq_small up to 16384
+ * elements (the map path beyond); reps launches back to back, *ms
  * (optional) = device time per launch; stats (optional, map path, 64
  * int32; zero when the replay ran) = 8 per component
  * of the last launch's walk: superblock tries / hits, group tries / hits,

@@ -820,8 +820,9 @@ int rst_debug_seq_sum(rst_ctx* ctx, const float* xyzw, int64_t n, int serial, in
   if (s >= 0 && (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess)) s = RST_E_HIP;
   if (s >= 0 && hipEventRecord(e0, ctx->stream) != hipSuccess) s = RST_E_HIP;
   // serial: 0 the product's choice by size, 1 k_seq_sum4, 2 the map pipeline
-  // at any size, 3 the one-wavefront replay (k_sq_serial) at any size
-  const int stages = 7 | (serial == 2 ? kSqForceMaps : serial == 3 ? kSqForceSerial : 0);
+  // at any size, 3 the one-wavefront replay (k_sq_serial) at any size, 4 the
+  // one-workgroup-per-chain kernel (k_sq_small) up to its 16384 elements
+  const int stages = 7 | (serial == 2 ? kSqForceMaps : serial == 3 ? kSqForceSerial : serial == 4 ? kSqForceSmall : 0);
   if (stats && serial != 1 && hipMemsetAsync(dstats, 0, 256, ctx->stream) != hipSuccess) s = RST_E_HIP;
   for (int r = 0; r < reps && s >= 0; ++r)
     s = serial == 1 ? seq_sum4_device(ctx, (const float4*)d, n, dout)

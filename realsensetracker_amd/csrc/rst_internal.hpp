@@ -314,8 +314,10 @@ int seq_sum4_device(rst_ctx* ctx, const float4* d_x, int64_t n, float* d_out);
 // ws holds seqsum_bytes(n).  stages: bits 1 / 2 / 4 the map pipeline's
 // front / maps / walk; with all three, streams of <= RST_SQ_SERIAL_MAX
 // elements take the one-wavefront replay (k_sq_serial) instead, unless
-// kSqForceMaps; kSqForceSerial takes it at any size.
-constexpr int kSqForceSerial = 16, kSqForceMaps = 32;
+// kSqForceMaps; kSqForceSerial takes it at any size; streams of <= 16384
+// elements take the one-workgroup-per-chain kernel (k_sq_small), forced by
+// kSqForceSmall.
+constexpr int kSqForceSerial = 16, kSqForceMaps = 32, kSqForceSmall = 64;
 size_t seqsum_bytes(int64_t n);
 // a stretch of a longer chain (the sharded loop's relay, comm.hip): per chain
 // the fp64 prefix before the stretch (guesses only) and the chain's value at

@@ -1719,6 +1719,351 @@ __global__ __launch_bounds__(kWave) void k_sq_walk_b(const SqPair* __restrict__ 
   sq_walk_body(v, p.out, blockIdx.x);
 }
 
+
+// ---- 5: small streams, one workgroup per chain -----------------------------------
+// Streams of <= kSmallMax elements (the reference callers' 5 cm clouds,
+// ~15k points, rs_replay_app.cpp:246-251) take the map pipeline's whole
+// statement on one CU per chain, in one launch: the chain's elements staged
+// in LDS (padded 17 words per 16), a thread per 16-element window -- the
+// window's fp64 total, block scan, the block start at the largest |prefix|
+// among window positions [kJLo, kJHi] (the front's rule), the block's
+// unmonitored float run from its fp64 guess and a scan of those increments
+// (the drift-corrected guesses), then candidate 0's monitored run (extra
+// candidates listed, one lane each) -- every leaf map in LDS; group maps
+// over 16-block windows (lattice, (group, candidate) composites, the big
+// kernel's branch-free steps); then wavefront 0 walks the <= 64 group maps
+// (spec_walk), descending to a group's leaf maps and a block's own adds.
+// No global tables, no bound checks that can trip: sizes are the launch's.
+// A chain with a non-finite element is replayed by wavefront 0 (the
+// reference loop itself). r10: the pipeline's five launches cost ~50-65 us
+// an iteration at these sizes whatever the length.
+constexpr int kSmT = 1024;             // threads: one 16-element window each
+constexpr int kSmallMax = kSmT * kW;   // 16384 elements
+constexpr int kSmGroups = kSmT / kGW;  // 64 group windows
+constexpr int kSmXs = kSmallMax + 2 * kW;
+constexpr int kSmXsPad = kSmXs + kSmXs / kW;
+constexpr int kSmList = (kLeafR - 1) * kSmT;
+struct GroupMapS {  // a group map without the global layout's padding
+  MapHdr h;
+  MapEnt e[kGroupR];
+};
+struct SmallLds {
+  union {
+    float xs[kSmXsPad];          // the chain's elements, xs(i) at i + i / 16 (phase 1)
+    GroupMapS gm[kSmGroups];     // the group maps (phase 2: the elements are dead)
+  } u;
+  Leaf lf[kSmT];
+  int bst[kSmT + 1];             // block starts (elements)
+  int gst[kSmGroups + 1];        // group starts (blocks)
+  int8_t gexact[kSmGroups];      // a group's lattice beyond kGroupM: exact-only windows
+  int16_t xneed[kSmT][kLeafR - 1];
+  uint16_t list[kSmList];
+  double scan[kSmT / kWave + 1];
+  float xb[2 * kW + 32];         // the walk's block elements (its own adds)
+  int nlist, nf, ngr;
+};
+static_assert(sizeof(SmallLds) <= 160 * 1024, "small-stream LDS");
+
+__device__ __forceinline__ float& sm_x(SmallLds& W, int i) { return W.u.xs[i + (i >> 4)]; }
+
+__global__ __launch_bounds__(kSmT) void k_sq_small(const float4* __restrict__ x, int64_t n64, int nch,
+                                                   const double* __restrict__ p0, const float* __restrict__ s0,
+                                                   float* __restrict__ out, int* __restrict__ guard) {
+  __shared__ SmallLds W;
+  const int c = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & (kWave - 1);
+  const int n = (int)n64;
+  if (c >= nch) return;
+  if (tid == 0) {
+    W.nlist = 0;
+    W.nf = 0;
+  }
+  // -- the elements, coalesced float4 loads, component c into LDS
+  int fl = 0;
+#pragma unroll
+  for (int k = 0; k < kSmXs / kSmT + 1; ++k) {
+    const int i = tid + k * kSmT;
+    if (i < kSmXs) {
+      const float e = i < n ? comp(x[i], c) : 0.0f;
+      fl |= nf_flags(e);
+      sm_x(W, i) = e;
+    }
+  }
+  const float sst = s0 ? s0[c] : 0.0f;
+  const bool anynf = __syncthreads_or(fl != 0 || !isfinite(sst));
+  if (anynf) {  // (inf / NaN: the reference's own adds, in order)
+    if (tid < kWave) {
+      float s = sst;
+      for (int i0 = 0; i0 < n; i0 += 32) {
+        float xr[32];
+#pragma unroll
+        for (int j = 0; j < 32; ++j) xr[j] = i0 + j < n ? sm_x(W, i0 + j) : 0.0f;
+#pragma unroll
+        for (int j = 0; j < 32; ++j) s = s + xr[j];
+      }
+      if (tid == 0) out[c] = s;
+    }
+    return;
+  }
+  const double P = p0 ? p0[c] : 0.0;
+  const int nb = (n + kW - 1) / kW;
+  const bool act = tid < nb;
+  // -- the window's fp64 total and prefix; the block start
+  double wsum = 0.0;
+#pragma unroll
+  for (int j = 0; j < kW; ++j) wsum += (double)sm_x(W, tid * kW + j);  // (+0 past n)
+  double ttot;
+  const double wpre = P + block_scan_excl<kSmT>(act ? wsum : 0.0, W.scan, &ttot);
+  double best = wpre, run = wpre;
+  int bj = -1;
+#pragma unroll
+  for (int j = 0; j < kW; ++j) {
+    if (j >= kJLo && j <= kJHi && (bj < 0 || fabs(run) > fabs(best)) && tid * kW + j < n) {
+      best = run;
+      bj = j;
+    }
+    run += (double)sm_x(W, tid * kW + j);
+  }
+  if (bj < 0) {
+    best = wpre;
+    bj = 0;
+  }
+  if (tid == 0) {
+    best = p0 ? P : 0.0;
+    bj = 0;
+  }
+  if (act) W.bst[tid] = tid * kW + bj;
+  if (tid == 0) W.bst[nb] = n;
+  // group starts: the block of largest |start| among blocks [kJLo, kJHi] of
+  // each 16-block window (the front's rule)
+  {
+    const int wj = tid & (kGW - 1);
+    double key = act ? (wj >= kJLo && wj <= kJHi ? fabs(best) : -0.5) : -1.0;
+    int kid = act ? tid : INT_MAX;
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) {
+      const double ok = __shfl_xor(key, o, 16);
+      const int oi = __shfl_xor(kid, o, 16);
+      if (ok > key || (ok == key && oi < kid)) {
+        key = ok;
+        kid = oi;
+      }
+    }
+    const int q = tid / kGW;
+    const int ngr = (nb + kGW - 1) / kGW;
+    if ((tid & (kGW - 1)) == 0 && q < ngr) W.gst[q] = q == 0 ? 0 : kid;
+    if (tid == 0) {
+      W.gst[ngr] = nb;
+      W.ngr = ngr;
+    }
+  }
+  __syncthreads();
+  // -- the block's unmonitored run from its fp64 guess; the increments' scan
+  const int a0 = act ? W.bst[tid] : 0;
+  const int len = act ? W.bst[tid + 1] - a0 : 0;  // <= kW + kJHi - kJLo < 2 kW
+  float w[2 * kW];
+#pragma unroll
+  for (int j = 0; j < 2 * kW; ++j) w[j] = j < len ? sm_x(W, a0 + j) : 0.0f;
+  double incv = 0.0;
+  {
+    const float G0 = tid == 0 && !p0 ? 0.0f : (float)best;
+    float sr = G0;
+#pragma unroll
+    for (int j = 0; j < 2 * kW; ++j)
+      if (j < len) sr = sr + w[j];
+    incv = act ? (double)sr - (double)G0 : 0.0;
+  }
+  double itot;
+  const double ipre = block_scan_excl<kSmT>(incv, W.scan, &itot);
+  // -- leaves: candidate 0, the block's guess
+  const float G = candidate_base(tid == 0 && !p0 ? 0.0f : (float)(P + ipre), kLeafR);
+  const int e0 = grid_exp(G);
+  Run pr;
+  run_init(pr, G);
+  const int wmax = wave_max_small<5>(len);
+#pragma unroll
+  for (int j = 0; j < 2 * kW; ++j)
+    if (j < wmax && j < len) run_step(pr, w[j], e0);
+  const int m0 = pr.need == kNoNeed ? 0 : max(0, pr.need - e0);
+  const bool more = act && !pr.opaque && m0 >= 1 && m0 <= kLeafM;
+  if (act) W.lf[tid].h = MapHdr{G, e0, 0, 0};  // (the list lanes read G, e0)
+  if (more) {
+    const int at = atomicAdd(&W.nlist, kLeafR - 1);
+#pragma unroll
+    for (int r = 1; r < kLeafR; ++r) W.list[at + r - 1] = (uint16_t)(tid << 2 | r);  // (<= 3 per block)
+  }
+  __syncthreads();
+  {
+    // the listed extra candidates, one lane each (rare; uniform skip)
+    const int nl = W.nlist;
+    for (int j0 = 0; j0 < nl; j0 += kSmT) {
+      const int j = j0 + tid;
+      const int code = j < nl ? W.list[j] : 0;
+      const int bl = code >> 2, r = code & 3;
+      const int xa = j < nl ? W.bst[bl] : 0, xl = j < nl ? W.bst[bl + 1] - xa : 0;
+      const float xG = j < nl ? W.lf[bl].h.G : 0.0f;
+      const int xe0 = j < nl ? W.lf[bl].h.e0 : -149;
+      const int xw = wave_max_small<5>(xl);
+      if (xw > 0) {
+        float v[2 * kW];
+#pragma unroll
+        for (int q = 0; q < 2 * kW; ++q) v[q] = q < xl ? sm_x(W, xa + q) : 0.0f;
+        Run q;
+        run_init(q, cand(xG, xe0, r));
+#pragma unroll
+        for (int t = 0; t < 2 * kW; ++t)
+          if (t < xw && t < xl) run_step(q, v[t], xe0);
+        if (j < nl) {
+          W.lf[bl].e[r] = leaf_ent(q, xe0);
+          W.xneed[bl][r - 1] = q.need == kNoNeed ? kNeedNone : (int16_t)max(-32767, min(32767, q.need));
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (act) {
+    int need = pr.need;
+    if (more)
+#pragma unroll
+      for (int r = 1; r < kLeafR; ++r) {
+        const int xn = W.xneed[tid][r - 1];
+        need = max(need, xn == kNeedNone ? kNoNeed : xn);
+      }
+    const int mneed = need == kNoNeed ? 0 : max(0, need - e0);
+    const bool exact_only = mneed > kLeafM;
+    const int m = exact_only ? 0 : mneed;
+    Leaf o;
+    o.h = MapHdr{G, e0, m, pr.opaque ? kOpaque : 0};
+    o.e[0] = leaf_ent(pr, e0);
+#pragma unroll
+    for (int r = 1; r < kLeafR; ++r) o.e[r] = more ? W.lf[tid].e[r] : MapEnt{0.0f, 1, 0};
+#pragma unroll
+    for (int r = 0; r < kLeafR; ++r) {
+      if (r >= (1 << m)) {
+        o.e[r].LOu = 1;
+        o.e[r].HIu = 0;
+      } else if (exact_only) {
+        o.e[r].LOu = max(o.e[r].LOu, 0);
+        o.e[r].HIu = min(o.e[r].HIu, 0);
+      }
+    }
+    W.lf[tid] = o;
+  }
+  const int ngr = W.ngr;
+  if (tid == 0) W.nlist = ngr;  // the group list: every group's candidate 0 first
+  __syncthreads();
+  // -- groups (the elements are dead: the maps take their place)
+  if (tid < ngr) {
+    const int gi = tid;
+    const int g0 = W.gst[gi], g1 = W.gst[gi + 1];
+    GroupMapS& o = W.u.gm[gi];
+    const MapHdr h0 = W.lf[g0].h;
+    int lat = h0.e0 + h0.m;
+    for (int j = g0 + 1; j < g1; ++j) {
+      const MapHdr hj = W.lf[j].h;
+      lat = (hj.flags & kOpaque) ? lat : max(lat, hj.e0 + hj.m);
+    }
+    int m = max(0, lat - h0.e0);
+    const bool exact_only = m > kGroupM;
+    if (exact_only) m = 0;
+    const int R = 1 << m;
+    const float Gg = candidate_base(h0.G, R);
+    o.h = MapHdr{Gg, grid_exp(Gg), m, 0};
+    W.gexact[gi] = exact_only ? 1 : 0;
+    for (int r = 0; r < kGroupR; ++r) o.e[r] = MapEnt{0.0f, 1, 0};
+    if (R > 1) {
+      const int at = atomicAdd(&W.nlist, R - 1);
+      for (int r = 1; r < R; ++r) W.list[at + r - 1] = (uint16_t)(gi << 4 | r);  // (<= 64 x 16)
+    }
+  }
+  __syncthreads();
+  {
+    // lanes (group, candidate) through the group's leaf maps (the big
+    // kernel's branch-free composite, sq_build_body)
+    const int nl = W.nlist;  // <= kSmGroups x kGroupR = kSmT
+    const int j = tid;
+    if (j - lane < nl) {
+      const bool ea_ = j < nl;
+      const int code = !ea_ ? 0 : (j < ngr ? j << 4 : W.list[j]);
+      const int gi = code >> 4, r = code & (kGroupR - 1);
+      const int c0 = W.gst[gi], c1 = W.gst[gi + 1];
+      const MapHdr gh = W.u.gm[gi].h;
+      float xv = cand(gh.G, gh.e0, r);
+      double clo = -INFINITY, chi = INFINITY;
+      bool ok = ea_;
+      const int4* lq = reinterpret_cast<const int4*>(W.lf);
+      int4 q0 = lq[4 * c0], q1 = lq[4 * c0 + 1], q2 = lq[4 * c0 + 2], q3 = lq[4 * c0 + 3];
+      const int nst = wave_max_small<5>(ea_ ? c1 - c0 : 0);  // (a group <= 2 kGW - 1 blocks)
+      for (int st = 0; st < nst; ++st) {
+        const int jl = c0 + st;
+        const int jn = 4 * min(jl + 1, c1 - 1);
+        const int4 n0 = lq[jn], n1 = lq[jn + 1], n2 = lq[jn + 2], n3 = lq[jn + 3];
+        const MapHdr h{__int_as_float(q0.x), q0.y, q0.z, q0.w};
+        bool okj = ok && jl < c1;
+        const int kq = comp_off(xv, h, kLeafM, okj);
+        const int rr = kq & ((1 << (okj ? h.m : 0)) - 1);
+        const bool r0 = (rr & 1) != 0, r1 = (rr & 2) != 0;
+        MapEnt en;
+        en.E = __int_as_float(r1 ? (r0 ? q3.y : q2.z) : (r0 ? q1.w : q1.x));
+        en.LOu = r1 ? (r0 ? q3.z : q2.w) : (r0 ? q2.x : q1.y);
+        en.HIu = r1 ? (r0 ? q3.w : q3.x) : (r0 ? q2.y : q1.z);
+        comp_apply(xv, clo, chi, okj, h, kq, en);
+        ok = jl < c1 ? okj : ok;
+        q0 = n0;
+        q1 = n1;
+        q2 = n2;
+        q3 = n3;
+      }
+      if (ea_ && ok) {
+        if (W.gexact[gi]) {
+          clo = fmax(clo, 0.0);
+          chi = fmin(chi, 0.0);
+        }
+        W.u.gm[gi].e[r] = MapEnt{xv, lo_units(clo, gh.e0), hi_units(chi, gh.e0)};
+      }
+    }
+  }
+  __syncthreads();
+  if (tid >= kWave) return;
+  // -- the walk: wavefront 0 over the group maps, a missed group by its leaf
+  // maps, a missed block by its own adds
+  float sv = sst;
+  int q0 = 0;
+  while (q0 < ngr) {
+    const int qf = spec_walk<GroupMapS>(sv, W.u.gm + q0, ngr - q0, kGroupM);
+    const int q = q0 + qf;
+    if (q >= ngr) break;
+    if (qf == min(kWalkC, ngr - q0)) {
+      q0 = q;
+      continue;
+    }
+    const int b0 = __builtin_amdgcn_readfirstlane(W.gst[q]), b1 = __builtin_amdgcn_readfirstlane(W.gst[q + 1]);
+    int l0 = b0;
+    while (l0 < b1) {
+      const int lf = spec_walk<Leaf>(sv, W.lf + l0, b1 - l0, kLeafM);
+      const int bl = l0 + lf;
+      if (bl >= b1) break;
+      if (lf == min(kWalkC, b1 - l0)) {
+        l0 = bl;
+        continue;
+      }
+      // block bl by the reference's adds (its elements from global memory:
+      // the LDS copy is gone)
+      const int ea = __builtin_amdgcn_readfirstlane(W.bst[bl]);
+      const int ln = __builtin_amdgcn_readfirstlane(W.bst[bl + 1]) - ea;
+      if (lane < 2 * kW) W.xb[lane] = lane < ln ? comp(x[ea + lane], c) : 0.0f;
+      __builtin_amdgcn_s_waitcnt(0);
+      __builtin_amdgcn_wave_barrier();
+      serial_adds(sv, W.xb, ln);
+      l0 = bl + 1;
+    }
+    q0 = q + 1;
+  }
+  if (lane == 0) {
+    out[c] = sv;
+    if (g_sq_fault && guard) atomicOr(guard, kGuardSeqsum | (g_sq_fault << kGuardSeqsumShift));
+  }
+}
 }  // namespace
 
 // the workspace layout (seqsum_bytes sizes it for 4 chains)
@@ -1772,6 +2117,17 @@ static int64_t serial_max() {
     const char* e = getenv("RST_SQ_SERIAL_MAX");
     const long long v = e ? atoll(e) : (long long)kSerDefault;
     return (int64_t)(v < 0 ? 0 : v);
+  }();
+  return g;
+}
+
+// the one-workgroup-per-chain kernel's ceiling (elements; RST_SQ_SMALL_MAX:
+// tuning knob, 0 = never; at most kSmallMax)
+static int64_t small_max() {
+  static const int64_t g = [] {
+    const char* e = getenv("RST_SQ_SMALL_MAX");
+    const long long v = e ? atoll(e) : (long long)kSmallMax;
+    return (int64_t)(v < 0 ? 0 : std::min<long long>(v, kSmallMax));
   }();
   return g;
 }
@@ -1876,10 +2232,18 @@ int seqsum_enqueue(const float4* d_x, int64_t n, int nch, void* ws, float* d_out
     return RST_OK;
   }
   if (n > (int64_t)INT_MAX - 2 * kTile) return RST_E_ARG;
-  // small streams: one wavefront replays the chains (the whole sum, no stats)
+  // short streams: one wavefront replays the chains; small ones: a
+  // workgroup per chain maps and walks its chain on one CU (the whole sum in
+  // one launch, no stats)
   const bool whole = (stages & 7) == 7;
-  if (whole && !(stages & kSqForceMaps) && ((stages & kSqForceSerial) || n <= serial_max())) {
+  const bool forced = (stages & (kSqForceMaps | kSqForceSerial | kSqForceSmall)) != 0;
+  if (whole && ((stages & kSqForceSerial) || (!forced && n <= serial_max()))) {
     k_sq_serial<<<1, kWave, 0, st>>>(d_x, n, nch, s0, d_out);
+    RST_HIP(hipGetLastError());
+    return RST_OK;
+  }
+  if (whole && n <= kSmallMax && ((stages & kSqForceSmall) || (!forced && n <= small_max()))) {
+    k_sq_small<<<nch, kSmT, 0, st>>>(d_x, n, nch, stretch ? stretch->p0 : nullptr, s0, d_out, d_guard);
     RST_HIP(hipGetLastError());
     return RST_OK;
   }

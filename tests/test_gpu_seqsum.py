@@ -56,14 +56,15 @@ def same(a, b):
 CASES = cases()
 
 
-PATHS = {"auto": 0, "maps": 2, "replay": 3}
+PATHS = {"auto": 0, "maps": 2, "replay": 3, "small": 4}
 
 
 @pytest.mark.parametrize("path", sorted(PATHS))
 @pytest.mark.parametrize("name", sorted(CASES))
 def test_parallel_seq_sum_bitexact(ctx, name, path):
-    """Every edge case by both paths (the map pipeline and the one-wavefront
-    replay k_sq_serial, forced at any size) and by the size rule."""
+    """Every edge case by every path (the map pipeline and the one-wavefront
+    replay k_sq_serial, forced at any size; the one-workgroup-per-chain
+    k_sq_small, forced up to its 16384 elements) and by the size rule."""
     x = CASES[name]
     got, _ = seq_sum(ctx, x, serial=PATHS[path])
     assert same(got, want(x)), (name, path, got, want(x))
@@ -130,3 +131,50 @@ def test_replay_chosen_where_faster(ctx):
     print(f"\nseq sums of 4096 float4: auto {ms_auto * 1e3:.1f} us, maps {ms_maps * 1e3:.1f} us, "
           f"replay {ms_rep * 1e3:.1f} us")
     assert ms_rep < ms_maps
+
+
+@pytest.mark.parametrize("n", [1, 2, 15, 16, 17, 255, 256, 257, 1023, 4097, 8191, 15_239, 16_383, 16_384])
+@pytest.mark.parametrize("kind", ["normal", "drift", "ties"])
+def test_small_kernel_edges(ctx, n, kind):
+    """k_sq_small (one workgroup per chain: leaf maps in LDS, 16-block
+    group maps, one walking wavefront) around its window, group and size
+    edges, on chains whose sums grow through many binades (the z-like
+    drift), cross zero, and tie on every step: bit-exact against numpy's
+    sequential float32 sums and equal to the map pipeline's."""
+    rng = np.random.default_rng(1000 + n)
+    if kind == "normal":
+        x = (rng.standard_normal((n, 4)) * np.array([1e3, 1e-3, 1.0, 1e6])).astype(np.float32)
+        x[:, 2] -= np.float32(0.25)
+    elif kind == "drift":  # coordinates of a 0.3-5 m scene: sums up to ~8e4, crossing binades
+        x = np.stack([rng.uniform(-2, 2, n), rng.uniform(-1.5, 1.5, n), rng.uniform(0.3, 5.0, n),
+                      rng.uniform(0, 1e-4, n)], 1).astype(np.float32)
+    else:  # a half-ulp tie at every step of the first chain
+        x = np.zeros((n, 4), np.float32)
+        x[:, 0] = np.float32(1.0)
+        x[1:, 0] = np.float32(2.0 ** -24)
+        x[:, 1] = np.float32(3.0)
+        x[:, 2] = rng.choice(np.array([0.5, -0.25, 2.0 ** -30], np.float32), n)
+        x[:, 3] = np.float32(0.1)
+    a, _ = seq_sum(ctx, x, serial=4)
+    b, _ = seq_sum(ctx, x, serial=2)
+    assert same(a, want(x)) and same(b, want(x)), (n, kind, a, b, want(x))
+
+
+def test_small_kernel_timing(ctx):
+    """The size rule between the replay, k_sq_small and the map pipeline at
+    the reference callers' sizes (rs_replay_app.cpp:246-251: ~15k points at
+    5 cm; ~4k at the tracker's 10 cm): k_sq_small is faster than the map
+    pipeline at 15k."""
+    rng = np.random.default_rng(6)
+    res = {}
+    for n in (1024, 2048, 4096, 8192, 15_239):
+        x = np.stack([rng.uniform(-2, 2, n), rng.uniform(-1.5, 1.5, n), rng.uniform(0.3, 5.0, n),
+                      rng.uniform(0, 1e-4, n)], 1).astype(np.float32)
+        t = {}
+        for name, code in (("small", 4), ("maps", 2), ("replay", 3), ("auto", 0)):
+            got, ms = seq_sum(ctx, x, serial=code, reps=20)
+            assert same(got, want(x)), (n, name)
+            t[name] = ms * 1e3
+        res[n] = t
+        print(f"\nseq sums of {n} float4: " + ", ".join(f"{k} {v:.1f} us" for k, v in t.items()))
+    assert res[15_239]["small"] < res[15_239]["maps"]
