@@ -182,12 +182,17 @@ def callers_cpu_baseline(raw, iters: int):
                       "leaf 16 built per call), preprocessing included"}
 
 
-def load_traffic():
+DEFAULT_CONFIG = "stream_640x480_p2point_ref"
+
+
+def load_traffic(config: str = DEFAULT_CONFIG):
     """HBM bytes per pair iteration of the NN pass (k_icp_nn + k_icp_fb, or
     a batched launch's share per pair) from a
-    committed PMC summary (profiles/pmc_*.json, scripts/pmc_traffic.py) --
-    only one stamped with this library's source hash (lib/BUILD_INFO.json):
-    a pass of other code is not reported.  Returns (bytes | None, origin)."""
+    committed PMC summary (profiles/pmc_*.json, scripts/pmc_traffic.py) of
+    this workload (`config`: workload_WxH_mode; summaries without one are of
+    the default) -- only one stamped with this library's source hash
+    (lib/BUILD_INFO.json): a pass of other code is not reported.  Returns
+    (bytes | None, origin)."""
     try:
         cur = json.loads((ROOT / "realsensetracker_amd" / "lib" / "BUILD_INFO.json").read_text())
         cur = cur.get("source_hash")
@@ -198,9 +203,10 @@ def load_traffic():
             d = json.loads(f.read_text())
         except ValueError:
             continue
-        if cur and d.get("source_hash") == cur and "nn_pass_bytes_per_pair_iteration" in d:
+        if (cur and d.get("source_hash") == cur and "nn_pass_bytes_per_pair_iteration" in d and
+                d.get("config", DEFAULT_CONFIG) == config):
             return d["nn_pass_bytes_per_pair_iteration"], f.name
-    return None, f"no PMC pass of this build (source hash {cur}) under profiles/"
+    return None, f"no PMC pass of this build (source hash {cur}) of {config} under profiles/"
 
 
 def p2point_alg_bytes(n: float, m: float) -> float:
@@ -210,6 +216,49 @@ def p2point_alg_bytes(n: float, m: float) -> float:
     while nleaves * 16 < m:
         nleaves *= 2
     return 12 * n + 12 * m + 64 * nleaves + 4 * (nleaves + 1)
+
+
+def pyramid_level_roofline(a, d_depth, K, nfr, c, pctx, opts, normals_k, pyr_iters):
+    """configs[4]'s roofline per level: each level's NN pass (k_icp_nn +
+    k_icp_fb) -- its algorithmic bytes (SURVEY.md §8d with that level's n, m)
+    over its own average kernel time (HIP events around every iteration) --
+    over --roof-steps frame pairs, the levels aligned coarsest first with the
+    pose chained, as rst_icp_align_pyramid_async runs them."""
+    out = [{"level": lv, "iters": pyr_iters[lv], "n": 0, "m": 0, "nn_us": 0.0, "launches": 0}
+           for lv in range(a.levels)]
+    c.enable_kernel_timing(1)
+    try:
+        for k in range(1, a.roof_steps + 1):
+            cur = A.Target.pyramid_from_depth_device(d_depth[pingpong(k, nfr)].value, K, a.levels,
+                                                     normals_k, pctx)
+            prv = A.Target.pyramid_from_depth_device(d_depth[pingpong(k - 1, nfr)].value, K,
+                                                     a.levels, normals_k, pctx)
+            pctx.synchronize()
+            pose = np.eye(4, dtype=np.float32)
+            for lv in reversed(range(a.levels)):
+                o = L.default_opts(max_iter=pyr_iters[lv], sum_mode=opts.sum_mode, mode=opts.mode)
+                r = A.align_prepared_async(cur[lv], prv[lv], c, pose, o).wait()
+                it3, nl = c.last_iteration_times()
+                x = out[lv]
+                x["n"] += len(cur[lv])
+                x["m"] += len(prv[lv])
+                x["nn_us"] += 1000.0 * (it3[0] + it3[1]) * nl
+                x["launches"] += nl
+                if r.ok:
+                    pose = r.pose
+            for t in cur + prv:
+                t.free()
+    finally:
+        c.enable_kernel_timing(0)
+    for x in out:
+        f = max(1, a.roof_steps)
+        x["n"] /= f
+        x["m"] /= f
+        x["nn_us"] /= max(1, x["launches"])
+        x["alg_bytes"] = p2point_alg_bytes(x["n"], x["m"])
+        x["achieved_GBps"] = x["alg_bytes"] / (x["nn_us"] * 1e-6) / 1e9 if x["nn_us"] > 0 else 0.0
+        x["frac"] = x["achieved_GBps"] / HBM_PEAK_GBS
+    return out
 
 
 def run_sharded(a, K, frames, d_depth, hip, world, rank, local, rdv, barrier, max_over_ranks):
@@ -701,23 +750,33 @@ def main():
         for name, sm in (("ref_sums", L.RST_SUM_REF), ("fp64_sums", L.RST_SUM_FP64)):
             o = L.default_opts(sum_mode=sm)
 
+            ph = [0.0, 0.0]  # prepare (RemoveNans + DownsampleVoxel of both), align
+
             def pair(k):
+                t = time.perf_counter()
                 cur = A.DownsampleVoxel(A.RemoveNans(raw[k]), 0.05)
                 prv = A.DownsampleVoxel(A.RemoveNans(raw[k - 1]), 0.05)
+                t2 = time.perf_counter()
                 T = np.eye(4, dtype=np.float32)
                 A.AlignIcp3d(cur, prv, a.iters, T, opts=o)
+                ph[0] += t2 - t
+                ph[1] += time.perf_counter() - t2
                 return len(cur)
 
             pair(1)  # warm the context's pools
+            ph[0] = ph[1] = 0.0
             t5 = time.perf_counter()
             npts = [pair(k) for k in range(2, 5)]
             dtc = (time.perf_counter() - t5) / 3
             callers[name] = {"ms_per_pair": 1000.0 * dtc, "pairs_per_s": 1.0 / dtc,
                              "iterations_per_s": a.iters / dtc,
+                             "prepare_ms": 1000.0 * ph[0] / 3, "align_ms": 1000.0 * ph[1] / 3,
                              "points_per_cloud": int(np.mean(npts))}
         callers["note"] = ("rs_replay_app.cpp:229,246-251 per frame: RemoveNans, DownsampleVoxel "
-                           "0.05 of both clouds, AlignIcp3d(curr_down, prev_down, 128) with its "
-                           "index built per call; host clouds (PCIe-inclusive), one pair at a time")
+                           "0.05 of both clouds (prepare_ms: with their unordered_map order, "
+                           "k_umap_order), AlignIcp3d(curr_down, prev_down, 128) with its "
+                           "index built per call (align_ms); host clouds (PCIe-inclusive), one "
+                           "pair at a time")
         if not a.no_cpu and world == 1:
             callers["cpu_baseline"] = callers_cpu_baseline(raw, a.iters)
             for name in ("ref_sums", "fp64_sums"):
@@ -756,12 +815,26 @@ def main():
     # (point-to-plane also reads the target normals: 12 m more)
     alg_bytes = (p2point_alg_bytes(n_avg, m_avg) + (12 * m_avg if plane else 0)) * pairs_per_launch
     achieved = alg_bytes / (nn_us * 1e-6) / 1e9 if nn_us > 0 else 0.0
-    # the committed PMC pass is of the default workload only
-    traffic, traffic_src = (load_traffic() if (a.workload, a.width, a.height, plane) ==
-                            ("stream", 640, 480, False) else
-                            (None, "the PMC pass is of the 640x480 P2POINT_REF stream"))
+    # the committed PMC pass of this workload (scripts/gpu_evidence.sh,
+    # gpu_configs.sh: the stream configs; the pyramid's levels and the
+    # sharded pair have none)
+    cfg_key = f"{a.workload}_{a.width}x{a.height}_{'p2plane' if plane else 'p2point_ref'}"
+    traffic, traffic_src = (load_traffic(cfg_key) if a.workload == "stream" else
+                            (None, "no PMC pass of this workload (its NN kernels run per level / "
+                                   "per shard)"))
     if traffic is not None:
         traffic *= pairs_per_launch
+    # the pyramid: every level's NN pass over its own kernel time (the levels
+    # chained as the value leg runs them, one pair in flight)
+    lv_roof = None
+    if pyr:
+        lv_roof = pyramid_level_roofline(a, d_depth, K, nfr, actx[0], pctx, opts_main, nk_main,
+                                         pyr_iters)
+        tb = sum(x["alg_bytes"] * x["iters"] for x in lv_roof)
+        tt = sum(x["nn_us"] * x["iters"] for x in lv_roof)
+        alg_bytes, nn_us = tb / max(1, sum(x["iters"] for x in lv_roof)), tt / max(1, sum(
+            x["iters"] for x in lv_roof))
+        achieved = tb / (tt * 1e-6) / 1e9 if tt > 0 else 0.0
 
     if rank != 0:
         rdv.close()
@@ -831,6 +904,10 @@ def main():
                                 "k_icp_nn+k_icp_fb (one ICP iteration's NN pass: certificate "
                                 "stream + compacted searches)"),
                      "pairs_per_launch": pairs_per_launch,
+                     **({"levels": lv_roof,
+                         "levels_note": "each level's NN-pass bytes over its own kernel time; "
+                                        "achieved / frac above: all levels' bytes x iterations "
+                                        "over their kernel time x iterations"} if lv_roof else {}),
                      "avg_us": nn_us, "alg_bytes_per_launch": alg_bytes,
                      "kernels_avg_us": {"k_icp_nn": kern_us[0], "k_icp_fb": kern_us[1],
                                         "rest_of_iteration": kern_us[2]},

@@ -16,7 +16,19 @@ step() {  # name, limit, command...
   echo "$name rc=$rc"; tail -3 gpurun_out/${TAG}_$name.log
   [ $rc -eq 0 ] || exit $rc
 }
-[ -n "$SKIP_TESTS" ] || step pytest_gpu 600 python -u -m pytest tests/ -x -v -m gpu --timeout 120 --timeout-method thread
+[ -n "$SKIP_TESTS" ] || step pytest_gpu 600 python -u -m pytest tests/ -x -v -m gpu --timeout 300 --timeout-method thread
+# PMC passes (FETCH / WRITE, batched NN kernels) of the 720p reference loop and
+# the 640x480 point-to-plane stream, before their bench lines (which read them)
+PMCB="--steps 6 --warmup 1 --batch 8 --inflight 1 --no-cpu --no-p2plane --no-host-api --no-gicp --ref-steps 0"
+pmc() {  # key, Acc, bench args...
+  local key=$1 acc=$2; shift 2
+  step pmcf_$key 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcf_${TAG}_$key -o run -- python3 bench.py $PMCB "$@"
+  step pmcw_$key 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcw_${TAG}_$key -o run -- python3 bench.py $PMCB "$@"
+  python3 scripts/pmc_traffic.py gpurun_out/pmc_${TAG}_$key.json $(find gpurun_out/pmcf_${TAG}_$key -name "*counter_collection.csv") $(find gpurun_out/pmcw_${TAG}_$key -name "*counter_collection.csv") $acc 8 $key
+  cp gpurun_out/pmc_${TAG}_$key.json profiles/pmc_${TAG}_$key.json
+}
+pmc stream_1280x720_p2point_ref RefAcc --width 1280 --height 720
+pmc stream_640x480_p2plane P2PlaneAcc --mode p2plane
 step bench_pyramid 300 python bench.py --workload pyramid --graphs --no-p2plane
 step bench_sharded 300 python bench.py --workload sharded --steps 5 --warmup 1
 step bench_720p 300 python bench.py --width 1280 --height 720 --no-host-api --no-gicp

@@ -11,13 +11,18 @@ A batched run (k_icp_nn_b / k_icp_fb_b: one launch per batch of PAIRS frame
 pairs, every batch full) is divided by PAIRS: the JSON holds bytes per pair
 iteration, bench.py scales them by its pairs per launch.
 
-  python scripts/pmc_traffic.py OUT.json FETCH.csv WRITE.csv [RefAcc|P2PointAcc] [PAIRS]"""
+CONFIG (optional 6th argument, bench.py's workload key, e.g.
+stream_1280x720_p2point_ref or stream_640x480_p2plane; default the value's
+stream_640x480_p2point_ref) stamps the workload the pass measured.
+
+  python scripts/pmc_traffic.py OUT.json FETCH.csv WRITE.csv [RefAcc|P2PointAcc|P2PlaneAcc] [PAIRS] [CONFIG]"""
 import csv
 import json
 import sys
 
 ACC = sys.argv[4] if len(sys.argv) > 4 else "RefAcc"
 PAIRS = int(sys.argv[5]) if len(sys.argv) > 5 else 1
+CONFIG = sys.argv[6] if len(sys.argv) > 6 else "stream_640x480_p2point_ref"
 
 
 def per_dispatch(path, counter, kernel):
@@ -53,6 +58,7 @@ def main():
                                        "bytes_per_launch": fm + wm,
                                        "fetch_size_kib_median_raw": f[len(f) // 2]}
         tot += fm + wm
+    d["config"] = CONFIG
     d["nn_pass_bytes_per_iteration"] = tot  # per launch
     d["nn_pass_bytes_per_pair_iteration"] = tot / d["pairs_per_launch"]
     try:

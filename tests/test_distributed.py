@@ -216,7 +216,7 @@ def _relay_worker(rank, world, port, out, x):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_ref_sums_relay_gloo(world):
     """The sharded loop's sequential sums without moving correspondences:
     every rank gets the unsharded chain's bits (numpy's sequential float32
@@ -237,7 +237,10 @@ def test_ref_sums_relay_gloo(world):
     want = np.add.accumulate(np.concatenate([np.zeros((1, 4), np.float32), x]), axis=0,
                              dtype=np.float32)[-1].view(np.uint32).tolist()
     assert all(g[0] == want for g in got), (got, want)
-    # (every rank's superblock jumps: most hit with the fp64-prefix guesses)
+    # (every rank's superblock jumps: most hit with the fp64-prefix guesses;
+    # a stretch's first superblock starts from the raw fp64 prefix -- no
+    # previous iteration's drift in this one-shot chain -- and at 8 ranks of
+    # 15k elements those are a quarter of the tries: 99 / 128 measured)
     hits = sum(sum(h for _, h in g[1]) for g in got)
     tries = sum(sum(t for t, _ in g[1]) for g in got)
-    assert hits >= 0.8 * tries, (hits, tries)
+    assert hits >= (0.75 if world >= 8 else 0.8) * tries, (hits, tries)

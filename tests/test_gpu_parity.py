@@ -1226,3 +1226,23 @@ def test_frame_targets_equal_host_targets(ctx, mode):
         rh = A.align_prepared(sh, th, None, o)
         assert np.array_equal(rf.pose, rh.pose), name
         assert rf.ok == rh.ok and rf.iterations == rh.iterations
+
+
+@pytest.mark.parametrize("wh,level", [((640, 480), 0), ((1280, 720), 0), ((1280, 720), 1)])
+def test_knn16_normals_grid_equal_bvh(ctx, wh, level):
+    """ComputeNormals' exact kNN-16 (point_cloud_utils.cpp:176-216) through a
+    frame target's pixel windows (k_normals_grid) against the BVH search
+    (k_normals) on the same points: every normal bit-identical (the same 16
+    neighbours in the same (d2, index) order, the same fp32 sums)."""
+    K = driver.intrinsics(*wh)
+    sc = driver.SyntheticScene(4)
+    d = sc.render(sc.trajectory(3), K, noise_seed=9)
+    dd = A.DeviceBuffer.from_array(d, ctx)
+    tf = A.Target.pyramid_from_depth_device(dd.ptr, K, level + 1, 16, ctx)[level]
+    pts = O.unproject(d, [K.fx, K.fy, K.cx, K.cy], stride=1 << level)
+    tb = A.Target.build(pts, ctx)  # no pixel grid: the BVH search
+    assert len(tb) == len(tf)
+    ng = tf.normals()
+    nb = A.ComputeNormals(pts, tb, 16)
+    bad = np.flatnonzero(np.any(ng.view(np.uint32) != nb.view(np.uint32), axis=1))
+    assert bad.size == 0, (bad.size, bad[:5])
