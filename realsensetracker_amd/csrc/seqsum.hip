@@ -1748,23 +1748,38 @@ struct GroupMapS {  // a group map without the global layout's padding
   MapEnt e[kGroupR];
 };
 struct SmallLds {
-  union {
-    float xs[kSmXsPad];          // the chain's elements, xs(i) at i + i / 16 (phase 1)
-    GroupMapS gm[kSmGroups];     // the group maps (phase 2: the elements are dead)
-  } u;
+  float xs[kSmXsPad];            // the chain's elements, xs(i) at i + i / 16 (the walk's own
+                                 // adds read them too: r10a, from global memory, ~60 us a call)
   Leaf lf[kSmT];
+  union {
+    int16_t xneed[kSmT][kLeafR - 1];  // the leaves' extra candidates' needs (leaf phase)
+    GroupMapS gm[kSmGroups];          // the group maps (group phase on)
+  } u;
   int bst[kSmT + 1];             // block starts (elements)
   int gst[kSmGroups + 1];        // group starts (blocks)
   int8_t gexact[kSmGroups];      // a group's lattice beyond kGroupM: exact-only windows
-  int16_t xneed[kSmT][kLeafR - 1];
-  uint16_t list[kSmList];
+  uint16_t list[kSmList];        // the leaves' extra candidates, then the groups'
   double scan[kSmT / kWave + 1];
-  float xb[2 * kW + 32];         // the walk's block elements (its own adds)
-  int nlist, nf, ngr;
+  int nlist, ngr;
 };
 static_assert(sizeof(SmallLds) <= 160 * 1024, "small-stream LDS");
 
-__device__ __forceinline__ float& sm_x(SmallLds& W, int i) { return W.u.xs[i + (i >> 4)]; }
+__device__ __forceinline__ float& sm_x(SmallLds& W, int i) { return W.xs[i + (i >> 4)]; }
+
+// s <- the reference's adds over elements [a, a + cnt) of the padded LDS copy
+// (serial_adds' rounds: 32 broadcast reads, then 32 dependent adds; +0 past cnt)
+__device__ __forceinline__ void serial_adds_sm(float& s, SmallLds& W, int a, int cnt) {
+  constexpr int kR = 32;
+  cnt = __builtin_amdgcn_readfirstlane(cnt);
+  a = __builtin_amdgcn_readfirstlane(a);
+  for (int c0 = 0; c0 < cnt; c0 += kR) {
+    float xr[kR];
+#pragma unroll
+    for (int i = 0; i < kR; ++i) xr[i] = c0 + i < cnt ? sm_x(W, a + c0 + i) : 0.0f;
+#pragma unroll
+    for (int i = 0; i < kR; ++i) s = s + xr[i];
+  }
+}
 
 __global__ __launch_bounds__(kSmT) void k_sq_small(const float4* __restrict__ x, int64_t n64, int nch,
                                                    const double* __restrict__ p0, const float* __restrict__ s0,
@@ -1774,10 +1789,7 @@ __global__ __launch_bounds__(kSmT) void k_sq_small(const float4* __restrict__ x,
   const int tid = threadIdx.x, lane = tid & (kWave - 1);
   const int n = (int)n64;
   if (c >= nch) return;
-  if (tid == 0) {
-    W.nlist = 0;
-    W.nf = 0;
-  }
+  if (tid == 0) W.nlist = 0;
   // -- the elements, coalesced float4 loads, component c into LDS
   int fl = 0;
 #pragma unroll
@@ -1915,7 +1927,7 @@ __global__ __launch_bounds__(kSmT) void k_sq_small(const float4* __restrict__ x,
           if (t < xw && t < xl) run_step(q, v[t], xe0);
         if (j < nl) {
           W.lf[bl].e[r] = leaf_ent(q, xe0);
-          W.xneed[bl][r - 1] = q.need == kNoNeed ? kNeedNone : (int16_t)max(-32767, min(32767, q.need));
+          W.u.xneed[bl][r - 1] = q.need == kNoNeed ? kNeedNone : (int16_t)max(-32767, min(32767, q.need));
         }
       }
     }
@@ -1926,7 +1938,7 @@ __global__ __launch_bounds__(kSmT) void k_sq_small(const float4* __restrict__ x,
     if (more)
 #pragma unroll
       for (int r = 1; r < kLeafR; ++r) {
-        const int xn = W.xneed[tid][r - 1];
+        const int xn = W.u.xneed[tid][r - 1];
         need = max(need, xn == kNeedNone ? kNoNeed : xn);
       }
     const int mneed = need == kNoNeed ? 0 : max(0, need - e0);
@@ -1952,7 +1964,7 @@ __global__ __launch_bounds__(kSmT) void k_sq_small(const float4* __restrict__ x,
   const int ngr = W.ngr;
   if (tid == 0) W.nlist = ngr;  // the group list: every group's candidate 0 first
   __syncthreads();
-  // -- groups (the elements are dead: the maps take their place)
+  // -- groups (their maps take the leaves' needs' place)
   if (tid < ngr) {
     const int gi = tid;
     const int g0 = W.gst[gi], g1 = W.gst[gi + 1];
@@ -2047,14 +2059,10 @@ __global__ __launch_bounds__(kSmT) void k_sq_small(const float4* __restrict__ x,
         l0 = bl;
         continue;
       }
-      // block bl by the reference's adds (its elements from global memory:
-      // the LDS copy is gone)
+      // block bl by the reference's adds (its elements in LDS)
       const int ea = __builtin_amdgcn_readfirstlane(W.bst[bl]);
       const int ln = __builtin_amdgcn_readfirstlane(W.bst[bl + 1]) - ea;
-      if (lane < 2 * kW) W.xb[lane] = lane < ln ? comp(x[ea + lane], c) : 0.0f;
-      __builtin_amdgcn_s_waitcnt(0);
-      __builtin_amdgcn_wave_barrier();
-      serial_adds(sv, W.xb, ln);
+      serial_adds_sm(sv, W, ea, ln);
       l0 = bl + 1;
     }
     q0 = q + 1;

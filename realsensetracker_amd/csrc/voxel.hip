@@ -277,11 +277,21 @@ __device__ int64_t wg_scan(int32_t* a, int64_t n, bool suffix, int64_t* part) {
   const int64_t b0 = t * per, b1 = min(n, b0 + per);
   int64_t sum = 0;
   for (int64_t i = b0; i < b1; ++i) sum += ld(a + (suffix ? n - 1 - i : i));
-  part[t] = sum;
+  // the partials' exclusive scan: wave-level shuffles, then the 16 wave
+  // totals (r10a: one thread walking the 1024 partials took ~25 us per scan,
+  // two scans per rehash level -- k_umap_order ~0.9 ms a call at 15k keys)
+  const int lane = t & (kWave - 1), wv = t / kWave;
+  int64_t inc = sum;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const int64_t y = __shfl_up(inc, o, kWave);
+    if (lane >= o) inc += y;
+  }
+  if (lane == kWave - 1) part[wv] = inc;
   __syncthreads();
   if (t == 0) {
     int64_t run = 0;
-    for (int k = 0; k < kUmapT; ++k) {
+    for (int k = 0; k < kUmapT / kWave; ++k) {
       const int64_t v = part[k];
       part[k] = run;
       run += v;
@@ -289,7 +299,7 @@ __device__ int64_t wg_scan(int32_t* a, int64_t n, bool suffix, int64_t* part) {
     part[kUmapT] = run;
   }
   __syncthreads();
-  int64_t run = part[t];
+  int64_t run = part[wv] + inc - sum;
   for (int64_t i = b0; i < b1; ++i) {
     const int64_t j = suffix ? n - 1 - i : i;
     const int32_t v = ld(a + j);
