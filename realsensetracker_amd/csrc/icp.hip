@@ -513,9 +513,16 @@ __global__ __launch_bounds__(kBS) void k_gather_orig(const float4* __restrict__ 
 #define RST_COV_BLOCKS 256
 #endif
 constexpr int kCovBlocks = RST_COV_BLOCKS;
+// the covariance grid of a cloud of n points: kCovBlocks, or for small clouds
+// (<= 32768 points, the reference callers' 5 cm voxels) ~8 points a thread --
+// the solve then reduces a few rows (the fp64 sum order, i.e. the last bits of
+// a double, follows n alone: a pair's batched and single aligns agree)
+__host__ __device__ __forceinline__ int cov_blocks(int64_t n) {
+  return n > 32768 ? kCovBlocks : (int)((n + 8 * kBS - 1) / (8 * kBS)) + (n == 0 ? 1 : 0);
+}
 __device__ __forceinline__ void cov_ref_body(const float4* __restrict__ srco, const float4* __restrict__ corr,
                                              int64_t n, int64_t n_total, const IcpState* __restrict__ st,
-                                             double* __restrict__ slab) {
+                                             double* __restrict__ slab, int nblk) {
   __shared__ double lds[(kBS / kWave) * 9];
 #if RST_TIMELINE
   RST_TL(const_cast<IcpState*>(st)->tl[0][0], st->iter, 6);
@@ -529,7 +536,7 @@ __device__ __forceinline__ void cov_ref_body(const float4* __restrict__ srco, co
 #pragma unroll
   for (int k = 0; k < 9; ++k) v[k] = 0.0;
   for (int64_t i = blockIdx.x * (int64_t)kBS + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * kBS) {
+       i += (int64_t)nblk * kBS) {
     const float4 s = srco[i];
     const float4 c = corr[i];
     // d2 of the search (:112), recomputed: the records of lanes that kept
@@ -554,7 +561,7 @@ __global__ __launch_bounds__(kBS) void k_cov_ref(const float4* __restrict__ srco
                                                  int64_t n_total,
                                                  const IcpState* __restrict__ st,
                                                  double* __restrict__ slab) {
-  cov_ref_body(srco, corr, n, n_total, st, slab);
+  cov_ref_body(srco, corr, n, n_total, st, slab, (int)gridDim.x);
 }
 
 // ---- kernel 1: adjacency search, one point per thread ----------------------------------
@@ -1449,7 +1456,7 @@ union FbScratch {
   BallScratch b;
 };
 
-template <class Acc>
+template <class Acc, bool PUB = Acc::kPubPrefix>
 __device__ __forceinline__ void icp_fb_body(const BvhView& bv, const AdjView& av, const PixView& pv,
                                             const AccArgs& aa, const float4* __restrict__ src,
                                             IcpState* __restrict__ st, float4* __restrict__ nnq,
@@ -1475,7 +1482,7 @@ __device__ __forceinline__ void icp_fb_body(const BvhView& bv, const AdjView& av
   // SIMD, 117.6 -> 195 us; the fp64 P2POINT loop measured 45.4k vs 40.9k
   // it/s for publishing)
   int E, EF;
-  if constexpr (!Acc::kPubPrefix) {
+  if constexpr (!PUB) {
     queue_prefix(qcnt, nb1, pref, blockIdx.x == 0 ? st : nullptr);
     __syncthreads();
     queue_prefix(qcntf, nb1, preff, nullptr);
@@ -1516,7 +1523,7 @@ __device__ __forceinline__ void icp_fb_body(const BvhView& bv, const AdjView& av
   const int nfar = (!many && fg0 < EF) ? (EF - fg0 + W - 1) / W : 0;
   // a block without an entry (most of the grid in the steady state) loads no
   // prefix; without sums to fold (RST_SUM_REF) it is done
-  if constexpr (Acc::kPubPrefix) {
+  if constexpr (PUB) {
     if (__syncthreads_or(e0 < e1 || nfar > 0)) {
       const int32_t* __restrict__ gpref = qcnt + 2 * nb1 + 64;
       for (int j = threadIdx.x; j < 2 * (nb1 + 1); j += kBS) pref[j] = gpref[j];
@@ -1720,7 +1727,7 @@ __device__ __forceinline__ void icp_fb_body(const BvhView& bv, const AdjView& av
                                          Acc::RS, blockIdx.x, gridDim.x);
 }
 
-template <class Acc>
+template <class Acc, bool PUB = Acc::kPubPrefix>
 __global__ __launch_bounds__(kBS, Acc::kFbMinWaves) void k_icp_fb(BvhView bv, AdjView av, PixView pv,
                                                 AccArgs aa,
                                                 const float4* __restrict__ src,
@@ -1731,7 +1738,7 @@ __global__ __launch_bounds__(kBS, Acc::kFbMinWaves) void k_icp_fb(BvhView bv, Ad
                                                 const int32_t* __restrict__ qcnt, int nb1,
                                                 int lane_min, const double* __restrict__ slab1,
                                                 double* __restrict__ slab2, int64_t n) {
-  icp_fb_body<Acc>(bv, av, pv, aa, src, st, nnq, cert, qbuf, qcnt, nb1, lane_min, slab1, slab2, n);
+  icp_fb_body<Acc, PUB>(bv, av, pv, aa, src, st, nnq, cert, qbuf, qcnt, nb1, lane_min, slab1, slab2, n);
 }
 
 // the batch forms (PairArgs, pair = blockIdx.z)
@@ -1749,13 +1756,16 @@ __global__ __launch_bounds__(kBS, Acc::kFbMinWaves) void k_icp_fb_b(const PairAr
 
 __global__ __launch_bounds__(kBS) void k_cov_ref_b(const PairArgs* __restrict__ pa) {
   const PairArgs& A = pa[blockIdx.z];
-  cov_ref_body(A.srco, A.corr, A.n, A.n_total, A.st, A.slab2);
+  const int nb = cov_blocks(A.n);
+  if ((int)blockIdx.x >= nb) return;
+  cov_ref_body(A.srco, A.corr, A.n, A.n_total, A.st, A.slab2, nb);
 }
 
 template <class Acc>
 __global__ __launch_bounds__(kRedBS) void k_reduce_solve_b(const PairArgs* __restrict__ pa, int rows2max) {
   const PairArgs& A = pa[blockIdx.z];
-  reduce_solve_body<Acc>(A.slab, 0, A.slab2, rows2max, A.prm, A.st, nullptr);
+  const int rows = std::is_same<Acc, RefAcc>::value ? cov_blocks(A.n) : rows2max;
+  reduce_solve_body<Acc>(A.slab, 0, A.slab2, rows, A.prm, A.st, nullptr);
 }
 
 template <class A>
@@ -1890,6 +1900,14 @@ static int fb_grid_size() {
   return g;
 }
 
+static int64_t small_fb_n() {
+  static const int64_t g = [] {
+    const char* e = getenv("RST_SMALL_FB_N");
+    return e ? (int64_t)atoll(e) : (int64_t)32768;
+  }();
+  return g;
+}
+
 static IcpParams make_params(const rst_icp_opts& opts, int64_t n_total, int64_t n_local) {
   IcpParams prm;
   prm.n = n_total;
@@ -1910,8 +1928,13 @@ static IcpParams make_params(const rst_icp_opts& opts, int64_t n_total, int64_t 
     const char* e = getenv("RST_LANE_MIN_DIV");
     return e ? atoi(e) : 0;
   }();
+  // (RST_LANE_MIN_FLOOR: the smallest such queue -- tuning knob)
+  static const int lane_floor = [] {
+    const char* e = getenv("RST_LANE_MIN_FLOOR");
+    return e ? atoi(e) : 16384;
+  }();
   prm.lane_min = (int)std::max<int64_t>(
-      16384, lane_div > 0 ? n_local / lane_div
+      lane_floor, lane_div > 0 ? n_local / lane_div
                           : (n_local < RST_LANE_SMALL_N ? (3 * n_local) / 4 : n_local / 3));
   return prm;
 }
@@ -2050,6 +2073,11 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
 
   const int fb_grid = fb_grid_size();
   const IcpParams prm = make_params(opts, n_total, n_local);
+  // RST_SUM_REF on a small cloud (<= RST_SMALL_FB_N points): the fallback
+  // blocks scan the few queue counts themselves, no prefix launch (RefAcc:
+  // no sums, results independent of the grid)
+  const bool small_fb = refsum && n_local <= small_fb_n();
+  const int fb_grid_small = fb_grid;  // (r10c: 2 blocks per kernel-1 block, 231 vs 111 us a cold iteration)
 
   const BvhView bv = view_of(tgt);
   const bool timing = ctx->timing && opts.max_iter > 0;
@@ -2085,10 +2113,20 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
         k_icp_nn<RefAcc><<<nblk, kBS, 0, st>>>(bv, av, tgt->pix, aa, src->pts, n_local, ctx->d_state,
                                                nnq, cert, qbuf, qcnt, slab);
         RST_CHECK(mark(1));
-        k_queue_prefix<<<1, kBS, 0, st>>>(qcnt, nblk, ctx->d_state);
-        k_icp_fb<RefAcc><<<fb_grid, kBS, fb_lds, st>>>(bv, av, tgt->pix, aa, src->pts, ctx->d_state, nnq,
-                                                       cert, qbuf, qcnt, nblk, prm.lane_min, slab, slab2,
-                                                       n_local);
+        if (small_fb) {
+          // small clouds (the reference callers' 5 cm voxels): no prefix
+          // launch -- each fallback block scans the few queue counts itself
+          // -- over a grid sized to the cloud (RefAcc folds no sums: the
+          // grid moves no bit)
+          k_icp_fb<RefAcc, false><<<fb_grid_small, kBS, fb_lds, st>>>(bv, av, tgt->pix, aa, src->pts,
+                                                                      ctx->d_state, nnq, cert, qbuf, qcnt, nblk,
+                                                                      prm.lane_min, slab, slab2, n_local);
+        } else {
+          k_queue_prefix<<<1, kBS, 0, st>>>(qcnt, nblk, ctx->d_state);
+          k_icp_fb<RefAcc><<<fb_grid, kBS, fb_lds, st>>>(bv, av, tgt->pix, aa, src->pts, ctx->d_state, nnq,
+                                                         cert, qbuf, qcnt, nblk, prm.lane_min, slab, slab2,
+                                                         n_local);
+        }
       } else {
         RST_CHECK(mark(1));
       }
@@ -2112,8 +2150,8 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
 #endif
                                  &ctx->d_state->guard));
       if (n_local > 0)
-        k_cov_ref<<<kCovBlocks, kBS, 0, st>>>(srco, corr, n_local, n_total, ctx->d_state, slab2);
-      k_reduce_solve<RefAcc><<<1, kRedBS, 0, st>>>(slab, 0, slab2, n_local > 0 ? kCovBlocks : 0, prm,
+        k_cov_ref<<<cov_blocks(n_local), kBS, 0, st>>>(srco, corr, n_local, n_total, ctx->d_state, slab2);
+      k_reduce_solve<RefAcc><<<1, kRedBS, 0, st>>>(slab, 0, slab2, n_local > 0 ? cov_blocks(n_local) : 0, prm,
                                                    ctx->d_state, red_out);
       if (comm) {
         RST_CHECK(comm_allreduce_sum_f64(comm, totals, RefAcc::NV, st));

@@ -1783,26 +1783,41 @@ __device__ __forceinline__ void serial_adds_sm(float& s, SmallLds& W, int a, int
 
 __global__ __launch_bounds__(kSmT) void k_sq_small(const float4* __restrict__ x, int64_t n64, int nch,
                                                    const double* __restrict__ p0, const float* __restrict__ s0,
-                                                   float* __restrict__ out, int* __restrict__ guard) {
+                                                   float* __restrict__ out, int* __restrict__ guard,
+                                                   int* __restrict__ stats) {
   __shared__ SmallLds W;
+  // (diagnostics, rst_debug_seq_sum's stats: chain 0's phase clocks and walk
+  // counts -- group tries / hits, leaf tries / hits, blocks added serially)
+  const bool stm = stats && blockIdx.x == 0 && threadIdx.x == 0;
+  const long long ck0 = stm ? (long long)__builtin_amdgcn_s_memtime() : 0;
+  auto mark = [&](int j) {
+    if (stm) stats[j] = (int)((long long)__builtin_amdgcn_s_memtime() - ck0);
+  };
   const int c = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & (kWave - 1);
   const int n = (int)n64;
   if (c >= nch) return;
   if (tid == 0) W.nlist = 0;
-  // -- the elements, coalesced float4 loads, component c into LDS
+  // -- the elements, coalesced float4 loads, component c into LDS (every
+  // load issued before the first store: r10b, a load-store pair per element
+  // waited out a memory round trip each, ~30 us at any length)
+  constexpr int kLd = kSmXs / kSmT + 1;
+  float tv[kLd];
+#pragma unroll
+  for (int k = 0; k < kLd; ++k) {
+    const int i = tid + k * kSmT;
+    tv[k] = i < n ? comp(x[i], c) : 0.0f;
+  }
   int fl = 0;
 #pragma unroll
-  for (int k = 0; k < kSmXs / kSmT + 1; ++k) {
+  for (int k = 0; k < kLd; ++k) {
     const int i = tid + k * kSmT;
-    if (i < kSmXs) {
-      const float e = i < n ? comp(x[i], c) : 0.0f;
-      fl |= nf_flags(e);
-      sm_x(W, i) = e;
-    }
+    fl |= nf_flags(tv[k]);
+    if (i < kSmXs) sm_x(W, i) = tv[k];
   }
   const float sst = s0 ? s0[c] : 0.0f;
   const bool anynf = __syncthreads_or(fl != 0 || !isfinite(sst));
+  mark(0);
   if (anynf) {  // (inf / NaN: the reference's own adds, in order)
     if (tid < kWave) {
       float s = sst;
@@ -1870,6 +1885,7 @@ __global__ __launch_bounds__(kSmT) void k_sq_small(const float4* __restrict__ x,
     }
   }
   __syncthreads();
+  mark(1);
   // -- the block's unmonitored run from its fp64 guess; the increments' scan
   const int a0 = act ? W.bst[tid] : 0;
   const int len = act ? W.bst[tid + 1] - a0 : 0;  // <= kW + kJHi - kJLo < 2 kW
@@ -1905,6 +1921,7 @@ __global__ __launch_bounds__(kSmT) void k_sq_small(const float4* __restrict__ x,
     for (int r = 1; r < kLeafR; ++r) W.list[at + r - 1] = (uint16_t)(tid << 2 | r);  // (<= 3 per block)
   }
   __syncthreads();
+  mark(2);
   {
     // the listed extra candidates, one lane each (rare; uniform skip)
     const int nl = W.nlist;
@@ -1964,6 +1981,7 @@ __global__ __launch_bounds__(kSmT) void k_sq_small(const float4* __restrict__ x,
   const int ngr = W.ngr;
   if (tid == 0) W.nlist = ngr;  // the group list: every group's candidate 0 first
   __syncthreads();
+  mark(3);
   // -- groups (their maps take the leaves' needs' place)
   if (tid < ngr) {
     const int gi = tid;
@@ -2036,7 +2054,9 @@ __global__ __launch_bounds__(kSmT) void k_sq_small(const float4* __restrict__ x,
     }
   }
   __syncthreads();
+  mark(4);
   if (tid >= kWave) return;
+  int ngt = 0, ngh = 0, nlt = 0, nlh = 0, nser = 0;
   // -- the walk: wavefront 0 over the group maps, a missed group by its leaf
   // maps, a missed block by its own adds
   float sv = sst;
@@ -2044,6 +2064,8 @@ __global__ __launch_bounds__(kSmT) void k_sq_small(const float4* __restrict__ x,
   while (q0 < ngr) {
     const int qf = spec_walk<GroupMapS>(sv, W.u.gm + q0, ngr - q0, kGroupM);
     const int q = q0 + qf;
+    ngt += min(qf + 1, ngr - q0);
+    ngh += qf;
     if (q >= ngr) break;
     if (qf == min(kWalkC, ngr - q0)) {
       q0 = q;
@@ -2054,6 +2076,8 @@ __global__ __launch_bounds__(kSmT) void k_sq_small(const float4* __restrict__ x,
     while (l0 < b1) {
       const int lf = spec_walk<Leaf>(sv, W.lf + l0, b1 - l0, kLeafM);
       const int bl = l0 + lf;
+      nlt += min(lf + 1, b1 - l0);
+      nlh += lf;
       if (bl >= b1) break;
       if (lf == min(kWalkC, b1 - l0)) {
         l0 = bl;
@@ -2063,9 +2087,19 @@ __global__ __launch_bounds__(kSmT) void k_sq_small(const float4* __restrict__ x,
       const int ea = __builtin_amdgcn_readfirstlane(W.bst[bl]);
       const int ln = __builtin_amdgcn_readfirstlane(W.bst[bl + 1]) - ea;
       serial_adds_sm(sv, W, ea, ln);
+      ++nser;
       l0 = bl + 1;
     }
     q0 = q + 1;
+  }
+  mark(5);
+  if (stm) {
+    stats[8] = ngt;
+    stats[9] = ngh;
+    stats[10] = nlt;
+    stats[11] = nlh;
+    stats[12] = nser;
+    stats[13] = ngr;
   }
   if (lane == 0) {
     out[c] = sv;
@@ -2251,7 +2285,7 @@ int seqsum_enqueue(const float4* d_x, int64_t n, int nch, void* ws, float* d_out
     return RST_OK;
   }
   if (whole && n <= kSmallMax && ((stages & kSqForceSmall) || (!forced && n <= small_max()))) {
-    k_sq_small<<<nch, kSmT, 0, st>>>(d_x, n, nch, stretch ? stretch->p0 : nullptr, s0, d_out, d_guard);
+    k_sq_small<<<nch, kSmT, 0, st>>>(d_x, n, nch, stretch ? stretch->p0 : nullptr, s0, d_out, d_guard, d_stats);
     RST_HIP(hipGetLastError());
     return RST_OK;
   }

@@ -247,6 +247,7 @@ int compact(rst_ctx* ctx, const float* d_xyz, int64_t n, int mode, const uint8_t
 // (both size_t(k)), Boost <= 1.80's classic form (oracle/rst_oracle_umap.cpp
 // pins the model against a real std::unordered_map, tests/test_oracle.py).
 constexpr int kUmapT = 1024;
+constexpr int kUmapIl = 4;  // elements per thread with their loads interleaved
 constexpr int kUmapMaxLevels = 48;
 struct UmapSched {
   int nl;
@@ -349,26 +350,65 @@ __global__ __launch_bounds__(kUmapT) void k_umap_order(const float* __restrict__
     for (int64_t b = t; b < B; b += kUmapT) st(w.start + b, ld(w.cnt + b));
     __syncthreads();
     wg_scan(w.start, B, false, part);
-    for (int64_t e = t; e < nl; e += kUmapT) {
-      const int32_t b = ld(w.bk + e), a = ld(w.arr + e);
-      const int32_t slot = ld(w.start + b) + atomicAdd(w.fill + b, 1);
-      st(w.mem + slot, (int32_t)e);
-      if (a == ld(w.ctime + b)) st(w.hs + a, ld(w.cnt + b));
+    for (int64_t e0 = t; e0 < nl; e0 += (int64_t)kUmapIl * kUmapT) {  // (interleaved as below)
+      int32_t b[kUmapIl], a[kUmapIl], sl[kUmapIl], ct[kUmapIl], cn[kUmapIl];
+#pragma unroll
+      for (int u = 0; u < kUmapIl; ++u) {
+        const int64_t e = e0 + (int64_t)u * kUmapT;
+        b[u] = e < nl ? ld(w.bk + e) : -1;
+        a[u] = e < nl ? ld(w.arr + e) : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < kUmapIl; ++u) {
+        sl[u] = b[u] >= 0 ? ld(w.start + b[u]) + atomicAdd(w.fill + b[u], 1) : 0;
+        ct[u] = b[u] >= 0 ? ld(w.ctime + b[u]) : -1;
+        cn[u] = b[u] >= 0 ? ld(w.cnt + b[u]) : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < kUmapIl; ++u) {
+        if (b[u] < 0) continue;
+        st(w.mem + sl[u], (int32_t)(e0 + (int64_t)u * kUmapT));
+        if (a[u] == ct[u]) st(w.hs + a[u], cn[u]);
+      }
     }
     __syncthreads();
     // hs[a] = the elements of buckets created after arrival a: a run's start
     wg_scan(w.hs, nl, true, part);
-    // each bucket's members by arrival, descending, from its run's start
-    for (int64_t b = t; b < B; b += kUmapT) {
-      const int32_t c = ld(w.cnt + b);
-      if (c == 0) continue;
-      const int32_t s0 = ld(w.start + b), base = ld(w.hs + ld(w.ctime + b));
-      for (int32_t i = 0; i < c; ++i) {
-        const int32_t ei = ld(w.mem + s0 + i), ai = ld(w.arr + ei);
-        int32_t rank = 0;  // members arriving later come first
-        for (int32_t j = 0; j < c; ++j) rank += ld(w.arr + ld(w.mem + s0 + j)) > ai ? 1 : 0;
-        st(w.pos + ei, base + rank);
+    // each element's place: its bucket's run start plus the members of its
+    // bucket arriving later (they come first).  Per element, kUmapIl of
+    // them interleaved so their dependent loads overlap (r10b: a loop over
+    // the buckets -- most empty -- walked one L2 round trip after another,
+    // ~60 us a rehash level at 15k keys)
+    for (int64_t e0 = t; e0 < nl; e0 += (int64_t)kUmapIl * kUmapT) {
+      int32_t b[kUmapIl], a[kUmapIl], c[kUmapIl], s0[kUmapIl], ct[kUmapIl], rank[kUmapIl];
+      bool ok[kUmapIl];
+#pragma unroll
+      for (int u = 0; u < kUmapIl; ++u) {
+        const int64_t e = e0 + (int64_t)u * kUmapT;
+        ok[u] = e < nl;
+        b[u] = ok[u] ? ld(w.bk + e) : 0;
+        a[u] = ok[u] ? ld(w.arr + e) : 0;
       }
+#pragma unroll
+      for (int u = 0; u < kUmapIl; ++u) {
+        c[u] = ok[u] ? ld(w.cnt + b[u]) : 0;
+        s0[u] = ok[u] ? ld(w.start + b[u]) : 0;
+        ct[u] = ok[u] ? ld(w.ctime + b[u]) : 0;
+        rank[u] = 0;
+      }
+      int cm = 0;
+#pragma unroll
+      for (int u = 0; u < kUmapIl; ++u) cm = max(cm, c[u]);
+      for (int32_t j = 0; j < cm; ++j) {
+        int32_t m[kUmapIl];
+#pragma unroll
+        for (int u = 0; u < kUmapIl; ++u) m[u] = j < c[u] ? ld(w.mem + s0[u] + j) : -1;
+#pragma unroll
+        for (int u = 0; u < kUmapIl; ++u) rank[u] += (m[u] >= 0 && ld(w.arr + m[u]) > a[u]) ? 1 : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < kUmapIl; ++u)
+        if (ok[u]) st(w.pos + e0 + (int64_t)u * kUmapT, ld(w.hs + ct[u]) + rank[u]);
     }
     __syncthreads();
   }

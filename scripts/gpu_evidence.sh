@@ -19,7 +19,7 @@ step() {  # name, limit, command...
 }
 SHORT="--steps 6 --warmup 1 --no-cpu --no-p2plane --no-host-api --no-gicp --ref-steps 0"
 PMCB="--steps 6 --warmup 1 --batch 8 --inflight 1 --no-cpu --no-p2plane --no-host-api --no-gicp --ref-steps 0"
-step pytest_gpu 600 python -u -m pytest tests/ -x -v -m gpu --timeout 120 --timeout-method thread
+step pytest_gpu 900 python -u -m pytest tests/ -x -v -m gpu --timeout 300 --timeout-method thread
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 # the PMC passes first, so that the bench line below carries this build's
 # traffic (bench.py reads profiles/pmc_*.json; the copy stays on the box)
@@ -33,3 +33,7 @@ python3 scripts/profile_summary.py $(find gpurun_out/prof_${TAG} -name "*kernel_
 step iter 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/iter_${TAG} -o run -- python3 bench.py --batch 0 --inflight 1 $SHORT --steps 3
 python3 scripts/iter_profile_all.py $(find gpurun_out/iter_${TAG} -name "*kernel_trace.csv") > gpurun_out/${TAG}_iteration_profile.txt
 step diag 200 env RST_LIB=realsensetracker_amd/lib/variants/diag.so python tools/diag_fb.py
+# the reference callers' workload (~15k-point clouds), every kernel per iteration
+step callers 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/callers_${TAG} -o run -- python3 tools/callers_prof.py ref 3
+python3 scripts/iter_profile_all.py $(find gpurun_out/callers_${TAG} -name "*kernel_trace.csv") > gpurun_out/${TAG}_callers_iteration_profile.txt
+cp gpurun_out/${TAG}_callers.log gpurun_out/${TAG}_callers_pairs.txt
