@@ -268,66 +268,69 @@ __global__ __launch_bounds__(kBS) void k_normals(BvhView bv, int64_t m, float vx
 // point p are found in a pixel window -- seeded by the 5 x 5 pixels around
 // p's own (their K-th nearest bounds the K-th distance), then the window of
 // that ball (pix_window: every target point within the radius projects
-// inside it) scanned for the rest.  Candidates are ranked by (d2, original
-// index) as the BVH search ranks them, so the K nearest -- and the normal --
-// are the same bits; a ball whose window is too wide (depth edges, too few
-// seeds) takes the BVH search.  r09: the BVH search per lane, 1.2 ms a
-// 640x480 frame.
-constexpr int kKnnSeedR = 2;          // the seed: (2 r + 1)^2 pixels
-constexpr float kKnnMaxHalf = 8.0f;   // widest window scanned (level pixels)
+// inside it) scanned for the rest.  A 16 x 16 block of pixels stages its
+// tile and an 8-pixel halo in LDS (one 16-byte load per pixel), so every
+// window up to 8 pixels is scanned from LDS.  Candidates are ranked by (d2,
+// original index) as the BVH search ranks them, so the K nearest -- and the
+// normal -- are the same bits; a ball whose window is wider (depth edges,
+// too few seeds) takes the BVH search.  r09: the BVH search per lane, 1.2 ms
+// a 640x480 frame; r10: the windows per lane from global memory, 0.87 ms.
+constexpr int kKnnT = 16;              // tile side (pixels)
+constexpr int kKnnHalo = 8;            // staged halo = the widest window scanned
+constexpr int kKnnTW = kKnnT + 2 * kKnnHalo;
+constexpr int kKnnSeedR = 2;           // the seed: (2 r + 1)^2 pixels
 template <int K>
-__global__ __launch_bounds__(kBS) void k_normals_grid(BvhView bv, PixView pv, int64_t m, float vx, float vy,
-                                                      float vz, float4* __restrict__ nrm) {
-  const int64_t i = blockIdx.x * (int64_t)kBS + threadIdx.x;
-  if (i >= m) return;
-  const float4 p = bv.pts[i];
+__global__ __launch_bounds__(kKnnT* kKnnT) void k_normals_grid(BvhView bv, PixView pv, float vx, float vy,
+                                                                float vz, float4* __restrict__ nrm) {
+  __shared__ float4 tile[kKnnTW * kKnnTW];
+  const int u0 = blockIdx.x * kKnnT - kKnnHalo, v0 = blockIdx.y * kKnnT - kKnnHalo;
+  for (int k = threadIdx.x; k < kKnnTW * kKnnTW; k += kKnnT * kKnnT) {
+    const int uu = u0 + k % kKnnTW, vv = v0 + k / kKnnTW;
+    tile[k] = (uu >= 0 && vv >= 0 && uu < pv.w && vv < pv.h) ? pv.pts[(int64_t)vv * pv.w + uu]
+                                                             : make_float4(NAN, NAN, NAN, 0.f);
+  }
+  __syncthreads();
+  const int lu = threadIdx.x % kKnnT, lv = threadIdx.x / kKnnT;
+  const int u = blockIdx.x * kKnnT + lu, v = blockIdx.y * kKnnT + lv;
+  if (u >= pv.w || v >= pv.h) return;
+  const int pos = pv.map[(int64_t)v * pv.w + u];
+  if (pos < 0) return;
+  const int tu = lu + kKnnHalo, tv = lv + kKnnHalo;  // the pixel in the tile
+  const float4 p = tile[tv * kKnnTW + tu];
   BestK<K> L;
   L.init();
   bool done = false;
-  if (p.z > 0.f) {
-    const float s = (float)pv.s;
-    const float iz = 1.0f / p.z;
-    const float u = (pv.fx * p.x * iz + pv.cx) / s, v = (pv.fy * p.y * iz + pv.cy) / s;
-    if (u > -1.f && v > -1.f && u < (float)pv.w && v < (float)pv.h) {
-      const int uc = (int)floorf(u + 0.5f), vc = (int)floorf(v + 0.5f);
-      // the seed pixels (an invalid pixel is NaN: its distance fails every test)
-      float4 sp[(2 * kKnnSeedR + 1) * (2 * kKnnSeedR + 1)];
 #pragma unroll
-      for (int k = 0; k < (2 * kKnnSeedR + 1) * (2 * kKnnSeedR + 1); ++k) {
-        const int uu = uc + k % (2 * kKnnSeedR + 1) - kKnnSeedR, vv = vc + k / (2 * kKnnSeedR + 1) - kKnnSeedR;
-        const bool in = uu >= 0 && vv >= 0 && uu < pv.w && vv < pv.h;
-        sp[k] = in ? pv.pts[(int64_t)vv * pv.w + uu] : make_float4(NAN, NAN, NAN, 0.f);
-      }
+  for (int k = 0; k < (2 * kKnnSeedR + 1) * (2 * kKnnSeedR + 1); ++k) {
+    const float4 q = tile[(tv + k / (2 * kKnnSeedR + 1) - kKnnSeedR) * kKnnTW + (tu + k % (2 * kKnnSeedR + 1) - kKnnSeedR)];
+    const float d = d2_ref(p.x, p.y, p.z, q.x, q.y, q.z);  // (NaN: no point)
+    if (d <= L.bound()) L.offer(d, f2i(q.w), kPosPending);
+  }
+  int a0, a1, b0, b1;
+  float rc;
+  if (pix_window(pv, p.x, p.y, p.z, L.bound(), (float)kKnnHalo, a0, a1, b0, b1, rc) && a0 >= u0 &&
+      a1 < u0 + kKnnTW && b0 >= v0 && b1 < v0 + kKnnTW) {
+    for (int b = b0; b <= b1; ++b) {
+      const float4* row = tile + (b - v0) * kKnnTW - u0;
+      const bool inrow = b >= v - kKnnSeedR && b <= v + kKnnSeedR;
+      for (int a = a0; a <= a1; a += 4) {
+        float4 t[4];
 #pragma unroll
-      for (int k = 0; k < (2 * kKnnSeedR + 1) * (2 * kKnnSeedR + 1); ++k) {
-        const float d = d2_ref(p.x, p.y, p.z, sp[k].x, sp[k].y, sp[k].z);
-        if (d <= L.bound()) L.offer(d, f2i(sp[k].w), kPosPending);
-      }
-      int a0, a1, b0, b1;
-      float rc;
-      if (pix_window(pv, p.x, p.y, p.z, L.bound(), kKnnMaxHalf, a0, a1, b0, b1, rc)) {
-        for (int b = b0; b <= b1; ++b) {
-          const bool inrow = b >= vc - kKnnSeedR && b <= vc + kKnnSeedR;
-          for (int a = a0; a <= a1; a += 4) {
-            float4 t[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const int aa = a + j;
-              const bool seen = inrow && aa >= uc - kKnnSeedR && aa <= uc + kKnnSeedR;  // (offered above)
-              t[j] = aa <= a1 && !seen ? pv.pts[(int64_t)b * pv.w + aa] : make_float4(NAN, NAN, NAN, 0.f);
-            }
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const float d = d2_ref(p.x, p.y, p.z, t[j].x, t[j].y, t[j].z);
-              if (d <= L.bound()) L.offer(d, f2i(t[j].w), kPosPending);
-            }
-          }
+        for (int j = 0; j < 4; ++j) {
+          const int aa = a + j;
+          const bool seen = inrow && aa >= u - kKnnSeedR && aa <= u + kKnnSeedR;  // (offered above)
+          t[j] = aa <= a1 && !seen ? row[aa] : make_float4(NAN, NAN, NAN, 0.f);
         }
-        // every one of the K within the covered radius (always, the seeds
-        // being inside it; checked anyway)
-        done = L.pos[K - 1] >= 0 && margin_sqrt(L.bound()) * 1.00001f + 1e-30f < rc;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float d = d2_ref(p.x, p.y, p.z, t[j].x, t[j].y, t[j].z);
+          if (d <= L.bound()) L.offer(d, f2i(t[j].w), kPosPending);
+        }
       }
     }
+    // every one of the K within the covered radius (always, the seeds being
+    // inside it; checked anyway)
+    done = L.pos[K - 1] >= 0 && margin_sqrt(L.bound()) * 1.00001f + 1e-30f < rc;
   }
   if (done) {
 #pragma unroll
@@ -336,9 +339,9 @@ __global__ __launch_bounds__(kBS) void k_normals_grid(BvhView bv, PixView pv, in
   }
   if (!done) {  // the BVH search from the point's own leaf
     L.init();
-    search(bv, (int)i, p.x, p.y, p.z, L);
+    search(bv, pos, p.x, p.y, p.z, L);
   }
-  nrm[i] = knn_normal<K>(bv, L, p, vx, vy, vz);
+  nrm[pos] = knn_normal<K>(bv, L, p, vx, vy, vz);
 }
 
 // Image-grid normals (the point-to-plane perf mode; the reference's
@@ -519,7 +522,8 @@ int compute_normals(rst_ctx* ctx, rst_target* tgt, int k, const float vp[3]) {
     return !e || atoi(e) != 0;
   }();
   if (tgt->pix.map && grid_ok && k == 16)
-    k_normals_grid<16><<<blocks_for(tgt->m), kBS, 0, st>>>(v, tgt->pix, tgt->m, x, y, z, tgt->nrm);
+    k_normals_grid<16><<<dim3((tgt->pix.w + kKnnT - 1) / kKnnT, (tgt->pix.h + kKnnT - 1) / kKnnT),
+                         kKnnT * kKnnT, 0, st>>>(v, tgt->pix, x, y, z, tgt->nrm);
   else if (k == 8)
     k_normals<8><<<blocks_for(tgt->m), kBS, 0, st>>>(v, tgt->m, x, y, z, tgt->nrm);
   else if (k == 16)
