@@ -406,6 +406,9 @@ def main():
                     help="frame pairs per batched align (rst_icp_align_batch_async: one launch of "
                          "each loop kernel for the whole batch, r06h: 8 x 4 in flight 23.0k it/s "
                          "vs 15.1k for 24 single aligns); 0 = one pair per align")
+    ap.add_argument("--prep-threads", type=int, default=3,
+                    help="frame-preparation contexts / host threads of the batched legs (each "
+                         "frame's unproject + index build is host-synchronous; r10 one context)")
     ap.add_argument("--roof-steps", type=int, default=4,
                     help="frames of the one-pair-in-flight kernel timing pass (roofline; "
                          "batched: the value leg's --steps pairs, one batch in flight)")
@@ -477,6 +480,16 @@ def main():
     # of independent pairs overlap on the GPU
     pctx = A.Context(local)
     actx = [A.Context(local) for _ in range(max(1, a.inflight))]
+    # frame preparation (unproject + index build, host-synchronous per frame)
+    # on --prep-threads contexts and host threads, so a batch's frames are
+    # prepared in parallel and ahead of the aligns that use them
+    import queue
+    from concurrent.futures import ThreadPoolExecutor
+    prep_ctxs = [pctx] + [A.Context(local) for _ in range(max(0, a.prep_threads - 1))]
+    prep_free: "queue.Queue" = queue.Queue()
+    for c_ in prep_ctxs:
+        prep_free.put(c_)
+    prep_pool = ThreadPoolExecutor(max_workers=len(prep_ctxs))
 
     def run(nsteps: int, opts, normals_k: int, stats: dict | None, ctxs=None):
         ctxs = ctxs or actx
@@ -537,8 +550,15 @@ def main():
         # each loop kernel covers the batch); len(ctxs) batches in flight
         pending = deque()
 
-        def prep(f):
-            return A.Target.from_depth_device(d_depth[f].value, K, normals_k, pctx)
+        def prep_job(f):  # on a free preparation context (one thread each)
+            pc = prep_free.get()
+            try:
+                return A.Target.from_depth_device(d_depth[f].value, K, normals_k, pc)
+            finally:
+                prep_free.put(pc)
+
+        def submit(k0, nb):  # the frames of a batch, prepared in parallel
+            return [prep_pool.submit(prep_job, pingpong(k0 + j, nfr)) for j in range(nb)]
 
         def finish_one():
             pb, c, curs, prevs = pending.popleft()
@@ -562,17 +582,21 @@ def main():
             for tg in prevs:  # each a target here and a source of a finished pair
                 tg.free()
 
-        prev = prep(0)
+        prev = prep_job(0)
         k, s, nbatch = 1, 0, 0
+        futs = submit(k, min(B, nsteps))
         while s < nsteps:
             nb = min(B, nsteps - s)
             curs, prevs = [], []
-            for _ in range(nb):
-                cur = prep(pingpong(k, nfr))
+            for fu in futs:
+                cur = fu.result()
                 curs.append(cur)
                 prevs.append(prev)
                 prev = cur
                 k += 1
+            # the next batch's frames are prepared (other streams, host threads)
+            # while this thread waits for the GPU below
+            futs = submit(k, min(B, nsteps - s - nb)) if s + nb < nsteps else []
             if len(pending) == len(ctxs):
                 finish_one()
             c = ctxs[nbatch % len(ctxs)]
@@ -597,7 +621,7 @@ def main():
             c.enable_kernel_timing(0 if a.graphs else int(on))
 
     def sync_all():
-        for c in [pctx] + actx:
+        for c in prep_ctxs + actx:
             c.synchronize()
 
     # ---- throughput mode (value): no events in the timed region -----------------
