@@ -495,11 +495,16 @@ def main():
         ctxs = ctxs or actx
         pending = deque()
 
-        def prep(f):  # frame -> its level targets (one level unless pyramid)
-            if pyr:
-                return A.Target.pyramid_from_depth_device(d_depth[f].value, K, a.levels,
-                                                          normals_k, pctx)
-            return [A.Target.from_depth_device(d_depth[f].value, K, normals_k, pctx)]
+        def prep(f):  # frame -> its level targets (one level unless pyramid), on a
+            # free preparation context (one host thread each)
+            pc = prep_free.get()
+            try:
+                if pyr:
+                    return A.Target.pyramid_from_depth_device(d_depth[f].value, K, a.levels,
+                                                              normals_k, pc)
+                return [A.Target.from_depth_device(d_depth[f].value, K, normals_k, pc)]
+            finally:
+                prep_free.put(pc)
 
         def finish_one():
             pa, c, cur, tgt = pending.popleft()
@@ -527,8 +532,13 @@ def main():
         lv_iters = pyr_iters if opts.mode == L.RST_P2POINT_REF else [opts.max_iter] * a.levels
         prev = prep(0)
         k = 1
+        # the frames of the next steps prepared ahead, in parallel
+        ahead = deque(prep_pool.submit(prep, pingpong(1 + j, nfr))
+                      for j in range(min(len(prep_ctxs), nsteps)))
         for s in range(nsteps):
-            cur = prep(pingpong(k, nfr))
+            cur = ahead.popleft().result()
+            if s + len(ahead) + 1 < nsteps:
+                ahead.append(prep_pool.submit(prep, pingpong(s + len(ahead) + 2, nfr)))
             if len(pending) == len(ctxs):
                 finish_one()
             c = ctxs[s % len(ctxs)]

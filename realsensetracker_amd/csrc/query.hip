@@ -265,7 +265,7 @@ __global__ __launch_bounds__(kBS) void k_normals(BvhView bv, int64_t m, float vx
 // ComputeNormals' exact kNN through a frame target's pixel grid (the
 // reference's kd-tree search, kdtree.hpp:51-57, k = 16 at its call sites):
 // every point of a frame lies on the ray of its pixel, so the K nearest of
-// point p are found in a pixel window -- seeded by the 5 x 5 pixels around
+// point p are found in a pixel window -- seeded by the 7 x 7 pixels around
 // p's own (their K-th nearest bounds the K-th distance), then the window of
 // that ball (pix_window: every target point within the radius projects
 // inside it) scanned for the rest.  A 16 x 16 block of pixels stages its
@@ -278,7 +278,8 @@ __global__ __launch_bounds__(kBS) void k_normals(BvhView bv, int64_t m, float vx
 constexpr int kKnnT = 16;              // tile side (pixels)
 constexpr int kKnnHalo = 8;            // staged halo = the widest window scanned
 constexpr int kKnnTW = kKnnT + 2 * kKnnHalo;
-constexpr int kKnnSeedR = 2;           // the seed: (2 r + 1)^2 pixels
+constexpr int kKnnSeedR = 3;           // the seed: (2 r + 1)^2 pixels (7 x 7: beside a depth edge
+                                       // ~half of them lie on the point's own surface, enough for 16)
 template <int K>
 __global__ __launch_bounds__(kKnnT* kKnnT) void k_normals_grid(BvhView bv, PixView pv, float vx, float vy,
                                                                 float vz, float4* __restrict__ nrm) {
