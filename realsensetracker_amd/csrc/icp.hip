@@ -91,7 +91,7 @@ constexpr int kPixChunk = RST_PIX_CHUNK;
 #define RST_SQ_FUSE_FROM 0  // ... from this iteration on only (0: never; RST_SQ_FUSE_FROM env overrides), once the pose barely moves
 #endif
 #ifndef RST_PIX_COLD_ITERS
-#define RST_PIX_COLD_ITERS 4  // iterations [1, RST_PIX_COLD_ITERS) take the cold windows below (r04a: 4 vs 3, +1.6 %)
+#define RST_PIX_COLD_ITERS 8  // iterations [1, RST_PIX_COLD_ITERS) take the cold windows below (r04a: 4 vs 3, +1.6 %; r10g: 8 vs 4 27.6k vs 27.2k, 6 27.4k)
 #endif
 #ifndef RST_PIX_MAX_HALF_REF
 #define RST_PIX_MAX_HALF_REF 4.0f  // RST_SUM_REF's k_icp_nn window cap (level pixels; RST_PIX_MAX_HALF elsewhere)

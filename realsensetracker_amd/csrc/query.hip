@@ -282,7 +282,8 @@ constexpr int kKnnSeedR = 3;           // the seed: (2 r + 1)^2 pixels (7 x 7: b
                                        // ~half of them lie on the point's own surface, enough for 16)
 template <int K>
 __global__ __launch_bounds__(kKnnT* kKnnT) void k_normals_grid(BvhView bv, PixView pv, float vx, float vy,
-                                                                float vz, float4* __restrict__ nrm) {
+                                                                float vz, float4* __restrict__ nrm,
+                                                                int32_t* __restrict__ fbq) {
   __shared__ float4 tile[kKnnTW * kKnnTW];
   const int u0 = blockIdx.x * kKnnT - kKnnHalo, v0 = blockIdx.y * kKnnT - kKnnHalo;
   for (int k = threadIdx.x; k < kKnnTW * kKnnTW; k += kKnnT * kKnnT) {
@@ -338,11 +339,44 @@ __global__ __launch_bounds__(kKnnT* kKnnT) void k_normals_grid(BvhView bv, PixVi
     for (int j = 0; j < K; ++j) L.pos[j] = (uint32_t)L.id[j] < (uint32_t)bv.m ? pv.inv[L.id[j]] : -1;
     done = L.pos[K - 1] >= 0;
   }
-  if (!done) {  // the BVH search from the point's own leaf
-    L.init();
-    search(bv, pos, p.x, p.y, p.z, L);
+  if (!done) {  // the BVH search, compacted into k_normals_queue (a wave here
+    // would wait on its slowest lane's search: r10g, 0.72 ms a frame),
+    // capped by the seeds' K-th distance (no point beyond it can be among
+    // the K nearest: r10g, uncapped, ~1 ms for a few thousand points)
+    const int at = atomicAdd(fbq, 1);
+    fbq[2 + 2 * at] = pos;
+    fbq[3 + 2 * at] = __float_as_int(L.bound());
+    return;
   }
   nrm[pos] = knn_normal<K>(bv, L, p, vx, vy, vz);
+}
+
+// The K nearest within d2 <= cap (the caller knows K points within it, so
+// the K nearest are among them): the BVH walk prunes every box beyond it.
+template <int K>
+struct BestKCap {
+  BestK<K> L;
+  float cap;
+  RST_HD float bound() const { return fminf(cap, L.bound()); }
+  RST_HD void offer(float nd, int nid, int np) {
+    if (nd <= cap) L.offer(nd, nid, np);
+  }
+};
+
+// the grid search's leftovers: the BVH search from the point's own leaf
+template <int K>
+__global__ __launch_bounds__(kBS) void k_normals_queue(BvhView bv, const int32_t* __restrict__ fbq, float vx,
+                                                       float vy, float vz, float4* __restrict__ nrm) {
+  const int j = blockIdx.x * kBS + threadIdx.x;
+  if (j >= fbq[0]) return;
+  const int pos = fbq[2 + 2 * j];
+  if ((uint32_t)pos >= (uint32_t)bv.m) return;
+  const float4 p = bv.pts[pos];
+  BestKCap<K> R;
+  R.L.init();
+  R.cap = __int_as_float(fbq[3 + 2 * j]);  // (FLT_MAX: fewer than K seeds)
+  search(bv, pos, p.x, p.y, p.z, R);
+  nrm[pos] = knn_normal<K>(bv, R.L, p, vx, vy, vz);
 }
 
 // Image-grid normals (the point-to-plane perf mode; the reference's
@@ -522,10 +556,14 @@ int compute_normals(rst_ctx* ctx, rst_target* tgt, int k, const float vp[3]) {
     const char* e = getenv("RST_KNN_GRID");
     return !e || atoi(e) != 0;
   }();
-  if (tgt->pix.map && grid_ok && k == 16)
+  if (tgt->pix.map && grid_ok && k == 16) {
+    int32_t* fbq = nullptr;  // [count, positions...]
+    RST_CHECK(ctx_workspace(ctx, sizeof(int32_t) * (2 * (size_t)tgt->m + 64), (void**)&fbq));
+    RST_HIP(hipMemsetAsync(fbq, 0, sizeof(int32_t), st));
     k_normals_grid<16><<<dim3((tgt->pix.w + kKnnT - 1) / kKnnT, (tgt->pix.h + kKnnT - 1) / kKnnT),
-                         kKnnT * kKnnT, 0, st>>>(v, tgt->pix, x, y, z, tgt->nrm);
-  else if (k == 8)
+                         kKnnT * kKnnT, 0, st>>>(v, tgt->pix, x, y, z, tgt->nrm, fbq);
+    k_normals_queue<16><<<blocks_for(tgt->m), kBS, 0, st>>>(v, fbq, x, y, z, tgt->nrm);
+  } else if (k == 8)
     k_normals<8><<<blocks_for(tgt->m), kBS, 0, st>>>(v, tgt->m, x, y, z, tgt->nrm);
   else if (k == 16)
     k_normals<16><<<blocks_for(tgt->m), kBS, 0, st>>>(v, tgt->m, x, y, z, tgt->nrm);
