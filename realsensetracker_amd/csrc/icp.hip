@@ -93,6 +93,12 @@ constexpr int kPixChunk = RST_PIX_CHUNK;
 #ifndef RST_PIX_COLD_ITERS
 #define RST_PIX_COLD_ITERS 8  // iterations [1, RST_PIX_COLD_ITERS) take the cold windows below (r04a: 4 vs 3, +1.6 %; r10g: 8 vs 4 27.6k vs 27.2k, 6 27.4k)
 #endif
+#ifndef RST_SEED_SPARSE
+#define RST_SEED_SPARSE 0  // cold seeds: a (2R+1)^2 ring of pixel samples besides the 3x3 (proj_seed)
+#endif
+#ifndef RST_SEED_STRIDE
+#define RST_SEED_STRIDE 4
+#endif
 #ifndef RST_PIX_MAX_HALF_REF
 #define RST_PIX_MAX_HALF_REF 4.0f  // RST_SUM_REF's k_icp_nn window cap (level pixels; RST_PIX_MAX_HALF elsewhere)
 #endif
@@ -664,6 +670,32 @@ __device__ __forceinline__ void proj_seed(const BvhView& bv, const PixView& pv, 
       r.offer(d2_ref(x, y, z, w.x, w.y, w.z), f2i(w.w), c);
     }
   }
+#if RST_SEED_SPARSE
+  // Cold lanes only (iteration 0 / new lanes): a sparse ring of samples
+  // stride RST_SEED_STRIDE pixels apart out to RST_SEED_SPARSE strides, so
+  // that the seed -- the fallback's first ball -- already sits near the
+  // surface point a rotation of a few degrees moved the query onto.  Seeds
+  // only bound the search; the answer is the exact search's.
+  constexpr int R = RST_SEED_SPARSE, S = RST_SEED_STRIDE, D = 2 * R + 1;
+  for (int row = 0; row < D; ++row) {
+    const int vv = vc + (row - R) * S;
+    if (vv < 0 || vv >= pv.h) continue;
+    int cs[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      const int uu = uc + (k - R) * S;
+      cs[k] = (uu >= 0 && uu < pv.w) ? pv.map[(int64_t)vv * pv.w + uu] : -1;
+    }
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      const int c = cs[k];
+      if ((uint32_t)c < (uint32_t)bv.m) {
+        const float4 w = bv.pts[c];
+        r.offer(d2_ref(x, y, z, w.x, w.y, w.z), f2i(w.w), c);
+      }
+    }
+  }
+#endif
 }
 
 // Per source point the loop keeps its neighbour and certificate:

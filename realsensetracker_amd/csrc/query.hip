@@ -363,6 +363,156 @@ struct BestKCap {
   }
 };
 
+// The grid search's leftovers (~0.7% of a 640x480 frame: oblique surfaces
+// whose 7 x 7 seeds' K-th distance maps to a window just wider than the
+// staged halo -- median 10 pixels, the true K-th's 6), one wavefront each:
+// the window of the cap (<= kNwHalf pixels) scanned from global memory, 64
+// pixels a lane round, the candidates within the bound appended to an LDS
+// list; a list near full is cut to its K smallest (rank by counting,
+// ties by original index as BestK), which tightens the bound.  A cap whose
+// window is wider first scans the kNwProbe box around the point's pixel for
+// a bound.  Windows beyond that (isolated points: a few a frame) take lane
+// 0's BVH search, capped.  Same (d2, index) order, so the same K and the
+// same normal as k_normals.  r10h: the per-lane BVH search of the same
+// queue took 0.85 ms (its slowest lanes).
+#ifndef RST_KNN_WAVE
+#define RST_KNN_WAVE 1  // 0: the leftovers' per-lane BVH search (k_normals_queue)
+#endif
+constexpr int kNwCap = 192;  // list entries per wavefront (cut at > kNwCap - 64)
+constexpr int kNwHalf = 32;   // widest window scanned (pixels)
+constexpr int kNwProbe = 12;  // the probe box's half side (pixels)
+constexpr int kNwWaves = 4;
+
+template <int K>
+struct NwList {
+  float d[kNwCap];
+  int id[kNwCap];
+  float td[K];
+  int tid[K];
+};
+
+// cut the list to its K smallest (d, id), sorted; returns the new length
+template <int K>
+__device__ __forceinline__ int nw_select(NwList<K>& s, int n, int lane) {
+  for (int c = lane; c < n; c += kWave) {
+    const float dc = s.d[c];
+    const int ic = s.id[c];
+    int rank = 0;
+    for (int j = 0; j < n; ++j) rank += lex_less(s.d[j], s.id[j], dc, ic) ? 1 : 0;
+    if (rank < K) {
+      s.td[rank] = dc;
+      s.tid[rank] = ic;
+    }
+  }
+  wave_sync();
+  const int nk = min(n, K);
+  if (lane < nk) {
+    s.d[lane] = s.td[lane];
+    s.id[lane] = s.tid[lane];
+  }
+  wave_sync();
+  return nk;
+}
+
+// the pixels [a0, a1] x [b0, b1] into the list (candidates d2 <= *bound)
+template <int K>
+__device__ __forceinline__ int nw_scan(const PixView& pv, const float4& p, int a0, int a1, int b0, int b1,
+                                       NwList<K>& s, int n, float* bound, int lane) {
+  const int ww = a1 - a0 + 1, np = ww * (b1 - b0 + 1);
+  const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  for (int base = 0; base < np; base += 4 * kWave) {
+    float4 t[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {  // four loads in flight per lane
+      const int k = base + j * kWave + lane;
+      t[j] = k < np ? pv.pts[(int64_t)(b0 + k / ww) * pv.w + (a0 + k % ww)] : make_float4(NAN, NAN, NAN, 0.f);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float d = d2_ref(p.x, p.y, p.z, t[j].x, t[j].y, t[j].z);  // (NaN: no point)
+      const bool in = d <= *bound;
+      const uint64_t m = __ballot(in);
+      if (in) {
+        const int at = n + __popcll(m & lt);
+        s.d[at] = d;
+        s.id[at] = f2i(t[j].w);
+      }
+      n += __popcll(m);
+      if (n > kNwCap - kWave) {  // (uniform)
+        wave_sync();
+        n = nw_select<K>(s, n, lane);
+        if (n == K) *bound = s.d[K - 1];
+      }
+    }
+  }
+  wave_sync();
+  return n;
+}
+
+template <int K>
+__global__ __launch_bounds__(kWave* kNwWaves) void k_normals_wave(BvhView bv, PixView pv,
+                                                                   const int32_t* __restrict__ fbq, float vx,
+                                                                   float vy, float vz,
+                                                                   float4* __restrict__ nrm) {
+  __shared__ NwList<K> lists[kNwWaves];
+  const int w = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  NwList<K>& s = lists[w];
+  const int nq = fbq[0];
+  for (int j = blockIdx.x * kNwWaves + w; j < nq; j += gridDim.x * kNwWaves) {
+    const int pos = fbq[2 + 2 * j];
+    if ((uint32_t)pos >= (uint32_t)bv.m) continue;  // (uniform)
+    const float4 p = bv.pts[pos];
+    float bound = __int_as_float(fbq[3 + 2 * j]);  // K points lie within it (FLT_MAX: unknown)
+    int a0, a1, b0, b1;
+    float rc;
+    bool win = pix_window(pv, p.x, p.y, p.z, bound, (float)kNwHalf, a0, a1, b0, b1, rc);
+    if (!win && p.z > 0.f) {  // a bound from the probe box
+      const float iz = 1.0f / p.z;
+      const int uc = (int)floorf((pv.fx * p.x * iz + pv.cx) / (float)pv.s + 0.5f);
+      const int vc = (int)floorf((pv.fy * p.y * iz + pv.cy) / (float)pv.s + 0.5f);
+      const int pa0 = max(0, uc - kNwProbe), pa1 = min(pv.w - 1, uc + kNwProbe);
+      const int pb0 = max(0, vc - kNwProbe), pb1 = min(pv.h - 1, vc + kNwProbe);
+      if (pa0 <= pa1 && pb0 <= pb1) {
+        const int n = nw_scan<K>(pv, p, pa0, pa1, pb0, pb1, s, 0, &bound, lane);
+        if (n >= K) {
+          nw_select<K>(s, n, lane);
+          bound = s.d[K - 1];
+        }
+        win = pix_window(pv, p.x, p.y, p.z, bound, (float)kNwHalf, a0, a1, b0, b1, rc);
+      }
+    }
+    bool done = false;
+    if (win) {
+      int n = nw_scan<K>(pv, p, a0, a1, b0, b1, s, 0, &bound, lane);
+      if (n >= K) {
+        n = nw_select<K>(s, n, lane);
+        done = margin_sqrt(s.d[K - 1]) * 1.00001f + 1e-30f < rc;
+      }
+    }
+    if (lane == 0) {
+      BestK<K> L;
+      if (done) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          L.d[k] = s.d[k];
+          L.id[k] = s.id[k];
+          L.pos[k] = (uint32_t)s.id[k] < (uint32_t)bv.m ? pv.inv[s.id[k]] : -1;
+        }
+        done = L.pos[K - 1] >= 0;
+      }
+      if (!done) {
+        BestKCap<K> R;
+        R.L.init();
+        R.cap = __int_as_float(fbq[3 + 2 * j]);
+        search(bv, pos, p.x, p.y, p.z, R);
+        L = R.L;
+      }
+      nrm[pos] = knn_normal<K>(bv, L, p, vx, vy, vz);
+    }
+    wave_sync();
+  }
+}
+
 // the grid search's leftovers: the BVH search from the point's own leaf
 template <int K>
 __global__ __launch_bounds__(kBS) void k_normals_queue(BvhView bv, const int32_t* __restrict__ fbq, float vx,
@@ -562,7 +712,11 @@ int compute_normals(rst_ctx* ctx, rst_target* tgt, int k, const float vp[3]) {
     RST_HIP(hipMemsetAsync(fbq, 0, sizeof(int32_t), st));
     k_normals_grid<16><<<dim3((tgt->pix.w + kKnnT - 1) / kKnnT, (tgt->pix.h + kKnnT - 1) / kKnnT),
                          kKnnT * kKnnT, 0, st>>>(v, tgt->pix, x, y, z, tgt->nrm, fbq);
+#if RST_KNN_WAVE
+    k_normals_wave<16><<<512, kWave * kNwWaves, 0, st>>>(v, tgt->pix, fbq, x, y, z, tgt->nrm);
+#else
     k_normals_queue<16><<<blocks_for(tgt->m), kBS, 0, st>>>(v, fbq, x, y, z, tgt->nrm);
+#endif
   } else if (k == 8)
     k_normals<8><<<blocks_for(tgt->m), kBS, 0, st>>>(v, tgt->m, x, y, z, tgt->nrm);
   else if (k == 16)
