@@ -94,7 +94,7 @@ constexpr int kPixChunk = RST_PIX_CHUNK;
 #define RST_PIX_COLD_ITERS 8  // iterations [1, RST_PIX_COLD_ITERS) take the cold windows below (r04a: 4 vs 3, +1.6 %; r10g: 8 vs 4 27.6k vs 27.2k, 6 27.4k)
 #endif
 #ifndef RST_SEED_SPARSE
-#define RST_SEED_SPARSE 0  // cold seeds: a (2R+1)^2 ring of pixel samples besides the 3x3 (proj_seed)
+#define RST_SEED_SPARSE 3  // cold seeds: a (2R+1)^2 ring of pixel samples besides the 3x3 (proj_seed; r11c: with the iteration-0 windows below 28.3k vs 27.7k it/s)
 #endif
 #ifndef RST_SEED_STRIDE
 #define RST_SEED_STRIDE 4
@@ -112,10 +112,10 @@ constexpr int kPixChunk = RST_PIX_CHUNK;
 #define RST_PIX_COLD_CHUNKS 6  // their staging rounds per wave
 #endif
 #ifndef RST_PIX_I0_HALF
-#define RST_PIX_I0_HALF 0.0f  // > 0: a pair's first iteration takes windows of this cap (level pixels)
+#define RST_PIX_I0_HALF 24.0f  // > 0: a pair's first iteration takes windows of this cap (level pixels; r11c: iteration 0 nn + fb 1,082 -> 825 us a pair, 16 / 20 px 1,120 / 837; without the sparse seeds no gain)
 #endif
 #ifndef RST_PIX_I0_CHUNKS
-#define RST_PIX_I0_CHUNKS 2  // ... over this many staging rounds per wave
+#define RST_PIX_I0_CHUNKS 12  // ... over this many staging rounds per wave
 #endif
 #ifndef RST_DIAG
 #define RST_DIAG 0  // 1: per-iteration certificate counters (rst_debug_queue_trace)
@@ -911,9 +911,10 @@ __device__ __forceinline__ void icp_nn_body(const BvhView& bv, const AdjView& av
     // a pair's iterations 1-3: larger windows over more
     // staging rounds (the pose still moves by centimetres, beyond the steady
     // state's cap, which would queue them for k_icp_fb's per-lane searches).
-    // Not the first: its seeds are the projective / Morton guesses, and
-    // k_icp_fb's ball tiles answer that whole queue faster (r03u: 1.06 vs
-    // 1.97 ms; iterations 1-2 0.65 -> 0.23-0.38 ms)
+    // The first takes windows up to RST_PIX_I0_HALF pixels: its seeds, the
+    // sparse ring around the projection (proj_seed), lie within a few pixels
+    // of the neighbour (r03u, with 3 x 3 seeds only, k_icp_fb's ball tiles
+    // answered that whole queue faster: 1.06 vs 1.97 ms)
     const bool cold = st->iter >= 1 && st->iter < RST_PIX_COLD_ITERS;
     // (the REF loop's steady-state windows capped smaller: the pass waits on
     // its slowest wavefronts, whose few wide windows the queue's row

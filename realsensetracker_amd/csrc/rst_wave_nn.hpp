@@ -1286,6 +1286,12 @@ __device__ __forceinline__ bool ball_tile_search(const BvhView& bv, bool act, fl
 #ifndef RST_PIX_MAX_HALF
 #define RST_PIX_MAX_HALF 6.0f  // half-width cap of a lane's window (level pixels; r02: 6 -> 24.4k it/s, 8 -> 23.6k, 4 -> 22.9k)
 #endif
+#ifndef RST_RESEED_RING
+#define RST_RESEED_RING 0  // > 0: pix_seed_d2 also samples a (2R+1)^2 ring (below)
+#endif
+#ifndef RST_RESEED_STRIDE
+#define RST_RESEED_STRIDE 3
+#endif
 #ifndef RST_PIX_MIN_PX
 #define RST_PIX_MIN_PX 1.5f  // smallest window half-width: the certificate radius
 #endif
@@ -1364,6 +1370,24 @@ __device__ __forceinline__ float pix_seed_d2(const PixView& pv, float qx, float 
   float d = FLT_MAX;
 #pragma unroll
   for (int k = 0; k < 9; ++k) d = fminf(d, d2_ref(qx, qy, qz, p[k].x, p[k].y, p[k].z));  // NaN: skipped
+#if RST_RESEED_RING
+  // a sparse ring of samples RST_RESEED_STRIDE pixels apart out to
+  // RST_RESEED_RING strides (the pose moved by centimetres: the point's
+  // surface is a few pixels off its projection)
+  constexpr int R = RST_RESEED_RING, S = RST_RESEED_STRIDE, D = 2 * R + 1;
+  for (int row = 0; row < D; ++row) {
+    const int vv = vc + (row - R) * S;
+    if (vv < 0 || vv >= pv.h) continue;
+    float4 t[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      const int uu = uc + (k - R) * S;
+      t[k] = (uu >= 0 && uu < pv.w) ? pv.pts[(int64_t)vv * pv.w + uu] : make_float4(NAN, NAN, NAN, 0.f);
+    }
+#pragma unroll
+    for (int k = 0; k < D; ++k) d = fminf(d, d2_ref(qx, qy, qz, t[k].x, t[k].y, t[k].z));
+  }
+#endif
   return d;
 }
 
