@@ -420,6 +420,180 @@ __global__ __launch_bounds__(kUmapT) void k_umap_order(const float* __restrict__
   }
 }
 
+// The same replay for up to kUsMaxN keys (the reference callers' 5 cm
+// clouds, ~15k voxels), on one CU from LDS: per level a counting sort of
+// the elements by bucket (16-bit counts, two a word), each element's bucket
+// read from the sort -- its creation time (the members' least arrival), its
+// size, the element's rank (members arriving later) -- then one suffix scan
+// over arrivals for the runs' starts.  Every element stays with one thread
+// across the levels, its hash in registers; 11 levels at 15k keys with
+// LDS atomics and scans in place of k_umap_order's global round trips
+// (r10: ~570 us a call).
+constexpr int kUsT = 1024;
+constexpr int kUsMaxN = 16384;
+constexpr int kUsPer = kUsMaxN / kUsT;  // elements a thread
+constexpr int kUsMaxB = 20753;          // the schedule's last bucket count at kUsMaxN keys
+struct UsLds {
+  uint32_t cs[kUsMaxB / 2 + 2];  // bucket b's count, then start: half b & 1 of word b >> 1
+  int16_t bk[kUsMaxN];           // the element's bucket
+  int16_t arr[kUsMaxN];          // its arrival; at a level's end its place
+  int16_t mem[kUsMaxN];          // the buckets' members; then a creation arrival's run start
+  int part[kUsT / kWave + 1];
+};
+static_assert(sizeof(UsLds) <= 160 * 1024, "k_umap_small LDS");
+static_assert(kUsMaxN <= 32767, "16-bit arrivals");
+
+// exclusive scan of one int per thread over the workgroup; returns the total
+__device__ __forceinline__ int us_scan(int v, int* part, int& excl) {
+  const int t = threadIdx.x, lane = t & (kWave - 1), wv = t / kWave;
+  int inc = v;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const int y = __shfl_up(inc, o, kWave);
+    if (lane >= o) inc += y;
+  }
+  if (lane == kWave - 1) part[wv] = inc;
+  __syncthreads();
+  if (t < kWave) {
+    const int pv = t < kUsT / kWave ? part[t] : 0;
+    int pi = pv;
+#pragma unroll
+    for (int o = 1; o < kUsT / kWave; o <<= 1) {
+      const int y = __shfl_up(pi, o, kWave);
+      if (lane >= o) pi += y;
+    }
+    if (t < kUsT / kWave) part[t] = pi - pv;
+    if (t == kUsT / kWave - 1) part[kUsT / kWave] = pi;
+  }
+  __syncthreads();
+  excl = part[wv] + inc - v;
+  const int tot = part[kUsT / kWave];
+  __syncthreads();
+  return tot;
+}
+
+__device__ __forceinline__ int us_get(const uint32_t* cs, int b) { return (int)((cs[b >> 1] >> (16 * (b & 1))) & 0xffffu); }
+
+__global__ __launch_bounds__(kUsT) void k_umap_small(const float* __restrict__ pts, int n, float v, int kind,
+                                                    UmapSched sc, float* __restrict__ out) {
+  __shared__ UsLds W;
+  const int t = threadIdx.x;
+  uint64_t h[kUsPer];  // element t + j kUsT's hash
+#pragma unroll
+  for (int j = 0; j < kUsPer; ++j) {
+    const int e = t + j * kUsT;
+    h[j] = e < n ? boost_combine3(vox_of(pts, e, v, kind)) : 0;
+  }
+  for (int l = 0; l < sc.nl; ++l) {
+    const int r = (int)sc.r[l], B = (int)sc.B[l];
+    const int nl = l + 1 < sc.nl ? (int)sc.r[l + 1] : n;
+    const int nw = B / 2 + 1;
+    for (int k = t; k < nw; k += kUsT) W.cs[k] = 0;
+    __syncthreads();
+    // arrivals (the walked list's place, kept from the last level, or the
+    // insertion index) and buckets; the buckets' counts
+#pragma unroll
+    for (int j = 0; j < kUsPer; ++j) {
+      const int e = t + j * kUsT;
+      if (e < nl) {
+        const int b = (int)(h[j] % (uint64_t)B);
+        W.bk[e] = (int16_t)b;
+        if (e >= r) W.arr[e] = (int16_t)e;
+        atomicAdd(&W.cs[b >> 1], 1u << (16 * (b & 1)));
+      }
+    }
+    __syncthreads();
+    // the counts -> the buckets' starts (thread t: words [t per, (t + 1) per))
+    {
+      const int per = (nw + kUsT - 1) / kUsT;
+      const int w0 = min(nw, t * per), w1 = min(nw, w0 + per);
+      int sum = 0;
+      for (int k = w0; k < w1; ++k) sum += (int)(W.cs[k] & 0xffffu) + (int)(W.cs[k] >> 16);
+      int run;
+      us_scan(sum, W.part, run);
+      for (int k = w0; k < w1; ++k) {
+        const uint32_t c = W.cs[k];
+        const int lo = run;
+        run += (int)(c & 0xffffu);
+        W.cs[k] = (uint32_t)lo | ((uint32_t)run << 16);
+        run += (int)(c >> 16);
+      }
+    }
+    __syncthreads();
+    // members by bucket (each start advances to its bucket's end)
+#pragma unroll
+    for (int j = 0; j < kUsPer; ++j) {
+      const int e = t + j * kUsT;
+      if (e < nl) {
+        const int b = W.bk[e];
+        const uint32_t old = atomicAdd(&W.cs[b >> 1], 1u << (16 * (b & 1)));
+        W.mem[(old >> (16 * (b & 1))) & 0xffffu] = (int16_t)e;
+      }
+    }
+    __syncthreads();
+    // per element: its bucket's creation, size, and the members after it
+    int rk[kUsPer], ct[kUsPer], sz[kUsPer];
+#pragma unroll
+    for (int j = 0; j < kUsPer; ++j) {
+      const int e = t + j * kUsT;
+      rk[j] = 0;
+      ct[j] = -1;
+      sz[j] = 0;
+      if (e < nl) {
+        const int b = W.bk[e];
+        const int end = us_get(W.cs, b), beg = b == 0 ? 0 : us_get(W.cs, b - 1);
+        const int a = W.arr[e];
+        int c = a, rr = 0;
+        for (int k = beg; k < end; ++k) {
+          const int am = W.arr[W.mem[k]];
+          rr += am > a ? 1 : 0;
+          c = min(c, am);
+        }
+        rk[j] = rr;
+        ct[j] = c;
+        sz[j] = end - beg;
+      }
+    }
+    __syncthreads();
+    // a run's start per creation arrival: the elements of buckets created later
+    for (int k = t; k < nl; k += kUsT) W.mem[k] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kUsPer; ++j) {
+      const int e = t + j * kUsT;
+      if (e < nl && ct[j] == W.arr[e]) W.mem[ct[j]] = (int16_t)sz[j];
+    }
+    __syncthreads();
+    {
+      // suffix form: thread t over arrivals [nl - (t + 1) per, nl - t per), descending
+      const int per = (nl + kUsT - 1) / kUsT;
+      const int i1 = max(0, nl - t * per), i0 = max(0, i1 - per);
+      int sum = 0;
+      for (int k = i0; k < i1; ++k) sum += W.mem[k];
+      int run;
+      us_scan(sum, W.part, run);
+      for (int k = i1 - 1; k >= i0; --k) {
+        const int c = W.mem[k];
+        W.mem[k] = (int16_t)run;
+        run += c;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kUsPer; ++j) {
+      const int e = t + j * kUsT;
+      if (e < nl) W.arr[e] = (int16_t)(W.mem[ct[j]] + rk[j]);
+    }
+    __syncthreads();
+  }
+  for (int e = t; e < n; e += kUsT) {
+    const int o = W.arr[e];
+    out[3 * o + 0] = pts[3 * e + 0];
+    out[3 * o + 1] = pts[3 * e + 1];
+    out[3 * o + 2] = pts[3 * e + 2];
+  }
+}
+
 // the rehash points of a default-constructed std::unordered_map receiving
 // n distinct keys one by one, from libstdc++'s own policy (max load 1, one
 // bucket before the first insert): (elements before the insert, new count)
@@ -450,6 +624,15 @@ int umap_order_device(rst_ctx* ctx, const float* d_pts, int64_t n, float v, int 
   UmapSched sc;
   RST_CHECK(umap_schedule(n, &sc));
   const int64_t bmax = sc.B[sc.nl - 1];
+  static const bool small_ok = [] {
+    const char* e = getenv("RST_UMAP_SMALL");
+    return !e || atoi(e) != 0;
+  }();
+  if (small_ok && n <= kUsMaxN && bmax <= kUsMaxB) {  // one CU, LDS (k_umap_small)
+    k_umap_small<<<1, kUsT, 0, ctx->stream>>>(d_pts, (int)n, v, kind, sc, d_out);
+    RST_HIP(hipGetLastError());
+    return RST_OK;
+  }
   const size_t bytes = sizeof(uint64_t) * n + sizeof(int32_t) * (6 * (size_t)n + 4 * (size_t)bmax) + 256;
   void* p = nullptr;
   size_t cls = 0;
