@@ -100,10 +100,10 @@ constexpr int kPixChunk = RST_PIX_CHUNK;
 #define RST_SEED_STRIDE 4
 #endif
 #ifndef RST_PIX_MAX_HALF_REF
-#define RST_PIX_MAX_HALF_REF 4.0f  // RST_SUM_REF's k_icp_nn window cap (level pixels; RST_PIX_MAX_HALF elsewhere)
+#define RST_PIX_MAX_HALF_REF 20.0f  // RST_SUM_REF's k_icp_nn window cap (level pixels; RST_PIX_MAX_HALF elsewhere; r11 ab1-ab6 sweep with 8 staging rounds: 4 28.2k, 8 29.2k, 12 30.0k, 16 30.8k, 20 31.1k, 24 31.1k, 32 30.7k it/s)
 #endif
 #ifndef RST_PIX_CHUNKS
-#define RST_PIX_CHUNKS 2  // staging rounds per wave of the steady-state pixel windows
+#define RST_PIX_CHUNKS 8  // staging rounds per wave of the steady-state pixel windows (r11: 2 -> 8 with the 20-pixel cap)
 #endif
 #ifndef RST_PIX_COLD_HALF
 #define RST_PIX_COLD_HALF 16.0f  // their half-width cap (level pixels)

@@ -1284,7 +1284,7 @@ __device__ __forceinline__ bool ball_tile_search(const BvhView& bv, bool act, fl
 // whose query lies within 2 r of the camera plane, and waves whose union
 // exceeds kPixMaxW x 8 chunks, are left to the BVH searches (false).
 #ifndef RST_PIX_MAX_HALF
-#define RST_PIX_MAX_HALF 6.0f  // half-width cap of a lane's window (level pixels; r02: 6 -> 24.4k it/s, 8 -> 23.6k, 4 -> 22.9k)
+#define RST_PIX_MAX_HALF 24.0f  // half-width cap of a lane's window (level pixels; r02: 6 -> 24.4k it/s, 8 -> 23.6k, 4 -> 22.9k; r11, the batched REF loop's k_icp_fb rows: 6 31.0k, 10 31.2k, 16 31.5k, 24 31.6k, 32 31.5k)
 #endif
 #ifndef RST_RESEED_RING
 #define RST_RESEED_RING 0  // > 0: pix_seed_d2 also samples a (2R+1)^2 ring (below)

@@ -19,6 +19,7 @@ import numpy as np
 
 
 def short(name):
+    name = name.replace("(anonymous namespace)::", "").replace("rst::", "")
     m = re.search(r"(k_\w+?)(<[^>(]*>)?\(", name)
     return (m.group(1) + (m.group(2) or "")) if m else name[:40]
 
