@@ -1,20 +1,19 @@
 """Benchmark: ICP iterations/s + frames/s on a 640x480 synthetic RGB-D stream
 (BASELINE.json metric, configs[1]).
 
-One step = one batch of --batch (8) incoming frames of the stream, fully on
+One step = one batch of --batch (12) incoming frames of the stream, fully on
 the GPU, per frame:
     u16 depth (already in HBM) -> unprojection -> Morton sort + BVH build
     (the frame's index, reused as the next pair's target)
     -> AlignIcp3d(curr, prev) with the reference's P2POINT_REF loop,
        128 fixed iterations (rs_replay_app.cpp:246-251),
-the batch's 8 frame pairs aligned in lockstep by one
+the batch's 12 frame pairs aligned in lockstep by one
 rst_icp_align_batch_async (--batch 0: a step is one frame pair, one align).
 value = ICP iterations/s over all ranks (pairs * 128 / time).  Frame
-preparation runs on its own HIP stream and --inflight frame pairs (default
-24 in the reference-rounding mode, 4 in the fp64 mode; 24 HIP hardware
-queues: --hw-queues) are aligned concurrently, each on its own
-context/stream: one pair's iteration chain is launch/latency-bound, so
-independent pairs overlap on the GPU.  A second timed loop runs the build's point-to-plane mode on the same
+preparation runs on --prep-threads contexts of its own, and --inflight
+batches (default 4; 24 HIP hardware queues: --hw-queues) are aligned
+concurrently, each on its own context/stream: one batch's iteration chain
+is latency-bound, so independent batches overlap on the GPU.  A second timed loop runs the build's point-to-plane mode on the same
 frames (reported as extra fields).
 
 The value line runs the drop-in default, RST_SUM_REF: the reference's
@@ -402,10 +401,11 @@ def main():
                     help="frame pairs in flight in the reference-rounding leg: its sequential "
                          "sums run one wavefront per component for most of an iteration, so "
                          "more pairs share the GPU")
-    ap.add_argument("--batch", type=int, default=8,
+    ap.add_argument("--batch", type=int, default=12,
                     help="frame pairs per batched align (rst_icp_align_batch_async: one launch of "
                          "each loop kernel for the whole batch, r06h: 8 x 4 in flight 23.0k it/s "
-                         "vs 15.1k for 24 single aligns); 0 = one pair per align")
+                         "vs 15.1k for 24 single aligns; r11 shape sweep, 480 pairs: 8 x 4 "
+                         "31.95k, 10 x 4 32.5k, 12 x 4 32.6k, 16 x 3 32.4k); 0 = one pair per align")
     ap.add_argument("--prep-threads", type=int, default=3,
                     help="frame-preparation contexts / host threads of the batched legs (each "
                          "frame's unproject + index build is host-synchronous; r10 one context)")
@@ -676,7 +676,7 @@ def main():
 
     # ---- point-to-plane mode (extra fields) ---------------------------------------
     def p2plane_leg(normals_k: int) -> dict:
-        # 4 aligns in flight, batched as the value leg (8 pairs each) unless
+        # 4 aligns in flight, batched as the value leg (--batch pairs each) unless
         # --batch 0: a ~7-iteration pair is bound by its frame's preparation,
         # which a deeper queue of aligns only delays
         pctxs = actx[:4]
