@@ -322,6 +322,7 @@ __device__ __forceinline__ Uni load_uni(const IcpState* __restrict__ st) {
   return u;
 }
 
+constexpr float kPixHalfLone = 4.0f, kRowHalfLone = 6.0f;  // window caps of a lone (sharded) align
 struct AccArgs {
   const float4* __restrict__ nrm;  // P2PLANE: target normals, sorted order
   float4* __restrict__ corr;       // RST_SUM_REF: (q, d2) per original source index
@@ -330,6 +331,8 @@ struct AccArgs {
   int32_t pos0;                    // sorted position of dst[0]
   int32_t full_from;               // RST_SUM_REF: from this iteration on every lane writes
                                    // its record (q, d2): the last one, whose cost chain reads d2
+  float pix_half;                  // > 0: k_icp_nn's steady-state window cap (level pixels),
+  float row_half;                  // k_icp_fb's rows' cap; 0: the build's (RST_PIX_MAX_HALF*)
 };
 
 // P2POINT_REF.  Single pass over the correspondences with the source
@@ -920,7 +923,8 @@ __device__ __forceinline__ void icp_nn_body(const BvhView& bv, const AdjView& av
     // its slowest wavefronts, whose few wide windows the queue's row
     // searches take in parallel instead; r04j: nn 35 -> 25 us, same
     // throughput.  The fp64 loop keeps the wider cap, r02's throughput best)
-    constexpr float kPixHalf = std::is_same<Acc, RefAcc>::value ? RST_PIX_MAX_HALF_REF : RST_PIX_MAX_HALF;
+    constexpr float kPixHalfDef = std::is_same<Acc, RefAcc>::value ? RST_PIX_MAX_HALF_REF : RST_PIX_MAX_HALF;
+    const float kPixHalf = aa.pix_half > 0.f ? aa.pix_half : kPixHalfDef;
     bool pok;
     if (RST_PIX_I0_HALF > 0.0f && st->iter == 0)  // (uniform)
       pok = pix_tile_search<kPixChunk, RST_PIX_I0_CHUNKS>(bv, pv, need, px, py, pz, d0, pr, pq, pscr[wid], prc,
@@ -1655,7 +1659,8 @@ __device__ __forceinline__ void icp_fb_body(const BvhView& bv, const AdjView& av
         const bool act = has && fin;
         // frame targets: the query's pixel window first (rows of 16 lanes)
         float rcp = 0.f;
-        const bool pe = RST_ROW_PIX && pv.map && row_pix(bv, pv, act, px, py, pz, r2, rcp);
+        const bool pe = RST_ROW_PIX && pv.map &&
+                        row_pix(bv, pv, act, px, py, pz, r2, rcp, aa.row_half > 0.f ? aa.row_half : RST_PIX_MAX_HALF);
         const float rc =
             row_adj2(bv, av, act && !pe, r2.pos[0], px, py, pz, r2, rtags[wid][lane >> 4]);
         if (pe) {
@@ -2101,6 +2106,12 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
   // (the last iteration's records all written: its cost chain reads d2;
   // every iteration's under the sums' trace)
   aa.full_from = ctx->seq_trace ? 0 : opts.max_iter - 1;
+  // the window caps: the build's wide ones pay where many aligns share the
+  // chip (batches, aligns in flight); a sharded align is one large pair alone,
+  // latency-bound, and takes the narrow ones (r11: the 1M pair 2,517 it/s with
+  // 4 / 6 pixels, 2,267 with 20 / 24)
+  aa.pix_half = comm ? kPixHalfLone : 0.f;
+  aa.row_half = comm ? kRowHalfLone : 0.f;
   const AdjView av = adj_of(tgt);
   const size_t fb_lds = 2 * sizeof(int) * ((size_t)nblk + 1);
 
@@ -2691,6 +2702,7 @@ int icp_debug_partials(rst_ctx* ctx, const rst_target* src, const rst_target* tg
   AccArgs aa;
   aa.corr = nullptr;
   aa.full_from = 0;
+  aa.pix_half = aa.row_half = 0.f;
   aa.nrm = tgt->nrm;
   aa.pmu = opts.p2plane_mu;
   aa.max_d2 = opts.p2plane_max_dist > 0 ? opts.p2plane_max_dist * opts.p2plane_max_dist : FLT_MAX;

@@ -1538,11 +1538,12 @@ __device__ __forceinline__ bool pix_tile_search(const BvhView& bv, const PixView
 // r holds the seeds (r.d[0] = the seed distance); on true r is the exact two
 // nearest within rc.  Whole rows call it (act uniform per row).
 __device__ __forceinline__ bool row_pix(const BvhView& bv, const PixView& pv, bool act, float qx,
-                                        float qy, float qz, Best2& r, float& rc) {
+                                        float qy, float qz, Best2& r, float& rc,
+                                        float maxh = RST_PIX_MAX_HALF) {
   const int sub = __lane_id() & 15;
   int a0 = 0, a1 = -1, b0 = 0, b1 = -1;
   rc = 0.f;
-  const bool ok = act && pix_window(pv, qx, qy, qz, r.d[0], RST_PIX_MAX_HALF, a0, a1, b0, b1, rc);
+  const bool ok = act && pix_window(pv, qx, qy, qz, r.d[0], maxh, a0, a1, b0, b1, rc);
   Best2 mine;
   mine.init();
   const int wa = a1 - a0 + 1;
