@@ -152,6 +152,7 @@ __device__ __forceinline__ int xcd_tile(int b, int nb) {
 constexpr int kFarBit = 1 << 29;
 constexpr int kPosMask = kFarBit - 1;
 constexpr int kFbBlocks = 2048;  // largest fallback grid (RST_FB_BLOCKS)
+constexpr int kFbBatchRef = 64;  // a batch's REF fallback grid per pair (fb_grid_batch_ref)
 constexpr int kFbDefault = 384;  // fallback grid (r02 sweep, pixel windows in k_icp_nn: 384 -> 26.2k it/s, 256 26.3k, 512 25.8k, 1024 23.5k; 720p 7.0k vs 6.4k, 720p pyramid 137 vs 130 frames/s)
 // From a queue of lane_min entries (IcpParams: the cold first iterations,
 // where most lanes' last neighbour is far or missing) kernel 2 finishes the
@@ -1929,6 +1930,20 @@ static int sq_fuse_from() {
   return g;
 }
 
+// a batch's RST_SUM_REF fallback grid per pair (RST_FB_BLOCKS_BATCH): RefAcc
+// folds no sums there, so the grid moves no bit, and the batch's pairs fill
+// the chip together (r11 sweep, 12-pair batches: 384 32.5k, 128 33.1k, 96
+// 33.3k, 64 33.5k it/s -- where one pair alone wants 384 or more: the
+// reference-shaped host API 29.8 ms a pair at 384, 48 at 128)
+static int fb_grid_batch_ref() {
+  static const int g = [] {
+    const char* e = getenv("RST_FB_BLOCKS_BATCH");
+    const int v = e ? atoi(e) : kFbBatchRef;
+    return (v >= 1 && v <= kFbBlocks) ? v : kFbBatchRef;
+  }();
+  return g;
+}
+
 static int fb_grid_size() {
   static const int g = [] {
     const char* e = getenv("RST_FB_BLOCKS");
@@ -2540,7 +2555,7 @@ int icp_launch_batch(rst_ctx* ctx, int nb, const rst_target* const* src, const r
       ctx->ev.push_back(e);
     }
   }
-  const dim3 gnn(nblk_max, 1, B), gfb(fb_grid, 1, B), gone(1, 1, B);
+  const dim3 gnn(nblk_max, 1, B), gfb(fb_grid, 1, B), gone(1, 1, B), gfb_ref(fb_grid_batch_ref(), 1, B);
   for (int it = 0; it < opts.max_iter; ++it) {
     const bool tm = timing && it % ctx->timing_stride == 0;
     auto mark = [&](int k) -> int {
@@ -2552,7 +2567,7 @@ int icp_launch_batch(rst_ctx* ctx, int nb, const rst_target* const* src, const r
       k_icp_nn_b<RefAcc><<<gnn, kBS, 0, st>>>(d_pa);
       RST_CHECK(mark(1));
       k_queue_prefix_b<<<gone, kBS, 0, st>>>(d_pa);
-      k_icp_fb_b<RefAcc><<<gfb, kBS, fb_lds, st>>>(d_pa);
+      k_icp_fb_b<RefAcc><<<gfb_ref, kBS, fb_lds, st>>>(d_pa);
       RST_CHECK(mark(2));
       RST_CHECK(seqsum_enqueue_batch(d_sq, B, nmax, it + 1 == opts.max_iter ? 4 : 3, it, st, it > 0 ? 3 : 0));
       k_cov_ref_b<<<dim3(kCovBlocks, 1, B), kBS, 0, st>>>(d_pa);
