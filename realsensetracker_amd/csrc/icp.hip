@@ -46,6 +46,9 @@ constexpr int kNP2Plane = 30;  // A (21), b (6), sum w r^2, count, sum d2
 #define RST_FB_MIN_WAVES 4  // k_icp_fb occupancy target (r01: 128 VGPRs, 4 waves/SIMD; r02: the kernel's paths need 201, the compiler settles at 2 waves/SIMD; forcing 3 spills: 22.8k vs 23.6k it/s)
 #endif
 constexpr int kCertBit = 1 << 30;
+#ifndef RST_FB_MIN_WAVES_REF
+#define RST_FB_MIN_WAVES_REF 3  // the REF loop's k_icp_fb (r11: 3 vs 4 waves/SIMD 33.8k vs 33.4k it/s batched; the fp64 loop 49.0k vs 50.0k, so it keeps 4)
+#endif
 #ifndef RST_COLD_FAST
 #define RST_COLD_FAST 1
 #endif
@@ -415,7 +418,7 @@ struct P2PlaneAcc {
 struct RefAcc {
   static constexpr int NV = 9;   // k_cov_ref's rows: the 3x3 covariance
   static constexpr int RS = 16;
-  static constexpr int kFbMinWaves = RST_FB_MIN_WAVES;
+  static constexpr int kFbMinWaves = RST_FB_MIN_WAVES_REF;
   static constexpr bool kPubPrefix = true;
   static constexpr bool kCanFinish = false;
   static constexpr bool kSums = false;
