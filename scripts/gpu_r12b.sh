@@ -1,0 +1,8 @@
+#!/bin/bash
+# shrinking pixel windows: GPU suite, then A/B against the fixed windows
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp GPU_MAX_HW_QUEUES=24
+timeout -k 10 900 python -u -m pytest tests/ -x -q -m gpu --timeout 300 --timeout-method thread > gpurun_out/r12b_tests.log 2>&1
+rc=$?; echo "tests rc=$rc"; tail -1 gpurun_out/r12b_tests.log; [ $rc -eq 0 ] || { grep -E "Error|assert|FAILED" gpurun_out/r12b_tests.log | head -20; exit $rc; }
+TAG=r12b VARIANTS="shr0" TESTS=tests/test_gpu_batch.py bash scripts/gpu_variants.sh
