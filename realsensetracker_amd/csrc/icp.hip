@@ -155,7 +155,8 @@ __device__ __forceinline__ int xcd_tile(int b, int nb) {
 constexpr int kFarBit = 1 << 29;
 constexpr int kPosMask = kFarBit - 1;
 constexpr int kFbBlocks = 2048;  // largest fallback grid (RST_FB_BLOCKS)
-constexpr int kFbBatchRef = 64;  // a batch's REF fallback grid per pair (fb_grid_batch_ref)
+constexpr int kFbBatchRef = 64;
+constexpr int kFbRefSingle = 1536;  // a single REF align's fallback grid (fb_grid_ref_single)  // a batch's REF fallback grid per pair (fb_grid_batch_ref)
 constexpr int kFbDefault = 384;  // fallback grid (r02 sweep, pixel windows in k_icp_nn: 384 -> 26.2k it/s, 256 26.3k, 512 25.8k, 1024 23.5k; 720p 7.0k vs 6.4k, 720p pyramid 137 vs 130 frames/s)
 // From a queue of lane_min entries (IcpParams: the cold first iterations,
 // where most lanes' last neighbour is far or missing) kernel 2 finishes the
@@ -1947,6 +1948,19 @@ static int fb_grid_batch_ref() {
   return g;
 }
 
+// a single REF align's fallback grid (RST_FB_BLOCKS_REF; RefAcc folds no sums,
+// so the grid moves no bit): one large pair alone wants every CU (r12 sweep,
+// the reference-shaped host API on 640x480 clouds: 384 blocks 29.8 ms a pair,
+// 768 26.6, 1024 25.8, 1536 25.4; the sharded 1M pair 2,651 -> 2,870 it/s)
+static int fb_grid_ref_single() {
+  static const int g = [] {
+    const char* e = getenv("RST_FB_BLOCKS_REF");
+    const int v = e ? atoi(e) : kFbRefSingle;
+    return (v >= 1 && v <= kFbBlocks) ? v : kFbRefSingle;
+  }();
+  return g;
+}
+
 static int fb_grid_size() {
   static const int g = [] {
     const char* e = getenv("RST_FB_BLOCKS");
@@ -2139,7 +2153,7 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
   // blocks scan the few queue counts themselves, no prefix launch (RefAcc:
   // no sums, results independent of the grid)
   const bool small_fb = refsum && n_local <= small_fb_n();
-  const int fb_grid_small = fb_grid;  // (r10c: 2 blocks per kernel-1 block, 231 vs 111 us a cold iteration)
+  const int fb_grid_small = fb_grid_ref_single();  // (r10c: 2 blocks per kernel-1 block, 231 vs 111 us a cold iteration)
 
   const BvhView bv = view_of(tgt);
   const bool timing = ctx->timing && opts.max_iter > 0;
@@ -2185,7 +2199,7 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
                                                                       prm.lane_min, slab, slab2, n_local);
         } else {
           k_queue_prefix<<<1, kBS, 0, st>>>(qcnt, nblk, ctx->d_state);
-          k_icp_fb<RefAcc><<<fb_grid, kBS, fb_lds, st>>>(bv, av, tgt->pix, aa, src->pts, ctx->d_state, nnq,
+          k_icp_fb<RefAcc><<<fb_grid_ref_single(), kBS, fb_lds, st>>>(bv, av, tgt->pix, aa, src->pts, ctx->d_state, nnq,
                                                          cert, qbuf, qcnt, nblk, prm.lane_min, slab, slab2,
                                                          n_local);
         }
