@@ -72,7 +72,7 @@ constexpr int kCertBit = 1 << 30;
 #define RST_PIX_ITERS (1 << 30)  // k_icp_nn's pixel windows in a pair's first iterations (r02: 24 -> 11.7 ms per pair alone vs 13.2, but 20.7k vs 23.6k it/s with 4 pairs in flight; default: all)
 #endif
 #ifndef RST_PIX_CHUNK
-#define RST_PIX_CHUNK 512  // pixels staged per wave and round (10 KB of LDS per wave; r02: 512 vs 256 same throughput, one pair 13.4 vs 13.9 ms)
+#define RST_PIX_CHUNK 384  // pixels staged per wave and round (6 KB of LDS per wave; r02: 512 vs 256 same throughput, one pair 13.4 vs 13.9 ms; r12: 384 with the 5-wave hint below, k_icp_nn at 24.6 KB of LDS and 96 VGPRs a block -- five waves a SIMD --, 33.9k -> 34.7k it/s, fp64 50.2k -> 52.3k)
 #endif
 constexpr int kPixChunk = RST_PIX_CHUNK;
 #ifndef RST_NN_COMPACT
@@ -85,7 +85,7 @@ constexpr int kPixChunk = RST_PIX_CHUNK;
 #define RST_NN_CLK_ITER 64
 #endif
 #ifndef RST_NN_MIN_WAVES
-#define RST_NN_MIN_WAVES 1  // k_icp_nn occupancy hint (waves per SIMD)
+#define RST_NN_MIN_WAVES 5  // k_icp_nn occupancy hint (waves per SIMD; 6 with 320-pixel chunks spilled: 32.9k)
 #endif
 #ifndef RST_SQ_FUSE_FRONT
 #define RST_SQ_FUSE_FRONT 0  // REF loop: the front kernel without the totals launch, the previous iteration's tile prefixes (r04b: front + totals 14.5 -> 13.3 us, but the walk +1 ms per pair: stale guesses in the first iterations)
@@ -106,19 +106,19 @@ constexpr int kPixChunk = RST_PIX_CHUNK;
 #define RST_PIX_MAX_HALF_REF 20.0f  // RST_SUM_REF's k_icp_nn window cap (level pixels; RST_PIX_MAX_HALF elsewhere; r11 ab1-ab6 sweep with 8 staging rounds: 4 28.2k, 8 29.2k, 12 30.0k, 16 30.8k, 20 31.1k, 24 31.1k, 32 30.7k it/s)
 #endif
 #ifndef RST_PIX_CHUNKS
-#define RST_PIX_CHUNKS 8  // staging rounds per wave of the steady-state pixel windows (r11: 2 -> 8 with the 20-pixel cap)
+#define RST_PIX_CHUNKS 11  // staging rounds per wave of the steady-state pixel windows (r11: 2 -> 8 with the 20-pixel cap; 11 at 384-pixel chunks)
 #endif
 #ifndef RST_PIX_COLD_HALF
 #define RST_PIX_COLD_HALF 16.0f  // their half-width cap (level pixels)
 #endif
 #ifndef RST_PIX_COLD_CHUNKS
-#define RST_PIX_COLD_CHUNKS 6  // their staging rounds per wave
+#define RST_PIX_COLD_CHUNKS 8  // their staging rounds per wave
 #endif
 #ifndef RST_PIX_I0_HALF
 #define RST_PIX_I0_HALF 24.0f  // > 0: a pair's first iteration takes windows of this cap (level pixels; r11c: iteration 0 nn + fb 1,082 -> 825 us a pair, 16 / 20 px 1,120 / 837; without the sparse seeds no gain)
 #endif
 #ifndef RST_PIX_I0_CHUNKS
-#define RST_PIX_I0_CHUNKS 12  // ... over this many staging rounds per wave
+#define RST_PIX_I0_CHUNKS 16  // ... over this many staging rounds per wave
 #endif
 #ifndef RST_DIAG
 #define RST_DIAG 0  // 1: per-iteration certificate counters (rst_debug_queue_trace)
