@@ -46,6 +46,10 @@ constexpr int kNP2Plane = 30;  // A (21), b (6), sum w r^2, count, sum d2
 #define RST_FB_MIN_WAVES 4  // k_icp_fb occupancy target (r01: 128 VGPRs, 4 waves/SIMD; r02: the kernel's paths need 201, the compiler settles at 2 waves/SIMD; forcing 3 spills: 22.8k vs 23.6k it/s)
 #endif
 constexpr int kCertBit = 1 << 30;
+#ifndef RST_BALL_CHUNK_REF
+#define RST_BALL_CHUNK_REF 256  // the REF loop's k_icp_fb ball-tile chunk (points): 25 KB less LDS a block (r12 A/B 34.6k -> 35.1k it/s; the fp64 loop at 256 lost 14%, so it keeps 512)
+#endif
+constexpr int kBallChunkDefault = 512;
 #ifndef RST_FB_MIN_WAVES_REF
 #define RST_FB_MIN_WAVES_REF 3  // the REF loop's k_icp_fb (r11: 3 vs 4 waves/SIMD 33.8k vs 33.4k it/s batched; the fp64 loop 49.0k vs 50.0k, so it keeps 4)
 #endif
@@ -349,6 +353,7 @@ struct P2PointAcc {
   static constexpr int NV = kNP2Point;  // sum w q u^T (9), sum w u (3), sum q (3), sum d2
   static constexpr int RS = 16;         // slab row stride (doubles; divides kRedBS)
   static constexpr int kFbMinWaves = RST_FB_MIN_WAVES;  // k_icp_fb occupancy
+  static constexpr int kBallChunk = kBallChunkDefault;
   static constexpr bool kPubPrefix = true;  // k_queue_prefix publishes the queues' prefixes
   static constexpr bool kCanFinish = false;
   static constexpr bool kSums = true;  // the search kernels write slab rows
@@ -379,6 +384,7 @@ struct P2PlaneAcc {
   static constexpr int NV = kNP2Plane;  // A (21), b (6), sum w r^2, count, sum d2
   static constexpr int RS = 32;
   static constexpr int kFbMinWaves = 1;
+  static constexpr int kBallChunk = kBallChunkDefault;
   static constexpr bool kPubPrefix = false;  // k_icp_fb scans the queue counts per block (see there)
   static constexpr bool kCanFinish = true;
   static constexpr bool kSums = true;
@@ -420,6 +426,7 @@ struct RefAcc {
   static constexpr int NV = 9;   // k_cov_ref's rows: the 3x3 covariance
   static constexpr int RS = 16;
   static constexpr int kFbMinWaves = RST_FB_MIN_WAVES_REF;
+  static constexpr int kBallChunk = RST_BALL_CHUNK_REF;  // k_icp_fb's ball-tile staging (points)
   static constexpr bool kPubPrefix = true;
   static constexpr bool kCanFinish = false;
   static constexpr bool kSums = false;
@@ -1493,9 +1500,10 @@ __device__ __forceinline__ void fb_record(double (&v)[Acc::NV], const BvhView& b
 }
 
 // per-wave LDS: the deep search's staging or the ball tiles (never both)
-union FbScratch {
+template <int C>
+union FbScratchT {
   WnnScratch w;
-  BallScratch b;
+  BallScratchT<C> b;
 };
 
 template <class Acc, bool PUB = Acc::kPubPrefix>
@@ -1515,7 +1523,7 @@ __device__ __forceinline__ void icp_fb_body(const BvhView& bv, const AdjView& av
   const int32_t* __restrict__ qcntf = qcnt + nb1;
   __shared__ double lds[(kBS / kWave) * Acc::NV];
   __shared__ int rtags[kBS / kWave][kWave / 16][kAdjK];  // row_adj2 candidates
-  __shared__ FbScratch scr[kBS / kWave];
+  __shared__ FbScratchT<Acc::kBallChunk> scr[kBS / kWave];
   __shared__ int4 left[kBS / kWave][kWave / 16];  // a round's leftovers (i, seeds)
   if (Acc::kCanFinish && st->done) return;  // converged: nothing reads the slabs
   // The queues' prefixes as k_queue_prefix published them (near [0, nb1],

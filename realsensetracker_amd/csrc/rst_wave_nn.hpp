@@ -1065,19 +1065,22 @@ __device__ __forceinline__ bool box_meets(const float4& lo, const float4& hi, fl
 // certificate.  Returns false (lanes keep a
 // valid but unfinished r) when the walk exceeds kBallMaxChunks chunks: the
 // caller finishes those lanes alone.
-constexpr int kBallChunk = 512;    // staged points per scan
+constexpr int kBallChunk = 512;    // staged points per scan (a loop's own choice: BallScratchT)
 constexpr int kBallLeaves = 128;   // collected leaves (a round adds <= 64)
 constexpr int kBallStack = 320;    // node ids
 #ifndef RST_BALL_MAX_CHUNKS
 #define RST_BALL_MAX_CHUNKS 48
 #endif
 constexpr int kBallMaxChunks = RST_BALL_MAX_CHUNKS;
-struct BallScratch {               // per-wave LDS (~12.5 KB)
-  float4 pts[kBallChunk];          // x, y, z, original index bits
-  int pos[kBallChunk];             // sorted position
+template <int C>
+struct BallScratchT {              // per-wave LDS (~12.5 KB at C = 512)
+  static constexpr int kChunk = C;
+  float4 pts[C];                   // x, y, z, original index bits
+  int pos[C];                      // sorted position
   int stack[kBallStack];
   int leaves[kBallLeaves];
 };
+using BallScratch = BallScratchT<kBallChunk>;
 
 __device__ __forceinline__ float wave_min_f(float x) {
 #pragma unroll
@@ -1115,13 +1118,14 @@ __device__ __forceinline__ void ball_box(bool act, float qx, float qy, float qz,
 // Scan the leaves ts.leaves[0, nlv) for every lane: their points staged
 // kBallChunk at a time, 16 lanes per leaf.  Returns the chunk count, or -1
 // when an index guard trips (never expected).
-__device__ __forceinline__ int ball_flush(const BvhView& bv, BallScratch& ts, int nlv, float qx,
+template <class TS>
+__device__ __forceinline__ int ball_flush(const BvhView& bv, TS& ts, int nlv, float qx,
                                           float qy, float qz, Best2& r, int4& det) {
   const int lane = __lane_id();
   int chunks = 0;
   for (int l0 = 0; l0 < nlv;) {
     // leaves [l0, l1) fill one chunk (<= 16 points each)
-    const int l1 = min(nlv, l0 + kBallChunk / 16);
+    const int l1 = min(nlv, l0 + TS::kChunk / 16);
     int b = 0, c = 0;
     bool bad = false;
     if (lane < l1 - l0) {
@@ -1198,9 +1202,11 @@ __device__ __forceinline__ int ball_flush(const BvhView& bv, BallScratch& ts, in
 // outside of the final box, margins applied: the lane's first is exact when
 // it lies within Mq (every point inside the box was scanned).  The whole
 // wave calls it.
+template <class TS>
 __device__ __forceinline__ bool ball_tile_search(const BvhView& bv, bool act, float qx, float qy,
-                                                 float qz, Best2& r, float& mq, BallScratch& ts,
+                                                 float qz, Best2& r, float& mq, TS& ts,
                                                  int& gfail, int4& det, int& chunks) {
+  constexpr int kMaxChunks = kBallMaxChunks * kBallChunk / TS::kChunk;  // (the same staged points)
   const int lane = __lane_id();
   const int nl = bv.nleaves;
   const uint64_t lt = (1ull << lane) - 1ull;
@@ -1253,7 +1259,7 @@ __device__ __forceinline__ bool ball_tile_search(const BvhView& bv, bool act, fl
     }
     chunks += c;
     nlv = 0;
-    if (chunks > kBallMaxChunks) return false;
+    if (chunks > kMaxChunks) return false;
     ball_box(act, qx, qy, qz, r, lo, hi);  // the balls shrink
   }
   const float m = fminf(fminf(fminf(qx - lo.x, hi.x - qx), fminf(qy - lo.y, hi.y - qy)),
