@@ -1,13 +1,13 @@
 """Benchmark: ICP iterations/s + frames/s on a 640x480 synthetic RGB-D stream
 (BASELINE.json metric, configs[1]).
 
-One step = one batch of --batch (12) incoming frames of the stream, fully on
+One step = one batch of --batch (16) incoming frames of the stream, fully on
 the GPU, per frame:
     u16 depth (already in HBM) -> unprojection -> Morton sort + BVH build
     (the frame's index, reused as the next pair's target)
     -> AlignIcp3d(curr, prev) with the reference's P2POINT_REF loop,
        128 fixed iterations (rs_replay_app.cpp:246-251),
-the batch's 12 frame pairs aligned in lockstep by one
+the batch's 16 frame pairs aligned in lockstep by one
 rst_icp_align_batch_async (--batch 0: a step is one frame pair, one align).
 value = ICP iterations/s over all ranks (pairs * 128 / time).  Frame
 preparation runs on --prep-threads contexts of its own, and --inflight
@@ -401,11 +401,13 @@ def main():
                     help="frame pairs in flight in the reference-rounding leg: its sequential "
                          "sums run one wavefront per component for most of an iteration, so "
                          "more pairs share the GPU")
-    ap.add_argument("--batch", type=int, default=12,
+    ap.add_argument("--batch", type=int, default=16,
                     help="frame pairs per batched align (rst_icp_align_batch_async: one launch of "
                          "each loop kernel for the whole batch, r06h: 8 x 4 in flight 23.0k it/s "
                          "vs 15.1k for 24 single aligns; r11 shape sweep, 480 pairs: 8 x 4 "
-                         "31.95k, 10 x 4 32.5k, 12 x 4 32.6k, 16 x 3 32.4k); 0 = one pair per align")
+                         "31.95k, 10 x 4 32.5k, 12 x 4 32.6k, 16 x 3 32.4k; r15 build, 480 pairs: "
+                         "12 x 4 35.2k, 16 x 4 36.0k, 16 x 3 34.9k, 20 x 3 35.1k, 12 x 5 33.4k); "
+                         "0 = one pair per align")
     ap.add_argument("--prep-threads", type=int, default=3,
                     help="frame-preparation contexts / host threads of the batched legs (each "
                          "frame's unproject + index build is host-synchronous; r10 one context)")
