@@ -401,13 +401,14 @@ def main():
                     help="frame pairs in flight in the reference-rounding leg: its sequential "
                          "sums run one wavefront per component for most of an iteration, so "
                          "more pairs share the GPU")
-    ap.add_argument("--batch", type=int, default=16,
+    ap.add_argument("--batch", type=int, default=-1,
                     help="frame pairs per batched align (rst_icp_align_batch_async: one launch of "
                          "each loop kernel for the whole batch, r06h: 8 x 4 in flight 23.0k it/s "
                          "vs 15.1k for 24 single aligns; r11 shape sweep, 480 pairs: 8 x 4 "
                          "31.95k, 10 x 4 32.5k, 12 x 4 32.6k, 16 x 3 32.4k; r15 build, 480 pairs: "
-                         "12 x 4 35.2k, 16 x 4 36.0k, 16 x 3 34.9k, 20 x 3 35.1k, 12 x 5 33.4k); "
-                         "0 = one pair per align")
+                         "12 x 4 35.2k, 16 x 4 36.0k, 16 x 3 34.9k, 20 x 3 35.1k, 12 x 5 33.4k; "
+                         "720p: 8 8.9k, 12 9.4k, 16 8.1k); 0 = one pair per align; default 16 "
+                         "up to 640x480, 12 above")
     ap.add_argument("--prep-threads", type=int, default=3,
                     help="frame-preparation contexts / host threads of the batched legs (each "
                          "frame's unproject + index build is host-synchronous; r10 one context)")
@@ -422,6 +423,8 @@ def main():
         return RV.launch(a.gpus, sys.argv[1:], str(Path(__file__).resolve()))
     dw, dh = WORKLOADS[a.workload]
     a.width, a.height = a.width or dw, a.height or dh
+    if a.batch < 0:  # (a batch's points: 16 VGA frames, 12 at 720p -- the sweeps above)
+        a.batch = 16 if a.width * a.height <= 640 * 480 else 12
     pyr = a.workload == "pyramid"
     pyr_iters = [int(x) for x in a.pyr_iters.split(",")] if pyr else [a.iters]
     if pyr and len(pyr_iters) != a.levels:

@@ -26,6 +26,7 @@ pmc() {  # key, Acc, bench args...
   step pmcw_$key 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcw_${TAG}_$key -o run -- python3 bench.py $PMCB "$@"
   python3 scripts/pmc_traffic.py gpurun_out/pmc_${TAG}_$key.json $(find gpurun_out/pmcf_${TAG}_$key -name "*counter_collection.csv") $(find gpurun_out/pmcw_${TAG}_$key -name "*counter_collection.csv") $acc 8 $key
   cp gpurun_out/pmc_${TAG}_$key.json profiles/pmc_${TAG}_$key.json
+  rm -rf gpurun_out/pmcf_${TAG}_$key gpurun_out/pmcw_${TAG}_$key  # (gpurun copies back <= 64 MiB)
 }
 pmc stream_1280x720_p2point_ref RefAcc --width 1280 --height 720
 pmc stream_640x480_p2plane P2PlaneAcc --mode p2plane
