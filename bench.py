@@ -260,89 +260,130 @@ def pyramid_level_roofline(a, d_depth, K, nfr, c, pctx, opts, normals_k, pyr_ite
     return out
 
 
-def run_sharded(a, K, frames, d_depth, hip, world, rank, local, rdv, barrier, max_over_ranks):
+SHARDED_MODES = {  # --workload sharded --mode / --sum-mode -> the align's options
+    "ref": ("RST_SUM_REF: the reference's sequential fp32 sums, bit-exact (within the 1e-4 gate)",
+            "per iteration the sequential fp32 sums relayed rank to rank (an all-gather of 32 B "
+            "fp64 totals per rank, 16 B chain values sent on, a 16 B broadcast; each rank maps "
+            "and walks its own stretch), one all-reduce of 9 fp64"),
+    "fp64": ("RST_SUM_FP64: fp64 partial sums (outside the 1e-4 gate of the reference's fp32 "
+             "sums: tests/golden/fp64_gate.json)", "one RCCL all-reduce of 16 fp64 per iteration"),
+    "p2plane": ("fp64 6x6 / 6x1 point-to-plane normal equations (absent in the reference, "
+                "SURVEY.md §8 a11), image-grid normals",
+                "one RCCL all-reduce of the 30-double normal equations per iteration (the "
+                "north_star's split), every rank the same Cholesky solve"),
+}
+
+
+def sharded_leg(kind: str, width: int, height: int, iters: int, steps: int, warmup: int,
+                frames_dev, local: int, rank: int, world: int, rdv, barrier, max_over_ranks,
+                hip, K=None):
     """configs[3]: one large scan pair (default 1000x1000 depth, ~1M points),
-    the source sharded across the ranks (contiguous point ranges), the target
-    index replicated; per iteration one RCCL all-reduce of the 16 fp64
-    partial sums over xGMI (rst_icp_align_sharded_device).  A step = one
-    AlignIcp3d of the pair (128 iterations); total work is fixed as N grows
-    (strong scaling), value = the pair's ICP iterations/s."""
+    the source sharded across the ranks (contiguous point ranges of its
+    original order, shard_bounds), the target index replicated; per
+    iteration the exchange of `kind` (SHARDED_MODES) over RCCL / xGMI
+    (rst_icp_align_sharded_device).  A step = one AlignIcp3d of the pair
+    (`iters` iterations; point-to-plane to convergence, <= 30); total work is
+    fixed as N grows (strong scaling).  frames_dev: the two depth frames in
+    HBM (target, source).  Returns the timing dict (every rank; timing is
+    max over ranks)."""
     from realsensetracker_amd.shard import ShardedAligner, shard_bounds
+    K = K or driver.intrinsics(width, height)
     ctx = A.Context(local)
-    tgt = A.Target.from_depth_device(d_depth[0].value, K, 0, ctx)
-    npx = a.width * a.height
+    plane = kind == "p2plane"
+    tgt = A.Target.from_depth_device(frames_dev[0].value, K, -2 if plane else 0, ctx)
     d_src = C.c_void_p()
-    assert hip.hipMalloc(C.byref(d_src), C.c_size_t(12 * npx)) == 0
+    assert hip.hipMalloc(C.byref(d_src), C.c_size_t(12 * width * height)) == 0
     n = C.c_int64(0)
-    L.check(L.lib().rst_unproject_device(ctx.handle, d_depth[1], C.byref(K), 0, d_src,
+    L.check(L.lib().rst_unproject_device(ctx.handle, frames_dev[1], C.byref(K), 0, d_src,
                                          C.byref(n)), "rst_unproject_device")
     lo, hi = shard_bounds(n.value, world, rank)
     sh = ShardedAligner(ctx, rendezvous=rdv)
-    ref = a.sum_mode == "ref"
-    opts = L.default_opts(max_iter=a.iters, sum_mode=L.RST_SUM_REF if ref else L.RST_SUM_FP64)
+    if plane:
+        opts = L.default_opts(mode=L.RST_P2PLANE, max_iter=30)
+    else:
+        opts = L.default_opts(max_iter=iters,
+                              sum_mode=L.RST_SUM_REF if kind == "ref" else L.RST_SUM_FP64)
     ptr = d_src.value + 12 * lo
+    try:
+        def step():  # every rank knows the global count: no host round trip per align
+            ok, pose, _ = sh.align(ptr, hi - lo, tgt, opts, n_total=n.value)
+            return ok, pose
 
-    def step():  # every rank knows the global count: no host round trip per align
-        ok, pose, _ = sh.align(ptr, hi - lo, tgt, opts, n_total=n.value)
-        return ok, pose
+        for _ in range(warmup):
+            step()
+        ctx.enable_kernel_timing(8)
+        kms, kl, oks, its = 0.0, 0, 0, 0
+        barrier()
+        ctx.synchronize()
+        t0 = time.perf_counter()
+        pose = np.eye(4, dtype=np.float32)
+        for _ in range(steps):
+            ok, pose = step()
+            oks += int(ok)
+            its += ctx.last_iterations()  # (point-to-plane: to convergence; every rank alike)
+            ms, nl = ctx.last_kernel_time()
+            kms += ms * nl
+            kl += nl
+        ctx.synchronize()
+        barrier()
+        dt = max_over_ranks(time.perf_counter() - t0)
+        ctx.enable_kernel_timing(0)
+        it_pair = its / max(1, steps)
+        avg_ms = kms / max(1, kl)
+        alg = p2point_alg_bytes(hi - lo, len(tgt)) + (12 * len(tgt) if plane else 0)
+        achieved = alg / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+        return {"kind": kind, "value": its / dt, "unit": "ICP iterations/s",
+                "n_ranks": world, "steps": steps, "warmup": warmup,
+                "ms_per_step": 1000.0 * dt / steps, "iters_per_pair": it_pair,
+                "points": n.value, "target_points": len(tgt), "shard_points": hi - lo,
+                "pairs_ok": oks, "final_pose_t": [float(x) for x in pose[:3, 3]],
+                "accumulation": SHARDED_MODES[kind][0], "exchange": SHARDED_MODES[kind][1],
+                "nn_avg_us": 1000.0 * avg_ms, "alg_bytes_per_launch": alg,
+                "achieved_GBps": achieved}
+    finally:
+        sh.close()
+        tgt.free()
+        hip.hipFree(d_src)
+        ctx.close()
 
-    for _ in range(a.warmup):
-        step()
-    ctx.enable_kernel_timing(8)
-    kms, kl, oks = 0.0, 0, 0
-    barrier()
-    ctx.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        ok, pose = step()
-        oks += int(ok)
-        ms, nl = ctx.last_kernel_time()
-        kms += ms * nl
-        kl += nl
-    ctx.synchronize()
-    barrier()
-    dt = max_over_ranks(time.perf_counter() - t0)
-    ctx.enable_kernel_timing(0)
-    avg_ms = kms / max(1, kl)
-    alg = p2point_alg_bytes(hi - lo, len(tgt))
-    achieved = alg / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+
+def run_sharded(a, K, frames, d_depth, hip, world, rank, local, rdv, barrier, max_over_ranks):
+    """configs[3] as the bench line (--workload sharded): value = the pair's
+    ICP iterations/s with the source sharded over the ranks (sharded_leg)."""
+    kind = "p2plane" if a.mode == "p2plane" else a.sum_mode
+    r = sharded_leg(kind, a.width, a.height, a.iters, a.steps, a.warmup, d_depth, local, rank,
+                    world, rdv, barrier, max_over_ranks, hip, K)
     if rank == 0:
         cpu = None if a.no_cpu or world > 1 else cpu_baseline(a.width, a.height, a.cpu_iters)
-        value = a.steps * a.iters / dt
+        value = r["value"]
         out = {
             "metric": METRIC, "value": value, "unit": "ICP iterations/s", "n_gpus": world,
-            "steps": a.steps, "warmup": a.warmup, "ms_per_step": 1000.0 * dt / a.steps,
+            "steps": a.steps, "warmup": a.warmup, "ms_per_step": r["ms_per_step"],
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (seeded procedural room, ray-cast u16 depth, 1 mm noise, "
                     "~3% invalid)",
-            "config": {"workload": f"{a.width}x{a.height} scan pair ({n.value} source points), "
-                                   f"AlignIcp3d P2POINT_REF {a.iters} iters, source sharded "
-                                   f"over {world} rank(s), " + (
-                                       "per iteration the sequential fp32 sums relayed rank "
-                                       "to rank (an all-gather of 32 B fp64 totals per rank, "
-                                       "16 B chain values sent on, a 16 B broadcast; each "
-                                       "rank maps and walks its own stretch), one all-reduce "
-                                       "of 9 fp64" if ref else
-                                       "one RCCL all-reduce of 16 fp64 per iteration"),
-                       "width": a.width, "height": a.height, "iters_per_pair": a.iters,
-                       "points_per_frame": n.value, "target_points": len(tgt),
-                       "accumulation": ("RST_SUM_REF: the reference's sequential fp32 sums, "
-                                        "bit-exact" if ref else "RST_SUM_FP64: fp64 partial sums"),
+            "config": {"workload": f"{a.width}x{a.height} scan pair ({r['points']} source points), "
+                                   + ("point-to-plane to convergence (<= 30 iters)"
+                                      if kind == "p2plane" else
+                                      f"AlignIcp3d P2POINT_REF {a.iters} iters")
+                                   + f", source sharded over {world} rank(s), " + r["exchange"],
+                       "width": a.width, "height": a.height, "iters_per_pair": r["iters_per_pair"],
+                       "points_per_frame": r["points"], "target_points": r["target_points"],
+                       "mode": "P2PLANE" if kind == "p2plane" else "P2POINT_REF",
+                       "accumulation": r["accumulation"],
                        "parallelism": f"shard{world}"},
-            "frames_per_s": a.steps / dt, "pairs_ok": oks,
-            "final_pose_t": [float(x) for x in pose[:3, 3]],
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": "k_icp_nn", "avg_us": 1000.0 * avg_ms,
-                         "alg_bytes_per_launch": alg},
+            "frames_per_s": a.steps / (r["ms_per_step"] * a.steps * 1e-3), "pairs_ok": r["pairs_ok"],
+            "final_pose_t": r["final_pose_t"],
+            "roofline": {"bound": "hbm", "achieved": r["achieved_GBps"], "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": r["achieved_GBps"] / HBM_PEAK_GBS,
+                         "traffic": None, "kernel": "k_icp_nn+k_icp_fb (rank 0's shard)",
+                         "avg_us": r["nn_avg_us"],
+                         "alg_bytes_per_launch": r["alg_bytes_per_launch"]},
             "cpu_baseline": cpu,
         }
         if cpu is not None:
             out["speedup_vs_cpu_baseline"] = value / cpu["value"]
         print(json.dumps(out))
-    sh.close()
-    tgt.free()
-    hip.hipFree(d_src)
     rdv.close()
 
 
@@ -412,6 +453,12 @@ def main():
     ap.add_argument("--prep-threads", type=int, default=3,
                     help="frame-preparation contexts / host threads of the batched legs (each "
                          "frame's unproject + index build is host-synchronous; r10 one context)")
+    ap.add_argument("--no-sharded", action="store_true",
+                    help="skip the stream line's sharded_1M field (configs[3] over all ranks)")
+    ap.add_argument("--sharded-steps", type=int, default=5,
+                    help="timed aligns of each sharded_1M mode")
+    ap.add_argument("--sharded-timeout", type=float, default=120.0,
+                    help="watchdog of the sharded_1M field (s)")
     ap.add_argument("--roof-steps", type=int, default=4,
                     help="frames of the one-pair-in-flight kernel timing pass (roofline; "
                          "batched: the value leg's --steps pairs, one batch in flight)")
@@ -875,7 +922,68 @@ def main():
             x["iters"] for x in lv_roof))
         achieved = tb / (tt * 1e-6) / 1e9 if tt > 0 else 0.0
 
+    def sharded_extra() -> dict | None:
+        """configs[3] beside the stream's line, on every rank: the 1M pair
+        with its source sharded over ALL ranks of this run (RCCL over xGMI at
+        N > 1), in the gated mode (RST_SUM_REF's relay), the fp64 mode and
+        the north_star's point-to-plane split -- so a `--gpus N` run measures
+        the collectives, not only replicas.  A watchdog bounds it: a leg
+        that has not finished in --sharded-timeout s (a collective that never
+        completes) ends the process with the stream's line printed."""
+        if a.no_sharded or pyr or plane or a.workload != "stream":
+            return None
+        import threading
+        state = {"done": False}
+
+        def expire():
+            if state["done"]:
+                return
+            if rank == 0 and "line" in state:
+                line = dict(state["line"])
+                line["sharded_1M"] = {"error": f"not finished in {a.sharded_timeout} s (watchdog)"}
+                print(json.dumps(line), flush=True)
+            os._exit(0)
+
+        wd = threading.Timer(a.sharded_timeout, expire)
+        wd.daemon = True
+        state["timer"] = wd
+        sw, sh_ = WORKLOADS["sharded"]
+        Ks = driver.intrinsics(sw, sh_)
+        sfr = render_frames(seed=0, n=2, K=Ks, stride=1)  # one pair, the same on every rank
+        d_s = []
+        for f in sfr:
+            p = C.c_void_p()
+            assert hip.hipMalloc(C.byref(p), C.c_size_t(2 * sw * sh_)) == 0
+            assert hip.hipMemcpy(p, f.ctypes.data_as(C.c_void_p), C.c_size_t(2 * sw * sh_), 1) == 0
+            d_s.append(p)
+        return {"frames": d_s, "K": Ks, "size": (sw, sh_), "state": state}
+
+    def sharded_run(prep) -> dict:
+        st_ = prep["state"]
+        st_["timer"].start()
+        res = {"note": "configs[3]: one 1000x1000 pair (~1M points), the source sharded over "
+                       f"all {world} rank(s) of this run, strong scaling; value = the pair's ICP "
+                       "iterations/s (max over ranks); multi-rank RCCL unmeasured by the builder "
+                       "(1-GPU boxes)", "n_ranks": world}
+        try:
+            for kind in ("ref", "fp64", "p2plane"):
+                r = sharded_leg(kind, prep["size"][0], prep["size"][1], a.iters, a.sharded_steps, 2,
+                                prep["frames"], local, rank, world, rdv, barrier, max_over_ranks,
+                                hip, prep["K"])
+                res[kind] = {k: r[k] for k in ("value", "ms_per_step", "iters_per_pair", "points",
+                                               "shard_points", "pairs_ok", "nn_avg_us",
+                                               "achieved_GBps", "accumulation", "exchange")}
+        finally:
+            st_["done"] = True
+            st_["timer"].cancel()
+            for p in prep["frames"]:
+                hip.hipFree(p)
+        return res
+
+    sh_prep = sharded_extra()
     if rank != 0:
+        if sh_prep is not None:
+            sharded_run(sh_prep)
         rdv.close()
         return 0
     # the measured HBM ceiling on this box (stream copy, read + write bytes),
@@ -969,6 +1077,9 @@ def main():
         out["gicp"] = gicp
     if cpu is not None:
         out["speedup_vs_cpu_baseline"] = value / cpu["value"]
+    if sh_prep is not None:
+        sh_prep["state"]["line"] = out  # (printed by the watchdog if the leg never finishes)
+        out["sharded_1M"] = sharded_run(sh_prep)
     print(json.dumps(out))
     rdv.close()
     return 0

@@ -59,8 +59,10 @@ typedef enum {
    * float products.  Bit-identical means and cost; the default. */
   RST_SUM_REF = 0,
   /* fp64 partial sums in any order (one pass, no sequential step): the
-   * throughput mode.  Differs from the reference by its own fp32-vs-fp64
-   * sensitivity (~1e-5 m typical, 1.5e-4 m seen on one golden pair). */
+   * throughput mode.  Differs from the reference by the loop's own
+   * fp32-vs-fp64 sensitivity: NOT within a 1e-4 pose gate of it -- up to
+   * ~1e-3 m / 2e-4 rad after 128 iterations on 640x480 frame pairs
+   * (tests/golden/fp64_gate.json). */
   RST_SUM_FP64 = 1
 } rst_sum_mode;
 
@@ -73,9 +75,9 @@ typedef struct {
   float p2plane_eps;      /* P2PLANE: stop when |xi| < eps (1e-6) */
   float p2plane_mu;       /* P2PLANE: GM scale on plane residual (m^2) */
   float p2plane_max_dist; /* P2PLANE: reject NN beyond this (m); 0 = off */
-  int32_t sum_mode;       /* rst_sum_mode (P2POINT_REF only; the sharded
-                           * align always runs RST_SUM_FP64: a sequential
-                           * sum has no shard decomposition) */
+  int32_t sum_mode;       /* rst_sum_mode (P2POINT_REF only; sharded, the
+                           * RST_SUM_REF chains are relayed rank to rank:
+                           * every rank gets the same bit-exact sums) */
   int32_t n_total;        /* sharded align: the points of ALL shards when the
                            * caller knows them (> 0: no count all-reduce and no
                            * host round trip before the loop; must equal the
@@ -118,6 +120,9 @@ int rst_ctx_last_kernel_time(rst_ctx* ctx, float* avg_ms, int32_t* launches);
  * searches), [2] = the rest (reductions and the solve; RST_SUM_REF: also the
  * sequential sums). */
 int rst_ctx_last_iteration_times(rst_ctx* ctx, float avg_ms[3], int32_t* iterations);
+/* Iterations run by the last align finished on this context (the entry
+ * points without an iterations_run output: the sharded aligns). */
+int rst_ctx_last_iterations(rst_ctx* ctx, int32_t* iterations);
 /* hipGraph mode (BASELINE configs[4]): each align's iteration loop is
  * captured and replayed as one graph (the executable for a given iteration
  * count and mode is kept on the context and updated in place with the next
@@ -274,7 +279,8 @@ int rst_solve_kabsch(rst_ctx* ctx, const float* src, int64_t n,
                      const float* dst, int64_t m, const int32_t* pairs,
                      const float* weights, int64_t k, float pose_out[16]);
 
-/* ComputeCentroid (point_cloud_utils.cpp:92-98), fp64 accumulation. */
+/* ComputeCentroid (point_cloud_utils.cpp:92-98): the reference's fp32
+ * sequential sum in input order times float(1.0 / n), bit-exact. */
 int rst_compute_centroid(rst_ctx* ctx, const float* xyz, int64_t n,
                          float out[3]);
 
@@ -421,9 +427,13 @@ int rst_comm_get_unique_id(char id_out[RST_COMM_ID_BYTES]);
 int rst_comm_create(rst_ctx* ctx, const char id[RST_COMM_ID_BYTES],
                     int nranks, int rank, rst_comm** out);
 int rst_comm_destroy(rst_comm* comm);
-/* Every rank passes its own source shard and the full (replicated) target;
- * the fp64 partial sums are all-reduced each iteration and every rank
- * solves the same pose.  n_total = sum of shard sizes (ranks agree). */
+/* Every rank passes its own source shard -- rank r the r-th contiguous
+ * stretch of the source's order -- and the full (replicated) target; every
+ * rank solves the same pose.  Per iteration: RST_SUM_FP64 one all-reduce of
+ * 16 fp64 partial sums, RST_P2PLANE one of the 30-double 6x6 / 6x1 normal
+ * equations, RST_SUM_REF the sequential sums' relay (an all-gather of 32 B
+ * per rank, a 16 B hop per rank, a 16 B broadcast) and one all-reduce of the
+ * 9 covariance sums.  n_total = sum of shard sizes (ranks agree). */
 int rst_icp_align_sharded_device(rst_ctx* ctx, rst_comm* comm,
                                  const float* d_src_shard, int64_t n_shard,
                                  const rst_target* tgt,

@@ -36,7 +36,8 @@ int rst_debug_enable_seq_trace(rst_ctx* ctx, int enable);
 /* With the trace enabled, per iteration of the last align (first n <= 256)
  * the walks' statistics, 64 int32 each (the layout of rst_debug_seq_sum's
  * stats: per chain superblock tries / hits, group tries / hits, leaf tries
- * / hits, serial blocks, walker clocks). */
+ * / hits, serial blocks, walker clocks; zero for chains of <= 16,384
+ * elements, which k_sq_serial / k_sq_small sum without walk statistics). */
 int rst_debug_seq_walk_stats(rst_ctx* ctx, int32_t* out, int32_t n);
 /* Test hook: every sequential-sum walk after this call ORs `bits` (1..127,
  * 0 = off; process-wide) into its table bound-check word, as a corrupted map
@@ -84,7 +85,9 @@ int rst_debug_seq_sum4(rst_ctx* ctx, const float* xyzw, int64_t n, float out[4])
  * at any size, 3 k_sq_serial at any size, 4 k_sq_small up to 16384
  * elements (the map path beyond); reps launches back to back, *ms
  * (optional) = device time per launch; stats (optional, map path, 64
- * int32; zero when the replay ran) = 8 per component
+ * int32; untouched when k_sq_serial or the unforced k_sq_small ran; with
+ * serial = 4, k_sq_small's own layout: [0..5] chain 0's phase clocks,
+ * [8..13] group / leaf tries and hits, serial blocks, groups) = 8 per component
  * of the last launch's walk: superblock tries / hits, group tries / hits,
  * block tries / hits, blocks added serially, walker clocks; stats[32] =
  * the map kernels' bound-check failure bits (0 = none); stats[33 + c] =

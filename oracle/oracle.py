@@ -93,6 +93,10 @@ def lib():
         L.orc_align_p2plane.restype = C.c_int
         L.orc_align_p2plane.argtypes = [_f, C.c_int64, _f, _f, C.c_int64, P, C.c_int,
                                         C.c_float, C.c_float, C.c_float, _f, _f]
+        L.orc_p2plane_partials.argtypes = [_f, C.c_int64, P, _f, _f, _d, _d, C.c_float,
+                                           C.c_float, _d]
+        L.orc_p2plane_update.restype = C.c_int
+        L.orc_p2plane_update.argtypes = [_d, _d, _d, _d, _d]
         _lib = L
     return _lib
 
@@ -449,3 +453,29 @@ def align_p2plane(src, dst, dst_normals, max_iter=30, eps=1e-6, mu=4e-4, max_dis
                                  tree.h if tree is not None else None, max_iter, eps, mu,
                                  max_dist, _fp(buf), C.byref(mc))
     return it, _uncm(buf), float(mc.value)
+
+
+def p2plane_partials(src, tree: KDTree, dst_normals, Rd, td, mu=4e-4, max_dist=0.0):
+    """One point-to-plane iteration's normal equations over `src` (a shard)
+    at the double pose (Rd 3x3, td 3): 29 doubles (21 lower-triangle sum
+    w J J^T, 6 sum w J r, count, sum d2) -- orc_align_p2plane's own sums."""
+    s, nn = _cloud(src), _cloud(dst_normals)
+    out = np.zeros(29)
+    R = np.ascontiguousarray(np.asarray(Rd, np.float64).T).reshape(9)
+    t = np.ascontiguousarray(np.asarray(td, np.float64)).reshape(3)
+    lib().orc_p2plane_partials(_fp(s), s.shape[0], tree.h, _fp(tree.cloud), _fp(nn),
+                               R.ctypes.data_as(_d), t.ctypes.data_as(_d), float(mu),
+                               float(max_dist), out.ctypes.data_as(_d))
+    return out
+
+
+def p2plane_update(tot, Rd, td):
+    """The solve + pose update on the all-reduced sums.  Returns (ok, Rd, td,
+    |xi|, cost)."""
+    t_ = np.ascontiguousarray(np.asarray(tot, np.float64)).copy()
+    R = np.ascontiguousarray(np.asarray(Rd, np.float64).T).reshape(9).copy()
+    t = np.ascontiguousarray(np.asarray(td, np.float64)).reshape(3).copy()
+    xn, cost = C.c_double(0), C.c_double(0)
+    ok = lib().orc_p2plane_update(t_.ctypes.data_as(_d), R.ctypes.data_as(_d),
+                                  t.ctypes.data_as(_d), C.byref(xn), C.byref(cost))
+    return bool(ok), R.reshape(3, 3).T.copy(), t, xn.value, cost.value

@@ -1093,6 +1093,84 @@ static int chol_solve6(const double A[36], const double b[6], double x[6]) {
   return 1;
 }
 
+/* One iteration's normal equations over source points [0, n) at the pose
+ * (Rd, td) (column-major 3x3 + 3, double; rounded to float for the
+ * transform): out[0..20] = sum w J J^T (lower triangle, row a, c <= a),
+ * out[21..26] = sum w J r, out[27] = count, out[28] = sum d2, summed in
+ * ascending i.  A shard's partials: the sharded loop all-reduces them (the
+ * north_star's per-iteration RCCL all-reduce of the 6x6 / 6x1 system). */
+void orc_p2plane_partials(const float* src, int64_t n, const orc_kdtree* tree,
+                          const float* dst, const float* dst_normals, const double Rd[9],
+                          const double td[3], float mu0, float max_dist, double out[29]) {
+  float R[9], t[3];
+  for (int q = 0; q < 9; ++q) R[q] = (float)Rd[q];
+  for (int r = 0; r < 3; ++r) t[r] = (float)td[r];
+  const float md2 = max_dist > 0 ? max_dist * max_dist : FLT_MAX;
+  double A[21] = {0}, b[6] = {0}, cnt = 0, d2sum = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    float p[3];
+    xform(R, t, src + 3 * i, p);
+    int32_t j = 0;
+    float d2 = 0;
+    orc_kdtree_knn(tree, p, 1, &j, &d2);
+    if (!(d2 <= md2)) continue;
+    const float* q = dst + 3 * (int64_t)j;
+    const float* nn = dst_normals + 3 * (int64_t)j;
+    const float e0 = p[0] - q[0], e1 = p[1] - q[1], e2 = p[2] - q[2];
+    const float r = (nn[0] * e0 + nn[1] * e1) + nn[2] * e2;
+    const double dr = (double)r;
+    const double l = (double)mu0 / (dr * dr + (double)mu0);
+    const double w = l * l;
+    const double P[3] = {p[0], p[1], p[2]}, N[3] = {nn[0], nn[1], nn[2]};
+    const double J[6] = {P[1] * N[2] - P[2] * N[1], P[2] * N[0] - P[0] * N[2],
+                         P[0] * N[1] - P[1] * N[0], N[0], N[1], N[2]};
+    for (int a = 0, k = 0; a < 6; ++a) {
+      for (int c = 0; c <= a; ++c, ++k) A[k] += w * J[a] * J[c];
+      b[a] += w * J[a] * dr;
+    }
+    cnt += 1.0;
+    d2sum += (double)d2;
+  }
+  memcpy(out, A, sizeof(A));
+  memcpy(out + 21, b, sizeof(b));
+  out[27] = cnt;
+  out[28] = d2sum;
+}
+
+/* The solve every rank runs on the (all-reduced) normal equations: A xi = -b
+ * by Cholesky, T <- exp([w]x) T + v.  Returns 0 when the system is
+ * unusable (< 6 correspondences, not positive definite): the align fails. */
+int orc_p2plane_update(const double tot[29], double Rd[9], double td[3], double* xi_norm,
+                       double* cost) {
+  if (tot[27] < 6) return 0;
+  double A[36], nb[6], xi[6];
+  for (int a = 0, k = 0; a < 6; ++a)
+    for (int c = 0; c <= a; ++c, ++k) A[a * 6 + c] = A[c * 6 + a] = tot[k];
+  for (int a = 0; a < 6; ++a) nb[a] = -tot[21 + a];
+  if (!chol_solve6(A, nb, xi)) return 0;
+  double dR[9];
+  rodrigues(xi, dR);
+  double nR[9], nt[3];
+  for (int c = 0; c < 3; ++c)
+    for (int r = 0; r < 3; ++r) {
+      double s = 0;
+      for (int l2 = 0; l2 < 3; ++l2) s += A3(dR, r, l2) * A3(Rd, l2, c);
+      A3(nR, r, c) = s;
+    }
+  for (int r = 0; r < 3; ++r) {
+    double s = 0;
+    for (int l2 = 0; l2 < 3; ++l2) s += A3(dR, r, l2) * td[l2];
+    nt[r] = s + xi[3 + r];
+  }
+  memcpy(Rd, nR, sizeof(nR));
+  memcpy(td, nt, sizeof(nt));
+  *cost = sqrt(tot[28] / tot[27]);
+  double nx = 0;
+  for (int a = 0; a < 6; ++a) nx += xi[a] * xi[a];
+  *xi_norm = sqrt(nx);
+  return 1;
+}
+
 int orc_align_p2plane(const float* src, int64_t n, const float* dst,
                       const float* dst_normals, int64_t m,
                       const orc_kdtree* tree, int max_iter, float eps,
@@ -1108,71 +1186,17 @@ int orc_align_p2plane(const float* src, int64_t n, const float* dst,
   for (int c = 0; c < 3; ++c)
     for (int r = 0; r < 3; ++r) Rd[c * 3 + r] = pose_inout[c * 4 + r];
   for (int r = 0; r < 3; ++r) td[r] = pose_inout[12 + r];
-  const float md2 = max_dist > 0 ? max_dist * max_dist : FLT_MAX;
   int it = 0, ok = 1;
   double last_cost = 0;
   for (it = 0; it < max_iter;) {
-    float R[9], t[3];
-    for (int q = 0; q < 9; ++q) R[q] = (float)Rd[q];
-    for (int r = 0; r < 3; ++r) t[r] = (float)td[r];
-    double A[36] = {0}, b[6] = {0}, cnt = 0, d2sum = 0;
-    for (int64_t i = 0; i < n; ++i) {
-      float p[3];
-      xform(R, t, src + 3 * i, p);
-      int32_t j = 0;
-      float d2 = 0;
-      orc_kdtree_knn(tree, p, 1, &j, &d2);
-      if (!(d2 <= md2)) continue;
-      const float* q = dst + 3 * (int64_t)j;
-      const float* nn = dst_normals + 3 * (int64_t)j;
-      const float e0 = p[0] - q[0], e1 = p[1] - q[1], e2 = p[2] - q[2];
-      const float r = (nn[0] * e0 + nn[1] * e1) + nn[2] * e2;
-      const double dr = (double)r;
-      const double l = (double)mu0 / (dr * dr + (double)mu0);
-      const double w = l * l;
-      const double P[3] = {p[0], p[1], p[2]}, N[3] = {nn[0], nn[1], nn[2]};
-      const double J[6] = {P[1] * N[2] - P[2] * N[1], P[2] * N[0] - P[0] * N[2],
-                           P[0] * N[1] - P[1] * N[0], N[0], N[1], N[2]};
-      for (int a = 0; a < 6; ++a) {
-        for (int c = 0; c <= a; ++c) A[a * 6 + c] += w * J[a] * J[c];
-        b[a] += w * J[a] * dr;
-      }
-      cnt += 1.0;
-      d2sum += (double)d2;
-    }
-    if (cnt < 6) {
+    double tot[29], xn = 0;
+    orc_p2plane_partials(src, n, tree, dst, dst_normals, Rd, td, mu0, max_dist, tot);
+    if (!orc_p2plane_update(tot, Rd, td, &xn, &last_cost)) {
       ok = 0;
       break;
     }
-    for (int a = 0; a < 6; ++a)
-      for (int c = a + 1; c < 6; ++c) A[a * 6 + c] = A[c * 6 + a];
-    double nb[6], xi[6];
-    for (int a = 0; a < 6; ++a) nb[a] = -b[a];
-    if (!chol_solve6(A, nb, xi)) {
-      ok = 0;
-      break;
-    }
-    double dR[9];
-    rodrigues(xi, dR);
-    double nR[9], nt[3];
-    for (int c = 0; c < 3; ++c)
-      for (int r = 0; r < 3; ++r) {
-        double s = 0;
-        for (int l2 = 0; l2 < 3; ++l2) s += A3(dR, r, l2) * A3(Rd, l2, c);
-        A3(nR, r, c) = s;
-      }
-    for (int r = 0; r < 3; ++r) {
-      double s = 0;
-      for (int l2 = 0; l2 < 3; ++l2) s += A3(dR, r, l2) * td[l2];
-      nt[r] = s + xi[3 + r];
-    }
-    memcpy(Rd, nR, sizeof(nR));
-    memcpy(td, nt, sizeof(nt));
-    last_cost = sqrt(d2sum / cnt);
     ++it;
-    double nx = 0;
-    for (int a = 0; a < 6; ++a) nx += xi[a] * xi[a];
-    if (sqrt(nx) < (double)eps) break;
+    if (xn < (double)eps) break;
   }
   if (ok) {
     for (int c = 0; c < 3; ++c) {

@@ -193,6 +193,16 @@ int orc_align_p2plane(const float* src, int64_t n, const float* dst,
                       const orc_kdtree* tree, int max_iter, float eps,
                       float mu0, float max_dist, float pose_inout[16],
                       float* mean_cost);
+/* Its two halves, for the sharded loop (one all-reduce of `out` a step):
+ * the normal equations of source points [0, n) at the pose (Rd col-major,
+ * td) -- out[0..20] sum w J J^T lower triangle, [21..26] sum w J r, [27]
+ * count, [28] sum d2 --, and the solve + pose update on their totals
+ * (returns 0 when the system is unusable: the align fails). */
+void orc_p2plane_partials(const float* src, int64_t n, const orc_kdtree* tree,
+                          const float* dst, const float* dst_normals, const double Rd[9],
+                          const double td[3], float mu0, float max_dist, double out[29]);
+int orc_p2plane_update(const double tot[29], double Rd[9], double td[3], double* xi_norm,
+                       double* cost);
 
 #ifdef __cplusplus
 }

@@ -58,6 +58,7 @@ PROTOTYPES = {
     "rst_ctx_synchronize": (C.c_int, [_P]),
     "rst_ctx_last_kernel_time": (C.c_int, [_P, c_float_p, c_int32_p]),
     "rst_ctx_last_iteration_times": (C.c_int, [_P, c_float_p, c_int32_p]),
+    "rst_ctx_last_iterations": (C.c_int, [_P, c_int32_p]),
     "rst_ctx_enable_kernel_timing": (C.c_int, [_P, C.c_int]),
     "rst_target_build": (C.c_int, [_P, c_float_p, C.c_int64, C.POINTER(_P)]),
     "rst_target_build_device": (C.c_int, [_P, _P, C.c_int64, C.POINTER(_P)]),

@@ -76,6 +76,12 @@ class Context:
         L.check(L.lib().rst_ctx_last_iteration_times(self._h, L.fptr(ms), C.byref(n)), "timing")
         return [float(x) for x in ms], n.value
 
+    def last_iterations(self) -> int:
+        """Iterations run by the last align finished on this context."""
+        n = C.c_int32(0)
+        L.check(L.lib().rst_ctx_last_iterations(self._h, C.byref(n)), "rst_ctx_last_iterations")
+        return n.value
+
     def close(self):
         if self._h:
             L.lib().rst_ctx_destroy(self._h)

@@ -372,6 +372,12 @@ int rst_ctx_last_iteration_times(rst_ctx* ctx, float avg_ms[3], int32_t* iterati
   return RST_OK;
 }
 
+int rst_ctx_last_iterations(rst_ctx* ctx, int32_t* iterations) {
+  if (!ctx || !iterations) return RST_E_ARG;
+  *iterations = ctx->last_iters;
+  return RST_OK;
+}
+
 int rst_ctx_enable_graphs(rst_ctx* ctx, int enable) {
   if (!ctx) return RST_E_ARG;
   ctx->graphs = enable != 0;

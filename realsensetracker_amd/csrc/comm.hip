@@ -35,6 +35,7 @@ struct rst_comm {
   int64_t* d_cnt = nullptr;     // device scratch of the count all-gather [R + 1]
   int64_t* d_layout = nullptr;  // the exchanged counts on the device [R]
   double* d_relay = nullptr;    // comm_relay_seqsum's exchange buffers
+  int32_t* d_guards = nullptr;  // comm_agree_guard's all-gather [R + 1]
 };
 
 namespace rst {
@@ -127,6 +128,31 @@ int comm_shard_layout(rst_comm* comm, int64_t n_local, int64_t n_total_hint, hip
 int comm_layout_check(rst_comm* comm, hipStream_t st, int32_t* d_guard) {
   if (!comm || !comm->d_cnt) return RST_E_ARG;
   k_layout_check<<<1, 64, 0, st>>>(comm->d_cnt, comm->d_layout, comm->nranks, d_guard);
+  RST_HIP(hipGetLastError());
+  return RST_OK;
+}
+
+namespace {
+__global__ void k_guard_copy(const int32_t* __restrict__ guard, int32_t* __restrict__ out) {
+  if (threadIdx.x == 0) *out = *guard;
+}
+__global__ void k_guard_or(const int32_t* __restrict__ all, int R, int32_t* __restrict__ guard) {
+  if (threadIdx.x != 0) return;
+  int32_t g = *guard;
+  for (int r = 0; r < R; ++r) g |= all[r];
+  *guard = g;
+}
+}  // namespace
+
+int comm_agree_guard(rst_comm* comm, hipStream_t st, int32_t* d_guard) {
+  if (!comm || !comm->comm || !d_guard) return RST_E_ARG;
+  const int R = comm->nranks;
+  if (!comm->d_guards && hipMalloc(&comm->d_guards, sizeof(int32_t) * (R + 1)) != hipSuccess) return RST_E_NOMEM;
+  k_guard_copy<<<1, 64, 0, st>>>(d_guard, comm->d_guards + R);
+  RST_HIP(hipGetLastError());
+  if (ncclAllGather(comm->d_guards + R, comm->d_guards, 1, ncclInt32, comm->comm, st) != ncclSuccess)
+    return RST_E_COMM;
+  k_guard_or<<<1, 64, 0, st>>>(comm->d_guards, R, d_guard);
   RST_HIP(hipGetLastError());
   return RST_OK;
 }
@@ -244,10 +270,11 @@ int rst_comm_create(rst_ctx* ctx, const char id[RST_COMM_ID_BYTES], int nranks, 
 int rst_comm_destroy(rst_comm* comm) {
   if (!comm) return RST_OK;
   if (comm->comm) ncclCommDestroy(comm->comm);
-  if (comm->d_cnt || comm->d_relay) {
+  if (comm->d_cnt || comm->d_relay || comm->d_guards) {
     (void)hipSetDevice(comm->device);
     if (comm->d_cnt) (void)hipFree(comm->d_cnt);
     if (comm->d_relay) (void)hipFree(comm->d_relay);
+    if (comm->d_guards) (void)hipFree(comm->d_guards);
   }
   delete comm;
   return RST_OK;

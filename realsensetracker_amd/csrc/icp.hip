@@ -541,6 +541,10 @@ constexpr int kCovBlocks = RST_COV_BLOCKS;
 __host__ __device__ __forceinline__ int cov_blocks(int64_t n) {
   return n > 32768 ? kCovBlocks : (int)((n + 8 * kBS - 1) / (8 * kBS)) + (n == 0 ? 1 : 0);
 }
+// the batched loop launches kCovBlocks blocks per pair and its solve reads
+// cov_blocks(n) rows: the small-cloud grid (<= 32768 / (8 kBS) = 16 blocks)
+// must fit in it
+static_assert(kCovBlocks >= (32768 + 8 * kBS - 1) / (8 * kBS), "RST_COV_BLOCKS below the small-cloud grid");
 __device__ __forceinline__ void cov_ref_body(const float4* __restrict__ srco, const float4* __restrict__ corr,
                                              int64_t n, int64_t n_total, const IcpState* __restrict__ st,
                                              double* __restrict__ slab, int nblk) {
@@ -1581,6 +1585,10 @@ __device__ __forceinline__ void icp_fb_body(const BvhView& bv, const AdjView& av
     } else if constexpr (!Acc::kSums) {
       return;
     }
+  } else if constexpr (!Acc::kSums) {
+    // (the small-cloud REF path scans the counts per block above; a block
+    // without an entry then has nothing to fold either)
+    if (!__syncthreads_or(e0 < e1 || nfar > 0)) return;
   }
   int r0 = e0, nleft = 0, fdone = 0;
   while (true) {
@@ -2101,6 +2109,9 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
   }
 
   if (!chain) RST_HIP(hipMemsetAsync(&ctx->d_state->guard, 0, sizeof(int32_t), st));
+  // (walk statistics of this align only: short chains leave theirs zero)
+  if (ctx->seq_trace && ctx->d_sqstats && !chain)
+    RST_HIP(hipMemsetAsync(ctx->d_sqstats, 0, sizeof(int32_t) * 64 * kQTrace, st));
   InitArgs ia;
   memcpy(ia.pose, pose_in, sizeof(ia.pose));
   ia.mu0 = opts.mu0;
@@ -2161,7 +2172,10 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
   // blocks scan the few queue counts themselves, no prefix launch (RefAcc:
   // no sums, results independent of the grid)
   const bool small_fb = refsum && n_local <= small_fb_n();
-  const int fb_grid_small = fb_grid_ref_single();  // (r10c: 2 blocks per kernel-1 block, 231 vs 111 us a cold iteration)
+  // (the single REF align's grid, fb_grid_ref_single: a grid sized to the
+  // cloud -- r10c, 2 blocks per kernel-1 block -- spread the cold iterations'
+  // queue over too few waves, 231 vs 111 us a cold iteration)
+  const int fb_grid_small = fb_grid_ref_single();
 
   const BvhView bv = view_of(tgt);
   const bool timing = ctx->timing && opts.max_iter > 0;
@@ -2200,8 +2214,8 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
         if (small_fb) {
           // small clouds (the reference callers' 5 cm voxels): no prefix
           // launch -- each fallback block scans the few queue counts itself
-          // -- over a grid sized to the cloud (RefAcc folds no sums: the
-          // grid moves no bit)
+          // (<= 2 x 128 for n <= 32768) and, with no entry, returns (RefAcc
+          // folds no sums: the grid moves no bit)
           k_icp_fb<RefAcc, false><<<fb_grid_small, kBS, fb_lds, st>>>(bv, av, tgt->pix, aa, src->pts,
                                                                       ctx->d_state, nnq, cert, qbuf, qcnt, nblk,
                                                                       prm.lane_min, slab, slab2, n_local);
@@ -2279,6 +2293,10 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
     RST_CHECK(mark(3));
   }
   RST_HIP(hipGetLastError());
+  // sharded: a bound check that tripped on one rank fails the align on every
+  // rank (the relay hands the other ranks NaN sums, which alone
+  // would read as the reference's false there)
+  if (comm) RST_CHECK(comm_agree_guard(comm, st, &ctx->d_state->guard));
   RST_HIP(hipMemcpyAsync(ctx->h_state, ctx->d_state, sizeof(IcpState), hipMemcpyDeviceToHost, st));
   if (graph) {
     hipGraph_t g = nullptr;
@@ -2347,6 +2365,7 @@ int icp_finish(rst_ctx* ctx, float pose_inout[16], float* mean_cost, int32_t* it
     ctx->last_kernel_launches = cnt;
   }
   const IcpState& h = *ctx->h_state;
+  ctx->last_iters = h.iter;
   if (h.guard & kGuardLayout) {  // (every rank of the communicator alike)
     set_last_error(hipSuccess, "sharded align: a shard size changed while n_total did not (pass the new "
                    "n_total, or 0, on every rank)", __FILE__, __LINE__);

@@ -158,6 +158,7 @@ struct rst_ctx {
   float last_kernel_ms = 0.f;
   float last_iter_ms[3] = {0.f, 0.f, 0.f};  // k_icp_nn | k_icp_fb | the rest of the iteration
   int32_t last_kernel_launches = 0;
+  int32_t last_iters = 0;  // iterations the last finished align ran (rst_ctx_last_iterations)
   // hipGraph replay of the ICP iteration loop (rst_ctx_enable_graphs):
   // (pyramid level, iterations, P2PLANE, RST_SUM_REF) -> executable graph,
   // updated in place per align
@@ -380,6 +381,11 @@ int comm_shard_layout(rst_comm* comm, int64_t n_local, int64_t n_total_hint, hip
 // after k_init_state: this align's gathered counts against the cached
 // layout, kGuardLayout into *d_guard on a mismatch (every rank alike)
 int comm_layout_check(rst_comm* comm, hipStream_t st, int32_t* d_guard);
+// after the loop: every rank's guard word ORed into every rank's (one
+// all-gather of an int32 per rank), so a bound check that tripped on one
+// rank -- the sequential sums' tables, an index guard -- fails the align on
+// all of them alike (no rank goes on to a collective the others skip)
+int comm_agree_guard(rst_comm* comm, hipStream_t st, int32_t* d_guard);
 // the sequential sums of the ranks' consecutive stretches (d_x: this rank's,
 // n_local elements) relayed rank to rank: d_out[0..nch) the whole chains'
 // sums on every rank; d_drift: 4 doubles carried between iterations (or null)

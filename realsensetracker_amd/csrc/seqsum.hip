@@ -2285,7 +2285,11 @@ int seqsum_enqueue(const float4* d_x, int64_t n, int nch, void* ws, float* d_out
     return RST_OK;
   }
   if (whole && n <= kSmallMax && ((stages & kSqForceSmall) || (!forced && n <= small_max()))) {
-    k_sq_small<<<nch, kSmT, 0, st>>>(d_x, n, nch, stretch ? stretch->p0 : nullptr, s0, d_out, d_guard, d_stats);
+    // (its own stats layout -- phase clocks, group / leaf counts -- only for
+    // rst_debug_seq_sum's forced path; the loop's per-chain walk stats stay
+    // zero for such chains, rst_debug.h)
+    k_sq_small<<<nch, kSmT, 0, st>>>(d_x, n, nch, stretch ? stretch->p0 : nullptr, s0, d_out, d_guard,
+                                     (stages & kSqForceSmall) ? d_stats : nullptr);
     RST_HIP(hipGetLastError());
     return RST_OK;
   }

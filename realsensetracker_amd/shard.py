@@ -5,15 +5,19 @@ scaling of AlignIcp3d (align_icp.cpp:92-153) to one node:
 
 * the target index is replicated (every rank builds it from the same frame);
 * the source splits into contiguous shards, ``shard_bounds``;
-* per iteration every rank reduces its 16 (P2POINT_REF) / 30 (P2PLANE) fp64
-  partial sums to one row and ONE RCCL all-reduce over xGMI makes them
-  global; every rank then solves the same pose (no broadcast);
+* RST_SUM_FP64 / RST_P2PLANE: per iteration every rank reduces its 16 / 30
+  fp64 partial sums (P2PLANE: the 6x6 / 6x1 normal equations) to one row
+  and ONE RCCL all-reduce over xGMI makes them global; every rank then
+  solves the same pose (no broadcast);
 * the reference-rounding mode (RST_SUM_REF, the library default): the shards
-  are contiguous stretches of the source order, so each iteration every rank
-  all-gathers the correspondences (16 B per source point) into the whole
-  source's order and walks the sequential fp32 sums redundantly -- the same
-  bit-exact dst_mean and cost on every rank -- and the 9 covariance sums are
-  all-reduced.
+  are contiguous stretches of the source order, and a sequential fp32 sum is
+  one chain through them in rank order, so the chains' *values* travel
+  instead of the correspondences (comm.hip comm_relay_seqsum): an all-gather
+  of each rank's fp64 chain totals (32 B) seeds every rank's maps of its own
+  stretch, rank r - 1 sends rank r the exact chain values at its stretch
+  start (16 B), rank r walks its stretch and sends the end on, the last rank
+  broadcasts the sums (16 B) -- the same bit-exact dst_mean and cost on
+  every rank -- and the 9 covariance sums are all-reduced.
 
 Host logic only: the RCCL communicator is created from a unique id that
 rank 0 draws and broadcasts -- through ``rendezvous.Rendezvous`` (TCP; what

@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 export GPU_MAX_HW_QUEUES=${GPU_MAX_HW_QUEUES:-24}
 TAG=${TAG:-bab}
-B="--no-cpu --no-p2plane --no-gicp --ref-steps ${REFSTEPS:-48} --roof-steps 1 --no-host-api --batch 8 --inflight 4 --steps ${STEPS:-96}"
+B="--no-cpu --no-p2plane --no-gicp --no-sharded --ref-steps ${REFSTEPS:-48} --roof-steps 1 --no-host-api --batch 8 --inflight 4 --steps ${STEPS:-96}"
 for V in default ${VARIANTS}; do
   if [ "$V" = default ]; then LIBV=""; else LIBV="$PWD/realsensetracker_amd/lib/variants/$V.so"; fi
   RST_LIB=$LIBV timeout -k 10 300 python bench.py $B > gpurun_out/${TAG}_${V}.log 2>&1 || { tail -5 gpurun_out/${TAG}_${V}.log; exit 1; }

@@ -19,7 +19,7 @@ step() {  # name, limit, command...
 [ -n "$SKIP_TESTS" ] || step pytest_gpu 600 python -u -m pytest tests/ -x -v -m gpu --timeout 300 --timeout-method thread
 # PMC passes (FETCH / WRITE, batched NN kernels) of the 720p reference loop and
 # the 640x480 point-to-plane stream, before their bench lines (which read them)
-PMCB="--steps 6 --warmup 1 --batch 8 --inflight 1 --no-cpu --no-p2plane --no-host-api --no-gicp --ref-steps 0"
+PMCB="--steps 6 --warmup 1 --batch 8 --inflight 1 --no-cpu --no-p2plane --no-host-api --no-gicp --no-sharded --ref-steps 0"
 pmc() {  # key, Acc, bench args...
   local key=$1 acc=$2; shift 2
   step pmcf_$key 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcf_${TAG}_$key -o run -- python3 bench.py $PMCB "$@"
@@ -33,6 +33,6 @@ pmc stream_640x480_p2plane P2PlaneAcc --mode p2plane
 step bench_pyramid 300 python bench.py --workload pyramid --graphs --no-p2plane --steps 96
 step bench_sharded 300 python bench.py --workload sharded --steps 5 --warmup 1
 step bench_sharded_fp64 300 python bench.py --workload sharded --steps 5 --warmup 1 --sum-mode fp64
-step bench_720p 300 python bench.py --width 1280 --height 720 --no-host-api --no-gicp
-step bench_720p_p2plane 300 python bench.py --width 1280 --height 720 --mode p2plane --no-host-api --no-gicp
-step bench_p2plane 300 python bench.py --mode p2plane --no-host-api --no-gicp
+step bench_720p 300 python bench.py --width 1280 --height 720 --no-host-api --no-gicp --no-sharded
+step bench_720p_p2plane 300 python bench.py --width 1280 --height 720 --mode p2plane --no-host-api --no-gicp --no-sharded
+step bench_p2plane 300 python bench.py --mode p2plane --no-host-api --no-gicp --no-sharded

@@ -8,7 +8,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 export GPU_MAX_HW_QUEUES=${GPU_MAX_HW_QUEUES:-24}
 TAG=${TAG:-dvar}
-B="--no-cpu --no-p2plane --no-gicp --ref-steps 0 --roof-steps 1 --no-host-api --batch 8 --inflight 4 --steps 96"
+B="--no-cpu --no-p2plane --no-gicp --no-sharded --ref-steps 0 --roof-steps 1 --no-host-api --batch 8 --inflight 4 --steps 96"
 for V in default ${VARIANTS}; do
   if [ "$V" = default ]; then LIBV=""; else LIBV="$PWD/realsensetracker_amd/lib/variants/$V.so"; fi
   echo "== $V"

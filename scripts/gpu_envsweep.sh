@@ -3,7 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-B="--no-cpu --no-p2plane --no-gicp --ref-steps 0 --no-host-api --steps 20 --warmup 5"
+B="--no-cpu --no-p2plane --no-gicp --no-sharded --ref-steps 0 --no-host-api --steps 20 --warmup 5"
 run() {  # name, env..., -- , args
   local name=$1; shift
   env "$@" timeout -k 10 300 python bench.py $B $EXTRA > gpurun_out/env_$name.log 2>&1 || { tail -3 gpurun_out/env_$name.log; exit 1; }

@@ -17,8 +17,8 @@ step() {  # name, limit, command...
   echo "$name rc=$rc"; tail -2 gpurun_out/${TAG}_$name.log | cut -c1-300
   [ $rc -eq 0 ] || exit $rc
 }
-SHORT="--steps 6 --warmup 1 --no-cpu --no-p2plane --no-host-api --no-gicp --ref-steps 0"
-PMCB="--steps 6 --warmup 1 --batch 8 --inflight 1 --no-cpu --no-p2plane --no-host-api --no-gicp --ref-steps 0"
+SHORT="--steps 6 --warmup 1 --no-cpu --no-p2plane --no-host-api --no-gicp --no-sharded --ref-steps 0"
+PMCB="--steps 6 --warmup 1 --batch 8 --inflight 1 --no-cpu --no-p2plane --no-host-api --no-gicp --no-sharded --ref-steps 0"
 step pytest_gpu 900 python -u -m pytest tests/ -x -v -m gpu --timeout 300 --timeout-method thread
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 # the PMC passes first, so that the bench line below carries this build's

@@ -5,7 +5,7 @@ set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${TAG:-fbit}
-B="--no-cpu --no-p2plane --no-gicp --ref-steps 0 --roof-steps 1 --no-host-api --batch 8 --inflight 1 --steps 8 --warmup 1"
+B="--no-cpu --no-p2plane --no-gicp --no-sharded --ref-steps 0 --roof-steps 1 --no-host-api --batch 8 --inflight 1 --steps 8 --warmup 1"
 for V in default ${VARIANTS}; do
   if [ "$V" = default ]; then LIBV=""; else LIBV="$PWD/realsensetracker_amd/lib/variants/$V.so"; fi
   RST_LIB=$LIBV timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/fbit_${TAG}_$V -o run -- python3 bench.py $B > /dev/null 2>&1 || exit 1

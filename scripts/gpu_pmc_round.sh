@@ -10,7 +10,7 @@ export TMPDIR=/tmp
 # preloaded library makes before bench.py runs: set it here, not in bench.py
 export GPU_MAX_HW_QUEUES=24
 TAG=${TAG:-pmc}
-SHORT="--inflight 1 --steps 6 --warmup 1 --no-cpu --no-p2plane --no-host-api --no-gicp --ref-steps 0 --roof-steps 0"
+SHORT="--inflight 1 --steps 6 --warmup 1 --no-cpu --no-p2plane --no-host-api --no-gicp --no-sharded --ref-steps 0 --roof-steps 0"
 run() {  # name, limit, rocprof args...
   local name=$1 lim=$2; shift 2
   timeout -s KILL "$lim" rocprofv3 "$@" --output-format csv -d gpurun_out/${TAG}_$name -o run -- python3 bench.py $SHORT > gpurun_out/${TAG}_$name.log 2>&1

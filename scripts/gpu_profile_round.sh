@@ -17,7 +17,7 @@ step() {  # name, limit, command...
   echo "$name rc=$rc"; tail -3 gpurun_out/${TAG}_$name.log
   [ $rc -eq 0 ] || exit $rc
 }
-SHORT="--steps 6 --warmup 1 --no-cpu --no-p2plane --no-host-api --no-gicp"
+SHORT="--steps 6 --warmup 1 --no-cpu --no-p2plane --no-host-api --no-gicp --no-sharded"
 step pytest_gpu 600 python -u -m pytest tests/ -x -v -m gpu --timeout 120 --timeout-method thread
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 600 python bench.py

@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 export GPU_MAX_HW_QUEUES=${GPU_MAX_HW_QUEUES:-24}
 TAG=${TAG:-var}
 TESTS=${TESTS:-tests/test_gpu_batch.py}
-B="--no-cpu --no-p2plane --no-gicp --ref-steps 0 --no-host-api --steps 20 --warmup 5"
+B="--no-cpu --no-p2plane --no-gicp --no-sharded --ref-steps 0 --no-host-api --steps 20 --warmup 5"
 for V in default ${VARIANTS}; do
   if [ "$V" = default ]; then LIBV=""; else LIBV="$PWD/realsensetracker_amd/lib/variants/$V.so"; fi
   echo "== $V"
@@ -17,7 +17,7 @@ for V in default ${VARIANTS}; do
   [ $rc -eq 0 ] || { grep -E "Error|assert|FAILED" gpurun_out/${TAG}_${V}_tests.log | head -30; exit $rc; }
   RST_LIB=$LIBV timeout -k 10 300 python bench.py $B > gpurun_out/${TAG}_${V}_bench.log 2>&1 || { tail -5 gpurun_out/${TAG}_${V}_bench.log; exit 1; }
   python3 -c "import json;d=json.loads(open('gpurun_out/${TAG}_${V}_bench.log').read().strip().splitlines()[-1]);print('$V value', round(d['value']), 'ok', d['pairs_ok'], 'kernels', {k: round(v, 1) for k, v in d['roofline']['kernels_avg_us'].items()})"
-  RST_LIB=$LIBV timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/iter_${TAG}_${V} -o run -- python3 bench.py --batch 0 --inflight 1 --steps 3 --warmup 1 --no-cpu --no-p2plane --no-host-api --no-gicp --ref-steps 0 > gpurun_out/${TAG}_${V}_iter.log 2>&1 || { tail -5 gpurun_out/${TAG}_${V}_iter.log; exit 1; }
+  RST_LIB=$LIBV timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/iter_${TAG}_${V} -o run -- python3 bench.py --batch 0 --inflight 1 --steps 3 --warmup 1 --no-cpu --no-p2plane --no-host-api --no-gicp --no-sharded --ref-steps 0 > gpurun_out/${TAG}_${V}_iter.log 2>&1 || { tail -5 gpurun_out/${TAG}_${V}_iter.log; exit 1; }
   python3 scripts/iter_profile_all.py $(find gpurun_out/iter_${TAG}_${V} -name "*kernel_trace.csv") > gpurun_out/${TAG}_${V}_iteration_profile.txt
   head -9 gpurun_out/${TAG}_${V}_iteration_profile.txt | cut -c1-170
   tail -2 gpurun_out/${TAG}_${V}_iteration_profile.txt | cut -c1-300

@@ -89,6 +89,25 @@ def sharded_icp_ref(src, dst, tree, max_iter, lo, hi, allgather, allreduce):
     return T
 
 
+def sharded_p2plane(src, tree, normals, max_iter, lo, hi, allreduce, eps=1e-6):
+    """The north_star's sharded loop in the point-to-plane mode (the
+    structure of icp.hip's comm branch with P2PlaneAcc): each rank's shard
+    [lo, hi) gives its 6x6 / 6x1 normal equations (+ count, sum d2), ONE
+    all-reduce of those 29 doubles a step, and every rank runs the same
+    Cholesky solve and pose update (orc_p2plane_update) -- no broadcast."""
+    Rd, td = np.eye(3), np.zeros(3)
+    it = 0
+    for it in range(1, max_iter + 1):
+        part = (O.p2plane_partials(src[lo:hi], tree, normals, Rd, td) if hi > lo else np.zeros(29))
+        ok, Rd, td, xn, _ = O.p2plane_update(allreduce(part), Rd, td)
+        assert ok
+        if xn < eps:
+            break
+    T = np.eye(4, dtype=np.float32)
+    T[:3, :3], T[:3, 3] = Rd.astype(np.float32), td.astype(np.float32)
+    return T, it
+
+
 def _worker(rank, world, port, out, mode="fp64"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -114,6 +133,9 @@ def _worker(rank, world, port, out, mode="fp64"):
 
         if mode == "ref":
             T = sharded_icp_ref(src, dst, tree, 32, lo, hi, allgather, allreduce)
+        elif mode == "p2plane":
+            T, _ = sharded_p2plane(src, tree, O.compute_normals(dst, 16, tree=tree), 30, lo, hi,
+                                   allreduce)
         else:
             T = sharded_icp(src, dst, tree, 32, lo, hi, allreduce)
         poses = [None] * world
@@ -163,6 +185,31 @@ def test_sharded_ref_decomposition_gloo(world):
     assert max(pose_err(r["poses"][0], T1)) <= 1e-6
     _, To, _, _ = O.align_icp(g["src"], g["dst"], 32, sum_mode=0)
     e = pose_err(T1, To)
+    assert max(e) <= 1e-6, e
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_p2plane_decomposition_gloo(world):
+    """Point-to-plane sharded as the north_star asks: per iteration one
+    all-reduce of the 6x6 / 6x1 normal equations (29 doubles here; 30 on the
+    device) over gloo.  Every rank ends on the bitwise-same pose, within 1e-6
+    of the unsharded oracle loop (orc_align_p2plane: the same sums in another
+    association)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    mp.start_processes(_worker, args=(world, port, q, "p2plane"), nprocs=world,
+                       start_method="spawn", join=True)
+    r = q.get()
+    assert all(np.array_equal(p, r["poses"][0]) for p in r["poses"])
+    g = load_golden("pair_80x60_s0")
+    tree = O.KDTree(g["dst"])
+    nrm = O.compute_normals(g["dst"], 16, tree=tree)
+    T1, it1 = sharded_p2plane(g["src"], tree, nrm, 30, 0, len(g["src"]), lambda x: x)
+    ito, To, _ = O.align_p2plane(g["src"], g["dst"], nrm, 30, tree=tree)
+    assert ito == it1 and ito > 1
+    assert np.array_equal(T1, To)  # one shard: orc_align_p2plane's own sums, bit for bit
+    e = pose_err(r["poses"][0], To)
     assert max(e) <= 1e-6, e
 
 
@@ -237,10 +284,13 @@ def test_ref_sums_relay_gloo(world):
     want = np.add.accumulate(np.concatenate([np.zeros((1, 4), np.float32), x]), axis=0,
                              dtype=np.float32)[-1].view(np.uint32).tolist()
     assert all(g[0] == want for g in got), (got, want)
-    # (every rank's superblock jumps: most hit with the fp64-prefix guesses;
-    # a stretch's first superblock starts from the raw fp64 prefix -- no
-    # previous iteration's drift in this one-shot chain -- and at 8 ranks of
-    # 15k elements those are a quarter of the tries: 99 / 128 measured)
+    # (every rank's superblock jumps: most hit with the fp64-prefix guesses.
+    # A stretch's first superblock starts from the raw fp64 prefix -- no
+    # previous iteration's drift in this one-shot chain -- so each (rank,
+    # chain) may miss its first one: at 8 ranks of 15k elements those are a
+    # quarter of the tries, 99 / 128 hits measured.  The other superblocks
+    # must hit >= 80 %.)
     hits = sum(sum(h for _, h in g[1]) for g in got)
     tries = sum(sum(t for t, _ in g[1]) for g in got)
-    assert hits >= (0.75 if world >= 8 else 0.8) * tries, (hits, tries)
+    first = sum(sum(1 for t, _ in g[1] if t > 0) for g in got)  # one first superblock per walked chain
+    assert hits >= 0.8 * (tries - first), (hits, tries, first)

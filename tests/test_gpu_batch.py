@@ -86,10 +86,11 @@ def test_batch_of_one_and_reuse(ctx, frames):
 # ---- the bench's value path at its own size ------------------------------------------
 # bench.py's value leg: consecutive 640x480 frames of the seeded trajectory
 # (render_frames(seed=0): trajectory(i), noise_seed i), frame k the source of
-# pair k and the target of pair k + 1, 8 pairs per rst_icp_align_batch_async,
-# 128 RST_SUM_REF iterations (align_icp.cpp:92-153 as rs_replay_app.cpp:246-251
-# calls it); here also a ragged 4-pair batch (the tail of a run whose pair
-# count is not a multiple of 8).
+# pair k and the target of pair k + 1, 16 pairs per rst_icp_align_batch_async
+# (bench.py's default --batch at 640x480), 128 RST_SUM_REF iterations
+# (align_icp.cpp:92-153 as rs_replay_app.cpp:246-251 calls it); here also an
+# 8-pair batch (rounds 4-5's shape) and a ragged 4-pair batch (the tail of a
+# run whose pair count is not a multiple of the batch).
 
 
 def _batch_seq_trace(ctx, pair, n):
@@ -105,10 +106,10 @@ def _batch_seq_trace(ctx, pair, n):
 def bench_frames():
     K = driver.intrinsics(640, 480)
     sc = driver.SyntheticScene(0)  # bench.py render_frames(seed=rank 0, stride 1)
-    return K, [sc.render(sc.trajectory(i), K, noise_seed=i) for i in range(13)]
+    return K, [sc.render(sc.trajectory(i), K, noise_seed=i) for i in range(17)]
 
 
-@pytest.mark.parametrize("first,nb,traced", [(1, 8, (0, 7)), (9, 4, (3,))])
+@pytest.mark.parametrize("first,nb,traced", [(1, 16, (0, 15)), (1, 8, (7,)), (13, 4, (3,))])
 def test_bench_batch_640_ref_bitexact(ctx, bench_frames, first, nb, traced):
     """Pairs (frame k, frame k - 1), k = first .. first + nb - 1, in one
     lockstep batch: every pair's pose, mean cost, status and iteration count
@@ -145,6 +146,63 @@ def test_bench_batch_640_ref_bitexact(ctx, bench_frames, first, nb, traced):
             assert np.array_equal(got[p].pose, To) or np.abs(got[p].pose - To).max() <= 1e-6, p
     finally:
         O.set_threads(1)
+    for x in t:
+        x.free()
+
+
+def test_bench_batch_640_poses_vs_gate_fixture(ctx, bench_frames):
+    """The value's 16-pair batch in both sum modes against the oracle poses
+    of tests/golden/fp64_gate.json (the same 16 bench pairs, 128 iterations):
+    RST_SUM_REF equals the reference arithmetic's pose on every pair (the
+    north_star's 1e-4 gate; measured identical), RST_SUM_FP64 the fp64-sum
+    oracle's within 2e-5 -- and, like it, lies outside the gate of the
+    reference arithmetic on most pairs (the measured reason the gated lines
+    run RST_SUM_REF)."""
+    import json
+    from conftest import GOLDEN
+    from posemetric import pose_err
+    fx = json.loads((GOLDEN / "fp64_gate.json").read_text())["stream_640x480"][:16]
+    K, deps = bench_frames
+    t = _targets(ctx, K, deps[:17])
+    srcs, dsts = t[1:], t[:-1]
+    ref = A.align_batch_async(srcs, dsts, ctx, None,
+                              L.default_opts(max_iter=128, sum_mode=L.RST_SUM_REF)).wait()
+    f64 = A.align_batch_async(srcs, dsts, ctx, None,
+                              L.default_opts(max_iter=128, sum_mode=L.RST_SUM_FP64)).wait()
+    outside = 0
+    for k in range(16):
+        assert fx[k]["pair"] == k + 1 and fx[k]["n"] == len(srcs[k])
+        e_ref = pose_err(ref[k].pose, np.array(fx[k]["pose_ref"]))
+        e_64 = pose_err(f64[k].pose, np.array(fx[k]["pose_fp64"]))
+        assert max(e_ref) <= 1e-6, (k, e_ref)
+        assert max(e_64) <= 2e-5, (k, e_64)
+        gap = pose_err(f64[k].pose, ref[k].pose)
+        outside += int(max(gap) > 1e-4)
+    assert outside >= 8, outside
+    for x in t:
+        x.free()
+
+
+@pytest.mark.parametrize("normals_k", [-2, 16])
+def test_bench_batch_640_p2plane_16(ctx, bench_frames, normals_k):
+    """bench.py's `p2plane` leg at its own shape: 16 consecutive 640x480
+    pairs in one lockstep batch, point-to-plane to convergence (<= 30
+    iterations; image-grid and kNN-16 normals, the leg's two variants) --
+    every pair's pose, mean cost, status and iteration count bit-identical to
+    its single align (the batch folds each pair's 6x6 / 6x1 partial sums in
+    the single align's block order)."""
+    K, deps = bench_frames
+    t = _targets(ctx, K, deps[:17], normals_k)
+    srcs, dsts = t[1:], t[:-1]
+    opts = L.default_opts(mode=L.RST_P2PLANE, max_iter=30)
+    got = A.align_batch_async(srcs, dsts, ctx, None, opts).wait()
+    assert len(got) == 16
+    for k in range(16):
+        one = A.align_prepared_async(srcs[k], dsts[k], ctx, None, opts).wait()
+        assert got[k].ok == one.ok and one.ok, k
+        assert got[k].iterations == one.iterations, (k, got[k].iterations, one.iterations)
+        assert np.array_equal(got[k].pose, one.pose), (k, got[k].pose, one.pose)
+        assert got[k].mean_cost == one.mean_cost, k
     for x in t:
         x.free()
 

@@ -161,10 +161,11 @@ def test_pyramid_720p_graphs(ctx, sum_mode):
 def test_callers_workload_ref_inloop(ctx, voxel):
     """The reference callers' own sizes (rs_replay_app.cpp:229,246-251:
     RemoveNans, DownsampleVoxel 0.05 of both clouds, the 4-argument
-    AlignIcp3d 128): ~15k points, four superblocks of the map pipeline
-    per chain -- every iteration's sums bit-exact again; at 10 cm (~4k
-    points, the tracker's voxel, rs_tracker.cpp) the one-wavefront replay
-    k_sq_serial takes the sums instead, bit-exact the same way."""
+    AlignIcp3d 128): ~15k points, each chain's sums in one workgroup of
+    k_sq_small (seqsum.hip: chains of <= 16,384 elements, maps and walk in
+    LDS) -- every iteration's sums bit-exact again; at 10 cm (~4k points, the
+    tracker's voxel, rs_tracker.cpp) the one-wavefront replay k_sq_serial
+    takes the sums instead, bit-exact the same way."""
     K = driver.intrinsics(640, 480)
     da, db, _ = driver.make_pair(driver.SyntheticScene(0), K, seed=10)
     # the recorded clouds keep every pixel, invalid ones at the origin
@@ -177,7 +178,7 @@ def test_callers_workload_ref_inloop(ctx, voxel):
     ocur = O.downsample_voxel(O.remove_nans(raw[1]), voxel)
     oprv = O.downsample_voxel(O.remove_nans(raw[0]), voxel)
     assert np.array_equal(cur, ocur) and np.array_equal(prv, oprv)
-    # 5 cm: above the replay's 8192 (the map pipeline); 10 cm: below it
+    # 5 cm: above the replay's 8192 (k_sq_small); 10 cm: below it
     assert (8192 < len(cur) <= 16384) if voxel == 0.05 else (1000 < len(cur) <= 8192), len(cur)
     hctx = A.get_context()
     _enable_seq_trace(hctx, True)

@@ -188,6 +188,129 @@ def test_configs3_1M_shards(ctx):
         L.lib().rst_comm_destroy(comm)
 
 
+def _comm1(ctx):
+    uid = C.create_string_buffer(L.COMM_ID_BYTES)
+    L.check(L.lib().rst_comm_get_unique_id(uid), "uid")
+    comm = C.c_void_p()
+    L.check(L.lib().rst_comm_create(ctx.handle, uid, 1, 0, C.byref(comm)), "comm")
+    return comm
+
+
+def _sharded(ctx, comm, src, tgt, o):
+    """rst_icp_align_sharded_device over one rank's shard (here: all of it)."""
+    ds = A.DeviceBuffer.from_array(np.ascontiguousarray(src, np.float32), ctx)
+    try:
+        buf = L.pose_to_cm(np.eye(4))
+        mc = C.c_float(0)
+        st = L.check(L.lib().rst_icp_align_sharded_device(ctx.handle, comm, C.c_void_p(ds.ptr), len(src),
+                                                          tgt.handle, C.byref(o), L.fptr(buf),
+                                                          C.byref(mc)), "sharded")
+        return st, L.cm_to_pose(buf), mc.value
+    finally:
+        ctx.synchronize()
+        ds.free()
+
+
+@pytest.mark.parametrize("size", ["640x480", "1000x1000"])
+def test_sharded_p2plane_one_rank(ctx, size):
+    """The north_star's multi-GPU path itself: point-to-plane with the
+    source sharded and ONE RCCL all-reduce of the 6x6 / 6x1 normal equations
+    (30 doubles) per iteration (rst_icp_align_sharded_device, icp.hip's comm
+    branch: k_reduce_solve reduces only, ncclAllReduce, k_solve_only).  At
+    one rank the all-reduce is an identity, so the pose, mean cost and status
+    equal the unsharded loop's bit for bit -- at 640x480 and at configs[3]'s
+    ~1M points -- and the pose is within 1e-6 of the C restatement's."""
+    w, h = map(int, size.split("x"))
+    K, pa, pb, D = _pair(w, h, 5 if w == 640 else 2, 21 if w == 640 else 7)
+    t = A.Target.build(pa, ctx)
+    t.compute_normals(16)
+    o = L.default_opts(mode=L.RST_P2PLANE, max_iter=30)
+    r = A.align(pb, t, None, o)
+    assert r.ok
+    comm = _comm1(ctx)
+    try:
+        st, pose, mc = _sharded(ctx, comm, pb, t, o)
+        st2, pose2, _ = _sharded(ctx, comm, pb, t, o)  # cached layout, second align
+    finally:
+        L.lib().rst_comm_destroy(comm)
+    assert st == L.RST_OK and st2 == L.RST_OK
+    assert np.array_equal(pose, r.pose) and np.array_equal(pose2, r.pose), (pose, r.pose)
+    assert np.float32(mc) == np.float32(r.mean_cost)
+    if w == 640:
+        nrm = t.normals()
+        it, To, _ = O.align_p2plane(pb, pa, nrm, max_iter=30, eps=o.p2plane_eps, mu=o.p2plane_mu,
+                                    max_dist=o.p2plane_max_dist, tree=O.KDTree(pa))
+        e = pose_err(pose, To)
+        print(f"sharded P2PLANE {size}: {r.iterations} vs {it} iterations, vs restatement {e}")
+        assert max(e) <= 1e-6, e
+    for x in (t,):
+        x.free()
+
+
+def test_sharded_p2plane_frame_target_640(ctx):
+    """The same path on the bench's kind of target -- a 640x480 frame with
+    image-grid normals, searched through its pixel windows.  A sharded align
+    takes the narrow lone-pair window caps (kPixHalfLone), so its points
+    split differently between the search kernels' fp64 partial-sum rows: the
+    pose matches the unsharded loop and the C restatement to 1e-6, not bit
+    for bit."""
+    K = driver.intrinsics(640, 480)
+    da, db, D = driver.make_pair(driver.SyntheticScene(5), K, seed=21)
+    ba, bb = A.DeviceBuffer.from_array(da, ctx), A.DeviceBuffer.from_array(db, ctx)
+    tf = A.Target.from_depth_device(ba.ptr, K, -2, ctx)
+    sf = A.Target.from_depth_device(bb.ptr, K, 0, ctx)
+    o = L.default_opts(mode=L.RST_P2PLANE, max_iter=30)
+    r = A.align_prepared(sf, tf, None, o)
+    pb = driver.unproject(db, K)
+    comm = _comm1(ctx)
+    try:
+        st, pose, _ = _sharded(ctx, comm, pb, tf, o)
+    finally:
+        L.lib().rst_comm_destroy(comm)
+    assert st == L.RST_OK and r.ok
+    e = pose_err(pose, r.pose)
+    K4 = [K.fx, K.fy, K.cx, K.cy]
+    pa = O.unproject(da, K4)
+    it, To, _ = O.align_p2plane(O.unproject(db, K4), pa, tf.normals(), max_iter=30,
+                                eps=o.p2plane_eps, mu=o.p2plane_mu, max_dist=o.p2plane_max_dist,
+                                tree=O.KDTree(pa))
+    eo = pose_err(pose, To)
+    g = pose_err(pose, D)
+    print(f"sharded P2PLANE frame target: vs unsharded {e}, vs restatement {eo}, vs truth {g}")
+    assert max(e) <= 1e-6 and max(eo) <= 1e-6, (e, eo)
+    for x in (tf, sf, ba, bb):
+        x.free()
+
+
+def test_sharded_seqsum_guard_is_an_error(ctx, pair640):
+    """A tripped bound check of the sequential sums' tables inside the sharded
+    REF relay (forced by rst_debug_seqsum_fault) is RST_E_HIP from the sharded
+    align -- after comm_agree_guard has ORed every rank's guard word into every
+    rank's, so all ranks fail the align together -- and the same
+    communicator aligns normally once the hook is off."""
+    from realsensetracker_amd.shard import ShardedAligner
+    pa, pb, D, t = pair640
+    f = L.lib().rst_debug_seqsum_fault
+    f.restype, f.argtypes = C.c_int, [C.c_void_p, C.c_int32]
+    sh = ShardedAligner(ctx, world=1, rank=0)
+    ds = A.DeviceBuffer.from_array(pb, ctx)
+    o = L.default_opts(max_iter=8, sum_mode=L.RST_SUM_REF)
+    try:
+        L.check(f(ctx.handle, 4), "rst_debug_seqsum_fault")
+        try:
+            with pytest.raises(L.RstError) as ei:
+                sh.align(ds.ptr, len(pb), t, o, n_total=len(pb))
+            assert "sequential-sum" in str(ei.value)
+        finally:
+            L.check(f(ctx.handle, 0), "rst_debug_seqsum_fault")
+        ok, pose, _ = sh.align(ds.ptr, len(pb), t, o, n_total=len(pb))
+        r = A.align(pb, t, None, o)
+        assert ok and np.array_equal(pose, r.pose)
+    finally:
+        sh.close()
+        ds.free()
+
+
 def test_configs2_1280x720_tracks_oracle(ctx):
     """BASELINE configs[2] (1280x720, ~900k points): the device loop with
     fp64 sums against the fp64-sum oracle, and the NN at the final pose
