@@ -1977,6 +1977,13 @@ static int fb_grid_ref_single() {
   return g;
 }
 
+// a single REF align's window caps (icp_launch; run-time env)
+static float single_cap(const char* name, float def) {
+  const char* e = getenv(name);
+  const float v = e ? (float)atof(e) : def;
+  return v >= 0.f && v <= 64.f ? v : def;
+}
+
 static int fb_grid_size() {
   static const int g = [] {
     const char* e = getenv("RST_FB_BLOCKS");
@@ -2161,8 +2168,15 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
   // chip (batches, aligns in flight); a sharded align is one large pair alone,
   // latency-bound, and takes the narrow ones (r11: the 1M pair 2,517 it/s with
   // 4 / 6 pixels, 2,267 with 20 / 24)
-  aa.pix_half = comm ? kPixHalfLone : 0.f;
-  aa.row_half = comm ? kRowHalfLone : 0.f;
+  // A single REF align takes them too (the batches' 20-px
+  // cap made a lone 640x480 pair's steady k_icp_nn 70-93 us, its widest
+  // lanes' windows; RefAcc folds no sums, so the cap moves no bit -- the
+  // fp64 / point-to-plane loops keep the batch's caps, their single and
+  // batched aligns must agree bit for bit).  RST_PIX_HALF_SINGLE /
+  // RST_ROW_HALF_SINGLE (run-time env) override them; 0 = the batch caps.
+  const bool lone = comm || refsum;
+  aa.pix_half = lone ? (comm ? kPixHalfLone : single_cap("RST_PIX_HALF_SINGLE", kPixHalfLone)) : 0.f;
+  aa.row_half = lone ? (comm ? kRowHalfLone : single_cap("RST_ROW_HALF_SINGLE", kRowHalfLone)) : 0.f;
   const AdjView av = adj_of(tgt);
   const size_t fb_lds = 2 * sizeof(int) * ((size_t)nblk + 1);
 
