@@ -91,6 +91,9 @@ constexpr int kPixChunk = RST_PIX_CHUNK;
 #ifndef RST_NN_MIN_WAVES
 #define RST_NN_MIN_WAVES 5  // k_icp_nn occupancy hint (waves per SIMD; 6 with 320-pixel chunks spilled: 32.9k)
 #endif
+#ifndef RST_CERT_EAGER
+#define RST_CERT_EAGER 0  // k_icp_nn: load cert[] beside nnq[] (not after its flag)
+#endif
 #ifndef RST_SQ_FUSE_FRONT
 #define RST_SQ_FUSE_FRONT 0  // REF loop: the front kernel without the totals launch, the previous iteration's tile prefixes (r04b: front + totals 14.5 -> 13.3 us, but the walk +1 ms per pair: stale guesses in the first iterations)
 #endif
@@ -157,7 +160,29 @@ __device__ __forceinline__ int xcd_tile(int b, int nb) {
 // kFarBit (the last search needed more than the leaf adjacency: the next
 // search goes straight to the wave-wide deep search)
 constexpr int kFarBit = 1 << 29;
+#ifndef RST_PIX_DEFER
+#define RST_PIX_DEFER 0
+#endif
+#if RST_PIX_DEFER
+// kIdBit: the neighbour came from a pixel window of a frame target and nnq
+// holds its ORIGINAL index, not its sorted position -- k_icp_nn skips the
+// window's dependent inverse-map load (pix_resolve), k_icp_fb converts the
+// few it reads (nnq_pos).  RefAcc / P2PointAcc only (P2PLANE reads the
+// sorted normals at the position).
+constexpr int kIdBit = 1 << 28;
+constexpr int kPosMask = kIdBit - 1;
+#else
+constexpr int kIdBit = 0;
 constexpr int kPosMask = kFarBit - 1;
+#endif
+// an nnq word's sorted position (-1 kept; original indices mapped through
+// the frame's inverse map)
+__device__ __forceinline__ int nnq_pos(int w, const int32_t* __restrict__ inv, int m) {
+  if (w < 0) return w;
+  const int p = w & kPosMask;
+  if (kIdBit && (w & kIdBit)) return (inv && (uint32_t)p < (uint32_t)m) ? inv[p] : m;
+  return p;
+}
 constexpr int kFbBlocks = 2048;  // largest fallback grid (RST_FB_BLOCKS)
 constexpr int kFbBatchRef = 64;
 constexpr int kFbRefSingle = 1536;  // a single REF align's fallback grid (fb_grid_ref_single)  // a batch's REF fallback grid per pair (fb_grid_batch_ref)
@@ -773,7 +798,13 @@ __device__ __forceinline__ void icp_nn_body(const BvhView& bv, const AdjView& av
   const float4 tq = act ? nnq[i] : make_float4(0.f, 0.f, 0.f, i2f(-1));
   const int wb = f2i(tq.w);
   const bool has_cert = wb >= 0 && (wb & kCertBit);
+#if RST_CERT_EAGER
+  // (the certificate loaded beside nnq, not after its flags: one memory
+  // round trip before the test instead of two; unused when the flag is off)
+  const float4 c = act ? cert[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+#else
   const float4 c = (act && has_cert) ? cert[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+#endif
   float px, py, pz;
   xform(u.P, s.x, s.y, s.z, px, py, pz);  // align_icp.cpp:107
   const bool fin = finite3(px, py, pz);
@@ -942,23 +973,26 @@ __device__ __forceinline__ void icp_nn_body(const BvhView& bv, const AdjView& av
     constexpr float kPixHalfDef = std::is_same<Acc, RefAcc>::value ? RST_PIX_MAX_HALF_REF : RST_PIX_MAX_HALF;
     const float kPixHalf = aa.pix_half > 0.f ? aa.pix_half : kPixHalfDef;
     bool pok;
+    constexpr bool defer = RST_PIX_DEFER && !std::is_same<Acc, P2PlaneAcc>::value;
     if (RST_PIX_I0_HALF > 0.0f && st->iter == 0)  // (uniform)
-      pok = pix_tile_search<kPixChunk, RST_PIX_I0_CHUNKS>(bv, pv, need, px, py, pz, d0, pr, pq, pscr[wid], prc,
-                                                           RST_PIX_I0_HALF);
+      pok = pix_tile_search<kPixChunk, RST_PIX_I0_CHUNKS, !defer>(bv, pv, need, px, py, pz, d0, pr, pq, pscr[wid],
+                                                                  prc, RST_PIX_I0_HALF);
     else
-      pok = cold ? pix_tile_search<kPixChunk, RST_PIX_COLD_CHUNKS>(bv, pv, need, px, py, pz, d0, pr, pq,
-                                                                   pscr[wid], prc, RST_PIX_COLD_HALF)
-                 : pix_tile_search<kPixChunk, RST_PIX_CHUNKS>(bv, pv, need, px, py, pz, d0, pr, pq, pscr[wid],
-                                                              prc, kPixHalf);
+      pok = cold ? pix_tile_search<kPixChunk, RST_PIX_COLD_CHUNKS, !defer>(bv, pv, need, px, py, pz, d0, pr, pq,
+                                                                          pscr[wid], prc, RST_PIX_COLD_HALF)
+                 : pix_tile_search<kPixChunk, RST_PIX_CHUNKS, !defer>(bv, pv, need, px, py, pz, d0, pr, pq,
+                                                                     pscr[wid], prc, kPixHalf);
 #if RST_NN_CLK
     ck2 = __builtin_amdgcn_s_memtime();
 #endif
     if (pok) {
       const float g = cert_bound(pr, prc);
-      const int pos = pr.pos[0];
+      // (deferred: the original index, kIdBit -- compared with the last
+      // word in the same form; a changed form counts as a change)
+      const int pos = defer ? (pr.id[0] | kIdBit) : pr.pos[0];
       nnq[i] = make_float4(pq.x, pq.y, pq.z, i2f(pos | (g > 0.f ? kCertBit : 0)));
       if (g > 0.f) cert[i] = make_float4(px, py, pz, g);
-      Acc::add(v, bv, aa, u, s, px, py, pz, pr.d[0], pos, pq, wb >= 0 && pos == (wb & kPosMask));
+      Acc::add(v, bv, aa, u, s, px, py, pz, pr.d[0], pos, pq, wb >= 0 && pos == (wb & (kPosMask | kIdBit)));
       need = false;
     }
 #if RST_DIAG
@@ -1622,8 +1656,7 @@ __device__ __forceinline__ void icp_fb_body(const BvhView& bv, const AdjView& av
         s = src[i];
         xform(u.P, s.x, s.y, s.z, px, py, pz);
         fin = finite3(px, py, pz);  // (kernel 1 queues finite queries only)
-        int warm = f2i(nnq[i].w);
-        if (warm >= 0) warm &= kPosMask;
+        int warm = nnq_pos(f2i(nnq[i].w), pv.inv, bv.m);
         if (warm >= bv.m) {
           atomicOr(&st->guard, 2);
           warm = -1;
@@ -1749,8 +1782,7 @@ __device__ __forceinline__ void icp_fb_body(const BvhView& bv, const AdjView& av
       float px, py, pz;
       xform(u.P, s.x, s.y, s.z, px, py, pz);
       if (try1) {  // seeds as the lanes': the last neighbour and its sorted neighbour
-        int warm = f2i(nnq[di].w);
-        if (warm >= 0) warm &= kPosMask;
+        int warm = nnq_pos(f2i(nnq[di].w), pv.inv, bv.m);
         if (warm >= bv.m) {
           if (lane == 0) atomicOr(&st->guard, 2);
           warm = -1;
@@ -2051,7 +2083,7 @@ int icp_launch(rst_ctx* ctx, const rst_target* src, const rst_target* tgt,
   // are walked over the all-gathered correspondences, comm.hip)
   const bool refsum = !p2plane && opts.sum_mode == RST_SUM_REF;
   if (!tgt->has_bvh) return RST_E_ARG;
-  if (tgt->m >= kCertBit) return RST_E_ARG;  // positions carry kCertBit
+  if (tgt->m > kPosMask) return RST_E_ARG;  // positions / indices below the nnq flags
   if (p2plane && !tgt->nrm) return RST_E_STATE;
   int64_t n_local = src->m;
   int64_t n_total = n_local;
@@ -2455,7 +2487,7 @@ int icp_launch_batch(rst_ctx* ctx, int nb, const rst_target* const* src, const r
   std::vector<int> run;
   for (int p = 0; p < nb; ++p) {
     if (!src[p] || !tgt[p]) return RST_E_ARG;
-    if (!tgt[p]->has_bvh || tgt[p]->m >= kCertBit) return RST_E_ARG;
+    if (!tgt[p]->has_bvh || tgt[p]->m > kPosMask) return RST_E_ARG;
     if (p2plane && !tgt[p]->nrm) return RST_E_STATE;
     const int64_t n = src[p]->m;
     if (n < 3 || tgt[p]->m < 3 || (p2plane && n < 6)) continue;
@@ -2740,7 +2772,7 @@ int icp_debug_partials(rst_ctx* ctx, const rst_target* src, const rst_target* tg
   const bool p2plane = opts.mode == RST_P2PLANE;
   if (opts.mode != RST_P2POINT_REF && opts.mode != RST_P2PLANE) return RST_E_ARG;
   if (!p2plane && opts.sum_mode != RST_SUM_FP64) return RST_E_ARG;  // no shard decomposition
-  if (!tgt->has_bvh || tgt->m < 1 || tgt->m >= kCertBit) return RST_E_ARG;
+  if (!tgt->has_bvh || tgt->m < 1 || tgt->m > kPosMask) return RST_E_ARG;
   if (p2plane && !tgt->nrm) return RST_E_STATE;
   const int64_t n = src->m;
   *nv = p2plane ? kNP2Plane : kNP2Point;

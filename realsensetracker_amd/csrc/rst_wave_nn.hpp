@@ -1418,7 +1418,7 @@ __device__ __forceinline__ int row_max_i(int x) {
 // wave whose queries straddle a jump of the Morton order), laid out one
 // after the other; a wave needing more than MaxChunks chunks leaves its
 // lanes (false).  The whole wave calls it.
-template <int N, int MaxChunks>
+template <int N, int MaxChunks, bool Resolve = true>
 __device__ __forceinline__ bool pix_tile_search(const BvhView& bv, const PixView& pv, bool act,
                                                 float qx, float qy, float qz, float d0, Best2& r,
                                                 float4& q0, PixScratch<N>& ts, float& rc,
@@ -1534,7 +1534,9 @@ __device__ __forceinline__ bool pix_tile_search(const BvhView& bv, const PixView
     }
     wave_sync();
   }
-  if (ok) pix_resolve(bv, pv, r);
+  // (!Resolve: r.pos stays kPosPending / -1 -- the caller keeps r.id, the
+  // original indices, and maps them itself when it needs positions)
+  if (Resolve && ok) pix_resolve(bv, pv, r);
   // (the seed lies in the window, so the first is within rc; checked anyway)
   return ok && r.pos[0] >= 0 && margin_sqrt(r.d[0]) * 1.00001f + 1e-30f < rc;
 }
