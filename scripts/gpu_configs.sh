@@ -33,6 +33,7 @@ pmc stream_640x480_p2plane P2PlaneAcc --mode p2plane
 step bench_pyramid 300 python bench.py --workload pyramid --graphs --no-p2plane --steps 96
 step bench_sharded 300 python bench.py --workload sharded --steps 5 --warmup 1
 step bench_sharded_fp64 300 python bench.py --workload sharded --steps 5 --warmup 1 --sum-mode fp64
+step bench_sharded_p2plane 300 python bench.py --workload sharded --steps 5 --warmup 1 --mode p2plane
 step bench_720p 300 python bench.py --width 1280 --height 720 --no-host-api --no-gicp --no-sharded
 step bench_720p_p2plane 300 python bench.py --width 1280 --height 720 --mode p2plane --no-host-api --no-gicp --no-sharded
 step bench_p2plane 300 python bench.py --mode p2plane --no-host-api --no-gicp --no-sharded
