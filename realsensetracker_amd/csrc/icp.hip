@@ -1094,11 +1094,76 @@ struct PairArgs {
   int32_t lane_min;
 };
 
+// The batched kernels read their pointers from a device array, and a
+// pointer loaded from memory is a generic (flat) one: every load and store
+// of the inlined bodies then became flat_load / flat_store (r19: k_icp_nn_b
+// 141 flat and 0 global memory instructions; the single-pair k_icp_nn, its
+// pointers kernel arguments, 160 global).  A flat access counts on lgkmcnt
+// as well as vmcnt, so each LDS or scalar wait in the pixel windows'
+// staging (ds_bpermute shuffles, LDS reads) also waited for every memory
+// load in flight.  The pointers are read back as global (address space 1)
+// pointers instead -- they only ever hold hipMalloc'd memory -- and the
+// compiler's address-space inference carries that into the bodies
+// (as_glb, rst_device.hpp).
+__device__ __forceinline__ BvhView glb(const BvhView& b) {
+  BvhView r = b;
+  r.pts = as_glb(b.pts);
+  r.nodes = as_glb(b.nodes);
+  r.codes = as_glb(b.codes);
+  r.lstart = as_glb(b.lstart);
+  r.pleaf = as_glb(b.pleaf);
+  r.bbox = as_glb(b.bbox);
+  return r;
+}
+__device__ __forceinline__ AdjView glb(const AdjView& a) {
+  AdjView r = a;
+  r.ent = as_glb(a.ent);
+  r.reach = as_glb(a.reach);
+  r.ent2 = as_glb(a.ent2);
+  r.reach2 = as_glb(a.reach2);
+  r.ent3 = as_glb(a.ent3);
+  r.reach3 = as_glb(a.reach3);
+  return r;
+}
+__device__ __forceinline__ PixView glb(const PixView& v) {
+  PixView r = v;
+  r.map = as_glb(v.map);
+  r.pts = as_glb(v.pts);
+  r.inv = as_glb(v.inv);
+  return r;
+}
+__device__ __forceinline__ AccArgs glb(const AccArgs& a) {
+  AccArgs r = a;
+  r.nrm = as_glb(a.nrm);
+  r.corr = as_glb(a.corr);
+  return r;
+}
+// pair z's arguments with every pointer global
+__device__ __forceinline__ PairArgs glb_pair(const PairArgs& A) {
+  PairArgs r = A;
+  r.bv = glb(A.bv);
+  r.av = glb(A.av);
+  r.pv = glb(A.pv);
+  r.aa = glb(A.aa);
+  r.src = as_glb(A.src);
+  r.st = as_glb(A.st);
+  r.nnq = as_glb(A.nnq);
+  r.cert = as_glb(A.cert);
+  r.qbuf = as_glb(A.qbuf);
+  r.qcnt = as_glb(A.qcnt);
+  r.slab = as_glb(A.slab);
+  r.slab2 = as_glb(A.slab2);
+  r.srco = as_glb(A.srco);
+  r.corr = as_glb(A.corr);
+  return r;
+}
+
 template <class Acc>
 __global__ __launch_bounds__(kBS, RST_NN_MIN_WAVES) void k_icp_nn_b(const PairArgs* __restrict__ pa) {
   const PairArgs& A = pa[blockIdx.z];
   if ((int)blockIdx.x >= A.nb1) return;  // (uniform: the grid fits the batch's largest pair)
-  icp_nn_body<Acc>(A.bv, A.av, A.pv, A.aa, A.src, A.n, A.st, A.nnq, A.cert, A.qbuf, A.qcnt, A.slab, A.nb1);
+  icp_nn_body<Acc>(glb(A.bv), glb(A.av), glb(A.pv), glb(A.aa), as_glb(A.src), A.n, as_glb(A.st), as_glb(A.nnq),
+                   as_glb(A.cert), as_glb(A.qbuf), as_glb(A.qcnt), as_glb(A.slab), A.nb1);
 }
 
 // Kabsch solve (align_icp.cpp:139-151; SolveKabsch :58-69): fp64 SVD,
@@ -1834,19 +1899,19 @@ __global__ __launch_bounds__(kBS, Acc::kFbMinWaves) void k_icp_fb(BvhView bv, Ad
 
 // the batch forms (PairArgs, pair = blockIdx.z)
 __global__ __launch_bounds__(kBS) void k_queue_prefix_b(const PairArgs* __restrict__ pa) {
-  const PairArgs& A = pa[blockIdx.z];
+  const PairArgs A = glb_pair(pa[blockIdx.z]);
   queue_prefix_body(A.qcnt, A.nb1, A.st);
 }
 
 template <class Acc>
 __global__ __launch_bounds__(kBS, Acc::kFbMinWaves) void k_icp_fb_b(const PairArgs* __restrict__ pa) {
-  const PairArgs& A = pa[blockIdx.z];
+  const PairArgs A = glb_pair(pa[blockIdx.z]);
   icp_fb_body<Acc>(A.bv, A.av, A.pv, A.aa, A.src, A.st, A.nnq, A.cert, A.qbuf, A.qcnt, A.nb1, A.lane_min,
                    A.slab, A.slab2, A.n);
 }
 
 __global__ __launch_bounds__(kBS) void k_cov_ref_b(const PairArgs* __restrict__ pa) {
-  const PairArgs& A = pa[blockIdx.z];
+  const PairArgs A = glb_pair(pa[blockIdx.z]);
   const int nb = cov_blocks(A.n);
   if ((int)blockIdx.x >= nb) return;
   cov_ref_body(A.srco, A.corr, A.n, A.n_total, A.st, A.slab2, nb);
@@ -1854,7 +1919,7 @@ __global__ __launch_bounds__(kBS) void k_cov_ref_b(const PairArgs* __restrict__ 
 
 template <class Acc>
 __global__ __launch_bounds__(kRedBS) void k_reduce_solve_b(const PairArgs* __restrict__ pa, int rows2max) {
-  const PairArgs& A = pa[blockIdx.z];
+  const PairArgs A = glb_pair(pa[blockIdx.z]);
   const int rows = std::is_same<Acc, RefAcc>::value ? cov_blocks(A.n) : rows2max;
   reduce_solve_body<Acc>(A.slab, 0, A.slab2, rows, A.prm, A.st, nullptr);
 }

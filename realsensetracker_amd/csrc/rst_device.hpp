@@ -11,9 +11,31 @@
 #include <cfloat>
 #include <cstdint>
 
+#include <type_traits>
+
 #include "rst_bvh.hpp"
 
 namespace rst {
+
+// A pointer field of an argument struct read from device memory, typed as a
+// global (address space 1) pointer: a pointer loaded from memory is generic,
+// and every access through it a flat_load / flat_store -- which counts on
+// lgkmcnt as well as vmcnt, so each LDS or scalar wait also waits for the
+// memory loads in flight.  Only for fields that hold hipMalloc'd memory
+// (null stays null).  The round trip through an integer keeps the compiler
+// from folding the cast away; its address-space inference carries "global"
+// into the inlined bodies (the batched kernels, icp.hip / seqsum.hip).
+#ifndef RST_FLAT_ARGS
+#define RST_FLAT_ARGS 0  // 1: the batched kernels' accesses flat again (measurement only)
+#endif
+template <class P>
+__device__ __forceinline__ P as_glb(const P& field) {
+  if (RST_FLAT_ARGS) return field;
+  using T = typename std::remove_pointer<P>::type;
+  typedef __attribute__((address_space(1))) T GT;
+  GT* g = (GT*)(uintptr_t)field;
+  return (P)g;
+}
 
 constexpr int kWave = 64;
 

@@ -1683,8 +1683,31 @@ struct SqPair {
   float* out;
   SqView v;
 };
+// (every table pointer read back as a global pointer: as_glb, rst_device.hpp
+// -- loaded from the SqPair array they were generic, and the batched
+// kernels' accesses flat)
 __device__ __forceinline__ SqView sq_at(const SqPair& P, int nch, int iter) {
   SqView v = P.v;
+  v.soa = as_glb(P.v.soa);
+  v.wflg = as_glb(P.v.wflg);
+  v.bs = as_glb(P.v.bs);
+  v.gs = as_glb(P.v.gs);
+  v.ks = as_glb(P.v.ks);
+  v.inc = as_glb(P.v.inc);
+  v.ipre = as_glb(P.v.ipre);
+  v.tinc = as_glb(P.v.tinc);
+  v.leaf = as_glb(P.v.leaf);
+  v.grp = as_glb(P.v.grp);
+  v.sbm = as_glb(P.v.sbm);
+  v.stats = as_glb(P.v.stats);
+  v.ttot = as_glb(P.v.ttot);
+  v.ttot2 = as_glb(P.v.ttot2);
+  v.clk = as_glb(P.v.clk);
+  v.err = as_glb(P.v.err);
+  v.p0 = as_glb(P.v.p0);
+  v.s0 = as_glb(P.v.s0);
+  v.tl = as_glb(P.v.tl);
+  v.guard = as_glb(P.v.guard);
   v.nch = nch;
   v.it = iter;
   if (iter >= 0) v.ttot = v.ttot2 + (size_t)(iter & 1) * 4 * kTotQ * v.nk;
@@ -1694,7 +1717,7 @@ __global__ __launch_bounds__(kFrontT) void k_sq_tot_b(const SqPair* __restrict__
   const SqPair& p = P[blockIdx.z];
   const SqView v = sq_at(p, nch, iter);
   if ((int)blockIdx.x >= v.nk * kTotQ) return;
-  sq_tot_body(p.x, v, blockIdx.x);
+  sq_tot_body(as_glb(p.x), v, blockIdx.x);
 }
 template <bool FUSED>
 __global__ __launch_bounds__(kFrontT) void k_sq_front_b(const SqPair* __restrict__ P, int nch, int iter) {
@@ -1703,7 +1726,7 @@ __global__ __launch_bounds__(kFrontT) void k_sq_front_b(const SqPair* __restrict
   if ((int)blockIdx.x >= v.nk) return;
   if constexpr (FUSED) {  // (iter >= 1: the previous iteration's totals by parity)
     const double* tprev = v.ttot2 + (size_t)((iter - 1) & 1) * 4 * kTotQ * v.nk;
-    sq_front_body<true>(v, p.x, tprev, v.ttot, blockIdx.x, blockIdx.y);
+    sq_front_body<true>(v, as_glb(p.x), tprev, v.ttot, blockIdx.x, blockIdx.y);
   } else {
     sq_front_body<false>(v, nullptr, nullptr, nullptr, blockIdx.x, blockIdx.y);
   }
@@ -1716,7 +1739,7 @@ __global__ __launch_bounds__(kBuildT, kBuildWaves) void k_sq_build_b(const SqPai
 __global__ __launch_bounds__(kWave) void k_sq_walk_b(const SqPair* __restrict__ P, int nch, int iter) {
   const SqPair& p = P[blockIdx.z];
   const SqView v = sq_at(p, nch, iter);
-  sq_walk_body(v, p.out, blockIdx.x);
+  sq_walk_body(v, as_glb(p.out), blockIdx.x);
 }
 
 
