@@ -1397,7 +1397,31 @@ __device__ __forceinline__ float pix_seed_d2(const PixView& pv, float qx, float 
   return d;
 }
 
-// Min / max over the 16 lanes of a row.
+// Min / max over the 16 lanes of a row, every lane the result, by DPP (no
+// LDS trip: a ds_bpermute chain costs each step an LDS round trip, and in
+// the window searches' setup four such reductions ran back to back): quad
+// butterflies, then row_half_mirror (l <-> 7 - l) and row_mirror
+// (l <-> 15 - l) join the quads and the half rows.  The whole wave must be
+// active (every caller's is).
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int x) {
+  return __builtin_amdgcn_update_dpp(0, x, CTRL, 0xf, 0xf, false);
+}
+__device__ __forceinline__ int row_min_dpp(int x) {
+  x = min(x, dpp_i<kDppXor1>(x));
+  x = min(x, dpp_i<kDppXor2>(x));
+  x = min(x, dpp_i<kDppRowHalfMirror>(x));
+  return min(x, dpp_i<kDppRowMirror>(x));
+}
+__device__ __forceinline__ int row_max_dpp(int x) {
+  x = max(x, dpp_i<kDppXor1>(x));
+  x = max(x, dpp_i<kDppXor2>(x));
+  x = max(x, dpp_i<kDppRowHalfMirror>(x));
+  return max(x, dpp_i<kDppRowMirror>(x));
+}
+// row r's value (uniform within each row) at lane 16 r, as a scalar
+__device__ __forceinline__ int row_val(int x, int r) { return __builtin_amdgcn_readlane(x, 16 * r); }
+
 __device__ __forceinline__ int row_min_i(int x) {
 #pragma unroll
   for (int o = 8; o > 0; o >>= 1) x = min(x, __shfl_xor(x, o, 64));
@@ -1429,20 +1453,21 @@ __device__ __forceinline__ bool pix_tile_search(const BvhView& bv, const PixView
   rc = 0.f;
   const bool ok = act && pix_window(pv, qx, qy, qz, d0, maxh, a0, a1, b0, b1, rc);
   if (__ballot(ok) == 0) return false;
-  // the row boxes, then the wave box
-  int gA0 = row_min_i(ok ? a0 : INT_MAX), gA1 = row_max_i(ok ? a1 : INT_MIN);
-  int gB0 = row_min_i(ok ? b0 : INT_MAX), gB1 = row_max_i(ok ? b1 : INT_MIN);
+  // the row boxes (DPP, every lane of a row alike), then the wave box from
+  // the four rows' values (readlane: scalars)
+  int gA0 = row_min_dpp(ok ? a0 : INT_MAX), gA1 = row_max_dpp(ok ? a1 : INT_MIN);
+  int gB0 = row_min_dpp(ok ? b0 : INT_MAX), gB1 = row_max_dpp(ok ? b1 : INT_MIN);
   const bool gok = gA0 <= gA1;  // the row has a window
-  const int A0 = wave_min_i(gA0), A1 = wave_max_i(gA1);
-  const int B0 = wave_min_i(gB0), B1 = wave_max_i(gB1);
+  const int A0 = min(min(row_val(gA0, 0), row_val(gA0, 1)), min(row_val(gA0, 2), row_val(gA0, 3)));
+  const int A1 = max(max(row_val(gA1, 0), row_val(gA1, 1)), max(row_val(gA1, 2), row_val(gA1, 3)));
+  const int B0 = min(min(row_val(gB0, 0), row_val(gB0, 1)), min(row_val(gB0, 2), row_val(gB0, 3)));
+  const int B1 = max(max(row_val(gB1, 0), row_val(gB1, 1)), max(row_val(gB1, 2), row_val(gB1, 3)));
   if (!gok) gA0 = gA1 = gB0 = gB1 = 0;  // (an empty row box: area 0, never staged)
   const int garea = gok ? (gA1 - gA0 + 1) * (gB1 - gB0 + 1) : 0;
-  int gsum = garea, gmaxw = gok ? gA1 - gA0 + 1 : 0;
-#pragma unroll
-  for (int o = 16; o < 64; o <<= 1) {  // (rows' lanes agree: sum over rows 0..3)
-    gsum += __shfl_xor(gsum, o, 64);
-    gmaxw = max(gmaxw, __shfl_xor(gmaxw, o, 64));
-  }
+  const int gw = gok ? gA1 - gA0 + 1 : 0;
+  // (rows' lanes agree: sum / max over rows 0..3)
+  const int gsum = (row_val(garea, 0) + row_val(garea, 1)) + (row_val(garea, 2) + row_val(garea, 3));
+  const int gmaxw = max(max(row_val(gw, 0), row_val(gw, 1)), max(row_val(gw, 2), row_val(gw, 3)));
   const int warea = (A1 - A0 + 1) * (B1 - B0 + 1);
   const bool rows4 = gsum < warea;  // uniform
   if (!rows4) {
@@ -1458,10 +1483,10 @@ __device__ __forceinline__ bool pix_tile_search(const BvhView& bv, const PixView
   off[0] = 0;
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
-    bx[g] = __shfl(gA0, 16 * g, 64);
-    by[g] = __shfl(gB0, 16 * g, 64);
-    bw[g] = max(__shfl(gA1, 16 * g, 64) - bx[g] + 1, 1);
-    const int ar = rows4 ? __shfl(garea, 16 * g, 64) : (g == 0 ? warea : 0);
+    bx[g] = row_val(gA0, g);
+    by[g] = row_val(gB0, g);
+    bw[g] = max(row_val(gA1, g) - bx[g] + 1, 1);
+    const int ar = rows4 ? row_val(garea, g) : (g == 0 ? warea : 0);
     off[g + 1] = off[g] + ar;
   }
   const int mg = rows4 ? lane >> 4 : 0;  // my box
