@@ -86,29 +86,76 @@ constexpr float kWnnBigR = 0.012f;
 // object): its ordinary balls get one AABB per side of the jump.
 constexpr float kWnnJump = 0.05f;
 
+// Butterfly partners without LDS: the value of lane l's partner at level K
+// of an ASCENDING reduction -- K = 0, 1: l ^ 1, l ^ 2 (DPP quad_perm);
+// K = 2, 3: 7 - l within the half row, 15 - l within the row (DPP
+// row_half_mirror / row_mirror); K = 4, 5: the other row of the pair, the
+// other half of the wave (v_permlane16_swap / v_permlane32_swap).  After
+// levels 0..K-1 every aligned group of 2^K lanes holds one value, so the
+// mirror partner stands for the xor one; valid for merges that are
+// commutative, associative and idempotent (min, max, lexicographic top-k),
+// whose result does not depend on the order.  The whole wave must be active.
+// (r19: a ds_bpermute per exchange put an LDS round trip on every step of
+// the searches' wave reductions)
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int x) {
+  return __builtin_amdgcn_update_dpp(0, x, CTRL, 0xf, 0xf, false);
+}
+template <int K>
+__device__ __forceinline__ int bfly(int x) {
+  static_assert(K >= 0 && K <= 5, "levels 0..5 of a wave of 64");
+  if constexpr (K == 0) {
+    return dpp_i<kDppXor1>(x);
+  } else if constexpr (K == 1) {
+    return dpp_i<kDppXor2>(x);
+  } else if constexpr (K == 2) {
+    return dpp_i<kDppRowHalfMirror>(x);
+  } else if constexpr (K == 3) {
+    return dpp_i<kDppRowMirror>(x);
+  } else if constexpr (K == 4) {
+    const auto r = __builtin_amdgcn_permlane16_swap((unsigned)x, (unsigned)x, false, false);
+    return (__lane_id() & 16) ? (int)r[0] : (int)r[1];
+  } else {
+    const auto r = __builtin_amdgcn_permlane32_swap((unsigned)x, (unsigned)x, false, false);
+    return (__lane_id() & 32) ? (int)r[0] : (int)r[1];
+  }
+}
+template <int K>
+__device__ __forceinline__ float bfly(float x) {
+  return i2f(bfly<K>(f2i(x)));
+}
+// v <- op(v, partner) for levels 0 .. L-1 (L = 6: the wave, 4: rows of 16,
+// 3: groups of 8)
+template <int L, class T, class Op>
+__device__ __forceinline__ T bfly_reduce(T v, Op op) {
+  if constexpr (L > 0) v = op(v, bfly<0>(v));
+  if constexpr (L > 1) v = op(v, bfly<1>(v));
+  if constexpr (L > 2) v = op(v, bfly<2>(v));
+  if constexpr (L > 3) v = op(v, bfly<3>(v));
+  if constexpr (L > 4) v = op(v, bfly<4>(v));
+  if constexpr (L > 5) v = op(v, bfly<5>(v));
+  return v;
+}
+struct OpMinI {
+  __device__ int operator()(int a, int b) const { return min(a, b); }
+};
+struct OpMaxI {
+  __device__ int operator()(int a, int b) const { return max(a, b); }
+};
+struct OpMinF {
+  __device__ float operator()(float a, float b) const { return fminf(a, b); }
+};
+struct OpMaxF {
+  __device__ float operator()(float a, float b) const { return fmaxf(a, b); }
+};
+
 __device__ __forceinline__ float wnn_rl(float v, int l) {
   return i2f(__builtin_amdgcn_readlane(f2i(v), l));
 }
-__device__ __forceinline__ int wnn_min_i(int v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
-  return v;
-}
-__device__ __forceinline__ int wnn_max_i(int v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
-  return v;
-}
-__device__ __forceinline__ float wnn_min_f(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
-  return v;
-}
-__device__ __forceinline__ float wnn_max_f(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
-}
+__device__ __forceinline__ int wnn_min_i(int v) { return bfly_reduce<6>(v, OpMinI{}); }
+__device__ __forceinline__ int wnn_max_i(int v) { return bfly_reduce<6>(v, OpMaxI{}); }
+__device__ __forceinline__ float wnn_min_f(float v) { return bfly_reduce<6>(v, OpMinF{}); }
+__device__ __forceinline__ float wnn_max_f(float v) { return bfly_reduce<6>(v, OpMaxF{}); }
 
 // Cold lane: follow near children to one leaf and take its best point as
 // the starting bound (any real point will do; exactness comes later).
@@ -130,17 +177,9 @@ struct WnnRegion {
   }
 };
 
-// min / max over the 8 lanes of a group (xor 1, 2, 4 stays in the group)
-__device__ __forceinline__ float wnn_gmin(float v) {
-#pragma unroll
-  for (int o = 1; o < 8; o <<= 1) v = fminf(v, __shfl_xor(v, o, 64));
-  return v;
-}
-__device__ __forceinline__ float wnn_gmax(float v) {
-#pragma unroll
-  for (int o = 1; o < 8; o <<= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
-}
+// min / max over the 8 lanes of a group (levels 0-2 stay in the group)
+__device__ __forceinline__ float wnn_gmin(float v) { return bfly_reduce<3>(v, OpMinF{}); }
+__device__ __forceinline__ float wnn_gmax(float v) { return bfly_reduce<3>(v, OpMaxF{}); }
 
 // Regions of the current bounds, per 8-lane group (in LDS): the AABB of the
 // ordinary balls -- two AABBs, one per side, when the group straddles a
@@ -165,14 +204,16 @@ __device__ __forceinline__ WnnRegion wnn_regions(bool act, float qx, float qy, f
   }
   float gbest = gap;
   int gk = gl;
-#pragma unroll
-  for (int o = 1; o < 8; o <<= 1) {
-    const float og = __shfl_xor(gbest, o, 64);
-    const int ok = __shfl_xor(gk, o, 64);
+  // (the group's largest gap, lowest index on ties: a total order, so the
+  // butterfly's pairing does not matter)
+  auto gstep = [&](float og, int ok) {
     const bool take = (og > gbest) | ((og == gbest) & (ok < gk));
     gbest = take ? og : gbest;
     gk = take ? ok : gk;
-  }
+  };
+  gstep(bfly<0>(gbest), bfly<0>(gk));
+  gstep(bfly<1>(gbest), bfly<1>(gk));
+  gstep(bfly<2>(gbest), bfly<2>(gk));
   const int run = (gbest > kWnnJump * kWnnJump && gl >= gk) ? 1 : 0;
   float lx[2], ly[2], lz[2], hx[2], hy[2], hz[2];
 #pragma unroll
@@ -397,17 +438,25 @@ namespace rst {
 // points per step, one point per lane, and a lexicographic wave minimum
 // after every flush tightens the shared bound.  Latency ~ the depth of the
 // subtrees the ball touches, not the number of points in it.
+template <int K>
+__device__ __forceinline__ void lex_step1(Best1& b) {
+  const float od = bfly<K>(b.d);
+  const int oid = bfly<K>(b.id);
+  const int op = bfly<K>(b.pos);
+  const bool t = lex_less(od, oid, b.d, b.id) | ((od == b.d) & (oid == b.id) & (op > b.pos));
+  b.d = t ? od : b.d;
+  b.id = t ? oid : b.id;
+  b.pos = t ? op : b.pos;
+}
+// (a total order on (d, id, pos): the minimum does not depend on the
+// butterfly's pairing, bfly)
 __device__ __forceinline__ Best1 wave_lex_min(Best1 b) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const float od = __shfl_xor(b.d, o, 64);
-    const int oid = __shfl_xor(b.id, o, 64);
-    const int op = __shfl_xor(b.pos, o, 64);
-    const bool t = lex_less(od, oid, b.d, b.id) | ((od == b.d) & (oid == b.id) & (op > b.pos));
-    b.d = t ? od : b.d;
-    b.id = t ? oid : b.id;
-    b.pos = t ? op : b.pos;
-  }
+  lex_step1<0>(b);
+  lex_step1<1>(b);
+  lex_step1<2>(b);
+  lex_step1<3>(b);
+  lex_step1<4>(b);
+  lex_step1<5>(b);
   return b;
 }
 
@@ -415,33 +464,44 @@ __device__ __forceinline__ Best1 wave_lex_min(Best1 b) {
 // is commutative, so every lane ends with the same two entries; a point
 // held by both lists (same id) counts once.
 // (kTop = 8: the merge within each row of 16 lanes only)
+template <int K>
+__device__ __forceinline__ void lex_step2(Best2& b) {
+  const float od0 = bfly<K>(b.d[0]), od1 = bfly<K>(b.d[1]);
+  const int oi0 = bfly<K>(b.id[0]), oi1 = bfly<K>(b.id[1]);
+  const int op0 = bfly<K>(b.pos[0]), op1 = bfly<K>(b.pos[1]);
+  const bool of = lex_less(od0, oi0, b.d[0], b.id[0]);  // the other list leads
+  const float fd = of ? od0 : b.d[0];
+  const int fi = of ? oi0 : b.id[0], fp = of ? op0 : b.pos[0];
+  // second: the leader's second, or the other head (its second when the
+  // two heads are the same point)
+  const float wd = of ? od1 : b.d[1];
+  const int wi = of ? oi1 : b.id[1], wp = of ? op1 : b.pos[1];
+  const float hd = of ? b.d[0] : od0, h2d = of ? b.d[1] : od1;
+  const int hi = of ? b.id[0] : oi0, h2i = of ? b.id[1] : oi1;
+  const int hp = of ? b.pos[0] : op0, h2p = of ? b.pos[1] : op1;
+  const bool dup = hi == fi;
+  const float cd = dup ? h2d : hd;
+  const int ci = dup ? h2i : hi, cp = dup ? h2p : hp;
+  const bool c2 = lex_less(cd, ci, wd, wi);
+  b.d[0] = fd;
+  b.id[0] = fi;
+  b.pos[0] = fp;
+  b.d[1] = c2 ? cd : wd;
+  b.id[1] = c2 ? ci : wi;
+  b.pos[1] = c2 ? cp : wp;
+}
+// (the two smallest of the union: commutative, associative, idempotent --
+// the butterfly's pairing does not matter, bfly; levels 0-3 stay in a row)
 template <int kTop = 32>
 __device__ __forceinline__ Best2 wave_lex_min(Best2 b) {
-#pragma unroll
-  for (int o = kTop; o > 0; o >>= 1) {
-    const float od0 = __shfl_xor(b.d[0], o, 64), od1 = __shfl_xor(b.d[1], o, 64);
-    const int oi0 = __shfl_xor(b.id[0], o, 64), oi1 = __shfl_xor(b.id[1], o, 64);
-    const int op0 = __shfl_xor(b.pos[0], o, 64), op1 = __shfl_xor(b.pos[1], o, 64);
-    const bool of = lex_less(od0, oi0, b.d[0], b.id[0]);  // the other list leads
-    const float fd = of ? od0 : b.d[0];
-    const int fi = of ? oi0 : b.id[0], fp = of ? op0 : b.pos[0];
-    // second: the leader's second, or the other head (its second when the
-    // two heads are the same point)
-    const float wd = of ? od1 : b.d[1];
-    const int wi = of ? oi1 : b.id[1], wp = of ? op1 : b.pos[1];
-    const float hd = of ? b.d[0] : od0, h2d = of ? b.d[1] : od1;
-    const int hi = of ? b.id[0] : oi0, h2i = of ? b.id[1] : oi1;
-    const int hp = of ? b.pos[0] : op0, h2p = of ? b.pos[1] : op1;
-    const bool dup = hi == fi;
-    const float cd = dup ? h2d : hd;
-    const int ci = dup ? h2i : hi, cp = dup ? h2p : hp;
-    const bool c2 = lex_less(cd, ci, wd, wi);
-    b.d[0] = fd;
-    b.id[0] = fi;
-    b.pos[0] = fp;
-    b.d[1] = c2 ? cd : wd;
-    b.id[1] = c2 ? ci : wi;
-    b.pos[1] = c2 ? cp : wp;
+  static_assert(kTop == 8 || kTop == 32, "rows of 16 or the wave");
+  lex_step2<0>(b);
+  lex_step2<1>(b);
+  lex_step2<2>(b);
+  lex_step2<3>(b);
+  if constexpr (kTop == 32) {
+    lex_step2<4>(b);
+    lex_step2<5>(b);
   }
   return b;
 }
@@ -1082,17 +1142,8 @@ struct BallScratchT {              // per-wave LDS (~12.5 KB at C = 512)
 };
 using BallScratch = BallScratchT<kBallChunk>;
 
-__device__ __forceinline__ float wave_min_f(float x) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) x = fminf(x, __shfl_xor(x, o, 64));
-  return x;
-}
-
-__device__ __forceinline__ float wave_max_f(float x) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) x = fmaxf(x, __shfl_xor(x, o, 64));
-  return x;
-}
+__device__ __forceinline__ float wave_min_f(float x) { return bfly_reduce<6>(x, OpMinF{}); }
+__device__ __forceinline__ float wave_max_f(float x) { return bfly_reduce<6>(x, OpMaxF{}); }
 
 // The box of the active lanes' balls (radius: the first distance, rounded
 // up by the 1e-5 margins of every coverage test here, capped at
@@ -1150,7 +1201,7 @@ __device__ __forceinline__ int ball_flush(const BvhView& bv, TS& ts, int nlv, fl
       const int y = __shfl_up(inc, o, kWave);
       if (lane >= o) inc += y;
     }
-    const int total = __shfl(inc, kWave - 1, kWave);
+    const int total = __builtin_amdgcn_readlane(inc, kWave - 1);
     const int off = inc - c;
     const int g = lane >> 4, o = lane & 15;
     for (int k0 = 0; k0 < l1 - l0; k0 += 4) {  // one leaf per 16 lanes
@@ -1319,17 +1370,8 @@ __device__ __forceinline__ void pix_resolve(const BvhView& bv, const PixView& pv
   if (r.pos[1] >= 0) r.pos[1] = (uint32_t)r.id[1] < (uint32_t)bv.m ? pv.inv[r.id[1]] : -1;
 }
 
-__device__ __forceinline__ int wave_min_i(int x) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) x = min(x, __shfl_xor(x, o, 64));
-  return x;
-}
-
-__device__ __forceinline__ int wave_max_i(int x) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) x = max(x, __shfl_xor(x, o, 64));
-  return x;
-}
+__device__ __forceinline__ int wave_min_i(int x) { return bfly_reduce<6>(x, OpMinI{}); }
+__device__ __forceinline__ int wave_max_i(int x) { return bfly_reduce<6>(x, OpMaxI{}); }
 
 // The pixel window of the ball (q, r), r = max(the seed distance sqrt(d0)
 // with margins, RST_PIX_MIN_PX level pixels): false when it is too large
@@ -1403,36 +1445,13 @@ __device__ __forceinline__ float pix_seed_d2(const PixView& pv, float qx, float 
 // butterflies, then row_half_mirror (l <-> 7 - l) and row_mirror
 // (l <-> 15 - l) join the quads and the half rows.  The whole wave must be
 // active (every caller's is).
-template <int CTRL>
-__device__ __forceinline__ int dpp_i(int x) {
-  return __builtin_amdgcn_update_dpp(0, x, CTRL, 0xf, 0xf, false);
-}
-__device__ __forceinline__ int row_min_dpp(int x) {
-  x = min(x, dpp_i<kDppXor1>(x));
-  x = min(x, dpp_i<kDppXor2>(x));
-  x = min(x, dpp_i<kDppRowHalfMirror>(x));
-  return min(x, dpp_i<kDppRowMirror>(x));
-}
-__device__ __forceinline__ int row_max_dpp(int x) {
-  x = max(x, dpp_i<kDppXor1>(x));
-  x = max(x, dpp_i<kDppXor2>(x));
-  x = max(x, dpp_i<kDppRowHalfMirror>(x));
-  return max(x, dpp_i<kDppRowMirror>(x));
-}
+__device__ __forceinline__ int row_min_dpp(int x) { return bfly_reduce<4>(x, OpMinI{}); }
+__device__ __forceinline__ int row_max_dpp(int x) { return bfly_reduce<4>(x, OpMaxI{}); }
 // row r's value (uniform within each row) at lane 16 r, as a scalar
 __device__ __forceinline__ int row_val(int x, int r) { return __builtin_amdgcn_readlane(x, 16 * r); }
 
-__device__ __forceinline__ int row_min_i(int x) {
-#pragma unroll
-  for (int o = 8; o > 0; o >>= 1) x = min(x, __shfl_xor(x, o, 64));
-  return x;
-}
-
-__device__ __forceinline__ int row_max_i(int x) {
-#pragma unroll
-  for (int o = 8; o > 0; o >>= 1) x = max(x, __shfl_xor(x, o, 64));
-  return x;
-}
+__device__ __forceinline__ int row_min_i(int x) { return bfly_reduce<4>(x, OpMinI{}); }
+__device__ __forceinline__ int row_max_i(int x) { return bfly_reduce<4>(x, OpMaxI{}); }
 
 // act: the lane holds a finite query and d0 = the squared distance of some
 // target point (its seed).  On true, r (empty on entry) holds the lane's
