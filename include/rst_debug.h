@@ -44,6 +44,11 @@ int rst_debug_seq_walk_stats(rst_ctx* ctx, int32_t* out, int32_t n);
  * would.  An align whose sums tripped a check returns RST_E_HIP (with
  * rst_last_error's detail), never the reference's false. */
 int rst_debug_seqsum_fault(rst_ctx* ctx, int32_t bits);
+/* The sequential sums' DPP scans (seqsum.hip wave_scan_incl /
+ * block_scan_excl, the fp64 prefixes the maps' guesses come from) on one
+ * wave: in[0..64) -> out[0..64) inclusive scan; in[64..128) -> out[64..128)
+ * exclusive scan, out[128] the total. */
+int rst_debug_wave_scan(rst_ctx* ctx, const double* in, double* out);
 /* The context's reduction slab (first n doubles) as the last align left
  * it: diagnostics builds write kernel clocks there (tools/nn_clock.py). */
 int rst_debug_slab(rst_ctx* ctx, double* out, int64_t n);

@@ -402,6 +402,12 @@ int rst_debug_seqsum_fault(rst_ctx* ctx, int32_t bits) {
   return seqsum_debug_fault((int)bits);
 }
 
+int rst_debug_wave_scan(rst_ctx* ctx, const double* in, double* out) {
+  if (!ctx || !in || !out) return RST_E_ARG;
+  RST_HIP(hipSetDevice(ctx->device));
+  return seqsum_debug_wave_scan(ctx->stream, in, out);
+}
+
 int rst_debug_seq_walk_stats(rst_ctx* ctx, int32_t* out, int32_t n) {
   if (!ctx || !out || n < 0 || !ctx->d_sqstats) return RST_E_ARG;
   RST_HIP(hipSetDevice(ctx->device));

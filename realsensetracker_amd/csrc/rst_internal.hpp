@@ -335,6 +335,9 @@ int seqsum_enqueue(const float4* d_x, int64_t n, int nch, void* ws, float* d_out
                    unsigned long long* tl = nullptr, int* d_guard = nullptr);
 // diagnostics: err bits every walk adds (0 = off), to test the guard path
 int seqsum_debug_fault(int bits);
+// the sequential sums' DPP wave scan on 64 doubles (in[0..64)), and the block
+// scan on in[64..128): out[0..64) inclusive, out[64..128) exclusive, out[128] total
+int seqsum_debug_wave_scan(hipStream_t st, const double* h_in, double* h_out);
 // a batch of streams summed by one set of launches (the batched ICP loop):
 // a device array of records, one per stream (seqsum_pair_fill writes one
 // into host memory: the stream, its length, its workspace of

@@ -99,31 +99,52 @@ __device__ __forceinline__ int nf_flags(float x) {
   return 0;
 }
 
+// a double through a DPP lane move (both halves; lanes without a source,
+// or outside row_mask, get +0)
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ double dpp_d(double x) {
+  const uint2 u = __builtin_bit_cast(uint2, x);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)u.x, CTRL, ROWS, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)u.y, CTRL, ROWS, 0xf, false);
+  return __builtin_bit_cast(double, make_uint2((unsigned)lo, (unsigned)hi));
+}
+// inclusive scan of one double per lane over the wave, all by DPP (no LDS):
+// Hillis-Steele inside each row of 16 (row_shr 1, 2, 4, 8), then row 15's
+// total into rows 1 and 3 (row_bcast15) and lane 31's into rows 2 and 3
+// (row_bcast31).  The whole wave must be active.  (Its additions associate
+// differently from a serial sum: its users take these fp64 prefixes as
+// guesses only -- block starts, map candidates -- never as results.)
+__device__ __forceinline__ double wave_scan_incl(double x) {
+  x += dpp_d<0x111>(x);  // row_shr:1
+  x += dpp_d<0x112>(x);  // row_shr:2
+  x += dpp_d<0x114>(x);  // row_shr:4
+  x += dpp_d<0x118>(x);  // row_shr:8
+  x += dpp_d<0x142, 0xa>(x);  // row_bcast:15 -> rows 1, 3
+  x += dpp_d<0x143, 0xc>(x);  // row_bcast:31 -> rows 2, 3
+  return x;
+}
+
 // exclusive block scan of one double per thread (BS threads); returns the
 // prefix, *total = the block total
+// (r19: DPP scans instead of a ds_bpermute per step and thread 0's serial
+// pass over the waves' totals -- the guesses' prefixes only, see above)
 template <int BS>
 __device__ double block_scan_excl(double v, double* lds, double* total) {
+  constexpr int NW = BS / kWave;
+  static_assert(NW <= kWave, "one wave scans the waves' totals");
   const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
-  double inc = v;
-#pragma unroll
-  for (int o = 1; o < kWave; o <<= 1) {
-    const double y = __shfl_up(inc, o, kWave);
-    if (lane >= o) inc += y;
-  }
+  const double inc = wave_scan_incl(v);
   if (lane == kWave - 1) lds[w] = inc;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    double a = 0.0;
-    for (int i = 0; i < BS / kWave; ++i) {
-      const double t = lds[i];
-      lds[i] = a;
-      a += t;
-    }
-    lds[BS / kWave] = a;
+  if (w == 0) {
+    const double t = lane < NW ? lds[lane] : 0.0;
+    const double ti = wave_scan_incl(t);
+    if (lane < NW) lds[lane] = ti - t;
+    if (lane == NW - 1) lds[NW] = ti;
   }
   __syncthreads();
   const double r = lds[w] + inc - v;
-  *total = lds[BS / kWave];
+  *total = lds[NW];
   __syncthreads();
   return r;
 }
@@ -2256,6 +2277,35 @@ int seqsum_enqueue_batch(const void* d_pairs, int nbatch, int64_t nmax, int nch,
   k_sq_walk_b<<<dim3(nch, 1, nbatch), kWave, 0, st>>>(P, nch, iter);
   RST_HIP(hipGetLastError());
   return RST_OK;
+}
+
+namespace {
+// (test hook: the DPP scans on one wave of given values, rst_debug_wave_scan)
+__global__ __launch_bounds__(kWave) void k_wave_scan_test(const double* __restrict__ in, double* __restrict__ out) {
+  __shared__ double lds[kWave];
+  const int t = threadIdx.x;
+  out[t] = wave_scan_incl(in[t]);
+  double tot;
+  const double ex = block_scan_excl<kWave>(in[kWave + t], lds, &tot);
+  out[kWave + t] = ex;
+  if (t == 0) out[2 * kWave] = tot;
+}
+}  // namespace
+
+int seqsum_debug_wave_scan(hipStream_t st, const double* h_in, double* h_out) {
+  double* d = nullptr;
+  if (hipMalloc(&d, sizeof(double) * (4 * kWave + 1)) != hipSuccess) return RST_E_NOMEM;
+  int rc = RST_OK;
+  if (hipMemcpyAsync(d, h_in, sizeof(double) * 2 * kWave, hipMemcpyHostToDevice, st) != hipSuccess) rc = RST_E_HIP;
+  if (rc == RST_OK) {
+    k_wave_scan_test<<<1, kWave, 0, st>>>(d, d + 2 * kWave);
+    if (hipGetLastError() != hipSuccess ||
+        hipMemcpyAsync(h_out, d + 2 * kWave, sizeof(double) * (2 * kWave + 1), hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+      rc = RST_E_HIP;
+  }
+  (void)hipFree(d);
+  return rc;
 }
 
 int seqsum_debug_fault(int bits) {

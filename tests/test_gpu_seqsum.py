@@ -178,3 +178,24 @@ def test_small_kernel_timing(ctx):
         res[n] = t
         print(f"\nseq sums of {n} float4: " + ", ".join(f"{k} {v:.1f} us" for k, v in t.items()))
     assert res[15_239]["small"] < res[15_239]["maps"]
+
+
+def test_wave_scan_dpp(ctx):
+    """The DPP scans behind the maps' guesses (seqsum.hip wave_scan_incl,
+    block_scan_excl: row_shr / row_bcast lane moves, no LDS): an inclusive
+    and an exclusive scan of one wave of doubles and the total, against
+    numpy's -- their fp64 rounding differs from a serial sum (guesses only:
+    the sums themselves stay exact whatever the prefixes), so to 1e-12."""
+    import ctypes as C
+    rng = np.random.default_rng(5)
+    x = np.concatenate([rng.normal(size=64) * 1e3, rng.uniform(-2, 3, 64)]).astype(np.float64)
+    out = np.zeros(129, np.float64)
+    f = L.lib().rst_debug_wave_scan
+    f.restype, f.argtypes = C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]
+    L.check(f(ctx.handle, x.ctypes.data, out.ctypes.data), "rst_debug_wave_scan")
+    inc = np.cumsum(x[:64])
+    exc = np.concatenate([[0.0], np.cumsum(x[64:])[:-1]])
+    tol = 1e-12 * np.abs(x).sum()
+    assert np.max(np.abs(out[:64] - inc)) <= tol, out[:64] - inc
+    assert np.max(np.abs(out[64:128] - exc)) <= tol, out[64:128] - exc
+    assert abs(out[128] - x[64:].sum()) <= tol
