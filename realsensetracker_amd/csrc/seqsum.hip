@@ -663,7 +663,7 @@ __device__ __forceinline__ int affine_hist(int sb0, int Eb, int sh, int gb, int 
   const double val = A + (double)sg * ldexp((double)sb0, e);
   const bool okv = val == rint(val) && val >= -2147483648.0 && val < 2147483648.0;
   const int vi = okv ? (int)(int64_t)val : 0x7fc00000;
-  const int h = __shfl(vi, (lane + kWave - 1) & (kWave - 1), kWave);
+  const int h = __builtin_amdgcn_update_dpp(0, vi, 0x138, 0xf, 0xf, false);  // wave_shr:1: lane q <- q - 1 (no LDS trip)
   return lane == 0 ? sb0 : h;
 }
 
@@ -717,7 +717,7 @@ __device__ __forceinline__ bool comp_chain(float& x, double& clo, double& chi, c
     const int mkl = (1 << min(hl.m & 7, mmax)) - 1;
     const int sb0 = __builtin_amdgcn_readfirstlane((int)__float_as_uint(x));
     int hist = spec_hist(sb0, mp, ql, hl, gbl, sgl, mkl, nq);
-    const int nxb = __shfl(hist, lane + 1, kWave);
+    const int nxb = __builtin_amdgcn_update_dpp(0, hist, 0x130, 0xf, 0xf, false);  // wave_shl:1: lane q <- q + 1
     bool okl;
     double lo, hi;
     {
@@ -1291,7 +1291,7 @@ __device__ __forceinline__ int spec_chunk(float& s, const Map* maps, int nq, int
   const int sgl = gbl >> 31;
   const int mkl = (1 << min(hl.m & 7, mmax)) - 1;  // (clamped: r stays inside the entries)
   const int hist = spec_hist(__builtin_amdgcn_readfirstlane((int)__float_as_uint(s)), maps, ql, hl, gbl, sgl, mkl, nq);
-  const int nxb = __shfl(hist, lane + 1, kWave);
+  const int nxb = __builtin_amdgcn_update_dpp(0, hist, 0x130, 0xf, 0xf, false);  // wave_shl:1: lane q <- q + 1
   int okl;
   {
     const int kk = ((hist - gbl) ^ sgl) - sgl;
@@ -1586,7 +1586,7 @@ __device__ __forceinline__ void sq_walk_body(const SqView& v, float* __restrict_
     // included, so the bits differ by the offset in units), the map is usable, the
     // offset lies in the residue's window, E_r + du 2^e0 is exact
     // (Fast2Sum) and is what the step produced.
-    const int nxb = __shfl(hist, lane + 1, kWave);
+    const int nxb = __builtin_amdgcn_update_dpp(0, hist, 0x130, 0xf, 0xf, false);  // wave_shl:1: lane q <- q + 1
     int okl;
     {
       const int kk = ((hist - gbl) ^ sgl) - sgl;

@@ -19,7 +19,7 @@ step() {  # name, limit, command...
 }
 SHORT="--steps 6 --warmup 1 --no-cpu --no-p2plane --no-host-api --no-gicp --no-sharded --ref-steps 0"
 PMCB="--steps 6 --warmup 1 --batch 8 --inflight 1 --no-cpu --no-p2plane --no-host-api --no-gicp --no-sharded --ref-steps 0"
-step pytest_gpu 900 python -u -m pytest tests/ -x -v -m gpu --timeout 300 --timeout-method thread
+[ -n "$SKIP_TESTS" ] || step pytest_gpu 900 python -u -m pytest tests/ -x -v -m gpu --timeout 300 --timeout-method thread
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 # the PMC passes first, so that the bench line below carries this build's
 # traffic (bench.py reads profiles/pmc_*.json; the copy stays on the box)

@@ -7,7 +7,8 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp GPU_MAX_HW_QUEUES=${GPU_MAX_HW_QUEUES:-24}
 TAG=${TAG:-vab}
 TESTS=${TESTS:-tests/test_gpu_batch.py tests/test_gpu_configs.py}
-for V in ${TEST_DEFAULT:+default} ${VARIANTS}; do
+for V in ${TEST_DEFAULT:+default} ${NO_VARIANT_TESTS:-${VARIANTS}}; do
+  [ "$V" = 1 ] && continue
   LIBV=$PWD/realsensetracker_amd/lib/variants/$V.so; [ "$V" = default ] && LIBV=""
   RST_LIB=$LIBV timeout -k 10 600 python -u -m pytest $TESTS -x -q -m gpu \
     --timeout 300 --timeout-method thread > gpurun_out/${TAG}_${V}_tests.log 2>&1
