@@ -542,11 +542,17 @@ __device__ __forceinline__ void sq_front_body(const SqView& v, const float4* __r
 // wrong guess only costs hits), so the walk's results never depend on this
 // kernel's choices.  Leaf and group maps go to global memory for the walk's
 // descents.
-constexpr int kBuildT = 512;
-// three workgroups per CU: 24 waves, 6 per SIMD (<= 80 registers)
-constexpr int kBuildWaves = 3 * kBuildT / kWave / 4;
-static_assert(kBuildT >= kMaxSbBlocks + 1 && kBuildT >= kMaxSbGroups * kGroupR && kBuildT % kWave == 0,
-              "map workgroup size");
+// Five workgroups of 320 threads per CU (25 waves, <= 7 per SIMD: <= 72
+// registers; LDS <= 32 KB each).  r20: three of 512 threads (49 KB of LDS
+// each, the leaf maps whole) left the CU's LDS full while most of a
+// workgroup's time is one or two wavefronts' dependent composite chains --
+// the kernel was latency x residency bound (a lone superblock ~50k clocks,
+// 4.7 rounds of workgroups per 16-pair batch).  Blocks past the first 320
+// of a superblock (rare: ~256 on average) take a second round.
+constexpr int kBuildT = 320;
+constexpr int kBuildPerCU = 5;
+constexpr int kBuildWaves = (kBuildPerCU * kBuildT / kWave + 3) / 4;
+static_assert(kBuildT >= kWave && kBuildT % kWave == 0 && kBuildT > kMaxSbGroups, "map workgroup size");
 static_assert(sizeof(Leaf) == 64, "a leaf map is four int4");
 constexpr int kListCap = (kLeafR - 1) * kMaxSbBlocks;
 constexpr int16_t kNeedNone = INT16_MIN;  // kNoNeed in 16 bits
@@ -698,10 +704,10 @@ __device__ __forceinline__ int spec_hist(int sb0, const Map* maps, int ql, const
 // cannot pass (no map for it).  r06: a lane stepping through the maps with
 // an LDS read per step took ~13k clocks for a superblock's 16 groups.
 constexpr int kChainC = 16;
+// superblock candidates taken by comp_chain (more: a lane each); the group
+// composites are a lane each (r07: by comp_chain 19.7k -> 17.5k clocks a
+// group phase, the value unchanged)
 constexpr int kSbChainR = 4;
-#ifndef RST_SQ_GROUP_CHAIN
-#define RST_SQ_GROUP_CHAIN 0  // the group composites by comp_chain (else a lane each)
-#endif  // superblock candidates taken by comp_chain (more: a lane each)
 template <class Map>
 __device__ __forceinline__ bool comp_chain(float& x, double& clo, double& chi, const Map* maps, int n, int mmax) {
   const int lane = threadIdx.x & (kWave - 1);
@@ -781,12 +787,32 @@ __device__ __forceinline__ int wave_max_small(int v, int lo = 0) {
   return hi + lo;
 }
 
-// (<= 53 KB: three workgroups per CU -- the composites, a wavefront or two
-// each, beside other workgroups' leaves.  The leaves read their elements
-// from global memory themselves: r06, staged in LDS, 76 KB and two per CU)
+// A leaf map in LDS: its header and entry 0 (the only entry of ~99.7% of
+// the leaves, m = 0); entries 1..3 of the others are read from the global
+// map (written before the group phase) by the rare composite step that
+// needs them.  aux: during the leaf phase, candidate 0's lattice need.
+struct LeafL {  // 8 dwords: two int4
+  MapHdr h;
+  MapEnt e0;
+  int aux;
+};
+static_assert(sizeof(LeafL) == 32, "an LDS leaf map is two int4");
+// a group map in LDS: the global GroupMap without its padding, xo = the
+// exact-only flag (the global map's pad[0])
+struct GroupMapL {
+  MapHdr h;
+  MapEnt e[kGroupR];
+  int xo;
+};
+constexpr int kGroupMapLW = (int)(sizeof(GroupMapL) / 4);
+static_assert(kGroupMapLW == 53 && offsetof(GroupMap, pad) == 4 * 52, "GroupMapL = GroupMap's first 53 dwords");
+
+// (~31 KB: five workgroups per CU.  The leaves read their elements from
+// global memory themselves: r06, staged in LDS, 76 KB and two per CU; until
+// r20 the leaf maps whole and the group maps padded, 49 KB and three)
 struct BuildLds {
-  GroupMap gm[kMaxSbGroups];
-  Leaf lf[kMaxSbBlocks];
+  GroupMapL gm[kMaxSbGroups];
+  LeafL lf[kMaxSbBlocks];
   int sbs[kMaxSbBlocks + 1];   // block starts, relative to the superblock's first element
   int sgs[kMaxSbGroups + 1];   // group starts, relative to its first block
   int16_t xneed[kMaxSbBlocks][kLeafR - 1];  // the extra candidates' lattice needs (kNeedNone: none)
@@ -799,6 +825,7 @@ struct BuildLds {
   double base[2];              // fp64 increments of the tiles before the superblock's first
                                // tile and before the next
 };
+static_assert(sizeof(BuildLds) <= 160 * 1024 / kBuildPerCU, "the map workgroups' LDS per CU");
 
 // one monitored run of a block from candidate r: its len <= 2 kW - 1
 // elements X[a], X[a + 1], ... (the chain's SoA row, rows padded to 64
@@ -876,10 +903,11 @@ __device__ __forceinline__ void sq_build_body(const SqView& v, const int k, cons
   }
   const int ngr = gb - ga, nblk = bb - ba, nel = eb - ea;
   const float* X = v.soa + (int64_t)c * v.ns;
-  const bool act = tid < nblk;
-  const int b = ba + tid;
-  const double iv = act ? v.ipre[(int64_t)c * v.nb + b] : 0.0;
-  if (tid <= nblk) W.sbs[tid] = bsg[ba + tid] - ea;
+  const double* ipre = v.ipre + (int64_t)c * v.nb;
+  Leaf* leafg = v.leaf + (int64_t)c * v.nb + ba;  // the superblock's leaf maps (global)
+  // (the first round's increment prefixes in flight across the barrier)
+  const double iv0 = tid < nblk ? ipre[ba + tid] : 0.0;
+  for (int i = tid; i <= nblk; i += kBuildT) W.sbs[i] = bsg[ba + i] - ea;
   if (tid <= ngr) W.sgs[tid] = gsg[ga + tid] - ba;
   if (tid == 0) {
     W.nlist = 0;
@@ -899,15 +927,19 @@ __device__ __forceinline__ void sq_build_body(const SqView& v, const int k, cons
   }
   __syncthreads();
   if (tid == 0) clk[1] = (long long)__builtin_amdgcn_s_memtime();
-  // -- leaves: candidate 0 per block
-  Run p;
-  float G = 0.0f;
-  int e0 = -149, a0 = 0, len = 0;
-  bool more = false;
-  {
+  // -- leaves: candidate 0 per block, a lane each (rounds of kBuildT blocks);
+  // its header, entry and lattice need to LDS, h.m = 1 marking a block whose
+  // other candidates are listed
+  for (int b0 = 0; b0 < nblk; b0 += kBuildT) {
+    const int bi = b0 + tid;
+    const bool act = bi < nblk;
+    const int b = ba + bi;
+    float G = 0.0f;
+    int e0 = -149, a0 = 0, len = 0;
     if (act) {
-      a0 = W.sbs[tid];
-      len = W.sbs[tid + 1] - a0;
+      const double iv = b0 == 0 ? iv0 : ipre[b];
+      a0 = W.sbs[bi];
+      len = W.sbs[bi + 1] - a0;
       if (a0 < 0 || len < 1 || len > 2 * kW - 1 || a0 + len > nel) {
         atomicOr(v.err, 32);
         a0 = len = 0;
@@ -919,6 +951,7 @@ __device__ __forceinline__ void sq_build_body(const SqView& v, const int k, cons
     }
     // the wavefront's longest block bounds the unrolled steps
     const int wmax = wave_max_small<5>(len);  // (a block <= 2 kW - 1 elements)
+    Run p;
     if (wmax > 0) {
       leaf_run(p, X, v.ns, (int64_t)ea + a0, len, wmax, G, e0, 0);
     } else {
@@ -926,60 +959,63 @@ __device__ __forceinline__ void sq_build_body(const SqView& v, const int k, cons
     }
     if (act && len == 0) p.opaque = true;  // (a bad block: no map)
     const int m0 = p.need == kNoNeed ? 0 : max(0, p.need - e0);
-    more = act && !p.opaque && m0 >= 1 && m0 <= kLeafM;
+    const bool more = act && !p.opaque && m0 >= 1 && m0 <= kLeafM;
     if (more) {
       const int at = atomicAdd(&W.nlist, kLeafR - 1);
       if (at + kLeafR - 1 <= kListCap) {  // (always: kListCap covers every block)
 #pragma unroll
-        for (int r = 1; r < kLeafR; ++r) W.list[at + r - 1] = (uint16_t)(tid << 2 | r);
+        for (int r = 1; r < kLeafR; ++r) W.list[at + r - 1] = (uint16_t)(bi << 2 | r);
       } else {
         atomicOr(v.err, 64);
       }
     }
+    if (act) W.lf[bi] = LeafL{MapHdr{G, e0, more ? 1 : 0, p.opaque ? kOpaque : 0}, leaf_ent(p, e0), p.need};
   }
   __syncthreads();
   {
-    // the listed extra candidates, one lane each (rare; uniform skip)
+    // the listed extra candidates, one lane each (rare; uniform skip): their
+    // entries straight to the global map, their needs to LDS
     const int nl = min(W.nlist, kListCap);
     for (int j0 = 0; j0 < nl; j0 += kBuildT) {
       const int j = j0 + tid;
       const int code = j < nl ? W.list[j] : 0;
       const int bl = min(code >> 2, nblk - 1), r = code & 3;
       const int xa = j < nl ? W.sbs[bl] : 0, xl = j < nl ? W.sbs[bl + 1] - xa : 0;
-      const int xb = ba + bl;
-      const double base = (xb / kBlocksPerTile) == k ? W.base[0] : W.base[1];
-      const float xG = j < nl ? candidate_base(xb == 0 && !v.p0 ? 0.0f : (float)(base + v.ipre[(int64_t)c * v.nb + xb]),
-                                               kLeafR)
-                              : 0.0f;
+      const float xG = j < nl ? W.lf[bl].h.G : 0.0f;
       const int xe0 = grid_exp(xG);
       const int wmax = wave_max_small<5>(xl);
       if (wmax > 0) {
         Run q;
         leaf_run(q, X, v.ns, (int64_t)ea + xa, xl, wmax, xG, xe0, r);
         if (j < nl) {
-          W.lf[bl].e[r] = leaf_ent(q, xe0);
-          W.xneed[bl][r - 1] = q.need == kNoNeed ? kNeedNone : (int16_t)max(-32767, min(32767, q.need));
+          leafg[bl].e[r] = leaf_ent(q, xe0);
+          W.xneed[bl][r - 1] = q.need == kNeedNone ? kNeedNone : (int16_t)max(-32767, min(32767, q.need));
         }
       }
     }
   }
   __syncthreads();
-  if (act) {
-    int need = p.need;
+  // the leaf maps: lattice need over the candidates -> m; global map whole,
+  // LDS map header + entry 0
+  for (int bi = tid; bi < nblk; bi += kBuildT) {
+    const LeafL L = W.lf[bi];
+    const bool more = L.h.m != 0;
+    int need = L.aux;
     if (more)
 #pragma unroll
       for (int r = 1; r < kLeafR; ++r) {
-        const int xn = W.xneed[tid][r - 1];
+        const int xn = W.xneed[bi][r - 1];
         need = max(need, xn == kNeedNone ? kNoNeed : xn);
       }
+    const int e0 = L.h.e0;
     const int mneed = need == kNoNeed ? 0 : max(0, need - e0);
     const bool exact_only = mneed > kLeafM;
     const int m = exact_only ? 0 : mneed;
     Leaf o;
-    o.h = MapHdr{G, e0, m, p.opaque ? kOpaque : 0};
-    o.e[0] = leaf_ent(p, e0);
+    o.h = MapHdr{L.h.G, e0, m, L.h.flags};
+    o.e[0] = L.e0;
 #pragma unroll
-    for (int r = 1; r < kLeafR; ++r) o.e[r] = more ? W.lf[tid].e[r] : MapEnt{0.0f, 1, 0};
+    for (int r = 1; r < kLeafR; ++r) o.e[r] = more ? leafg[bi].e[r] : MapEnt{0.0f, 1, 0};
 #pragma unroll
     for (int r = 0; r < kLeafR; ++r) {
       if (r >= (1 << m)) {
@@ -990,23 +1026,25 @@ __device__ __forceinline__ void sq_build_body(const SqView& v, const int k, cons
         o.e[r].HIu = min(o.e[r].HIu, 0);
       }
     }
-    W.lf[tid] = o;
-    v.leaf[(int64_t)c * v.nb + b] = o;
+    W.lf[bi] = LeafL{o.h, o.e[0], 0};
+    leafg[bi] = o;
   }
   if (tid == 0) W.nlist = ngr;  // the group list: every group's candidate 0 first
   __syncthreads();
   if (tid == 0) clk[2] = (long long)__builtin_amdgcn_s_memtime();
   // -- groups: the lattice (lane per group), then lanes (group, candidate)
+  const int4* lq = reinterpret_cast<const int4*>(W.lf);  // leaf i: lq[2 i] header, lq[2 i + 1] entry 0
   if (tid < ngr) {
     const int gi = tid;
     const int c0 = W.sgs[gi], c1 = W.sgs[gi + 1];
     const bool gok = c0 >= 0 && c1 > c0 && c1 <= nblk && c1 - c0 <= 2 * kGW - 1;
-    GroupMap& o = W.gm[gi];
+    GroupMapL& o = W.gm[gi];
     int R = 1;
     if (!gok) {
       atomicOr(v.err, 2);
       W.bad = 1;
       o.h = MapHdr{0.0f, 0, 0, kOpaque};
+      o.xo = 0;
     } else {
       const MapHdr h0 = W.lf[c0].h;
       int lat = h0.e0 + h0.m;
@@ -1015,7 +1053,7 @@ __device__ __forceinline__ void sq_build_body(const SqView& v, const int k, cons
 #pragma unroll
       for (int j = 1; j < 2 * kGW - 1; ++j) {
         if (c0 + j < c1) {
-          const int4 hj = *reinterpret_cast<const int4*>(&W.lf[c0 + j].h);  // (one read, no branch)
+          const int4 hj = lq[2 * (c0 + j)];  // (one read, no branch)
           lat = (hj.w & kOpaque) ? lat : max(lat, hj.y + hj.z);
         }
       }
@@ -1025,7 +1063,7 @@ __device__ __forceinline__ void sq_build_body(const SqView& v, const int k, cons
       R = 1 << m;
       const float Gg = candidate_base(h0.G, R);
       o.h = MapHdr{Gg, grid_exp(Gg), m, 0};
-      o.pad[0] = exact_only ? 1 : 0;
+      o.xo = exact_only ? 1 : 0;
     }
     for (int r = 0; r < kGroupR; ++r) o.e[r] = MapEnt{0.0f, 1, 0};
     if (R > 1) {
@@ -1035,76 +1073,43 @@ __device__ __forceinline__ void sq_build_body(const SqView& v, const int k, cons
     }
   }
   __syncthreads();
-#if RST_SQ_GROUP_CHAIN
   {
-    // the listed (group, candidate) composites, one at a time per wavefront
-    // (comp_chain: the wavefront steps one candidate through the group's
-    // leaf maps), wavefront w taking list entries w, w + 8, ...
-    const int nl = min(W.nlist, kBuildT);
-    const int wv = tid / kWave;
-    for (int j = wv; j < nl; j += kBuildT / kWave) {
-      const int code = j < ngr ? j << 4 : W.list[j];
-      const int gi = min(code >> 4, ngr - 1), r = code & (kGroupR - 1);
-      const int c0 = W.sgs[gi], c1 = W.sgs[gi + 1];
-      const bool gok = c0 >= 0 && c1 > c0 && c1 <= nblk && c1 - c0 <= 2 * kGW - 1;
-      const MapHdr gh = W.gm[gi].h;
-      const bool exact_only = W.gm[gi].pad[0] != 0;  // (a lattice beyond kGroupM)
-      if (!gok || (gh.flags & kOpaque)) continue;
-      float x = cand(gh.G, gh.e0, r);
-      double clo = -INFINITY, chi = INFINITY;
-      if (comp_chain<Leaf>(x, clo, chi, W.lf + c0, c1 - c0, kLeafM) && lane == 0) {
-        if (exact_only) {
-          clo = fmax(clo, 0.0);
-          chi = fmin(chi, 0.0);
-        }
-        W.gm[gi].e[r] = MapEnt{x, lo_units(clo, gh.e0), hi_units(chi, gh.e0)};
-      }
-    }
-  }
-#else
-  {
-    const int nl = min(W.nlist, kBuildT);  // <= 31 x 16 <= kBuildT
-    const int j = tid;
-    if (j - lane < nl) {  // (uniform per wavefront: waves past the list skip)
+    const int nl = min(W.nlist, kMaxSbGroups * kGroupR);
+    for (int j0 = 0; j0 < nl; j0 += kBuildT) {
+      const int j = j0 + tid;
+      if (j - lane >= nl) break;  // (uniform per wavefront: waves past the list stop)
       const bool ea_ = j < nl;
       const int code = !ea_ ? 0 : (j < ngr ? j << 4 : W.list[j]);
       const int gi = code >> 4, r = code & (kGroupR - 1);
       const int c0 = W.sgs[gi], c1 = W.sgs[gi + 1];
       const bool gok = ea_ && c0 >= 0 && c1 > c0 && c1 <= nblk && c1 - c0 <= 2 * kGW - 1;
       const MapHdr gh = W.gm[gi].h;
-      const bool exact_only = W.gm[gi].pad[0] != 0;  // (a lattice beyond kGroupM)
+      const bool exact_only = W.gm[gi].xo != 0;  // (a lattice beyond kGroupM)
       float x = cand(gh.G, gh.e0, r);
       double clo = -INFINITY, chi = INFINITY;
       bool ok = gok && !(gh.flags & kOpaque);
-      // (leaf j + 1 in flight while leaf j is applied; its entry picked
-      // from registers: no LDS trip in the chain)
-      // (as four int4: a select between struct members would go through
-      // the stack)
-      const int4* lq = reinterpret_cast<const int4*>(W.lf);
+      // (leaf j + 1's header and entry 0 in flight while leaf j is applied:
+      // no LDS trip in the chain; entries 1..3 -- leaves with m >= 1 --
+      // from the global map, a uniform branch taken when a lane needs one)
       const int cc0 = gok ? c0 : 0, cc1 = gok ? c1 : 1;
-      int4 q0 = lq[4 * cc0], q1 = lq[4 * cc0 + 1], q2 = lq[4 * cc0 + 2], q3 = lq[4 * cc0 + 3];
+      int4 q0 = lq[2 * cc0], q1 = lq[2 * cc0 + 1];
       const int nst = wave_max_small<5>(cc1 - cc0);  // (a group <= 2 kGW - 1 blocks)
       for (int s = 0; s < nst; ++s) {
         const int jl = cc0 + s;
-        const int jn = 4 * min(jl + 1, cc1 - 1);
-        const int4 n0 = lq[jn], n1 = lq[jn + 1], n2 = lq[jn + 2], n3 = lq[jn + 3];
+        const int jn = 2 * min(jl + 1, cc1 - 1);
+        const int4 n0 = lq[jn], n1 = lq[jn + 1];
         const MapHdr h{__int_as_float(q0.x), q0.y, q0.z, q0.w};
         bool okj = ok && jl < cc1;
         const int kq = comp_off(x, h, kLeafM, okj);
         const int rr = kq & ((1 << (okj ? h.m : 0)) - 1);  // (m <= kLeafM when ok)
-        // (selects on the residue's bits: a chain of rr == i tests became a
-        // switch, i.e. branches)
-        const bool r0 = (rr & 1) != 0, r1 = (rr & 2) != 0;
-        MapEnt en;
-        en.E = __int_as_float(r1 ? (r0 ? q3.y : q2.z) : (r0 ? q1.w : q1.x));
-        en.LOu = r1 ? (r0 ? q3.z : q2.w) : (r0 ? q2.x : q1.y);
-        en.HIu = r1 ? (r0 ? q3.w : q3.x) : (r0 ? q2.y : q1.z);
+        MapEnt en{__int_as_float(q1.x), q1.y, q1.z};
+        if (__ballot(rr != 0) != 0) {
+          if (rr != 0) en = leafg[jl].e[rr];
+        }
         comp_apply(x, clo, chi, okj, h, kq, en);
         ok = jl < cc1 ? okj : ok;
         q0 = n0;
         q1 = n1;
-        q2 = n2;
-        q3 = n3;
       }
       if (ea_ && ok) {
         if (exact_only) {
@@ -1115,12 +1120,13 @@ __device__ __forceinline__ void sq_build_body(const SqView& v, const int k, cons
       }
     }
   }
-#endif
   __syncthreads();
   if (tid == 0) clk[3] = (long long)__builtin_amdgcn_s_memtime();
-  GroupMap* grpg = v.grp + (int64_t)c * v.ng;
-  for (int i = tid; i < ngr * (int)(sizeof(GroupMap) / 4); i += kBuildT)
-    reinterpret_cast<int*>(grpg + ga)[i] = reinterpret_cast<const int*>(W.gm)[i];
+  GroupMap* grpg = v.grp + (int64_t)c * v.ng + ga;
+  for (int i = tid; i < ngr * kGroupMapLW; i += kBuildT) {
+    const int g = i / kGroupMapLW, w = i - g * kGroupMapLW;
+    reinterpret_cast<int*>(grpg + g)[w] = reinterpret_cast<const int*>(W.gm + g)[w];
+  }
   if (tid == 0) clk[4] = (long long)__builtin_amdgcn_s_memtime();
   // -- the superblock: lanes = candidates, up to 64
   SbMap* so = v.sbm + (int64_t)c * v.nk + k;
@@ -1154,7 +1160,7 @@ __device__ __forceinline__ void sq_build_body(const SqView& v, const int k, cons
       for (int rc = 0; rc < R; ++rc) {
         float x = cand(Gs, se0, rc);
         double clo = -INFINITY, chi = INFINITY;
-        if (comp_chain<GroupMap>(x, clo, chi, W.gm, ngr, kGroupM)) {
+        if (comp_chain<GroupMapL>(x, clo, chi, W.gm, ngr, kGroupM)) {
           if (exact_only) {
             clo = fmax(clo, 0.0);
             chi = fmin(chi, 0.0);
