@@ -542,17 +542,18 @@ __device__ __forceinline__ void sq_front_body(const SqView& v, const float4* __r
 // wrong guess only costs hits), so the walk's results never depend on this
 // kernel's choices.  Leaf and group maps go to global memory for the walk's
 // descents.
-// Five workgroups of 320 threads per CU (25 waves, <= 7 per SIMD: <= 72
-// registers; LDS <= 32 KB each).  r20: three of 512 threads (49 KB of LDS
-// each, the leaf maps whole) left the CU's LDS full while most of a
-// workgroup's time is one or two wavefronts' dependent composite chains --
-// the kernel was latency x residency bound (a lone superblock ~50k clocks,
-// 4.7 rounds of workgroups per 16-pair batch).  Blocks past the first 320
-// of a superblock (rare: ~256 on average) take a second round.
+// k_sq_leaves: 320 threads (a lane per block; blocks past the first 320 of
+// a superblock -- rare: ~256 on average -- take a second round), six
+// workgroups per CU (30 waves, <= 8 per SIMD: <= 64 registers; LDS <= 26
+// KB each).  k_sq_comp: one wavefront.  r20 before the split: one workgroup
+// of 512 threads, three per CU, 38.1k it/s; of 320, five per CU, 40.8k.
 constexpr int kBuildT = 320;
-constexpr int kBuildPerCU = 5;
-constexpr int kBuildWaves = (kBuildPerCU * kBuildT / kWave + 3) / 4;
-static_assert(kBuildT >= kWave && kBuildT % kWave == 0 && kBuildT > kMaxSbGroups, "map workgroup size");
+#ifndef RST_SQ_LEAVES_PER_CU
+#define RST_SQ_LEAVES_PER_CU 6
+#endif
+constexpr int kLeavesPerCU = RST_SQ_LEAVES_PER_CU;
+constexpr int kLeavesWaves = (kLeavesPerCU * kBuildT / kWave + 3) / 4;
+static_assert(kBuildT >= kWave && kBuildT % kWave == 0, "leaf workgroup size");
 static_assert(sizeof(Leaf) == 64, "a leaf map is four int4");
 constexpr int kListCap = (kLeafR - 1) * kMaxSbBlocks;
 constexpr int16_t kNeedNone = INT16_MIN;  // kNoNeed in 16 bits
@@ -807,25 +808,32 @@ struct GroupMapL {
 constexpr int kGroupMapLW = (int)(sizeof(GroupMapL) / 4);
 static_assert(kGroupMapLW == 53 && offsetof(GroupMap, pad) == 4 * 52, "GroupMapL = GroupMap's first 53 dwords");
 
-// (~31 KB: five workgroups per CU.  The leaves read their elements from
-// global memory themselves: r06, staged in LDS, 76 KB and two per CU; until
-// r20 the leaf maps whole and the group maps padded, 49 KB and three)
-struct BuildLds {
-  GroupMapL gm[kMaxSbGroups];
+// The maps are built by two kernels per superblock (r20): k_sq_leaves (320
+// threads, a lane per block: the leaf runs) and k_sq_comp (one wavefront:
+// the group and superblock composites, the leaf maps read back from global
+// memory).  Until r20 one workgroup did both, and most of its time -- the
+// composites, one or two wavefronts' dependent chains -- held the LDS and
+// the wave slots its leaf phase needed: three workgroups per CU, 49 KB of
+// LDS each (r06: 76 KB and two per CU with the elements staged).
+struct LeafLds {  // ~24.5 KB: six workgroups per CU
   LeafL lf[kMaxSbBlocks];
   int sbs[kMaxSbBlocks + 1];   // block starts, relative to the superblock's first element
-  int sgs[kMaxSbGroups + 1];   // group starts, relative to its first block
   int16_t xneed[kMaxSbBlocks][kLeafR - 1];  // the extra candidates' lattice needs (kNeedNone: none)
   // extra leaf candidates (block << 2 | r): up to kLeafR - 1 per block (a
-  // stream of exact ties needs them for most blocks); then the group list
-  // (group << 4 | r), at most kMaxSbGroups x kGroupR
+  // stream of exact ties needs them for most blocks)
   uint16_t list[kListCap];
   int nlist;
-  int bad;
   double base[2];              // fp64 increments of the tiles before the superblock's first
                                // tile and before the next
 };
-static_assert(sizeof(BuildLds) <= 160 * 1024 / kBuildPerCU, "the map workgroups' LDS per CU");
+struct CompLds {  // ~7.7 KB
+  GroupMapL gm[kMaxSbGroups];
+  int sgs[kMaxSbGroups + 1];   // group starts, relative to its first block
+  uint16_t list[kMaxSbGroups * kGroupR];  // (group << 4 | r): every group's candidate 0 first
+  int nlist;
+  int bad;
+};
+static_assert(sizeof(LeafLds) <= 160 * 1024 / kLeavesPerCU, "the leaf workgroups' LDS per CU");
 
 // one monitored run of a block from candidate r: its len <= 2 kW - 1
 // elements X[a], X[a + 1], ... (the chain's SoA row, rows padded to 64
@@ -875,44 +883,56 @@ __device__ __forceinline__ MapEnt leaf_ent(const Run& p, int e0) {
   return en;
 }
 
-__device__ __forceinline__ void sq_build_body(const SqView& v, const int k, const int c) {
-  RST_TL(v.tl, v.it, 4);
-  __shared__ BuildLds W;
-  const int tid = threadIdx.x, lane = tid & (kWave - 1);
-  long long* clk = v.clk + ((int64_t)c * v.nk + k) * 8;
-  if (tid == 0) clk[0] = (long long)__builtin_amdgcn_s_memtime();
+// the superblock's group / block / element ranges, checked before each
+// dependent load (a bad table stops the workgroup instead of reading out of
+// range); false: stop
+struct SbRange {
+  int ga, gb, ba, bb, ea, eb;
+};
+__device__ __forceinline__ bool sb_range(const SqView& v, int k, int c, bool flag, SbRange& r) {
   const int* bsg = v.bs + (int64_t)c * (v.nb + 1);
   const int* gsg = v.gs + (int64_t)c * (v.ng + 1);
   const int* ksg = v.ks + (int64_t)c * (v.nk + 1);
-  // (sizes are checked before each dependent load: a bad table stops the
-  // workgroup instead of reading out of range)
-  const int ga = ksg[k], gb = ksg[k + 1];
-  if (ga < 0 || gb > v.ng || gb - ga < 1 || gb - ga > kMaxSbGroups) {
-    if (tid == 0) atomicOr(v.err, 1);
-    return;
+  r.ga = ksg[k];
+  r.gb = ksg[k + 1];
+  if (r.ga < 0 || r.gb > v.ng || r.gb - r.ga < 1 || r.gb - r.ga > kMaxSbGroups) {
+    if (flag) atomicOr(v.err, 1);
+    return false;
   }
-  const int ba = gsg[ga], bb = gsg[gb];
-  if (ba < 0 || bb > v.nb || bb - ba < 1 || bb - ba > kMaxSbBlocks) {
-    if (tid == 0) atomicOr(v.err, 1);
-    return;
+  r.ba = gsg[r.ga];
+  r.bb = gsg[r.gb];
+  if (r.ba < 0 || r.bb > v.nb || r.bb - r.ba < 1 || r.bb - r.ba > kMaxSbBlocks) {
+    if (flag) atomicOr(v.err, 1);
+    return false;
   }
-  const int ea = bsg[ba], eb = bsg[bb];
-  if (ea < 0 || eb > v.n || eb - ea < 1 || eb - ea > kMaxSbElems) {
-    if (tid == 0) atomicOr(v.err, 1);
-    return;
+  r.ea = bsg[r.ba];
+  r.eb = bsg[r.bb];
+  if (r.ea < 0 || r.eb > v.n || r.eb - r.ea < 1 || r.eb - r.ea > kMaxSbElems) {
+    if (flag) atomicOr(v.err, 1);
+    return false;
   }
-  const int ngr = gb - ga, nblk = bb - ba, nel = eb - ea;
+  return true;
+}
+
+// k_sq_leaves: every leaf map of superblock k of chain c (global v.leaf)
+__device__ __forceinline__ void sq_leaf_body(const SqView& v, const int k, const int c) {
+  RST_TL(v.tl, v.it, 4);
+  __shared__ LeafLds W;
+  const int tid = threadIdx.x, lane = tid & (kWave - 1);
+  long long* clk = v.clk + ((int64_t)c * v.nk + k) * 8;
+  if (tid == 0) clk[0] = (long long)__builtin_amdgcn_s_memtime();
+  SbRange sr;
+  if (!sb_range(v, k, c, tid == 0, sr)) return;
+  const int ba = sr.ba, ea = sr.ea;
+  const int nblk = sr.bb - sr.ba, nel = sr.eb - sr.ea;
+  const int* bsg = v.bs + (int64_t)c * (v.nb + 1);
   const float* X = v.soa + (int64_t)c * v.ns;
   const double* ipre = v.ipre + (int64_t)c * v.nb;
   Leaf* leafg = v.leaf + (int64_t)c * v.nb + ba;  // the superblock's leaf maps (global)
   // (the first round's increment prefixes in flight across the barrier)
   const double iv0 = tid < nblk ? ipre[ba + tid] : 0.0;
   for (int i = tid; i <= nblk; i += kBuildT) W.sbs[i] = bsg[ba + i] - ea;
-  if (tid <= ngr) W.sgs[tid] = gsg[ga + tid] - ba;
-  if (tid == 0) {
-    W.nlist = 0;
-    W.bad = 0;
-  }
+  if (tid == 0) W.nlist = 0;
   if (tid < kWave) {  // the tiles' increments before tile k (fixed order)
     const double* ti = v.tinc + (int64_t)c * v.nk;
     double s = 0.0;
@@ -927,8 +947,8 @@ __device__ __forceinline__ void sq_build_body(const SqView& v, const int k, cons
   }
   __syncthreads();
   if (tid == 0) clk[1] = (long long)__builtin_amdgcn_s_memtime();
-  // -- leaves: candidate 0 per block, a lane each (rounds of kBuildT blocks);
-  // its header, entry and lattice need to LDS, h.m = 1 marking a block whose
+  // -- candidate 0 per block, a lane each (rounds of kBuildT blocks): its
+  // header, entry and lattice need to LDS, h.m = 1 marking a block whose
   // other candidates are listed
   for (int b0 = 0; b0 < nblk; b0 += kBuildT) {
     const int bi = b0 + tid;
@@ -995,8 +1015,8 @@ __device__ __forceinline__ void sq_build_body(const SqView& v, const int k, cons
     }
   }
   __syncthreads();
-  // the leaf maps: lattice need over the candidates -> m; global map whole,
-  // LDS map header + entry 0
+  // the leaf maps: lattice need over the candidates -> m, the map whole to
+  // global memory
   for (int bi = tid; bi < nblk; bi += kBuildT) {
     const LeafL L = W.lf[bi];
     const bool more = L.h.m != 0;
@@ -1026,16 +1046,35 @@ __device__ __forceinline__ void sq_build_body(const SqView& v, const int k, cons
         o.e[r].HIu = min(o.e[r].HIu, 0);
       }
     }
-    W.lf[bi] = LeafL{o.h, o.e[0], 0};
     leafg[bi] = o;
   }
-  if (tid == 0) W.nlist = ngr;  // the group list: every group's candidate 0 first
+  if (tid == 0) clk[6] = (long long)__builtin_amdgcn_s_memtime();
+}
+
+// k_sq_comp (one wavefront): superblock k's group maps (v.grp) and its map
+// (v.sbm), composed through the leaf maps k_sq_leaves left in global memory
+__device__ __forceinline__ void sq_comp_body(const SqView& v, const int k, const int c) {
+  __shared__ CompLds W;
+  const int lane = threadIdx.x;
+  long long* clk = v.clk + ((int64_t)c * v.nk + k) * 8;
+  if (lane == 0) clk[2] = (long long)__builtin_amdgcn_s_memtime();
+  SbRange sr;
+  if (!sb_range(v, k, c, false, sr)) return;  // (k_sq_leaves flagged it)
+  const int ga = sr.ga, gb = sr.gb, ba = sr.ba;
+  const int ngr = gb - ga, nblk = sr.bb - sr.ba;
+  const int* gsg = v.gs + (int64_t)c * (v.ng + 1);
+  const Leaf* leafg = v.leaf + (int64_t)c * v.nb + ba;
+  // leaf i: lq[4 i] its header, lq[4 i + 1] entry 0 (and entry 1's E)
+  const int4* lq = reinterpret_cast<const int4*>(leafg);
+  if (lane <= ngr) W.sgs[lane] = gsg[ga + lane] - ba;
+  if (lane == 0) {
+    W.nlist = ngr;
+    W.bad = 0;
+  }
   __syncthreads();
-  if (tid == 0) clk[2] = (long long)__builtin_amdgcn_s_memtime();
   // -- groups: the lattice (lane per group), then lanes (group, candidate)
-  const int4* lq = reinterpret_cast<const int4*>(W.lf);  // leaf i: lq[2 i] header, lq[2 i + 1] entry 0
-  if (tid < ngr) {
-    const int gi = tid;
+  if (lane < ngr) {
+    const int gi = lane;
     const int c0 = W.sgs[gi], c1 = W.sgs[gi + 1];
     const bool gok = c0 >= 0 && c1 > c0 && c1 <= nblk && c1 - c0 <= 2 * kGW - 1;
     GroupMapL& o = W.gm[gi];
@@ -1046,22 +1085,22 @@ __device__ __forceinline__ void sq_build_body(const SqView& v, const int k, cons
       o.h = MapHdr{0.0f, 0, 0, kOpaque};
       o.xo = 0;
     } else {
-      const MapHdr h0 = W.lf[c0].h;
-      int lat = h0.e0 + h0.m;
+      const int4 h0 = lq[4 * c0];
+      int lat = h0.y + h0.z;
       // (unrolled and predicated: every header read in flight at once --
       // a rolled loop waited on each)
 #pragma unroll
       for (int j = 1; j < 2 * kGW - 1; ++j) {
         if (c0 + j < c1) {
-          const int4 hj = lq[2 * (c0 + j)];  // (one read, no branch)
+          const int4 hj = lq[4 * (c0 + j)];  // (one read, no branch)
           lat = (hj.w & kOpaque) ? lat : max(lat, hj.y + hj.z);
         }
       }
-      int m = max(0, lat - h0.e0);
+      int m = max(0, lat - h0.y);
       const bool exact_only = m > kGroupM;  // (the windows clamped to 0 below)
       if (exact_only) m = 0;
       R = 1 << m;
-      const float Gg = candidate_base(h0.G, R);
+      const float Gg = candidate_base(__int_as_float(h0.x), R);
       o.h = MapHdr{Gg, grid_exp(Gg), m, 0};
       o.xo = exact_only ? 1 : 0;
     }
@@ -1069,15 +1108,14 @@ __device__ __forceinline__ void sq_build_body(const SqView& v, const int k, cons
     if (R > 1) {
       const int at = atomicAdd(&W.nlist, R - 1);
       for (int r = 1; r < R; ++r)
-        if (at + r - 1 < kListCap) W.list[at + r - 1] = (uint16_t)(gi << 4 | r);  // (<= 496 entries: always)
+        if (at + r - 1 < kMaxSbGroups * kGroupR) W.list[at + r - 1] = (uint16_t)(gi << 4 | r);  // (always)
     }
   }
   __syncthreads();
   {
     const int nl = min(W.nlist, kMaxSbGroups * kGroupR);
-    for (int j0 = 0; j0 < nl; j0 += kBuildT) {
-      const int j = j0 + tid;
-      if (j - lane >= nl) break;  // (uniform per wavefront: waves past the list stop)
+    for (int j0 = 0; j0 < nl; j0 += kWave) {
+      const int j = j0 + lane;
       const bool ea_ = j < nl;
       const int code = !ea_ ? 0 : (j < ngr ? j << 4 : W.list[j]);
       const int gi = code >> 4, r = code & (kGroupR - 1);
@@ -1088,16 +1126,18 @@ __device__ __forceinline__ void sq_build_body(const SqView& v, const int k, cons
       float x = cand(gh.G, gh.e0, r);
       double clo = -INFINITY, chi = INFINITY;
       bool ok = gok && !(gh.flags & kOpaque);
-      // (leaf j + 1's header and entry 0 in flight while leaf j is applied:
-      // no LDS trip in the chain; entries 1..3 -- leaves with m >= 1 --
-      // from the global map, a uniform branch taken when a lane needs one)
+      // (leaves j + 1 and j + 2 -- header and entry 0 -- in flight while
+      // leaf j is applied; entries 1..3 -- leaves with m >= 1 -- by a
+      // uniform branch taken when a lane needs one)
       const int cc0 = gok ? c0 : 0, cc1 = gok ? c1 : 1;
-      int4 q0 = lq[2 * cc0], q1 = lq[2 * cc0 + 1];
+      int4 q0 = lq[4 * cc0], q1 = lq[4 * cc0 + 1];
+      const int j1 = 4 * min(cc0 + 1, cc1 - 1);
+      int4 n0 = lq[j1], n1 = lq[j1 + 1];
       const int nst = wave_max_small<5>(cc1 - cc0);  // (a group <= 2 kGW - 1 blocks)
       for (int s = 0; s < nst; ++s) {
         const int jl = cc0 + s;
-        const int jn = 2 * min(jl + 1, cc1 - 1);
-        const int4 n0 = lq[jn], n1 = lq[jn + 1];
+        const int j2 = 4 * min(jl + 2, cc1 - 1);
+        const int4 p0 = lq[j2], p1 = lq[j2 + 1];
         const MapHdr h{__int_as_float(q0.x), q0.y, q0.z, q0.w};
         bool okj = ok && jl < cc1;
         const int kq = comp_off(x, h, kLeafM, okj);
@@ -1110,6 +1150,8 @@ __device__ __forceinline__ void sq_build_body(const SqView& v, const int k, cons
         ok = jl < cc1 ? okj : ok;
         q0 = n0;
         q1 = n1;
+        n0 = p0;
+        n1 = p1;
       }
       if (ea_ && ok) {
         if (exact_only) {
@@ -1121,76 +1163,76 @@ __device__ __forceinline__ void sq_build_body(const SqView& v, const int k, cons
     }
   }
   __syncthreads();
-  if (tid == 0) clk[3] = (long long)__builtin_amdgcn_s_memtime();
+  if (lane == 0) clk[3] = (long long)__builtin_amdgcn_s_memtime();
   GroupMap* grpg = v.grp + (int64_t)c * v.ng + ga;
-  for (int i = tid; i < ngr * kGroupMapLW; i += kBuildT) {
+  for (int i = lane; i < ngr * kGroupMapLW; i += kWave) {
     const int g = i / kGroupMapLW, w = i - g * kGroupMapLW;
     reinterpret_cast<int*>(grpg + g)[w] = reinterpret_cast<const int*>(W.gm + g)[w];
   }
-  if (tid == 0) clk[4] = (long long)__builtin_amdgcn_s_memtime();
+  if (lane == 0) clk[4] = (long long)__builtin_amdgcn_s_memtime();
   // -- the superblock: lanes = candidates, up to 64
   SbMap* so = v.sbm + (int64_t)c * v.nk + k;
-  if (tid == 0) {
+  if (lane == 0) {
     so->ga = ga;
     so->gb = gb;
     so->ba = ba;
-    so->bb = bb;
-    so->ea = ea;
-    so->eb = eb;
+    so->bb = sr.bb;
+    so->ea = sr.ea;
+    so->eb = sr.eb;
   }
-  if (tid < kWave && W.bad) {
-    if (tid == 0) so->h.flags = kOpaque;
-  } else if (tid < kWave) {
-    const int r = tid;
-    const MapHdr h0 = W.gm[0].h;
-    // the lattice: the groups' e0 + m, lane per group, max over the wavefront
-    // (e0 + m in [-149, 105 + kGroupM]: 9 bits above -160)
-    const int lat = wave_max_small<9>(tid < ngr ? W.gm[tid].h.e0 + W.gm[tid].h.m : h0.e0 + h0.m, -160);
-    int m = max(0, lat - h0.e0);
-    const bool exact_only = m > kSbM;
-    if (exact_only) m = 0;
-    const int R = 1 << m;
-    const float Gs = candidate_base(h0.G, R);
-    const int se0 = grid_exp(Gs);
-    if (r == 0) so->h = MapHdr{Gs, se0, m, 0};
-    MapEnt en{0.0f, 1, 0};
-    if (R <= kSbChainR) {
-      // few candidates (R = 1 for ~87% of superblocks): one after another,
-      // each by the whole wavefront (comp_chain)
-      for (int rc = 0; rc < R; ++rc) {
-        float x = cand(Gs, se0, rc);
-        double clo = -INFINITY, chi = INFINITY;
-        if (comp_chain<GroupMapL>(x, clo, chi, W.gm, ngr, kGroupM)) {
-          if (exact_only) {
-            clo = fmax(clo, 0.0);
-            chi = fmin(chi, 0.0);
-          }
-          if (r == rc) en = MapEnt{x, lo_units(clo, se0), hi_units(chi, se0)};
-        }
-      }
-    } else if (r < R) {
-      float x = cand(Gs, se0, r);
+  if (W.bad) {
+    if (lane == 0) so->h.flags = kOpaque;
+    return;
+  }
+  const int r = lane;
+  const MapHdr h0 = W.gm[0].h;
+  // the lattice: the groups' e0 + m, lane per group, max over the wavefront
+  // (e0 + m in [-149, 105 + kGroupM]: 9 bits above -160)
+  const int lat = wave_max_small<9>(lane < ngr ? W.gm[lane].h.e0 + W.gm[lane].h.m : h0.e0 + h0.m, -160);
+  int m = max(0, lat - h0.e0);
+  const bool exact_only = m > kSbM;
+  if (exact_only) m = 0;
+  const int R = 1 << m;
+  const float Gs = candidate_base(h0.G, R);
+  const int se0 = grid_exp(Gs);
+  if (r == 0) so->h = MapHdr{Gs, se0, m, 0};
+  MapEnt en{0.0f, 1, 0};
+  if (R <= kSbChainR) {
+    // few candidates (R = 1 for ~87% of superblocks): one after another,
+    // each by the whole wavefront (comp_chain)
+    for (int rc = 0; rc < R; ++rc) {
+      float x = cand(Gs, se0, rc);
       double clo = -INFINITY, chi = INFINITY;
-      bool ok = true;
-      // (group j + 1's header in flight while group j is applied)
-      MapHdr H = W.gm[0].h;
-      for (int j = 0; j < ngr; ++j) {
-        const MapHdr Hn = W.gm[min(j + 1, ngr - 1)].h;
-        const int kq = comp_off(x, H, kGroupM, ok);
-        comp_apply(x, clo, chi, ok, H, kq, W.gm[j].e[kq & ((1 << (ok ? H.m : 0)) - 1)]);
-        H = Hn;
-      }
-      if (ok) {
+      if (comp_chain<GroupMapL>(x, clo, chi, W.gm, ngr, kGroupM)) {
         if (exact_only) {
           clo = fmax(clo, 0.0);
           chi = fmin(chi, 0.0);
         }
-        en = MapEnt{x, lo_units(clo, se0), hi_units(chi, se0)};
+        if (r == rc) en = MapEnt{x, lo_units(clo, se0), hi_units(chi, se0)};
       }
     }
-    so->e[r] = en;
-    if (tid == 0) clk[5] = (long long)__builtin_amdgcn_s_memtime();
+  } else if (r < R) {
+    float x = cand(Gs, se0, r);
+    double clo = -INFINITY, chi = INFINITY;
+    bool ok = true;
+    // (group j + 1's header in flight while group j is applied)
+    MapHdr H = W.gm[0].h;
+    for (int j = 0; j < ngr; ++j) {
+      const MapHdr Hn = W.gm[min(j + 1, ngr - 1)].h;
+      const int kq = comp_off(x, H, kGroupM, ok);
+      comp_apply(x, clo, chi, ok, H, kq, W.gm[j].e[kq & ((1 << (ok ? H.m : 0)) - 1)]);
+      H = Hn;
+    }
+    if (ok) {
+      if (exact_only) {
+        clo = fmax(clo, 0.0);
+        chi = fmin(chi, 0.0);
+      }
+      en = MapEnt{x, lo_units(clo, se0), hi_units(chi, se0)};
+    }
   }
+  so->e[r] = en;
+  if (lane == 0) clk[5] = (long long)__builtin_amdgcn_s_memtime();
 }
 
 
@@ -1695,7 +1737,8 @@ __global__ __launch_bounds__(kFrontT) void k_sq_front(SqView v, const float4* __
                                                      double* __restrict__ tnext) {
   sq_front_body<FUSED>(v, x, tprev, tnext, blockIdx.x, blockIdx.y);
 }
-__global__ __launch_bounds__(kBuildT, kBuildWaves) void k_sq_build(SqView v) { sq_build_body(v, blockIdx.x, blockIdx.y); }
+__global__ __launch_bounds__(kBuildT, kLeavesWaves) void k_sq_leaves(SqView v) { sq_leaf_body(v, blockIdx.x, blockIdx.y); }
+__global__ __launch_bounds__(kWave) void k_sq_comp(SqView v) { sq_comp_body(v, blockIdx.x, blockIdx.y); }
 __global__ __launch_bounds__(kWave) void k_sq_walk(SqView v, float* __restrict__ out) {
   sq_walk_body(v, out, blockIdx.x);
 }
@@ -1758,10 +1801,15 @@ __global__ __launch_bounds__(kFrontT) void k_sq_front_b(const SqPair* __restrict
     sq_front_body<false>(v, nullptr, nullptr, nullptr, blockIdx.x, blockIdx.y);
   }
 }
-__global__ __launch_bounds__(kBuildT, kBuildWaves) void k_sq_build_b(const SqPair* __restrict__ P, int nch, int iter) {
+__global__ __launch_bounds__(kBuildT, kLeavesWaves) void k_sq_leaves_b(const SqPair* __restrict__ P, int nch, int iter) {
   const SqView v = sq_at(P[blockIdx.z], nch, iter);
   if ((int)blockIdx.x >= v.nk) return;
-  sq_build_body(v, blockIdx.x, blockIdx.y);
+  sq_leaf_body(v, blockIdx.x, blockIdx.y);
+}
+__global__ __launch_bounds__(kWave) void k_sq_comp_b(const SqPair* __restrict__ P, int nch, int iter) {
+  const SqView v = sq_at(P[blockIdx.z], nch, iter);
+  if ((int)blockIdx.x >= v.nk) return;
+  sq_comp_body(v, blockIdx.x, blockIdx.y);
 }
 __global__ __launch_bounds__(kWave) void k_sq_walk_b(const SqPair* __restrict__ P, int nch, int iter) {
   const SqPair& p = P[blockIdx.z];
@@ -2279,7 +2327,8 @@ int seqsum_enqueue_batch(const void* d_pairs, int nbatch, int64_t nmax, int nch,
     k_sq_tot_b<<<dim3(nk * kTotQ, 1, nbatch), kFrontT, 0, st>>>(P, nch, iter);
     k_sq_front_b<false><<<dim3(nk, nch, nbatch), kFrontT, 0, st>>>(P, nch, iter);
   }
-  k_sq_build_b<<<dim3(nk, nch, nbatch), kBuildT, 0, st>>>(P, nch, iter);
+  k_sq_leaves_b<<<dim3(nk, nch, nbatch), kBuildT, 0, st>>>(P, nch, iter);
+  k_sq_comp_b<<<dim3(nk, nch, nbatch), kWave, 0, st>>>(P, nch, iter);
   k_sq_walk_b<<<dim3(nch, 1, nbatch), kWave, 0, st>>>(P, nch, iter);
   RST_HIP(hipGetLastError());
   return RST_OK;
@@ -2396,7 +2445,10 @@ int seqsum_enqueue(const float4* d_x, int64_t n, int nch, void* ws, float* d_out
       k_sq_front<false><<<dim3(v.nk, nch), kFrontT, 0, st>>>(v, nullptr, nullptr, nullptr);
     }
   }
-  if (stages & 2) k_sq_build<<<dim3(v.nk, nch), kBuildT, 0, st>>>(v);
+  if (stages & 2) {
+    k_sq_leaves<<<dim3(v.nk, nch), kBuildT, 0, st>>>(v);
+    k_sq_comp<<<dim3(v.nk, nch), kWave, 0, st>>>(v);
+  }
   if (stages & 4) k_sq_walk<<<nch, kWave, 0, st>>>(v, d_out);
   RST_HIP(hipGetLastError());
   return RST_OK;

@@ -76,11 +76,13 @@ def main():
     print("err bits", err)
     clk = ws[off["clk"]:off["clk"] + 64 * 4 * nk].view(np.int64).reshape(4, nk, 8)
     if stages & 2:
-        d = np.diff(clk[:, :, :6], axis=2).astype(np.float64)
-        # k_sq_build's stamps: start, staged, leaves done, group composites done,
-        # group maps stored, superblock done
-        names = ["staging", "leaves (+ extra candidates)", "group lattice + composites", "group store",
-                 "superblock"]
+        t = clk.astype(np.float64)
+        # stamps: k_sq_leaves start 0, staged 1, leaves done 6; k_sq_comp
+        # start 2, group composites done 3, group maps stored 4, superblock 5
+        d = np.stack([t[..., 1] - t[..., 0], t[..., 6] - t[..., 1], t[..., 2] - t[..., 6],
+                      t[..., 3] - t[..., 2], t[..., 4] - t[..., 3], t[..., 5] - t[..., 4]], axis=2)
+        names = ["staging", "leaves (+ extra candidates)", "launch gap", "group lattice + composites",
+                 "group store", "superblock"]
         print("map kernel phases (clocks, mean / max over superblocks):",
               {nm: (round(d[:, :, i].mean()), int(d[:, :, i].max())) for i, nm in enumerate(names)})
     from seqsum_emu import emulate_tables
