@@ -779,6 +779,10 @@ __device__ __forceinline__ void icp_nn_body(const BvhView& bv, const AdjView& av
 #if RST_NN_CLK  // diagnostics build: per wave latency and phases (diag[it][0..3])
   const uint64_t ck0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
   uint64_t ck1 = 0, ck2 = 0;
+  uint64_t pck[3] = {0, 0, 0};  // pix_tile_search's phases
+  uint64_t* const pckp = pck;
+#else
+  uint64_t* const pckp = nullptr;
 #endif
   const int tb = xcd_tile(blockIdx.x, nbk);
   // the far queue: the second half of qbuf / qcnt
@@ -972,6 +976,9 @@ __device__ __forceinline__ void icp_nn_body(const BvhView& bv, const AdjView& av
     // throughput.  The fp64 loop keeps the wider cap, r02's throughput best)
     constexpr float kPixHalfDef = std::is_same<Acc, RefAcc>::value ? RST_PIX_MAX_HALF_REF : RST_PIX_MAX_HALF;
     const float kPixHalf = aa.pix_half > 0.f ? aa.pix_half : kPixHalfDef;
+#if RST_NN_CLK
+    ck2 = __builtin_amdgcn_s_memtime();  // (the search's entry, after the reseed)
+#endif
     bool pok;
     constexpr bool defer = RST_PIX_DEFER && !std::is_same<Acc, P2PlaneAcc>::value;
     if (RST_PIX_I0_HALF > 0.0f && st->iter == 0)  // (uniform)
@@ -981,10 +988,7 @@ __device__ __forceinline__ void icp_nn_body(const BvhView& bv, const AdjView& av
       pok = cold ? pix_tile_search<kPixChunk, RST_PIX_COLD_CHUNKS, !defer>(bv, pv, need, px, py, pz, d0, pr, pq,
                                                                           pscr[wid], prc, RST_PIX_COLD_HALF)
                  : pix_tile_search<kPixChunk, RST_PIX_CHUNKS, !defer>(bv, pv, need, px, py, pz, d0, pr, pq,
-                                                                     pscr[wid], prc, kPixHalf);
-#if RST_NN_CLK
-    ck2 = __builtin_amdgcn_s_memtime();
-#endif
+                                                                     pscr[wid], prc, kPixHalf, pckp);
     if (pok) {
       const float g = cert_bound(pr, prc);
       // (deferred: the original index, kIdBit -- compared with the last
@@ -1047,8 +1051,12 @@ __device__ __forceinline__ void icp_nn_body(const BvhView& bv, const AdjView& av
     int64_t* o = reinterpret_cast<int64_t*>(slab) + (int64_t)tb * 16 + wid * 4;
     o[0] = (int64_t)rt0;
     o[1] = (int64_t)rt3;
-    o[2] = (int64_t)(ck1 - ck0);
-    o[3] = (int64_t)((ck2 ? ck2 - ck1 : 0) | ((ck3 - ck0) << 32));
+    // shader clocks from the wave's start (0: no such phase): to the
+    // certificate test | the search's entry (after the reseed) << 32; the
+    // first chunk staged | the scans done << 32
+    auto rel = [&](uint64_t t) { return t ? (int64_t)(t - ck0) : 0; };
+    o[2] = rel(ck1) | (rel(ck2) << 32);
+    o[3] = rel(pck[1]) | (rel(pck[2]) << 32);
   }
 #endif
 }

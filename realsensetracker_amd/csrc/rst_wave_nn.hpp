@@ -1465,7 +1465,11 @@ template <int N, int MaxChunks, bool Resolve = true>
 __device__ __forceinline__ bool pix_tile_search(const BvhView& bv, const PixView& pv, bool act,
                                                 float qx, float qy, float qz, float d0, Best2& r,
                                                 float4& q0, PixScratch<N>& ts, float& rc,
-                                                float maxh = RST_PIX_MAX_HALF) {
+                                                float maxh = RST_PIX_MAX_HALF, uint64_t* pclk = nullptr) {
+  // (pclk: diagnostics builds' phase clocks -- boxes set up, first chunk
+  // staged, scans done; tools/nn_clock.py.  r20: the scans as one flat run
+  // of each lane's window pixels, 4 / 6 / 8 LDS reads in flight, measured
+  // slower than these rows: k_icp_nn_b 261 -> 273 / 273 / 281 us)
   constexpr int kPer = N / kWave;
   const int lane = __lane_id();
   int a0 = 0, a1 = -1, b0 = 0, b1 = -1;
@@ -1513,6 +1517,7 @@ __device__ __forceinline__ bool pix_tile_search(const BvhView& bv, const PixView
   int moff = 0;
 #pragma unroll
   for (int g = 0; g < 4; ++g) moff = g == mg ? off[g] : moff;
+  if (pclk) pclk[0] = __builtin_amdgcn_s_memtime();
   for (int c0 = 0; c0 < total; c0 += N) {
     const int cnt = min(N, total - c0);
     float4 pp[kPer];
@@ -1545,6 +1550,7 @@ __device__ __forceinline__ bool pix_tile_search(const BvhView& bv, const PixView
       if (k < cnt) ts.pts[k] = pp[j];
     }
     wave_sync();
+    if (pclk && c0 == 0) pclk[1] = __builtin_amdgcn_s_memtime();
     if (ok) {
       // four pixels' LDS reads in flight at a time (a dependent read per
       // pixel would leave the scan bound by LDS latency); an invalid pixel
@@ -1578,6 +1584,7 @@ __device__ __forceinline__ bool pix_tile_search(const BvhView& bv, const PixView
     }
     wave_sync();
   }
+  if (pclk) pclk[2] = __builtin_amdgcn_s_memtime();
   // (!Resolve: r.pos stays kPosPending / -1 -- the caller keeps r.id, the
   // original indices, and maps them itself when it needs positions)
   if (Resolve && ok) pix_resolve(bv, pv, r);

@@ -31,16 +31,26 @@ raw = np.zeros(nblk * 16, np.float64)
 L.check(f(ctx.handle, raw.ctypes.data, len(raw)), "slab")
 w = raw.view(np.int64).reshape(nblk * 4, 4)
 t0, t1 = w[:, 0], w[:, 1]
-c1 = w[:, 2]
-cp = w[:, 3] & 0xffffffff
-ct = w[:, 3] >> 32
-print(f"{nblk} workgroups, {len(w)} waves")
+# shader clocks from each wave's start (0: no such phase)
+cert = w[:, 2] & 0xffffffff
+entry = w[:, 2] >> 32
+staged = w[:, 3] & 0xffffffff
+scans = w[:, 3] >> 32
+print(f"{nblk} workgroups, {len(w)} waves; {np.mean(entry > 0):.0%} enter the pixel search, "
+      f"{np.mean(staged > 0):.0%} stage")
 print(f"kernel span (first start -> last end): {(t1.max() - t0.min()) / 100:.1f} us")
 print(f"wave start spread: {(t0.max() - t0.min()) / 100:.1f} us; end spread {(t1.max() - t1.min()) / 100:.1f} us")
 lat = (t1 - t0) / 100
-for q in (50, 90, 99, 100):
-    print(f"wave latency p{q}: {np.percentile(lat, q):.1f} us; clocks: to cert {np.percentile(c1, q):.0f}, "
-          f"pix {np.percentile(cp, q):.0f}, total {np.percentile(ct, q):.0f}")
+s = staged > 0
+print("clocks from the wave's start, searching waves: to cert | reseed | window setup + first chunk trip | "
+      "scans (+ further chunks) | latency us")
+for q in (10, 50, 90, 99, 100):
+    print(f"  p{q}: cert {np.percentile(cert[s], q):.0f}  reseed {np.percentile(entry[s] - cert[s], q):.0f}  "
+          f"stage {np.percentile(staged[s] - entry[s], q):.0f}  scans {np.percentile(scans[s] - staged[s], q):.0f}  "
+          f"latency {np.percentile(lat[s], q):.1f}")
+ns = ~s
+for q in (50, 90, 99):
+    print(f"  non-staging waves p{q}: cert {np.percentile(cert[ns], q):.0f}  latency {np.percentile(lat[ns], q):.1f} us")
 srt = np.argsort(t0)
 print("starts by decile (us from first):", [round((np.percentile(t0, p) - t0.min()) / 100, 1) for p in range(0, 101, 10)])
 print("ends by decile (us from first start):", [round((np.percentile(t1, p) - t0.min()) / 100, 1) for p in range(0, 101, 10)])
