@@ -51,7 +51,7 @@ constexpr int kCertBit = 1 << 30;
 #endif
 constexpr int kBallChunkDefault = 512;
 #ifndef RST_FB_MIN_WAVES_REF
-#define RST_FB_MIN_WAVES_REF 3  // the REF loop's k_icp_fb (r11: 3 vs 4 waves/SIMD 33.8k vs 33.4k it/s batched; the fp64 loop 49.0k vs 50.0k, so it keeps 4)
+#define RST_FB_MIN_WAVES_REF 4  // the REF loop's k_icp_fb (r11: 3 vs 4 waves/SIMD 33.8k vs 33.4k it/s batched; the fp64 loop 49.0k vs 50.0k, so it keeps 4; r20j, with the REF k_icp_nn's below: 4)
 #endif
 #ifndef RST_COLD_FAST
 #define RST_COLD_FAST 1
@@ -90,6 +90,12 @@ constexpr int kPixChunk = RST_PIX_CHUNK;
 #endif
 #ifndef RST_NN_MIN_WAVES
 #define RST_NN_MIN_WAVES 5  // k_icp_nn occupancy hint (waves per SIMD; 6 with 320-pixel chunks spilled: 32.9k)
+#endif
+#ifndef RST_NN_MIN_WAVES_REF
+#define RST_NN_MIN_WAVES_REF 6  // ... of the REF loop's (r20j: with 320-pixel chunks, the batched fallback at 4 waves and the leaf maps at 5 workgroups per CU, 41.0k -> 41.8k it/s; 80 VGPRs, 20 B of scratch)
+#endif
+#ifndef RST_PIX_CHUNK_REF
+#define RST_PIX_CHUNK_REF 320  // pixels staged per wave and round, the REF loop (20.5 KB of LDS a block)
 #endif
 #ifndef RST_CERT_EAGER
 #define RST_CERT_EAGER 0  // k_icp_nn: load cert[] beside nnq[] (not after its flag)
@@ -378,6 +384,8 @@ struct P2PointAcc {
   static constexpr int NV = kNP2Point;  // sum w q u^T (9), sum w u (3), sum q (3), sum d2
   static constexpr int RS = 16;         // slab row stride (doubles; divides kRedBS)
   static constexpr int kFbMinWaves = RST_FB_MIN_WAVES;  // k_icp_fb occupancy
+  static constexpr int kNnMinWaves = RST_NN_MIN_WAVES;  // k_icp_nn occupancy
+  static constexpr int kPixChunk = RST_PIX_CHUNK;       // k_icp_nn's pixel staging
   static constexpr int kBallChunk = kBallChunkDefault;
   static constexpr bool kPubPrefix = true;  // k_queue_prefix publishes the queues' prefixes
   static constexpr bool kCanFinish = false;
@@ -409,6 +417,8 @@ struct P2PlaneAcc {
   static constexpr int NV = kNP2Plane;  // A (21), b (6), sum w r^2, count, sum d2
   static constexpr int RS = 32;
   static constexpr int kFbMinWaves = 1;
+  static constexpr int kNnMinWaves = RST_NN_MIN_WAVES;
+  static constexpr int kPixChunk = RST_PIX_CHUNK;
   static constexpr int kBallChunk = kBallChunkDefault;
   static constexpr bool kPubPrefix = false;  // k_icp_fb scans the queue counts per block (see there)
   static constexpr bool kCanFinish = true;
@@ -451,6 +461,8 @@ struct RefAcc {
   static constexpr int NV = 9;   // k_cov_ref's rows: the 3x3 covariance
   static constexpr int RS = 16;
   static constexpr int kFbMinWaves = RST_FB_MIN_WAVES_REF;
+  static constexpr int kNnMinWaves = RST_NN_MIN_WAVES_REF;
+  static constexpr int kPixChunk = RST_PIX_CHUNK_REF;
   static constexpr int kBallChunk = RST_BALL_CHUNK_REF;  // k_icp_fb's ball-tile staging (points)
   static constexpr bool kPubPrefix = true;
   static constexpr bool kCanFinish = false;
@@ -774,7 +786,7 @@ __device__ __forceinline__ void icp_nn_body(const BvhView& bv, const AdjView& av
   __shared__ double lds[(kBS / kWave) * Acc::NV];
   __shared__ int wq[2][kBS / kWave];
 #if RST_PIX_TILES
-  __shared__ PixScratch<kPixChunk> pscr[kBS / kWave];
+  __shared__ PixScratch<Acc::kPixChunk> pscr[kBS / kWave];
 #endif
 #if RST_NN_CLK  // diagnostics build: per wave latency and phases (diag[it][0..3])
   const uint64_t ck0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
@@ -899,9 +911,9 @@ __device__ __forceinline__ void icp_nn_body(const BvhView& bv, const AdjView& av
         float prc = 0.f;
         const bool cold = st->iter >= 1 && st->iter < RST_PIX_COLD_ITERS;
         const bool pok =
-            cold ? pix_tile_search<kPixChunk, RST_PIX_COLD_CHUNKS>(bv, pv, ea, q.x, q.y, q.z, q.w, pr, pq,
+            cold ? pix_tile_search<Acc::kPixChunk, RST_PIX_COLD_CHUNKS>(bv, pv, ea, q.x, q.y, q.z, q.w, pr, pq,
                                                                    pscr[wid], prc, RST_PIX_COLD_HALF)
-                 : pix_tile_search<kPixChunk, RST_PIX_CHUNKS>(bv, pv, ea, q.x, q.y, q.z, q.w, pr, pq, pscr[wid], prc);
+                 : pix_tile_search<Acc::kPixChunk, RST_PIX_CHUNKS>(bv, pv, ea, q.x, q.y, q.z, q.w, pr, pq, pscr[wid], prc);
         if (pok) {
           const float g = cert_bound(pr, prc);
           const int pos = pr.pos[0];
@@ -982,12 +994,12 @@ __device__ __forceinline__ void icp_nn_body(const BvhView& bv, const AdjView& av
     bool pok;
     constexpr bool defer = RST_PIX_DEFER && !std::is_same<Acc, P2PlaneAcc>::value;
     if (RST_PIX_I0_HALF > 0.0f && st->iter == 0)  // (uniform)
-      pok = pix_tile_search<kPixChunk, RST_PIX_I0_CHUNKS, !defer>(bv, pv, need, px, py, pz, d0, pr, pq, pscr[wid],
+      pok = pix_tile_search<Acc::kPixChunk, RST_PIX_I0_CHUNKS, !defer>(bv, pv, need, px, py, pz, d0, pr, pq, pscr[wid],
                                                                   prc, RST_PIX_I0_HALF);
     else
-      pok = cold ? pix_tile_search<kPixChunk, RST_PIX_COLD_CHUNKS, !defer>(bv, pv, need, px, py, pz, d0, pr, pq,
+      pok = cold ? pix_tile_search<Acc::kPixChunk, RST_PIX_COLD_CHUNKS, !defer>(bv, pv, need, px, py, pz, d0, pr, pq,
                                                                           pscr[wid], prc, RST_PIX_COLD_HALF)
-                 : pix_tile_search<kPixChunk, RST_PIX_CHUNKS, !defer>(bv, pv, need, px, py, pz, d0, pr, pq,
+                 : pix_tile_search<Acc::kPixChunk, RST_PIX_CHUNKS, !defer>(bv, pv, need, px, py, pz, d0, pr, pq,
                                                                      pscr[wid], prc, kPixHalf, pckp);
     if (pok) {
       const float g = cert_bound(pr, prc);
@@ -1062,7 +1074,7 @@ __device__ __forceinline__ void icp_nn_body(const BvhView& bv, const AdjView& av
 }
 
 template <class Acc>
-__global__ __launch_bounds__(kBS, RST_NN_MIN_WAVES) void k_icp_nn(BvhView bv, AdjView av, PixView pv, AccArgs aa,
+__global__ __launch_bounds__(kBS, Acc::kNnMinWaves) void k_icp_nn(BvhView bv, AdjView av, PixView pv, AccArgs aa,
                                                 const float4* __restrict__ src, int64_t n,
                                                 const IcpState* __restrict__ st,
                                                 float4* __restrict__ nnq,
@@ -1167,7 +1179,7 @@ __device__ __forceinline__ PairArgs glb_pair(const PairArgs& A) {
 }
 
 template <class Acc>
-__global__ __launch_bounds__(kBS, RST_NN_MIN_WAVES) void k_icp_nn_b(const PairArgs* __restrict__ pa) {
+__global__ __launch_bounds__(kBS, Acc::kNnMinWaves) void k_icp_nn_b(const PairArgs* __restrict__ pa) {
   const PairArgs& A = pa[blockIdx.z];
   if ((int)blockIdx.x >= A.nb1) return;  // (uniform: the grid fits the batch's largest pair)
   icp_nn_body<Acc>(glb(A.bv), glb(A.av), glb(A.pv), glb(A.aa), as_glb(A.src), A.n, as_glb(A.st), as_glb(A.nnq),

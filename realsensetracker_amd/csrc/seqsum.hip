@@ -543,13 +543,13 @@ __device__ __forceinline__ void sq_front_body(const SqView& v, const float4* __r
 // kernel's choices.  Leaf and group maps go to global memory for the walk's
 // descents.
 // k_sq_leaves: 320 threads (a lane per block; blocks past the first 320 of
-// a superblock -- rare: ~256 on average -- take a second round), six
-// workgroups per CU (30 waves, <= 8 per SIMD: <= 64 registers; LDS <= 26
-// KB each).  k_sq_comp: one wavefront.  r20 before the split: one workgroup
+// a superblock -- rare: ~256 on average -- take a second round), five
+// workgroups per CU (25 waves, <= 7 per SIMD: <= 72 registers; LDS <= 32
+// KB each; six, <= 64 registers, spilled 16 B).  k_sq_comp: one wavefront.  r20 before the split: one workgroup
 // of 512 threads, three per CU, 38.1k it/s; of 320, five per CU, 40.8k.
 constexpr int kBuildT = 320;
 #ifndef RST_SQ_LEAVES_PER_CU
-#define RST_SQ_LEAVES_PER_CU 6
+#define RST_SQ_LEAVES_PER_CU 5  // (r20b / r20j: 6 -> 5, 41.1k -> 41.3k it/s alone, part of r20j's combination)
 #endif
 constexpr int kLeavesPerCU = RST_SQ_LEAVES_PER_CU;
 constexpr int kLeavesWaves = (kLeavesPerCU * kBuildT / kWave + 3) / 4;
