@@ -384,6 +384,7 @@ struct P2PointAcc {
   static constexpr int NV = kNP2Point;  // sum w q u^T (9), sum w u (3), sum q (3), sum d2
   static constexpr int RS = 16;         // slab row stride (doubles; divides kRedBS)
   static constexpr int kFbMinWaves = RST_FB_MIN_WAVES;  // k_icp_fb occupancy
+  static constexpr int kFbMinWavesSingle = kFbMinWaves;
   static constexpr int kNnMinWaves = RST_NN_MIN_WAVES;  // k_icp_nn occupancy
   static constexpr int kPixChunk = RST_PIX_CHUNK;       // k_icp_nn's pixel staging
   static constexpr int kBallChunk = kBallChunkDefault;
@@ -417,6 +418,7 @@ struct P2PlaneAcc {
   static constexpr int NV = kNP2Plane;  // A (21), b (6), sum w r^2, count, sum d2
   static constexpr int RS = 32;
   static constexpr int kFbMinWaves = 1;
+  static constexpr int kFbMinWavesSingle = kFbMinWaves;
   static constexpr int kNnMinWaves = RST_NN_MIN_WAVES;
   static constexpr int kPixChunk = RST_PIX_CHUNK;
   static constexpr int kBallChunk = kBallChunkDefault;
@@ -461,6 +463,7 @@ struct RefAcc {
   static constexpr int NV = 9;   // k_cov_ref's rows: the 3x3 covariance
   static constexpr int RS = 16;
   static constexpr int kFbMinWaves = RST_FB_MIN_WAVES_REF;
+  static constexpr int kFbMinWavesSingle = 3;  // (the single align's, r11 / r19)
   static constexpr int kNnMinWaves = RST_NN_MIN_WAVES_REF;
   static constexpr int kPixChunk = RST_PIX_CHUNK_REF;
   static constexpr int kBallChunk = RST_BALL_CHUNK_REF;  // k_icp_fb's ball-tile staging (points)
@@ -1074,7 +1077,9 @@ __device__ __forceinline__ void icp_nn_body(const BvhView& bv, const AdjView& av
 }
 
 template <class Acc>
-__global__ __launch_bounds__(kBS, Acc::kNnMinWaves) void k_icp_nn(BvhView bv, AdjView av, PixView pv, AccArgs aa,
+// (the single align's kernels keep the r19 hints: a pair alone is latency,
+// and the REF batch's higher occupancy spills -- r21b, a lone pair 25.8 ms)
+__global__ __launch_bounds__(kBS, RST_NN_MIN_WAVES) void k_icp_nn(BvhView bv, AdjView av, PixView pv, AccArgs aa,
                                                 const float4* __restrict__ src, int64_t n,
                                                 const IcpState* __restrict__ st,
                                                 float4* __restrict__ nnq,
@@ -1904,7 +1909,7 @@ __device__ __forceinline__ void icp_fb_body(const BvhView& bv, const AdjView& av
 }
 
 template <class Acc, bool PUB = Acc::kPubPrefix>
-__global__ __launch_bounds__(kBS, Acc::kFbMinWaves) void k_icp_fb(BvhView bv, AdjView av, PixView pv,
+__global__ __launch_bounds__(kBS, Acc::kFbMinWavesSingle) void k_icp_fb(BvhView bv, AdjView av, PixView pv,
                                                 AccArgs aa,
                                                 const float4* __restrict__ src,
                                                 IcpState* __restrict__ st,

@@ -833,7 +833,7 @@ struct CompLds {  // ~7.7 KB
   int nlist;
   int bad;
 };
-static_assert(sizeof(LeafLds) <= 160 * 1024 / kLeavesPerCU, "the leaf workgroups' LDS per CU");
+static_assert(sizeof(LeafLds) + sizeof(CompLds) <= 160 * 1024 / kLeavesPerCU, "the map workgroups' LDS per CU");
 
 // one monitored run of a block from candidate r: its len <= 2 kW - 1
 // elements X[a], X[a + 1], ... (the chain's SoA row, rows padded to 64
@@ -883,6 +883,15 @@ __device__ __forceinline__ MapEnt leaf_ent(const Run& p, int e0) {
   return en;
 }
 
+// LDS ordering within a one-wavefront workgroup (no s_barrier: the fused
+// kernel's other wavefronts have ended)
+__device__ __forceinline__ void sq_wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
 // the superblock's group / block / element ranges, checked before each
 // dependent load (a bad table stops the workgroup instead of reading out of
 // range); false: stop
@@ -915,9 +924,11 @@ __device__ __forceinline__ bool sb_range(const SqView& v, int k, int c, bool fla
 }
 
 // k_sq_leaves: every leaf map of superblock k of chain c (global v.leaf)
-__device__ __forceinline__ void sq_leaf_body(const SqView& v, const int k, const int c) {
+// (lds_maps: the maps' headers and entries 0 also left in W.lf, the fused
+// kernel's composites read them there)
+__device__ __forceinline__ void sq_leaf_body(const SqView& v, const int k, const int c, LeafLds& W,
+                                             bool lds_maps) {
   RST_TL(v.tl, v.it, 4);
-  __shared__ LeafLds W;
   const int tid = threadIdx.x, lane = tid & (kWave - 1);
   long long* clk = v.clk + ((int64_t)c * v.nk + k) * 8;
   if (tid == 0) clk[0] = (long long)__builtin_amdgcn_s_memtime();
@@ -1047,15 +1058,18 @@ __device__ __forceinline__ void sq_leaf_body(const SqView& v, const int k, const
       }
     }
     leafg[bi] = o;
+    if (lds_maps) W.lf[bi] = LeafL{o.h, o.e[0], 0};
   }
   if (tid == 0) clk[6] = (long long)__builtin_amdgcn_s_memtime();
 }
 
 // k_sq_comp (one wavefront): superblock k's group maps (v.grp) and its map
 // (v.sbm), composed through the leaf maps k_sq_leaves left in global memory
-__device__ __forceinline__ void sq_comp_body(const SqView& v, const int k, const int c) {
-  __shared__ CompLds W;
-  const int lane = threadIdx.x;
+// (the single-stream k_sq_build: through its LDS copy).  (r21a: staging the
+// headers and entries 0 in LDS first measured no faster, 41.7k vs 41.6k)
+__device__ __forceinline__ void sq_comp_body(const SqView& v, const int k, const int c, CompLds& W,
+                                             const LeafL* lds_leaves) {
+  const int lane = threadIdx.x & (kWave - 1);
   long long* clk = v.clk + ((int64_t)c * v.nk + k) * 8;
   if (lane == 0) clk[2] = (long long)__builtin_amdgcn_s_memtime();
   SbRange sr;
@@ -1064,14 +1078,16 @@ __device__ __forceinline__ void sq_comp_body(const SqView& v, const int k, const
   const int ngr = gb - ga, nblk = sr.bb - sr.ba;
   const int* gsg = v.gs + (int64_t)c * (v.ng + 1);
   const Leaf* leafg = v.leaf + (int64_t)c * v.nb + ba;
-  // leaf i: lq[4 i] its header, lq[4 i + 1] entry 0 (and entry 1's E)
-  const int4* lq = reinterpret_cast<const int4*>(leafg);
+  // leaf i: lq[lqs i] its header, lq[lqs i + 1] entry 0 (the global map:
+  // lqs = 4, and entry 1's E; the fused kernel's LDS copy: lqs = 2)
+  const int4* lq = lds_leaves ? reinterpret_cast<const int4*>(lds_leaves) : reinterpret_cast<const int4*>(leafg);
+  const int lqs = lds_leaves ? 2 : 4;
   if (lane <= ngr) W.sgs[lane] = gsg[ga + lane] - ba;
   if (lane == 0) {
     W.nlist = ngr;
     W.bad = 0;
   }
-  __syncthreads();
+  sq_wave_sync();
   // -- groups: the lattice (lane per group), then lanes (group, candidate)
   if (lane < ngr) {
     const int gi = lane;
@@ -1085,14 +1101,14 @@ __device__ __forceinline__ void sq_comp_body(const SqView& v, const int k, const
       o.h = MapHdr{0.0f, 0, 0, kOpaque};
       o.xo = 0;
     } else {
-      const int4 h0 = lq[4 * c0];
+      const int4 h0 = lq[lqs * c0];
       int lat = h0.y + h0.z;
       // (unrolled and predicated: every header read in flight at once --
       // a rolled loop waited on each)
 #pragma unroll
       for (int j = 1; j < 2 * kGW - 1; ++j) {
         if (c0 + j < c1) {
-          const int4 hj = lq[4 * (c0 + j)];  // (one read, no branch)
+          const int4 hj = lq[lqs * (c0 + j)];  // (one read, no branch)
           lat = (hj.w & kOpaque) ? lat : max(lat, hj.y + hj.z);
         }
       }
@@ -1111,7 +1127,7 @@ __device__ __forceinline__ void sq_comp_body(const SqView& v, const int k, const
         if (at + r - 1 < kMaxSbGroups * kGroupR) W.list[at + r - 1] = (uint16_t)(gi << 4 | r);  // (always)
     }
   }
-  __syncthreads();
+  sq_wave_sync();
   {
     const int nl = min(W.nlist, kMaxSbGroups * kGroupR);
     for (int j0 = 0; j0 < nl; j0 += kWave) {
@@ -1127,16 +1143,16 @@ __device__ __forceinline__ void sq_comp_body(const SqView& v, const int k, const
       double clo = -INFINITY, chi = INFINITY;
       bool ok = gok && !(gh.flags & kOpaque);
       // (leaves j + 1 and j + 2 -- header and entry 0 -- in flight while
-      // leaf j is applied; entries 1..3 -- leaves with m >= 1 -- by a
-      // uniform branch taken when a lane needs one)
+      // leaf j is applied; entries 1..3 -- leaves with m >= 1 -- from the
+      // global map by a uniform branch taken when a lane needs one)
       const int cc0 = gok ? c0 : 0, cc1 = gok ? c1 : 1;
-      int4 q0 = lq[4 * cc0], q1 = lq[4 * cc0 + 1];
-      const int j1 = 4 * min(cc0 + 1, cc1 - 1);
+      int4 q0 = lq[lqs * cc0], q1 = lq[lqs * cc0 + 1];
+      const int j1 = lqs * min(cc0 + 1, cc1 - 1);
       int4 n0 = lq[j1], n1 = lq[j1 + 1];
       const int nst = wave_max_small<5>(cc1 - cc0);  // (a group <= 2 kGW - 1 blocks)
       for (int s = 0; s < nst; ++s) {
         const int jl = cc0 + s;
-        const int j2 = 4 * min(jl + 2, cc1 - 1);
+        const int j2 = lqs * min(jl + 2, cc1 - 1);
         const int4 p0 = lq[j2], p1 = lq[j2 + 1];
         const MapHdr h{__int_as_float(q0.x), q0.y, q0.z, q0.w};
         bool okj = ok && jl < cc1;
@@ -1162,7 +1178,7 @@ __device__ __forceinline__ void sq_comp_body(const SqView& v, const int k, const
       }
     }
   }
-  __syncthreads();
+  sq_wave_sync();
   if (lane == 0) clk[3] = (long long)__builtin_amdgcn_s_memtime();
   GroupMap* grpg = v.grp + (int64_t)c * v.ng + ga;
   for (int i = lane; i < ngr * kGroupMapLW; i += kWave) {
@@ -1737,8 +1753,17 @@ __global__ __launch_bounds__(kFrontT) void k_sq_front(SqView v, const float4* __
                                                      double* __restrict__ tnext) {
   sq_front_body<FUSED>(v, x, tprev, tnext, blockIdx.x, blockIdx.y);
 }
-__global__ __launch_bounds__(kBuildT, kLeavesWaves) void k_sq_leaves(SqView v) { sq_leaf_body(v, blockIdx.x, blockIdx.y); }
-__global__ __launch_bounds__(kWave) void k_sq_comp(SqView v) { sq_comp_body(v, blockIdx.x, blockIdx.y); }
+// the single-stream maps (a pair alone: latency) in one kernel -- the leaf
+// runs, then wavefront 0 composes from the LDS copy; r20: split in two
+// launches, a lone pair's maps 39 -> 50 us an iteration
+__global__ __launch_bounds__(kBuildT, kLeavesWaves) void k_sq_build(SqView v) {
+  __shared__ LeafLds WL;
+  __shared__ CompLds WC;
+  sq_leaf_body(v, blockIdx.x, blockIdx.y, WL, true);
+  __syncthreads();
+  if (threadIdx.x >= kWave) return;
+  sq_comp_body(v, blockIdx.x, blockIdx.y, WC, WL.lf);
+}
 __global__ __launch_bounds__(kWave) void k_sq_walk(SqView v, float* __restrict__ out) {
   sq_walk_body(v, out, blockIdx.x);
 }
@@ -1804,12 +1829,14 @@ __global__ __launch_bounds__(kFrontT) void k_sq_front_b(const SqPair* __restrict
 __global__ __launch_bounds__(kBuildT, kLeavesWaves) void k_sq_leaves_b(const SqPair* __restrict__ P, int nch, int iter) {
   const SqView v = sq_at(P[blockIdx.z], nch, iter);
   if ((int)blockIdx.x >= v.nk) return;
-  sq_leaf_body(v, blockIdx.x, blockIdx.y);
+  __shared__ LeafLds W;
+  sq_leaf_body(v, blockIdx.x, blockIdx.y, W, false);
 }
 __global__ __launch_bounds__(kWave) void k_sq_comp_b(const SqPair* __restrict__ P, int nch, int iter) {
   const SqView v = sq_at(P[blockIdx.z], nch, iter);
   if ((int)blockIdx.x >= v.nk) return;
-  sq_comp_body(v, blockIdx.x, blockIdx.y);
+  __shared__ CompLds W;
+  sq_comp_body(v, blockIdx.x, blockIdx.y, W, nullptr);
 }
 __global__ __launch_bounds__(kWave) void k_sq_walk_b(const SqPair* __restrict__ P, int nch, int iter) {
   const SqPair& p = P[blockIdx.z];
@@ -2445,10 +2472,7 @@ int seqsum_enqueue(const float4* d_x, int64_t n, int nch, void* ws, float* d_out
       k_sq_front<false><<<dim3(v.nk, nch), kFrontT, 0, st>>>(v, nullptr, nullptr, nullptr);
     }
   }
-  if (stages & 2) {
-    k_sq_leaves<<<dim3(v.nk, nch), kBuildT, 0, st>>>(v);
-    k_sq_comp<<<dim3(v.nk, nch), kWave, 0, st>>>(v);
-  }
+  if (stages & 2) k_sq_build<<<dim3(v.nk, nch), kBuildT, 0, st>>>(v);
   if (stages & 4) k_sq_walk<<<nch, kWave, 0, st>>>(v, d_out);
   RST_HIP(hipGetLastError());
   return RST_OK;
