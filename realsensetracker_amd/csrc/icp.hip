@@ -97,6 +97,9 @@ constexpr int kPixChunk = RST_PIX_CHUNK;
 #ifndef RST_PIX_CHUNK_REF
 #define RST_PIX_CHUNK_REF 320  // pixels staged per wave and round, the REF loop (20.5 KB of LDS a block)
 #endif
+#ifndef RST_NN_WAVEQ
+#define RST_NN_WAVEQ 1  // k_icp_nn (no block sums): queue reservations by LDS atomics, no end barrier
+#endif
 #ifndef RST_CERT_EAGER
 #define RST_CERT_EAGER 0  // k_icp_nn: load cert[] beside nnq[] (not after its flag)
 #endif
@@ -417,7 +420,7 @@ struct P2PointAcc {
 struct P2PlaneAcc {
   static constexpr int NV = kNP2Plane;  // A (21), b (6), sum w r^2, count, sum d2
   static constexpr int RS = 32;
-  static constexpr int kFbMinWaves = 1;
+  static constexpr int kFbMinWaves = 2;  // (unconstrained, the r19 DPP reductions took it to 256 VGPRs and one wave a SIMD: 720p point-to-plane 3.26k -> 2.72k it/s)
   static constexpr int kFbMinWavesSingle = kFbMinWaves;
   static constexpr int kNnMinWaves = RST_NN_MIN_WAVES;
   static constexpr int kPixChunk = RST_PIX_CHUNK;
@@ -807,6 +810,20 @@ __device__ __forceinline__ void icp_nn_body(const BvhView& bv, const AdjView& av
     if (threadIdx.x == 0) qcnt[tb] = qcntf[tb] = 0;
     return;
   }
+  // A loop without block sums (RefAcc) fills the queues without a workgroup
+  // barrier at the end: each wavefront reserves its entries in the block's
+  // segments by an LDS atomic and the last one to finish publishes the
+  // counts, so a wavefront with no search leaves (and frees its registers)
+  // instead of waiting for its workgroup's searches (r20h: such waves spent
+  // ~5 us of their ~7 at that barrier).  The entries of a segment are then
+  // in wavefront arrival order -- nothing the REF fallback's results depend
+  // on (a query's answer is its own; no sums fold over the queue).
+  constexpr bool kWaveQ = RST_NN_WAVEQ && !Acc::kSums;
+  __shared__ int qacc[3];  // near entries, far entries, wavefronts done
+  if constexpr (kWaveQ) {
+    if (threadIdx.x == 0) qacc[0] = qacc[1] = qacc[2] = 0;
+    __syncthreads();  // (at the start: the workgroup's waves arrive together)
+  }
   const Uni u = load_uni(st);
   double v[Acc::NV];
 #pragma unroll
@@ -1029,27 +1046,45 @@ __device__ __forceinline__ void icp_nn_body(const BvhView& bv, const AdjView& av
     if (lane == 0 && it < kQTrace) atomicAdd(&const_cast<IcpState*>(st)->path[it][0], __popcll(cm));
   }
 #endif
-  if (lane == 0) {
-    wq[0][wid] = __popcll(bm);
-    wq[1][wid] = __popcll(fm);
-  }
-  __syncthreads();
-  int before = 0, total = 0, beforef = 0, totalf = 0;
-#pragma unroll
-  for (int w = 0; w < kBS / kWave; ++w) {
-    before += w < wid ? wq[0][w] : 0;
-    total += wq[0][w];
-    beforef += w < wid ? wq[1][w] : 0;
-    totalf += wq[1][w];
-  }
   const uint64_t lt = (1ull << lane) - 1ull;
+  int before = 0, beforef = 0;
+  if constexpr (kWaveQ) {
+    if (lane == 0) {
+      before = atomicAdd(&qacc[0], __popcll(bm));
+      beforef = atomicAdd(&qacc[1], __popcll(fm));
+    }
+    before = __builtin_amdgcn_readfirstlane(before);
+    beforef = __builtin_amdgcn_readfirstlane(beforef);
+  } else {
+    if (lane == 0) {
+      wq[0][wid] = __popcll(bm);
+      wq[1][wid] = __popcll(fm);
+    }
+    __syncthreads();
+    int total = 0, totalf = 0;
+#pragma unroll
+    for (int w = 0; w < kBS / kWave; ++w) {
+      before += w < wid ? wq[0][w] : 0;
+      total += wq[0][w];
+      beforef += w < wid ? wq[1][w] : 0;
+      totalf += wq[1][w];
+    }
+    if (threadIdx.x == 0) {
+      qcnt[tb] = total;
+      qcntf[tb] = totalf;
+    }
+  }
   if (need && !far) qbuf[tb * (int64_t)kBS + before + __popcll(bm & lt)] = (int)i;
   // cold: k_icp_fb starts from nnq's position
   if (need && wb < 0) nnq[i] = make_float4(cq.x, cq.y, cq.z, i2f(cpos));
   if (need && far) qbuff[tb * (int64_t)kBS + beforef + __popcll(fm & lt)] = (int)i;
-  if (threadIdx.x == 0) {
-    qcnt[tb] = total;
-    qcntf[tb] = totalf;
+  if constexpr (kWaveQ) {
+    // the last wavefront publishes the counts (every wavefront's reservations
+    // returned before its own `done` increment, so they are all in)
+    if (lane == 0 && atomicAdd(&qacc[2], 1) == kBS / kWave - 1) {
+      qcnt[tb] = atomicAdd(&qacc[0], 0);
+      qcntf[tb] = atomicAdd(&qacc[1], 0);
+    }
   }
   if (certified)
     Acc::add(v, bv, aa, u, s, px, py, pz, dq, f2i(tq.w) & kPosMask, tq, true);
