@@ -577,6 +577,10 @@ __global__ __launch_bounds__(kBS) void k_gather_orig(const float4* __restrict__ 
 #define RST_COV_BLOCKS 256
 #endif
 constexpr int kCovBlocks = RST_COV_BLOCKS;
+#ifndef RST_COV_UNROLL
+#define RST_COV_UNROLL 4
+#endif
+constexpr int kCovU = RST_COV_UNROLL;
 // the covariance grid of a cloud of n points: kCovBlocks, or for small clouds
 // (<= 32768 points, the reference callers' 5 cm voxels) ~8 points a thread --
 // the solve then reduces a few rows (the fp64 sum order, i.e. the last bits of
@@ -603,23 +607,36 @@ __device__ __forceinline__ void cov_ref_body(const float4* __restrict__ srco, co
   double v[9];
 #pragma unroll
   for (int k = 0; k < 9; ++k) v[k] = 0.0;
-  for (int64_t i = blockIdx.x * (int64_t)kBS + threadIdx.x; i < n;
-       i += (int64_t)nblk * kBS) {
-    const float4 s = srco[i];
-    const float4 c = corr[i];
-    // d2 of the search (:112), recomputed: the records of lanes that kept
-    // their neighbour are not rewritten (RefAcc::add); the same transform and
-    // distance arithmetic, so the same bits; no neighbour -> FLT_MAX
-    float px, py, pz;
-    xform(P, s.x, s.y, s.z, px, py, pz);
-    const float d2 = finite3(px, py, pz) ? d2_ref(px, py, pz, c.x, c.y, c.z) : FLT_MAX;
-    const float l = mu / (d2 + mu);
-    const float w = l * l;
-    const float a0 = w * (c.x - dm0), a1 = w * (c.y - dm1), a2 = w * (c.z - dm2);
-    const float b0 = s.x - sm0, b1 = s.y - sm1, b2 = s.z - sm2;
-    v[0] += (double)(a0 * b0); v[1] += (double)(a0 * b1); v[2] += (double)(a0 * b2);
-    v[3] += (double)(a1 * b0); v[4] += (double)(a1 * b1); v[5] += (double)(a1 * b2);
-    v[6] += (double)(a2 * b0); v[7] += (double)(a2 * b1); v[8] += (double)(a2 * b2);
+  // (the thread's points RST_COV_UNROLL at a time, every load issued before
+  // the first product -- the same points in the same order, so the same
+  // sums; r20f: the kernel's waves spent 70 % of their cycles waiting)
+  const int64_t stride = (int64_t)nblk * kBS;
+  for (int64_t i0 = blockIdx.x * (int64_t)kBS + threadIdx.x; i0 < n; i0 += kCovU * stride) {
+    float4 sv[kCovU], cv[kCovU];
+#pragma unroll
+    for (int u = 0; u < kCovU; ++u) {
+      const int64_t i = i0 + u * stride;
+      sv[u] = i < n ? srco[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+      cv[u] = i < n ? corr[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < kCovU; ++u) {
+      if (i0 + u * stride >= n) break;
+      const float4 s = sv[u], c = cv[u];
+      // d2 of the search (:112), recomputed: the records of lanes that kept
+      // their neighbour are not rewritten (RefAcc::add); the same transform and
+      // distance arithmetic, so the same bits; no neighbour -> FLT_MAX
+      float px, py, pz;
+      xform(P, s.x, s.y, s.z, px, py, pz);
+      const float d2 = finite3(px, py, pz) ? d2_ref(px, py, pz, c.x, c.y, c.z) : FLT_MAX;
+      const float l = mu / (d2 + mu);
+      const float w = l * l;
+      const float a0 = w * (c.x - dm0), a1 = w * (c.y - dm1), a2 = w * (c.z - dm2);
+      const float b0 = s.x - sm0, b1 = s.y - sm1, b2 = s.z - sm2;
+      v[0] += (double)(a0 * b0); v[1] += (double)(a0 * b1); v[2] += (double)(a0 * b2);
+      v[3] += (double)(a1 * b0); v[4] += (double)(a1 * b1); v[5] += (double)(a1 * b2);
+      v[6] += (double)(a2 * b0); v[7] += (double)(a2 * b1); v[8] += (double)(a2 * b2);
+    }
   }
   block_sum_to_slab<9, kBS>(v, lds, slab + (int64_t)blockIdx.x * RefAcc::RS);
 }

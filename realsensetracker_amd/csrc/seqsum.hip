@@ -124,6 +124,27 @@ __device__ __forceinline__ double wave_scan_incl(double x) {
   return x;
 }
 
+// a lane's value from a DPP partner (int)
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int x) {
+  return __builtin_amdgcn_update_dpp(0, x, CTRL, 0xf, 0xf, false);
+}
+// the DPP partners of a 16-lane row butterfly: quad_perm [1,0,3,2] and
+// [2,3,0,1] (lane ^ 1, ^ 2), then row_half_mirror and row_mirror, whose
+// partners stand for ^ 4 and ^ 8 once the quads and the half rows agree --
+// valid for an associative, commutative, order-free merge (min, max, a
+// lexicographic max), not for sums (r22: in place of ds_bpermute steps)
+constexpr int kRowBfly[4] = {0xB1, 0x4E, 0x141, 0x140};
+// lane 0's double, as a scalar
+__device__ __forceinline__ double rd_lane0(double x) {
+  const uint2 u = __builtin_bit_cast(uint2, x);
+  return __builtin_bit_cast(double, make_uint2((unsigned)__builtin_amdgcn_readlane((int)u.x, 0),
+                                               (unsigned)__builtin_amdgcn_readlane((int)u.y, 0)));
+}
+// the whole wave's fp64 sum (a guess's: its association is the scan's) at
+// lane kWave - 1
+__device__ __forceinline__ double wave_sum_last(double x) { return wave_scan_incl(x); }
+
 // exclusive block scan of one double per thread (BS threads); returns the
 // prefix, *total = the block total
 // (r19: DPP scans instead of a ds_bpermute per step and thread 0's serial
@@ -312,11 +333,11 @@ __device__ __forceinline__ void sq_tot_body(const float4* __restrict__ x, const 
       if ((tid & 3) == 0 && w < v.nb) v.wflg[(int64_t)c * v.nb + w] = (uint8_t)f;
     }
   }
+  // (the wave's totals by DPP scans -- fp64 guesses, any association;
+  // r22: a ds_bpermute butterfly, 48 LDS round trips a wavefront)
 #pragma unroll
-  for (int o = kWave / 2; o > 0; o >>= 1)
-#pragma unroll
-    for (int c = 0; c < 4; ++c) part[c] += __shfl_xor(part[c], o, kWave);
-  if (lane == 0)
+  for (int c = 0; c < 4; ++c) part[c] = wave_sum_last(part[c]);
+  if (lane == kWave - 1)
 #pragma unroll
     for (int c = 0; c < 4; ++c) red[wv][c] = part[c];
   __syncthreads();
@@ -459,10 +480,17 @@ __device__ __forceinline__ void sq_front_body(const SqView& v, const float4* __r
   const int wj = tid & (kGW - 1);
   double key = b < v.nb ? (wj >= kJLo && wj <= kJHi ? fabs(sA[tid]) : -0.5) : -1.0;
   int kid = b < v.nb ? b : INT_MAX;
+  // (the row's lexicographic max by DPP: order-free, the same winner)
 #pragma unroll
-  for (int o = 8; o > 0; o >>= 1) {
-    const double ok = __shfl_xor(key, o, 16);
-    const int oi = __shfl_xor(kid, o, 16);
+  for (int st = 0; st < 4; ++st) {
+    double ok;
+    int oi;
+    switch (st) {  // (unrolled: constant controls)
+      case 0: ok = dpp_d<kRowBfly[0]>(key); oi = dpp_i<kRowBfly[0]>(kid); break;
+      case 1: ok = dpp_d<kRowBfly[1]>(key); oi = dpp_i<kRowBfly[1]>(kid); break;
+      case 2: ok = dpp_d<kRowBfly[2]>(key); oi = dpp_i<kRowBfly[2]>(kid); break;
+      default: ok = dpp_d<kRowBfly[3]>(key); oi = dpp_i<kRowBfly[3]>(kid); break;
+    }
     if (ok > key || (ok == key && oi < kid)) {
       key = ok;
       kid = oi;
@@ -749,13 +777,17 @@ __device__ __forceinline__ bool comp_chain(float& x, double& clo, double& chi, c
     // the verified steps' windows (lanes < qf < kChainC <= 16: one row)
     lo = lane < qf ? lo : -INFINITY;
     hi = lane < qf ? hi : INFINITY;
-#pragma unroll
-    for (int o = kChainC / 2; o > 0; o >>= 1) {
-      lo = fmax(lo, __shfl_xor(lo, o, kWave));
-      hi = fmin(hi, __shfl_xor(hi, o, kWave));
-    }
-    clo = fmax(clo, __shfl(lo, 0, kWave));
-    chi = fmin(chi, __shfl(hi, 0, kWave));
+    static_assert(kChainC == 16, "one row");
+    lo = fmax(lo, dpp_d<kRowBfly[0]>(lo));
+    hi = fmin(hi, dpp_d<kRowBfly[0]>(hi));
+    lo = fmax(lo, dpp_d<kRowBfly[1]>(lo));
+    hi = fmin(hi, dpp_d<kRowBfly[1]>(hi));
+    lo = fmax(lo, dpp_d<kRowBfly[2]>(lo));
+    hi = fmin(hi, dpp_d<kRowBfly[2]>(hi));
+    lo = fmax(lo, dpp_d<kRowBfly[3]>(lo));
+    hi = fmin(hi, dpp_d<kRowBfly[3]>(hi));
+    clo = fmax(clo, rd_lane0(lo));
+    chi = fmin(chi, rd_lane0(hi));
     x = __int_as_float(__builtin_amdgcn_readlane(hist, qf));
     if (qf == nq) {
       q0 += nq;
@@ -948,9 +980,8 @@ __device__ __forceinline__ void sq_leaf_body(const SqView& v, const int k, const
     const double* ti = v.tinc + (int64_t)c * v.nk;
     double s = 0.0;
     for (int i = lane; i < k; i += kWave) s += ti[i];
-#pragma unroll
-    for (int o = kWave / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, kWave);
-    if (lane == 0) {
+    s = wave_sum_last(s);  // (a guess's offset: any association)
+    if (lane == kWave - 1) {
       const double q = v.p0 ? v.p0[c] : 0.0;  // (a stretch of a longer chain)
       W.base[0] = s + q;
       W.base[1] = s + q + (k < v.nk ? ti[k] : 0.0);
@@ -1993,9 +2024,15 @@ __global__ __launch_bounds__(kSmT) void k_sq_small(const float4* __restrict__ x,
     double key = act ? (wj >= kJLo && wj <= kJHi ? fabs(best) : -0.5) : -1.0;
     int kid = act ? tid : INT_MAX;
 #pragma unroll
-    for (int o = 8; o > 0; o >>= 1) {
-      const double ok = __shfl_xor(key, o, 16);
-      const int oi = __shfl_xor(kid, o, 16);
+    for (int st = 0; st < 4; ++st) {  // (DPP, as the front kernel's)
+      double ok;
+      int oi;
+      switch (st) {
+        case 0: ok = dpp_d<kRowBfly[0]>(key); oi = dpp_i<kRowBfly[0]>(kid); break;
+        case 1: ok = dpp_d<kRowBfly[1]>(key); oi = dpp_i<kRowBfly[1]>(kid); break;
+        case 2: ok = dpp_d<kRowBfly[2]>(key); oi = dpp_i<kRowBfly[2]>(kid); break;
+        default: ok = dpp_d<kRowBfly[3]>(key); oi = dpp_i<kRowBfly[3]>(kid); break;
+      }
       if (ok > key || (ok == key && oi < kid)) {
         key = ok;
         kid = oi;
