@@ -376,6 +376,7 @@ __device__ __forceinline__ void sq_front_body(const SqView& v, const float4* __r
   if (t == 0 && c == 0 && tid == 0) *v.err = 0;
   // the tile (and the next tile's first window) of component c
   const float* Xs = v.soa + (int64_t)c * v.ns;
+  double P;
   {
     // (every load issued before the first LDS store: a rolled loop waited
     // out one memory round trip per element)
@@ -389,6 +390,10 @@ __device__ __forceinline__ void sq_front_body(const SqView& v, const float4* __r
       else
         tv[j] = i < kTile + kW && e0 + i < v.n ? Xs[e0 + i] : 0.0f;
     }
+    // fp64 prefix at the tile start (the quarter tiles' totals before it;
+    // r22: its loads in flight with the tile's, one memory trip, not two)
+    P = block_sum_global<kFrontT>((FUSED ? tprev : v.ttot) + (int64_t)c * v.nk * kTotQ, t * kTotQ, lds) +
+        (v.p0 ? v.p0[c] : 0.0);
     if (FUSED) {
       float* dst = v.soa + (int64_t)c * v.ns;
 #pragma unroll
@@ -403,10 +408,6 @@ __device__ __forceinline__ void sq_front_body(const SqView& v, const float4* __r
       if (i < kTile + kW) xs(i) = tv[j];
     }
   }
-  // fp64 prefix at the tile start (the quarter tiles' totals before it)
-  const double P = block_sum_global<kFrontT>((FUSED ? tprev : v.ttot) + (int64_t)c * v.nk * kTotQ,
-                                             t * kTotQ, lds) +
-                   (v.p0 ? v.p0[c] : 0.0);
   __syncthreads();
   // the thread's window: fp64 total and prefix
   const int b = t * kBlocksPerTile + tid;
@@ -972,19 +973,41 @@ __device__ __forceinline__ void sq_leaf_body(const SqView& v, const int k, const
   const float* X = v.soa + (int64_t)c * v.ns;
   const double* ipre = v.ipre + (int64_t)c * v.nb;
   Leaf* leafg = v.leaf + (int64_t)c * v.nb + ba;  // the superblock's leaf maps (global)
-  // (the first round's increment prefixes in flight across the barrier)
+  // (every staging load issued before the first store -- r22: the block
+  // starts and the tiles' increments were two dependent trips more; the
+  // first round's increment prefixes stay in flight across the barrier)
   const double iv0 = tid < nblk ? ipre[ba + tid] : 0.0;
-  for (int i = tid; i <= nblk; i += kBuildT) W.sbs[i] = bsg[ba + i] - ea;
+  constexpr int kSbR = (kMaxSbBlocks + 1 + kBuildT - 1) / kBuildT;  // block starts per thread
+  int sb[kSbR];
+#pragma unroll
+  for (int r = 0; r < kSbR; ++r) {
+    const int i = tid + r * kBuildT;
+    sb[r] = i <= nblk ? bsg[ba + i] : 0;
+  }
+  const double* ti = v.tinc + (int64_t)c * v.nk;
+  constexpr int kTiR = 4;  // the tiles' increments per lane in flight
+  double tv[kTiR];
+  double s = 0.0;
+  if (tid < kWave) {
+#pragma unroll
+    for (int r = 0; r < kTiR; ++r) tv[r] = lane + r * kWave < k ? ti[lane + r * kWave] : 0.0;
+    for (int i = lane + kTiR * kWave; i < k; i += kWave) s += ti[i];  // (> 256 tiles: a 1M-element chain)
+  }
+  const double tk = tid == kWave - 1 && k < v.nk ? ti[k] : 0.0;
+#pragma unroll
+  for (int r = 0; r < kSbR; ++r) {
+    const int i = tid + r * kBuildT;
+    if (i <= nblk) W.sbs[i] = sb[r] - ea;
+  }
   if (tid == 0) W.nlist = 0;
-  if (tid < kWave) {  // the tiles' increments before tile k (fixed order)
-    const double* ti = v.tinc + (int64_t)c * v.nk;
-    double s = 0.0;
-    for (int i = lane; i < k; i += kWave) s += ti[i];
+  if (tid < kWave) {  // the tiles' increments before tile k
+#pragma unroll
+    for (int r = 0; r < kTiR; ++r) s += tv[r];
     s = wave_sum_last(s);  // (a guess's offset: any association)
     if (lane == kWave - 1) {
       const double q = v.p0 ? v.p0[c] : 0.0;  // (a stretch of a longer chain)
       W.base[0] = s + q;
-      W.base[1] = s + q + (k < v.nk ? ti[k] : 0.0);
+      W.base[1] = s + q + tk;
     }
   }
   __syncthreads();
