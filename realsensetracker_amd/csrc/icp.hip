@@ -1033,11 +1033,19 @@ __device__ __forceinline__ void icp_nn_body(const BvhView& bv, const AdjView& av
     if (RST_PIX_I0_HALF > 0.0f && st->iter == 0)  // (uniform)
       pok = pix_tile_search<Acc::kPixChunk, RST_PIX_I0_CHUNKS, !defer>(bv, pv, need, px, py, pz, d0, pr, pq, pscr[wid],
                                                                   prc, RST_PIX_I0_HALF);
-    else
-      pok = cold ? pix_tile_search<Acc::kPixChunk, RST_PIX_COLD_CHUNKS, !defer>(bv, pv, need, px, py, pz, d0, pr, pq,
-                                                                          pscr[wid], prc, RST_PIX_COLD_HALF)
-                 : pix_tile_search<Acc::kPixChunk, RST_PIX_CHUNKS, !defer>(bv, pv, need, px, py, pz, d0, pr, pq,
-                                                                     pscr[wid], prc, kPixHalf, pckp);
+    else if (cold)
+      pok = pix_tile_search<Acc::kPixChunk, RST_PIX_COLD_CHUNKS, !defer>(bv, pv, need, px, py, pz, d0, pr, pq,
+                                                                        pscr[wid], prc, RST_PIX_COLD_HALF);
+    else {
+      // (few small windows: the row mode, pix_row_search; else the staged
+      // union box)
+      bool rows = false;
+      if (RST_PIX_ROWMODE && std::is_same<Acc, RefAcc>::value)
+        pok = pix_row_search<!defer>(bv, pv, need, px, py, pz, d0, pr, pq, prc, kPixHalf, rows);
+      if (!rows)
+        pok = pix_tile_search<Acc::kPixChunk, RST_PIX_CHUNKS, !defer>(bv, pv, need, px, py, pz, d0, pr, pq,
+                                                                      pscr[wid], prc, kPixHalf, pckp);
+    }
     if (pok) {
       const float g = cert_bound(pr, prc);
       // (deferred: the original index, kIdBit -- compared with the last

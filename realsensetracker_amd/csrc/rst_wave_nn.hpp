@@ -1592,6 +1592,117 @@ __device__ __forceinline__ bool pix_tile_search(const BvhView& bv, const PixView
   return ok && r.pos[0] >= 0 && margin_sqrt(r.d[0]) * 1.00001f + 1e-30f < rc;
 }
 
+// The row mode of the window search (r23): when a wavefront's searching
+// lanes are few (<= kRowQ) and every window small (<= kRowPx pixels), each
+// query takes a row of 16 lanes -- four at a time -- whose lanes load its
+// window's pixels straight from PixView::pts (8 per lane, one memory trip)
+// and merge their two nearest by DPP (wave_lex_min<8>): no union box, no
+// LDS staging, no per-lane scan of the window.  The same pixels as
+// pix_tile_search's window, the same (d2, index) order: the same two
+// nearest, the same covered radius rc, the same q0.  handled = false
+// (uniform): the wavefront does not qualify, nothing was done.  Measured
+// slower (r23c, 172/172 GPU tests bit-identical: k_icp_nn_b 247 -> 266 us,
+// 43.5k -> 41.3k it/s; at five waves a SIMD, without its 92 B of spills,
+// 261 us): off.
+#ifndef RST_PIX_ROWMODE
+#define RST_PIX_ROWMODE 0
+#endif
+constexpr int kRowPx = 16 * 8;
+constexpr int kRowQ = 8;
+__device__ __forceinline__ float rl_f(float x, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l));
+}
+template <bool Resolve>
+__device__ __forceinline__ bool pix_row_search(const BvhView& bv, const PixView& pv, bool act, float qx,
+                                               float qy, float qz, float d0, Best2& r, float4& q0, float& rc,
+                                               float maxh, bool& handled) {
+  const int lane = __lane_id(), row = lane >> 4, sub = lane & 15;
+  int a0 = 0, a1 = -1, b0 = 0, b1 = -1;
+  float rcl = 0.f;
+  const bool ok = act && pix_window(pv, qx, qy, qz, d0, maxh, a0, a1, b0, b1, rcl);
+  const int wa = a1 - a0 + 1, cnt = ok ? wa * (b1 - b0 + 1) : 0;
+  const uint64_t om = __ballot(ok);
+  handled = om != 0 && __popcll(om) <= kRowQ && __ballot(ok && cnt > kRowPx) == 0;
+  if (!handled) return false;
+  rc = rcl;
+  uint64_t rem = om;
+  while (rem) {  // (uniform) four queries a round, one a row
+    int L[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      L[g] = rem ? (int)__builtin_ctzll(rem) : -1;
+      rem &= rem ? rem - 1 : 0;
+    }
+    // this row's query (its lane's values, read as scalars)
+    float rx = 0.f, ry = 0.f, rz = 0.f;
+    int ra0 = 0, rb0 = 0, rwa = 1, rcnt = 0;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      if (L[g] >= 0) {  // (uniform)
+        const float x = rl_f(qx, L[g]), y = rl_f(qy, L[g]), z = rl_f(qz, L[g]);
+        const int ia = __builtin_amdgcn_readlane(a0, L[g]), ib = __builtin_amdgcn_readlane(b0, L[g]);
+        const int iw = __builtin_amdgcn_readlane(wa, L[g]), ic = __builtin_amdgcn_readlane(cnt, L[g]);
+        if (row == g) {
+          rx = x; ry = y; rz = z;
+          ra0 = ia; rb0 = ib; rwa = iw; rcnt = ic;
+        }
+      }
+    }
+    Best2 mine;
+    mine.init();
+    float4 mq = make_float4(NAN, NAN, NAN, 0.f);
+    {
+      const float rw = 1.0f / (float)max(rwa, 1);
+      float4 p[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {  // (every load in flight)
+        const int k = sub + 16 * j;
+        p[j] = make_float4(NAN, NAN, NAN, 0.f);
+        if (k < rcnt) {
+          const int rr = (int)(((float)k + 0.5f) * rw);  // k / rwa (exact: k < 2^12)
+          p[j] = pv.pts[(int64_t)(rb0 + rr) * pv.w + (ra0 + k - rr * rwa)];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = d2_ref(rx, ry, rz, p[j].x, p[j].y, p[j].z);
+        if (d <= mine.d[1]) {  // (NaN: no point)
+          const int id = f2i(p[j].w);
+          mine.offer(d, id, kPosPending);
+          if (mine.id[0] == id) mq = p[j];
+        }
+      }
+    }
+    const int pre = mine.id[0];
+    mine = wave_lex_min<8>(mine);
+    // the winner's point: the first lane of its row whose own first it was
+    const uint64_t hm = __ballot(mine.pos[0] >= 0 && pre == mine.id[0]);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      if (L[g] >= 0) {  // (uniform)
+        const int src = 16 * g;
+        const float e0 = rl_f(mine.d[0], src), e1 = rl_f(mine.d[1], src);
+        const int i0 = __builtin_amdgcn_readlane(mine.id[0], src), i1 = __builtin_amdgcn_readlane(mine.id[1], src);
+        const int p0 = __builtin_amdgcn_readlane(mine.pos[0], src), p1 = __builtin_amdgcn_readlane(mine.pos[1], src);
+        const uint64_t rb = (hm >> (16 * g)) & 0xffffull;
+        const int w = rb ? 16 * g + (int)__builtin_ctzll(rb) : src;
+        const float4 wq = make_float4(rl_f(mq.x, w), rl_f(mq.y, w), rl_f(mq.z, w), rl_f(mq.w, w));
+        if (lane == L[g]) {
+          r.d[0] = e0;
+          r.d[1] = e1;
+          r.id[0] = i0;
+          r.id[1] = i1;
+          r.pos[0] = p0;
+          r.pos[1] = p1;
+          if (rb) q0 = wq;
+        }
+      }
+    }
+  }
+  if (Resolve && ok) pix_resolve(bv, pv, r);
+  return ok && r.pos[0] >= 0 && margin_sqrt(r.d[0]) * 1.00001f + 1e-30f < rc;
+}
+
 // One query per row of 16 lanes (the fallback's short queues): the row's
 // lanes split the query's pixel window, then a row-wide (d2, index) merge.
 // r holds the seeds (r.d[0] = the seed distance); on true r is the exact two
