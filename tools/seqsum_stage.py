@@ -77,11 +77,13 @@ def main():
     clk = ws[off["clk"]:off["clk"] + 64 * 4 * nk].view(np.int64).reshape(4, nk, 8)
     if stages & 2:
         t = clk.astype(np.float64)
-        # stamps: k_sq_leaves start 0, staged 1, leaves done 6; k_sq_comp
-        # start 2, group composites done 3, group maps stored 4, superblock 5
+        # k_sq_build's stamps (the single-stream maps: leaf runs, then
+        # wavefront 0's composites): start 0, staged 1, leaves done 6;
+        # composites start 2, group composites done 3, group maps stored 4,
+        # superblock 5 (the batched k_sq_leaves_b / k_sq_comp_b stamp alike)
         d = np.stack([t[..., 1] - t[..., 0], t[..., 6] - t[..., 1], t[..., 2] - t[..., 6],
                       t[..., 3] - t[..., 2], t[..., 4] - t[..., 3], t[..., 5] - t[..., 4]], axis=2)
-        names = ["staging", "leaves (+ extra candidates)", "launch gap", "group lattice + composites",
+        names = ["staging", "leaves (+ extra candidates)", "barrier", "group lattice + composites",
                  "group store", "superblock"]
         print("map kernel phases (clocks, mean / max over superblocks):",
               {nm: (round(d[:, :, i].mean()), int(d[:, :, i].max())) for i, nm in enumerate(names)})
