@@ -118,8 +118,7 @@ int rst_debug_launch_rate(rst_ctx* ctx, int nstreams, int launches, int blocks, 
                           double* per_s);
 /* RST_TIMELINE builds (RST_DEFINES=-DRST_TIMELINE=1): the context's last
  * ICP align, per iteration and loop kernel (k_icp_nn, k_icp_fb, k_sq_tot,
- * k_sq_front, k_sq_build -- the batched loop's k_sq_leaves_b --, k_sq_walk,
- * k_cov_ref, k_reduce_solve) the
+ * k_sq_front, k_sq_build, k_sq_walk, k_cov_ref, k_reduce_solve) the
  * earliest wave start and the latest wave end on the 100 MHz device clock:
  * out[(iter * 8 + kernel) * 2 + {0, 1}], at most cap values; *iters = the
  * iterations run.  RST_E_STATE in other builds. */
