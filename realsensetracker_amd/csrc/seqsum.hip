@@ -583,6 +583,12 @@ constexpr int kBuildT = 320;
 constexpr int kLeavesPerCU = RST_SQ_LEAVES_PER_CU;
 constexpr int kLeavesWaves = (kLeavesPerCU * kBuildT / kWave + 3) / 4;
 static_assert(kBuildT >= kWave && kBuildT % kWave == 0, "leaf workgroup size");
+// the single-stream k_sq_build (a pair alone: latency, not residency): a lane
+// for every block of the largest superblock, one leaf round (r24: at 320
+// threads, the superblocks past 320 blocks took a second round and set the
+// kernel's time, 39 -> 45 us an iteration of a lone pair)
+constexpr int kBuildT1 = 512;
+static_assert(kBuildT1 >= kMaxSbBlocks, "one leaf round");
 static_assert(sizeof(Leaf) == 64, "a leaf map is four int4");
 constexpr int kListCap = (kLeafR - 1) * kMaxSbBlocks;
 constexpr int16_t kNeedNone = INT16_MIN;  // kNoNeed in 16 bits
@@ -959,6 +965,8 @@ __device__ __forceinline__ bool sb_range(const SqView& v, int k, int c, bool fla
 // k_sq_leaves: every leaf map of superblock k of chain c (global v.leaf)
 // (lds_maps: the maps' headers and entries 0 also left in W.lf, the fused
 // kernel's composites read them there)
+// (T threads: k_sq_leaves_b T, the single-stream k_sq_build T1)
+template <int T>
 __device__ __forceinline__ void sq_leaf_body(const SqView& v, const int k, const int c, LeafLds& W,
                                              bool lds_maps) {
   RST_TL(v.tl, v.it, 4);
@@ -977,11 +985,11 @@ __device__ __forceinline__ void sq_leaf_body(const SqView& v, const int k, const
   // starts and the tiles' increments were two dependent trips more; the
   // first round's increment prefixes stay in flight across the barrier)
   const double iv0 = tid < nblk ? ipre[ba + tid] : 0.0;
-  constexpr int kSbR = (kMaxSbBlocks + 1 + kBuildT - 1) / kBuildT;  // block starts per thread
+  constexpr int kSbR = (kMaxSbBlocks + 1 + T - 1) / T;  // block starts per thread
   int sb[kSbR];
 #pragma unroll
   for (int r = 0; r < kSbR; ++r) {
-    const int i = tid + r * kBuildT;
+    const int i = tid + r * T;
     sb[r] = i <= nblk ? bsg[ba + i] : 0;
   }
   const double* ti = v.tinc + (int64_t)c * v.nk;
@@ -996,7 +1004,7 @@ __device__ __forceinline__ void sq_leaf_body(const SqView& v, const int k, const
   const double tk = tid == kWave - 1 && k < v.nk ? ti[k] : 0.0;
 #pragma unroll
   for (int r = 0; r < kSbR; ++r) {
-    const int i = tid + r * kBuildT;
+    const int i = tid + r * T;
     if (i <= nblk) W.sbs[i] = sb[r] - ea;
   }
   if (tid == 0) W.nlist = 0;
@@ -1012,10 +1020,10 @@ __device__ __forceinline__ void sq_leaf_body(const SqView& v, const int k, const
   }
   __syncthreads();
   if (tid == 0) clk[1] = (long long)__builtin_amdgcn_s_memtime();
-  // -- candidate 0 per block, a lane each (rounds of kBuildT blocks): its
+  // -- candidate 0 per block, a lane each (rounds of T blocks): its
   // header, entry and lattice need to LDS, h.m = 1 marking a block whose
   // other candidates are listed
-  for (int b0 = 0; b0 < nblk; b0 += kBuildT) {
+  for (int b0 = 0; b0 < nblk; b0 += T) {
     const int bi = b0 + tid;
     const bool act = bi < nblk;
     const int b = ba + bi;
@@ -1061,7 +1069,7 @@ __device__ __forceinline__ void sq_leaf_body(const SqView& v, const int k, const
     // the listed extra candidates, one lane each (rare; uniform skip): their
     // entries straight to the global map, their needs to LDS
     const int nl = min(W.nlist, kListCap);
-    for (int j0 = 0; j0 < nl; j0 += kBuildT) {
+    for (int j0 = 0; j0 < nl; j0 += T) {
       const int j = j0 + tid;
       const int code = j < nl ? W.list[j] : 0;
       const int bl = min(code >> 2, nblk - 1), r = code & 3;
@@ -1082,7 +1090,7 @@ __device__ __forceinline__ void sq_leaf_body(const SqView& v, const int k, const
   __syncthreads();
   // the leaf maps: lattice need over the candidates -> m, the map whole to
   // global memory
-  for (int bi = tid; bi < nblk; bi += kBuildT) {
+  for (int bi = tid; bi < nblk; bi += T) {
     const LeafL L = W.lf[bi];
     const bool more = L.h.m != 0;
     int need = L.aux;
@@ -1810,10 +1818,10 @@ __global__ __launch_bounds__(kFrontT) void k_sq_front(SqView v, const float4* __
 // the single-stream maps (a pair alone: latency) in one kernel -- the leaf
 // runs, then wavefront 0 composes from the LDS copy; r20: split in two
 // launches, a lone pair's maps 39 -> 50 us an iteration
-__global__ __launch_bounds__(kBuildT, kLeavesWaves) void k_sq_build(SqView v) {
+__global__ __launch_bounds__(kBuildT1) void k_sq_build(SqView v) {
   __shared__ LeafLds WL;
   __shared__ CompLds WC;
-  sq_leaf_body(v, blockIdx.x, blockIdx.y, WL, true);
+  sq_leaf_body<kBuildT1>(v, blockIdx.x, blockIdx.y, WL, true);
   __syncthreads();
   if (threadIdx.x >= kWave) return;
   sq_comp_body(v, blockIdx.x, blockIdx.y, WC, WL.lf);
@@ -1884,7 +1892,7 @@ __global__ __launch_bounds__(kBuildT, kLeavesWaves) void k_sq_leaves_b(const SqP
   const SqView v = sq_at(P[blockIdx.z], nch, iter);
   if ((int)blockIdx.x >= v.nk) return;
   __shared__ LeafLds W;
-  sq_leaf_body(v, blockIdx.x, blockIdx.y, W, false);
+  sq_leaf_body<kBuildT>(v, blockIdx.x, blockIdx.y, W, false);
 }
 __global__ __launch_bounds__(kWave) void k_sq_comp_b(const SqPair* __restrict__ P, int nch, int iter) {
   const SqView v = sq_at(P[blockIdx.z], nch, iter);
@@ -2532,7 +2540,7 @@ int seqsum_enqueue(const float4* d_x, int64_t n, int nch, void* ws, float* d_out
       k_sq_front<false><<<dim3(v.nk, nch), kFrontT, 0, st>>>(v, nullptr, nullptr, nullptr);
     }
   }
-  if (stages & 2) k_sq_build<<<dim3(v.nk, nch), kBuildT, 0, st>>>(v);
+  if (stages & 2) k_sq_build<<<dim3(v.nk, nch), kBuildT1, 0, st>>>(v);
   if (stages & 4) k_sq_walk<<<nch, kWave, 0, st>>>(v, d_out);
   RST_HIP(hipGetLastError());
   return RST_OK;
